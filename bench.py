@@ -1,0 +1,256 @@
+"""bench.py — validity checks/sec on MI355X (BASELINE.json metric), one JSON line.
+
+Workload at N=1 = BASELINE configs[1] (C2): one track, 8 gates, 64 OBBs (40 gate + 24
+obstacle), 1,048,576 uniformly sampled states per step, StateValidator semantics
+(World::checkPointValidity(p, canPassGate=false), src/World.cpp:80-104).  Every step
+checks a FRESH batch of 1M states (a sampler streaming new samples): 16 resident batches
+(400 MB, larger than the 256 MB Infinity Cache) are rotated, so the timed kernels stream
+from HBM.  Inputs are resident in HBM before the timed region.
+
+Multi-GPU: one process per GPU (torchrun); every rank checks its own stream of states
+against its own copy of the world (independent samplers, no data-path collective:
+"scaling": "weak"); ranks synchronise with a barrier and the slowest rank's time is used.
+
+Side measurements (same JSON line, not the headline value): C3 motion checks (512 OBBs,
+analytic and 32-step discretised), the C5 batched min-snap refit (4096 x 12 segments),
+and the CPU oracle timed on the host (cpu_baseline).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "efficient-path-planner_amd")]
+
+N_STATES = 1 << 20
+N_BATCHES = 16
+BYTES_PER_STATE = 25  # 24 B xyz read + 1 B flag written
+BYTES_PER_EDGE = 49
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def _dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+class Dist:
+    def __init__(self, ws, rank, local):
+        self.ws, self.rank, self.local = ws, rank, local
+        self.pg = None
+        if ws > 1:
+            import torch
+            import torch.distributed as dist
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            self.dist, self.torch = dist, torch
+
+    def barrier(self):
+        if self.ws > 1:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if self.ws == 1:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.ws > 1:
+            self.dist.destroy_process_group()
+
+
+def timed_kernel_ms(capi, stream, fn, reps):
+    """Average device time of `fn` over `reps` launches, HIP events on `stream`."""
+    import ctypes as C
+    L = capi.lib()
+    e0, e1 = C.c_void_p(), C.c_void_p()
+    capi.check(L.epp_event_create(C.byref(e0)))
+    capi.check(L.epp_event_create(C.byref(e1)))
+    tot = 0.0
+    for r in range(reps):
+        capi.check(L.epp_event_record(e0, stream))
+        fn(r)
+        capi.check(L.epp_event_record(e1, stream))
+        ms = C.c_float()
+        capi.check(L.epp_event_elapsed_ms(e0, e1, C.byref(ms)))
+        tot += ms.value
+    L.epp_event_destroy(e0)
+    L.epp_event_destroy(e1)
+    return tot / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-side", action="store_true", help="skip the side measurements")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    args = ap.parse_args()
+
+    ws, rank, local = _dist_env()
+    dist = Dist(ws, rank, local)
+    import ctypes as C
+
+    from eppamd import capi, config, synth
+
+    L = capi.lib()
+    capi.check(L.epp_set_device(local))
+    stream = C.c_void_p()
+    capi.check(L.epp_stream_create(C.byref(stream)))
+    stream = stream.value
+
+    cfg = config.load(os.path.join(ROOT, "configs", "config.json"))
+    geom = config.geometry(cfg)
+    rg, ro = config.inflate_radii(cfg)
+    gates, obstacles = synth.track_world(42)
+    obbs = capi.build_obbs(geom, gates, obstacles)
+    world = capi.World(obbs, rg, ro)
+    lo, hi = synth.C2_BOUNDS
+
+    # ---- resident inputs: 16 fresh 1M-state batches per rank ------------------------
+    d_states = capi.DeviceBuffer(N_BATCHES * N_STATES * 24)
+    for b in range(N_BATCHES):
+        pts = synth.sample_states(7 + 1000 * rank, lo, hi, N_STATES, start=b * N_STATES)
+        capi.check(L.epp_memcpy_h2d(d_states.ptr + b * N_STATES * 24, pts.ctypes.data, pts.nbytes, stream))
+    d_valid = capi.DeviceBuffer(N_STATES)
+
+    def step(i):
+        world.check_states_dev(d_states.ptr + (i % N_BATCHES) * N_STATES * 24, N_STATES, 0, d_valid.ptr,
+                               stream=stream)
+
+    for i in range(args.warmup):
+        step(i)
+    capi.check(L.epp_stream_sync(stream))
+    dist.barrier()
+    capi.check(L.epp_stream_sync(stream))
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    capi.check(L.epp_stream_sync(stream))
+    dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = dist.max(t1 - t0)
+    value = ws * N_STATES * args.steps / elapsed
+
+    # dominant kernel's average launch time, HIP events on the launch stream
+    kms = timed_kernel_ms(capi, stream, step, max(10, min(args.steps, 50)))
+    achieved = BYTES_PER_STATE * N_STATES / (kms * 1e-3) / 1e9
+    n_valid = int(d_valid.download(np.uint8, N_STATES).sum())
+
+    side = {}
+    if not args.no_side and rank == 0:
+        side = side_measurements(capi, L, stream, geom, cfg, rg, ro)
+
+    cpu = None
+    if not args.no_cpu and rank == 0 and ws == 1:
+        cpu = cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi)
+
+    if rank == 0:
+        out = {
+            "metric": "validity checks/sec + full plan ms/track, 1/2/4/8 MI355X vs CPU ref",
+            "value": value,
+            "unit": "state validity checks/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (counter-based uniform states, seeded track world)",
+            "config": {"workload": "C2: 1 track, 8 gates, 64 OBBs, 1,048,576 sampled states per step",
+                       "states_per_step_per_gpu": N_STATES, "obbs": int(len(obbs)),
+                       "can_pass_gate": False, "valid_fraction": n_valid / N_STATES,
+                       "parallelism": f"replicas x{ws} (independent samplers)"},
+            "roofline": {"bound": "hbm", "kernel": "k_states<true,false>", "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "bytes_per_state": BYTES_PER_STATE, "kernel_ms": kms, "traffic": None},
+            "cpu_baseline": cpu,
+            "side": side,
+        }
+        print(json.dumps(out))
+    capi.check(L.epp_stream_destroy(stream))
+    dist.close()
+
+
+def side_measurements(capi, L, stream, geom, cfg, rg, ro):
+    from eppamd import synth
+    res = {}
+    # C3: 512 OBBs, 1M edges (analytic) and 32-step discretised
+    g3, o3 = synth.track_world(42, n_obstacles=472)
+    w3 = capi.World(capi.build_obbs(geom, g3, o3), rg, ro)
+    lo, hi = synth.C2_BOUNDS
+    n = N_STATES
+    s1, s2 = synth.edges(43, 8, lo, hi, n)
+    d1, d2 = capi.DeviceBuffer.from_array(s1, stream), capi.DeviceBuffer.from_array(s2, stream)
+    dv = capi.DeviceBuffer(n)
+    for mode, key in ((0, "c3_motion_analytic"), (1, "c3_motion_discrete32")):
+        f = lambda r: w3.check_motions_dev(d1.ptr, d2.ptr, n, 0, mode, dv.ptr, stream=stream)  # noqa: E731
+        f(0)
+        ms = timed_kernel_ms(capi, stream, f, 10)
+        res[key] = {"edges_per_s": n / (ms * 1e-3), "kernel_ms": ms,
+                    "hbm_frac": BYTES_PER_EDGE * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    res["c3_motion_discrete32"]["point_checks_per_s"] = 32 * res["c3_motion_discrete32"]["edges_per_s"]
+    # C5 batched: 4096 independent 12-segment refits per launch
+    nt = 4096
+    tracks = [synth.random_track_waypoints(10_000 + k, 12) for k in range(nt)]
+    wp = np.ascontiguousarray(np.concatenate(tracks))
+    off = np.arange(nt + 1, dtype=np.int32) * 13
+    d_wp, d_off = capi.DeviceBuffer.from_array(wp, stream), capi.DeviceBuffer.from_array(off, stream)
+    d_T, d_C, d_st = capi.DeviceBuffer(8 * 12 * nt), capi.DeviceBuffer(240 * 12 * nt), capi.DeviceBuffer(4 * nt)
+
+    def ms_fn(r):
+        capi.check(L.epp_minsnap_batch(d_wp.ptr, d_off.ptr, nt, 1.0, 2.0, None, None, d_T.ptr, d_C.ptr, d_st.ptr,
+                                       stream))
+    ms_fn(0)
+    ms = timed_kernel_ms(capi, stream, ms_fn, 10)
+    res["c5_minsnap_batch"] = {"problems_per_s": nt / (ms * 1e-3), "ms_per_launch": ms, "problems": nt,
+                               "segments": 12}
+    # C5 single refit latency (host buffers in/out, includes sampling at dt=0.1)
+    wp1 = tracks[0]
+    t = time.perf_counter()
+    for _ in range(20):
+        capi.generate_trajectory(wp1, 1.0, 2.0, 0.1)
+    res["c5_refit_latency_ms"] = (time.perf_counter() - t) / 20 * 1e3
+    return res
+
+
+def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi):
+    """CPU oracle (a port of the reference's World semantics, 1 thread like OMPL's
+    one-query-at-a-time plugin calls) on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from eppamd import synth
+    w = O.world_build(geom, gates, obstacles, rg, ro)
+    pts = synth.sample_states(7, lo, hi, N_STATES)
+    reps = 0
+    t = time.perf_counter()
+    while True:
+        O.check_states(w, rg, ro, pts, False, threads=1)
+        reps += 1
+        if time.perf_counter() - t > 10.0:
+            break
+    dt = time.perf_counter() - t
+    t2 = time.perf_counter()
+    nt = min(16, os.cpu_count() or 1)
+    O.check_states(w, rg, ro, pts, False, threads=nt)
+    dt2 = time.perf_counter() - t2
+    return {"value": reps * N_STATES / dt, "unit": "state validity checks/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} passes over the same 1,048,576-state C2 batch ({reps * N_STATES} checks, {dt:.1f} s)",
+            "all_cores_value": N_STATES / dt2, "all_cores_threads": nt}
+
+
+if __name__ == "__main__":
+    main()

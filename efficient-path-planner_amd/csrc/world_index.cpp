@@ -1,0 +1,251 @@
+// world_index.cpp — host side of the collision index: per-OBB AABBs (the Boost
+// rtree boxes of the reference) and a uniform cull grid, packed into one HBM blob.
+//
+// Reference: OBB::getAABB (src/OBB.cpp:93-123), World::addObject (src/World.cpp:57-67).
+// The rtree (include/Types.h:16, quadratic<16>) is replaced by a uniform grid whose
+// cell lists are a superset of the boxes that can contain / intersect a query; the
+// kernels then apply the rtree's exact predicate (strict `within` for points, closed
+// `intersects` for ray boxes) to every candidate, so the candidate set equals the
+// rtree's query result.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "epp_internal.h"
+
+namespace epp {
+namespace {
+
+// OBB::getAABB — src/OBB.cpp:93-123.  Corner order (:100-102) and the
+// `rotation * corners + centerStacked` evaluation (:110) are kept; min/max are
+// order independent.
+void compute_aabb(const epp_obb& o, double inflate, double lo[3], double hi[3]) {
+    static const double sx[8] = {-1, 1, 1, -1, -1, 1, 1, -1};
+    static const double sy[8] = {-1, -1, 1, 1, -1, -1, 1, 1};
+    static const double sz[8] = {-1, -1, -1, -1, 1, 1, 1, 1};
+    for (int j = 0; j < 8; ++j) {
+        const double c0 = sx[j] * o.half[0], c1 = sy[j] * o.half[1], c2 = sz[j] * o.half[2];
+        for (int i = 0; i < 3; ++i) {
+            const double g =
+                ((o.rot[3 * i] * c0 + o.rot[3 * i + 1] * c1) + o.rot[3 * i + 2] * c2) + o.center[i];
+            if (j == 0 || g < lo[i]) lo[i] = g;
+            if (j == 0 || g > hi[i]) hi[i] = g;
+        }
+    }
+    if (!o.filling) {  // only "collision" boxes are inflated (:117-121)
+        for (int i = 0; i < 3; ++i) {
+            lo[i] = lo[i] - inflate;
+            hi[i] = hi[i] + inflate;
+        }
+    }
+}
+
+bool is_rz(const epp_obb& o) {
+    const double* r = o.rot;
+    return r[2] == 0.0 && r[5] == 0.0 && r[6] == 0.0 && r[7] == 0.0 && r[8] == 1.0 &&
+           r[0] == r[4] && r[1] == -r[3];
+}
+
+inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+
+// Builds the blob (layout in epp_internal.h).  Returns false with an error set.
+bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
+    WorldView& v = hw.view;
+    const int n_pad = (n + 3) & ~3;
+    v.n_obb = n;
+    v.n_pad = n_pad;
+    hw.aabbs.assign((size_t)n * 6, 0.0);
+    std::vector<double> soa((size_t)EPP_NF * n_pad, 0.0);
+    std::vector<uint32_t> meta(n_pad, 0);
+    double g0[3] = {0, 0, 0}, g1[3] = {0, 0, 0};
+    for (int i = 0; i < n; ++i) {
+        const epp_obb& o = obbs[i];
+        if (!is_rz(o)) {
+            set_error("epp_world: OBB rotation must be a rotation about z (src/Object.cpp:38-47)");
+            return false;
+        }
+        const double r = o.is_gate ? hw.r_gate : hw.r_obst;  // src/World.cpp:89-90
+        double lo[3], hi[3];
+        compute_aabb(o, r, lo, hi);
+        for (int k = 0; k < 3; ++k) {
+            hw.aabbs[(size_t)i * 6 + k] = lo[k];
+            hw.aabbs[(size_t)i * 6 + 3 + k] = hi[k];
+            if (i == 0 || lo[k] < g0[k]) g0[k] = lo[k];
+            if (i == 0 || hi[k] > g1[k]) g1[k] = hi[k];
+        }
+        double* f = soa.data();
+        f[F_LOX * n_pad + i] = lo[0]; f[F_LOY * n_pad + i] = lo[1]; f[F_LOZ * n_pad + i] = lo[2];
+        f[F_HIX * n_pad + i] = hi[0]; f[F_HIY * n_pad + i] = hi[1]; f[F_HIZ * n_pad + i] = hi[2];
+        f[F_CX * n_pad + i] = o.center[0]; f[F_CY * n_pad + i] = o.center[1]; f[F_CZ * n_pad + i] = o.center[2];
+        f[F_COS * n_pad + i] = o.rot[0];  // R(0,0) = cos
+        f[F_SIN * n_pad + i] = o.rot[3];  // R(1,0) = sin
+        f[F_HX * n_pad + i] = o.half[0]; f[F_HY * n_pad + i] = o.half[1]; f[F_HZ * n_pad + i] = o.half[2];
+        f[F_R * n_pad + i] = r;
+        meta[i] = (o.filling ? META_FILLING : 0u) | (o.is_gate ? META_GATE : 0u);
+    }
+    // ---- cull grid -------------------------------------------------------------
+    int nd[3] = {1, 1, 1};
+    double inv[3] = {0, 0, 0};
+    if (n > 0) {
+        double ext[3], vol = 1.0;
+        for (int k = 0; k < 3; ++k) {
+            ext[k] = g1[k] - g0[k];
+            vol *= std::max(ext[k], 1e-3);
+        }
+        // ~4 cells per OBB, capped: keeps candidate lists at a handful of OBBs.
+        const double target = std::min(8192.0, std::max(64.0, 4.0 * n));
+        const double s = std::cbrt(vol / target);
+        for (int k = 0; k < 3; ++k) {
+            nd[k] = ext[k] > 0 ? (int)std::ceil(ext[k] / s) : 1;
+            nd[k] = std::max(1, std::min(kMaxGridAxis, nd[k]));
+            inv[k] = ext[k] > 0 ? (double)nd[k] / ext[k] : 0.0;
+        }
+    }
+    v.nx = nd[0]; v.ny = nd[1]; v.nz = nd[2];
+    v.gx0 = g0[0]; v.gy0 = g0[1]; v.gz0 = g0[2];
+    v.gx1 = g1[0]; v.gy1 = g1[1]; v.gz1 = g1[2];
+    v.icx = inv[0]; v.icy = inv[1]; v.icz = inv[2];
+    const int ncell = nd[0] * nd[1] * nd[2];
+    std::vector<std::vector<uint16_t>> cells(ncell);
+    for (int i = 0; i < n; ++i) {
+        const double* lo = &hw.aabbs[(size_t)i * 6];
+        const double* hi = lo + 3;
+        int c0[3], c1[3];
+        for (int k = 0; k < 3; ++k) {
+            c0[k] = cell_of(lo[k], g0[k], inv[k], nd[k]);
+            c1[k] = cell_of(hi[k], g0[k], inv[k], nd[k]);
+        }
+        meta[i] |= ((uint32_t)c0[0] << 8) | ((uint32_t)c0[1] << 16) | ((uint32_t)c0[2] << 24);
+        for (int z = c0[2]; z <= c1[2]; ++z)
+            for (int y = c0[1]; y <= c1[1]; ++y)
+                for (int x = c0[0]; x <= c1[0]; ++x)
+                    cells[((size_t)z * nd[1] + y) * nd[0] + x].push_back((uint16_t)i);
+    }
+    std::vector<uint32_t> cell_start(ncell + 1, 0);
+    for (int c = 0; c < ncell; ++c) cell_start[c + 1] = cell_start[c] + (uint32_t)cells[c].size();
+    const size_t n_entries = cell_start[ncell];
+    // ---- pack ------------------------------------------------------------------
+    const size_t bytes_soa = soa.size() * sizeof(double);
+    const size_t off_meta = bytes_soa;
+    const size_t off_cs = align16(off_meta + meta.size() * 4);
+    const size_t off_co = align16(off_cs + cell_start.size() * 4);
+    const size_t total = align16(off_co + n_entries * 2);
+    if (total > 0xFFFFFFFFull) {
+        set_error("epp_world: index too large");
+        return false;
+    }
+    hw.blob.assign(total, '\0');
+    char* b = &hw.blob[0];
+    std::memcpy(b, soa.data(), bytes_soa);
+    std::memcpy(b + off_meta, meta.data(), meta.size() * 4);
+    std::memcpy(b + off_cs, cell_start.data(), cell_start.size() * 4);
+    size_t pos = off_co;
+    for (int c = 0; c < ncell; ++c) {
+        if (!cells[c].empty()) std::memcpy(b + pos, cells[c].data(), cells[c].size() * 2);
+        pos += cells[c].size() * 2;
+    }
+    v.blob_bytes = (uint32_t)total;
+    v.off_meta = (uint32_t)off_meta;
+    v.off_cell_start = (uint32_t)off_cs;
+    v.off_cell_obb = (uint32_t)off_co;
+    return true;
+}
+
+bool upload(HostWorld& hw) {
+    const size_t bytes = hw.blob.size();
+    if (bytes > hw.d_capacity) {
+        if (hw.d_blob) (void)hipFree(hw.d_blob);
+        hw.d_blob = nullptr;
+        hw.d_capacity = 0;
+        hipError_t e = hipMalloc(&hw.d_blob, bytes);
+        if (e != hipSuccess) {
+            set_error(std::string("epp_world: hipMalloc: ") + hipGetErrorString(e));
+            return false;
+        }
+        hw.d_capacity = bytes;
+    }
+    hipError_t e = hipMemcpy(hw.d_blob, hw.blob.data(), bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        set_error(std::string("epp_world: hipMemcpy: ") + hipGetErrorString(e));
+        return false;
+    }
+    hw.view.blob = (const unsigned char*)hw.d_blob;
+    return true;
+}
+
+}  // namespace
+}  // namespace epp
+
+struct epp_world : epp::HostWorld {};
+
+extern "C" {
+
+epp_status epp_world_create(const epp_obb* obbs, int32_t n, double r_gate, double r_obst,
+                            epp_world** out) {
+    if (!out || n < 0 || (n > 0 && !obbs)) {
+        epp::set_error("epp_world_create: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    if (n > 65535) {
+        epp::set_error("epp_world_create: at most 65535 OBBs");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    epp_world* w = new (std::nothrow) epp_world();
+    if (!w) return EPP_ERR_RUNTIME;
+    w->r_gate = r_gate;
+    w->r_obst = r_obst;
+    (void)hipGetDevice(&w->device);
+    if (!epp::build_blob(*w, obbs, n)) {
+        delete w;
+        return EPP_ERR_UNSUPPORTED;
+    }
+    if (!epp::upload(*w)) {
+        delete w;
+        return EPP_ERR_HIP;
+    }
+    *out = w;
+    return EPP_OK;
+}
+
+epp_status epp_world_update(epp_world* w, const epp_obb* obbs, int32_t n) {
+    if (!w || n < 0 || n > 65535 || (n > 0 && !obbs)) {
+        epp::set_error("epp_world_update: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    // the previous blob may still be read by in-flight kernels on any stream
+    (void)hipDeviceSynchronize();
+    if (!epp::build_blob(*w, obbs, n)) return EPP_ERR_UNSUPPORTED;
+    if (!epp::upload(*w)) return EPP_ERR_HIP;
+    return EPP_OK;
+}
+
+epp_status epp_world_destroy(epp_world* w) {
+    if (!w) return EPP_OK;
+    if (w->d_blob) (void)hipFree(w->d_blob);
+    delete w;
+    return EPP_OK;
+}
+
+epp_status epp_world_num_obbs(const epp_world* w, int32_t* n) {
+    if (!w || !n) return EPP_ERR_INVALID_ARGUMENT;
+    *n = w->view.n_obb;
+    return EPP_OK;
+}
+
+epp_status epp_world_get_aabbs(const epp_world* w, double* lo_hi) {
+    if (!w || !lo_hi) return EPP_ERR_INVALID_ARGUMENT;
+    std::memcpy(lo_hi, w->aabbs.data(), w->aabbs.size() * sizeof(double));
+    return EPP_OK;
+}
+
+}  // extern "C"
+
+// Accessor for the kernels' launchers (collision.hip).
+namespace epp {
+const WorldView& world_view(const epp_world* w) { return w->view; }
+}  // namespace epp

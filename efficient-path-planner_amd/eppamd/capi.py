@@ -1,0 +1,290 @@
+"""ctypes binding of the C ABI in include/epp.h (libepp.so, built in-tree).
+
+This is the product path: every call goes to the HIP kernels in libepp.so.  There is
+no CPU fallback — if the library or a GPU is missing the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libepp.so")
+
+OBB_DTYPE = np.dtype([("center", "<f8", 3), ("half", "<f8", 3), ("rot", "<f8", 9),
+                      ("filling", "<i4"), ("is_gate", "<i4")])
+
+EPP_OK = 0
+EPP_ERR_INVALID_ARGUMENT = -1
+EPP_ERR_RUNTIME = -2
+EPP_ERR_HIP = -3
+EPP_ERR_UNSUPPORTED = -4
+EPP_ERR_CAPACITY = -5
+
+_lib = None
+
+
+class EppError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"epp error {code}: {msg}")
+        self.code = code
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} not built: run __graft_entry__.build()")
+        l = C.CDLL(LIB_PATH)
+        vp, i32, i64, u64, dp = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_double
+        sig = {
+            "epp_last_error": (C.c_char_p, []),
+            "epp_version": (C.c_char_p, []),
+            "epp_device_count": (i32, [C.POINTER(C.c_int)]),
+            "epp_set_device": (i32, [C.c_int]),
+            "epp_malloc": (i32, [C.POINTER(vp), u64]),
+            "epp_free": (i32, [vp]),
+            "epp_memcpy_h2d": (i32, [vp, vp, u64, vp]),
+            "epp_memcpy_d2h": (i32, [vp, vp, u64, vp]),
+            "epp_memset": (i32, [vp, C.c_int, u64, vp]),
+            "epp_stream_create": (i32, [C.POINTER(vp)]),
+            "epp_stream_destroy": (i32, [vp]),
+            "epp_stream_sync": (i32, [vp]),
+            "epp_device_sync": (i32, []),
+            "epp_event_create": (i32, [C.POINTER(vp)]),
+            "epp_event_destroy": (i32, [vp]),
+            "epp_event_record": (i32, [vp, vp]),
+            "epp_event_elapsed_ms": (i32, [vp, vp, C.POINTER(C.c_float)]),
+            "epp_build_obbs": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, i32, vp, i32, C.POINTER(i32)]),
+            "epp_world_create": (i32, [vp, i32, dp, dp, C.POINTER(vp)]),
+            "epp_world_update": (i32, [vp, vp, i32]),
+            "epp_world_destroy": (i32, [vp]),
+            "epp_world_num_obbs": (i32, [vp, C.POINTER(i32)]),
+            "epp_world_get_aabbs": (i32, [vp, vp]),
+            "epp_check_states": (i32, [vp, vp, i64, i32, vp, vp, vp, vp]),
+            "epp_check_states_mindist": (i32, [vp, vp, i64, dp, vp, vp]),
+            "epp_check_motions": (i32, [vp, vp, vp, i64, i32, i32, vp, vp]),
+            "epp_minsnap_batch": (i32, [vp, vp, i32, dp, dp, vp, vp, vp, vp, vp, vp]),
+            "epp_sample_count": (i32, [vp, vp, i32, dp, vp, vp]),
+            "epp_sample_batch": (i32, [vp, vp, vp, i32, dp, vp, vp, vp, vp]),
+            "epp_generate_trajectory_host": (i32, [vp, i32, dp, dp, dp, dp, vp, vp,
+                                                   C.POINTER(C.POINTER(C.c_double)), C.POINTER(i64)]),
+            "epp_host_free": (None, [vp]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(l, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = l
+    return _lib
+
+
+# every symbol include/epp.h declares (the CPU test checks the library exports them)
+EXPORTED = [
+    "epp_last_error", "epp_version", "epp_device_count", "epp_set_device", "epp_malloc", "epp_free",
+    "epp_memcpy_h2d", "epp_memcpy_d2h", "epp_memset", "epp_stream_create", "epp_stream_destroy",
+    "epp_stream_sync", "epp_device_sync", "epp_event_create", "epp_event_destroy", "epp_event_record",
+    "epp_event_elapsed_ms", "epp_build_obbs", "epp_world_create", "epp_world_update",
+    "epp_world_destroy", "epp_world_num_obbs", "epp_world_get_aabbs", "epp_check_states",
+    "epp_check_states_mindist", "epp_check_motions", "epp_minsnap_batch", "epp_sample_count",
+    "epp_sample_batch", "epp_generate_trajectory_host", "epp_host_free",
+]
+
+
+def check(rc: int) -> None:
+    if rc != EPP_OK:
+        raise EppError(rc, lib().epp_last_error().decode())
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+class DeviceBuffer:
+    """A raw HBM allocation (epp_malloc)."""
+
+    def __init__(self, nbytes: int):
+        p = C.c_void_p()
+        check(lib().epp_malloc(C.byref(p), max(int(nbytes), 16)))
+        self.ptr = p.value
+        self.nbytes = int(nbytes)
+
+    @classmethod
+    def from_array(cls, a: np.ndarray, stream=None) -> "DeviceBuffer":
+        a = np.ascontiguousarray(a)
+        b = cls(a.nbytes)
+        b.upload(a, stream)
+        return b
+
+    def upload(self, a: np.ndarray, stream=None) -> None:
+        a = np.ascontiguousarray(a)
+        assert a.nbytes <= self.nbytes
+        check(lib().epp_memcpy_h2d(self.ptr, _ptr(a), a.nbytes, stream))
+
+    def download(self, dtype, count: int, stream=None) -> np.ndarray:
+        out = np.empty(count, dtype=dtype)
+        assert out.nbytes <= self.nbytes
+        check(lib().epp_memcpy_d2h(_ptr(out), self.ptr, out.nbytes, stream))
+        return out
+
+    def zero(self, stream=None) -> None:
+        check(lib().epp_memset(self.ptr, 0, self.nbytes, stream))
+
+    def free(self) -> None:
+        if self.ptr:
+            lib().epp_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    check(lib().epp_device_count(C.byref(n)))
+    return n.value
+
+
+def sync() -> None:
+    check(lib().epp_device_sync())
+
+
+def build_obbs(geom, gates: np.ndarray, obstacles: np.ndarray) -> np.ndarray:
+    """World::addGate / addObstacle (src/World.cpp:13-55) on the host."""
+    gates = np.ascontiguousarray(np.asarray(gates, np.float64).reshape(-1, 7))
+    obstacles = np.ascontiguousarray(np.asarray(obstacles, np.float64).reshape(-1, 6))
+    cap = len(gates) * max(1, len(geom.gate_desc)) + len(obstacles) * max(1, len(geom.obst_desc))
+    out = np.zeros(max(cap, 1), OBB_DTYPE)
+    n = C.c_int32(0)
+    check(lib().epp_build_obbs(_ptr(geom.gate_desc), _ptr(geom.gate_desc_off), len(geom.gate_desc_off) - 1,
+                               _ptr(geom.obst_desc), len(geom.obst_desc), _ptr(gates), len(gates),
+                               _ptr(obstacles), len(obstacles), _ptr(out), len(out), C.byref(n)))
+    return out[: n.value].copy()
+
+
+class World:
+    """Device-resident OBB table + cull grid (epp_world)."""
+
+    def __init__(self, obbs: np.ndarray, r_gate: float, r_obst: float):
+        obbs = np.ascontiguousarray(obbs, dtype=OBB_DTYPE)
+        h = C.c_void_p()
+        check(lib().epp_world_create(_ptr(obbs) if len(obbs) else None, len(obbs), r_gate, r_obst, C.byref(h)))
+        self.handle = h.value
+        self.n = len(obbs)
+
+    def update(self, obbs: np.ndarray) -> None:
+        obbs = np.ascontiguousarray(obbs, dtype=OBB_DTYPE)
+        check(lib().epp_world_update(self.handle, _ptr(obbs) if len(obbs) else None, len(obbs)))
+        self.n = len(obbs)
+
+    def aabbs(self) -> np.ndarray:
+        out = np.zeros((max(self.n, 1), 6))
+        check(lib().epp_world_get_aabbs(self.handle, _ptr(out)))
+        return out[: self.n]
+
+    def close(self) -> None:
+        if self.handle:
+            lib().epp_world_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- device-pointer calls ----------------------------------------------------
+    def check_states_dev(self, xyz_ptr, n, can_pass_gate, valid_ptr, compact_ptr=None, nvalid_ptr=None,
+                         stream=None):
+        check(lib().epp_check_states(self.handle, xyz_ptr, n, int(can_pass_gate), valid_ptr, compact_ptr,
+                                     nvalid_ptr, stream))
+
+    def check_motions_dev(self, s1_ptr, s2_ptr, n, can_pass_gate, mode, valid_ptr, stream=None):
+        check(lib().epp_check_motions(self.handle, s1_ptr, s2_ptr, n, int(can_pass_gate), int(mode),
+                                      valid_ptr, stream))
+
+    # ---- host-array convenience (copies in/out) ----------------------------------
+    def check_states(self, xyz: np.ndarray, can_pass_gate: bool = False, compact: bool = False):
+        xyz = np.ascontiguousarray(xyz, np.float64).reshape(-1, 3)
+        n = len(xyz)
+        d_xyz = DeviceBuffer.from_array(xyz)
+        d_valid = DeviceBuffer(n)
+        if compact:
+            d_idx = DeviceBuffer(4 * max(n, 1))
+            d_cnt = DeviceBuffer(8)
+            d_cnt.zero()
+            self.check_states_dev(d_xyz.ptr, n, can_pass_gate, d_valid.ptr, d_idx.ptr, d_cnt.ptr)
+            sync()
+            cnt = int(d_cnt.download(np.int64, 1)[0])
+            return d_valid.download(np.uint8, n), d_idx.download(np.int32, cnt)
+        self.check_states_dev(d_xyz.ptr, n, can_pass_gate, d_valid.ptr)
+        sync()
+        return d_valid.download(np.uint8, n)
+
+    def check_states_mindist(self, xyz: np.ndarray, min_distance: float) -> np.ndarray:
+        xyz = np.ascontiguousarray(xyz, np.float64).reshape(-1, 3)
+        n = len(xyz)
+        d_xyz = DeviceBuffer.from_array(xyz)
+        d_valid = DeviceBuffer(n)
+        check(lib().epp_check_states_mindist(self.handle, d_xyz.ptr, n, float(min_distance), d_valid.ptr, None))
+        sync()
+        return d_valid.download(np.uint8, n)
+
+    def check_motions(self, s1: np.ndarray, s2: np.ndarray, can_pass_gate: bool = False, mode: int = 0):
+        s1 = np.ascontiguousarray(s1, np.float64).reshape(-1, 3)
+        s2 = np.ascontiguousarray(s2, np.float64).reshape(-1, 3)
+        n = len(s1)
+        d1, d2 = DeviceBuffer.from_array(s1), DeviceBuffer.from_array(s2)
+        d_valid = DeviceBuffer(n)
+        self.check_motions_dev(d1.ptr, d2.ptr, n, can_pass_gate, mode, d_valid.ptr)
+        sync()
+        return d_valid.download(np.uint8, n)
+
+
+def minsnap_batch(tracks, v_max, a_max, v0=None, a0=None):
+    """epp_minsnap_batch on a list of (W_k x 3) waypoint arrays.
+
+    Returns (seg_times list, coeffs list [M_k x 3 x 10], status array)."""
+    wp = np.ascontiguousarray(np.concatenate([np.asarray(t, np.float64).reshape(-1, 3) for t in tracks]))
+    off = np.zeros(len(tracks) + 1, np.int32)
+    off[1:] = np.cumsum([len(t) for t in tracks])
+    nt = len(tracks)
+    nseg = int(off[-1]) - nt
+    d_wp, d_off = DeviceBuffer.from_array(wp), DeviceBuffer.from_array(off)
+    d_v0 = DeviceBuffer.from_array(np.ascontiguousarray(v0, np.float64)) if v0 is not None else None
+    d_a0 = DeviceBuffer.from_array(np.ascontiguousarray(a0, np.float64)) if a0 is not None else None
+    d_T, d_C, d_st = DeviceBuffer(8 * max(nseg, 1)), DeviceBuffer(240 * max(nseg, 1)), DeviceBuffer(4 * nt)
+    check(lib().epp_minsnap_batch(d_wp.ptr, d_off.ptr, nt, float(v_max), float(a_max),
+                                  d_v0.ptr if d_v0 else None, d_a0.ptr if d_a0 else None,
+                                  d_T.ptr, d_C.ptr, d_st.ptr, None))
+    sync()
+    T = d_T.download(np.float64, nseg)
+    Cf = d_C.download(np.float64, nseg * 30).reshape(nseg, 3, 10)
+    st = d_st.download(np.int32, nt)
+    Ts, Cs = [], []
+    for k in range(nt):
+        a, b = int(off[k]) - k, int(off[k + 1]) - k - 1
+        Ts.append(T[a:max(a, b)])
+        Cs.append(Cf[a:max(a, b)])
+    return Ts, Cs, st
+
+
+def generate_trajectory(waypoints, v_max, a_max, dt, t0=0.0, v0=(0, 0, 0), a0=(0, 0, 0)) -> np.ndarray:
+    """poly_traj::generateTrajectory (src/trajectory_generator.cpp:12-100) on the GPU."""
+    wp = np.ascontiguousarray(np.asarray(waypoints, np.float64).reshape(-1, 3))
+    v0 = np.ascontiguousarray(v0, np.float64)
+    a0 = np.ascontiguousarray(a0, np.float64)
+    rows = C.POINTER(C.c_double)()
+    n = C.c_int64(0)
+    check(lib().epp_generate_trajectory_host(_ptr(wp), len(wp), float(v_max), float(a_max), float(dt), float(t0),
+                                             _ptr(v0), _ptr(a0), C.byref(rows), C.byref(n)))
+    if n.value == 0:
+        return np.zeros((0, 10))
+    out = np.ctypeslib.as_array(rows, shape=(n.value * 10,)).copy().reshape(-1, 10)
+    lib().epp_host_free(C.cast(rows, C.c_void_p))
+    return out

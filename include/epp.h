@@ -1,0 +1,161 @@
+/*
+ * epp.h — C ABI of the MI355X-native Efficient-Path-Planner hot path.
+ *
+ * Plain pointers and sizes only; no torch / Eigen / OMPL types.  Every compute
+ * entry point is stream-ordered on the hipStream_t passed as `void* stream`
+ * (NULL = the null stream) and takes DEVICE pointers for bulk data.  All
+ * functions return an epp_status (0 = ok, < 0 = error); the message of the last
+ * error on the calling thread is available from epp_last_error().
+ *
+ * Reference interfaces each entry point replaces (paths relative to the
+ * reference repository root):
+ *
+ *   epp_world_create / epp_world_update
+ *       World::addGate / addObstacle / updateGatePosition / resetWorld
+ *       (include/World.h:27-56, src/World.cpp:13-78) — OBB table + AABB index
+ *       (the Boost rtree `index`, include/World.h:109) uploaded to HBM.
+ *   epp_check_states
+ *       StateValidator::isValid (include/StateValidator.h:31, src/StateValidator.cpp:7-13)
+ *       -> World::checkPointValidity(p, canPassGate) (src/World.cpp:80-104), batched.
+ *   epp_check_states_mindist
+ *       World::checkPointValidity(p, minDistance) (src/World.cpp:106-128) as used by
+ *       PathPlanner::checkTrajectoryValidity (src/PathPlanner.cpp:267-280).
+ *   epp_check_motions
+ *       MotionValidator::checkMotion (include/MotionValidator.h:26, src/MotionValidator.cpp:8-17)
+ *       -> World::checkRayValid (src/World.cpp:130-162), batched; mode 1 adds the
+ *       32-step discretised check of BASELINE config 3.
+ *   epp_minsnap_batch / epp_sample_count / epp_sample_batch
+ *       poly_traj::generateTrajectory (external/poly_traj/include/poly_traj/trajectory_generator.h:20,
+ *       external/poly_traj/src/trajectory_generator.cpp:12-100), batched over tracks.
+ */
+#ifndef EPP_H_
+#define EPP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t epp_status;
+#define EPP_OK 0
+#define EPP_ERR_INVALID_ARGUMENT (-1) /* std::invalid_argument in the reference */
+#define EPP_ERR_RUNTIME (-2)          /* std::runtime_error in the reference */
+#define EPP_ERR_HIP (-3)              /* HIP runtime error */
+#define EPP_ERR_UNSUPPORTED (-4)      /* rotation other than about z (src/Object.cpp:38-47) */
+#define EPP_ERR_CAPACITY (-5)         /* an output buffer was too small */
+
+/* An oriented bounding box after the world build (reference class OBB,
+ * include/OBB.h:19-57).  rot is the row-major rotation matrix; the reference only
+ * produces rotations about z (src/Object.cpp:61-85) and so does this ABI. */
+typedef struct epp_obb {
+    double center[3];
+    double half[3];
+    double rot[9];
+    int32_t filling; /* OBB::type == "filling" (else "collision") */
+    int32_t is_gate; /* World key contains "gate": selects the gate inflate radius */
+} epp_obb;
+
+/* One OBB of a component's geometry (config `component_geometry.<comp>.<obb>`,
+ * src/ConfigParserYAML.cpp:54-73): position relative to the component origin and
+ * full size (the half size is size / 2). */
+typedef struct epp_obb_desc {
+    double pos[3];
+    double size[3];
+    int32_t filling; /* "filling" (1) or "collision" (0) */
+    int32_t pad;
+} epp_obb_desc;
+
+typedef struct epp_world epp_world; /* opaque, bound to one device */
+
+/* ---- runtime ---------------------------------------------------------------------- */
+const char* epp_last_error(void);
+const char* epp_version(void);
+epp_status epp_device_count(int* count);
+epp_status epp_set_device(int device);
+epp_status epp_malloc(void** ptr, uint64_t bytes);
+epp_status epp_free(void* ptr);
+epp_status epp_memcpy_h2d(void* dst, const void* src, uint64_t bytes, void* stream);
+epp_status epp_memcpy_d2h(void* dst, const void* src, uint64_t bytes, void* stream);
+epp_status epp_memset(void* dst, int value, uint64_t bytes, void* stream);
+epp_status epp_stream_create(void** stream);
+epp_status epp_stream_destroy(void* stream);
+epp_status epp_stream_sync(void* stream);
+epp_status epp_device_sync(void);
+epp_status epp_event_create(void** event);
+epp_status epp_event_destroy(void* event);
+epp_status epp_event_record(void* event, void* stream);
+epp_status epp_event_elapsed_ms(void* start, void* stop, float* ms);
+
+/* ---- world ------------------------------------------------------------------------ */
+/* World::addGate / World::addObstacle (src/World.cpp:13-55) via
+ * Object::createFromDescription (src/Object.cpp:26-85), on the host.
+ * gates: n_gates x 7 row-major (x, y, z, roll, pitch, yaw, type) — z is forced to 0
+ * (src/PathPlanner.cpp:68); obstacles: n_obstacles x 6 (x, y, z, roll, pitch, yaw).
+ * Gate type t uses gate_desc[gate_desc_off[t] .. gate_desc_off[t+1]).  Errors:
+ * EPP_ERR_UNSUPPORTED for |roll| or |pitch| > 1e-6, EPP_ERR_RUNTIME for an object
+ * centre z > 1e-6 or an unknown gate type, EPP_ERR_CAPACITY if out is too small
+ * (*n_out then holds the required count). */
+epp_status epp_build_obbs(const epp_obb_desc* gate_desc, const int32_t* gate_desc_off,
+                          int32_t n_gate_types, const epp_obb_desc* obst_desc, int32_t n_obst_desc,
+                          const double* gates, int32_t n_gates, const double* obstacles,
+                          int32_t n_obstacles, epp_obb* out, int32_t capacity, int32_t* n_out);
+
+/* Builds the AABB of every OBB (OBB::getAABB, src/OBB.cpp:93-123, inflated only for
+ * "collision" OBBs by r_gate or r_obst) and a uniform cull grid over them, and
+ * uploads both to the current device.  obbs is a HOST array. */
+epp_status epp_world_create(const epp_obb* obbs, int32_t n_obbs, double r_gate, double r_obst,
+                            epp_world** out);
+/* Replaces the OBB set (gate-pose update = full rebuild, src/OnlineTrajGenerator.cpp:146). */
+epp_status epp_world_update(epp_world* w, const epp_obb* obbs, int32_t n_obbs);
+epp_status epp_world_destroy(epp_world* w);
+epp_status epp_world_num_obbs(const epp_world* w, int32_t* n);
+/* Host copy of the AABBs computed for the index (lo[3], hi[3] per OBB). */
+epp_status epp_world_get_aabbs(const epp_world* w, double* lo_hi);
+
+/* ---- collision checks (device pointers) ------------------------------------------- */
+/* xyz: n x 3 f64 (AoS).  valid[i] = 1 if state i is collision free.  If compact_idx
+ * is non-NULL, the indices of valid states are appended to it and *n_valid (device
+ * int64, caller zeroes it) receives the count; the order of the compacted indices
+ * is unspecified (wavefront order is preserved, inter-wavefront order is not). */
+epp_status epp_check_states(const epp_world* w, const double* xyz, int64_t n, int32_t can_pass_gate,
+                            uint8_t* valid, int32_t* compact_idx, int64_t* n_valid, void* stream);
+epp_status epp_check_states_mindist(const epp_world* w, const double* xyz, int64_t n,
+                                    double min_distance, uint8_t* valid, void* stream);
+/* s1, s2: n x 3 f64.  mode 0 = analytic slab test (reference), 1 = discrete32:
+ * points s1 + (s2 - s1) * (k/32), k = 1..32, each checked like epp_check_states. */
+epp_status epp_check_motions(const epp_world* w, const double* s1, const double* s2, int64_t n,
+                             int32_t can_pass_gate, int32_t mode, uint8_t* valid, void* stream);
+
+/* ---- min-snap trajectory (device pointers) ---------------------------------------- */
+/* Track k owns waypoints [wp_offsets[k], wp_offsets[k+1]) of wp (x,y,z f64) and
+ * segments [wp_offsets[k]-k, wp_offsets[k+1]-k-1).  v0/a0: n_tracks x 3 (NULL = 0).
+ * Outputs: seg_times (total segments), coeffs (total segments x 3 x 10, increasing
+ * powers, the layout of mav_trajectory_generation::Polynomial).  status (n_tracks,
+ * may be NULL): 0 ok, -1 fewer than 2 waypoints, -2 non-positive segment time,
+ * -3 solver breakdown. */
+epp_status epp_minsnap_batch(const double* wp, const int32_t* wp_offsets, int32_t n_tracks,
+                             double v_max, double a_max, const double* v0, const double* a0,
+                             double* seg_times, double* coeffs, int32_t* status, void* stream);
+/* Number of rows Trajectory::evaluateRange produces for every track (device int64 out). */
+epp_status epp_sample_count(const double* seg_times, const int32_t* wp_offsets, int32_t n_tracks,
+                            double dt, int64_t* row_counts, void* stream);
+/* rows: written at row_offsets[k] (device int64, exclusive scan of the counts), each
+ * row [x,vx,ax,y,vy,ay,z,vz,az,t+t0[k]]; t0 may be NULL (= 0). */
+epp_status epp_sample_batch(const double* seg_times, const double* coeffs,
+                            const int32_t* wp_offsets, int32_t n_tracks, double dt, const double* t0,
+                            const int64_t* row_offsets, double* rows, void* stream);
+
+/* ---- host-buffer convenience (synchronous; used by the C++ API shims) ------------- */
+/* generateTrajectory for one track with host buffers.  Returns the row count in
+ * *n_rows; rows is (re)allocated with malloc and must be released with epp_host_free. */
+epp_status epp_generate_trajectory_host(const double* wp, int32_t n_wp, double v_max, double a_max,
+                                        double dt, double t0, const double v0[3], const double a0[3],
+                                        double** rows, int64_t* n_rows);
+void epp_host_free(void* p);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* EPP_H_ */

@@ -1,0 +1,64 @@
+"""CPU tests of the product boundary: libepp.so loads, exports every symbol of
+include/epp.h, and its host-side world build (no GPU involved) matches the oracle
+bit for bit."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle as O
+from eppamd import capi, config, synth
+
+from conftest import ROOT
+
+
+def _header_functions():
+    src = open(os.path.join(ROOT, "include", "epp.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(epp_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = ctypes.CDLL(capi.LIB_PATH)
+    declared = _header_functions()
+    assert len(declared) >= 25
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert sorted(capi.EXPORTED) == declared
+
+
+def test_pybind_modules_present():
+    pkg = os.path.join(ROOT, "efficient-path-planner_amd")
+    names = os.listdir(pkg)
+    for mod in ("polynomial_trajectory",):
+        assert any(n.startswith(mod) and n.endswith(".so") for n in names), mod
+
+
+@pytest.mark.parametrize("seed", [42, 100, 107])
+def test_build_obbs_matches_oracle(cfg, geom, seed):
+    rg, ro = config.inflate_radii(cfg)
+    gates, obstacles = synth.track_world(seed)
+    mine = capi.build_obbs(geom, gates, obstacles)
+    ref = O.world_build(geom, gates, obstacles, rg, ro)
+    assert len(mine) == len(ref) == 8 * 5 + 24
+    for f in ("center", "half", "rot"):
+        assert np.array_equal(mine[f], ref[f]), f
+    assert np.array_equal(mine["filling"], ref["filling"])
+    assert np.array_equal(mine["is_gate"], ref["is_gate"])
+
+
+def test_build_obbs_errors(geom):
+    with pytest.raises(capi.EppError) as e:
+        capi.build_obbs(geom, [[0, 0, 0, 0.0, 0.2, 0, 0]], np.zeros((0, 6)))
+    assert e.value.code == capi.EPP_ERR_UNSUPPORTED and "y axis" in str(e.value)
+    with pytest.raises(capi.EppError) as e:
+        capi.build_obbs(geom, np.zeros((0, 7)), [[0, 0, 0.01, 0, 0, 0]])
+    assert e.value.code == capi.EPP_ERR_RUNTIME and "z position" in str(e.value)
+    with pytest.raises(capi.EppError):
+        capi.build_obbs(geom, [[0, 0, 0, 0, 0, 0, 7]], np.zeros((0, 6)))
+    # gate z is forced to 0 (src/PathPlanner.cpp:68); negative obstacle z is accepted
+    a = capi.build_obbs(geom, [[1, 2, 3.0, 0, 0, 0.3, 1]], [[0, 0, -0.5, 0, 0, 0]])
+    b = capi.build_obbs(geom, [[1, 2, 0.0, 0, 0, 0.3, 1]], [[0, 0, -0.5, 0, 0, 0]])
+    assert np.array_equal(a, b)

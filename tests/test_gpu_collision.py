@@ -1,0 +1,196 @@
+"""GPU parity: OBB validity kernels (through the C ABI) vs the CPU oracle, bit-exact.
+
+Reference semantics: src/World.cpp:80-162, src/OBB.cpp:10-123.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from eppamd import capi, config, synth
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _worlds(cfg, geom):
+    rg, ro = config.inflate_radii(cfg)
+    out = {}
+    g, o, _, _ = synth.c1_world()
+    out["c1"] = (g, o, synth.C1_BOUNDS)
+    out["c2"] = synth.track_world(42) + (synth.C2_BOUNDS,)
+    g3, o3 = synth.track_world(42, n_obstacles=472)
+    out["c3"] = (g3, o3, synth.C2_BOUNDS)
+    return rg, ro, out
+
+
+def _adversarial_points(ref_w):
+    """Points exactly on / one ulp around every AABB face and corner."""
+    pts = []
+    for o in ref_w:
+        mid = (o["aabb_lo"] + o["aabb_hi"]) / 2
+        for k in range(3):
+            for v in (o["aabb_lo"][k], o["aabb_hi"][k]):
+                for w in (v, np.nextafter(v, np.inf), np.nextafter(v, -np.inf)):
+                    p = mid.copy()
+                    p[k] = w
+                    pts.append(p)
+        pts += [o["aabb_lo"].copy(), o["aabb_hi"].copy(), np.nextafter(o["aabb_hi"], -np.inf),
+                np.nextafter(o["aabb_lo"], np.inf), o["center"].copy()]
+        # points on the inflated OBB faces in local coordinates
+        c, s = o["rot"][0], o["rot"][3]
+        for sx in (-1, 1):
+            l = np.array([sx * (o["half"][0] + 0.2), 0.3 * o["half"][1], 0.0])
+            pts.append(o["center"] + np.array([c * l[0] - s * l[1], s * l[0] + c * l[1], l[2]]))
+    return np.array(pts)
+
+
+@pytest.fixture(scope="module")
+def worlds(cfg, geom):
+    return _worlds(cfg, geom)
+
+
+@pytest.mark.parametrize("name", ["c1", "c2", "c3"])
+def test_aabbs_match_oracle(geom, worlds, name):
+    rg, ro, ws = worlds
+    gates, obstacles, _ = ws[name]
+    obbs = capi.build_obbs(geom, gates, obstacles)
+    ref = O.world_build(geom, gates, obstacles, rg, ro)
+    w = capi.World(obbs, rg, ro)
+    a = w.aabbs()
+    assert np.array_equal(a[:, :3], ref["aabb_lo"]) and np.array_equal(a[:, 3:], ref["aabb_hi"])
+
+
+@pytest.mark.parametrize("name", ["c1", "c2", "c3"])
+@pytest.mark.parametrize("can_pass", [0, 1])
+def test_states_bit_exact(geom, worlds, name, can_pass):
+    rg, ro, ws = worlds
+    gates, obstacles, (lo, hi) = ws[name]
+    ref = O.world_build(geom, gates, obstacles, rg, ro)
+    w = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
+    pts = np.vstack([synth.sample_states(7, lo, hi, 200_003), _adversarial_points(ref)])
+    got = w.check_states(pts, can_pass)
+    exp = O.check_states(ref, rg, ro, pts, can_pass, threads=8)
+    assert exp.min() == 0 and exp.max() == 1  # both outcomes exercised
+    assert np.array_equal(got, exp), np.flatnonzero(got != exp)[:10]
+
+
+@pytest.mark.parametrize("name", ["c1", "c2"])
+def test_states_mindist(geom, worlds, name):
+    rg, ro, ws = worlds
+    gates, obstacles, (lo, hi) = ws[name]
+    ref = O.world_build(geom, gates, obstacles, rg, ro)
+    w = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
+    pts = np.vstack([synth.sample_states(9, lo, hi, 100_001), _adversarial_points(ref)])
+    for md in (0.0, 0.1, 0.2, 0.35):
+        got = w.check_states_mindist(pts, md)
+        exp = O.check_states_mindist(ref, pts, md)
+        assert np.array_equal(got, exp), md
+
+
+def test_compaction(geom, worlds):
+    rg, ro, ws = worlds
+    gates, obstacles, (lo, hi) = ws["c2"]
+    ref = O.world_build(geom, gates, obstacles, rg, ro)
+    w = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
+    pts = synth.sample_states(21, lo, hi, 65_537)
+    valid, idx = w.check_states(pts, False, compact=True)
+    exp = O.check_states(ref, rg, ro, pts, False, threads=8)
+    assert np.array_equal(valid, exp)
+    assert np.array_equal(np.sort(idx), np.flatnonzero(exp))
+
+
+@pytest.mark.parametrize("name", ["c1", "c2", "c3"])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_motions_bit_exact(geom, worlds, name, mode):
+    rg, ro, ws = worlds
+    gates, obstacles, (lo, hi) = ws[name]
+    ref = O.world_build(geom, gates, obstacles, rg, ro)
+    w = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
+    n = 100_000 if mode == 0 else 20_000
+    s1, s2 = synth.edges(43, 8, lo, hi, n, max_len=0.5 if name != "c1" else 1.5)
+    # near-parallel edges (|d_i| around the 1e-6 threshold of src/OBB.cpp:34)
+    k = 2000
+    t1 = synth.sample_states(5, lo, hi, k)
+    t2 = t1.copy()
+    t2[:, 0] += 0.8
+    t2[:, 1] += np.where(np.arange(k) % 2, 9.9e-7, 1.01e-6)
+    s1, s2 = np.vstack([s1, t1]), np.vstack([s2, t2])
+    for cp in (0, 1):
+        got = w.check_motions(s1, s2, cp, mode)
+        exp = O.check_motions(ref, rg, ro, s1, s2, cp, mode, threads=8)
+        assert exp.min() == 0 and exp.max() == 1
+        assert np.array_equal(got, exp), (cp, np.flatnonzero(got != exp)[:10])
+
+
+def test_boundary_known_answers():
+    f = json.load(open(os.path.join(GOLDEN, "obb_boundary.json")))
+
+    def descs(lst):
+        a = np.zeros(len(lst), config.OBB_DESC_DTYPE)
+        for i, d in enumerate(lst):
+            a[i]["pos"], a[i]["size"], a[i]["filling"] = d["pos"], d["size"], d["filling"]
+        return a
+    g = config.Geometry(descs(f["gate_desc"]), np.array([0, len(f["gate_desc"])], np.int32),
+                        descs(f["obst_desc"]), np.array([1.0]))
+    w = capi.World(capi.build_obbs(g, f["gates"], f["obstacles"]), f["r_gate"], f["r_obst"])
+    for c in f["points"]:
+        assert w.check_states(np.array([c["p"]]), c["can_pass"])[0] == c["valid"], c
+    for c in f["mindist"]:
+        assert w.check_states_mindist(np.array([c["p"]]), c["md"])[0] == c["valid"], c
+    for c in f["rays"]:
+        got = w.check_motions(np.array([c["s"]]), np.array([c["e"]]), c["can_pass"], c["mode"])[0]
+        assert got == c["valid"], c
+
+
+def test_golden_c1_states(geom):
+    f = json.load(open(os.path.join(GOLDEN, "c1_states.json")))
+    w = capi.World(capi.build_obbs(geom, f["gates"], f["obstacles"]), f["r_gate"], f["r_obst"])
+    for cp in ("0", "1"):
+        assert w.check_states(np.array(f["states"]), int(cp)).tolist() == f["valid"][cp]
+
+
+def test_edge_sizes_and_alignment(geom, worlds):
+    rg, ro, ws = worlds
+    gates, obstacles, (lo, hi) = ws["c2"]
+    ref = O.world_build(geom, gates, obstacles, rg, ro)
+    w = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
+    pts = synth.sample_states(3, lo, hi, 4099)
+    exp = O.check_states(ref, rg, ro, pts, False)
+    for n in (0, 1, 2, 3, 4, 5, 63, 64, 65, 255, 257, 1023, 4099):
+        assert np.array_equal(w.check_states(pts[:n]), exp[:n]), n
+    # unaligned input/output pointers (8-byte aligned xyz, odd flag offset)
+    d = capi.DeviceBuffer(8 * 3 * 4099 + 64)
+    d.upload(np.concatenate([[0.0], pts.ravel()]))
+    v = capi.DeviceBuffer(4099 + 8)
+    w.check_states_dev(d.ptr + 8, 4099, 0, v.ptr + 1)
+    capi.sync()
+    got = v.download(np.uint8, 4100)[1:]
+    assert np.array_equal(got, exp)
+
+
+def test_empty_world_and_update(geom, worlds):
+    rg, ro, ws = worlds
+    w = capi.World(np.zeros(0, capi.OBB_DTYPE), rg, ro)
+    pts = synth.sample_states(3, *synth.C2_BOUNDS, 1000)
+    assert w.check_states(pts).all()
+    assert w.check_motions(pts, pts[::-1].copy()).all()
+    gates, obstacles, _ = ws["c2"]
+    w.update(capi.build_obbs(geom, gates, obstacles))
+    ref = O.world_build(geom, gates, obstacles, rg, ro)
+    assert np.array_equal(w.check_states(pts), O.check_states(ref, rg, ro, pts))
+
+
+def test_global_memory_path_large_world(cfg, geom):
+    """A world whose index exceeds the LDS budget runs the global-memory kernel variant."""
+    rg, ro = config.inflate_radii(cfg)
+    gates, obstacles = synth.track_world(5, n_gates=8, n_obstacles=3000)
+    ref = O.world_build(geom, gates, obstacles, rg, ro)
+    w = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
+    pts = synth.sample_states(4, *synth.C2_BOUNDS, 50_000)
+    assert np.array_equal(w.check_states(pts), O.check_states(ref, rg, ro, pts, threads=8))
+    s1, s2 = synth.edges(1, 2, *synth.C2_BOUNDS, 20_000)
+    assert np.array_equal(w.check_motions(s1, s2), O.check_motions(ref, rg, ro, s1, s2, threads=8))

@@ -1,0 +1,277 @@
+"""CPU tests: pin the oracle against the reference's own known answers and invariants.
+
+Reference tests mirrored here: external/poly_traj/test/test_polynomial_optimization.cpp
+(TwoVerticesSetup :743-787, AMatrixInversion :731-741, checkPath :113-174,
+ConstraintPacking :505-564, TimeAllocation :566-606) and the hand-derived World/OBB
+known answers in tests/golden/obb_boundary.json.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import minsnap_np
+import oracle as O
+import pyref_obb
+from eppamd import config, synth
+from eppamd.config import OBB_DESC_DTYPE, Geometry
+
+from conftest import GOLDEN
+
+REF = json.load(open(os.path.join(GOLDEN, "reference_minsnap.json")))
+
+
+def _vertex_constraints(wp, max_derivative=4):
+    """createRandomVertices vertex set: ends fixed up to max_derivative (p, then 0), inner p."""
+    W, D = wp.shape
+    mask = np.zeros((W, 5), np.uint8)
+    val = np.zeros((W, 5, D))
+    for v in range(W):
+        mask[v, 0] = 1
+        val[v, 0] = wp[v]
+    for v in (0, W - 1):
+        mask[v, : max_derivative + 1] = 1
+    return mask, val
+
+
+def test_two_vertices_setup_golden():
+    c = REF["two_vertices_setup"]
+    mask = np.ones((2, 5), np.uint8)
+    val = np.zeros((2, 5, 1))
+    val[0, 0, 0], val[1, 0, 0] = c["start_x"], c["goal_x"]
+    coeffs = O.minsnap_solve(mask, val, [c["segment_time"]], 1, c["derivative"])[0, 0]
+    np.testing.assert_allclose(coeffs, c["matlab_coeffs"], rtol=0, atol=c["tolerance"])
+
+
+def test_a_matrix_inversion():
+    c = REF["a_matrix_inversion"]
+    for t in range(c["t_min"], c["t_max"] + 1):
+        A = O.mapping_matrix(float(t))
+        Ai = O.invert_mapping(A)
+        assert np.abs(Ai - np.linalg.inv(A)).max() < c["tolerance"], t
+
+
+def _check_path(wp, times, coeffs, mask, val, tol):
+    """checkPath: fixed constraints met, C0..C4 continuity at every vertex (tol 1e-6)."""
+    M = len(times)
+    D = wp.shape[1]
+    for i in range(M):
+        for k in range(5):
+            for d in range(D):
+                beg = O.poly_eval(coeffs[i, d], 0.0, k)
+                end = O.poly_eval(coeffs[i, d], times[i], k)
+                if mask[i, k]:
+                    assert abs(beg - val[i, k, d]) < tol
+                if mask[i + 1, k]:
+                    assert abs(end - val[i + 1, k, d]) < tol
+                if i > 0:
+                    prev = O.poly_eval(coeffs[i - 1, d], times[i - 1], k)
+                    assert abs(prev - beg) < tol
+
+
+@pytest.mark.parametrize("ps", REF["parameter_sets"], ids=lambda p: p["name"])
+def test_unconstrained_linear_estimate_segment_times(ps):
+    D = ps["D"]
+    wp = O.random_vertices(ps["segments"], D, -ps["pos"], ps["pos"], ps["seed"])
+    assert wp.shape == (ps["segments"] + 1, D)
+    assert (wp <= ps["pos"]).all() and (wp >= -ps["pos"]).all()  # VertexGeneration
+    times = O.segment_times(wp, ps["v_max"], ps["a_max"])
+    assert ((times > 0) & (times < REF["time_allocation"]["upper"])).all()  # TimeAllocation
+    mask, val = _vertex_constraints(wp)
+    coeffs = O.minsnap_solve(mask, val, times, D, ps["deriv"])
+    _check_path(wp, times, coeffs, mask, val, REF["check_path_tolerance"]["tol"])
+    # v/a within 2.5x limits (numerical maximum, test_utils.h getMaximumMagnitude)
+    if ps["deriv"] == 4:
+        vm = am = 0.0
+        for i in range(len(times)):
+            for t in np.arange(0, times[i], 0.01):
+                v = [O.poly_eval(coeffs[i, d], t, 1) for d in range(D)]
+                a = [O.poly_eval(coeffs[i, d], t, 2) for d in range(D)]
+                vm, am = max(vm, np.linalg.norm(v)), max(am, np.linalg.norm(a))
+        assert vm < 2.5 * ps["v_max"] and am < 2.5 * ps["a_max"]
+
+
+@pytest.mark.parametrize("D", [1, 3])
+def test_constraint_packing(D):
+    c = REF["constraint_packing"]
+    for k in range(c["setups"]):
+        wp = O.random_vertices(10, D, -c["pos"], c["pos"], c["seed"] + k)
+        times = O.segment_times(wp, c["v_max"], c["a_max"])
+        mask, val = _vertex_constraints(wp)
+        coeffs = O.minsnap_solve(mask, val, times, D, 4)
+        # p -> d: A_i p_i reproduces [d(vertex i); d(vertex i+1)] and is continuous
+        for i, T in enumerate(times):
+            A = O.mapping_matrix(T)
+            for d in range(D):
+                dd = A @ coeffs[i, d]
+                if i > 0:
+                    prev = O.mapping_matrix(times[i - 1]) @ coeffs[i - 1, d]
+                    np.testing.assert_allclose(dd[:5], prev[5:], atol=c["tol"])
+                np.testing.assert_allclose(dd[0], wp[i, d], atol=c["tol"])
+                np.testing.assert_allclose(dd[5], wp[i + 1, d], atol=c["tol"])
+
+
+def test_oracle_vs_numpy_kkt():
+    """Independent formulation (KKT in normalised time) agrees with the oracle."""
+    for s in range(6):
+        wp = synth.random_track_waypoints(50 + s, 12)
+        T, Cf = O.minsnap_track(wp, 1.0, 2.0)
+        Cn = minsnap_np.track(wp, T)
+        assert np.abs(Cf - Cn).max() < 1e-7
+
+
+def test_oracle_vs_high_precision():
+    """30-digit KKT solve (mpmath) on a small track pins the absolute accuracy."""
+    mp = pytest.importorskip("mpmath")
+    from math import factorial
+    mp.mp.dps = 30
+    wp = synth.random_track_waypoints(7, 4)
+    T, Cf = O.minsnap_track(wp, 1.0, 2.0)
+    N, K, M = 10, 4, len(T)
+    ff = lambda j, k: mp.mpf(factorial(j)) / factorial(j - k) if j >= k else mp.mpf(0)  # noqa: E731
+    Tm = [mp.mpf(float(t)) for t in T]
+    nv = N * M
+    fixed = {(0, k): (wp[0] if k == 0 else np.zeros(3)) for k in range(5)}
+    fixed.update({(M, k): (wp[M] if k == 0 else np.zeros(3)) for k in range(5)})
+    fixed.update({(v, 0): wp[v] for v in range(1, M)})
+    rows, rhs = [], []
+
+    def drow(k, tau, seg):
+        r = [mp.mpf(0)] * nv
+        for j in range(k, N):
+            r[N * seg + j] = ff(j, k) * (mp.mpf(tau) ** (j - k) if j > k else 1) / Tm[seg] ** k
+        return r
+    for v in range(M + 1):
+        for k in range(5):
+            if (v, k) in fixed:
+                for seg, tau in ((v - 1, 1), (v, 0)):
+                    if 0 <= seg < M:
+                        rows.append(drow(k, tau, seg))
+                        rhs.append([mp.mpf(float(x)) for x in fixed[(v, k)]])
+            elif 0 < v < M:
+                a, b = drow(k, 1, v - 1), drow(k, 0, v)
+                rows.append([x - y for x, y in zip(a, b)])
+                rhs.append([mp.mpf(0)] * 3)
+    nc = len(rows)
+    A = mp.zeros(nv + nc, nv + nc)
+    for i in range(M):
+        for a in range(K, N):
+            for b in range(K, N):
+                A[N * i + a, N * i + b] = 2 * ff(a, K) * ff(b, K) / (a + b - 2 * K + 1) / Tm[i] ** (2 * K - 1)
+    for r in range(nc):
+        for c in range(nv):
+            if rows[r][c] != 0:
+                A[nv + r, c] = rows[r][c]
+                A[c, nv + r] = rows[r][c]
+    for d in range(3):
+        x = mp.lu_solve(A, mp.matrix([0] * nv + [rhs[r][d] for r in range(nc)]))
+        exact = np.array([[float(x[N * i + j] / Tm[i] ** j) for j in range(N)] for i in range(M)])
+        assert np.abs(Cf[:, d, :] - exact).max() < 1e-7  # well inside the 1e-6 parity budget
+
+
+def test_evaluate_range_recurrence():
+    """Sample count/time column follow Trajectory::evaluateRange (src/trajectory.cpp:81-141)."""
+    wp = synth.random_track_waypoints(3, 5)
+    T, Cf = O.minsnap_track(wp, 1.0, 2.0)
+    rows = O.sample_traj(T, Cf, 0.1, t0=2.0)
+    acc, i, tis, times = 0.0, 0, 0.0, []
+    t_end = 0.0
+    for t in T:
+        t_end += t
+    while acc < t_end:
+        if tis > T[i]:
+            tis -= T[i]
+            i += 1
+            if i >= len(T):
+                break
+            continue
+        times.append(acc + 2.0)
+        tis += 0.1
+        acc += 0.1
+    assert len(rows) == len(times)
+    assert (rows[:, 9] == np.array(times)).all()
+    assert abs(rows[0, 0] - wp[0, 0]) < 1e-12 and abs(rows[0, 1]) < 1e-12
+
+
+def test_golden_tracks_oracle():
+    g = json.load(open(os.path.join(GOLDEN, "minsnap_tracks.json")))
+    for tr in g["tracks"][:6]:
+        T, Cf = O.minsnap_track(np.array(tr["wp"]), tr["v_max"], tr["a_max"], tr["v0"], tr["a0"])
+        assert np.array_equal(T, np.array(tr["times"]))
+        assert np.abs(Cf - np.array(tr["coeffs"])).max() < 1e-12
+
+
+def _boundary_world():
+    f = json.load(open(os.path.join(GOLDEN, "obb_boundary.json")))
+
+    def descs(lst):
+        a = np.zeros(len(lst), OBB_DESC_DTYPE)
+        for i, d in enumerate(lst):
+            a[i]["pos"], a[i]["size"], a[i]["filling"] = d["pos"], d["size"], d["filling"]
+        return a
+    g = Geometry(descs(f["gate_desc"]), np.array([0, len(f["gate_desc"])], np.int32), descs(f["obst_desc"]),
+                 np.array([1.0]))
+    return f, g
+
+
+def test_obb_boundary_known_answers():
+    f, g = _boundary_world()
+    w = O.world_build(g, f["gates"], f["obstacles"], f["r_gate"], f["r_obst"])
+    for c in f["points"]:
+        assert O.check_states(w, f["r_gate"], f["r_obst"], np.array([c["p"]]), c["can_pass"])[0] == c["valid"], c
+    for c in f["mindist"]:
+        assert O.check_states_mindist(w, np.array([c["p"]]), c["md"])[0] == c["valid"], c
+    for c in f["rays"]:
+        got = O.check_motions(w, f["r_gate"], f["r_obst"], np.array([c["s"]]), np.array([c["e"]]),
+                              c["can_pass"], c["mode"])[0]
+        assert got == c["valid"], c
+
+
+def test_oracle_vs_pure_python_track_world(cfg, geom):
+    rg, ro = config.inflate_radii(cfg)
+    gates, obstacles = synth.track_world(42)
+    w = O.world_build(geom, gates, obstacles, rg, ro)
+    gd = [{"pos": d["pos"].tolist(), "size": d["size"].tolist(), "filling": int(d["filling"])} for d in geom.gate_desc]
+    od = [{"pos": d["pos"].tolist(), "size": d["size"].tolist(), "filling": int(d["filling"])} for d in geom.obst_desc]
+    pw = pyref_obb.build(gd, geom.gate_desc_off.tolist(), od, gates, obstacles, rg, ro)
+    for k, o in enumerate(w):
+        assert list(o["aabb_lo"]) == pw[k]["aabb_lo"] and list(o["aabb_hi"]) == pw[k]["aabb_hi"]
+        assert list(o["center"]) == pw[k]["center"]
+    lo, hi = synth.C2_BOUNDS
+    pts = synth.sample_states(11, lo, np.array([6.0, 6.0, 1.6]), 1500)
+    for cp in (0, 1):
+        got = O.check_states(w, rg, ro, pts, cp)
+        ref = np.array([pyref_obb.point_valid(pw, rg, ro, list(p), cp) for p in pts], np.uint8)
+        assert (got == ref).all()
+    s1, s2 = synth.edges(12, 13, lo, np.array([6.0, 6.0, 1.6]), 600, max_len=1.5)
+    for mode in (0, 1):
+        got = O.check_motions(w, rg, ro, s1, s2, False, mode)
+        fn = pyref_obb.ray_valid if mode == 0 else pyref_obb.ray_valid_d32
+        ref = np.array([fn(pw, rg, ro, list(a), list(b), False) for a, b in zip(s1, s2)], np.uint8)
+        assert (got == ref).all()
+    md = O.check_states_mindist(w, pts, 0.3)
+    ref = np.array([pyref_obb.point_valid_mindist(pw, list(p), 0.3) for p in pts], np.uint8)
+    assert (md == ref).all()
+
+
+def test_golden_c1_states_oracle(geom):
+    f = json.load(open(os.path.join(GOLDEN, "c1_states.json")))
+    w = O.world_build(geom, f["gates"], f["obstacles"], f["r_gate"], f["r_obst"])
+    for cp in ("0", "1"):
+        got = O.check_states(w, f["r_gate"], f["r_obst"], np.array(f["states"]), int(cp))
+        assert got.tolist() == f["valid"][cp]
+
+
+def test_world_build_errors(geom):
+    with pytest.raises(ValueError):
+        O.world_build(geom, [[0, 0, 0, 0.1, 0, 0, 0]], np.zeros((0, 6)), 0.2, 0.2)  # roll
+    with pytest.raises(ValueError):
+        O.world_build(geom, np.zeros((0, 7)), [[0, 0, 0.5, 0, 0, 0]], 0.2, 0.2)  # obstacle z
+
+
+def test_counter_sampler_matches_oracle():
+    lo, hi = synth.C2_BOUNDS
+    a = synth.sample_states(7, lo, hi, 5000)
+    b = O.sample_states(7, lo, hi, 5000)
+    assert np.array_equal(a, b)
