@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 
 #include "epp_internal.h"
@@ -25,25 +26,33 @@ const WorldView& world_view(const epp_world* w);
 namespace {
 
 constexpr int kBlock = 256;
-constexpr uint32_t kLdsBudget = 64 * 1024;
+constexpr uint32_t kLdsBudget = 150 * 1024;
 
 struct Acc {
     const double* f;
     int n_pad;
     const uint32_t* meta;
+    const unsigned long long* mask;
     const uint32_t* cs;
     const uint16_t* co;
     __device__ __forceinline__ double g(int field, int i) const { return f[field * n_pad + i]; }
 };
 
-__device__ __forceinline__ Acc make_acc(const unsigned char* base, const WorldView& w) {
+// `front` holds cell_mask + cell_start (LDS or HBM), `base` the whole blob.
+__device__ __forceinline__ Acc make_acc(const unsigned char* front, const unsigned char* base,
+                                        const WorldView& w) {
     Acc a;
-    a.f = reinterpret_cast<const double*>(base);
+    a.f = reinterpret_cast<const double*>(base + w.off_soa);
     a.n_pad = w.n_pad;
     a.meta = reinterpret_cast<const uint32_t*>(base + w.off_meta);
-    a.cs = reinterpret_cast<const uint32_t*>(base + w.off_cell_start);
+    a.mask = reinterpret_cast<const unsigned long long*>(front + w.off_cell_mask);
+    a.cs = reinterpret_cast<const uint32_t*>(front + w.off_cell_start);
     a.co = reinterpret_cast<const uint16_t*>(base + w.off_cell_obb);
     return a;
+}
+
+__device__ __forceinline__ double owner_r(const WorldView& w, uint32_t m) {
+    return (m & META_GATE) ? w.r_gate : w.r_obst;  // src/World.cpp:89-90
 }
 
 // OBB::checkCollisionWithPoint — src/OBB.cpp:63-91.  R = Rz, so
@@ -103,18 +112,39 @@ __device__ __forceinline__ bool obb_ray_hit(const Acc& a, int i, uint32_t m, con
     return 0 <= tMin && tMin <= 1 && 0 <= tMax && tMax <= 1;  // :60
 }
 
+// Occupancy test of a state's fine sub-cell; returns the number of candidate OBBs (its
+// coarse cell's list, starting at `start`), 0 if no AABB can contain the state.
+// Branch-free: every lane reads the (clamped) cell, so the four states of a lane
+// interleave and no exec-mask juggling is needed.
+__device__ __forceinline__ uint32_t classify(const Acc& a, const WorldView& w, double px, double py,
+                                             double pz, uint32_t& start) {
+    const float fx = fine_coord(px, w.ofx, w.i4x);
+    const float fy = fine_coord(py, w.ofy, w.i4y);
+    const float fz = fine_coord(pz, w.ofz, w.i4z);
+    // outside the union of the AABBs (conservative, see epp_internal.h); NaN -> outside
+    const bool in = (fx >= 0.0f) & (fx <= w.limx) & (fy >= 0.0f) & (fy <= w.limy) & (fz >= 0.0f) &
+                    (fz <= w.limz);
+    const int ix = (int)fminf(fmaxf(fx, 0.0f), w.fmaxx);
+    const int iy = (int)fminf(fmaxf(fy, 0.0f), w.fmaxy);
+    const int iz = (int)fminf(fmaxf(fz, 0.0f), w.fmaxz);
+    const int cell = ((iz >> 2) * w.ny + (iy >> 2)) * w.nx + (ix >> 2);
+    const uint32_t bit = (uint32_t)((((iz & 3) << 2) + (iy & 3)) * 4 + (ix & 3));
+    const unsigned long long m = a.mask[cell];
+    const uint32_t word = (bit & 32u) ? (uint32_t)(m >> 32) : (uint32_t)m;
+    const bool occ = in & (((word >> (bit & 31u)) & 1u) != 0u);
+    const uint32_t s0 = a.cs[cell], s1 = a.cs[cell + 1];
+    start = s0;
+    return occ ? s1 - s0 : 0u;
+}
+
 // World::checkPointValidity — src/World.cpp:80-128.  The rtree query
 // contains(point) == strict interior of the AABB.
 template <bool MINDIST>
 __device__ __forceinline__ bool point_valid(const Acc& a, const WorldView& w, double px, double py,
                                             double pz, bool can_pass, double md) {
-    if (!(w.gx0 < px && px < w.gx1 && w.gy0 < py && py < w.gy1 && w.gz0 < pz && pz < w.gz1))
-        return true;  // outside every AABB
-    const int cx = cell_of(px, w.gx0, w.icx, w.nx);
-    const int cy = cell_of(py, w.gy0, w.icy, w.ny);
-    const int cz = cell_of(pz, w.gz0, w.icz, w.nz);
-    const int cell = (cz * w.ny + cy) * w.nx + cx;
-    const uint32_t b = a.cs[cell], e = a.cs[cell + 1];
+    uint32_t b = 0;
+    const uint32_t c = classify(a, w, px, py, pz, b);
+    const uint32_t e = b + c;
     for (uint32_t k = b; k < e; ++k) {
         const int i = a.co[k];
         if (!(a.g(F_LOX, i) < px && px < a.g(F_HIX, i) && a.g(F_LOY, i) < py && py < a.g(F_HIY, i) &&
@@ -126,7 +156,7 @@ __device__ __forceinline__ bool point_valid(const Acc& a, const WorldView& w, do
             if (obb_point_hit(a, i, m, px, py, pz, md)) return false;
         } else {
             if ((m & META_FILLING) && can_pass) continue;  // :92-95
-            if (obb_point_hit(a, i, m, px, py, pz, a.g(F_R, i))) return false;
+            if (obb_point_hit(a, i, m, px, py, pz, owner_r(w, m))) return false;
         }
     }
     return true;
@@ -146,9 +176,12 @@ __device__ __forceinline__ bool ray_valid(const Acc& a, const WorldView& w, cons
     if (hi[0] < w.gx0 || w.gx1 < lo[0] || hi[1] < w.gy0 || w.gy1 < lo[1] || hi[2] < w.gz0 ||
         w.gz1 < lo[2])
         return true;
-    const int x0 = cell_of(lo[0], w.gx0, w.icx, w.nx), x1 = cell_of(hi[0], w.gx0, w.icx, w.nx);
-    const int y0 = cell_of(lo[1], w.gy0, w.icy, w.ny), y1 = cell_of(hi[1], w.gy0, w.icy, w.ny);
-    const int z0 = cell_of(lo[2], w.gz0, w.icz, w.nz), z1 = cell_of(hi[2], w.gz0, w.icz, w.nz);
+    const int x0 = fine_index(fine_coord(lo[0], w.ofx, w.i4x), w.nx) >> 2;
+    const int x1 = fine_index(fine_coord(hi[0], w.ofx, w.i4x), w.nx) >> 2;
+    const int y0 = fine_index(fine_coord(lo[1], w.ofy, w.i4y), w.ny) >> 2;
+    const int y1 = fine_index(fine_coord(hi[1], w.ofy, w.i4y), w.ny) >> 2;
+    const int z0 = fine_index(fine_coord(lo[2], w.ofz, w.i4z), w.nz) >> 2;
+    const int z1 = fine_index(fine_coord(hi[2], w.ofz, w.i4z), w.nz) >> 2;
     for (int z = z0; z <= z1; ++z)
         for (int y = y0; y <= y1; ++y)
             for (int x = x0; x <= x1; ++x) {
@@ -165,7 +198,7 @@ __device__ __forceinline__ bool ray_valid(const Acc& a, const WorldView& w, cons
                         hi[1] < a.g(F_LOY, i) || a.g(F_HIZ, i) < lo[2] || hi[2] < a.g(F_LOZ, i))
                         continue;
                     if ((m & META_FILLING) && can_pass) continue;  // :150-153
-                    if (obb_ray_hit(a, i, m, s, e, a.g(F_R, i))) return false;
+                    if (obb_ray_hit(a, i, m, s, e, owner_r(w, m))) return false;
                 }
             }
     return true;
@@ -184,10 +217,12 @@ __device__ __forceinline__ bool ray_valid_d32(const Acc& a, const WorldView& w, 
     return true;
 }
 
-__device__ __forceinline__ const unsigned char* stage_world(const WorldView& w, unsigned char* lds) {
+// Copies the first `bytes` of the blob into LDS (block-wide, ends with a barrier).
+__device__ __forceinline__ const unsigned char* stage_world(const WorldView& w, unsigned char* lds,
+                                                            uint32_t bytes) {
     const uint4* src = reinterpret_cast<const uint4*>(w.blob);
     uint4* dst = reinterpret_cast<uint4*>(lds);
-    const uint32_t n16 = w.blob_bytes / 16;
+    const uint32_t n16 = bytes / 16;
     for (uint32_t o = threadIdx.x; o < n16; o += blockDim.x) dst[o] = src[o];
     __syncthreads();
     return lds;
@@ -220,53 +255,225 @@ __device__ __forceinline__ void store4(uint8_t* __restrict__ out, int64_t first,
     }
 }
 
-template <bool LDS, bool MINDIST>
+// ---- k_states: wave-cooperative candidate testing ----------------------------------
+// Phase 1 (per lane, 4 states): bounds + fine-mask test.  A state whose sub-cell is
+// occupied owns a segment of (state, candidate OBB) pairs: its coarse cell's list.
+// Phase 2 (per wave): the segments are compacted into LDS (wave prefix sums) and the 64
+// lanes take one pair each (a binary search over the segment offsets finds the pair's
+// state), setting per-state "hit" bits with LDS atomics.  Only ~6% of uniform samples
+// have candidates; without this a wavefront would run its slowest lane's candidate loop
+// for every state slot.
+constexpr int kSegCap = 96;     // needy states a wave handles cooperatively per group
+constexpr int kPairCap = 512;   // (state, candidate) pairs a wave handles cooperatively
+struct WaveScratch {
+    double xyz[kSegCap][3];        // coordinates of the needy states
+    uint32_t seg_start[kSegCap];   // exclusive prefix of pair counts
+    uint32_t seg_state[kSegCap];   // sid (8 bits) | first candidate entry << 8
+    uint8_t head[kPairCap];        // segment index at its first pair, 0 elsewhere
+    uint32_t bits[8];              // hit bits of the 256 states of the wave's group
+};
+constexpr uint32_t kScratchBytes = (kBlock / 64) * ((sizeof(WaveScratch) + 15) & ~15u);
+
+__device__ __forceinline__ void wave_lds_sync() {
+    // LDS operations of one wavefront complete in order; this only stops the compiler
+    // from moving memory accesses across the point (no vmcnt drain: the prefetched
+    // loads of the next group stay in flight).
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Wave-wide inclusive scans with DPP (GFX9 row_shr / row_bcast): six cross-lane
+// adds, no LDS round trips.  Lanes without a source read `old` = identity.
+__device__ __forceinline__ uint32_t dpp_incl_add(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+__device__ __forceinline__ uint32_t dpp_incl_max(uint32_t x) {
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));
+    return x;
+}
+// Exclusive prefix sum over the wave and the wave total.
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, int /*lane*/, uint32_t& total) {
+    const uint32_t incl = dpp_incl_add(x);
+    total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    return incl - x;
+}
+
+template <bool MINDIST>
+__device__ __forceinline__ bool pair_hit(const Acc& a, const WorldView& w, int i, double px, double py,
+                                         double pz, bool can_pass, double md) {
+    if (!(a.g(F_LOX, i) < px && px < a.g(F_HIX, i) && a.g(F_LOY, i) < py && py < a.g(F_HIY, i) &&
+          a.g(F_LOZ, i) < pz && pz < a.g(F_HIZ, i)))
+        return false;  // rtree contains(point): strict  src/World.cpp:83
+    const uint32_t m = a.meta[i];
+    if (MINDIST) return !(m & META_FILLING) && obb_point_hit(a, i, m, px, py, pz, md);  // :116-125
+    return !((m & META_FILLING) && can_pass) && obb_point_hit(a, i, m, px, py, pz, owner_r(w, m));  // :92-100
+}
+
+// Candidate walk of one state by its own lane (tail states and overflow).
+template <bool MINDIST>
+__device__ __forceinline__ bool state_valid_scalar(const Acc& a, const WorldView& w, double px,
+                                                   double py, double pz, bool can_pass, double md) {
+    uint32_t st = 0;
+    const uint32_t c = classify(a, w, px, py, pz, st);
+    for (uint32_t j = 0; j < c; ++j)
+        if (pair_hit<MINDIST>(a, w, a.co[st + j], px, py, pz, can_pass, md)) return false;
+    return true;
+}
+
+// STAGE: 0 = world read from HBM/L2, 1 = front (masks, cell starts) in LDS, 2 = all in LDS
+template <int STAGE, bool MINDIST, bool ALIGNED>
 __global__ __launch_bounds__(kBlock) void k_states(WorldView w, const double* __restrict__ xyz,
                                                    int64_t n, int can_pass, double md,
                                                    uint8_t* __restrict__ valid,
                                                    int32_t* __restrict__ compact_idx,
                                                    unsigned long long* __restrict__ n_valid,
-                                                   int aligned) {
+                                                   uint32_t stage_bytes) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const unsigned char* base = LDS ? stage_world(w, lds) : w.blob;
-    const Acc a = make_acc(base, w);
-    const int64_t groups = (n + 3) / 4;
+    const int lane = threadIdx.x & 63;
+    // full groups of 4 states; the (< 4) tail states are handled after the main loop
+    const int64_t groups = n / 4;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
-    // wave-uniform trip count: every lane of a wave runs every iteration (ballot/shfl)
-    for (int64_t g0 = (int64_t)blockIdx.x * kBlock; g0 < groups; g0 += stride) {
-        const int64_t g = g0 + threadIdx.x;
-        const int64_t first = 4 * g;
-        uint32_t f[4] = {0, 0, 0, 0};
-        if (g < groups) {
-            double v[12];
-            load4(xyz, first, n, aligned != 0, v);
+    // Loads are unconditional (clamped to the last full group) so the compiler keeps
+    // the next group's six loads in flight with a counted vmcnt.
+    auto load = [&](int64_t grp, double (&dst)[12]) {
+        grp = grp < groups ? grp : groups - 1;
+        if (ALIGNED) {
+            const double2* q = reinterpret_cast<const double2*>(xyz + 12 * grp);
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                const double2 t = q[k];
+                dst[2 * k] = t.x;
+                dst[2 * k + 1] = t.y;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 12; ++k) dst[k] = xyz[12 * grp + k];
+        }
+    };
+    int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    double va[12], vb[12];
+    if (groups > 0) load(g, va);  // first loads before the world staging
+    WaveScratch* ws = reinterpret_cast<WaveScratch*>(lds + (threadIdx.x >> 6) * ((sizeof(WaveScratch) + 15) & ~15u));
+    const unsigned char* staged = STAGE ? stage_world(w, lds + kScratchBytes, stage_bytes) : w.blob;
+    const Acc a = make_acc(staged, STAGE == 2 ? staged : w.blob, w);
+
+    auto process = [&](int64_t gg, const double (&v)[12]) {
+        const bool live = gg < groups;
+        const int64_t first = 4 * gg;
+        // phase 1
+        uint32_t cst[4], cnt[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t c = classify(a, w, v[3 * k], v[3 * k + 1], v[3 * k + 2], cst[k]);
+            cnt[k] = live ? c : 0u;
+        }
+        const uint32_t mine = cnt[0] + cnt[1] + cnt[2] + cnt[3];
+        const uint32_t nseg = (cnt[0] > 0) + (cnt[1] > 0) + (cnt[2] > 0) + (cnt[3] > 0);
+        uint32_t total, S;
+        const uint32_t pexcl = wave_excl_scan(mine, lane, total);
+        const uint32_t sexcl = wave_excl_scan(nseg, lane, S);
+        uint32_t hits = 0;
+        if (total && S <= (uint32_t)kSegCap && total <= (uint32_t)kPairCap) {
+            // wave-uniform: cooperative pair testing.  Pair p belongs to the last segment
+            // starting at or before p: heads are scattered to LDS and propagated with a
+            // wave max-scan (carried across rounds), no search.
+            if (lane < 8) ws->bits[lane] = 0;
+            for (uint32_t p = lane; p < total; p += 64) ws->head[p] = 0;
+            wave_lds_sync();
+            uint32_t si = sexcl, pp = pexcl;
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (first + k < n)
-                    f[k] = point_valid<MINDIST>(a, w, v[3 * k], v[3 * k + 1], v[3 * k + 2],
-                                                can_pass != 0, md)
-                               ? 1u
-                               : 0u;
-            store4(valid, first, n, f);
+                if (cnt[k]) {
+                    ws->seg_start[si] = pp;
+                    ws->seg_state[si] = (uint32_t)(lane * 4 + k) | (cst[k] << 8);
+                    ws->xyz[si][0] = v[3 * k];
+                    ws->xyz[si][1] = v[3 * k + 1];
+                    ws->xyz[si][2] = v[3 * k + 2];
+                    ws->head[pp] = (uint8_t)si;
+                    ++si;
+                    pp += cnt[k];
+                }
+            wave_lds_sync();
+            uint32_t carry = 0;
+            for (uint32_t r = 0; r < total; r += 64) {  // wave-uniform rounds
+                const uint32_t p = r + lane;
+                const uint32_t hd = p < total ? (uint32_t)ws->head[p] : 0u;
+                const uint32_t j = max(dpp_incl_max(hd), carry);
+                carry = (uint32_t)__builtin_amdgcn_readlane((int)j, 63);
+                if (p < total) {
+                    const uint32_t e = ws->seg_state[j];
+                    const int i = a.co[(e >> 8) + (p - ws->seg_start[j])];
+                    if (pair_hit<MINDIST>(a, w, i, ws->xyz[j][0], ws->xyz[j][1], ws->xyz[j][2],
+                                          can_pass != 0, md)) {
+                        const uint32_t sid = e & 255u;
+                        atomicOr(&ws->bits[sid >> 5], 1u << (sid & 31));
+                    }
+                }
+            }
+            wave_lds_sync();
+            hits = (ws->bits[lane >> 3] >> ((lane & 7) * 4)) & 15u;
+            wave_lds_sync();  // scratch is rewritten by the next group
+        } else if (total) {  // rare: too many needy states, every lane walks its own lists
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                for (uint32_t j = 0; j < cnt[k]; ++j)
+                    if (pair_hit<MINDIST>(a, w, a.co[cst[k] + j], v[3 * k], v[3 * k + 1], v[3 * k + 2],
+                                          can_pass != 0, md)) {
+                        hits |= 1u << k;
+                        break;
+                    }
+        }
+        const uint32_t fl = live ? (~hits & 15u) : 0u;  // bit k: state first+k valid
+        if (live) {
+            if (ALIGNED)
+                *reinterpret_cast<uint32_t*>(valid + first) =
+                    (fl & 1u) | ((fl & 2u) << 7) | ((fl & 4u) << 14) | ((fl & 8u) << 21);
+            else
+                for (int k = 0; k < 4; ++k) valid[first + k] = (uint8_t)((fl >> k) & 1u);
         }
         if (compact_idx) {  // wave-ballot compaction (uniform branch)
-            const int lane = threadIdx.x & 63;
-            const uint32_t cnt = f[0] + f[1] + f[2] + f[3];
-            uint32_t incl = cnt;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t t = __shfl_up(incl, d, 64);
-                if (lane >= d) incl += t;
-            }
-            const uint32_t total = __shfl(incl, 63, 64);
+            const uint32_t c = (uint32_t)__popc(fl);
+            uint32_t ctot;
+            const uint32_t cex = wave_excl_scan(c, lane, ctot);
             unsigned long long wbase = 0;
-            if (lane == 0 && total) wbase = atomicAdd(n_valid, (unsigned long long)total);
+            if (lane == 0 && ctot) wbase = atomicAdd(n_valid, (unsigned long long)ctot);
             wbase = __shfl(wbase, 0, 64);
-            uint64_t pos = wbase + incl - cnt;
+            uint64_t pos = wbase + cex;
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (f[k]) compact_idx[pos++] = (int32_t)(first + k);
+                if ((fl >> k) & 1u) compact_idx[pos++] = (int32_t)(first + k);
         }
+    };
+    // block-uniform trip count: every lane runs every iteration (ballots, wave scratch);
+    // ping-pong register buffers: the next group loads while this one is processed
+    for (int64_t g0 = (int64_t)blockIdx.x * kBlock; g0 < groups; g0 += 2 * stride, g += 2 * stride) {
+        load(g + stride, vb);
+        process(g, va);
+        if (g0 + stride >= groups) break;
+        load(g + 2 * stride, va);
+        process(g + stride, vb);
+    }
+    // tail: the last n % 4 states, one lane each
+    if (blockIdx.x == 0 && threadIdx.x < (int)(n - 4 * groups)) {
+        const int64_t i = 4 * groups + threadIdx.x;
+        const bool ok = state_valid_scalar<MINDIST>(a, w, xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2],
+                                                    can_pass != 0, md);
+        valid[i] = ok ? 1 : 0;
+        if (compact_idx && ok) compact_idx[atomicAdd(n_valid, 1ull)] = (int32_t)i;
     }
 }
 
@@ -276,8 +483,8 @@ __global__ __launch_bounds__(kBlock) void k_motions(WorldView w, const double* _
                                                     int can_pass, uint8_t* __restrict__ valid,
                                                     int aligned) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const unsigned char* base = LDS ? stage_world(w, lds) : w.blob;
-    const Acc a = make_acc(base, w);
+    const unsigned char* base = LDS ? stage_world(w, lds, w.blob_bytes) : w.blob;
+    const Acc a = make_acc(base, base, w);
     const int64_t groups = (n + 3) / 4;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < groups; g += stride) {
@@ -319,13 +526,35 @@ int cu_count() {
     return g_dev[d].cus;
 }
 
+int env_int(const char* name, int dflt) {
+    const char* v = std::getenv(name);
+    return v && *v ? std::atoi(v) : dflt;
+}
+
+// Persistent grid: at most `per_cu` resident 256-thread blocks per CU (LDS permitting),
+// each looping over item groups, so the world is staged into LDS once per block.
 int grid_for(int64_t groups, uint32_t lds_bytes) {
     const int64_t need = (groups + kBlock - 1) / kBlock;
-    int per_cu = 8;
-    if (lds_bytes > 0) per_cu = (int)std::max<uint32_t>(1u, std::min<uint32_t>(8u, (160u * 1024u) / lds_bytes));
+    int per_cu = env_int("EPP_WG_PER_CU", 4);
+    if (lds_bytes > 0)
+        per_cu = std::max(1, std::min<int>(per_cu, (int)((160u * 1024u) / lds_bytes)));
     const int64_t cap = (int64_t)cu_count() * per_cu;
     int64_t g = need < cap ? need : cap;
     return (int)(g < 1 ? 1 : g);
+}
+
+bool use_lds(const WorldView& w) {
+    return w.blob_bytes <= kLdsBudget && !env_int("EPP_NO_LDS", 0) && !env_int("EPP_RAY_NO_LDS", 1);
+}
+
+template <typename K>
+void allow_lds(K kernel) {
+    static bool done = false;  // per process; same limit on every device
+    if (!done) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget);
+        done = true;
+    }
 }
 
 epp_status launch_error(const char* what) {
@@ -342,6 +571,40 @@ epp_status launch_error(const char* what) {
 
 using namespace epp;
 
+namespace {
+template <bool MINDIST>
+epp_status launch_states(const WorldView& w, const double* xyz, int64_t n, int32_t can_pass, double md,
+                         uint8_t* valid, int32_t* compact_idx, int64_t* n_valid, void* stream) {
+    // 16-byte loads and 4-byte flag stores need aligned buffers (hipMalloc gives 256 B)
+    const bool aligned = ((reinterpret_cast<uintptr_t>(xyz) & 15) | (reinterpret_cast<uintptr_t>(valid) & 3)) == 0;
+    const int64_t groups = std::max<int64_t>(1, n / 4);
+    // Stage the whole world when it is small (keeps several blocks per CU), else only
+    // the front (occupancy masks + cell starts) and read the OBB table through L1/L2.
+    const bool lds = w.front_bytes + kScratchBytes <= kLdsBudget && !env_int("EPP_NO_LDS", 0);
+    const uint32_t full_cap = (uint32_t)env_int("EPP_STAGE_FULL_MAX", 40 * 1024);
+    const uint32_t stage = !lds ? 0u : (w.blob_bytes <= full_cap ? w.blob_bytes : w.front_bytes);
+    const uint32_t shm = kScratchBytes + stage;
+    const int grid = grid_for(groups, shm);
+    hipStream_t st = (hipStream_t)stream;
+    auto nv = reinterpret_cast<unsigned long long*>(n_valid);
+#define EPP_LAUNCH_STATES(L, A)                                                                       \
+    do {                                                                                              \
+        allow_lds(k_states<L, MINDIST, A>);                                                           \
+        hipLaunchKernelGGL((k_states<L, MINDIST, A>), dim3(grid), dim3(kBlock), shm, st, w, xyz, n,   \
+                           can_pass, md, valid, compact_idx, nv, stage);                              \
+    } while (0)
+    const int mode = stage == 0 ? 0 : (stage == w.blob_bytes ? 2 : 1);
+    if (mode == 2 && aligned) EPP_LAUNCH_STATES(2, true);
+    else if (mode == 2) EPP_LAUNCH_STATES(2, false);
+    else if (mode == 1 && aligned) EPP_LAUNCH_STATES(1, true);
+    else if (mode == 1) EPP_LAUNCH_STATES(1, false);
+    else if (aligned) EPP_LAUNCH_STATES(0, true);
+    else EPP_LAUNCH_STATES(0, false);
+#undef EPP_LAUNCH_STATES
+    return launch_error(MINDIST ? "epp_check_states_mindist" : "epp_check_states");
+}
+}  // namespace
+
 extern "C" {
 
 epp_status epp_check_states(const epp_world* world, const double* xyz, int64_t n,
@@ -352,21 +615,8 @@ epp_status epp_check_states(const epp_world* world, const double* xyz, int64_t n
         return EPP_ERR_INVALID_ARGUMENT;
     }
     if (n == 0) return EPP_OK;
-    const WorldView& w = world_view(world);
-    const int aligned = (reinterpret_cast<uintptr_t>(xyz) & 15) == 0;
-    const int64_t groups = (n + 3) / 4;
-    const bool lds = w.blob_bytes <= kLdsBudget;
-    const uint32_t shm = lds ? w.blob_bytes : 0;
-    const int grid = grid_for(groups, shm);
-    if (lds)
-        hipLaunchKernelGGL((k_states<true, false>), dim3(grid), dim3(kBlock), shm, (hipStream_t)stream, w,
-                           xyz, n, can_pass_gate, 0.0, valid, compact_idx,
-                           reinterpret_cast<unsigned long long*>(n_valid), aligned);
-    else
-        hipLaunchKernelGGL((k_states<false, false>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, w,
-                           xyz, n, can_pass_gate, 0.0, valid, compact_idx,
-                           reinterpret_cast<unsigned long long*>(n_valid), aligned);
-    return launch_error("epp_check_states");
+    return launch_states<false>(world_view(world), xyz, n, can_pass_gate, 0.0, valid, compact_idx, n_valid,
+                                stream);
 }
 
 epp_status epp_check_states_mindist(const epp_world* world, const double* xyz, int64_t n,
@@ -376,19 +626,7 @@ epp_status epp_check_states_mindist(const epp_world* world, const double* xyz, i
         return EPP_ERR_INVALID_ARGUMENT;
     }
     if (n == 0) return EPP_OK;
-    const WorldView& w = world_view(world);
-    const int aligned = (reinterpret_cast<uintptr_t>(xyz) & 15) == 0;
-    const int64_t groups = (n + 3) / 4;
-    const bool lds = w.blob_bytes <= kLdsBudget;
-    const uint32_t shm = lds ? w.blob_bytes : 0;
-    const int grid = grid_for(groups, shm);
-    if (lds)
-        hipLaunchKernelGGL((k_states<true, true>), dim3(grid), dim3(kBlock), shm, (hipStream_t)stream, w,
-                           xyz, n, 0, min_distance, valid, nullptr, nullptr, aligned);
-    else
-        hipLaunchKernelGGL((k_states<false, true>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, w,
-                           xyz, n, 0, min_distance, valid, nullptr, nullptr, aligned);
-    return launch_error("epp_check_states_mindist");
+    return launch_states<true>(world_view(world), xyz, n, 0, min_distance, valid, nullptr, nullptr, stream);
 }
 
 epp_status epp_check_motions(const epp_world* world, const double* s1, const double* s2, int64_t n,
@@ -402,11 +640,13 @@ epp_status epp_check_motions(const epp_world* world, const double* s1, const dou
     const int aligned =
         ((reinterpret_cast<uintptr_t>(s1) | reinterpret_cast<uintptr_t>(s2)) & 15) == 0;
     const int64_t groups = (n + 3) / 4;
-    const bool lds = w.blob_bytes <= kLdsBudget;
+    const bool lds = use_lds(w);
     const uint32_t shm = lds ? w.blob_bytes : 0;
     const int grid = grid_for(groups, shm);
     hipStream_t st = (hipStream_t)stream;
     if (lds) {
+        allow_lds(k_motions<true, 0>);
+        allow_lds(k_motions<true, 1>);
         if (mode == 0)
             hipLaunchKernelGGL((k_motions<true, 0>), dim3(grid), dim3(kBlock), shm, st, w, s1, s2, n,
                                can_pass_gate, valid, aligned);

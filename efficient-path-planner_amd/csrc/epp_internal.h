@@ -1,15 +1,17 @@
 // epp_internal.h — layouts shared by the host library and the HIP kernels.
 //
-// The world lives in HBM as one contiguous blob so that a workgroup can stage it
-// into LDS with straight 16-byte copies:
+// The world lives in HBM as one contiguous blob.  Its front part (what every state
+// query touches) can be staged into LDS with straight 16-byte copies:
 //
-//   double  soa[EPP_NF][n_pad]   field-major OBB table (see enum below)
+//   uint64  cell_mask[ncell]     occupancy of the 4x4x4 fine sub-cells of each coarse cell
+//   uint32  cell_start[ncell+1]  CSR offsets of the coarse cells' OBB lists
+//   -------------------------    (front: front_bytes)
+//   uint16  cell_obb[...]        OBB ids per coarse cell
 //   uint32  meta[n_pad]          bit0 filling, bit1 gate, bits 8-15/16-23/24-31 = first
-//                                cull-grid cell (x, y, z) the OBB's AABB touches
-//   uint32  cell_start[ncell+1]  CSR offsets of the cull grid
-//   uint16  cell_obb[...]        OBB ids per cell
+//                                coarse cell (x, y, z) the OBB's AABB touches
+//   double  soa[EPP_NF][n_pad]   field-major OBB table (see enum below)
 //
-// n_pad rounds n_obbs up to a multiple of 2 so every array stays 16-byte aligned.
+// n_pad rounds n_obbs up to a multiple of 4; every array starts 16-byte aligned.
 #pragma once
 #include <stdint.h>
 
@@ -26,7 +28,6 @@ enum Field : int {
     F_CX, F_CY, F_CZ,                              // OBB centre
     F_COS, F_SIN,                                  // R = [[c,-s,0],[s,c,0],[0,0,1]]
     F_HX, F_HY, F_HZ,                              // half sizes
-    F_R,                                           // owner inflate radius (gate/obstacle)
     EPP_NF
 };
 
@@ -41,12 +42,20 @@ struct WorldView {
     int32_t n_obb;
     int32_t n_pad;
     int32_t nx, ny, nz;
-    uint32_t off_meta;        // byte offsets inside the blob
+    uint32_t front_bytes;     // bytes of cell_mask + cell_start (16-byte multiple)
+    uint32_t off_cell_mask;   // byte offsets inside the blob
     uint32_t off_cell_start;
     uint32_t off_cell_obb;
+    uint32_t off_meta;
+    uint32_t off_soa;
     double gx0, gy0, gz0;     // grid origin = min AABB lo
     double gx1, gy1, gz1;     // grid far corner = max AABB hi
-    double icx, icy, icz;     // 1 / cell size
+    double icx, icy, icz;     // 1 / coarse cell size
+    float ofx, ofy, ofz;      // grid origin rounded to float
+    float i4x, i4y, i4z;      // 4 / coarse cell size, as float (fine-index scale)
+    float limx, limy, limz;   // ~4n: fine coordinates beyond are outside every AABB
+    float fmaxx, fmaxy, fmaxz; // 4 * n - 1: largest fine index
+    double r_gate, r_obst;    // inflate radii (src/World.cpp:89-90)
 };
 
 // Host-side world: the upload plus host copies (for AABB introspection and rebuilds).
@@ -60,19 +69,26 @@ struct HostWorld {
     std::vector<double> aabbs;   // n x 6
 };
 
-// Cell index along one axis: same double operations on host and device, so the
-// candidate lists are exact (no rounding slack needed: floor(fl((p-o)*inv)) is
-// monotone in p).
+// Fine (sub-cell) coordinate along one axis, computed in float with the same
+// operations on host and device.  Every step is monotone in p, so the candidate lists
+// and occupancy masks built from AABB corners are exact supersets of the rtree query
+// results without any rounding slack.  A point strictly inside an AABB has
+// 0 <= f <= 4n(1 + 3 * 2^-24) < lim; the fine index is F = min((int)f, 4n-1), coarse = F >> 2.
 #if defined(__HIPCC__)
 __host__ __device__
 #endif
-inline int cell_of(double p, double o, double inv, int n) {
-    double f = (p - o) * inv;
-    int c;
-    if (!(f >= 0.0)) c = 0;                    // also catches NaN
-    else if (f >= (double)n) c = n - 1;
-    else c = (int)f;                           // f >= 0: truncation == floor
-    return c < n ? c : n - 1;
+inline float fine_coord(double p, float o, float inv4) {
+    return ((float)p - o) * inv4;
+}
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline int fine_index(float f, int n) {
+    const int nf = 4 * n;
+    if (!(f >= 0.0f)) return 0;  // also catches NaN
+    if (f >= (float)nf) return nf - 1;
+    const int c = (int)f;        // f >= 0: truncation == floor
+    return c < nf ? c : nf - 1;
 }
 
 void set_error(const std::string& msg);

@@ -243,14 +243,11 @@ __global__ __launch_bounds__(kWave) void k_minsnap(const double* __restrict__ wp
             cB[4][a] * cB[4][b] * pow(Tm[i], ex) * 2.0 / ex;
     }
     __syncthreads();
-    for (int e = lane; e < M * 55; e += kWave) {
-        const int i = e / 55;
-        int j = e % 55, r = 0;
-        while (j >= N - r) {  // unpack upper-triangle index (r <= c)
-            j -= N - r;
-            ++r;
-        }
-        const int c = r + j;
+    // All 100 entries are computed (no mirroring of a triangle): each row then keeps
+    // the exact translation invariance H[r][0] == -H[r][5] that the reference's full
+    // product has; mirroring breaks it and costs ~1e-6 on long, stiff tracks.
+    for (int e = lane; e < M * 100; e += kWave) {
+        const int i = e / 100, r = (e % 100) / 10, c = e % 10;
         const double* S = scr + (size_t)i * SegScratch::kSize;
         const double* Ai = S + SegScratch::kAinv;
         const double* Q = S + SegScratch::kQ;
@@ -262,7 +259,6 @@ __global__ __launch_bounds__(kWave) void k_minsnap(const double* __restrict__ wp
         }
         double* H = const_cast<double*>(S) + SegScratch::kH;
         H[r * N + c] = h;
-        H[c * N + r] = h;
     }
     __syncthreads();
     // ---- phase 3: block-tridiagonal system over the inner vertices ----------------
@@ -411,25 +407,35 @@ struct RangeIter {
     }
 };
 
-__global__ void k_sample_count(const double* __restrict__ seg_times, const int32_t* __restrict__ wp_off,
-                               int n_tracks, double dt, int64_t* __restrict__ counts) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+// One wavefront per track: the lanes stage the segment times in LDS, lane 0 runs the
+// recurrence (every step reads T[i] from LDS, not from memory).
+__global__ __launch_bounds__(kWave) void k_sample_count(const double* __restrict__ seg_times,
+                                                        const int32_t* __restrict__ wp_off,
+                                                        int n_tracks, double dt,
+                                                        int64_t* __restrict__ counts) {
+    extern __shared__ __attribute__((aligned(16))) double sT[];
+    const int t = blockIdx.x;
     if (t >= n_tracks) return;
     const int M = wp_off[t + 1] - wp_off[t] - 1;
     if (M < 1 || !(dt > 0)) {
-        counts[t] = 0;
+        if (threadIdx.x == 0) counts[t] = 0;
         return;
     }
-    RangeIter it;
-    it.init(seg_times + (wp_off[t] - t), M);
-    int64_t n = 0;
-    int seg;
-    double tin, tac;
-    while (it.next(seg, tin, tac)) {
-        ++n;
-        it.advance(dt);
+    const double* T = seg_times + (wp_off[t] - t);
+    for (int i = threadIdx.x; i < M; i += kWave) sT[i] = T[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        RangeIter it;
+        it.init(sT, M);
+        int64_t n = 0;
+        int seg;
+        double tin, tac;
+        while (it.next(seg, tin, tac)) {
+            ++n;
+            it.advance(dt);
+        }
+        counts[t] = n;
     }
-    counts[t] = n;
 }
 
 // Polynomial::evaluate(t, k) — polynomial.h:136-149
@@ -449,20 +455,27 @@ __global__ __launch_bounds__(kWave) void k_sample_rows(const double* __restrict_
                                                        const double* __restrict__ t0,
                                                        const int64_t* __restrict__ row_off,
                                                        double* __restrict__ rows) {
-    __shared__ int s_seg[kWave];
-    __shared__ double s_tin[kWave], s_tac[kWave];
-    __shared__ int s_cnt, s_done;
+    // one dynamic LDS array (Guideline 17): [T (M) | tin (64) | tac (64) | seg (64) | cnt, done]
+    extern __shared__ __attribute__((aligned(16))) double sm[];
     const int t = blockIdx.x;
     if (t >= n_tracks) return;
     const int lane = threadIdx.x;
     const int M = wp_off[t + 1] - wp_off[t] - 1;
     if (M < 1 || !(dt > 0)) return;
     const int seg0 = wp_off[t] - t;
+    double* sT = sm;
+    double* s_tin = sT + ((M + 1) & ~1);
+    double* s_tac = s_tin + kWave;
+    int* s_seg = reinterpret_cast<int*>(s_tac + kWave);
+    int& s_cnt = s_seg[kWave];
+    int& s_done = s_seg[kWave + 1];
+    for (int i = lane; i < M; i += kWave) sT[i] = seg_times[seg0 + i];
     const double toff = t0 ? t0[t] : 0.0;
-    double* out = rows + row_off[t] * 10;
+    double* out = rows + (row_off ? row_off[t] : 0) * 10;
     RangeIter it;
+    __syncthreads();
     if (lane == 0) {
-        it.init(seg_times + seg0, M);
+        it.init(sT, M);
         s_done = 0;
     }
     int64_t base = 0;
@@ -528,6 +541,21 @@ epp_status ensure_consts() {
     }
     if (dev >= 0 && dev < 64) g_consts_ready[dev] = true;
     return EPP_OK;
+}
+
+// Largest segment count of a batch (the offsets live on the device).
+int max_segments(const int32_t* d_off, int n_tracks, hipStream_t s, int* out) {
+    std::vector<int32_t> off(n_tracks + 1);
+    hipError_t e = hipMemcpyAsync(off.data(), d_off, off.size() * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+        set_error(std::string("epp: reading track offsets: ") + hipGetErrorString(e));
+        return -1;
+    }
+    int m = 1;
+    for (int t = 0; t < n_tracks; ++t) m = std::max(m, off[t + 1] - off[t] - 1);
+    *out = m;
+    return 0;
 }
 
 }  // namespace
@@ -612,8 +640,10 @@ epp_status epp_sample_count(const double* seg_times, const int32_t* wp_offsets, 
         return EPP_ERR_INVALID_ARGUMENT;
     }
     if (n_tracks == 0) return EPP_OK;
-    hipLaunchKernelGGL(k_sample_count, dim3((n_tracks + 63) / 64), dim3(64), 0, (hipStream_t)stream,
-                       seg_times, wp_offsets, n_tracks, dt, row_counts);
+    int max_m = 0;
+    if (max_segments(wp_offsets, n_tracks, (hipStream_t)stream, &max_m)) return EPP_ERR_HIP;
+    hipLaunchKernelGGL(k_sample_count, dim3(n_tracks), dim3(kWave), (size_t)(max_m + 2) * 8,
+                       (hipStream_t)stream, seg_times, wp_offsets, n_tracks, dt, row_counts);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_error(std::string("epp_sample_count: ") + hipGetErrorString(e));
@@ -633,7 +663,10 @@ epp_status epp_sample_batch(const double* seg_times, const double* coeffs, const
     if (n_tracks == 0) return EPP_OK;
     epp_status st = ensure_consts();
     if (st) return st;
-    hipLaunchKernelGGL(k_sample_rows, dim3(n_tracks), dim3(kWave), 0, (hipStream_t)stream, seg_times,
+    int max_m = 0;
+    if (max_segments(wp_offsets, n_tracks, (hipStream_t)stream, &max_m)) return EPP_ERR_HIP;
+    const size_t shm = ((size_t)((max_m + 1) & ~1) + 3 * kWave + 2) * 8;
+    hipLaunchKernelGGL(k_sample_rows, dim3(n_tracks), dim3(kWave), shm, (hipStream_t)stream, seg_times,
                        coeffs, wp_offsets, n_tracks, dt, t0, row_offsets, rows);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

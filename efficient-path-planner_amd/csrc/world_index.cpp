@@ -85,7 +85,6 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
         f[F_COS * n_pad + i] = o.rot[0];  // R(0,0) = cos
         f[F_SIN * n_pad + i] = o.rot[3];  // R(1,0) = sin
         f[F_HX * n_pad + i] = o.half[0]; f[F_HY * n_pad + i] = o.half[1]; f[F_HZ * n_pad + i] = o.half[2];
-        f[F_R * n_pad + i] = r;
         meta[i] = (o.filling ? META_FILLING : 0u) | (o.is_gate ? META_GATE : 0u);
     }
     // ---- cull grid -------------------------------------------------------------
@@ -97,8 +96,8 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
             ext[k] = g1[k] - g0[k];
             vol *= std::max(ext[k], 1e-3);
         }
-        // ~4 cells per OBB, capped: keeps candidate lists at a handful of OBBs.
-        const double target = std::min(8192.0, std::max(64.0, 4.0 * n));
+        // ~2 coarse cells per OBB (each split into 4x4x4 occupancy sub-cells), capped.
+        const double target = std::min(4096.0, std::max(32.0, 2.0 * n));
         const double s = std::cbrt(vol / target);
         for (int k = 0; k < 3; ++k) {
             nd[k] = ext[k] > 0 ? (int)std::ceil(ext[k] / s) : 1;
@@ -110,49 +109,74 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
     v.gx0 = g0[0]; v.gy0 = g0[1]; v.gz0 = g0[2];
     v.gx1 = g1[0]; v.gy1 = g1[1]; v.gz1 = g1[2];
     v.icx = inv[0]; v.icy = inv[1]; v.icz = inv[2];
+    v.r_gate = hw.r_gate;
+    v.r_obst = hw.r_obst;
+    const float of[3] = {(float)g0[0], (float)g0[1], (float)g0[2]};
+    const float i4[3] = {(float)(4.0 * inv[0]), (float)(4.0 * inv[1]), (float)(4.0 * inv[2])};
+    v.ofx = of[0]; v.ofy = of[1]; v.ofz = of[2];
+    v.i4x = i4[0]; v.i4y = i4[1]; v.i4z = i4[2];
+    // fine coordinate of any point strictly inside an AABB is <= 4n (1 + 3 * 2^-24)
+    v.limx = (float)(4 * nd[0]) * (1.0f + 0x1.0p-20f);
+    v.limy = (float)(4 * nd[1]) * (1.0f + 0x1.0p-20f);
+    v.limz = (float)(4 * nd[2]) * (1.0f + 0x1.0p-20f);
+    v.fmaxx = (float)(4 * nd[0] - 1); v.fmaxy = (float)(4 * nd[1] - 1); v.fmaxz = (float)(4 * nd[2] - 1);
     const int ncell = nd[0] * nd[1] * nd[2];
     std::vector<std::vector<uint16_t>> cells(ncell);
+    std::vector<uint64_t> mask(ncell, 0);
     for (int i = 0; i < n; ++i) {
         const double* lo = &hw.aabbs[(size_t)i * 6];
         const double* hi = lo + 3;
-        int c0[3], c1[3];
+        int f0[3], f1[3];
         for (int k = 0; k < 3; ++k) {
-            c0[k] = cell_of(lo[k], g0[k], inv[k], nd[k]);
-            c1[k] = cell_of(hi[k], g0[k], inv[k], nd[k]);
+            f0[k] = fine_index(fine_coord(lo[k], of[k], i4[k]), nd[k]);
+            f1[k] = fine_index(fine_coord(hi[k], of[k], i4[k]), nd[k]);
         }
-        meta[i] |= ((uint32_t)c0[0] << 8) | ((uint32_t)c0[1] << 16) | ((uint32_t)c0[2] << 24);
-        for (int z = c0[2]; z <= c1[2]; ++z)
-            for (int y = c0[1]; y <= c1[1]; ++y)
-                for (int x = c0[0]; x <= c1[0]; ++x)
+        meta[i] |= ((uint32_t)(f0[0] >> 2) << 8) | ((uint32_t)(f0[1] >> 2) << 16) |
+                   ((uint32_t)(f0[2] >> 2) << 24);
+        for (int z = f0[2] >> 2; z <= f1[2] >> 2; ++z)
+            for (int y = f0[1] >> 2; y <= f1[1] >> 2; ++y)
+                for (int x = f0[0] >> 2; x <= f1[0] >> 2; ++x)
                     cells[((size_t)z * nd[1] + y) * nd[0] + x].push_back((uint16_t)i);
+        for (int z = f0[2]; z <= f1[2]; ++z)
+            for (int y = f0[1]; y <= f1[1]; ++y)
+                for (int x = f0[0]; x <= f1[0]; ++x) {
+                    const size_t c = ((size_t)(z >> 2) * nd[1] + (y >> 2)) * nd[0] + (x >> 2);
+                    mask[c] |= 1ull << (((z & 3) * 4 + (y & 3)) * 4 + (x & 3));
+                }
     }
     std::vector<uint32_t> cell_start(ncell + 1, 0);
     for (int c = 0; c < ncell; ++c) cell_start[c + 1] = cell_start[c] + (uint32_t)cells[c].size();
     const size_t n_entries = cell_start[ncell];
-    // ---- pack ------------------------------------------------------------------
-    const size_t bytes_soa = soa.size() * sizeof(double);
-    const size_t off_meta = bytes_soa;
-    const size_t off_cs = align16(off_meta + meta.size() * 4);
-    const size_t off_co = align16(off_cs + cell_start.size() * 4);
-    const size_t total = align16(off_co + n_entries * 2);
+    // ---- pack (layout in epp_internal.h) ---------------------------------------
+    const size_t off_mask = 0;
+    const size_t off_cs = align16(off_mask + mask.size() * 8);
+    const size_t front = align16(off_cs + cell_start.size() * 4);
+    const size_t off_co = front;
+    const size_t off_meta = align16(off_co + n_entries * 2);
+    const size_t off_soa = align16(off_meta + meta.size() * 4);
+    const size_t total = align16(off_soa + soa.size() * sizeof(double));
     if (total > 0xFFFFFFFFull) {
         set_error("epp_world: index too large");
         return false;
     }
     hw.blob.assign(total, '\0');
     char* b = &hw.blob[0];
-    std::memcpy(b, soa.data(), bytes_soa);
-    std::memcpy(b + off_meta, meta.data(), meta.size() * 4);
+    std::memcpy(b + off_mask, mask.data(), mask.size() * 8);
     std::memcpy(b + off_cs, cell_start.data(), cell_start.size() * 4);
     size_t pos = off_co;
     for (int c = 0; c < ncell; ++c) {
         if (!cells[c].empty()) std::memcpy(b + pos, cells[c].data(), cells[c].size() * 2);
         pos += cells[c].size() * 2;
     }
+    std::memcpy(b + off_meta, meta.data(), meta.size() * 4);
+    std::memcpy(b + off_soa, soa.data(), soa.size() * sizeof(double));
     v.blob_bytes = (uint32_t)total;
-    v.off_meta = (uint32_t)off_meta;
+    v.front_bytes = (uint32_t)front;
+    v.off_cell_mask = (uint32_t)off_mask;
     v.off_cell_start = (uint32_t)off_cs;
     v.off_cell_obb = (uint32_t)off_co;
+    v.off_meta = (uint32_t)off_meta;
+    v.off_soa = (uint32_t)off_soa;
     return true;
 }
 
