@@ -1,0 +1,202 @@
+// online_traj_planner — drop-in for the reference's pybind module (src/pybind.cpp:10-27):
+// the OnlineTrajGenerator class with the same method names, argument names and return
+// shapes (numpy arrays where the reference returns Eigen objects), plus the Vector3d /
+// MatrixXd helper classes.  Every call releases the GIL while the GPU path runs.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "epp/OnlineTrajGenerator.h"
+
+namespace py = pybind11;
+using epp::Matrix;
+using epp::Vec3;
+
+using DArr = py::array_t<double, py::array::c_style | py::array::forcecast>;
+
+static Vec3 to_vec3(const py::object& o) {
+    if (py::isinstance<Vec3>(o)) return o.cast<Vec3>();
+    DArr a = DArr::ensure(o);
+    if (!a || a.size() != 3) throw std::invalid_argument("expected 3 values");
+    return Vec3(a.data()[0], a.data()[1], a.data()[2]);
+}
+
+static Matrix to_matrix(const py::object& o) {
+    if (py::isinstance<Matrix>(o)) return o.cast<Matrix>();
+    DArr a = DArr::ensure(o);
+    if (!a) throw std::invalid_argument("expected a 2-D array");
+    if (a.ndim() == 1 && a.size() == 0) return Matrix();
+    if (a.ndim() != 2) throw std::invalid_argument("expected a 2-D array");
+    Matrix m((size_t)a.shape(0), (size_t)a.shape(1));
+    if (a.size()) std::memcpy(m.data.data(), a.data(), (size_t)a.size() * sizeof(double));
+    return m;
+}
+
+static py::array_t<double> from_matrix(const Matrix& m) {
+    py::array_t<double> out({(py::ssize_t)m.rows, (py::ssize_t)m.cols});
+    if (!m.data.empty()) std::memcpy(out.mutable_data(), m.data.data(), m.data.size() * sizeof(double));
+    return out;
+}
+
+PYBIND11_MODULE(online_traj_planner, m) {
+    m.doc() = "MI355X drop-in of the online_traj_planner module (OnlineTrajGenerator)";
+
+    py::class_<Vec3>(m, "Vector3d")
+        .def(py::init([](const py::object& o) { return to_vec3(o); }))
+        .def("__array__", [](const Vec3& v, py::args, py::kwargs) {
+            py::array_t<double> a(3);
+            a.mutable_data()[0] = v.x;
+            a.mutable_data()[1] = v.y;
+            a.mutable_data()[2] = v.z;
+            return a;
+        })
+        .def("__repr__", [](const Vec3& v) {
+            return "Vector3d(" + std::to_string(v.x) + ", " + std::to_string(v.y) + ", " + std::to_string(v.z) + ")";
+        });
+
+    py::class_<Matrix>(m, "MatrixXd")
+        .def(py::init([](const py::object& o) { return to_matrix(o); }))
+        .def("__array__", [](const Matrix& mat, py::args, py::kwargs) { return from_matrix(mat); })
+        .def_property_readonly("shape", [](const Matrix& mat) { return py::make_tuple(mat.rows, mat.cols); });
+
+    // PathPlanner (include/PathPlanner.h:30-80) — not bound by the reference, exposed here
+    // so its planner, pruning and trajectory check can be driven and tested from Python.
+    py::class_<epp::PathPlanner>(m, "PathPlanner")
+        .def(py::init([](const py::object& gates, const py::object& obstacles, const std::string& configPath) {
+                 Matrix gm = to_matrix(gates), om = to_matrix(obstacles);
+                 auto cfg = std::make_shared<epp::ConfigParser>(configPath);
+                 py::gil_scoped_release release;
+                 return new epp::PathPlanner(gm, om, cfg);
+             }),
+             py::arg("nominalGatePositionAndType"), py::arg("nominalObstaclePosition"), py::arg("configPath"))
+        .def(
+            "plan_path",
+            [](const epp::PathPlanner& self, const py::object& start, const py::object& goal,
+               double timeLimit) -> py::object {
+                Vec3 s = to_vec3(start), g = to_vec3(goal);
+                std::vector<Vec3> path;
+                bool ok;
+                {
+                    py::gil_scoped_release release;
+                    ok = self.planPath(s, g, timeLimit, path);
+                }
+                if (!ok) return py::none();
+                py::array_t<double> out({(py::ssize_t)path.size(), (py::ssize_t)3});
+                for (size_t i = 0; i < path.size(); ++i)
+                    for (int k = 0; k < 3; ++k) out.mutable_data()[i * 3 + k] = path[i][k];
+                return out;
+            },
+            py::arg("start"), py::arg("goal"), py::arg("timeLimit") = 1.0)
+        .def(
+            "include_gates2",
+            [](const epp::PathPlanner& self, const py::list& segments) {
+                std::vector<std::vector<Vec3>> wp;
+                for (const auto& s : segments) {
+                    Matrix m = to_matrix(py::reinterpret_borrow<py::object>(s));
+                    if (m.cols != 3) throw std::invalid_argument("segments must be (n, 3) arrays");
+                    std::vector<Vec3> seg;
+                    for (size_t i = 0; i < m.rows; ++i) seg.emplace_back(m(i, 0), m(i, 1), m(i, 2));
+                    if (seg.empty()) throw std::invalid_argument("empty segment");
+                    wp.push_back(std::move(seg));
+                }
+                if (wp.empty()) throw std::invalid_argument("no segments");
+                std::vector<Vec3> flat;
+                {
+                    py::gil_scoped_release release;
+                    flat = self.includeGates2(wp);
+                }
+                py::array_t<double> out({(py::ssize_t)flat.size(), (py::ssize_t)3});
+                for (size_t i = 0; i < flat.size(); ++i)
+                    for (int k = 0; k < 3; ++k) out.mutable_data()[i * 3 + k] = flat[i][k];
+                return out;
+            },
+            py::arg("waypoints"))
+        .def(
+            "check_trajectory_validity",
+            [](const epp::PathPlanner& self, const py::object& traj, double minDistance) {
+                Matrix m = to_matrix(traj);
+                py::gil_scoped_release release;
+                return self.checkTrajectoryValidity(m, minDistance);
+            },
+            py::arg("trajectory"), py::arg("minDistance"))
+        .def(
+            "check_point_validity",
+            [](const epp::PathPlanner& self, const py::object& p, bool canPassGate) {
+                return self.worldPtr->checkPointValidity(to_vec3(p), canPassGate);
+            },
+            py::arg("point"), py::arg("canPassGate"))
+        .def(
+            "check_ray_valid",
+            [](const epp::PathPlanner& self, const py::object& a, const py::object& b, bool canPassGate) {
+                return self.worldPtr->checkRayValid(to_vec3(a), to_vec3(b), canPassGate);
+            },
+            py::arg("start"), py::arg("end"), py::arg("canPassGate") = false)
+        .def("update_gate_pos",
+             [](epp::PathPlanner& self, int gateId, const std::vector<double>& pose) { self.updateGatePos(gateId, pose); })
+        .def("set_seed", &epp::PathPlanner::setSeed)
+        .def("set_neighbours", &epp::PathPlanner::setNeighbours)
+        .def("last_stats", [](const epp::PathPlanner& self) {
+            const auto& s = self.lastStats();
+            py::dict d;
+            d["states_sampled"] = s.states_sampled;
+            d["states_valid"] = s.states_valid;
+            d["edges_checked"] = s.edges_checked;
+            d["edges_valid"] = s.edges_valid;
+            d["attempts"] = s.attempts;
+            d["ms"] = s.ms;
+            return d;
+        });
+
+    py::class_<epp::OnlineTrajGenerator>(m, "OnlineTrajGenerator")
+        .def(py::init([](const py::object& start, const py::object& goal, const py::object& gates,
+                         const py::object& obstacles, const std::string& configPath) {
+                 Vec3 s = to_vec3(start), g = to_vec3(goal);
+                 Matrix gm = to_matrix(gates), om = to_matrix(obstacles);
+                 py::gil_scoped_release release;
+                 return new epp::OnlineTrajGenerator(s, g, gm, om, configPath);
+             }),
+             py::arg("start"), py::arg("goal"), py::arg("nominalGatePositionAndType"),
+             py::arg("nominalObstaclePosition"), py::arg("configPath"))
+        .def("pre_compute_traj", &epp::OnlineTrajGenerator::preComputeTraj, py::arg("takeoffTime"),
+             py::call_guard<py::gil_scoped_release>())
+        .def(
+            "update_gate_pos",
+            [](epp::OnlineTrajGenerator& self, int gateId, const py::object& newPose, const py::object& dronePos,
+               bool nextGateWithinRange, double flightTime) {
+                DArr p = DArr::ensure(newPose);
+                if (!p || p.size() < 6) throw std::invalid_argument("newPose needs 6 values");
+                std::vector<double> pose(p.data(), p.data() + p.size());
+                Vec3 d = to_vec3(dronePos);
+                py::gil_scoped_release release;
+                return self.updateGatePos(gateId, pose, d, nextGateWithinRange, flightTime);
+            },
+            py::arg("gateId"), py::arg("newPose"), py::arg("dronePos"), py::arg("nextGateWithinRange"),
+            py::arg("flightTime"))
+        .def(
+            "sample_traj",
+            [](const epp::OnlineTrajGenerator& self, double t) {
+                std::vector<double> r = self.sampleTraj(t);
+                py::array_t<double> out((py::ssize_t)r.size());
+                std::memcpy(out.mutable_data(), r.data(), r.size() * sizeof(double));
+                return out;
+            },
+            py::arg("currentTime"))
+        .def("get_traj_end_time", &epp::OnlineTrajGenerator::getTrajEndTime)
+        .def("get_planned_traj", [](const epp::OnlineTrajGenerator& self) { return from_matrix(self.getPlannedTraj()); })
+        // additions of this build
+        .def("wait_for_update", &epp::OnlineTrajGenerator::waitForUpdate, py::call_guard<py::gil_scoped_release>())
+        .def(
+            "planner", [](epp::OnlineTrajGenerator& self) -> epp::PathPlanner& { return self.planner(); },
+            py::return_value_policy::reference_internal)
+        .def("get_checkpoints", [](const epp::OnlineTrajGenerator& self) {
+            const auto& c = self.getCheckpoints();
+            py::array_t<double> out({(py::ssize_t)c.size(), (py::ssize_t)3});
+            for (size_t i = 0; i < c.size(); ++i)
+                for (int k = 0; k < 3; ++k) out.mutable_data()[i * 3 + k] = c[i][k];
+            return out;
+        });
+}

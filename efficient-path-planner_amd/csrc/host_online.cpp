@@ -1,0 +1,280 @@
+// host_online.cpp — epp::OnlineTrajGenerator, the drop-in for the reference's
+// OnlineTrajGenerator (src/OnlineTrajGenerator.cpp).  Each function cites the lines it
+// follows; planning and the min-snap refit run on the GPU (PathPlanner,
+// poly_traj::generateTrajectory).
+#include <chrono>
+#include <cmath>
+#include <iostream>
+#include <limits>
+#include <stdexcept>
+
+#include "epp/OnlineTrajGenerator.h"
+#include "epp/trajectory_generator.h"
+
+namespace epp {
+
+OnlineTrajGenerator::OnlineTrajGenerator(const Vec3& start, const Vec3& goal, const Matrix& gates,
+                                         const Matrix& obstacles, const std::string& configPath)
+    : OnlineTrajGenerator(start, goal, gates, obstacles, std::make_shared<ConfigParser>(configPath)) {}
+
+OnlineTrajGenerator::OnlineTrajGenerator(const Vec3& start, const Vec3& goal, const Matrix& gates,
+                                         const Matrix& obstacles, std::shared_ptr<ConfigParser> config)
+    : configParser(std::move(config)),
+      pathPlanner(gates, obstacles, configParser),
+      nominalGatePositionAndType(gates),
+      nominalObstaclePosition(obstacles) {
+    init(start, goal);
+}
+
+OnlineTrajGenerator::~OnlineTrajGenerator() {
+    try {
+        waitForUpdate();
+    } catch (...) {
+    }
+}
+
+void OnlineTrajGenerator::waitForUpdate() {
+    if (pending.valid()) pending.get();
+}
+
+std::vector<double> OnlineTrajGenerator::gateRow(int gateId) const {
+    if (gateId < 0 || (size_t)gateId >= nominalGatePositionAndType.rows)
+        throw std::out_of_range("gate id " + std::to_string(gateId));
+    return std::vector<double>(nominalGatePositionAndType.row(gateId),
+                               nominalGatePositionAndType.row(gateId) + nominalGatePositionAndType.cols);
+}
+
+// checkpoints — src/OnlineTrajGenerator.cpp:32-47
+void OnlineTrajGenerator::init(const Vec3& start, const Vec3& goal) {
+    checkpoints.push_back(start);
+    const double offset = configParser->getPathPlannerProperties().checkpointGateOffset;
+    for (size_t i = 0; i < nominalGatePositionAndType.rows; ++i) {
+        Vec3 center, normal;
+        getGateCenterAndNormal(gateRow((int)i), center, normal);
+        checkpoints.push_back(center - normal * offset);
+        checkpoints.push_back(center + normal * offset);
+    }
+    checkpoints.push_back(goal);
+}
+
+// src/OnlineTrajGenerator.cpp:50-70
+bool OnlineTrajGenerator::getGateCenterAndNormal(const std::vector<double>& g, Vec3& center, Vec3& normal) const {
+    if (g[3] != 0 || g[4] != 0) {
+        std::cerr << "Only simple rotation around z axis is supported" << std::endl;
+        return false;
+    }
+    const double h = configParser->getObjectPropertiesByTypeId((int)g[6]).height;
+    center = Vec3(g[0], g[1], g[2]) + Vec3(0, 0, h);
+    normal = Vec3(-std::sin(g[5]), std::cos(g[5]), 0);
+    const double nn = normal.norm();
+    if (nn > 0) normal = normal / nn;  // normalize()
+    return true;
+}
+
+Matrix OnlineTrajGenerator::generate(const std::vector<Vec3>& path, double t0, const Vec3& v0, const Vec3& a0) const {
+    const auto& tg = configParser->getTrajectoryGeneratorProperties();
+    if (tg.type == "snap") {
+        Matrix traj;
+        poly_traj::generateTrajectory(path, tg.maxVelocity, tg.maxAcceleration, tg.samplingInterval, t0, v0, a0, traj);
+        return traj;
+    }
+    if (tg.type == "spline" || tg.type == "optimal")
+        throw std::runtime_error("Trajectory type '" + tg.type +
+                                 "' is not part of this build (only \"snap\", the min-snap path, is)");
+    std::cerr << "Trajectory type not supported" << std::endl;
+    throw std::runtime_error("Trajectory type not supported");
+}
+
+// OnlineTrajGenerator::preComputeTraj — src/OnlineTrajGenerator.cpp:72-121
+void OnlineTrajGenerator::preComputeTraj(double takeoffTime) {
+    waitForUpdate();
+    const double timeLimit = configParser->getPathPlannerProperties().timeLimitOffline;
+    pathSegments.clear();
+    for (size_t i = 0; i + 1 < checkpoints.size(); i += 2) {
+        std::vector<Vec3> path;
+        if (!pathPlanner.planPath(checkpoints[i], checkpoints[i + 1], timeLimit, path))
+            throw std::runtime_error("Path not found");
+        pathSegments.push_back(path);
+    }
+    const std::vector<Vec3> pruned = pathPlanner.includeGates2(pathSegments);
+    Matrix traj = generate(pruned, takeoffTime, Vec3(0, 0, 0), Vec3(0, 0, 0));
+    std::lock_guard<std::mutex> lk(trajMu);
+    plannedTraj = std::move(traj);
+}
+
+// OnlineTrajGenerator::checkGatePassed — src/OnlineTrajGenerator.cpp:228-256
+bool OnlineTrajGenerator::checkGatePassed(const Vec3& pos1, const Vec3& pos2, int gateId) const {
+    const std::vector<double> gate = gateRow(gateId);
+    Vec3 center, normal;
+    getGateCenterAndNormal(gate, center, normal);
+    const double c = std::cos(gate[5]), s = std::sin(gate[5]);
+    const Vec3 t1 = pos1 - center, t2 = pos2 - center;
+    const Vec3 g1(c * t1.x - s * t1.y, s * t1.x + c * t1.y, t1.z);
+    const Vec3 g2(c * t2.x - s * t2.y, s * t2.x + c * t2.y, t2.z);
+    if (g1.y < 0 && g2.y > 0) {
+        const Vec3 m = (g1 + g2) / 2;
+        const double edgeLength = 0.425;
+        if (std::abs(m.x) <= edgeLength && std::abs(m.z) <= edgeLength) return true;
+    }
+    return false;
+}
+
+// OnlineTrajGenerator::updateGatePos — src/OnlineTrajGenerator.cpp:123-226
+bool OnlineTrajGenerator::updateGatePos(int gateId, const std::vector<double>& newPose, const Vec3& dronePos,
+                                        bool nextGateWithinRange, double flightTime) {
+    if (!nextGateWithinRange) return false;
+    if (gatesObservedWithinRange.count(gateId)) return false;
+    if (!pathPlanner.worldPtr->checkPointValidity(dronePos, false)) return false;
+    if (newPose.size() < 6) throw std::invalid_argument("newPose needs 6 values");
+    waitForUpdate();
+    gatesObservedWithinRange.insert(gateId);
+    for (int k = 0; k < 6; ++k) nominalGatePositionAndType(gateId, k) = newPose[k];
+    pathPlanner.parseGatesAndObstacles(nominalGatePositionAndType, nominalObstaclePosition);
+
+    Matrix traj;
+    {
+        std::lock_guard<std::mutex> lk(trajMu);
+        traj = plannedTraj;
+    }
+    if (traj.rows == 0) throw std::runtime_error("No trajectory data available.");
+    const size_t tc = traj.cols - 1;
+    size_t startIdx = 0;
+    double best = std::numeric_limits<double>::infinity();
+    for (size_t i = 0; i < traj.rows; ++i) {  // timeDifferences.minCoeff(&startIdx): first minimum
+        const double d = std::abs(traj(i, tc) - flightTime);
+        if (d < best) {
+            best = d;
+            startIdx = i;
+        }
+    }
+    const size_t next = 2 * (size_t)gateId + 3 < checkpoints.size() ? 2 * (size_t)gateId + 3 : checkpoints.size() - 1;
+    const Vec3 nc = checkpoints[next];
+    size_t endIdx = 0;
+    best = std::numeric_limits<double>::infinity();
+    for (size_t i = 0; i < traj.rows; ++i) {
+        const double d = (Vec3(traj(i, 0), traj(i, 3), traj(i, 6)) - nc).norm();
+        if (d < best) {
+            best = d;
+            endIdx = i;
+        }
+    }
+    Matrix look(endIdx > startIdx ? endIdx - startIdx : 0, traj.cols);
+    for (size_t i = 0; i < look.rows; ++i)
+        for (size_t c = 0; c < traj.cols; ++c) look(i, c) = traj(startIdx + i, c);
+    bool passing = false, valid = false;
+    for (size_t i = 0; i + 1 < look.rows; ++i) {
+        if (checkGatePassed(Vec3(look(i, 0), look(i, 3), look(i, 6)), Vec3(look(i + 1, 0), look(i + 1, 3), look(i + 1, 6)),
+                            gateId)) {
+            passing = true;
+            break;
+        }
+    }
+    if (passing)
+        valid = pathPlanner.checkTrajectoryValidity(look, configParser->getPathPlannerProperties().minDistCheckTrajCollision);
+    if (valid && passing) return false;
+    if (trajectoryCurrentlyUpdating) {
+        std::cerr << "Call to update trajectory, while previous update is still going on";
+        throw std::runtime_error("Call to update trajectory, while previous update is still going on");
+    }
+    trajectoryCurrentlyUpdating = true;
+    if (configParser->getPathPlannerProperties().recalculateOnline) {
+        pending = std::async(std::launch::async, [this, gateId, dronePos, flightTime] {
+            recomputeTraj(gateId, dronePos, flightTime);
+        });
+    } else {
+        recomputeTraj(gateId, dronePos, flightTime);
+    }
+    return true;
+}
+
+// OnlineTrajGenerator::recomputeTraj — src/OnlineTrajGenerator.cpp:258-421
+void OnlineTrajGenerator::recomputeTraj(int gateId, const Vec3& /*dronePos*/, double flightTime) {
+    struct Reset {
+        bool& f;
+        ~Reset() { f = false; }
+    } reset{trajectoryCurrentlyUpdating};
+    const auto& pp = configParser->getPathPlannerProperties();
+    const int segPre = gateId, segPost = gateId + 1;
+    const size_t cpPre = 2 * (size_t)gateId + 1, cpPost = 2 * (size_t)gateId + 2, cpNext = 2 * (size_t)gateId + 3;
+    Vec3 center, normal;
+    getGateCenterAndNormal(gateRow(segPre), center, normal);
+    checkpoints[cpPre] = center - normal * pp.checkpointGateOffset;
+    checkpoints[cpPost] = center + normal * pp.checkpointGateOffset;
+
+    double advancedTime = flightTime;
+    if (pp.advanceForCalculation) advancedTime += pp.timeLimitOnline + 0.01;
+    Matrix traj;
+    {
+        std::lock_guard<std::mutex> lk(trajMu);
+        traj = plannedTraj;
+    }
+    const size_t tc = traj.cols - 1;
+    size_t startAdv = 0;
+    for (; startAdv < traj.rows; ++startAdv)
+        if (traj(startAdv, tc) > advancedTime) break;
+    const size_t sRow = std::min(startAdv + 1, traj.rows - 1);  // plannedTraj.row(startIdxAdvanced + 1)
+    const Vec3 posA(traj(sRow, 0), traj(sRow, 3), traj(sRow, 6));
+    const Vec3 velA(traj(sRow, 1), traj(sRow, 4), traj(sRow, 7));
+    const Vec3 accA(traj(sRow, 2), traj(sRow, 5), traj(sRow, 8));
+    if (!pathPlanner.worldPtr->checkPointValidity(posA, pp.canPassGate)) {
+        std::cerr << "Advanced trajectory does not end at valid position. No recomputation and hope for best"
+                  << std::endl;
+        return;
+    }
+    if (cpNext >= checkpoints.size()) throw std::runtime_error("Post segment path not found. Exiting");
+    // the two segments are planned back to back; each is one batched GPU pass
+    std::vector<Vec3> pre, post;
+    const bool okPre = pathPlanner.planPath(posA, checkpoints[cpPre], pp.timeLimitOnline, pre);
+    const bool okPost = pathPlanner.planPath(checkpoints[cpPost], checkpoints[cpNext], pp.timeLimitOnline, post);
+    if (!okPre) {
+        std::cerr << "Pre path not found. Exiting" << std::endl;
+        throw std::runtime_error("Pre path not found. Exiting");
+    }
+    pathSegments[segPre] = pre;
+    if (!okPost) {
+        std::cerr << "Post segment path not found. Exiting" << std::endl;
+        throw std::runtime_error("Post segment path not found. Exiting");
+    }
+    pathSegments[segPost] = post;
+    std::vector<std::vector<Vec3>> slice(pathSegments.begin() + segPre, pathSegments.end());
+    const std::vector<Vec3> filled = pathPlanner.includeGates2(slice);
+    const Matrix postTraj = generate(filled, advancedTime, velA, accA);
+    Matrix merged(startAdv + postTraj.rows, traj.cols);
+    for (size_t i = 0; i < startAdv; ++i)
+        for (size_t c = 0; c < traj.cols; ++c) merged(i, c) = traj(i, c);
+    for (size_t i = 0; i < postTraj.rows; ++i)
+        for (size_t c = 0; c < traj.cols; ++c) merged(startAdv + i, c) = postTraj(i, c);
+    std::lock_guard<std::mutex> lk(trajMu);
+    plannedTraj = std::move(merged);
+}
+
+// src/OnlineTrajGenerator.cpp:423-439
+std::vector<double> OnlineTrajGenerator::sampleTraj(double currentTime) const {
+    std::lock_guard<std::mutex> lk(trajMu);
+    if (plannedTraj.rows == 0) throw std::runtime_error("No trajectory data available.");
+    const size_t tc = plannedTraj.cols - 1;
+    size_t best_i = 0;
+    double best = std::numeric_limits<double>::infinity();
+    for (size_t i = 0; i < plannedTraj.rows; ++i) {
+        const double d = std::abs(plannedTraj(i, tc) - currentTime);
+        if (d < best) {
+            best = d;
+            best_i = i;
+        }
+    }
+    return std::vector<double>(plannedTraj.row(best_i), plannedTraj.row(best_i) + plannedTraj.cols);
+}
+
+double OnlineTrajGenerator::getTrajEndTime() const {
+    std::lock_guard<std::mutex> lk(trajMu);
+    if (plannedTraj.rows == 0) throw std::runtime_error("No trajectory data available.");
+    return plannedTraj(plannedTraj.rows - 1, plannedTraj.cols - 1);
+}
+
+Matrix OnlineTrajGenerator::getPlannedTraj() const {
+    std::lock_guard<std::mutex> lk(trajMu);
+    if (plannedTraj.rows == 0) throw std::runtime_error("No trajectory data available.");
+    return plannedTraj;
+}
+
+}  // namespace epp

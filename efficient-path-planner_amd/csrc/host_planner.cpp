@@ -1,0 +1,301 @@
+// host_planner.cpp — epp::PathPlanner (drop-in for src/PathPlanner.cpp) on the batch
+// GPU planner.  See include/epp/PathPlanner.h for the algorithm.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <iostream>
+#include <limits>
+#include <mutex>
+#include <queue>
+#include <stdexcept>
+#include <utility>
+
+#include "epp/PathPlanner.h"
+#include "host_scratch.h"
+
+namespace epp {
+
+namespace {
+std::mutex g_stats_mu;
+
+uint64_t mix(uint64_t a, uint64_t b) {
+    uint64_t x = a ^ (b + 0x9E3779B97F4A7C15ull + (a << 6) + (a >> 2));
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+uint64_t bits_of(double d) {
+    uint64_t u;
+    std::memcpy(&u, &d, 8);
+    return u;
+}
+}  // namespace
+
+PathPlanner::PathPlanner(const Matrix& gates, const Matrix& obstacles, std::shared_ptr<ConfigParser> cp)
+    : configParser(std::move(cp)) {
+    worldPtr = std::make_shared<World>(configParser);
+    parseGatesAndObstacles(gates, obstacles);  // src/PathPlanner.cpp:27-35
+}
+
+// src/PathPlanner.cpp:60-78
+void PathPlanner::parseGatesAndObstacles(const Matrix& gates, const Matrix& obstacles) {
+    worldPtr->resetWorld();
+    for (size_t i = 0; i < gates.rows; ++i) {
+        std::vector<double> g(gates.row(i), gates.row(i) + gates.cols);
+        if (g.size() < 7) throw std::invalid_argument("gate rows need 7 columns");
+        g[2] = 0.0;  // put all gates to ground  :68
+        worldPtr->addGate((int)i, g);
+    }
+    for (size_t i = 0; i < obstacles.rows; ++i) {
+        std::vector<double> o(obstacles.row(i), obstacles.row(i) + obstacles.cols);
+        if (o.size() < 6) throw std::invalid_argument("obstacle rows need 6 columns");
+        worldPtr->addObstacle((int)i, o);
+    }
+}
+
+void PathPlanner::updateGatePos(int gateId, const std::vector<double>& newPose) {
+    worldPtr->updateGatePosition(gateId, newPose);  // src/PathPlanner.cpp:170-173
+}
+
+bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples, uint64_t seed,
+                           std::vector<Vec3>& out) const {
+    const auto& pp = configParser->getPathPlannerProperties();
+    const auto& wp = configParser->getWorldProperties();
+    const bool canPass = pp.canPassGate;  // validators get can_pass_gate  src/PathPlanner.cpp:47-50
+    const epp_world* w = worldPtr->device();
+    const int k = k_;
+    ThreadScratch& ts = ThreadScratch::get();
+    void* st = ts.stream();
+    // ---- 1. sample + validate states (StateValidator::isValid) --------------------------
+    const size_t n_s = (size_t)samples;
+    ts.reset(ThreadScratch::rounded(n_s * 24) + ThreadScratch::rounded(n_s));
+    double* d_s = static_cast<double*>(ts.carve(n_s * 24));
+    uint8_t* d_v = static_cast<uint8_t*>(ts.carve(n_s));
+    const double lo[3] = {wp.lowerBound.x, wp.lowerBound.y, wp.lowerBound.z};
+    const double hi[3] = {wp.upperBound.x, wp.upperBound.y, wp.upperBound.z};
+    check(epp_sample_uniform(seed, lo, hi, samples, 0, d_s, st), "sample");
+    check(epp_check_states(w, d_s, samples, canPass ? 1 : 0, d_v, nullptr, nullptr, st), "state check");
+    std::vector<double> xyz(n_s * 3);
+    std::vector<uint8_t> valid(n_s);
+    check(epp_memcpy_d2h(xyz.data(), d_s, n_s * 24, st), "download");
+    check(epp_memcpy_d2h(valid.data(), d_v, n_s, st), "download");
+    // nodes: start, goal, then the valid samples in sample order
+    std::vector<double> nodes = {start.x, start.y, start.z, goal.x, goal.y, goal.z};
+    for (size_t i = 0; i < n_s; ++i)
+        if (valid[i]) nodes.insert(nodes.end(), &xyz[3 * i], &xyz[3 * i + 3]);
+    const int32_t n = (int32_t)(nodes.size() / 3);
+    // ---- 2. k-NN graph + batched motion checks (MotionValidator::checkMotion) --------
+    const size_t m = (size_t)n * k;
+    ts.reset(ThreadScratch::rounded((size_t)n * 24) + ThreadScratch::rounded(m * 4) +
+             2 * ThreadScratch::rounded(m * 24) + ThreadScratch::rounded(m));
+    double* d_nodes = static_cast<double*>(ts.carve((size_t)n * 24));
+    int32_t* d_nbr = static_cast<int32_t*>(ts.carve(m * 4));
+    double* d_e1 = static_cast<double*>(ts.carve(m * 24));
+    double* d_e2 = static_cast<double*>(ts.carve(m * 24));
+    uint8_t* d_ev = static_cast<uint8_t*>(ts.carve(m));
+    check(epp_memcpy_h2d(d_nodes, nodes.data(), (uint64_t)n * 24, st), "upload");
+    check(epp_knn(d_nodes, n, k, 0.0, d_nbr, st), "knn");
+    check(epp_knn_edges(d_nodes, d_nbr, n, k, d_e1, d_e2, st), "edges");
+    check(epp_check_motions(w, d_e1, d_e2, (int64_t)m, canPass ? 1 : 0, 0, d_ev, st), "motion check");
+    std::vector<int32_t> nbr(m);
+    std::vector<uint8_t> ev(m);
+    check(epp_memcpy_d2h(nbr.data(), d_nbr, m * 4, st), "download");
+    check(epp_memcpy_d2h(ev.data(), d_ev, m, st), "download");
+    // ---- 3. shortest path over the valid edges (undirected), start = 0, goal = 1 ------
+    std::vector<std::vector<std::pair<int, double>>> adj(n);
+    int64_t n_valid_edges = 0;
+    for (int i = 0; i < n; ++i)
+        for (int c = 0; c < k; ++c) {
+            const int j = nbr[(size_t)i * k + c];
+            if (j < 0 || !ev[(size_t)i * k + c]) continue;
+            const double dx = nodes[3 * j] - nodes[3 * i], dy = nodes[3 * j + 1] - nodes[3 * i + 1],
+                         dz = nodes[3 * j + 2] - nodes[3 * i + 2];
+            const double d = std::sqrt((dx * dx + dy * dy) + dz * dz);
+            adj[i].push_back({j, d});
+            adj[j].push_back({i, d});
+            ++n_valid_edges;
+        }
+    {
+        std::lock_guard<std::mutex> lk(g_stats_mu);
+        stats_.states_sampled += samples;
+        stats_.states_valid += n - 2;
+        stats_.edges_checked += (int64_t)m;
+        stats_.edges_valid += n_valid_edges;
+    }
+    std::vector<double> dist(n, std::numeric_limits<double>::infinity());
+    std::vector<int> prev(n, -1);
+    using QE = std::pair<double, int>;
+    std::priority_queue<QE, std::vector<QE>, std::greater<QE>> q;
+    dist[0] = 0.0;
+    q.push({0.0, 0});
+    while (!q.empty()) {
+        const auto [d, u] = q.top();
+        q.pop();
+        if (d > dist[u]) continue;
+        if (u == 1) break;
+        for (const auto& [v, c] : adj[u]) {
+            const double nd = d + c;
+            if (nd < dist[v]) {
+                dist[v] = nd;
+                prev[v] = u;
+                q.push({nd, v});
+            }
+        }
+    }
+    if (prev[1] < 0) return false;
+    std::vector<Vec3> path;
+    for (int v = 1; v >= 0; v = prev[v]) path.push_back({nodes[3 * v], nodes[3 * v + 1], nodes[3 * v + 2]});
+    std::reverse(path.begin(), path.end());
+    out = shortcut(path);
+    return true;
+}
+
+// Greedy shortcutting with one batched check of every vertex pair (the role of
+// PathSimplifier::reduceVertices in src/PathPlanner.cpp:138-139).
+std::vector<Vec3> PathPlanner::shortcut(const std::vector<Vec3>& p) const {
+    const size_t L = p.size();
+    if (L < 3) return p;
+    std::vector<double> s1, s2;
+    std::vector<std::pair<int, int>> idx;
+    for (size_t i = 0; i < L; ++i)
+        for (size_t j = i + 2; j < L; ++j) {
+            s1.insert(s1.end(), {p[i].x, p[i].y, p[i].z});
+            s2.insert(s2.end(), {p[j].x, p[j].y, p[j].z});
+            idx.push_back({(int)i, (int)j});
+        }
+    std::vector<uint8_t> ok(idx.size());
+    worldPtr->checkRays(s1.data(), s2.data(), (int64_t)idx.size(), configParser->getPathPlannerProperties().canPassGate,
+                        ok.data());
+    std::vector<std::vector<uint8_t>> vis(L, std::vector<uint8_t>(L, 0));
+    for (size_t e = 0; e < idx.size(); ++e) vis[idx[e].first][idx[e].second] = ok[e];
+    std::vector<Vec3> out = {p[0]};
+    size_t cur = 0;
+    while (cur + 1 < L) {
+        size_t nxt = cur + 1;  // a path edge, valid by construction
+        for (size_t j = L - 1; j > cur + 1; --j)
+            if (vis[cur][j]) {
+                nxt = j;
+                break;
+            }
+        out.push_back(p[nxt]);
+        cur = nxt;
+    }
+    return out;
+}
+
+// PathPlanner::planPath — src/PathPlanner.cpp:80-158
+bool PathPlanner::planPath(const Vec3& start, const Vec3& goal, double timeLimit, std::vector<Vec3>& resultPath) const {
+    if (!resultPath.empty()) {
+        resultPath.clear();
+        std::cerr << "Result path not empty, clearing it" << std::endl;
+    }
+    const auto& pp = configParser->getPathPlannerProperties();
+    if (pp.planner != "rrt" && pp.planner != "fmt") {
+        std::cerr << "Unknown planner" << std::endl;
+        throw std::runtime_error("Unknown planner");  // :121-123
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    int64_t samples = pp.samplesFMT > 0 ? pp.samplesFMT : 4096;
+    const uint64_t call = __atomic_fetch_add(&calls_, 1, __ATOMIC_RELAXED);
+    uint64_t seed = mix(seed_, call);
+    for (int d = 0; d < 3; ++d) seed = mix(mix(seed, bits_of(start[d])), bits_of(goal[d]));
+    bool ok = false;
+    int attempt = 0;
+    for (; attempt < 4 && !ok; ++attempt) {
+        ok = planOnce(start, goal, samples, mix(seed, attempt), resultPath);
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (!ok && el > timeLimit) break;  // out of time: give up like solve(timeLimit)
+        samples *= 2;
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_stats_mu);
+        stats_.attempts = attempt;
+        stats_.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    if (!ok) resultPath.clear();
+    return ok;
+}
+
+// PathPlanner::includeGates2 — src/PathPlanner.cpp:175-230
+std::vector<Vec3> PathPlanner::includeGates2(std::vector<std::vector<Vec3>> waypoints) const {
+    std::vector<Vec3> gateCenters;
+    for (size_t s = 0; s + 1 < waypoints.size(); ++s) {
+        const Vec3& a = waypoints[s].back();
+        const Vec3& b = waypoints[s + 1].front();
+        gateCenters.push_back((a + b) / 2);
+    }
+    for (size_t i = 0; i < gateCenters.size(); ++i) {
+        waypoints[i].push_back(gateCenters[i]);
+        waypoints[i + 1].insert(waypoints[i + 1].begin(), gateCenters[i]);
+    }
+    const std::string method = configParser->getPathPlannerProperties().pathSimplification;
+    std::vector<Vec3> flat;
+    for (const auto& seg : waypoints) {
+        std::vector<Vec3> pruned;
+        if (method == "none") {
+            pruned = seg;
+        } else if (method == "custom") {
+            pruned = pruneWaypoints(seg);
+        } else if (method == "ompl") {
+            // smoothBSpline (OMPL) is not part of this build; the shortcut keeps the path valid
+            pruned = shortcut(seg);
+        } else {
+            std::cerr << "Unknown pruning method" << std::endl;
+            throw std::runtime_error("Unknown pruning method");
+        }
+        for (const auto& w : pruned) {
+            if (!flat.empty() && (flat.back() - w).norm() < 0.05) continue;  // :222
+            flat.push_back(w);
+        }
+    }
+    return flat;
+}
+
+// PathPlanner::pruneWaypoints — src/PathPlanner.cpp:232-265.  The reference checks
+// ray(reference, current) one at a time; every pair it could ask for is checked in one
+// batch and the same greedy walk is replayed on the answers.
+std::vector<Vec3> PathPlanner::pruneWaypoints(const std::vector<Vec3>& w) const {
+    if (w.size() < 3) return w;
+    const size_t L = w.size();
+    std::vector<double> s1, s2;
+    std::vector<std::pair<int, int>> idx;
+    for (size_t i = 0; i < L; ++i)
+        for (size_t j = i + 2; j < L; ++j) {
+            s1.insert(s1.end(), {w[i].x, w[i].y, w[i].z});
+            s2.insert(s2.end(), {w[j].x, w[j].y, w[j].z});
+            idx.push_back({(int)i, (int)j});
+        }
+    std::vector<uint8_t> ok(idx.size());
+    worldPtr->checkRays(s1.data(), s2.data(), (int64_t)idx.size(), true, ok.data());  // canPassGate = true
+    std::vector<std::vector<uint8_t>> vis(L, std::vector<uint8_t>(L, 1));
+    for (size_t e = 0; e < idx.size(); ++e) vis[idx[e].first][idx[e].second] = ok[e];
+    std::vector<Vec3> pruned = {w[0]};
+    size_t ref = 0;
+    for (size_t cur = 2; cur < L; ++cur) {
+        if (!vis[ref][cur]) {
+            pruned.push_back(w[cur - 1]);
+            ref = cur - 1;
+        }
+    }
+    pruned.push_back(w[L - 1]);
+    return pruned;
+}
+
+// PathPlanner::checkTrajectoryValidity — src/PathPlanner.cpp:267-280 (one batched launch)
+bool PathPlanner::checkTrajectoryValidity(const Matrix& traj, double minDistance) const {
+    if (traj.rows == 0) return true;
+    std::vector<double> xyz(traj.rows * 3);
+    for (size_t i = 0; i < traj.rows; ++i) {
+        xyz[3 * i] = traj(i, 0);
+        xyz[3 * i + 1] = traj(i, 3);
+        xyz[3 * i + 2] = traj(i, 6);
+    }
+    std::vector<uint8_t> ok(traj.rows);
+    worldPtr->checkPointsMinDistance(xyz.data(), (int64_t)traj.rows, minDistance, ok.data());
+    for (uint8_t v : ok)
+        if (!v) return false;
+    return true;
+}
+
+}  // namespace epp

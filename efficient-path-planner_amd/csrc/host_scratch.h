@@ -1,0 +1,65 @@
+// host_scratch.h — per-host-thread device staging used by the C++ API shims: one
+// non-blocking stream and one growable HBM buffer per thread, so host-array calls
+// from several threads (the reference plans two segments concurrently,
+// src/OnlineTrajGenerator.cpp:324-340) never share a stream or a buffer.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+#include "epp.h"
+
+namespace epp {
+
+inline void check(epp_status rc, const char* what) {
+    if (rc != EPP_OK) {
+        const std::string msg = std::string(what) + ": " + epp_last_error();
+        if (rc == EPP_ERR_INVALID_ARGUMENT) throw std::invalid_argument(msg);
+        throw std::runtime_error(msg);
+    }
+}
+
+class ThreadScratch {
+public:
+    static ThreadScratch& get() {
+        thread_local ThreadScratch s;
+        return s;
+    }
+    void* stream() {
+        if (!stream_) check(epp_stream_create(&stream_), "stream");
+        return stream_;
+    }
+    // Device buffer of at least `bytes`, 256-byte aligned sub-allocations handed out
+    // by `carve` until the next reset().
+    void reset(size_t bytes) {
+        bytes = (bytes + 255) & ~size_t(255);
+        if (bytes > cap_) {
+            if (buf_) epp_free(buf_);
+            buf_ = nullptr;
+            cap_ = 0;
+            check(epp_malloc(&buf_, bytes), "device scratch");
+            cap_ = bytes;
+        }
+        used_ = 0;
+    }
+    void* carve(size_t bytes) {
+        bytes = (bytes + 255) & ~size_t(255);
+        if (used_ + bytes > cap_) throw std::runtime_error("device scratch overflow");
+        void* p = static_cast<char*>(buf_) + used_;
+        used_ += bytes;
+        return p;
+    }
+    static size_t rounded(size_t bytes) { return (bytes + 255) & ~size_t(255); }
+    ~ThreadScratch() {
+        if (buf_) epp_free(buf_);
+        if (stream_) epp_stream_destroy(stream_);
+    }
+
+private:
+    void* stream_ = nullptr;
+    void* buf_ = nullptr;
+    size_t cap_ = 0, used_ = 0;
+};
+
+}  // namespace epp

@@ -72,6 +72,9 @@ def lib() -> C.CDLL:
             "epp_generate_trajectory_host": (i32, [vp, i32, dp, dp, dp, dp, vp, vp,
                                                    C.POINTER(C.POINTER(C.c_double)), C.POINTER(i64)]),
             "epp_host_free": (None, [vp]),
+            "epp_sample_uniform": (i32, [C.c_uint64, vp, vp, i64, i64, vp, vp]),
+            "epp_knn": (i32, [vp, i32, i32, dp, vp, vp]),
+            "epp_knn_edges": (i32, [vp, vp, i32, i32, vp, vp, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(l, name)
@@ -89,7 +92,8 @@ EXPORTED = [
     "epp_event_elapsed_ms", "epp_build_obbs", "epp_world_create", "epp_world_update",
     "epp_world_destroy", "epp_world_num_obbs", "epp_world_get_aabbs", "epp_check_states",
     "epp_check_states_mindist", "epp_check_motions", "epp_minsnap_batch", "epp_sample_count",
-    "epp_sample_batch", "epp_generate_trajectory_host", "epp_host_free",
+    "epp_sample_batch", "epp_generate_trajectory_host", "epp_host_free", "epp_sample_uniform", "epp_knn",
+    "epp_knn_edges",
 ]
 
 
@@ -288,3 +292,36 @@ def generate_trajectory(waypoints, v_max, a_max, dt, t0=0.0, v0=(0, 0, 0), a0=(0
     out = np.ctypeslib.as_array(rows, shape=(n.value * 10,)).copy().reshape(-1, 10)
     lib().epp_host_free(C.cast(rows, C.c_void_p))
     return out
+
+
+def sample_uniform(seed: int, lo, hi, n: int, start: int = 0) -> np.ndarray:
+    """epp_sample_uniform: n counter-based uniform states (rows start..start+n-1)."""
+    lo = np.ascontiguousarray(lo, np.float64)
+    hi = np.ascontiguousarray(hi, np.float64)
+    d = DeviceBuffer(24 * max(n, 1))
+    check(lib().epp_sample_uniform(int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(lo), _ptr(hi), int(n), int(start), d.ptr, None))
+    sync()
+    return d.download(np.float64, 3 * n).reshape(n, 3)
+
+
+def knn(nodes: np.ndarray, k: int, max_dist: float = 0.0) -> np.ndarray:
+    """epp_knn: (n, k) neighbour indices, nearest first, -1 where fewer than k exist."""
+    nodes = np.ascontiguousarray(np.asarray(nodes, np.float64).reshape(-1, 3))
+    n = len(nodes)
+    d_n = DeviceBuffer.from_array(nodes)
+    d_k = DeviceBuffer(4 * max(n * k, 1))
+    check(lib().epp_knn(d_n.ptr, n, int(k), float(max_dist), d_k.ptr, None))
+    sync()
+    return d_k.download(np.int32, n * k).reshape(n, k)
+
+
+def knn_edges(nodes: np.ndarray, nbr: np.ndarray):
+    """epp_knn_edges: the (node, neighbour) endpoint arrays of every k-NN edge."""
+    nodes = np.ascontiguousarray(np.asarray(nodes, np.float64).reshape(-1, 3))
+    nbr = np.ascontiguousarray(nbr, np.int32)
+    n, k = nbr.shape
+    d_n, d_k = DeviceBuffer.from_array(nodes), DeviceBuffer.from_array(nbr)
+    d_1, d_2 = DeviceBuffer(24 * max(n * k, 1)), DeviceBuffer(24 * max(n * k, 1))
+    check(lib().epp_knn_edges(d_n.ptr, d_k.ptr, n, k, d_1.ptr, d_2.ptr, None))
+    sync()
+    return d_1.download(np.float64, 3 * n * k).reshape(-1, 3), d_2.download(np.float64, 3 * n * k).reshape(-1, 3)

@@ -146,6 +146,20 @@ epp_status epp_sample_batch(const double* seg_times, const double* coeffs,
                             const int32_t* wp_offsets, int32_t n_tracks, double dt, const double* t0,
                             const int64_t* row_offsets, double* rows, void* stream);
 
+/* ---- batch planner building blocks (device pointers) ------------------------------- */
+/* Replace OMPL's sampler / nearest-neighbour structure behind PathPlanner::planPath
+ * (src/PathPlanner.cpp:80-158).  Counter-based uniform states in [lo, hi]:
+ * u = (splitmix64(seed ^ (3 (start + i) + d)) >> 11) * 2^-53, x_d = lo_d + (hi_d - lo_d) u. */
+epp_status epp_sample_uniform(uint64_t seed, const double lo[3], const double hi[3], int64_t n,
+                              int64_t start, double* xyz, void* stream);
+/* k nearest neighbours (k in {4, 8, 16, 32}) of every node within max_dist (<= 0: no
+ * limit), sorted by distance, ties to the lower index; missing entries are -1. */
+epp_status epp_knn(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr, void* stream);
+/* Edge endpoints for every (node i, neighbour c): s1 = nodes[i], s2 = nodes[nbr[i k + c]]
+ * (s2 = s1 for a missing neighbour).  s1, s2: n k x 3. */
+epp_status epp_knn_edges(const double* nodes, const int32_t* nbr, int32_t n, int32_t k, double* s1,
+                         double* s2, void* stream);
+
 /* ---- host-buffer convenience (synchronous; used by the C++ API shims) ------------- */
 /* generateTrajectory for one track with host buffers.  Returns the row count in
  * *n_rows; rows is (re)allocated with malloc and must be released with epp_host_free. */

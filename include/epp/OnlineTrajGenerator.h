@@ -1,0 +1,63 @@
+// epp/OnlineTrajGenerator.h — drop-in for the reference's OnlineTrajGenerator
+// (include/OnlineTrajGenerator.h:26-77, src/OnlineTrajGenerator.cpp).
+//
+// Concurrency: the reference recomputes on a detached std::thread and writes the
+// trajectory while Python may read it.  Here every access to the planned
+// trajectory goes through one mutex; with recalculate_online the recomputation runs on
+// a worker thread whose completion is awaited by the next update or the destructor.
+#pragma once
+#include <future>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "epp/ConfigParser.h"
+#include "epp/PathPlanner.h"
+#include "epp/types.h"
+
+namespace epp {
+
+class OnlineTrajGenerator {
+public:
+    OnlineTrajGenerator(const Vec3& start, const Vec3& goal, const Matrix& nominalGatePositionAndType,
+                        const Matrix& nominalObstaclePosition, const std::string& configPath);
+    OnlineTrajGenerator(const Vec3& start, const Vec3& goal, const Matrix& nominalGatePositionAndType,
+                        const Matrix& nominalObstaclePosition, std::shared_ptr<ConfigParser> config);
+    ~OnlineTrajGenerator();
+
+    void preComputeTraj(double takeoffTime);
+    bool updateGatePos(int gateId, const std::vector<double>& newPose, const Vec3& dronePos,
+                       bool nextGateWithinRange, double flightTime);
+    std::vector<double> sampleTraj(double currentTime) const;
+    double getTrajEndTime() const;
+    Matrix getPlannedTraj() const;
+
+    const std::vector<Vec3>& getCheckpoints() const { return checkpoints; }
+    PathPlanner& planner() { return pathPlanner; }
+    // waits for an in-flight online recomputation (recalculate_online)
+    void waitForUpdate();
+
+private:
+    void init(const Vec3& start, const Vec3& goal);
+    bool getGateCenterAndNormal(const std::vector<double>& gate, Vec3& center, Vec3& normal) const;
+    bool checkGatePassed(const Vec3& p1, const Vec3& p2, int gateId) const;
+    void recomputeTraj(int gateId, const Vec3& dronePos, double flightTime);
+    Matrix generate(const std::vector<Vec3>& path, double t0, const Vec3& v0, const Vec3& a0) const;
+    std::vector<double> gateRow(int gateId) const;
+
+    std::shared_ptr<ConfigParser> configParser;
+    PathPlanner pathPlanner;
+    Matrix nominalGatePositionAndType;
+    Matrix nominalObstaclePosition;
+    std::vector<Vec3> checkpoints;
+    std::set<int> gatesObservedWithinRange;
+    std::vector<std::vector<Vec3>> pathSegments;
+    Matrix plannedTraj;
+    mutable std::mutex trajMu;
+    bool trajectoryCurrentlyUpdating = false;
+    std::future<void> pending;
+};
+
+}  // namespace epp

@@ -1,0 +1,67 @@
+// epp/PathPlanner.h — drop-in for the reference's PathPlanner (include/PathPlanner.h:30-80,
+// src/PathPlanner.cpp).  OMPL is replaced by a batch planner on the GPU:
+//
+//   planPath:  sample `samples_fmt` states in the world bounds (counter RNG), check them
+//              (StateValidator semantics), connect every node to its k = 16 nearest
+//              neighbours, check all edges at once (MotionValidator semantics), search the
+//              shortest valid path on the host, then shortcut it greedily with one batched
+//              motion check of all vertex pairs (the role of reduceVertices).
+//   includeGates2 / pruneWaypoints / checkTrajectoryValidity: the reference's host logic,
+//              with every validity query batched into one GPU launch.
+//
+// Unlike RRT* with no cost threshold (which always runs to timeLimit), planPath returns
+// as soon as the batch search is done; timeLimit only bounds the retries with more
+// samples when no path is found.
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "epp/ConfigParser.h"
+#include "epp/World.h"
+#include "epp/types.h"
+
+namespace epp {
+
+struct PlannerStats {
+    int64_t states_sampled = 0;
+    int64_t states_valid = 0;
+    int64_t edges_checked = 0;
+    int64_t edges_valid = 0;
+    int attempts = 0;
+    double ms = 0;
+};
+
+class PathPlanner {
+public:
+    PathPlanner(const Matrix& nominalGatePositionAndType, const Matrix& nominalObstaclePosition,
+                std::shared_ptr<ConfigParser> configParser);
+
+    void parseGatesAndObstacles(const Matrix& nominalGatePositionAndType, const Matrix& nominalObstaclePosition);
+    bool planPath(const Vec3& start, const Vec3& goal, double timeLimit, std::vector<Vec3>& resultPath) const;
+    void updateGatePos(int gateId, const std::vector<double>& newPose);
+    bool checkTrajectoryValidity(const Matrix& trajectory, double minDistance) const;
+    std::vector<Vec3> includeGates2(std::vector<std::vector<Vec3>> waypoints) const;
+
+    // batch-planner knobs (defaults follow the config: samples_fmt samples, k = 16)
+    void setSeed(uint64_t seed) { seed_ = seed; }
+    void setNeighbours(int k) { k_ = k; }
+    const PlannerStats& lastStats() const { return stats_; }
+
+    std::shared_ptr<World> worldPtr;
+
+private:
+    std::vector<Vec3> pruneWaypoints(const std::vector<Vec3>& waypoints) const;
+    std::vector<Vec3> shortcut(const std::vector<Vec3>& path) const;
+    bool planOnce(const Vec3& start, const Vec3& goal, int64_t samples, uint64_t seed,
+                  std::vector<Vec3>& out) const;
+
+    std::shared_ptr<ConfigParser> configParser;
+    uint64_t seed_ = 0x5eedull;
+    int k_ = 16;
+    mutable uint64_t calls_ = 0;
+    mutable PlannerStats stats_;
+};
+
+}  // namespace epp

@@ -1,0 +1,362 @@
+"""GPU tests of the batch planner building blocks and the C++ API shell.
+
+* epp_sample_uniform / epp_knn / epp_knn_edges vs CPU restatements (bit-exact).
+* PathPlanner (include/epp/PathPlanner.h, the drop-in of src/PathPlanner.cpp): paths are
+  checked against the oracle's StateValidator/MotionValidator semantics; includeGates2's
+  "custom" pruning is replayed on the oracle's ray answers (src/PathPlanner.cpp:175-265);
+  checkTrajectoryValidity vs the oracle's minDistance check (:267-280).
+* OnlineTrajGenerator through the online_traj_planner module (src/pybind.cpp:10-27,
+  src/OnlineTrajGenerator.cpp): checkpoints, offline trajectory, sampling, gate updates.
+
+The batch planner is a re-design (OMPL's RRT*/FMT* are third-party): its paths are not
+the reference's paths, so the bar is validity under the oracle, not equality.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from eppamd import capi, config, synth
+
+from conftest import CONFIG
+
+pytestmark = pytest.mark.gpu
+
+
+def _write_config(tmp_path, **over):
+    c = json.load(open(CONFIG))
+    for k, v in over.items():
+        sect, key = k.split("__")
+        c[sect][key] = v
+    p = tmp_path / "config.json"
+    p.write_text(json.dumps(c))
+    return str(p), c
+
+
+def _ot():
+    import online_traj_planner
+    return online_traj_planner
+
+
+# ---------------------------------------------------------------------------- device blocks
+@pytest.mark.parametrize("start", [0, 1, 12345])
+def test_sample_uniform_bit_exact(start):
+    lo, hi = np.array([-6.0, -6.0, 0.0]), np.array([6.0, 6.0, 2.0])
+    n = 5000
+    got = capi.sample_uniform(0xC0FFEE, lo, hi, n, start)
+    ref = synth.sample_states(0xC0FFEE, lo, hi, n, start)
+    assert np.array_equal(got, ref)
+    if start == 0:
+        assert np.array_equal(got, O.sample_states(0xC0FFEE, lo, hi, n))
+
+
+def _knn_ref(nodes, k, max_dist=0.0):
+    n = len(nodes)
+    out = np.full((n, k), -1, np.int32)
+    r2 = max_dist * max_dist if max_dist > 0 else 1e300
+    for i in range(n):
+        d = nodes - nodes[i]
+        d2 = (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2]
+        cand = np.nonzero((d2 < r2) & (np.arange(n) != i))[0]
+        order = cand[np.lexsort((cand, d2[cand]))][:k]  # distance, then lower index
+        out[i, :len(order)] = order
+    return out
+
+
+@pytest.mark.parametrize("k", [4, 8, 16, 32])
+def test_knn_vs_bruteforce(k):
+    nodes = synth.sample_states(7 + k, [-2, -2, 0], [2, 2, 2], 700)
+    nodes[10] = nodes[3]              # duplicate: tie broken by index
+    nodes[500:520] = nodes[0] + 0.01  # a cluster of identical distances
+    got = capi.knn(nodes, k)
+    assert np.array_equal(got, _knn_ref(nodes, k))
+
+
+def test_knn_radius_and_small_n():
+    nodes = synth.sample_states(3, [-1, -1, 0], [1, 1, 1], 300)
+    assert np.array_equal(capi.knn(nodes, 16, 0.3), _knn_ref(nodes, 16, 0.3))
+    few = nodes[:5]
+    got = capi.knn(few, 8)
+    assert np.array_equal(got, _knn_ref(few, 8))
+    assert (got[:, 4:] == -1).all()
+    with pytest.raises(capi.EppError):
+        capi.knn(nodes, 5)
+
+
+def test_knn_edges():
+    nodes = synth.sample_states(11, [-1, -1, 0], [1, 1, 1], 40)
+    nbr = capi.knn(nodes[:6], 8)          # ragged: -1 entries become degenerate edges
+    s1, s2 = capi.knn_edges(nodes[:6], nbr)
+    i = np.repeat(np.arange(6), 8)
+    j = nbr.reshape(-1)
+    assert np.array_equal(s1, nodes[i])
+    assert np.array_equal(s2, nodes[np.where(j < 0, i, j)])
+
+
+# ---------------------------------------------------------------------------- PathPlanner
+@pytest.fixture(scope="module")
+def c1(cfg, geom):
+    g, o, start, goal = synth.c1_world()
+    rg, ro = config.inflate_radii(cfg)
+    w = O.world_build(geom, g, o, rg, ro)
+    return g, o, start, goal, w, rg, ro
+
+
+def _path_valid(path, w, rg, ro, can_pass):
+    assert O.check_states(w, rg, ro, path, can_pass).all()
+    assert O.check_motions(w, rg, ro, path[:-1], path[1:], can_pass, 0).all()
+
+
+@pytest.mark.parametrize("planner", ["fmt", "rrt"])
+def test_plan_path_valid(tmp_path, c1, planner):
+    g, o, start, goal, w, rg, ro = c1
+    path_cfg, _ = _write_config(tmp_path, path_planner_properties__planner=planner)
+    pp = _ot().PathPlanner(g, o, path_cfg)
+    path = pp.plan_path(start, goal, 2.0)
+    assert path is not None and len(path) >= 2
+    assert np.array_equal(path[0], start) and np.array_equal(path[-1], goal)
+    _path_valid(path, w, rg, ro, False)
+    st = pp.last_stats()
+    assert st["states_sampled"] >= 4096 and st["edges_checked"] > 0
+
+
+def test_plan_path_seeded_is_deterministic(c1):
+    g, o, start, goal, *_ = c1
+    a = _ot().PathPlanner(g, o, CONFIG)
+    b = _ot().PathPlanner(g, o, CONFIG)
+    pa, pb = a.plan_path(start, goal, 2.0), b.plan_path(start, goal, 2.0)
+    assert np.array_equal(pa, pb)
+
+
+def test_plan_path_blocked_goal(c1):
+    g, o, start, _, *_ = c1
+    pp = _ot().PathPlanner(g, o, CONFIG)
+    assert pp.plan_path(start, np.array([1.0, 0.5, 0.5]), 0.2) is None  # inside an obstacle
+
+
+def test_unknown_planner(tmp_path, c1):
+    g, o, start, goal, *_ = c1
+    path_cfg, _ = _write_config(tmp_path, path_planner_properties__planner="prm")
+    pp = _ot().PathPlanner(g, o, path_cfg)
+    with pytest.raises(RuntimeError, match="Unknown planner"):
+        pp.plan_path(start, goal, 1.0)
+
+
+def _prune_ref(seg, w, rg, ro):
+    """pruneWaypoints (src/PathPlanner.cpp:232-265) on the oracle's checkRayValid(.., true)."""
+    if len(seg) < 3:
+        return list(seg)
+    out = [seg[0]]
+    ref = 0
+    for cur in range(2, len(seg)):
+        ok = O.check_motions(w, rg, ro, seg[ref][None], seg[cur][None], True, 0)[0]
+        if not ok:
+            out.append(seg[cur - 1])
+            ref = cur - 1
+    out.append(seg[-1])
+    return out
+
+
+def _include_gates2_ref(segs, w, rg, ro, method):
+    segs = [list(map(np.asarray, s)) for s in segs]
+    centers = [(segs[i][-1] + segs[i + 1][0]) / 2 for i in range(len(segs) - 1)]
+    for i, c in enumerate(centers):
+        segs[i].append(c)
+        segs[i + 1].insert(0, c)
+    flat = []
+    for s in segs:
+        pr = s if method == "none" else _prune_ref(s, w, rg, ro)
+        for p in pr:
+            if flat:
+                d = flat[-1] - p
+                if np.sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]) < 0.05:
+                    continue
+            flat.append(p)
+    return np.array(flat)
+
+
+@pytest.mark.parametrize("method", ["custom", "none"])
+def test_include_gates2_matches_restatement(tmp_path, c1, method):
+    g, o, _, _, w, rg, ro = c1
+    path_cfg, _ = _write_config(tmp_path, path_planner_properties__path_simplification=method)
+    pp = _ot().PathPlanner(g, o, path_cfg)
+    rs = np.random.RandomState(5)
+    segs = []
+    for s in range(3):
+        n = 3 + 4 * s
+        segs.append(np.cumsum(rs.uniform(-0.3, 0.3, (n, 3)), 0) + [0, 0, 1.0])
+    segs[1][0] = segs[0][-1] + 0.01  # a gate centre within the 0.05 de-duplication radius
+    got = pp.include_gates2(segs)
+    ref = _include_gates2_ref(segs, w, rg, ro, method)
+    assert np.array_equal(got, ref)
+
+
+def test_include_gates2_unknown_method(tmp_path, c1):
+    g, o, *_ = c1
+    path_cfg, _ = _write_config(tmp_path, path_planner_properties__path_simplification="bogus")
+    pp = _ot().PathPlanner(g, o, path_cfg)
+    with pytest.raises(RuntimeError, match="Unknown pruning method"):
+        pp.include_gates2([np.zeros((2, 3)), np.ones((2, 3))])
+
+
+def test_check_trajectory_validity(c1):
+    g, o, start, goal, w, rg, ro = c1
+    pp = _ot().PathPlanner(g, o, CONFIG)
+    pts = synth.sample_states(77, [-2, -2, 0], [2, 2, 2], 400)
+    ok = O.check_states_mindist(w, pts, 0.1)
+    traj = np.zeros((len(pts), 10))
+    traj[:, 0], traj[:, 3], traj[:, 6] = pts[:, 0], pts[:, 1], pts[:, 2]
+    good = traj[ok == 1]
+    assert pp.check_trajectory_validity(good, 0.1)
+    assert pp.check_trajectory_validity(traj, 0.1) == bool(ok.all())
+    for i in np.nonzero(ok == 0)[0][:5]:
+        assert not pp.check_trajectory_validity(traj[i:i + 1], 0.1)
+    assert pp.check_trajectory_validity(np.zeros((0, 10)), 0.1)
+
+
+# ---------------------------------------------------------------------------- OnlineTrajGenerator
+@pytest.fixture(scope="module")
+def track(tmp_path_factory, cfg):
+    tmp = tmp_path_factory.mktemp("track")
+    c = json.load(open(CONFIG))
+    c["world_properties"]["lower_bound"] = [-6, -6, 0]
+    c["world_properties"]["upper_bound"] = [6, 6, 2]
+    p = tmp / "config.json"
+    p.write_text(json.dumps(c))
+    gates, obstacles = synth.track_world(42)
+    # start 0.55 m before gate 0, goal 0.55 m after gate 7 (obstacles keep >= 0.95 m from
+    # every gate centre, so both are free)
+    cps = synth.gate_checkpoints(gates, np.array([1.0, 0.525]), 0.55)
+    start, goal = cps[0], cps[-1]
+    return str(p), c, gates, obstacles, start, goal
+
+
+def _lateral(gate, d):
+    """Gate pose shifted by d metres inside its own plane (perpendicular to the normal)."""
+    pose = np.array(gate[:6], float)
+    pose[0] += d * np.cos(gate[5])
+    pose[1] += d * np.sin(gate[5])
+    return list(pose)
+
+
+def test_online_checkpoints(track, geom):
+    path, c, gates, obstacles, start, goal = track
+    otg = _ot().OnlineTrajGenerator(start, goal, gates, obstacles, path)
+    cps = otg.get_checkpoints()
+    ref = synth.gate_checkpoints(gates, geom.gate_height, c["path_planner_properties"]["checkpoint_gate_offset"])
+    assert np.array_equal(cps[0], start) and np.array_equal(cps[-1], goal)
+    np.testing.assert_allclose(cps[1:-1], ref, rtol=0, atol=1e-15)
+
+
+def test_online_no_traj_errors(track):
+    path, c, gates, obstacles, start, goal = track
+    otg = _ot().OnlineTrajGenerator(start, goal, gates, obstacles, path)
+    for f in (otg.get_planned_traj, otg.get_traj_end_time):
+        with pytest.raises(RuntimeError, match="No trajectory data available."):
+            f()
+    with pytest.raises(RuntimeError, match="No trajectory data available."):
+        otg.sample_traj(0.0)
+
+
+@pytest.fixture(scope="module")
+def planned(track):
+    path, c, gates, obstacles, start, goal = track
+    otg = _ot().OnlineTrajGenerator(start, goal, gates, obstacles, path)
+    otg.pre_compute_traj(1.5)
+    return otg
+
+
+def test_online_precompute(track, planned, geom):
+    path, c, gates, obstacles, start, goal = track
+    traj = planned.get_planned_traj()
+    assert traj.shape[1] == 10 and len(traj) > 100
+    dt = c["trajectory_generator_properties"]["sampling_interval"]
+    assert traj[0, 9] == 1.5
+    assert np.allclose(np.diff(traj[:, 9]), dt, atol=1e-9)
+    np.testing.assert_allclose(traj[0, [0, 3, 6]], start, atol=1e-12)
+    np.testing.assert_allclose(traj[0, [1, 4, 7, 2, 5, 8]], 0, atol=1e-9)
+    assert np.linalg.norm(traj[-1, [0, 3, 6]] - goal) < 0.1
+    assert planned.get_traj_end_time() == traj[-1, 9]
+    # the trajectory passes every gate centre (includeGates2 inserts them as waypoints)
+    pos = traj[:, [0, 3, 6]]
+    for gt in gates:
+        centre = gt[:3] + [0, 0, geom.gate_height[int(gt[6])]]
+        assert np.min(np.linalg.norm(pos - centre, axis=1)) < 0.1
+    # continuity of position and velocity between rows
+    v = traj[:, [1, 4, 7]]
+    assert np.abs(np.diff(pos, axis=0)).max() < 0.5
+    assert np.abs(np.diff(v, axis=0)).max() < 0.6
+
+
+def test_online_sample_traj(planned):
+    traj = planned.get_planned_traj()
+    for t in (0.0, 1.5, 1.54, 1.56, 7.77, 1e6):
+        row = planned.sample_traj(t)
+        i = int(np.argmin(np.abs(traj[:, 9] - t)))
+        assert np.array_equal(row, traj[i])
+
+
+def test_online_update_gate_pos(track, geom):
+    path, c, gates, obstacles, start, goal = track
+    otg = _ot().OnlineTrajGenerator(start, goal, gates, obstacles, path)
+    otg.pre_compute_traj(0.0)
+    before = otg.get_planned_traj()
+    gid = 2
+    # 0.3 m sideways: the old path still crosses the gate plane within the 0.425 m
+    # opening test but runs 0.1 m from a bar, so the lookahead check fails -> replan
+    pose = _lateral(gates[gid], 0.3)
+    # early outs (src/OnlineTrajGenerator.cpp:125-140)
+    assert otg.update_gate_pos(gid, pose, start, False, 1.0) is False
+    inside = obstacles[0, :3] + [0, 0, 0.5]  # drone inside an obstacle
+    assert otg.update_gate_pos(gid, pose, inside, True, 1.0) is False
+    t_fly = 2.0
+    i = int(np.argmin(np.abs(before[:, 9] - t_fly)))
+    drone = before[i, [0, 3, 6]]
+    assert otg.update_gate_pos(gid, pose, drone, True, t_fly) is True
+    after = otg.get_planned_traj()
+    # the prefix up to the advanced time is kept, the rest is replanned
+    adv = t_fly + c["path_planner_properties"]["time_limit_online"] + 0.01
+    k = int(np.argmax(before[:, 9] > adv))
+    assert np.array_equal(after[:k], before[:k])
+    assert not np.array_equal(after, before)
+    moved = np.array(pose[:3]) + [0, 0, geom.gate_height[int(gates[gid, 6])]]
+    assert np.min(np.linalg.norm(after[:, [0, 3, 6]] - moved, axis=1)) < 0.1
+    # already observed gate: no second update
+    assert otg.update_gate_pos(gid, pose, drone, True, t_fly) is False
+
+
+def test_online_async_update(track):
+    path, c, gates, obstacles, start, goal = track
+    c2 = json.loads(json.dumps(c))
+    c2["path_planner_properties"]["recalculate_online"] = True
+    p2 = os.path.join(os.path.dirname(path), "config_async.json")
+    open(p2, "w").write(json.dumps(c2))
+    otg = _ot().OnlineTrajGenerator(start, goal, gates, obstacles, p2)
+    otg.pre_compute_traj(0.0)
+    before = otg.get_planned_traj()
+    pose = _lateral(gates[4], 0.3)
+    i = int(np.argmin(np.abs(before[:, 9] - 5.0)))
+    assert otg.update_gate_pos(4, pose, before[i, [0, 3, 6]], True, 5.0) is True
+    otg.wait_for_update()
+    assert not np.array_equal(otg.get_planned_traj(), before)
+
+
+def test_trajectory_type_not_supported(tmp_path, track):
+    path, c, gates, obstacles, start, goal = track
+    c2 = json.loads(json.dumps(c))
+    c2["trajectory_generator_properties"]["type"] = "linear"
+    p2 = tmp_path / "c.json"
+    p2.write_text(json.dumps(c2))
+    otg = _ot().OnlineTrajGenerator(start, goal, gates, obstacles, str(p2))
+    with pytest.raises(RuntimeError, match="Trajectory type not supported"):
+        otg.pre_compute_traj(0.0)
+
+
+def test_vector_and_matrix_helpers():
+    ot = _ot()
+    v = ot.Vector3d(np.array([1.0, 2.0, 3.0]))
+    assert np.array_equal(np.asarray(v), [1, 2, 3])
+    m = ot.MatrixXd(np.arange(6.0).reshape(2, 3))
+    assert m.shape == (2, 3) and np.array_equal(np.asarray(m), np.arange(6.0).reshape(2, 3))
