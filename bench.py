@@ -11,6 +11,13 @@ Multi-GPU: one process per GPU (torchrun); every rank checks its own stream of s
 against its own copy of the world (independent samplers, no data-path collective:
 "scaling": "weak"); ranks synchronise with a barrier and the slowest rank's time is used.
 
+Full plan ms/track (the metric's second half, BASELINE configs[3] = C4): every rank plans
+its own randomised track (world seed 100 + rank, 8 gates, 24 obstacles, bounds
+[-6,6]^2 x [0,2]) end to end through the C++ API (OnlineTrajGenerator::preComputeTraj:
+9 gate-to-gate batch plans with 65,536 samples and k = 16 neighbours each, includeGates2,
+min-snap fit, sampling at dt = 0.1), then the final waypoint sets of all tracks are
+all-gathered over RCCL (the path's only exchange step).
+
 Side measurements (same JSON line, not the headline value): C3 motion checks (512 OBBs,
 analytic and 32-step discretised), the C5 batched min-snap refit (4096 x 12 segments),
 and the CPU oracle timed on the host (cpu_baseline).
@@ -33,40 +40,6 @@ N_BATCHES = 16
 BYTES_PER_STATE = 25  # 24 B xyz read + 1 B flag written
 BYTES_PER_EDGE = 49
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-
-
-def _dist_env():
-    ws = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    return ws, rank, local
-
-
-class Dist:
-    def __init__(self, ws, rank, local):
-        self.ws, self.rank, self.local = ws, rank, local
-        self.pg = None
-        if ws > 1:
-            import torch
-            import torch.distributed as dist
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-            self.dist, self.torch = dist, torch
-
-    def barrier(self):
-        if self.ws > 1:
-            self.dist.barrier()
-
-    def max(self, x: float) -> float:
-        if self.ws == 1:
-            return x
-        t = self.torch.tensor([x], dtype=self.torch.float64, device="cuda")
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
-
-    def close(self):
-        if self.ws > 1:
-            self.dist.destroy_process_group()
 
 
 def timed_kernel_ms(capi, stream, fn, reps):
@@ -96,10 +69,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-side", action="store_true", help="skip the side measurements")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--no-plan", action="store_true", help="skip the full-plan (C4) leg")
+    ap.add_argument("--plan-reps", type=int, default=3)
     args = ap.parse_args()
 
-    ws, rank, local = _dist_env()
-    dist = Dist(ws, rank, local)
+    from eppamd.dist import Dist, env
+    ws, rank, local = env()
+    dist = Dist(ws, rank, local, "nccl")
     import ctypes as C
 
     from eppamd import capi, config, synth
@@ -148,6 +124,10 @@ def main():
     achieved = BYTES_PER_STATE * N_STATES / (kms * 1e-3) / 1e9
     n_valid = int(d_valid.download(np.uint8, N_STATES).sum())
 
+    plan = None
+    if not args.no_plan:
+        plan = full_plan(dist, rank, args.plan_reps)
+
     side = {}
     if not args.no_side and rank == 0:
         side = side_measurements(capi, L, stream, geom, cfg, rg, ro)
@@ -177,12 +157,59 @@ def main():
             "roofline": {"bound": "hbm", "kernel": "k_states<true,false>", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "bytes_per_state": BYTES_PER_STATE, "kernel_ms": kms, "traffic": None},
+            "full_plan_ms_per_track": plan["ms_per_track"] if plan else None,
+            "full_plan": plan,
             "cpu_baseline": cpu,
             "side": side,
         }
         print(json.dumps(out))
     capi.check(L.epp_stream_destroy(stream))
     dist.close()
+
+
+PLAN_SAMPLES = 65536
+
+
+def full_plan(dist, rank, reps):
+    """C4: plan this rank's track end to end (OnlineTrajGenerator.preComputeTraj), time it,
+    all-gather the waypoint sets.  Returns the slowest rank's mean ms per track."""
+    import tempfile
+
+    import online_traj_planner as otp
+    from eppamd import config, synth
+
+    cfg = config.load(os.path.join(ROOT, "configs", "config.json"))
+    cfg["world_properties"]["lower_bound"] = [-6, -6, 0]
+    cfg["world_properties"]["upper_bound"] = [6, 6, 2]
+    cfg["path_planner_properties"]["samples_fmt"] = PLAN_SAMPLES
+    geom = config.geometry(cfg)
+    fd, path = tempfile.mkstemp(suffix=".json")
+    with os.fdopen(fd, "w") as f:
+        json.dump(cfg, f)
+    gates, obstacles = synth.track_world(100 + rank)
+    cps = synth.gate_checkpoints(gates, geom.gate_height, 0.55)
+    start, goal = cps[0], cps[-1]
+    otg = otp.OnlineTrajGenerator(start, goal, gates, obstacles, path)
+    otg.pre_compute_traj(0.0)  # warm-up: allocations, first launches
+    dist.barrier()
+    t = time.perf_counter()
+    for _ in range(reps):
+        otg.pre_compute_traj(0.0)
+    ms = (time.perf_counter() - t) / reps * 1e3
+    os.unlink(path)
+    ms_max = dist.max(ms)
+    wp = np.ascontiguousarray(otg.get_waypoints())
+    traj = otg.get_planned_traj()
+    t = time.perf_counter()
+    sets = dist.all_gather_waypoints(wp)
+    gather_ms = dist.max((time.perf_counter() - t) * 1e3)
+    return {"ms_per_track": ms_max, "tracks": dist.ws, "samples_per_segment": PLAN_SAMPLES, "k": 16,
+            "segments_per_track": 9, "reps": reps, "waypoints_per_track": [len(x) for x in sets],
+            "traj_rows": int(len(traj)), "traj_duration_s": float(traj[-1, 9] - traj[0, 9]),
+            "all_gather_ms": gather_ms,
+            "reference_configured_budget_ms": 9 * 2000.0,  # RRT* solve(time_limit_offline=2 s) x 9 segments
+            "workload": "C4: per rank one track (seed 100+rank), 8 gates + 24 obstacles, 9 gate-to-gate "
+                        "batch plans (65,536 samples, k=16) + includeGates2 + min-snap + sampling"}
 
 
 def side_measurements(capi, L, stream, geom, cfg, rg, ro):

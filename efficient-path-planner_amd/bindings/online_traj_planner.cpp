@@ -192,6 +192,13 @@ PYBIND11_MODULE(online_traj_planner, m) {
         .def(
             "planner", [](epp::OnlineTrajGenerator& self) -> epp::PathPlanner& { return self.planner(); },
             py::return_value_policy::reference_internal)
+        .def("get_waypoints", [](const epp::OnlineTrajGenerator& self) {
+            const auto c = self.getWaypoints();
+            py::array_t<double> out({(py::ssize_t)c.size(), (py::ssize_t)3});
+            for (size_t i = 0; i < c.size(); ++i)
+                for (int k = 0; k < 3; ++k) out.mutable_data()[i * 3 + k] = c[i][k];
+            return out;
+        })
         .def("get_checkpoints", [](const epp::OnlineTrajGenerator& self) {
             const auto& c = self.getCheckpoints();
             py::array_t<double> out({(py::ssize_t)c.size(), (py::ssize_t)3});

@@ -100,6 +100,7 @@ void OnlineTrajGenerator::preComputeTraj(double takeoffTime) {
     Matrix traj = generate(pruned, takeoffTime, Vec3(0, 0, 0), Vec3(0, 0, 0));
     std::lock_guard<std::mutex> lk(trajMu);
     plannedTraj = std::move(traj);
+    waypoints = pruned;
 }
 
 // OnlineTrajGenerator::checkGatePassed — src/OnlineTrajGenerator.cpp:228-256
@@ -246,6 +247,7 @@ void OnlineTrajGenerator::recomputeTraj(int gateId, const Vec3& /*dronePos*/, do
         for (size_t c = 0; c < traj.cols; ++c) merged(startAdv + i, c) = postTraj(i, c);
     std::lock_guard<std::mutex> lk(trajMu);
     plannedTraj = std::move(merged);
+    waypoints = filled;
 }
 
 // src/OnlineTrajGenerator.cpp:423-439
@@ -263,6 +265,11 @@ std::vector<double> OnlineTrajGenerator::sampleTraj(double currentTime) const {
         }
     }
     return std::vector<double>(plannedTraj.row(best_i), plannedTraj.row(best_i) + plannedTraj.cols);
+}
+
+std::vector<Vec3> OnlineTrajGenerator::getWaypoints() const {
+    std::lock_guard<std::mutex> lk(trajMu);
+    return waypoints;
 }
 
 double OnlineTrajGenerator::getTrajEndTime() const {

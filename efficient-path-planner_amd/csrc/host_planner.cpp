@@ -196,6 +196,10 @@ bool PathPlanner::planPath(const Vec3& start, const Vec3& goal, double timeLimit
         throw std::runtime_error("Unknown planner");  // :121-123
     }
     const auto t0 = std::chrono::steady_clock::now();
+    {
+        std::lock_guard<std::mutex> lk(g_stats_mu);
+        stats_ = PlannerStats();
+    }
     int64_t samples = pp.samplesFMT > 0 ? pp.samplesFMT : 4096;
     const uint64_t call = __atomic_fetch_add(&calls_, 1, __ATOMIC_RELAXED);
     uint64_t seed = mix(seed_, call);

@@ -1,0 +1,73 @@
+"""Multi-GPU plumbing of the hot path: one process per GPU, independent
+tracks per rank, and one exchange step — the all-gather of the final waypoint sets.
+
+Backend "nccl" is RCCL on ROCm (xGMI between the GPUs of a node); "gloo" runs the same
+code on CPU tensors (used by the world_size-2 tests in this container).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+
+def env():
+    """(world_size, rank, local_rank) from the torchrun environment."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+class Dist:
+    def __init__(self, ws: int, rank: int, local: int, backend: str = "nccl"):
+        self.ws, self.rank, self.local, self.backend = ws, rank, local, backend
+        self.device = "cpu"
+        if ws > 1:
+            import torch
+            import torch.distributed as dist
+            self.torch, self.dist = torch, dist
+            if backend == "nccl":
+                torch.cuda.set_device(local)
+                self.device = f"cuda:{local}"
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group(backend)
+
+    def barrier(self):
+        if self.ws > 1:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if self.ws == 1:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x: float) -> float:
+        if self.ws == 1:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def all_gather_waypoints(self, wp: np.ndarray) -> list[np.ndarray]:
+        """All-gather of every rank's (W_r, 3) float64 waypoint set: the counts first, then
+        the sets padded to max W (two collectives, a few KB each)."""
+        wp = np.ascontiguousarray(np.asarray(wp, np.float64).reshape(-1, 3))
+        if self.ws == 1:
+            return [wp]
+        torch, dist = self.torch, self.dist
+        n = torch.tensor([len(wp)], dtype=torch.int64, device=self.device)
+        ns = [torch.zeros_like(n) for _ in range(self.ws)]
+        dist.all_gather(ns, n)
+        counts = [int(x.item()) for x in ns]
+        buf = torch.zeros((max(counts), 3), dtype=torch.float64, device=self.device)
+        if len(wp):
+            buf[:len(wp)] = torch.from_numpy(wp).to(self.device)
+        outs = [torch.zeros_like(buf) for _ in range(self.ws)]
+        dist.all_gather(outs, buf)
+        return [o[:c].cpu().numpy() for o, c in zip(outs, counts)]
+
+    def close(self):
+        if self.ws > 1:
+            self.dist.destroy_process_group()

@@ -35,6 +35,8 @@ public:
     Matrix getPlannedTraj() const;
 
     const std::vector<Vec3>& getCheckpoints() const { return checkpoints; }
+    // waypoints of the last (re)planned trajectory, after includeGates2
+    std::vector<Vec3> getWaypoints() const;
     PathPlanner& planner() { return pathPlanner; }
     // waits for an in-flight online recomputation (recalculate_online)
     void waitForUpdate();
@@ -55,6 +57,7 @@ private:
     std::set<int> gatesObservedWithinRange;
     std::vector<std::vector<Vec3>> pathSegments;
     Matrix plannedTraj;
+    std::vector<Vec3> waypoints;  // guarded by trajMu
     mutable std::mutex trajMu;
     bool trajectoryCurrentlyUpdating = false;
     std::future<void> pending;
