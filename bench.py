@@ -43,23 +43,23 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
 def timed_kernel_ms(capi, stream, fn, reps):
-    """Average device time of `fn` over `reps` launches, HIP events on `stream`."""
+    """Average device time per launch of `fn`: HIP events on `stream` around `reps`
+    back-to-back launches (the steady state the timed region runs in; per-launch event
+    pairs would add the host launch latency to every launch)."""
     import ctypes as C
     L = capi.lib()
     e0, e1 = C.c_void_p(), C.c_void_p()
     capi.check(L.epp_event_create(C.byref(e0)))
     capi.check(L.epp_event_create(C.byref(e1)))
-    tot = 0.0
+    capi.check(L.epp_event_record(e0, stream))
     for r in range(reps):
-        capi.check(L.epp_event_record(e0, stream))
         fn(r)
-        capi.check(L.epp_event_record(e1, stream))
-        ms = C.c_float()
-        capi.check(L.epp_event_elapsed_ms(e0, e1, C.byref(ms)))
-        tot += ms.value
+    capi.check(L.epp_event_record(e1, stream))
+    ms = C.c_float()
+    capi.check(L.epp_event_elapsed_ms(e0, e1, C.byref(ms)))
     L.epp_event_destroy(e0)
     L.epp_event_destroy(e1)
-    return tot / reps
+    return ms.value / reps
 
 
 def main():
@@ -128,6 +128,8 @@ def main():
     if not args.no_plan:
         plan = full_plan(dist, rank, args.plan_reps)
 
+    traffic, traffic_src = committed_traffic()
+
     side = {}
     if not args.no_side and rank == 0:
         side = side_measurements(capi, L, stream, geom, cfg, rg, ro)
@@ -154,9 +156,12 @@ def main():
                        "states_per_step_per_gpu": N_STATES, "obbs": int(len(obbs)),
                        "can_pass_gate": False, "valid_fraction": n_valid / N_STATES,
                        "parallelism": f"replicas x{ws} (independent samplers)"},
-            "roofline": {"bound": "hbm", "kernel": "k_states<true,false>", "achieved": achieved,
+            "roofline": {"bound": "hbm", "kernel": "k_states", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "bytes_per_state": BYTES_PER_STATE, "kernel_ms": kms, "traffic": None},
+                         "traffic": traffic, "traffic_unit": "bytes per launch",
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": BYTES_PER_STATE * N_STATES,
+                         "bytes_per_state": BYTES_PER_STATE, "kernel_ms": kms},
             "full_plan_ms_per_track": plan["ms_per_track"] if plan else None,
             "full_plan": plan,
             "cpu_baseline": cpu,
@@ -168,6 +173,24 @@ def main():
 
 
 PLAN_SAMPLES = 65536
+
+
+def committed_traffic():
+    """HBM bytes per k_states launch from the newest committed PMC summary
+    (profiles/rNN_traffic.json, written by scripts/profile_summary.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this bench)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
+    if not files:
+        return None, None
+    try:
+        d = json.load(open(files[-1]))
+    except (OSError, ValueError):
+        return None, None
+    for name, v in d.items():
+        if "k_states<" in name and ", false," in name:
+            return v["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+    return None, None
 
 
 def full_plan(dist, rank, reps):

@@ -74,9 +74,11 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn(const double* __restrict__ no
             if (d < bd[K - 1] && t0 + c != i) {  // strict: earlier index wins ties
                 double vd = d;
                 int vi = t0 + c;
+                bool shift = false;  // once placed, the tail shifts down by one (keeps tie order)
 #pragma unroll
-                for (int k = 0; k < K; ++k) {  // insertion into the sorted list
-                    if (vd < bd[k]) {
+                for (int k = 0; k < K; ++k) {  // insertion after any equal distances
+                    shift = shift || vd < bd[k];
+                    if (shift) {
                         const double td = bd[k];
                         const int ti = bi[k];
                         bd[k] = vd;

@@ -1,5 +1,6 @@
 #!/bin/bash
-# One GPU session: parity tests, smoke, a short bench, a rocprofv3 kernel-trace summary.
+# One GPU session: parity tests, smoke, the bench, a rocprofv3 kernel-trace summary of the
+# bench, and the two PMC passes (FETCH_SIZE, WRITE_SIZE) for the roofline traffic figure.
 # Every GPU step has its own time limit; a fault/abort/timeout stops the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -12,17 +13,23 @@ stop_on_fault() {  # $1 = exit code, $2 = step name
   esac
 }
 echo "== pytest -m gpu"
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+timeout -k 10 900 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 tail -5 gpurun_out/pytest_gpu.log; stop_on_fault $rc pytest
 echo "== smoke"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
 tail -3 gpurun_out/smoke.log; stop_on_fault $rc smoke
 echo "== bench"
 timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?
-tail -c 3000 gpurun_out/bench.json; tail -3 gpurun_out/bench.err; stop_on_fault $rc bench
-echo "== rocprofv3 kernel trace"
+tail -c 1500 gpurun_out/bench.json; tail -3 gpurun_out/bench.err; stop_on_fault $rc bench
+echo "== rocprofv3 kernel trace of the bench"
 rm -rf gpurun_out/prof
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 50 --no-cpu > gpurun_out/prof_bench.json 2> gpurun_out/prof.err; rc=$?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu > gpurun_out/prof_bench.json 2> gpurun_out/prof.err; rc=$?
 tail -3 gpurun_out/prof.err; stop_on_fault $rc rocprof
-find gpurun_out/prof -name "*stats*" | head
+for c in FETCH_SIZE WRITE_SIZE; do
+  echo "== rocprofv3 --pmc $c"
+  rm -rf gpurun_out/pmc_$c
+  timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_$c -o run -- python3 bench.py --no-cpu --no-side --no-plan > gpurun_out/pmc_$c.json 2> gpurun_out/pmc_$c.err; rc=$?
+  tail -2 gpurun_out/pmc_$c.err; stop_on_fault $rc pmc_$c
+done
+python3 scripts/profile_summary.py gpurun_out r01 > gpurun_out/profile_summary.log 2>&1; cat gpurun_out/profile_summary.log
 echo done
