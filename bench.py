@@ -219,6 +219,11 @@ def full_plan(dist, rank, reps):
     for _ in range(reps):
         otg.pre_compute_traj(0.0)
     ms = (time.perf_counter() - t) / reps * 1e3
+    # one gate-to-gate segment alone, with the planner's device / host split
+    pp = otp.PathPlanner(gates, obstacles, path)
+    all_cps = otg.get_checkpoints()
+    pp.plan_path(all_cps[2], all_cps[3], 2.0)
+    seg = pp.last_stats()
     os.unlink(path)
     ms_max = dist.max(ms)
     wp = np.ascontiguousarray(otg.get_waypoints())
@@ -229,7 +234,7 @@ def full_plan(dist, rank, reps):
     return {"ms_per_track": ms_max, "tracks": dist.ws, "samples_per_segment": PLAN_SAMPLES, "k": 16,
             "segments_per_track": 9, "reps": reps, "waypoints_per_track": [len(x) for x in sets],
             "traj_rows": int(len(traj)), "traj_duration_s": float(traj[-1, 9] - traj[0, 9]),
-            "all_gather_ms": gather_ms,
+            "all_gather_ms": gather_ms, "one_segment": seg,
             "reference_configured_budget_ms": 9 * 2000.0,  # RRT* solve(time_limit_offline=2 s) x 9 segments
             "workload": "C4: per rank one track (seed 100+rank), 8 gates + 24 obstacles, 9 gate-to-gate "
                         "batch plans (65,536 samples, k=16) + includeGates2 + min-snap + sampling"}

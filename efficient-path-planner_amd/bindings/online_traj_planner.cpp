@@ -148,6 +148,8 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["edges_valid"] = s.edges_valid;
             d["attempts"] = s.attempts;
             d["ms"] = s.ms;
+            d["ms_device"] = s.ms_device;
+            d["ms_search"] = s.ms_search;
             return d;
         });
 
@@ -198,6 +200,16 @@ PYBIND11_MODULE(online_traj_planner, m) {
             for (size_t i = 0; i < c.size(); ++i)
                 for (int k = 0; k < 3; ++k) out.mutable_data()[i * 3 + k] = c[i][k];
             return out;
+        })
+        .def("planner_stats", [](epp::OnlineTrajGenerator& self) {
+            const auto& s = self.planner().lastStats();
+            py::dict d;
+            d["states_sampled"] = s.states_sampled;
+            d["edges_checked"] = s.edges_checked;
+            d["ms"] = s.ms;
+            d["ms_device"] = s.ms_device;
+            d["ms_search"] = s.ms_search;
+            return d;
         })
         .def("get_checkpoints", [](const epp::OnlineTrajGenerator& self) {
             const auto& c = self.getCheckpoints();

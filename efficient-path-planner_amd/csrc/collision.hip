@@ -22,6 +22,7 @@
 
 namespace epp {
 const WorldView& world_view(const epp_world* w);
+const WorldView* world_dview(const epp_world* w);
 
 namespace {
 
@@ -341,9 +342,19 @@ __global__ __launch_bounds__(kBlock) void k_states(WorldView w, const double* __
                                                    uint8_t* __restrict__ valid,
                                                    int32_t* __restrict__ compact_idx,
                                                    unsigned long long* __restrict__ n_valid,
-                                                   uint32_t stage_bytes) {
+                                                   uint32_t stage_bytes, unsigned long long* __restrict__ tl) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int lane = threadIdx.x & 63;
+    // optional per-wave timeline (debug entry epp_dbg_states_timeline): s_memrealtime
+    // (100 MHz, chip-wide) at entry, data arrival, after staging, after the groups
+    const int gwave = (int)((blockIdx.x * kBlock + threadIdx.x) >> 6);
+    auto mark = [&](int k) {
+        if (tl) {
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            if (lane == 0) tl[gwave * 8 + k] = t;
+        }
+    };
+    mark(0);
     // full groups of 4 states; the (< 4) tail states are handled after the main loop
     const int64_t groups = n / 4;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
@@ -367,9 +378,14 @@ __global__ __launch_bounds__(kBlock) void k_states(WorldView w, const double* __
     int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     double va[12], vb[12];
     if (groups > 0) load(g, va);  // first loads before the world staging
+    if (tl) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        mark(1);
+    }
     WaveScratch* ws = reinterpret_cast<WaveScratch*>(lds + (threadIdx.x >> 6) * ((sizeof(WaveScratch) + 15) & ~15u));
     const unsigned char* staged = STAGE ? stage_world(w, lds + kScratchBytes, stage_bytes) : w.blob;
     const Acc a = make_acc(staged, STAGE == 2 ? staged : w.blob, w);
+    mark(2);
 
     auto process = [&](int64_t gg, const double (&v)[12]) {
         const bool live = gg < groups;
@@ -467,11 +483,241 @@ __global__ __launch_bounds__(kBlock) void k_states(WorldView w, const double* __
         load(g + 2 * stride, va);
         process(g + stride, vb);
     }
+    mark(3);
+    if (tl && lane == 0) {
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        tl[gwave * 8 + 4] = hw;
+        tl[gwave * 8 + 5] = xcc;
+        tl[gwave * 8 + 6] = __builtin_amdgcn_s_memtime();
+    }
     // tail: the last n % 4 states, one lane each
     if (blockIdx.x == 0 && threadIdx.x < (int)(n - 4 * groups)) {
         const int64_t i = 4 * groups + threadIdx.x;
         const bool ok = state_valid_scalar<MINDIST>(a, w, xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2],
                                                     can_pass != 0, md);
+        valid[i] = ok ? 1 : 0;
+        if (compact_idx && ok) compact_idx[atomicAdd(n_valid, 1ull)] = (int32_t)i;
+    }
+}
+
+// ---- k_states_bm: flat-bitmap fast path ----------------------------------------------
+// Per state: three float cell coordinates and ONE bitmap word (global, L1/L2 resident);
+// a clear bit proves the state lies outside every inflated AABB (valid, no OBB test).
+// The few states on set bits are compacted per wave (ballots) into an LDS queue; one
+// lane per queued state walks its coarse-cell candidate list with the exact fp64
+// rtree-prefilter + OBB tests, and the hit flags are read back from LDS.
+constexpr int kQueueCap = 256;  // a wave's whole group (64 lanes x 4 states)
+struct StateQueue {
+    double xyz[kQueueCap][3];
+    uint8_t hit[kQueueCap];
+};
+
+// Fast-path parameters of the bitmap (kept in SGPRs; the rest of the WorldView is read
+// through the scalar cache only on the rare exact path).
+typedef const __attribute__((address_space(1))) uint32_t* gptr_u32;  // global, not flat
+
+struct BmParams {
+    gptr_u32 bm;
+    float ox, oy, oz, ix, iy, iz;
+    uint32_t nx, ny, nz, sentinel;
+};
+
+__device__ __forceinline__ uint32_t bm_word_index(const BmParams& p, double px, double py, double pz,
+                                                  uint32_t& bit) {
+    const int ix = bm_axis(px, p.ox, p.ix), iy = bm_axis(py, p.oy, p.iy), iz = bm_axis(pz, p.oz, p.iz);
+    const bool in = (unsigned)ix < p.nx && (unsigned)iy < p.ny && (unsigned)iz < p.nz;
+    // dims <= 4096 per axis, so the products fit 24-bit multiplies
+    const uint32_t c = __umul24(__umul24((uint32_t)iz, p.ny) + (uint32_t)iy, p.nx) + (uint32_t)ix;
+    bit = c & 31u;
+    return in ? (c >> 5) : p.sentinel;  // the sentinel word is 0
+}
+
+// Exact test of one queued state: rtree prefilter + OBB tests on its coarse-cell list.
+// The WorldView pointer is laundered through an empty asm so the compiler cannot hoist
+// the field loads into the streaming loop: the rare path reads them through the scalar
+// cache instead of pinning ~50 SGPRs for the whole kernel.
+// `base` is the blob: its LDS copy (STAGE) or the HBM original.
+template <bool MINDIST>
+__device__ __forceinline__ bool states_exact_hit(const WorldView* wvp, const unsigned char* base, double px,
+                                                 double py, double pz, int can_pass, double md) {
+    // constant address space: the fields come in by scalar loads (lgkmcnt), not flat
+    // loads that would also wait for the in-flight prefetch
+#if defined(__HIP_DEVICE_COMPILE__)  // (the host pass only parses device bodies)
+    typedef const __attribute__((address_space(4))) WorldView* cwv_ptr;
+    cwv_ptr p = (cwv_ptr)wvp;
+    asm volatile("" : "+s"(p));
+    const WorldView w = *p;
+#else
+    const WorldView& w = *wvp;
+#endif
+    const Acc a = make_acc(base, base, w);
+    uint32_t st = 0;
+    const uint32_t c = classify(a, w, px, py, pz, st);
+    for (uint32_t j = 0; j < c; ++j)
+        if (pair_hit<MINDIST>(a, w, a.co[st + j], px, py, pz, can_pass != 0, md)) return true;
+    return false;
+}
+
+// STAGE: the blob up to the bitmap (cull grid, lists, OBB table) is copied into LDS once
+// per workgroup, so the exact path runs on LDS reads (lgkmcnt) and never waits behind
+// the in-flight prefetch of the next group (vmcnt counts in order).
+template <bool MINDIST, bool ALIGNED, bool STAGE>
+__global__ __launch_bounds__(kBlock) void k_states_bm(const WorldView* __restrict__ wv, const double* __restrict__ xyz,
+                                                      int64_t n, int can_pass, double md,
+                                                      uint8_t* __restrict__ valid,
+                                                      int32_t* __restrict__ compact_idx,
+                                                      unsigned long long* __restrict__ n_valid,
+                                                      unsigned long long* __restrict__ tl, uint32_t stage_bytes) {
+    __shared__ StateQueue queues[kBlock / 64];
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_blob[];
+    const int lane = threadIdx.x & 63;
+    StateQueue* qu = &queues[threadIdx.x >> 6];
+    const int gwave = (int)((blockIdx.x * kBlock + threadIdx.x) >> 6);
+    auto mark = [&](int k) {
+        if (tl) {
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            if (lane == 0) tl[gwave * 8 + k] = t;
+        }
+    };
+    mark(0);
+    BmParams bp;
+    bp.bm = (gptr_u32)(wv->blob + wv->off_bitmap);
+    bp.ox = wv->bofx; bp.oy = wv->bofy; bp.oz = wv->bofz;
+    bp.ix = wv->bix; bp.iy = wv->biy; bp.iz = wv->biz;
+    bp.nx = (uint32_t)wv->bnx; bp.ny = (uint32_t)wv->bny; bp.nz = (uint32_t)wv->bnz;
+    bp.sentinel = wv->bm_words;
+    const unsigned char* xbase = nullptr;  // blob for the exact path: LDS copy or HBM (set below)
+    const int64_t groups = n / 4;  // full groups of 4; the n % 4 tail states come last
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    auto load = [&](int64_t grp, double (&dst)[12]) {
+        grp = grp < groups ? grp : groups - 1;  // unconditional (clamped): no branch, counted vmcnt
+        if (ALIGNED) {
+            const double2* q = reinterpret_cast<const double2*>(xyz + 12 * grp);
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                const double2 t = q[k];
+                dst[2 * k] = t.x;
+                dst[2 * k + 1] = t.y;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 12; ++k) dst[k] = xyz[12 * grp + k];
+        }
+    };
+    // the current group's four bitmap words are requested BEFORE the next group's
+    // prefetch, so waiting for them (vmcnt counts in order) leaves the prefetch in flight
+    auto words = [&](const double (&v)[12], uint32_t (&wd)[4], uint32_t (&bit)[4]) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) wd[k] = bp.bm[bm_word_index(bp, v[3 * k], v[3 * k + 1], v[3 * k + 2], bit[k])];
+    };
+    auto finish = [&](int64_t gg, const double (&v)[12], const uint32_t (&wd)[4], const uint32_t (&bit)[4]) {
+        const int64_t first = 4 * gg;
+        const bool live = gg < groups;
+        bool needy[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) needy[k] = live & (((wd[k] >> bit[k]) & 1u) != 0u);
+        unsigned long long bal[4];
+        uint32_t total = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            bal[k] = __ballot(needy[k]);
+            total += (uint32_t)__popcll(bal[k]);
+        }
+        uint32_t hits = 0;
+        if (total > 0) {  // wave-uniform: queue the needy states, one lane per state
+            uint32_t pos[4];
+            uint32_t base = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                pos[k] = base + lanes_below(bal[k]);
+                base += (uint32_t)__popcll(bal[k]);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (needy[k]) {
+                    qu->xyz[pos[k]][0] = v[3 * k];
+                    qu->xyz[pos[k]][1] = v[3 * k + 1];
+                    qu->xyz[pos[k]][2] = v[3 * k + 2];
+                }
+            wave_lds_sync();
+            for (uint32_t e = lane; e < total; e += 64)  // rounds of 64 (almost always one)
+                qu->hit[e] = states_exact_hit<MINDIST>(wv, xbase, qu->xyz[e][0], qu->xyz[e][1], qu->xyz[e][2],
+                                                       can_pass, md)
+                                 ? 1
+                                 : 0;
+            wave_lds_sync();
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (needy[k] && qu->hit[pos[k]]) hits |= 1u << k;
+            wave_lds_sync();  // the queue is rewritten by the next group
+        }
+        const uint32_t fl = live ? (~hits & 15u) : 0u;  // bit k: state first+k valid
+        if (live) {
+            if (ALIGNED)
+                *reinterpret_cast<uint32_t*>(valid + first) =
+                    (fl & 1u) | ((fl & 2u) << 7) | ((fl & 4u) << 14) | ((fl & 8u) << 21);
+            else
+                for (int k = 0; k < 4; ++k) valid[first + k] = (uint8_t)((fl >> k) & 1u);
+        }
+        if (compact_idx) {  // wave-ballot compaction (uniform branch)
+            const uint32_t c = (uint32_t)__popc(fl);
+            uint32_t ctot;
+            const uint32_t cex = wave_excl_scan(c, lane, ctot);
+            unsigned long long wbase = 0;
+            if (lane == 0 && ctot) wbase = atomicAdd(n_valid, (unsigned long long)ctot);
+            wbase = __shfl(wbase, 0, 64);
+            uint64_t p = wbase + cex;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if ((fl >> k) & 1u) compact_idx[p++] = (int32_t)(first + k);
+        }
+    };
+    int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    double va[12], vb[12];
+    uint32_t wd[4], bit[4];
+    if (groups > 0) load(g, va);
+    if (tl) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        mark(1);
+    }
+    if (STAGE) {
+        const uint4* src = reinterpret_cast<const uint4*>(wv->blob);
+        uint4* dst = reinterpret_cast<uint4*>(lds_blob);
+        for (uint32_t o = threadIdx.x; o < stage_bytes / 16; o += kBlock) dst[o] = src[o];
+        __syncthreads();
+        xbase = lds_blob;
+    } else {
+        xbase = wv->blob;
+    }
+    mark(2);
+    // block-uniform trip count: every lane runs every iteration (ballots, wave queue)
+    for (int64_t g0 = (int64_t)blockIdx.x * kBlock; g0 < groups; g0 += 2 * stride, g += 2 * stride) {
+        words(va, wd, bit);
+        load(g + stride, vb);
+        finish(g, va, wd, bit);
+        if (g0 + stride >= groups) break;
+        words(vb, wd, bit);
+        load(g + 2 * stride, va);
+        finish(g + stride, vb, wd, bit);
+    }
+    mark(3);
+    if (tl && lane == 0) {
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        tl[gwave * 8 + 4] = hw;
+        tl[gwave * 8 + 5] = xcc;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (int)(n - 4 * groups)) {  // tail: the last n % 4 states
+        const int64_t i = 4 * groups + threadIdx.x;
+        const double px = xyz[3 * i], py = xyz[3 * i + 1], pz = xyz[3 * i + 2];
+        uint32_t b;
+        const uint32_t word = bp.bm[bm_word_index(bp, px, py, pz, b)];
+        const bool ok = !(((word >> b) & 1u) && states_exact_hit<MINDIST>(wv, xbase, px, py, pz, can_pass, md));
         valid[i] = ok ? 1 : 0;
         if (compact_idx && ok) compact_idx[atomicAdd(n_valid, 1ull)] = (int32_t)i;
     }
@@ -572,9 +818,18 @@ epp_status launch_error(const char* what) {
 using namespace epp;
 
 namespace {
+bool bm_stage(const WorldView& w) {
+    return w.off_bitmap + (kBlock / 64) * sizeof(StateQueue) <= kLdsBudget && !env_int("EPP_NO_LDS", 0);
+}
+int bm_grid(const WorldView& w, int64_t groups) {
+    const uint32_t queue_bytes = (kBlock / 64) * sizeof(StateQueue);
+    return grid_for(groups, bm_stage(w) ? w.off_bitmap + queue_bytes : queue_bytes);
+}
+
 template <bool MINDIST>
-epp_status launch_states(const WorldView& w, const double* xyz, int64_t n, int32_t can_pass, double md,
-                         uint8_t* valid, int32_t* compact_idx, int64_t* n_valid, void* stream) {
+epp_status launch_states(const WorldView& w, const WorldView* dw, const double* xyz, int64_t n, int32_t can_pass, double md,
+                         uint8_t* valid, int32_t* compact_idx, int64_t* n_valid, void* stream,
+                         unsigned long long* tl = nullptr) {
     // 16-byte loads and 4-byte flag stores need aligned buffers (hipMalloc gives 256 B)
     const bool aligned = ((reinterpret_cast<uintptr_t>(xyz) & 15) | (reinterpret_cast<uintptr_t>(valid) & 3)) == 0;
     const int64_t groups = std::max<int64_t>(1, n / 4);
@@ -591,8 +846,25 @@ epp_status launch_states(const WorldView& w, const double* xyz, int64_t n, int32
     do {                                                                                              \
         allow_lds(k_states<L, MINDIST, A>);                                                           \
         hipLaunchKernelGGL((k_states<L, MINDIST, A>), dim3(grid), dim3(kBlock), shm, st, w, xyz, n,   \
-                           can_pass, md, valid, compact_idx, nv, stage);                              \
+                           can_pass, md, valid, compact_idx, nv, stage, tl);                          \
     } while (0)
+    if (env_int("EPP_STATES_IMPL", 1) == 1) {  // flat-bitmap kernel (default)
+        const uint32_t sb = w.off_bitmap;  // everything the exact path reads
+        const bool stg = bm_stage(w);
+        const int g2 = bm_grid(w, groups);
+#define EPP_LAUNCH_BM(A, S)                                                                            \
+    do {                                                                                               \
+        allow_lds(k_states_bm<MINDIST, A, S>);                                                         \
+        hipLaunchKernelGGL((k_states_bm<MINDIST, A, S>), dim3(g2), dim3(kBlock), S ? sb : 0, st, dw, xyz, n, \
+                           can_pass, md, valid, compact_idx, nv, tl, sb);                              \
+    } while (0)
+        if (aligned && stg) EPP_LAUNCH_BM(true, true);
+        else if (aligned) EPP_LAUNCH_BM(true, false);
+        else if (stg) EPP_LAUNCH_BM(false, true);
+        else EPP_LAUNCH_BM(false, false);
+#undef EPP_LAUNCH_BM
+        return launch_error(MINDIST ? "epp_check_states_mindist" : "epp_check_states");
+    }
     const int mode = stage == 0 ? 0 : (stage == w.blob_bytes ? 2 : 1);
     if (mode == 2 && aligned) EPP_LAUNCH_STATES(2, true);
     else if (mode == 2) EPP_LAUNCH_STATES(2, false);
@@ -615,8 +887,8 @@ epp_status epp_check_states(const epp_world* world, const double* xyz, int64_t n
         return EPP_ERR_INVALID_ARGUMENT;
     }
     if (n == 0) return EPP_OK;
-    return launch_states<false>(world_view(world), xyz, n, can_pass_gate, 0.0, valid, compact_idx, n_valid,
-                                stream);
+    return launch_states<false>(world_view(world), world_dview(world), xyz, n, can_pass_gate, 0.0, valid,
+                                compact_idx, n_valid, stream);
 }
 
 epp_status epp_check_states_mindist(const epp_world* world, const double* xyz, int64_t n,
@@ -626,7 +898,23 @@ epp_status epp_check_states_mindist(const epp_world* world, const double* xyz, i
         return EPP_ERR_INVALID_ARGUMENT;
     }
     if (n == 0) return EPP_OK;
-    return launch_states<true>(world_view(world), xyz, n, 0, min_distance, valid, nullptr, nullptr, stream);
+    return launch_states<true>(world_view(world), world_dview(world), xyz, n, 0, min_distance, valid, nullptr,
+                               nullptr, stream);
+}
+
+// Debug entry (not part of include/epp.h): k_states on C ABI arguments plus an 8-word
+// per-wave timeline buffer (grid waves x 8 u64; see k_states).  Returns the grid size.
+epp_status epp_dbg_states_timeline(const epp_world* world, const double* xyz, int64_t n, uint8_t* valid,
+                                   unsigned long long* tl, int32_t* grid_waves, void* stream) {
+    if (!world || n <= 0 || !xyz || !valid || !tl || !grid_waves) return EPP_ERR_INVALID_ARGUMENT;
+    const WorldView& w = world_view(world);
+    const bool lds = w.front_bytes + kScratchBytes <= kLdsBudget && !env_int("EPP_NO_LDS", 0);
+    const uint32_t full_cap = (uint32_t)env_int("EPP_STAGE_FULL_MAX", 40 * 1024);
+    const uint32_t stage = !lds ? 0u : (w.blob_bytes <= full_cap ? w.blob_bytes : w.front_bytes);
+    *grid_waves = (env_int("EPP_STATES_IMPL", 1) == 1 ? bm_grid(w, std::max<int64_t>(1, n / 4))
+                                                      : grid_for(std::max<int64_t>(1, n / 4), kScratchBytes + stage)) *
+                  (kBlock / 64);
+    return launch_states<false>(w, world_dview(world), xyz, n, 0, 0.0, valid, nullptr, nullptr, stream, tl);
 }
 
 epp_status epp_check_motions(const epp_world* world, const double* s1, const double* s2, int64_t n,

@@ -10,9 +10,13 @@
 //   uint32  meta[n_pad]          bit0 filling, bit1 gate, bits 8-15/16-23/24-31 = first
 //                                coarse cell (x, y, z) the OBB's AABB touches
 //   double  soa[EPP_NF][n_pad]   field-major OBB table (see enum below)
+//   uint32  bitmap[bm_words+1]   flat occupancy bitmap over the padded union box (one
+//                                bit per cell: some inflated AABB may contain a point of
+//                                it); the extra last word is 0 (out-of-range lookups)
 //
 // n_pad rounds n_obbs up to a multiple of 4; every array starts 16-byte aligned.
 #pragma once
+#include <math.h>
 #include <stdint.h>
 
 #include <string>
@@ -56,7 +60,25 @@ struct WorldView {
     float limx, limy, limz;   // ~4n: fine coordinates beyond are outside every AABB
     float fmaxx, fmaxy, fmaxz; // 4 * n - 1: largest fine index
     double r_gate, r_obst;    // inflate radii (src/World.cpp:89-90)
+    // flat occupancy bitmap (k_states fast path)
+    uint32_t off_bitmap;
+    uint32_t bm_words;        // index of the zero sentinel word
+    int32_t bnx, bny, bnz;    // cells per axis
+    float bofx, bofy, bofz;   // origin (float)
+    float bix, biy, biz;      // 1 / cell size (float)
 };
+
+// Bitmap cell index along one axis: the same float operations on host and device, so
+// the host marks exactly the cells the kernels look up; monotone in p.  Values
+// outside [0, n) mean "outside every AABB".
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline int bm_axis(double p, float o, float inv) {
+    float f = ((float)p - o) * inv;
+    f = fminf(fmaxf(f, -1.0f), 16777216.0f);  // NaN -> -1 (outside); keeps (int) defined
+    return (int)f;                             // truncation toward zero
+}
 
 // Host-side world: the upload plus host copies (for AABB introspection and rebuilds).
 struct HostWorld {
@@ -64,6 +86,7 @@ struct HostWorld {
     double r_gate = 0, r_obst = 0;
     int device = 0;
     void* d_blob = nullptr;
+    const WorldView* d_view = nullptr;  // device copy of `view` (after the blob)
     size_t d_capacity = 0;
     std::string blob;            // host image of the device blob
     std::vector<double> aabbs;   // n x 6

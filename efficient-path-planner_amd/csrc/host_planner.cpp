@@ -67,6 +67,7 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     const int k = k_;
     ThreadScratch& ts = ThreadScratch::get();
     void* st = ts.stream();
+    const auto t_dev0 = std::chrono::steady_clock::now();
     // ---- 1. sample + validate states (StateValidator::isValid) --------------------------
     const size_t n_s = (size_t)samples;
     ts.reset(ThreadScratch::rounded(n_s * 24) + ThreadScratch::rounded(n_s));
@@ -102,20 +103,30 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     std::vector<uint8_t> ev(m);
     check(epp_memcpy_d2h(nbr.data(), d_nbr, m * 4, st), "download");
     check(epp_memcpy_d2h(ev.data(), d_ev, m, st), "download");
+    const auto t_dev1 = std::chrono::steady_clock::now();
     // ---- 3. shortest path over the valid edges (undirected), start = 0, goal = 1 ------
-    std::vector<std::vector<std::pair<int, double>>> adj(n);
+    // CSR of the symmetrised valid k-NN edges, then A* with the Euclidean distance to
+    // the goal (admissible and consistent for Euclidean edge costs: an optimal path).
+    std::vector<int32_t> deg(n + 1, 0);
     int64_t n_valid_edges = 0;
-    for (int i = 0; i < n; ++i)
-        for (int c = 0; c < k; ++c) {
-            const int j = nbr[(size_t)i * k + c];
-            if (j < 0 || !ev[(size_t)i * k + c]) continue;
-            const double dx = nodes[3 * j] - nodes[3 * i], dy = nodes[3 * j + 1] - nodes[3 * i + 1],
-                         dz = nodes[3 * j + 2] - nodes[3 * i + 2];
-            const double d = std::sqrt((dx * dx + dy * dy) + dz * dz);
-            adj[i].push_back({j, d});
-            adj[j].push_back({i, d});
-            ++n_valid_edges;
-        }
+    for (size_t e = 0; e < m; ++e) {
+        const int j = nbr[e];
+        if (j < 0 || !ev[e]) continue;
+        ++deg[e / k];
+        ++deg[j];
+        ++n_valid_edges;
+    }
+    std::vector<int32_t> off(n + 1, 0);
+    for (int i = 0; i < n; ++i) off[i + 1] = off[i] + deg[i];
+    std::vector<int32_t> adj(off[n]);
+    for (int i = 0; i < n; ++i) deg[i] = off[i];
+    for (size_t e = 0; e < m; ++e) {
+        const int j = nbr[e];
+        if (j < 0 || !ev[e]) continue;
+        const int i = (int)(e / k);
+        adj[deg[i]++] = j;
+        adj[deg[j]++] = i;
+    }
     {
         std::lock_guard<std::mutex> lk(g_stats_mu);
         stats_.states_sampled += samples;
@@ -123,31 +134,48 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
         stats_.edges_checked += (int64_t)m;
         stats_.edges_valid += n_valid_edges;
     }
+    auto node = [&](int v) { return Vec3(nodes[3 * v], nodes[3 * v + 1], nodes[3 * v + 2]); };
+    const Vec3 gp = node(1);
     std::vector<double> dist(n, std::numeric_limits<double>::infinity());
     std::vector<int> prev(n, -1);
-    using QE = std::pair<double, int>;
+    std::vector<uint8_t> closed(n, 0);
+    using QE = std::pair<double, int>;  // (g + h, node)
     std::priority_queue<QE, std::vector<QE>, std::greater<QE>> q;
     dist[0] = 0.0;
-    q.push({0.0, 0});
+    q.push({(node(0) - gp).norm(), 0});
     while (!q.empty()) {
-        const auto [d, u] = q.top();
+        const int u = q.top().second;
         q.pop();
-        if (d > dist[u]) continue;
+        if (closed[u]) continue;
+        closed[u] = 1;
         if (u == 1) break;
-        for (const auto& [v, c] : adj[u]) {
-            const double nd = d + c;
+        const Vec3 pu = node(u);
+        for (int32_t a = off[u]; a < off[u + 1]; ++a) {
+            const int v = adj[a];
+            if (closed[v]) continue;
+            const double nd = dist[u] + (node(v) - pu).norm();
             if (nd < dist[v]) {
                 dist[v] = nd;
                 prev[v] = u;
-                q.push({nd, v});
+                q.push({nd + (node(v) - gp).norm(), v});
             }
         }
     }
-    if (prev[1] < 0) return false;
+    auto account = [&] {
+        const auto t_end = std::chrono::steady_clock::now();
+        std::lock_guard<std::mutex> lk(g_stats_mu);
+        stats_.ms_device += std::chrono::duration<double, std::milli>(t_dev1 - t_dev0).count();
+        stats_.ms_search += std::chrono::duration<double, std::milli>(t_end - t_dev1).count();
+    };
+    if (prev[1] < 0) {
+        account();
+        return false;
+    }
     std::vector<Vec3> path;
     for (int v = 1; v >= 0; v = prev[v]) path.push_back({nodes[3 * v], nodes[3 * v + 1], nodes[3 * v + 2]});
     std::reverse(path.begin(), path.end());
     out = shortcut(path);
+    account();
     return true;
 }
 

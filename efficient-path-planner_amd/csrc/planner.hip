@@ -95,6 +95,219 @@ __global__ __launch_bounds__(kKnnBlock) void k_knn(const double* __restrict__ no
         for (int k = 0; k < K; ++k) nbr[(int64_t)i * K + k] = bi[k];
 }
 
+// ---- k-NN over a uniform grid (exact; same answer as k_knn) ------------------------
+// Cells of edge h hold ~3 nodes; every query walks shells of cells around its own cell
+// until the k-th best squared distance is below the squared distance to the nearest
+// face of the searched block (minus a rounding margin) — then no unvisited node can
+// enter the list.  Candidates are ranked by (distance, index), so the visiting order
+// (atomics in the scatter) never changes the result.
+struct KnnGrid {
+    double lo[3];
+    double h, inv_h;
+    int dims[3];
+    int ncell;
+};
+
+constexpr int kBoundsThreads = 1024;
+
+__global__ __launch_bounds__(kBoundsThreads) void k_knn_bounds(const double* __restrict__ nodes, int n,
+                                                               int cell_cap, KnnGrid* __restrict__ g) {
+    __shared__ double smin[3][kBoundsThreads / 64], smax[3][kBoundsThreads / 64];
+    double mn[3] = {1e308, 1e308, 1e308}, mx[3] = {-1e308, -1e308, -1e308};
+    for (int i = threadIdx.x; i < n; i += kBoundsThreads)
+        for (int d = 0; d < 3; ++d) {
+            const double v = nodes[3 * i + d];
+            mn[d] = fmin(mn[d], v);
+            mx[d] = fmax(mx[d], v);
+        }
+    for (int d = 0; d < 3; ++d)
+        for (int o = 32; o > 0; o >>= 1) {
+            mn[d] = fmin(mn[d], __shfl_xor(mn[d], o, 64));
+            mx[d] = fmax(mx[d], __shfl_xor(mx[d], o, 64));
+        }
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
+        for (int d = 0; d < 3; ++d) {
+            smin[d][wv] = mn[d];
+            smax[d][wv] = mx[d];
+        }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBoundsThreads / 64; ++w)
+            for (int d = 0; d < 3; ++d) {
+                mn[d] = fmin(mn[d], smin[d][w]);
+                mx[d] = fmax(mx[d], smax[d][w]);
+            }
+        double ext[3], vol = 1.0, emax = 0.0;
+        for (int d = 0; d < 3; ++d) {
+            ext[d] = mx[d] - mn[d];
+            emax = fmax(emax, ext[d]);
+        }
+        const double floor_ext = fmax(emax, 1e-9) * 1e-3;  // flat point sets: thin slabs
+        for (int d = 0; d < 3; ++d) vol *= fmax(ext[d], floor_ext);
+        double h = cbrt(3.0 * vol / (double)max(n, 1));
+        h = fmax(h, 1e-12);
+        int dims[3];
+        long long cells;
+        for (;;) {
+            cells = 1;
+            for (int d = 0; d < 3; ++d) {
+                dims[d] = (int)fmin(ext[d] / h, 1023.0) + 1;
+                cells *= dims[d];
+            }
+            if (cells <= cell_cap) break;
+            h *= 1.25;
+        }
+        for (int d = 0; d < 3; ++d) {
+            g->lo[d] = mn[d];
+            g->dims[d] = dims[d];
+        }
+        g->h = h;
+        g->inv_h = 1.0 / h;
+        g->ncell = (int)cells;
+    }
+}
+
+__device__ __forceinline__ int knn_cell_axis(double v, const KnnGrid& g, int d) {
+    const int c = (int)((v - g.lo[d]) * g.inv_h);
+    return c < 0 ? 0 : (c >= g.dims[d] ? g.dims[d] - 1 : c);
+}
+
+__global__ void k_knn_count(const double* __restrict__ nodes, int n, const KnnGrid* __restrict__ gp,
+                            int* __restrict__ cell_of, int* __restrict__ cnt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const KnnGrid g = *gp;
+    const int cx = knn_cell_axis(nodes[3 * i], g, 0), cy = knn_cell_axis(nodes[3 * i + 1], g, 1),
+              cz = knn_cell_axis(nodes[3 * i + 2], g, 2);
+    const int c = (cz * g.dims[1] + cy) * g.dims[0] + cx;
+    cell_of[i] = c;
+    atomicAdd(&cnt[c], 1);
+}
+
+// exclusive scan of cnt[0..ncell) into start[0..ncell], one block
+__global__ __launch_bounds__(kBoundsThreads) void k_knn_scan(const KnnGrid* __restrict__ gp,
+                                                             const int* __restrict__ cnt,
+                                                             int* __restrict__ start) {
+    __shared__ int part[kBoundsThreads];
+    const int nc = gp->ncell;
+    const int per = (nc + kBoundsThreads - 1) / kBoundsThreads;
+    const int b = threadIdx.x * per, e = min(nc, b + per);
+    int s = 0;
+    for (int c = b; c < e; ++c) s += cnt[c];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int t = 0; t < kBoundsThreads; ++t) {
+            const int v = part[t];
+            part[t] = acc;
+            acc += v;
+        }
+        start[nc] = acc;
+    }
+    __syncthreads();
+    int acc = part[threadIdx.x];
+    for (int c = b; c < e; ++c) {
+        start[c] = acc;
+        acc += cnt[c];
+    }
+}
+
+__global__ void k_knn_scatter(const double* __restrict__ nodes, int n, const int* __restrict__ cell_of,
+                              const int* __restrict__ start, int* __restrict__ fill,
+                              double* __restrict__ sxyz, int* __restrict__ sidx) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int c = cell_of[i];
+    const int pos = start[c] + atomicAdd(&fill[c], 1);
+    if (pos >= start[c + 1]) return;  // cannot happen with cleared counters; never write out of range
+    sidx[pos] = i;
+    sxyz[3 * pos] = nodes[3 * i];
+    sxyz[3 * pos + 1] = nodes[3 * i + 1];
+    sxyz[3 * pos + 2] = nodes[3 * i + 2];
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_knn_grid(const KnnGrid* __restrict__ gp, int n, double r2max,
+                                                  const double* __restrict__ sxyz,
+                                                  const int* __restrict__ sidx,
+                                                  const int* __restrict__ start,
+                                                  int32_t* __restrict__ nbr) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;  // queries in cell order: coherent walks
+    if (t >= n) return;
+    const KnnGrid g = *gp;
+    const int self = sidx[t];
+    const double px = sxyz[3 * t], py = sxyz[3 * t + 1], pz = sxyz[3 * t + 2];
+    const int c[3] = {knn_cell_axis(px, g, 0), knn_cell_axis(py, g, 1), knn_cell_axis(pz, g, 2)};
+    const double p[3] = {px, py, pz};
+    double bd[K];
+    int bi[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        bd[k] = r2max;
+        bi[k] = 0x7fffffff;
+    }
+    const int rmax = max(g.dims[0], max(g.dims[1], g.dims[2]));
+    for (int r = 0; r <= rmax; ++r) {
+        for (int dz = -r; dz <= r; ++dz) {
+            const int z = c[2] + dz;
+            if (z < 0 || z >= g.dims[2]) continue;
+            for (int dy = -r; dy <= r; ++dy) {
+                const int y = c[1] + dy;
+                if (y < 0 || y >= g.dims[1]) continue;
+                const bool face = (dz == -r || dz == r || dy == -r || dy == r);
+                const int step = (face || r == 0) ? 1 : 2 * r;
+                for (int dx = -r; dx <= r; dx += step) {
+                    const int x = c[0] + dx;
+                    if (x < 0 || x >= g.dims[0]) continue;
+                    const int cell = (z * g.dims[1] + y) * g.dims[0] + x;
+                    const int e = start[cell + 1];
+                    for (int q = start[cell]; q < e; ++q) {
+                        const int j = sidx[q];
+                        const double ddx = sxyz[3 * q] - px, ddy = sxyz[3 * q + 1] - py, ddz = sxyz[3 * q + 2] - pz;
+                        const double d = (ddx * ddx + ddy * ddy) + ddz * ddz;
+                        if (j == self || !(d < bd[K - 1] || (d == bd[K - 1] && j < bi[K - 1]))) continue;
+                        double vd = d;
+                        int vi = j;
+                        bool shift = false;
+#pragma unroll
+                        for (int k = 0; k < K; ++k) {
+                            shift = shift || vd < bd[k] || (vd == bd[k] && vi < bi[k]);
+                            if (shift) {
+                                const double td = bd[k];
+                                const int ti = bi[k];
+                                bd[k] = vd;
+                                bi[k] = vi;
+                                vd = td;
+                                vi = ti;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        // distance from p to the nearest face of the searched block that has cells beyond it
+        double dmin = 1e300;
+        bool all = true;
+        for (int d = 0; d < 3; ++d) {
+            if (c[d] - r > 0) {
+                dmin = fmin(dmin, p[d] - (g.lo[d] + (double)(c[d] - r) * g.h));
+                all = false;
+            }
+            if (c[d] + r < g.dims[d] - 1) {
+                dmin = fmin(dmin, (g.lo[d] + (double)(c[d] + r + 1) * g.h) - p[d]);
+                all = false;
+            }
+        }
+        if (all) break;
+        dmin -= g.h * 1e-6;  // cell assignment rounds; stay conservative
+        if (dmin > 0 && bd[K - 1] < dmin * dmin) break;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) nbr[(int64_t)self * K + k] = bi[k] == 0x7fffffff ? -1 : bi[k];
+}
+
 __global__ void k_knn_edges(const double* __restrict__ nodes, const int32_t* __restrict__ nbr, int64_t m,
                             int k, double* __restrict__ s1, double* __restrict__ s2) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -137,7 +350,8 @@ epp_status epp_sample_uniform(uint64_t seed, const double lo[3], const double hi
     return last("epp_sample_uniform");
 }
 
-epp_status epp_knn(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr, void* stream) {
+epp_status epp_knn_bruteforce(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr,
+                              void* stream) {
     if (n < 0 || (n > 0 && (!nodes || !nbr)) || (k != 4 && k != 8 && k != 16 && k != 32)) {
         set_error("epp_knn: invalid argument (k must be 4, 8, 16 or 32)");
         return EPP_ERR_INVALID_ARGUMENT;
@@ -152,7 +366,64 @@ epp_status epp_knn(const double* nodes, int32_t n, int32_t k, double max_dist, i
         case 16: hipLaunchKernelGGL(k_knn<16>, grid, block, 0, s, nodes, n, r2, nbr); break;
         default: hipLaunchKernelGGL(k_knn<32>, grid, block, 0, s, nodes, n, r2, nbr); break;
     }
-    return last("epp_knn");
+    return last("epp_knn_bruteforce");
+}
+
+epp_status epp_knn(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr, void* stream) {
+    // the grid pays off from a few thousand nodes; both give the same answer
+    return n <= 2048 ? epp_knn_bruteforce(nodes, n, k, max_dist, nbr, stream)
+                     : epp_knn_grid(nodes, n, k, max_dist, nbr, stream);
+}
+
+epp_status epp_knn_grid(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr, void* stream) {
+    if (n < 0 || (n > 0 && (!nodes || !nbr)) || (k != 4 && k != 8 && k != 16 && k != 32)) {
+        set_error("epp_knn_grid: invalid argument (k must be 4, 8, 16 or 32)");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    if (n == 0) return EPP_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const int cap = max(64, n);
+    // scratch layout, every part 256-byte aligned: grid params | cell_of[n] | sidx[n] |
+    // sxyz[3n] | cnt[cap+1] | start[cap+1] | fill[cap+1]
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t o_cell = 256, o_sidx = o_cell + al((size_t)n * 4), o_sxyz = o_sidx + al((size_t)n * 4),
+                 o_cnt = o_sxyz + al((size_t)n * 24), o_start = o_cnt + al((size_t)(cap + 1) * 4),
+                 o_fill = o_start + al((size_t)(cap + 1) * 4), bytes = o_fill + al((size_t)(cap + 1) * 4);
+    char* buf = nullptr;
+    hipError_t e = hipMallocAsync((void**)&buf, bytes, s);
+    if (e != hipSuccess) {
+        set_error(std::string("epp_knn_grid: hipMallocAsync: ") + hipGetErrorString(e));
+        return EPP_ERR_HIP;
+    }
+    KnnGrid* g = reinterpret_cast<KnnGrid*>(buf);
+    int* cell_of = reinterpret_cast<int*>(buf + o_cell);
+    int* sidx = reinterpret_cast<int*>(buf + o_sidx);
+    double* sxyz = reinterpret_cast<double*>(buf + o_sxyz);
+    int* cnt = reinterpret_cast<int*>(buf + o_cnt);
+    int* start = reinterpret_cast<int*>(buf + o_start);
+    int* fill = reinterpret_cast<int*>(buf + o_fill);
+    e = hipMemsetAsync(cnt, 0, (size_t)(cap + 1) * 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(fill, 0, (size_t)(cap + 1) * 4, s);
+    if (e != hipSuccess) {  // never launch the scatter on counters that were not cleared
+        set_error(std::string("epp_knn_grid: hipMemsetAsync: ") + hipGetErrorString(e));
+        (void)hipFreeAsync(buf, s);
+        return EPP_ERR_HIP;
+    }
+    const double r2 = max_dist > 0 ? max_dist * max_dist : 1e300;
+    const dim3 g256((n + 255) / 256), b256(256);
+    hipLaunchKernelGGL(k_knn_bounds, dim3(1), dim3(kBoundsThreads), 0, s, nodes, n, cap, g);
+    hipLaunchKernelGGL(k_knn_count, g256, b256, 0, s, nodes, n, g, cell_of, cnt);
+    hipLaunchKernelGGL(k_knn_scan, dim3(1), dim3(kBoundsThreads), 0, s, g, cnt, start);
+    hipLaunchKernelGGL(k_knn_scatter, g256, b256, 0, s, nodes, n, cell_of, start, fill, sxyz, sidx);
+    switch (k) {
+        case 4: hipLaunchKernelGGL(k_knn_grid<4>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
+        case 8: hipLaunchKernelGGL(k_knn_grid<8>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
+        case 16: hipLaunchKernelGGL(k_knn_grid<16>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
+        default: hipLaunchKernelGGL(k_knn_grid<32>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
+    }
+    const epp_status rc = last("epp_knn_grid");
+    (void)hipFreeAsync(buf, s);
+    return rc;
 }
 
 epp_status epp_knn_edges(const double* nodes, const int32_t* nbr, int32_t n, int32_t k, double* s1,

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -144,6 +145,59 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
                     mask[c] |= 1ull << (((z & 3) * 4 + (y & 3)) * 4 + (x & 3));
                 }
     }
+    // ---- flat occupancy bitmap (k_states fast path) ------------------------------
+    std::vector<uint32_t> bitmap;
+    {
+        const char* env = std::getenv("EPP_BITMAP_BITS");
+        const double target = env && *env ? std::max(64.0, std::atof(env)) : double(1 << 18);
+        int bd[3] = {1, 1, 1};
+        float bo[3] = {0, 0, 0}, bi[3] = {1, 1, 1};
+        if (n > 0) {
+            double ext[3], vol = 1.0;
+            for (int k = 0; k < 3; ++k) {
+                ext[k] = std::max(g1[k] - g0[k], 1e-3);
+                vol *= ext[k];
+            }
+            double h = std::cbrt(vol / target);
+            for (int pass = 0;; ++pass) {
+                bool ok = true;
+                for (int k = 0; k < 3; ++k) {
+                    bd[k] = std::min(4096, (int)std::ceil(ext[k] / h) + 2 + pass);
+                    bo[k] = (float)(g0[k] - h);
+                    bi[k] = (float)(1.0 / h);
+                }
+                // every AABB corner must map inside the grid (else widen and retry)
+                for (int i = 0; i < n && ok; ++i)
+                    for (int k = 0; k < 3; ++k) {
+                        const int a = bm_axis(hw.aabbs[(size_t)i * 6 + k], bo[k], bi[k]);
+                        const int b = bm_axis(hw.aabbs[(size_t)i * 6 + 3 + k], bo[k], bi[k]);
+                        if (a < 0 || b >= bd[k]) ok = false;
+                    }
+                if (ok) break;
+                if (pass > 8) h *= 1.1;
+            }
+        }
+        const size_t cells = (size_t)bd[0] * bd[1] * bd[2];
+        const size_t words = (cells + 31) / 32;
+        bitmap.assign(words + 1, 0u);  // + zero sentinel
+        for (int i = 0; i < n; ++i) {
+            int a[3], b[3];
+            for (int k = 0; k < 3; ++k) {
+                a[k] = bm_axis(hw.aabbs[(size_t)i * 6 + k], bo[k], bi[k]);
+                b[k] = bm_axis(hw.aabbs[(size_t)i * 6 + 3 + k], bo[k], bi[k]);
+            }
+            for (int z = a[2]; z <= b[2]; ++z)
+                for (int y = a[1]; y <= b[1]; ++y)
+                    for (int x = a[0]; x <= b[0]; ++x) {
+                        const size_t c = ((size_t)z * bd[1] + y) * bd[0] + x;
+                        bitmap[c >> 5] |= 1u << (c & 31);
+                    }
+        }
+        v.bnx = bd[0]; v.bny = bd[1]; v.bnz = bd[2];
+        v.bofx = bo[0]; v.bofy = bo[1]; v.bofz = bo[2];
+        v.bix = bi[0]; v.biy = bi[1]; v.biz = bi[2];
+        v.bm_words = (uint32_t)words;
+    }
     std::vector<uint32_t> cell_start(ncell + 1, 0);
     for (int c = 0; c < ncell; ++c) cell_start[c + 1] = cell_start[c] + (uint32_t)cells[c].size();
     const size_t n_entries = cell_start[ncell];
@@ -154,7 +208,8 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
     const size_t off_co = front;
     const size_t off_meta = align16(off_co + n_entries * 2);
     const size_t off_soa = align16(off_meta + meta.size() * 4);
-    const size_t total = align16(off_soa + soa.size() * sizeof(double));
+    const size_t off_bm = align16(off_soa + soa.size() * sizeof(double));
+    const size_t total = align16(off_bm + bitmap.size() * 4);
     if (total > 0xFFFFFFFFull) {
         set_error("epp_world: index too large");
         return false;
@@ -170,6 +225,8 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
     }
     std::memcpy(b + off_meta, meta.data(), meta.size() * 4);
     std::memcpy(b + off_soa, soa.data(), soa.size() * sizeof(double));
+    std::memcpy(b + off_bm, bitmap.data(), bitmap.size() * 4);
+    v.off_bitmap = (uint32_t)off_bm;
     v.blob_bytes = (uint32_t)total;
     v.front_bytes = (uint32_t)front;
     v.off_cell_mask = (uint32_t)off_mask;
@@ -180,25 +237,32 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
     return true;
 }
 
+// The device allocation holds the blob followed by a copy of the WorldView (kernels
+// that keep only a pointer to it read the fields they need through the scalar cache).
 bool upload(HostWorld& hw) {
     const size_t bytes = hw.blob.size();
-    if (bytes > hw.d_capacity) {
+    const size_t view_off = (bytes + 255) & ~size_t(255);
+    const size_t need = view_off + sizeof(WorldView);
+    if (need > hw.d_capacity) {
         if (hw.d_blob) (void)hipFree(hw.d_blob);
         hw.d_blob = nullptr;
         hw.d_capacity = 0;
-        hipError_t e = hipMalloc(&hw.d_blob, bytes);
+        hipError_t e = hipMalloc(&hw.d_blob, need);
         if (e != hipSuccess) {
             set_error(std::string("epp_world: hipMalloc: ") + hipGetErrorString(e));
             return false;
         }
-        hw.d_capacity = bytes;
+        hw.d_capacity = need;
     }
+    hw.view.blob = (const unsigned char*)hw.d_blob;
+    hw.d_view = reinterpret_cast<const WorldView*>(static_cast<char*>(hw.d_blob) + view_off);
     hipError_t e = hipMemcpy(hw.d_blob, hw.blob.data(), bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(static_cast<char*>(hw.d_blob) + view_off, &hw.view, sizeof(WorldView), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         set_error(std::string("epp_world: hipMemcpy: ") + hipGetErrorString(e));
         return false;
     }
-    hw.view.blob = (const unsigned char*)hw.d_blob;
     return true;
 }
 
@@ -272,4 +336,5 @@ epp_status epp_world_get_aabbs(const epp_world* w, double* lo_hi) {
 // Accessor for the kernels' launchers (collision.hip).
 namespace epp {
 const WorldView& world_view(const epp_world* w) { return w->view; }
+const WorldView* world_dview(const epp_world* w) { return w->d_view; }
 }  // namespace epp

@@ -74,6 +74,8 @@ def lib() -> C.CDLL:
             "epp_host_free": (None, [vp]),
             "epp_sample_uniform": (i32, [C.c_uint64, vp, vp, i64, i64, vp, vp]),
             "epp_knn": (i32, [vp, i32, i32, dp, vp, vp]),
+            "epp_knn_bruteforce": (i32, [vp, i32, i32, dp, vp, vp]),
+            "epp_knn_grid": (i32, [vp, i32, i32, dp, vp, vp]),
             "epp_knn_edges": (i32, [vp, vp, i32, i32, vp, vp, vp]),
         }
         for name, (res, args) in sig.items():
@@ -93,7 +95,7 @@ EXPORTED = [
     "epp_world_destroy", "epp_world_num_obbs", "epp_world_get_aabbs", "epp_check_states",
     "epp_check_states_mindist", "epp_check_motions", "epp_minsnap_batch", "epp_sample_count",
     "epp_sample_batch", "epp_generate_trajectory_host", "epp_host_free", "epp_sample_uniform", "epp_knn",
-    "epp_knn_edges",
+    "epp_knn_bruteforce", "epp_knn_grid", "epp_knn_edges",
 ]
 
 
@@ -304,13 +306,16 @@ def sample_uniform(seed: int, lo, hi, n: int, start: int = 0) -> np.ndarray:
     return d.download(np.float64, 3 * n).reshape(n, 3)
 
 
-def knn(nodes: np.ndarray, k: int, max_dist: float = 0.0) -> np.ndarray:
-    """epp_knn: (n, k) neighbour indices, nearest first, -1 where fewer than k exist."""
+def knn(nodes: np.ndarray, k: int, max_dist: float = 0.0, method: str = "auto") -> np.ndarray:
+    """epp_knn (method "auto"), epp_knn_bruteforce ("brute") or epp_knn_grid ("grid"):
+    (n, k) neighbour indices, nearest first, ties to the lower index, -1 where fewer
+    than k exist."""
     nodes = np.ascontiguousarray(np.asarray(nodes, np.float64).reshape(-1, 3))
     n = len(nodes)
     d_n = DeviceBuffer.from_array(nodes)
     d_k = DeviceBuffer(4 * max(n * k, 1))
-    check(lib().epp_knn(d_n.ptr, n, int(k), float(max_dist), d_k.ptr, None))
+    fn = {"auto": lib().epp_knn, "brute": lib().epp_knn_bruteforce, "grid": lib().epp_knn_grid}[method]
+    check(fn(d_n.ptr, n, int(k), float(max_dist), d_k.ptr, None))
     sync()
     return d_k.download(np.int32, n * k).reshape(n, k)
 

@@ -155,6 +155,11 @@ epp_status epp_sample_uniform(uint64_t seed, const double lo[3], const double hi
 /* k nearest neighbours (k in {4, 8, 16, 32}) of every node within max_dist (<= 0: no
  * limit), sorted by distance, ties to the lower index; missing entries are -1. */
 epp_status epp_knn(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr, void* stream);
+/* The two strategies behind epp_knn (same answers): all-pairs with LDS tiles, and a
+ * uniform grid walked in shells (stream-ordered scratch from hipMallocAsync). */
+epp_status epp_knn_bruteforce(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr,
+                              void* stream);
+epp_status epp_knn_grid(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr, void* stream);
 /* Edge endpoints for every (node i, neighbour c): s1 = nodes[i], s2 = nodes[nbr[i k + c]]
  * (s2 = s1 for a missing neighbour).  s1, s2: n k x 3. */
 epp_status epp_knn_edges(const double* nodes, const int32_t* nbr, int32_t n, int32_t k, double* s1,

@@ -55,41 +55,55 @@ def main():
 
     diag = C.CDLL(os.path.join(ROOT, "scripts", "libdiag.so"))
     diag.diag_stream.argtypes = [C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_void_p]
-    for mode in (0, 1, 2):
-        for blocks in (1024, 2048, 4096):
-            f = lambda r: diag.diag_stream(mode, d.ptr + (r % NB) * N * 24, N, dv.ptr, blocks, st)  # noqa
-            f(0)
-            ms = timed_kernel_ms(capi, st, f, 32)
-            res[f"stream_mode{mode}_blocks{blocks}"] = {"us": ms * 1e3, "GBs": 25 * N / (ms * 1e-3) / 1e9}
-            print(f"stream_mode{mode}_blocks{blocks}", res[f"stream_mode{mode}_blocks{blocks}"], flush=True)
-        # asymptotic: 16M states in one launch
-        f = lambda r: diag.diag_stream(mode, d.ptr, NB * N, dv.ptr, 4096, st)  # noqa
-        dbig = capi.DeviceBuffer(NB * N)
+    dbig = capi.DeviceBuffer(NB * N)
+    for mode in (0,):
+        f = lambda r: diag.diag_stream(mode, d.ptr + (r % NB) * N * 24, N, dv.ptr, 1024, st)  # noqa
+        f(0)
+        ms = timed_kernel_ms(capi, st, f, 32)
+        res[f"stream_mode{mode}"] = {"us": ms * 1e3, "GBs": 25 * N / (ms * 1e-3) / 1e9}
+        print(f"stream_mode{mode}", res[f"stream_mode{mode}"], flush=True)
         f = lambda r: diag.diag_stream(mode, d.ptr, NB * N, dbig.ptr, 4096, st)  # noqa
         f(0)
         ms = timed_kernel_ms(capi, st, f, 8)
         res[f"stream_mode{mode}_16M"] = {"us": ms * 1e3, "GBs": 25 * NB * N / (ms * 1e-3) / 1e9}
         print(f"stream_mode{mode}_16M", res[f"stream_mode{mode}_16M"], flush=True)
-    run("c2_uniform", w2, d)
-    # 16M states in one launch (asymptotic rate of the real kernel)
-    dbig = capi.DeviceBuffer(NB * N)
-    f = lambda r: w2.check_states_dev(d.ptr, NB * N, 0, dbig.ptr, stream=st)  # noqa
-    f(0)
-    ms = timed_kernel_ms(capi, st, f, 8)
-    res["c2_uniform_16M"] = {"us": ms * 1e3, "GBs": 25 * NB * N / (ms * 1e-3) / 1e9}
-    print("c2_uniform_16M", res["c2_uniform_16M"], flush=True)
-    run("c2_above_union_box", w2, dz)
-    run("empty_world", w0, d)
-    for k in (1, 2, 4, 8, 16):
-        run(f"c2_wg_per_cu_{k}", w2, d, {"EPP_WG_PER_CU": k})
-    run("c2_no_lds", w2, d, {"EPP_NO_LDS": 1})
+
+    def big(name, world, env=None):
+        for k, v in (env or {}).items():
+            os.environ[k] = str(v)
+        f = lambda r: world.check_states_dev(d.ptr, NB * N, 0, dbig.ptr, stream=st)  # noqa
+        f(0)
+        ms = timed_kernel_ms(capi, st, f, 8)
+        for k in (env or {}):
+            del os.environ[k]
+        res[name] = {"us": ms * 1e3, "GBs": 25 * NB * N / (ms * 1e-3) / 1e9}
+        print(name, res[name], flush=True)
+
+    for impl in (0, 1):
+        e = {"EPP_STATES_IMPL": impl}
+        run(f"c2_impl{impl}", w2, d, e)
+        big(f"c2_impl{impl}_16M", w2, e)
+        run(f"c2_impl{impl}_above_union_box", w2, dz, e)
+        run(f"c2_impl{impl}_empty_world", w0, d, e)
+    run("c2_impl1_nolds", w2, d, {"EPP_NO_LDS": 1})
+    big("c2_impl1_nolds_16M", w2, {"EPP_NO_LDS": 1})
+    for k in (2, 4, 6, 8):
+        run(f"c2_impl1_wg_per_cu_{k}", w2, d, {"EPP_WG_PER_CU": k})
+        big(f"c2_impl1_wg_per_cu_{k}_16M", w2, {"EPP_WG_PER_CU": k})
+    for bits in (1 << 14, 1 << 16, 1 << 20, 1 << 22):
+        os.environ["EPP_BITMAP_BITS"] = str(bits)
+        wb = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
+        del os.environ["EPP_BITMAP_BITS"]
+        run(f"c2_impl1_bitmap_{bits}", wb, d)
+        big(f"c2_impl1_bitmap_{bits}_16M", wb)
+        wb.close()
     # motions, C3
     g3, o3 = synth.track_world(42, n_obstacles=472)
     w3 = capi.World(capi.build_obbs(geom, g3, o3), rg, ro)
     s1, s2 = synth.edges(43, 8, lo, hi, N)
     d1, d2 = capi.DeviceBuffer.from_array(s1), capi.DeviceBuffer.from_array(s2)
     for mode in (0, 1):
-        for env in ({}, {"EPP_NO_LDS": 1}):
+        for env in ({},):
             for k, v in env.items():
                 os.environ[k] = str(v)
             f = lambda r: w3.check_motions_dev(d1.ptr, d2.ptr, N, 0, mode, dv.ptr, stream=st)  # noqa

@@ -65,13 +65,39 @@ def _knn_ref(nodes, k, max_dist=0.0):
     return out
 
 
+@pytest.mark.parametrize("method", ["brute", "grid"])
 @pytest.mark.parametrize("k", [4, 8, 16, 32])
-def test_knn_vs_bruteforce(k):
+def test_knn_vs_bruteforce(k, method):
     nodes = synth.sample_states(7 + k, [-2, -2, 0], [2, 2, 2], 700)
     nodes[10] = nodes[3]              # duplicate: tie broken by index
     nodes[500:520] = nodes[0] + 0.01  # a cluster of identical distances
-    got = capi.knn(nodes, k)
+    got = capi.knn(nodes, k, method=method)
     assert np.array_equal(got, _knn_ref(nodes, k))
+
+
+@pytest.mark.parametrize("k", [4, 16, 32])
+def test_knn_grid_large(k):
+    """Grid k-NN (used above 2048 nodes) vs the all-pairs kernel and numpy: clustered,
+    duplicated and lattice (many exact ties) nodes."""
+    rs = np.random.RandomState(k)
+    nodes = synth.sample_states(100 + k, [-6, -6, 0], [6, 6, 2], 4000)
+    nodes[:300] = rs.normal(0, 0.05, (300, 3)) + [1, 1, 1]          # a dense cluster
+    nodes[300:400] = nodes[400:500]                                  # duplicates
+    g = np.stack(np.meshgrid(np.arange(8), np.arange(8), np.arange(4)), -1).reshape(-1, 3) * 0.25
+    nodes[500:756] = g                                               # lattice: exact ties
+    got = capi.knn(nodes, k, method="grid")
+    assert np.array_equal(got, capi.knn(nodes, k, method="brute"))
+    assert np.array_equal(got, _knn_ref(nodes, k))
+    assert np.array_equal(capi.knn(nodes, k), got)                   # auto -> grid
+
+
+def test_knn_grid_flat_and_radius():
+    nodes = synth.sample_states(5, [-3, -3, 0.7], [3, 3, 0.7], 3000)  # all z equal: flat grid
+    assert np.array_equal(capi.knn(nodes, 16, method="grid"), _knn_ref(nodes, 16))
+    nodes3 = synth.sample_states(6, [-3, -3, 0], [3, 3, 2], 3000)
+    assert np.array_equal(capi.knn(nodes3, 8, 0.35, method="grid"), _knn_ref(nodes3, 8, 0.35))
+    one = np.array([[0.5, 0.5, 0.5]])
+    assert (capi.knn(one, 4, method="grid") == -1).all()
 
 
 def test_knn_radius_and_small_n():
