@@ -16,6 +16,8 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
+#include <set>
 #include <string>
 
 #include "epp_internal.h"
@@ -314,14 +316,20 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t x, int /*lane*/, uin
 }
 
 template <bool MINDIST>
-__device__ __forceinline__ bool pair_hit(const Acc& a, const WorldView& w, int i, double px, double py,
-                                         double pz, bool can_pass, double md) {
+__device__ __forceinline__ bool pair_hit_r(const Acc& a, double r_gate, double r_obst, int i, double px, double py,
+                                           double pz, bool can_pass, double md) {
     if (!(a.g(F_LOX, i) < px && px < a.g(F_HIX, i) && a.g(F_LOY, i) < py && py < a.g(F_HIY, i) &&
           a.g(F_LOZ, i) < pz && pz < a.g(F_HIZ, i)))
         return false;  // rtree contains(point): strict  src/World.cpp:83
     const uint32_t m = a.meta[i];
     if (MINDIST) return !(m & META_FILLING) && obb_point_hit(a, i, m, px, py, pz, md);  // :116-125
-    return !((m & META_FILLING) && can_pass) && obb_point_hit(a, i, m, px, py, pz, owner_r(w, m));  // :92-100
+    return !((m & META_FILLING) && can_pass) &&
+           obb_point_hit(a, i, m, px, py, pz, (m & META_GATE) ? r_gate : r_obst);  // :89-100
+}
+template <bool MINDIST>
+__device__ __forceinline__ bool pair_hit(const Acc& a, const WorldView& w, int i, double px, double py,
+                                         double pz, bool can_pass, double md) {
+    return pair_hit_r<MINDIST>(a, w.r_gate, w.r_obst, i, px, py, pz, can_pass, md);
 }
 
 // Candidate walk of one state by its own lane (tail states and overflow).
@@ -512,53 +520,106 @@ __global__ __launch_bounds__(kBlock) void k_states(WorldView w, const double* __
 constexpr int kQueueCap = 256;  // a wave's whole group (64 lanes x 4 states)
 struct StateQueue {
     double xyz[kQueueCap][3];
+    uint32_t cls[kQueueCap];
     uint8_t hit[kQueueCap];
 };
 
 // Fast-path parameters of the bitmap (kept in SGPRs; the rest of the WorldView is read
 // through the scalar cache only on the rare exact path).
-typedef const __attribute__((address_space(1))) uint32_t* gptr_u32;  // global, not flat
+typedef const __attribute__((address_space(1))) uint16_t* gptr_u16;  // global, not flat
 
 struct BmParams {
-    gptr_u32 bm;
+    gptr_u16 cls;
     float ox, oy, oz, ix, iy, iz;
     uint32_t nx, ny, nz, sentinel;
 };
 
-__device__ __forceinline__ uint32_t bm_word_index(const BmParams& p, double px, double py, double pz,
-                                                  uint32_t& bit) {
+// index of the fine cell of p in cls[] (the zero sentinel when p is outside the grid)
+__device__ __forceinline__ uint32_t cls_index(const BmParams& p, double px, double py, double pz) {
     const int ix = bm_axis(px, p.ox, p.ix), iy = bm_axis(py, p.oy, p.iy), iz = bm_axis(pz, p.oz, p.iz);
     const bool in = (unsigned)ix < p.nx && (unsigned)iy < p.ny && (unsigned)iz < p.nz;
     // dims <= 4096 per axis, so the products fit 24-bit multiplies
     const uint32_t c = __umul24(__umul24((uint32_t)iz, p.ny) + (uint32_t)iy, p.nx) + (uint32_t)ix;
-    bit = c & 31u;
-    return in ? (c >> 5) : p.sentinel;  // the sentinel word is 0
+    return in ? c : p.sentinel;
 }
 
 // Exact test of one queued state: rtree prefilter + OBB tests on its coarse-cell list.
 // The WorldView pointer is laundered through an empty asm so the compiler cannot hoist
 // the field loads into the streaming loop: the rare path reads them through the scalar
 // cache instead of pinning ~50 SGPRs for the whole kernel.
-// `base` is the blob: its LDS copy (STAGE) or the HBM original.
+// `base` is the blob: its LDS copy (STAGE) or the HBM original.  `cls` is the state's
+// fine-cell class: the first chunk of its candidate list.
 template <bool MINDIST>
 __device__ __forceinline__ bool states_exact_hit(const WorldView* wvp, const unsigned char* base, double px,
-                                                 double py, double pz, int can_pass, double md) {
+                                                 double py, double pz, uint32_t cls, int can_pass, double md) {
     // constant address space: the fields come in by scalar loads (lgkmcnt), not flat
     // loads that would also wait for the in-flight prefetch
 #if defined(__HIP_DEVICE_COMPILE__)  // (the host pass only parses device bodies)
     typedef const __attribute__((address_space(4))) WorldView* cwv_ptr;
     cwv_ptr p = (cwv_ptr)wvp;
     asm volatile("" : "+s"(p));
-    const WorldView w = *p;
 #else
-    const WorldView& w = *wvp;
+    const WorldView* p = wvp;
 #endif
-    const Acc a = make_acc(base, base, w);
-    uint32_t st = 0;
-    const uint32_t c = classify(a, w, px, py, pz, st);
-    for (uint32_t j = 0; j < c; ++j)
-        if (pair_hit<MINDIST>(a, w, a.co[st + j], px, py, pz, can_pass != 0, md)) return true;
+    // list path: only the few fields it needs (keeps SGPR pressure low)
+    Acc a;
+    a.f = reinterpret_cast<const double*>(base + p->off_soa);
+    a.n_pad = p->n_pad;
+    a.meta = reinterpret_cast<const uint32_t*>(base + p->off_meta);
+    const double rg = p->r_gate, ro = p->r_obst;
+    const uint32_t hd = reinterpret_cast<const uint32_t*>(base + p->off_lists)[cls];
+    const uint16_t* ids = reinterpret_cast<const uint16_t*>(base + p->off_ids) + (hd >> 12);
+    const uint32_t cnt = hd & 4095u;
+    for (uint32_t j = 0; j < cnt; ++j)
+        if (pair_hit_r<MINDIST>(a, rg, ro, ids[j], px, py, pz, can_pass != 0, md)) return true;
     return false;
+}
+
+// Same predicate as pair_hit_r on one AoS record (rec: kRecDoubles doubles).
+template <bool MINDIST>
+__device__ __forceinline__ bool rec_hit(const double* rec, double rg, double ro, double px, double py, double pz,
+                                        bool can_pass, double md) {
+    if (!(rec[F_LOX] < px && px < rec[F_HIX] && rec[F_LOY] < py && py < rec[F_HIY] && rec[F_LOZ] < pz &&
+          pz < rec[F_HIZ]))
+        return false;  // rtree contains(point): strict  src/World.cpp:83
+    const uint32_t m = (uint32_t)__double_as_longlong(rec[R_META]);
+    double r;
+    if (MINDIST) {
+        if (m & META_FILLING) return false;  // :116-118
+        r = md;
+    } else {
+        if ((m & META_FILLING) && can_pass) return false;  // :92-95
+        r = (m & META_GATE) ? rg : ro;                     // :89-90
+    }
+    // OBB::checkCollisionWithPoint — src/OBB.cpp:63-91 (same evaluation as obb_point_hit)
+    const double c = rec[F_COS], s = rec[F_SIN];
+    const double dx = px - rec[F_CX], dy = py - rec[F_CY], dz = pz - rec[F_CZ];
+    const double lx = c * dx + s * dy;
+    const double ly = c * dy - s * dx;
+    double tx = rec[F_HX], ty = rec[F_HY], tz = rec[F_HZ];
+    if (!(m & META_FILLING)) {
+        tx = tx + r;
+        ty = ty + r;
+        tz = tz + r;
+    }
+    return fabs(lx) <= tx && fabs(ly) <= ty && fabs(dz) <= tz;
+}
+
+// Exact test on the AoS records + the cell's candidate list (no early exit: the lists
+// are short and straight-line control flow keeps the wave converged).  `sbase` points
+// at the records (LDS copy or HBM); `lists_off` / `ids_off` are relative to it.
+template <bool MINDIST>
+__device__ __forceinline__ bool states_exact_rec(const unsigned char* sbase, uint32_t lists_off, uint32_t ids_off,
+                                                 double rg, double ro, double px, double py, double pz, uint32_t cls,
+                                                 int can_pass, double md) {
+    const double* recs = reinterpret_cast<const double*>(sbase);
+    const uint32_t h = reinterpret_cast<const uint32_t*>(sbase + lists_off)[cls];
+    const uint16_t* ids = reinterpret_cast<const uint16_t*>(sbase + ids_off) + (h >> 12);
+    const uint32_t cnt = h & 4095u;
+    bool hit = false;
+    for (uint32_t j = 0; j < cnt; ++j)
+        hit |= rec_hit<MINDIST>(recs + (size_t)ids[j] * kRecDoubles, rg, ro, px, py, pz, can_pass != 0, md);
+    return hit;
 }
 
 // STAGE: the blob up to the bitmap (cull grid, lists, OBB table) is copied into LDS once
@@ -584,12 +645,13 @@ __global__ __launch_bounds__(kBlock) void k_states_bm(const WorldView* __restric
     };
     mark(0);
     BmParams bp;
-    bp.bm = (gptr_u32)(wv->blob + wv->off_bitmap);
+    bp.cls = (gptr_u16)(wv->blob + wv->off_bitmap);
     bp.ox = wv->bofx; bp.oy = wv->bofy; bp.oz = wv->bofz;
     bp.ix = wv->bix; bp.iy = wv->biy; bp.iz = wv->biz;
     bp.nx = (uint32_t)wv->bnx; bp.ny = (uint32_t)wv->bny; bp.nz = (uint32_t)wv->bnz;
     bp.sentinel = wv->bm_words;
-    const unsigned char* xbase = nullptr;  // blob for the exact path: LDS copy or HBM (set below)
+    const unsigned char* xbase = nullptr;
+    uint32_t total_needy_dbg = 0;  // blob for the exact path: LDS copy or HBM (set below)
     const int64_t groups = n / 4;  // full groups of 4; the n % 4 tail states come last
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     auto load = [&](int64_t grp, double (&dst)[12]) {
@@ -607,18 +669,18 @@ __global__ __launch_bounds__(kBlock) void k_states_bm(const WorldView* __restric
             for (int k = 0; k < 12; ++k) dst[k] = xyz[12 * grp + k];
         }
     };
-    // the current group's four bitmap words are requested BEFORE the next group's
+    // the current group's four cell classes are requested BEFORE the next group's
     // prefetch, so waiting for them (vmcnt counts in order) leaves the prefetch in flight
-    auto words = [&](const double (&v)[12], uint32_t (&wd)[4], uint32_t (&bit)[4]) {
+    auto words = [&](const double (&v)[12], uint32_t (&wd)[4]) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) wd[k] = bp.bm[bm_word_index(bp, v[3 * k], v[3 * k + 1], v[3 * k + 2], bit[k])];
+        for (int k = 0; k < 4; ++k) wd[k] = bp.cls[cls_index(bp, v[3 * k], v[3 * k + 1], v[3 * k + 2])];
     };
-    auto finish = [&](int64_t gg, const double (&v)[12], const uint32_t (&wd)[4], const uint32_t (&bit)[4]) {
+    auto finish = [&](int64_t gg, const double (&v)[12], const uint32_t (&wd)[4]) {
         const int64_t first = 4 * gg;
         const bool live = gg < groups;
         bool needy[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) needy[k] = live & (((wd[k] >> bit[k]) & 1u) != 0u);
+        for (int k = 0; k < 4; ++k) needy[k] = live & (wd[k] != 0u);
         unsigned long long bal[4];
         uint32_t total = 0;
 #pragma unroll
@@ -626,6 +688,8 @@ __global__ __launch_bounds__(kBlock) void k_states_bm(const WorldView* __restric
             bal[k] = __ballot(needy[k]);
             total += (uint32_t)__popcll(bal[k]);
         }
+        mark(4);
+        total_needy_dbg += total;
         uint32_t hits = 0;
         if (total > 0) {  // wave-uniform: queue the needy states, one lane per state
             uint32_t pos[4];
@@ -641,14 +705,16 @@ __global__ __launch_bounds__(kBlock) void k_states_bm(const WorldView* __restric
                     qu->xyz[pos[k]][0] = v[3 * k];
                     qu->xyz[pos[k]][1] = v[3 * k + 1];
                     qu->xyz[pos[k]][2] = v[3 * k + 2];
+                    qu->cls[pos[k]] = wd[k];
                 }
             wave_lds_sync();
             for (uint32_t e = lane; e < total; e += 64)  // rounds of 64 (almost always one)
                 qu->hit[e] = states_exact_hit<MINDIST>(wv, xbase, qu->xyz[e][0], qu->xyz[e][1], qu->xyz[e][2],
-                                                       can_pass, md)
+                                                       qu->cls[e], can_pass, md)
                                  ? 1
                                  : 0;
             wave_lds_sync();
+            mark(5);
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (needy[k] && qu->hit[pos[k]]) hits |= 1u << k;
@@ -677,7 +743,7 @@ __global__ __launch_bounds__(kBlock) void k_states_bm(const WorldView* __restric
     };
     int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     double va[12], vb[12];
-    uint32_t wd[4], bit[4];
+    uint32_t wd[4];
     if (groups > 0) load(g, va);
     if (tl) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -695,13 +761,13 @@ __global__ __launch_bounds__(kBlock) void k_states_bm(const WorldView* __restric
     mark(2);
     // block-uniform trip count: every lane runs every iteration (ballots, wave queue)
     for (int64_t g0 = (int64_t)blockIdx.x * kBlock; g0 < groups; g0 += 2 * stride, g += 2 * stride) {
-        words(va, wd, bit);
+        words(va, wd);
         load(g + stride, vb);
-        finish(g, va, wd, bit);
+        finish(g, va, wd);
         if (g0 + stride >= groups) break;
-        words(vb, wd, bit);
+        words(vb, wd);
         load(g + 2 * stride, va);
-        finish(g + stride, vb, wd, bit);
+        finish(g + stride, vb, wd);
     }
     mark(3);
     if (tl && lane == 0) {
@@ -709,17 +775,288 @@ __global__ __launch_bounds__(kBlock) void k_states_bm(const WorldView* __restric
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         unsigned xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        tl[gwave * 8 + 4] = hw;
-        tl[gwave * 8 + 5] = xcc;
+        tl[gwave * 8 + 6] = hw;
+        tl[gwave * 8 + 7] = xcc | ((unsigned long long)total_needy_dbg << 32);
     }
     if (blockIdx.x == 0 && threadIdx.x < (int)(n - 4 * groups)) {  // tail: the last n % 4 states
         const int64_t i = 4 * groups + threadIdx.x;
         const double px = xyz[3 * i], py = xyz[3 * i + 1], pz = xyz[3 * i + 2];
-        uint32_t b;
-        const uint32_t word = bp.bm[bm_word_index(bp, px, py, pz, b)];
-        const bool ok = !(((word >> b) & 1u) && states_exact_hit<MINDIST>(wv, xbase, px, py, pz, can_pass, md));
+        const uint32_t c = bp.cls[cls_index(bp, px, py, pz)];
+        const bool ok = !(c != 0u && states_exact_hit<MINDIST>(wv, xbase, px, py, pz, c, can_pass, md));
         valid[i] = ok ? 1 : 0;
         if (compact_idx && ok) compact_idx[atomicAdd(n_valid, 1ull)] = (int32_t)i;
+    }
+}
+
+// ---- k_states_v3: occupancy instead of software prefetch --------------------------
+// 512-thread workgroups, <= 64 VGPRs (8 waves per SIMD), two states per lane (48 B, three
+// 16-B loads) and no double buffer: at 1M states every wave of the chip holds exactly one
+// item and the latency chains (state load -> cell class -> LDS candidate tests) of 32
+// waves per CU overlap.  Same fast path / queue / exact path as k_states_bm.
+constexpr int kBlock3 = 512;
+constexpr int kQueue3 = 128;  // a wave's item: 64 lanes x 2 states
+struct StateQueue3 {
+    double xyz[kQueue3][3];
+    uint16_t cls[kQueue3];
+    uint8_t hit[kQueue3];
+};
+
+// COMPACT: also append the valid indices; TL: per-wave timeline (debug entry only)
+template <bool MINDIST, bool STAGE, bool COMPACT, bool TL>
+__global__ __launch_bounds__(kBlock3) void k_states_v3(const WorldView* __restrict__ wv,
+                                                          const double* __restrict__ xyz, int64_t n, int can_pass,
+                                                          double md, uint8_t* __restrict__ valid,
+                                                          int32_t* __restrict__ compact_idx,
+                                                          unsigned long long* __restrict__ n_valid,
+                                                          unsigned long long* __restrict__ tl, uint32_t stage_bytes) {
+    __shared__ StateQueue3 queues[kBlock3 / 64];
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_blob[];
+    const int lane = threadIdx.x & 63;
+    StateQueue3* qu = &queues[threadIdx.x >> 6];
+    const int gwave = (int)((blockIdx.x * kBlock3 + threadIdx.x) >> 6);
+    auto mark = [&](int k) {
+        if (TL) {
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            if (lane == 0) tl[gwave * 8 + k] = t;
+        }
+    };
+    mark(0);
+    BmParams bp;
+    bp.cls = (gptr_u16)(wv->blob + wv->off_bitmap);
+    bp.ox = wv->bofx; bp.oy = wv->bofy; bp.oz = wv->bofz;
+    bp.ix = wv->bix; bp.iy = wv->biy; bp.iz = wv->biz;
+    bp.nx = (uint32_t)wv->bnx; bp.ny = (uint32_t)wv->bny; bp.nz = (uint32_t)wv->bnz;
+    bp.sentinel = wv->bm_words;
+    const int64_t items = n / 2;  // pairs of states; an odd last state comes after the loop
+    const int64_t stride = (int64_t)gridDim.x * kBlock3;
+    int64_t it = (int64_t)blockIdx.x * kBlock3 + threadIdx.x;
+    double v[6];
+    auto load = [&](int64_t i) {
+        i = i < items ? i : items - 1;
+        const double2* q = reinterpret_cast<const double2*>(xyz + 6 * i);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const double2 t = q[k];
+            v[2 * k] = t.x;
+            v[2 * k + 1] = t.y;
+        }
+    };
+    if (items > 0) load(it);
+    // records + lists: [off_aos, off_bitmap) of the blob, staged into LDS
+    const uint32_t lists_off = wv->off_lists - wv->off_aos, ids_off = wv->off_ids - wv->off_aos;
+    const double rg = wv->r_gate, ro = wv->r_obst;
+    const unsigned char* xbase;
+    if (STAGE) {
+        const uint4* src = reinterpret_cast<const uint4*>(wv->blob + wv->off_aos);
+        uint4* dst = reinterpret_cast<uint4*>(lds_blob);
+        for (uint32_t o = threadIdx.x; o < stage_bytes / 16; o += kBlock3) dst[o] = src[o];
+        __syncthreads();
+        xbase = lds_blob;
+    } else {
+        xbase = wv->blob + wv->off_aos;
+    }
+    mark(2);
+    uint32_t total_needy_dbg = 0;
+    // block-uniform trip count: every lane runs every iteration (ballots, wave queue)
+    for (int64_t i0 = (int64_t)blockIdx.x * kBlock3; i0 < items; i0 += stride, it += stride) {
+        if (i0 != (int64_t)blockIdx.x * kBlock3) load(it);
+        const bool live = it < items;
+        const uint32_t c0 = bp.cls[cls_index(bp, v[0], v[1], v[2])];
+        const uint32_t c1 = bp.cls[cls_index(bp, v[3], v[4], v[5])];
+        const bool n0 = live & (c0 != 0u), n1 = live & (c1 != 0u);
+        const unsigned long long b0 = __ballot(n0), b1 = __ballot(n1);
+        const uint32_t t0 = (uint32_t)__popcll(b0), total = t0 + (uint32_t)__popcll(b1);
+        mark(4);
+        if (TL) total_needy_dbg += total;
+        uint32_t hits = 0;
+        if (total > 0) {  // wave-uniform
+            const uint32_t p0 = lanes_below(b0), p1 = t0 + lanes_below(b1);
+            if (n0) {
+                qu->xyz[p0][0] = v[0];
+                qu->xyz[p0][1] = v[1];
+                qu->xyz[p0][2] = v[2];
+                qu->cls[p0] = (uint16_t)c0;
+            }
+            if (n1) {
+                qu->xyz[p1][0] = v[3];
+                qu->xyz[p1][1] = v[4];
+                qu->xyz[p1][2] = v[5];
+                qu->cls[p1] = (uint16_t)c1;
+            }
+            wave_lds_sync();
+            for (uint32_t e = lane; e < total; e += 64)
+                qu->hit[e] = states_exact_rec<MINDIST>(xbase, lists_off, ids_off, rg, ro, qu->xyz[e][0], qu->xyz[e][1],
+                                                       qu->xyz[e][2], qu->cls[e], can_pass, md)
+                                 ? 1
+                                 : 0;
+            wave_lds_sync();
+            mark(5);
+            hits = (n0 && qu->hit[p0] ? 1u : 0u) | (n1 && qu->hit[p1] ? 2u : 0u);
+            wave_lds_sync();  // the queue is rewritten next
+        }
+        const uint32_t fl = live ? (~hits & 3u) : 0u;
+        if (live) *reinterpret_cast<uint16_t*>(valid + 2 * it) = (uint16_t)((fl & 1u) | ((fl & 2u) << 7));
+        if (COMPACT) {  // wave-ballot compaction
+            const uint32_t c = (uint32_t)__popc(fl);
+            uint32_t ctot;
+            const uint32_t cex = wave_excl_scan(c, lane, ctot);
+            unsigned long long wbase = 0;
+            if (lane == 0 && ctot) wbase = atomicAdd(n_valid, (unsigned long long)ctot);
+            wbase = __shfl(wbase, 0, 64);
+            uint64_t p = wbase + cex;
+            if (fl & 1u) compact_idx[p++] = (int32_t)(2 * it);
+            if (fl & 2u) compact_idx[p] = (int32_t)(2 * it + 1);
+        }
+    }
+    mark(3);
+    if (TL && lane == 0) {
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        unsigned xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        tl[gwave * 8 + 6] = hw;
+        tl[gwave * 8 + 7] = xcc | ((unsigned long long)total_needy_dbg << 32);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 1)) {  // odd last state
+        const int64_t i = n - 1;
+        const double px = xyz[3 * i], py = xyz[3 * i + 1], pz = xyz[3 * i + 2];
+        const uint32_t c = bp.cls[cls_index(bp, px, py, pz)];
+        const bool ok = !(c != 0u && states_exact_rec<MINDIST>(xbase, lists_off, ids_off, rg, ro, px, py, pz, c, can_pass, md));
+        valid[i] = ok ? 1 : 0;
+        if (COMPACT && ok) compact_idx[atomicAdd(n_valid, 1ull)] = (int32_t)i;
+    }
+}
+
+// ---- k_states_v4: workgroup-wide queue of the exact tests -------------------------
+// As k_states_v3 (512 threads, two states per lane, high occupancy), but the states on
+// occupied cells of the whole workgroup (~9% of 1024) are gathered into ONE LDS queue
+// and tested by the first ceil(T/64) waves only, so the exact path runs on full
+// wavefronts instead of ~10 active lanes in each of 8 waves.  Three barriers per item.
+constexpr int kBlock4 = 512;
+constexpr int kQueue4 = 2 * kBlock4;
+struct StateQueue4 {
+    double x[kQueue4], y[kQueue4], z[kQueue4];
+    uint16_t cls[kQueue4];
+    uint8_t hit[kQueue4];
+    uint32_t wcnt[kBlock4 / 64];
+};
+
+// Block-wide copy of `bytes` (16-byte multiple) HBM -> LDS with global (not flat) loads,
+// so waiting for the copy never waits on LDS traffic or vice versa.  No barrier.
+__device__ __forceinline__ void stage_copy(unsigned char* dst, const unsigned char* src, uint32_t bytes,
+                                           uint32_t nthreads) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(1))) uint4* gptr_u4;
+    const gptr_u4 s = (gptr_u4)src;
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    for (uint32_t o = threadIdx.x; o < bytes / 16; o += nthreads) d[o] = s[o];
+#endif
+}
+
+template <bool MINDIST, bool STAGE, bool COMPACT>
+__global__ __launch_bounds__(kBlock4) void k_states_v4(const WorldView* __restrict__ wv,
+                                                       const double* __restrict__ xyz, uint32_t items,
+                                                       int64_t n, int can_pass, double md,
+                                                       uint8_t* __restrict__ valid,
+                                                       int32_t* __restrict__ compact_idx,
+                                                       unsigned long long* __restrict__ n_valid,
+                                                       uint32_t stage_bytes) {
+    __shared__ StateQueue4 q;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_blob[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
+    BmParams bp;
+    bp.cls = (gptr_u16)(wv->blob + wv->off_bitmap);
+    bp.ox = wv->bofx; bp.oy = wv->bofy; bp.oz = wv->bofz;
+    bp.ix = wv->bix; bp.iy = wv->biy; bp.iz = wv->biz;
+    bp.nx = (uint32_t)wv->bnx; bp.ny = (uint32_t)wv->bny; bp.nz = (uint32_t)wv->bnz;
+    bp.sentinel = wv->bm_words;
+    const uint32_t stride = gridDim.x * kBlock4;
+    uint32_t it = blockIdx.x * kBlock4 + threadIdx.x;
+    double v[6];
+    auto load = [&](uint32_t i) {
+        i = i < items ? i : items - 1;
+        const double2* p = reinterpret_cast<const double2*>(xyz) + 3 * (size_t)i;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const double2 t = p[k];
+            v[2 * k] = t.x;
+            v[2 * k + 1] = t.y;
+        }
+    };
+    if (items > 0) load(it);
+    // records + lists: [off_aos, off_bitmap) of the blob, staged into LDS
+    const uint32_t lists_off = wv->off_lists - wv->off_aos, ids_off = wv->off_ids - wv->off_aos;
+    const double rg = wv->r_gate, ro = wv->r_obst;
+    const unsigned char* xbase;
+    if (STAGE) {
+        stage_copy(lds_blob, wv->blob + wv->off_aos, stage_bytes, kBlock4);
+        xbase = lds_blob;  // (the first barrier below orders the copy before any use)
+    } else {
+        xbase = wv->blob + wv->off_aos;
+    }
+    // block-uniform trip count: every thread runs every iteration (barriers)
+    for (uint32_t i0 = blockIdx.x * kBlock4; i0 < items; i0 += stride, it += stride) {
+        if (i0 != blockIdx.x * kBlock4) load(it);
+        const bool live = it < items;
+        const uint32_t c0 = bp.cls[cls_index(bp, v[0], v[1], v[2])];
+        const uint32_t c1 = bp.cls[cls_index(bp, v[3], v[4], v[5])];
+        const bool n0 = live & (c0 != 0u), n1 = live & (c1 != 0u);
+        const unsigned long long b0 = __ballot(n0), b1 = __ballot(n1);
+        const uint32_t t0 = (uint32_t)__popcll(b0), tw = t0 + (uint32_t)__popcll(b1);
+        if (lane == 0) q.wcnt[wave] = tw;
+        __syncthreads();
+        // wave offset and block total (scalar loops over the 8 counters: no per-wave masks)
+        uint32_t off = 0, T = 0;
+        for (int w = 0; w < wave; ++w) off += q.wcnt[w];
+        T = off;
+        for (int w = wave; w < kBlock4 / 64; ++w) T += q.wcnt[w];
+        uint32_t hits = 0;
+        if (T > 0) {  // block-uniform
+            const uint32_t p0 = off + lanes_below(b0), p1 = off + t0 + lanes_below(b1);
+            if (n0) {
+                q.x[p0] = v[0];
+                q.y[p0] = v[1];
+                q.z[p0] = v[2];
+                q.cls[p0] = (uint16_t)c0;
+            }
+            if (n1) {
+                q.x[p1] = v[3];
+                q.y[p1] = v[4];
+                q.z[p1] = v[5];
+                q.cls[p1] = (uint16_t)c1;
+            }
+            __syncthreads();
+            for (uint32_t e = threadIdx.x; e < T; e += kBlock4)  // only the first ceil(T/64) waves
+                q.hit[e] = states_exact_rec<MINDIST>(xbase, lists_off, ids_off, rg, ro, q.x[e], q.y[e], q.z[e], q.cls[e],
+                                                     can_pass, md)
+                               ? 1
+                               : 0;
+            __syncthreads();
+            hits = (n0 && q.hit[p0] ? 1u : 0u) | (n1 && q.hit[p1] ? 2u : 0u);
+        }
+        const uint32_t fl = live ? (~hits & 3u) : 0u;
+        if (live) *reinterpret_cast<uint16_t*>(valid + 2 * (size_t)it) = (uint16_t)((fl & 1u) | ((fl & 2u) << 7));
+        if (COMPACT) {  // wave-ballot compaction
+            const uint32_t c = (uint32_t)__popc(fl);
+            uint32_t ctot;
+            const uint32_t cex = wave_excl_scan(c, lane, ctot);
+            unsigned long long wbase = 0;
+            if (lane == 0 && ctot) wbase = atomicAdd(n_valid, (unsigned long long)ctot);
+            wbase = __shfl(wbase, 0, 64);
+            uint64_t p = wbase + cex;
+            if (fl & 1u) compact_idx[p++] = (int32_t)(2 * (size_t)it);
+            if (fl & 2u) compact_idx[p] = (int32_t)(2 * (size_t)it + 1);
+        }
+    }
+    if (STAGE && items == 0) __syncthreads();  // (no loop ran: nothing read the copy)
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 1)) {  // odd last state
+        const int64_t i = n - 1;
+        const double px = xyz[3 * i], py = xyz[3 * i + 1], pz = xyz[3 * i + 2];
+        const uint32_t c = bp.cls[cls_index(bp, px, py, pz)];
+        const bool ok = !(c != 0u && states_exact_rec<MINDIST>(xbase, lists_off, ids_off, rg, ro, px, py, pz, c, can_pass, md));
+        valid[i] = ok ? 1 : 0;
+        if (COMPACT && ok) compact_idx[atomicAdd(n_valid, 1ull)] = (int32_t)i;
     }
 }
 
@@ -793,13 +1130,19 @@ bool use_lds(const WorldView& w) {
     return w.blob_bytes <= kLdsBudget && !env_int("EPP_NO_LDS", 0) && !env_int("EPP_RAY_NO_LDS", 1);
 }
 
+// Opt a kernel in to more than 64 KB of dynamic LDS (static LDS counts against the same
+// 160 KB).  A failure here must not linger as the thread's last HIP error.
 template <typename K>
-void allow_lds(K kernel) {
-    static bool done = false;  // per process; same limit on every device
-    if (!done) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget);
-        done = true;
+void allow_lds(K kernel, uint32_t static_bytes = 0) {
+    // once per kernel and process (kernels of one signature share K, so key by address)
+    static std::mutex mu;
+    static std::set<const void*> done;
+    const void* f = reinterpret_cast<const void*>(kernel);
+    std::lock_guard<std::mutex> lk(mu);
+    if (done.insert(f).second) {
+        const int dyn = (int)std::min<uint32_t>(kLdsBudget, 160u * 1024u - static_bytes);
+        if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, dyn) != hipSuccess)
+            (void)hipGetLastError();
     }
 }
 
@@ -818,8 +1161,33 @@ epp_status launch_error(const char* what) {
 using namespace epp;
 
 namespace {
+bool v4_stage(const WorldView& w) {
+    return (w.off_bitmap - w.off_aos) + sizeof(StateQueue4) <= 160u * 1024u && !env_int("EPP_NO_LDS", 0);
+}
+// resident workgroups only (every block loops): LDS-, register- and env-limited per CU
+int v4_grid(const WorldView& w, int64_t n) {
+    const int64_t items = std::max<int64_t>(1, n / 2);
+    const int64_t need = (items + kBlock4 - 1) / kBlock4;
+    const uint32_t lds = sizeof(StateQueue4) + (v4_stage(w) ? w.off_bitmap - w.off_aos : 0u);
+    const int per_cu = std::max(1, std::min<int>(env_int("EPP_WG_PER_CU", 3), (int)((160u * 1024u) / lds)));
+    const int64_t cap = (int64_t)cu_count() * per_cu;
+    return (int)std::max<int64_t>(1, std::min(need, cap));
+}
+bool v3_stage(const WorldView& w) {
+    return (w.off_bitmap - w.off_aos) + (kBlock3 / 64) * sizeof(StateQueue3) <= 160u * 1024u &&
+           !env_int("EPP_NO_LDS", 0);
+}
+// all resident waves at once: up to 4 workgroups of 512 per CU (LDS permitting)
+int v3_grid(const WorldView& w, int64_t n) {
+    const int64_t items = std::max<int64_t>(1, n / 2);
+    const int64_t need = (items + kBlock3 - 1) / kBlock3;
+    const uint32_t lds = (kBlock3 / 64) * sizeof(StateQueue3) + (v3_stage(w) ? w.off_bitmap - w.off_aos : 0u);
+    const int per_cu = std::max(1, std::min<int>(env_int("EPP_WG_PER_CU", 4), (int)((160u * 1024u) / lds)));
+    const int64_t cap = (int64_t)cu_count() * per_cu;
+    return (int)std::max<int64_t>(1, std::min(need, cap));
+}
 bool bm_stage(const WorldView& w) {
-    return w.off_bitmap + (kBlock / 64) * sizeof(StateQueue) <= kLdsBudget && !env_int("EPP_NO_LDS", 0);
+    return w.off_bitmap + (kBlock / 64) * sizeof(StateQueue) <= 160u * 1024u && !env_int("EPP_NO_LDS", 0);
 }
 int bm_grid(const WorldView& w, int64_t groups) {
     const uint32_t queue_bytes = (kBlock / 64) * sizeof(StateQueue);
@@ -848,13 +1216,59 @@ epp_status launch_states(const WorldView& w, const WorldView* dw, const double* 
         hipLaunchKernelGGL((k_states<L, MINDIST, A>), dim3(grid), dim3(kBlock), shm, st, w, xyz, n,   \
                            can_pass, md, valid, compact_idx, nv, stage, tl);                          \
     } while (0)
-    if (env_int("EPP_STATES_IMPL", 1) == 1) {  // flat-bitmap kernel (default)
+    const int impl = env_int("EPP_STATES_IMPL", 4);
+    if (impl == 4 && (reinterpret_cast<uintptr_t>(xyz) & 15) == 0 && (reinterpret_cast<uintptr_t>(valid) & 1) == 0 &&
+        n / 2 < 0xFFFFFFFFll && !tl) {
+        const uint32_t sb = w.off_bitmap - w.off_aos;
+        const bool stg = v4_stage(w);
+        const int g4 = v4_grid(w, n);
+        const uint32_t items = (uint32_t)(n / 2);
+#define EPP_LAUNCH_V4(S, C)                                                                             \
+    do {                                                                                                \
+        allow_lds(k_states_v4<MINDIST, S, C>, sizeof(StateQueue4));                                     \
+        hipLaunchKernelGGL((k_states_v4<MINDIST, S, C>), dim3(g4), dim3(kBlock4), S ? sb : 0, st, dw, xyz, items, \
+                           n, can_pass, md, valid, compact_idx, nv, sb);                                \
+    } while (0)
+        if (compact_idx) {
+            if (stg) EPP_LAUNCH_V4(true, true);
+            else EPP_LAUNCH_V4(false, true);
+        } else {
+            if (stg) EPP_LAUNCH_V4(true, false);
+            else EPP_LAUNCH_V4(false, false);
+        }
+#undef EPP_LAUNCH_V4
+        return launch_error(MINDIST ? "epp_check_states_mindist" : "epp_check_states");
+    }
+    if ((impl == 3 || impl == 4) && (reinterpret_cast<uintptr_t>(xyz) & 15) == 0 && (reinterpret_cast<uintptr_t>(valid) & 1) == 0) {
+        const uint32_t sb = w.off_bitmap - w.off_aos;
+        const bool stg = v3_stage(w);
+        const int g3 = v3_grid(w, n);
+#define EPP_LAUNCH_V3(S, C, T)                                                                          \
+    do {                                                                                                \
+        allow_lds(k_states_v3<MINDIST, S, C, T>, sizeof(StateQueue3) * (kBlock3 / 64));                 \
+        hipLaunchKernelGGL((k_states_v3<MINDIST, S, C, T>), dim3(g3), dim3(kBlock3), S ? sb : 0, st, dw, xyz, \
+                           n, can_pass, md, valid, compact_idx, nv, tl, sb);                            \
+    } while (0)
+        if (tl) {
+            if (stg) EPP_LAUNCH_V3(true, false, true);
+            else EPP_LAUNCH_V3(false, false, true);
+        } else if (compact_idx) {
+            if (stg) EPP_LAUNCH_V3(true, true, false);
+            else EPP_LAUNCH_V3(false, true, false);
+        } else {
+            if (stg) EPP_LAUNCH_V3(true, false, false);
+            else EPP_LAUNCH_V3(false, false, false);
+        }
+#undef EPP_LAUNCH_V3
+        return launch_error(MINDIST ? "epp_check_states_mindist" : "epp_check_states");
+    }
+    if (impl != 0) {  // flat-bitmap kernel with prefetch (also the fallback for unaligned buffers)
         const uint32_t sb = w.off_bitmap;  // everything the exact path reads
         const bool stg = bm_stage(w);
         const int g2 = bm_grid(w, groups);
 #define EPP_LAUNCH_BM(A, S)                                                                            \
     do {                                                                                               \
-        allow_lds(k_states_bm<MINDIST, A, S>);                                                         \
+        allow_lds(k_states_bm<MINDIST, A, S>, (kBlock / 64) * sizeof(StateQueue));                    \
         hipLaunchKernelGGL((k_states_bm<MINDIST, A, S>), dim3(g2), dim3(kBlock), S ? sb : 0, st, dw, xyz, n, \
                            can_pass, md, valid, compact_idx, nv, tl, sb);                              \
     } while (0)
@@ -911,9 +1325,13 @@ epp_status epp_dbg_states_timeline(const epp_world* world, const double* xyz, in
     const bool lds = w.front_bytes + kScratchBytes <= kLdsBudget && !env_int("EPP_NO_LDS", 0);
     const uint32_t full_cap = (uint32_t)env_int("EPP_STAGE_FULL_MAX", 40 * 1024);
     const uint32_t stage = !lds ? 0u : (w.blob_bytes <= full_cap ? w.blob_bytes : w.front_bytes);
-    *grid_waves = (env_int("EPP_STATES_IMPL", 1) == 1 ? bm_grid(w, std::max<int64_t>(1, n / 4))
-                                                      : grid_for(std::max<int64_t>(1, n / 4), kScratchBytes + stage)) *
-                  (kBlock / 64);
+    const int impl = env_int("EPP_STATES_IMPL", 4);
+    if (impl == 3 || impl == 4)  // (the timeline runs k_states_v3 for impl 4 too)
+        *grid_waves = v3_grid(w, n) * (kBlock3 / 64);
+    else
+        *grid_waves = (impl == 1 ? bm_grid(w, std::max<int64_t>(1, n / 4))
+                                 : grid_for(std::max<int64_t>(1, n / 4), kScratchBytes + stage)) *
+                      (kBlock / 64);
     return launch_states<false>(w, world_dview(world), xyz, n, 0, 0.0, valid, nullptr, nullptr, stream, tl);
 }
 

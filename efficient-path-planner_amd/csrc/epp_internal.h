@@ -10,9 +10,13 @@
 //   uint32  meta[n_pad]          bit0 filling, bit1 gate, bits 8-15/16-23/24-31 = first
 //                                coarse cell (x, y, z) the OBB's AABB touches
 //   double  soa[EPP_NF][n_pad]   field-major OBB table (see enum below)
-//   uint32  bitmap[bm_words+1]   flat occupancy bitmap over the padded union box (one
-//                                bit per cell: some inflated AABB may contain a point of
-//                                it); the extra last word is 0 (out-of-range lookups)
+//   double  aos[n_obb][17]       the OBB table again as 136-byte records (exact path)
+//   uint32  hdr[n_lists]         candidate lists of the fine cells: start << 12 | count
+//   uint16  ids[...]             the lists' OBB ids
+//   -------------------------    (everything above: staged into LDS by k_states_bm)
+//   uint16  cls[ncells+1]        fine-cell class over the padded union box: 0 = outside
+//                                every inflated AABB, else list index; the extra last
+//                                entry is 0 (out-of-range lookups)
 //
 // n_pad rounds n_obbs up to a multiple of 4; every array starts 16-byte aligned.
 #pragma once
@@ -34,6 +38,13 @@ enum Field : int {
     F_HX, F_HY, F_HZ,                              // half sizes
     EPP_NF
 };
+
+// AoS OBB record of the fine-cell exact path: 17 doubles (136 B: consecutive records
+// fall in different LDS banks), fields in the order of enum Field, meta bits in the last.
+constexpr int kRecDoubles = 17;
+constexpr int R_META = 16;
+
+constexpr size_t kListMaxLen = 4095;  // OBBs per fine-cell list (12-bit count)
 
 constexpr uint32_t META_FILLING = 1u;
 constexpr uint32_t META_GATE = 2u;
@@ -60,9 +71,13 @@ struct WorldView {
     float limx, limy, limz;   // ~4n: fine coordinates beyond are outside every AABB
     float fmaxx, fmaxy, fmaxz; // 4 * n - 1: largest fine index
     double r_gate, r_obst;    // inflate radii (src/World.cpp:89-90)
-    // flat occupancy bitmap (k_states fast path)
-    uint32_t off_bitmap;
-    uint32_t bm_words;        // index of the zero sentinel word
+    // fine cell classes (k_states fast path)
+    uint32_t off_aos;         // OBB records (kRecDoubles each), then the lists
+    uint32_t off_lists;       // list headers (u32: start << 12 | count)
+    uint32_t off_ids;         // list OBB ids (u16)
+    uint32_t n_lists;
+    uint32_t off_bitmap;      // cls[] (u16 per fine cell)
+    uint32_t bm_words;        // index of the zero sentinel class
     int32_t bnx, bny, bnz;    // cells per axis
     float bofx, bofy, bofz;   // origin (float)
     float bix, biy, biz;      // 1 / cell size (float)

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <map>
 #include <cstring>
 #include <new>
 #include <string>
@@ -145,11 +146,18 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
                     mask[c] |= 1ull << (((z & 3) * 4 + (y & 3)) * 4 + (x & 3));
                 }
     }
-    // ---- flat occupancy bitmap (k_states fast path) ------------------------------
-    std::vector<uint32_t> bitmap;
-    {
-        const char* env = std::getenv("EPP_BITMAP_BITS");
-        const double target = env && *env ? std::max(64.0, std::atof(env)) : double(1 << 18);
+    // ---- fine cell classes (k_states fast path) ------------------------------------
+    // Per fine cell a u16 class: 0 = no inflated AABB reaches it (valid, no test), else
+    // 1 + index of the cell's candidate list (the OBBs whose AABB covers the cell; equal
+    // lists are shared).  A list of more than kListInline OBBs is stored as
+    // count = kListOverflow: such states take the coarse-grid candidate walk.
+    std::vector<uint16_t> cls;
+    std::vector<uint32_t> hdr;    // per list: start << 12 | count
+    std::vector<uint16_t> flat;   // the lists' OBB ids
+    const char* env_bits = std::getenv("EPP_BITMAP_BITS");
+    double setenv_target = env_bits && *env_bits ? std::max(64.0, std::atof(env_bits)) : double(1 << 16);
+    for (;;) {
+        const double target = setenv_target;
         int bd[3] = {1, 1, 1};
         float bo[3] = {0, 0, 0}, bi[3] = {1, 1, 1};
         if (n > 0) {
@@ -169,34 +177,64 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
                 // every AABB corner must map inside the grid (else widen and retry)
                 for (int i = 0; i < n && ok; ++i)
                     for (int k = 0; k < 3; ++k) {
-                        const int a = bm_axis(hw.aabbs[(size_t)i * 6 + k], bo[k], bi[k]);
-                        const int b = bm_axis(hw.aabbs[(size_t)i * 6 + 3 + k], bo[k], bi[k]);
-                        if (a < 0 || b >= bd[k]) ok = false;
+                        const int lo_i = bm_axis(hw.aabbs[(size_t)i * 6 + k], bo[k], bi[k]);
+                        const int hi_i = bm_axis(hw.aabbs[(size_t)i * 6 + 3 + k], bo[k], bi[k]);
+                        if (lo_i < 0 || hi_i >= bd[k]) ok = false;
                     }
                 if (ok) break;
                 if (pass > 8) h *= 1.1;
             }
         }
         const size_t cells = (size_t)bd[0] * bd[1] * bd[2];
-        const size_t words = (cells + 31) / 32;
-        bitmap.assign(words + 1, 0u);  // + zero sentinel
+        std::vector<std::vector<uint16_t>> sets(cells);
         for (int i = 0; i < n; ++i) {
-            int a[3], b[3];
+            int lo_i[3], hi_i[3];
             for (int k = 0; k < 3; ++k) {
-                a[k] = bm_axis(hw.aabbs[(size_t)i * 6 + k], bo[k], bi[k]);
-                b[k] = bm_axis(hw.aabbs[(size_t)i * 6 + 3 + k], bo[k], bi[k]);
+                lo_i[k] = bm_axis(hw.aabbs[(size_t)i * 6 + k], bo[k], bi[k]);
+                hi_i[k] = bm_axis(hw.aabbs[(size_t)i * 6 + 3 + k], bo[k], bi[k]);
             }
-            for (int z = a[2]; z <= b[2]; ++z)
-                for (int y = a[1]; y <= b[1]; ++y)
-                    for (int x = a[0]; x <= b[0]; ++x) {
-                        const size_t c = ((size_t)z * bd[1] + y) * bd[0] + x;
-                        bitmap[c >> 5] |= 1u << (c & 31);
-                    }
+            for (int z = lo_i[2]; z <= hi_i[2]; ++z)
+                for (int y = lo_i[1]; y <= hi_i[1]; ++y)
+                    for (int x = lo_i[0]; x <= hi_i[0]; ++x)
+                        sets[((size_t)z * bd[1] + y) * bd[0] + x].push_back((uint16_t)i);
+        }
+        cls.assign(cells + 1, 0);  // + the zero sentinel (out-of-grid lookups)
+        std::map<std::vector<uint16_t>, uint16_t> ids;
+        hdr.assign(1, 0u);  // list 0: unused (class 0 = free)
+        flat.clear();
+        bool full = false;
+        for (size_t c = 0; c < cells && !full; ++c) {
+            if (sets[c].empty()) continue;
+            auto it = ids.find(sets[c]);
+            if (it != ids.end()) {
+                cls[c] = it->second;
+                continue;
+            }
+            const size_t m = sets[c].size();
+            if (hdr.size() >= 65535 || flat.size() + m >= (size_t(1) << 20) || m > kListMaxLen) {
+                full = true;
+                break;
+            }
+            const uint16_t id = (uint16_t)hdr.size();
+            hdr.push_back((uint32_t)(flat.size() << 12) | (uint32_t)m);  // start : 20, count : 12
+            flat.insert(flat.end(), sets[c].begin(), sets[c].end());
+            ids.emplace(sets[c], id);
+            cls[c] = id;
+        }
+        if (full) {  // more distinct lists than a u16 class can name: a coarser grid
+            if (target <= 8.0) {
+                set_error("epp_world: candidate list table overflow");
+                return false;
+            }
+            setenv_target = target / 8;
+            continue;
         }
         v.bnx = bd[0]; v.bny = bd[1]; v.bnz = bd[2];
         v.bofx = bo[0]; v.bofy = bo[1]; v.bofz = bo[2];
         v.bix = bi[0]; v.biy = bi[1]; v.biz = bi[2];
-        v.bm_words = (uint32_t)words;
+        v.bm_words = (uint32_t)cells;  // index of the sentinel class
+        v.n_lists = (uint32_t)hdr.size();
+        break;
     }
     std::vector<uint32_t> cell_start(ncell + 1, 0);
     for (int c = 0; c < ncell; ++c) cell_start[c + 1] = cell_start[c] + (uint32_t)cells[c].size();
@@ -208,8 +246,21 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
     const size_t off_co = front;
     const size_t off_meta = align16(off_co + n_entries * 2);
     const size_t off_soa = align16(off_meta + meta.size() * 4);
-    const size_t off_bm = align16(off_soa + soa.size() * sizeof(double));
-    const size_t total = align16(off_bm + bitmap.size() * 4);
+    // AoS OBB records for the fine-cell exact path (kRecDoubles doubles each)
+    std::vector<double> aos((size_t)n * kRecDoubles, 0.0);
+    for (int i = 0; i < n; ++i) {
+        double* r = &aos[(size_t)i * kRecDoubles];
+        const double* f = soa.data();
+        const int fields[14] = {F_LOX, F_LOY, F_LOZ, F_HIX, F_HIY, F_HIZ, F_CX, F_CY, F_CZ, F_COS, F_SIN, F_HX, F_HY, F_HZ};
+        for (int k = 0; k < 14; ++k) r[k] = f[(size_t)fields[k] * n_pad + i];
+        uint64_t m = meta[i];
+        std::memcpy(&r[R_META], &m, 8);
+    }
+    const size_t off_aos = align16(off_soa + soa.size() * sizeof(double));
+    const size_t off_lists = align16(off_aos + aos.size() * sizeof(double));
+    const size_t off_ids = off_lists + hdr.size() * 4;
+    const size_t off_bm = align16(off_ids + flat.size() * 2);
+    const size_t total = align16(off_bm + cls.size() * 2);
     if (total > 0xFFFFFFFFull) {
         set_error("epp_world: index too large");
         return false;
@@ -225,7 +276,13 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
     }
     std::memcpy(b + off_meta, meta.data(), meta.size() * 4);
     std::memcpy(b + off_soa, soa.data(), soa.size() * sizeof(double));
-    std::memcpy(b + off_bm, bitmap.data(), bitmap.size() * 4);
+    if (!aos.empty()) std::memcpy(b + off_aos, aos.data(), aos.size() * sizeof(double));
+    std::memcpy(b + off_lists, hdr.data(), hdr.size() * 4);
+    if (!flat.empty()) std::memcpy(b + off_ids, flat.data(), flat.size() * 2);
+    v.off_ids = (uint32_t)off_ids;
+    v.off_aos = (uint32_t)off_aos;
+    std::memcpy(b + off_bm, cls.data(), cls.size() * 2);
+    v.off_lists = (uint32_t)off_lists;
     v.off_bitmap = (uint32_t)off_bm;
     v.blob_bytes = (uint32_t)total;
     v.front_bytes = (uint32_t)front;
@@ -338,3 +395,18 @@ namespace epp {
 const WorldView& world_view(const epp_world* w) { return w->view; }
 const WorldView* world_dview(const epp_world* w) { return w->d_view; }
 }  // namespace epp
+
+// Debug entry (not part of include/epp.h): sizes of the device index, for tests and
+// kernel tuning.  out: blob_bytes, staged prefix bytes, n_lists, fine cells, coarse
+// cells, n_obb.
+extern "C" epp_status epp_dbg_world_info(const epp_world* w, int64_t out[6]) {
+    if (!w || !out) return EPP_ERR_INVALID_ARGUMENT;
+    const epp::WorldView& v = w->view;
+    out[0] = v.blob_bytes;
+    out[1] = v.off_bitmap;
+    out[2] = v.n_lists;
+    out[3] = (int64_t)v.bnx * v.bny * v.bnz;
+    out[4] = (int64_t)v.nx * v.ny * v.nz;
+    out[5] = v.n_obb;
+    return EPP_OK;
+}

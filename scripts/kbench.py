@@ -79,23 +79,23 @@ def main():
         res[name] = {"us": ms * 1e3, "GBs": 25 * NB * N / (ms * 1e-3) / 1e9}
         print(name, res[name], flush=True)
 
-    for impl in (0, 1):
+    for impl in (0, 1, 3, 4):
         e = {"EPP_STATES_IMPL": impl}
         run(f"c2_impl{impl}", w2, d, e)
         big(f"c2_impl{impl}_16M", w2, e)
-        run(f"c2_impl{impl}_above_union_box", w2, dz, e)
         run(f"c2_impl{impl}_empty_world", w0, d, e)
-    run("c2_impl1_nolds", w2, d, {"EPP_NO_LDS": 1})
-    big("c2_impl1_nolds_16M", w2, {"EPP_NO_LDS": 1})
-    for k in (2, 4, 6, 8):
-        run(f"c2_impl1_wg_per_cu_{k}", w2, d, {"EPP_WG_PER_CU": k})
-        big(f"c2_impl1_wg_per_cu_{k}_16M", w2, {"EPP_WG_PER_CU": k})
-    for bits in (1 << 14, 1 << 16, 1 << 20, 1 << 22):
+    for impl in (3, 4):
+        for k in (2, 3, 4):
+            e = {"EPP_STATES_IMPL": impl, "EPP_WG_PER_CU": k}
+            run(f"c2_impl{impl}_wg_per_cu_{k}", w2, d, e)
+            big(f"c2_impl{impl}_wg_per_cu_{k}_16M", w2, e)
+    for bits in (1 << 14, 1 << 17):
         os.environ["EPP_BITMAP_BITS"] = str(bits)
         wb = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
         del os.environ["EPP_BITMAP_BITS"]
-        run(f"c2_impl1_bitmap_{bits}", wb, d)
-        big(f"c2_impl1_bitmap_{bits}_16M", wb)
+        for impl in (3, 4):
+            run(f"c2_impl{impl}_cells_{bits}", wb, d, {"EPP_STATES_IMPL": impl})
+            big(f"c2_impl{impl}_cells_{bits}_16M", wb, {"EPP_STATES_IMPL": impl})
         wb.close()
     # motions, C3
     g3, o3 = synth.track_world(42, n_obstacles=472)

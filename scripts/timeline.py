@@ -38,9 +38,15 @@ for n in (1 << 20, 1 << 24):
     us = lambda x: x * 0.01  # noqa: E731  (100 MHz ticks)
     ph = {"entry": us(t[:, 0] - t0), "data": us(t[:, 1] - t[:, 0]), "stage": us(t[:, 2] - t[:, 1]),
           "groups": us(t[:, 3] - t[:, 2]), "end": us(t[:, 3] - t0)}
+    if n == 1 << 20:  # one group per wave: its sub-phases (bitmap words, exact path)
+        has = t[:, 5] > 0
+        ph["words"] = us(t[:, 4] - t[:, 2])
+        ph["exact"] = us(t[has, 5] - t[has, 4])
+        ph["after_exact"] = us(t[has, 3] - t[has, 5])
+        ph["needy_per_wave"] = (t[:, 7] >> 32).astype(np.float64)
     out = {k: {p: float(np.percentile(v, p)) for p in (0, 10, 50, 90, 100)} for k, v in ph.items()}
     out["waves"] = int(gw.value)
-    xcc = t[:, 5]
+    xcc = t[:, 7] & 0xFFFFFFFF
     out["end_by_xcc_max"] = {int(x): float(us(t[xcc == x, 3] - t0).max()) for x in np.unique(xcc)}
     res[str(n)] = out
     print(n, json.dumps(out, indent=None))
