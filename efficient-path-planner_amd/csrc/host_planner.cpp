@@ -88,15 +88,17 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     const int32_t n = (int32_t)(nodes.size() / 3);
     // ---- 2. k-NN graph + batched motion checks (MotionValidator::checkMotion) --------
     const size_t m = (size_t)n * k;
+    const size_t ws_bytes = (size_t)epp_knn_workspace_size(n);
     ts.reset(ThreadScratch::rounded((size_t)n * 24) + ThreadScratch::rounded(m * 4) +
-             2 * ThreadScratch::rounded(m * 24) + ThreadScratch::rounded(m));
+             2 * ThreadScratch::rounded(m * 24) + ThreadScratch::rounded(m) + ThreadScratch::rounded(ws_bytes));
     double* d_nodes = static_cast<double*>(ts.carve((size_t)n * 24));
     int32_t* d_nbr = static_cast<int32_t*>(ts.carve(m * 4));
     double* d_e1 = static_cast<double*>(ts.carve(m * 24));
     double* d_e2 = static_cast<double*>(ts.carve(m * 24));
     uint8_t* d_ev = static_cast<uint8_t*>(ts.carve(m));
+    void* d_ws = ts.carve(ws_bytes);
     check(epp_memcpy_h2d(d_nodes, nodes.data(), (uint64_t)n * 24, st), "upload");
-    check(epp_knn(d_nodes, n, k, 0.0, d_nbr, st), "knn");
+    check(epp_knn_ws(d_nodes, n, k, 0.0, d_nbr, d_ws, ws_bytes, st), "knn");
     check(epp_knn_edges(d_nodes, d_nbr, n, k, d_e1, d_e2, st), "edges");
     check(epp_check_motions(w, d_e1, d_e2, (int64_t)m, canPass ? 1 : 0, 0, d_ev, st), "motion check");
     std::vector<int32_t> nbr(m);

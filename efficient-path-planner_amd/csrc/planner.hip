@@ -10,6 +10,8 @@
 // (collision.hip); the host runs the shortest-path search over the valid edges.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <mutex>
 #include <string>
 
 #include "epp_internal.h"
@@ -322,6 +324,67 @@ __global__ void k_knn_edges(const double* __restrict__ nodes, const int32_t* __r
     }
 }
 
+// Scratch of the grid k-NN, every part 256-byte aligned: grid params | cell_of[n] |
+// sidx[n] | sxyz[3n] | cnt[cap+1] | fill[cap+1] | start[cap+1]   (cap = max(64, n))
+struct KnnLayout {
+    size_t cell, sidx, sxyz, cnt, start, fill, bytes;
+    int cap;
+};
+KnnLayout knn_layout(int n) {
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    KnnLayout L;
+    L.cap = max(64, n);
+    L.cell = 256;
+    L.sidx = L.cell + al((size_t)n * 4);
+    L.sxyz = L.sidx + al((size_t)n * 4);
+    L.cnt = L.sxyz + al((size_t)n * 24);
+    L.fill = L.cnt + al((size_t)(L.cap + 1) * 4);
+    L.start = L.fill + al((size_t)(L.cap + 1) * 4);
+    L.bytes = L.start + al((size_t)(L.cap + 1) * 4);
+    return L;
+}
+
+epp_status last(const char* what);
+
+epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, int32_t* nbr, char* buf,
+                           const KnnLayout& L, hipStream_t s) {
+    KnnGrid* g = reinterpret_cast<KnnGrid*>(buf);
+    int* cell_of = reinterpret_cast<int*>(buf + L.cell);
+    int* sidx = reinterpret_cast<int*>(buf + L.sidx);
+    double* sxyz = reinterpret_cast<double*>(buf + L.sxyz);
+    int* cnt = reinterpret_cast<int*>(buf + L.cnt);
+    int* start = reinterpret_cast<int*>(buf + L.start);
+    int* fill = reinterpret_cast<int*>(buf + L.fill);
+    // cnt and fill are adjacent: one clear (never launch the scatter on stale counters)
+    const hipError_t e = hipMemsetAsync(cnt, 0, L.start - L.cnt, s);
+    if (e != hipSuccess) {
+        set_error(std::string("epp_knn_grid: hipMemsetAsync: ") + hipGetErrorString(e));
+        return EPP_ERR_HIP;
+    }
+    const double r2 = max_dist > 0 ? max_dist * max_dist : 1e300;
+    const dim3 g256((n + 255) / 256), b256(256);
+    hipLaunchKernelGGL(k_knn_bounds, dim3(1), dim3(kBoundsThreads), 0, s, nodes, n, L.cap, g);
+    hipLaunchKernelGGL(k_knn_count, g256, b256, 0, s, nodes, n, g, cell_of, cnt);
+    hipLaunchKernelGGL(k_knn_scan, dim3(1), dim3(kBoundsThreads), 0, s, g, cnt, start);
+    hipLaunchKernelGGL(k_knn_scatter, g256, b256, 0, s, nodes, n, cell_of, start, fill, sxyz, sidx);
+    switch (k) {
+        case 4: hipLaunchKernelGGL(k_knn_grid<4>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
+        case 8: hipLaunchKernelGGL(k_knn_grid<8>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
+        case 16: hipLaunchKernelGGL(k_knn_grid<16>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
+        default: hipLaunchKernelGGL(k_knn_grid<32>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
+    }
+    return last("epp_knn_grid");
+}
+
+struct CachedWs {
+    std::mutex mu;
+    void* buf = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+    bool used = false;
+};
+CachedWs g_knn_ws[64];
+
 epp_status last(const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -371,58 +434,68 @@ epp_status epp_knn_bruteforce(const double* nodes, int32_t n, int32_t k, double 
 
 epp_status epp_knn(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr, void* stream) {
     // the grid pays off from a few thousand nodes; both give the same answer
-    return n <= 2048 ? epp_knn_bruteforce(nodes, n, k, max_dist, nbr, stream)
-                     : epp_knn_grid(nodes, n, k, max_dist, nbr, stream);
+    // (EPP_KNN_IMPL=1 / 2 forces all-pairs / grid: diagnostics)
+    const char* f = std::getenv("EPP_KNN_IMPL");
+    const int impl = f && *f ? std::atoi(f) : 0;
+    const bool brute = impl == 1 || (impl == 0 && n <= 2048);
+    return brute ? epp_knn_bruteforce(nodes, n, k, max_dist, nbr, stream)
+                 : epp_knn_grid(nodes, n, k, max_dist, nbr, stream);
 }
 
+uint64_t epp_knn_workspace_size(int32_t n) { return n <= 0 ? 0 : (uint64_t)knn_layout(n).bytes; }
+
+epp_status epp_knn_ws(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr, void* ws,
+                      uint64_t ws_bytes, void* stream) {
+    if (n > 2048) return epp_knn_grid_ws(nodes, n, k, max_dist, nbr, ws, ws_bytes, stream);
+    return epp_knn_bruteforce(nodes, n, k, max_dist, nbr, stream);
+}
+
+epp_status epp_knn_grid_ws(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr, void* ws,
+                           uint64_t ws_bytes, void* stream) {
+    if (n < 0 || (n > 0 && (!nodes || !nbr)) || (k != 4 && k != 8 && k != 16 && k != 32)) {
+        set_error("epp_knn_grid: invalid argument (k must be 4, 8, 16 or 32)");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    if (n == 0) return EPP_OK;
+    const KnnLayout L = knn_layout(n);
+    if (!ws || ws_bytes < L.bytes || (reinterpret_cast<uintptr_t>(ws) & 255)) {
+        set_error("epp_knn_grid: workspace missing, unaligned or smaller than epp_knn_workspace_size(n)");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    return knn_grid_launch(nodes, n, k, max_dist, nbr, static_cast<char*>(ws), L, (hipStream_t)stream);
+}
+
+// Without a caller workspace: one cached workspace per device.  Reuse is ordered on the
+// GPU (the next user's stream waits for the previous user's completion event), growth
+// frees the old buffer only after the device drained it (hipFree synchronises).
 epp_status epp_knn_grid(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr, void* stream) {
     if (n < 0 || (n > 0 && (!nodes || !nbr)) || (k != 4 && k != 8 && k != 16 && k != 32)) {
         set_error("epp_knn_grid: invalid argument (k must be 4, 8, 16 or 32)");
         return EPP_ERR_INVALID_ARGUMENT;
     }
     if (n == 0) return EPP_OK;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    CachedWs& c = g_knn_ws[dev & 63];
+    std::lock_guard<std::mutex> lk(c.mu);
     hipStream_t s = (hipStream_t)stream;
-    const int cap = max(64, n);
-    // scratch layout, every part 256-byte aligned: grid params | cell_of[n] | sidx[n] |
-    // sxyz[3n] | cnt[cap+1] | start[cap+1] | fill[cap+1]
-    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
-    const size_t o_cell = 256, o_sidx = o_cell + al((size_t)n * 4), o_sxyz = o_sidx + al((size_t)n * 4),
-                 o_cnt = o_sxyz + al((size_t)n * 24), o_start = o_cnt + al((size_t)(cap + 1) * 4),
-                 o_fill = o_start + al((size_t)(cap + 1) * 4), bytes = o_fill + al((size_t)(cap + 1) * 4);
-    char* buf = nullptr;
-    hipError_t e = hipMallocAsync((void**)&buf, bytes, s);
+    const KnnLayout L = knn_layout(n);
+    hipError_t e = hipSuccess;
+    if (!c.done) e = hipEventCreateWithFlags(&c.done, hipEventDisableTiming);
+    if (e == hipSuccess && c.used) e = hipStreamWaitEvent(s, c.done, 0);
+    if (e == hipSuccess && L.bytes > c.cap) {
+        if (c.buf) e = hipFree(c.buf);
+        c.buf = nullptr;
+        c.cap = 0;
+        if (e == hipSuccess) e = hipMalloc(&c.buf, L.bytes);
+        if (e == hipSuccess) c.cap = L.bytes;
+    }
     if (e != hipSuccess) {
-        set_error(std::string("epp_knn_grid: hipMallocAsync: ") + hipGetErrorString(e));
+        set_error(std::string("epp_knn_grid: workspace: ") + hipGetErrorString(e));
         return EPP_ERR_HIP;
     }
-    KnnGrid* g = reinterpret_cast<KnnGrid*>(buf);
-    int* cell_of = reinterpret_cast<int*>(buf + o_cell);
-    int* sidx = reinterpret_cast<int*>(buf + o_sidx);
-    double* sxyz = reinterpret_cast<double*>(buf + o_sxyz);
-    int* cnt = reinterpret_cast<int*>(buf + o_cnt);
-    int* start = reinterpret_cast<int*>(buf + o_start);
-    int* fill = reinterpret_cast<int*>(buf + o_fill);
-    e = hipMemsetAsync(cnt, 0, (size_t)(cap + 1) * 4, s);
-    if (e == hipSuccess) e = hipMemsetAsync(fill, 0, (size_t)(cap + 1) * 4, s);
-    if (e != hipSuccess) {  // never launch the scatter on counters that were not cleared
-        set_error(std::string("epp_knn_grid: hipMemsetAsync: ") + hipGetErrorString(e));
-        (void)hipFreeAsync(buf, s);
-        return EPP_ERR_HIP;
-    }
-    const double r2 = max_dist > 0 ? max_dist * max_dist : 1e300;
-    const dim3 g256((n + 255) / 256), b256(256);
-    hipLaunchKernelGGL(k_knn_bounds, dim3(1), dim3(kBoundsThreads), 0, s, nodes, n, cap, g);
-    hipLaunchKernelGGL(k_knn_count, g256, b256, 0, s, nodes, n, g, cell_of, cnt);
-    hipLaunchKernelGGL(k_knn_scan, dim3(1), dim3(kBoundsThreads), 0, s, g, cnt, start);
-    hipLaunchKernelGGL(k_knn_scatter, g256, b256, 0, s, nodes, n, cell_of, start, fill, sxyz, sidx);
-    switch (k) {
-        case 4: hipLaunchKernelGGL(k_knn_grid<4>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
-        case 8: hipLaunchKernelGGL(k_knn_grid<8>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
-        case 16: hipLaunchKernelGGL(k_knn_grid<16>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
-        default: hipLaunchKernelGGL(k_knn_grid<32>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
-    }
-    const epp_status rc = last("epp_knn_grid");
-    (void)hipFreeAsync(buf, s);
+    const epp_status rc = knn_grid_launch(nodes, n, k, max_dist, nbr, static_cast<char*>(c.buf), L, s);
+    if (hipEventRecord(c.done, s) == hipSuccess) c.used = true;
     return rc;
 }
 

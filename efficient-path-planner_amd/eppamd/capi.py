@@ -76,6 +76,9 @@ def lib() -> C.CDLL:
             "epp_knn": (i32, [vp, i32, i32, dp, vp, vp]),
             "epp_knn_bruteforce": (i32, [vp, i32, i32, dp, vp, vp]),
             "epp_knn_grid": (i32, [vp, i32, i32, dp, vp, vp]),
+            "epp_knn_workspace_size": (C.c_uint64, [i32]),
+            "epp_knn_ws": (i32, [vp, i32, i32, dp, vp, vp, C.c_uint64, vp]),
+            "epp_knn_grid_ws": (i32, [vp, i32, i32, dp, vp, vp, C.c_uint64, vp]),
             "epp_knn_edges": (i32, [vp, vp, i32, i32, vp, vp, vp]),
         }
         for name, (res, args) in sig.items():
@@ -95,7 +98,8 @@ EXPORTED = [
     "epp_world_destroy", "epp_world_num_obbs", "epp_world_get_aabbs", "epp_check_states",
     "epp_check_states_mindist", "epp_check_motions", "epp_minsnap_batch", "epp_sample_count",
     "epp_sample_batch", "epp_generate_trajectory_host", "epp_host_free", "epp_sample_uniform", "epp_knn",
-    "epp_knn_bruteforce", "epp_knn_grid", "epp_knn_edges",
+    "epp_knn_bruteforce", "epp_knn_grid", "epp_knn_workspace_size", "epp_knn_ws", "epp_knn_grid_ws",
+    "epp_knn_edges",
 ]
 
 
@@ -314,8 +318,13 @@ def knn(nodes: np.ndarray, k: int, max_dist: float = 0.0, method: str = "auto") 
     n = len(nodes)
     d_n = DeviceBuffer.from_array(nodes)
     d_k = DeviceBuffer(4 * max(n * k, 1))
-    fn = {"auto": lib().epp_knn, "brute": lib().epp_knn_bruteforce, "grid": lib().epp_knn_grid}[method]
-    check(fn(d_n.ptr, n, int(k), float(max_dist), d_k.ptr, None))
+    if method in ("ws", "grid_ws"):  # caller workspace variants
+        d_w = DeviceBuffer(max(int(lib().epp_knn_workspace_size(n)), 256))
+        fn = lib().epp_knn_ws if method == "ws" else lib().epp_knn_grid_ws
+        check(fn(d_n.ptr, n, int(k), float(max_dist), d_k.ptr, d_w.ptr, d_w.nbytes, None))
+    else:
+        fn = {"auto": lib().epp_knn, "brute": lib().epp_knn_bruteforce, "grid": lib().epp_knn_grid}[method]
+        check(fn(d_n.ptr, n, int(k), float(max_dist), d_k.ptr, None))
     sync()
     return d_k.download(np.int32, n * k).reshape(n, k)
 

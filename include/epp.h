@@ -156,10 +156,19 @@ epp_status epp_sample_uniform(uint64_t seed, const double lo[3], const double hi
  * limit), sorted by distance, ties to the lower index; missing entries are -1. */
 epp_status epp_knn(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr, void* stream);
 /* The two strategies behind epp_knn (same answers): all-pairs with LDS tiles, and a
- * uniform grid walked in shells (stream-ordered scratch from hipMallocAsync). */
+ * uniform grid walked in shells. */
 epp_status epp_knn_bruteforce(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr,
                               void* stream);
 epp_status epp_knn_grid(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr, void* stream);
+/* Caller-workspace variants (no allocation, no cross-stream ordering inside): `ws` is a
+ * 256-byte aligned device buffer of at least epp_knn_workspace_size(n) bytes that no
+ * other stream touches until this call's kernels completed.  epp_knn / epp_knn_grid
+ * use a cached per-device workspace whose reuse is ordered by a completion event. */
+uint64_t epp_knn_workspace_size(int32_t n);
+epp_status epp_knn_ws(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr, void* ws,
+                      uint64_t ws_bytes, void* stream);
+epp_status epp_knn_grid_ws(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr, void* ws,
+                           uint64_t ws_bytes, void* stream);
 /* Edge endpoints for every (node i, neighbour c): s1 = nodes[i], s2 = nodes[nbr[i k + c]]
  * (s2 = s1 for a missing neighbour).  s1, s2: n k x 3. */
 epp_status epp_knn_edges(const double* nodes, const int32_t* nbr, int32_t n, int32_t k, double* s1,

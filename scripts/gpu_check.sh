@@ -13,7 +13,7 @@ stop_on_fault() {  # $1 = exit code, $2 = step name
   esac
 }
 echo "== pytest -m gpu"
-timeout -k 10 900 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 tail -5 gpurun_out/pytest_gpu.log; stop_on_fault $rc pytest
 echo "== smoke"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?

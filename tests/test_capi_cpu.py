@@ -62,3 +62,13 @@ def test_build_obbs_errors(geom):
     a = capi.build_obbs(geom, [[1, 2, 3.0, 0, 0, 0.3, 1]], [[0, 0, -0.5, 0, 0, 0]])
     b = capi.build_obbs(geom, [[1, 2, 0.0, 0, 0, 0.3, 1]], [[0, 0, -0.5, 0, 0, 0]])
     assert np.array_equal(a, b)
+
+
+def test_knn_workspace_size_host_only():
+    """epp_knn_workspace_size is host arithmetic (no GPU): 0 for n <= 0, grows with n,
+    256-byte granular."""
+    L = capi.lib()
+    assert L.epp_knn_workspace_size(0) == 0
+    a, b = L.epp_knn_workspace_size(3000), L.epp_knn_workspace_size(65538)
+    assert 0 < a < b and a % 256 == 0 and b % 256 == 0
+    assert b >= 65538 * (4 + 4 + 24 + 3 * 4)

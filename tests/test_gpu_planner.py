@@ -89,6 +89,31 @@ def test_knn_grid_large(k):
     assert np.array_equal(got, capi.knn(nodes, k, method="brute"))
     assert np.array_equal(got, _knn_ref(nodes, k))
     assert np.array_equal(capi.knn(nodes, k), got)                   # auto -> grid
+    assert np.array_equal(capi.knn(nodes, k, method="ws"), got)      # caller workspace
+    assert np.array_equal(capi.knn(nodes, k, method="grid_ws"), got)
+
+
+def test_knn_grid_back_to_back_streams():
+    """Cached-workspace reuse is ordered on the GPU: grid k-NN launched on two streams and
+    repeatedly without host syncs in between gives the synchronous answer every time."""
+    import ctypes as C
+    L = capi.lib()
+    nodes = synth.sample_states(77, [-6, -6, 0], [6, 6, 2], 60000)
+    ref = capi.knn(nodes, 16, method="grid")
+    d_n = capi.DeviceBuffer.from_array(nodes)
+    outs = [capi.DeviceBuffer(4 * 16 * len(nodes)) for _ in range(4)]
+    sts = []
+    for _ in range(2):
+        s = C.c_void_p()
+        capi.check(L.epp_stream_create(C.byref(s)))
+        sts.append(s.value)
+    for r, o in enumerate(outs):
+        capi.check(L.epp_knn_grid(d_n.ptr, len(nodes), 16, 0.0, o.ptr, sts[r % 2]))
+    for s in sts:
+        capi.check(L.epp_stream_sync(s))
+        capi.check(L.epp_stream_destroy(s))
+    for o in outs:
+        assert np.array_equal(o.download(np.int32, 16 * len(nodes)).reshape(-1, 16), ref)
 
 
 def test_knn_grid_flat_and_radius():
