@@ -575,34 +575,33 @@ __device__ __forceinline__ bool states_exact_hit(const WorldView* wvp, const uns
     return false;
 }
 
-// Same predicate as pair_hit_r on one AoS record (rec: kRecDoubles doubles).
+// Same predicate as pair_hit_r on one AoS record (rec: kRecDoubles doubles), written
+// branch-free: all fields are read up front (one LDS round trip instead of a
+// short-circuit chain of dependent read -> compare -> branch steps) and the outcome is
+// a conjunction of the same fp64 comparisons, so the booleans are unchanged.
 template <bool MINDIST>
 __device__ __forceinline__ bool rec_hit(const double* rec, double rg, double ro, double px, double py, double pz,
                                         bool can_pass, double md) {
-    if (!(rec[F_LOX] < px && px < rec[F_HIX] && rec[F_LOY] < py && py < rec[F_HIY] && rec[F_LOZ] < pz &&
-          pz < rec[F_HIZ]))
-        return false;  // rtree contains(point): strict  src/World.cpp:83
-    const uint32_t m = (uint32_t)__double_as_longlong(rec[R_META]);
-    double r;
-    if (MINDIST) {
-        if (m & META_FILLING) return false;  // :116-118
-        r = md;
-    } else {
-        if ((m & META_FILLING) && can_pass) return false;  // :92-95
-        r = (m & META_GATE) ? rg : ro;                     // :89-90
-    }
+    double f[kRecDoubles];
+#pragma unroll
+    for (int k = 0; k <= F_HZ; ++k) f[k] = rec[k];
+    f[R_META] = rec[R_META];  // (the two padding doubles are not read)
+    const uint32_t m = (uint32_t)__double_as_longlong(f[R_META]);
+    // rtree contains(point): strict  src/World.cpp:83
+    const bool in = (f[F_LOX] < px) & (px < f[F_HIX]) & (f[F_LOY] < py) & (py < f[F_HIY]) & (f[F_LOZ] < pz) &
+                    (pz < f[F_HIZ]);
+    const bool fill = (m & META_FILLING) != 0u;
+    // MINDIST skips every filling OBB (:116-118), else only with canPassGate (:92-95)
+    const bool skip = MINDIST ? fill : (fill & can_pass);
+    const double r = MINDIST ? md : ((m & META_GATE) ? rg : ro);  // :89-90
     // OBB::checkCollisionWithPoint — src/OBB.cpp:63-91 (same evaluation as obb_point_hit)
-    const double c = rec[F_COS], s = rec[F_SIN];
-    const double dx = px - rec[F_CX], dy = py - rec[F_CY], dz = pz - rec[F_CZ];
+    const double c = f[F_COS], s = f[F_SIN];
+    const double dx = px - f[F_CX], dy = py - f[F_CY], dz = pz - f[F_CZ];
     const double lx = c * dx + s * dy;
     const double ly = c * dy - s * dx;
-    double tx = rec[F_HX], ty = rec[F_HY], tz = rec[F_HZ];
-    if (!(m & META_FILLING)) {
-        tx = tx + r;
-        ty = ty + r;
-        tz = tz + r;
-    }
-    return fabs(lx) <= tx && fabs(ly) <= ty && fabs(dz) <= tz;
+    const double ix = f[F_HX] + r, iy = f[F_HY] + r, iz = f[F_HZ] + r;  // shouldBeInflated()
+    const double tx = fill ? f[F_HX] : ix, ty = fill ? f[F_HY] : iy, tz = fill ? f[F_HZ] : iz;
+    return in & !skip & (fabs(lx) <= tx) & (fabs(ly) <= ty) & (fabs(dz) <= tz);
 }
 
 // Exact test on the AoS records + the cell's candidate list (no early exit: the lists
@@ -1060,6 +1059,230 @@ __global__ __launch_bounds__(kBlock4) void k_states_v4(const WorldView* __restri
     }
 }
 
+// ---- k_states_v5: the whole decision runs out of LDS ------------------------------
+// Persistent workgroups (one per CU), four states per lane (96 B = six 16-B loads),
+// the next group prefetched while the current one is classified.  The world's
+// records, candidate lists and fine-cell class table are staged into LDS once per
+// workgroup while the first group's HBM loads are in flight.  Per state: class lookup
+// (LDS, ~15 VALU: the class grid's empty margin cells make a clamp do the bounds test)
+// -> ballot; a group with needy states queues them in the wave's LDS queue and, in the
+// common case (<= 64 needy states and <= 64 candidate pairs), tests each (state,
+// candidate) pair on its own lane with the hits returned by one ballot; otherwise each
+// queued state walks its own list.  One 32-bit store writes a lane's four flags.
+// The per-state VALU count matters: at 1M states/launch the kernel's critical path is
+// the last-arriving data plus the VALU work behind it (PMC: SQ_INSTS_VALU).
+constexpr int kBlock5 = 1024;  // threads per workgroup (BLOCK template default)
+struct WaveQueue5 {
+    double x[64], y[64], z[64];
+    uint32_t pair[64];  // queue slot << 20 | index into the list ids
+    uint16_t cls[64];
+    uint8_t hit[64];
+};
+template <int BLOCK>
+constexpr uint32_t queue5_bytes() { return (BLOCK / 64) * sizeof(WaveQueue5); }
+
+// hardware f32 -> i32 conversion (NaN -> 0, saturating), then clamp to [0, n-1]
+__device__ __forceinline__ uint32_t cell_axis5(double p, float off, float inv, uint32_t nm1) {
+    const float f = fmaf((float)p, inv, off);
+    int i;
+    asm("v_cvt_i32_f32 %0, %1" : "=v"(i) : "v"(f));
+    return min((uint32_t)i, nm1);  // negative -> huge -> last (empty) cell
+}
+
+// TL: per-wave timeline (debug entry only; 8 u64 per wave: entry, data + staging
+// arrived, -, end, first group classified, first group's exact path done, HW_ID,
+// XCC_ID | needy states << 32)
+// PREFETCH: groups per lane > 1 (the next group's loads overlap this one's work);
+// single-pass launches (e.g. 1M states on 256 CUs) drop the second buffer's registers.
+template <bool MINDIST, bool COMPACT, bool TL, int BLOCK, bool PREFETCH>
+__global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict__ wv,
+                                                     const double* __restrict__ xyz, int64_t groups, int64_t n,
+                                                     int can_pass, double md, uint8_t* __restrict__ valid,
+                                                     int32_t* __restrict__ compact_idx,
+                                                     unsigned long long* __restrict__ n_valid, uint32_t stage_bytes,
+                                                     int fast, unsigned long long* __restrict__ tl) {
+    __shared__ WaveQueue5 queues[BLOCK / 64];
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_blob[];
+    const int lane = threadIdx.x & 63;
+    const int gwave = (int)((blockIdx.x * BLOCK + threadIdx.x) >> 6);
+    uint32_t tl_needy = 0, tl_item = 0;
+    auto mark = [&](int k) {
+        if (TL) {
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            if (lane == 0) tl[gwave * 8 + k] = t;
+        }
+    };
+    mark(0);
+    WaveQueue5* qu = &queues[threadIdx.x >> 6];
+    const int64_t stride = (int64_t)gridDim.x * BLOCK;
+    const int64_t gfirst = (int64_t)blockIdx.x * BLOCK;
+    int64_t g = gfirst + threadIdx.x;
+    double va[12], vb[12];
+    auto load = [&](int64_t grp, double (&dst)[12]) {
+        grp = grp < groups ? grp : groups - 1;
+        const double2* q = reinterpret_cast<const double2*>(xyz) + 6 * grp;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const double2 t = q[k];
+            dst[2 * k] = t.x;
+            dst[2 * k + 1] = t.y;
+        }
+    };
+    if (gfirst < groups) load(g, va);
+    // [off_aos, blob_bytes): records, list headers, list ids, class table, copied while
+    // the group's loads are in flight.  (LDS-DMA variants were tried: hipcc then drains
+    // vmcnt at the first use of any group, prefetched ones included.)
+    stage_copy(lds_blob, wv->blob + wv->off_aos, stage_bytes, BLOCK);
+    const uint32_t lists_off = wv->off_lists - wv->off_aos, ids_off = wv->off_ids - wv->off_aos;
+    const uint16_t* cls_tab = reinterpret_cast<const uint16_t*>(lds_blob + (wv->off_bitmap - wv->off_aos));
+    const uint32_t* hdrs = reinterpret_cast<const uint32_t*>(lds_blob + lists_off);
+    const uint16_t* ids_all = reinterpret_cast<const uint16_t*>(lds_blob + ids_off);
+    const double* recs = reinterpret_cast<const double*>(lds_blob);
+    const float ox = wv->bofx, oy = wv->bofy, oz = wv->bofz, ix = wv->bix, iy = wv->biy, iz = wv->biz;
+    const uint32_t nx = (uint32_t)wv->bnx, ny = (uint32_t)wv->bny, nz = (uint32_t)wv->bnz;
+    const double rg = wv->r_gate, ro = wv->r_obst;
+    __syncthreads();
+    mark(1);
+    mark(2);
+    auto cls_of = [&](double px, double py, double pz) -> uint32_t {
+        const uint32_t cx = cell_axis5(px, ox, ix, nx - 1), cy = cell_axis5(py, oy, iy, ny - 1),
+                       cz = cell_axis5(pz, oz, iz, nz - 1);
+        return (uint32_t)cls_tab[__umul24(__umul24(cz, ny) + cy, nx) + cx];
+    };
+    auto process = [&](int64_t gg, const double (&v)[12]) {
+        const bool live = gg < groups;
+        uint32_t c[4];
+        bool needy[4];
+        unsigned long long b[4];
+        uint32_t base[4], total = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c[k] = cls_of(v[3 * k], v[3 * k + 1], v[3 * k + 2]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            needy[k] = live & (c[k] != 0u);
+            b[k] = __ballot(needy[k]);
+            base[k] = total;
+            total += (uint32_t)__popcll(b[k]);
+        }
+        if (TL) {
+            tl_needy += total;
+            if (tl_item == 0) mark(4);
+        }
+        uint32_t hits = 0;
+        if (fast == 2) {  // ablation (diagnostics only, wrong answers): needy states count as hits
+#pragma unroll
+            for (int k = 0; k < 4; ++k) hits |= needy[k] ? 1u << k : 0u;
+        } else if (total > 0) {  // wave-uniform
+            uint32_t pos[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) pos[k] = base[k] + lanes_below(b[k]);
+            // queue the needy states (slot = rank in the wave), rounds of 64
+            for (uint32_t r0 = 0; r0 < total; r0 += 64) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t slot = pos[k] - r0;
+                    if (needy[k] && slot < 64u) {
+                        qu->x[slot] = v[3 * k];
+                        qu->y[slot] = v[3 * k + 1];
+                        qu->z[slot] = v[3 * k + 2];
+                        qu->cls[slot] = (uint16_t)c[k];
+                    }
+                }
+                wave_lds_sync();
+                const uint32_t tq = min(total - r0, 64u);
+                // lane e < tq owns queued state e: its candidate list
+                const bool act = (uint32_t)lane < tq;
+                const uint32_t hd = hdrs[act ? (uint32_t)qu->cls[lane] : 0u];  // list 0 is empty
+                const uint32_t cnt = hd & 4095u, first = hd >> 12;
+                uint32_t ptot;
+                const uint32_t poff = wave_excl_scan(cnt, lane, ptot);
+                bool hit_e = false;
+                if (fast && ptot <= 64u) {
+                    // one (state, candidate) pair per lane: lane q finds its state as the
+                    // max-scan of segment heads (state e marks position poff_e)
+                    qu->pair[lane] = 0u;
+                    if (act) qu->pair[poff] = (uint32_t)lane;  // cnt >= 1 for queued states
+                    wave_lds_sync();
+                    const uint32_t e = dpp_incl_max(qu->pair[lane]);
+                    const uint32_t pe = (uint32_t)__shfl((int)poff, (int)e, 64);
+                    const uint32_t fe = (uint32_t)__shfl((int)first, (int)e, 64);
+                    bool h = false;
+                    if ((uint32_t)lane < ptot)
+                        h = rec_hit<MINDIST>(recs + (size_t)ids_all[fe + (uint32_t)lane - pe] * kRecDoubles, rg, ro,
+                                             qu->x[e], qu->y[e], qu->z[e], can_pass != 0, md);
+                    const unsigned long long m = __ballot(h);
+                    const unsigned long long msk = cnt >= 64u ? ~0ull : ((1ull << cnt) - 1ull);
+                    hit_e = act && ((m >> poff) & msk) != 0ull;
+                } else if (act) {  // long lists: each queued state walks its own
+                    hit_e = states_exact_rec<MINDIST>(lds_blob, lists_off, ids_off, rg, ro, qu->x[lane], qu->y[lane],
+                                                      qu->z[lane], qu->cls[lane], can_pass, md);
+                }
+                // back to the owners: state slot r0 + e lives on lane e
+                const unsigned long long hm = __ballot(hit_e);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t slot = pos[k] - r0;
+                    if (needy[k] && slot < 64u && ((hm >> slot) & 1ull)) hits |= 1u << k;
+                }
+                wave_lds_sync();  // the queue is rewritten next
+            }
+            if (TL && tl_item == 0) mark(5);
+        }
+        if (TL) ++tl_item;
+        const uint32_t fl = live ? (~hits & 15u) : 0u;  // bit k: state 4 gg + k valid
+        if (live)
+            *reinterpret_cast<uint32_t*>(valid + 4 * gg) =
+                (fl & 1u) | ((fl & 2u) << 7) | ((fl & 4u) << 14) | ((fl & 8u) << 21);
+        if (COMPACT) {  // wave-ballot compaction
+            const uint32_t cnt = (uint32_t)__popc(fl);
+            uint32_t ctot;
+            const uint32_t cex = wave_excl_scan(cnt, lane, ctot);
+            unsigned long long wbase = 0;
+            if (lane == 0 && ctot) wbase = atomicAdd(n_valid, (unsigned long long)ctot);
+            wbase = __shfl(wbase, 0, 64);
+            uint64_t p = wbase + cex;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if ((fl >> k) & 1u) compact_idx[p++] = (int32_t)(4 * gg + k);
+        }
+    };
+    // block-uniform trip count; the next group's loads are issued before this one is
+    // classified (vmcnt counts in order: the class lookups never wait on them)
+    if (PREFETCH) {  // prefetch loads unconditional (clamped): counted vmcnt, no merge points
+        for (int64_t g0 = gfirst; g0 < groups; g0 += 2 * stride, g += 2 * stride) {
+            load(g + stride, vb);
+            process(g, va);
+            if (g0 + stride >= groups) break;
+            load(g + 2 * stride, va);
+            process(g + stride, vb);
+        }
+    } else {
+        for (int64_t g0 = gfirst; g0 < groups; g0 += stride, g += stride) {
+            if (g0 != gfirst) load(g, va);
+            process(g, va);
+        }
+    }
+    if (TL) {
+        mark(3);
+        if (lane == 0) {
+            unsigned hw, xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            tl[gwave * 8 + 6] = hw;
+            tl[gwave * 8 + 7] = xcc | ((unsigned long long)tl_needy << 32);
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (int)(n - 4 * groups)) {  // tail: the last n % 4 states
+        const int64_t i = 4 * groups + threadIdx.x;
+        const double px = xyz[3 * i], py = xyz[3 * i + 1], pz = xyz[3 * i + 2];
+        const uint32_t c = cls_of(px, py, pz);
+        const bool ok = !(c != 0u && states_exact_rec<MINDIST>(lds_blob, lists_off, ids_off, rg, ro, px, py, pz, c,
+                                                               can_pass, md));
+        valid[i] = ok ? 1 : 0;
+        if (COMPACT && ok) compact_idx[atomicAdd(n_valid, 1ull)] = (int32_t)i;
+    }
+}
+
 template <bool LDS, int MODE>
 __global__ __launch_bounds__(kBlock) void k_motions(WorldView w, const double* __restrict__ s1,
                                                     const double* __restrict__ s2, int64_t n,
@@ -1161,6 +1384,16 @@ epp_status launch_error(const char* what) {
 using namespace epp;
 
 namespace {
+// k_states_v5 stages [off_aos, blob_bytes) next to its wave queues
+int v5_block(int dflt) {
+    const int b = env_int("EPP_V5_BLOCK", dflt);
+    return b == 256 ? 256 : (b == 512 ? 512 : 1024);
+}
+bool v5_fits(const WorldView& w) {
+    const uint32_t q = queue5_bytes<1024>();
+    return (w.blob_bytes - w.off_aos) + q <= 160u * 1024u && !env_int("EPP_NO_LDS", 0);
+}
+int v5_cap() { return cu_count() * std::max(1, env_int("EPP_WG_PER_CU5", 1)); }
 bool v4_stage(const WorldView& w) {
     return (w.off_bitmap - w.off_aos) + sizeof(StateQueue4) <= 160u * 1024u && !env_int("EPP_NO_LDS", 0);
 }
@@ -1216,8 +1449,43 @@ epp_status launch_states(const WorldView& w, const WorldView* dw, const double* 
         hipLaunchKernelGGL((k_states<L, MINDIST, A>), dim3(grid), dim3(kBlock), shm, st, w, xyz, n,   \
                            can_pass, md, valid, compact_idx, nv, stage, tl);                          \
     } while (0)
-    const int impl = env_int("EPP_STATES_IMPL", 4);
-    if (impl == 4 && (reinterpret_cast<uintptr_t>(xyz) & 15) == 0 && (reinterpret_cast<uintptr_t>(valid) & 1) == 0 &&
+    const int impl = env_int("EPP_STATES_IMPL", 5);
+    if (impl == 5 && v5_fits(w) && (reinterpret_cast<uintptr_t>(xyz) & 15) == 0 &&
+        (reinterpret_cast<uintptr_t>(valid) & 3) == 0) {
+        const int64_t g5 = n / 4;
+        const uint32_t sb = w.blob_bytes - w.off_aos;
+        const int fast = env_int("EPP_V5_PAIRS", 1);
+        // single pass: 1024-thread workgroups; multi-pass (prefetching): 512 (VGPR budget)
+        const bool single = g5 <= (int64_t)v5_cap() * 1024;
+        const int bs = v5_block(single ? 1024 : 512);
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((g5 + bs - 1) / bs, v5_cap()));
+        const bool pf = g5 > (int64_t)grid * bs;  // more than one group per lane
+#define EPP_LAUNCH_V5(C, T, B, P)                                                                                \
+    do {                                                                                                         \
+        allow_lds(k_states_v5<MINDIST, C, T, B, P>, queue5_bytes<B>());                                          \
+        hipLaunchKernelGGL((k_states_v5<MINDIST, C, T, B, P>), dim3(grid), dim3(B), sb, st, dw, xyz, g5, n,       \
+                           can_pass, md, valid, compact_idx, nv, sb, fast, tl);                                  \
+    } while (0)
+#define EPP_LAUNCH_V5B(B)                                          \
+    do {                                                           \
+        if (pf) {                                                  \
+            if (tl) EPP_LAUNCH_V5(false, true, B, true);           \
+            else if (compact_idx) EPP_LAUNCH_V5(true, false, B, true); \
+            else EPP_LAUNCH_V5(false, false, B, true);             \
+        } else {                                                   \
+            if (tl) EPP_LAUNCH_V5(false, true, B, false);          \
+            else if (compact_idx) EPP_LAUNCH_V5(true, false, B, false); \
+            else EPP_LAUNCH_V5(false, false, B, false);            \
+        }                                                          \
+    } while (0)
+        if (bs == 256) EPP_LAUNCH_V5B(256);
+        else if (bs == 512) EPP_LAUNCH_V5B(512);
+        else EPP_LAUNCH_V5B(1024);
+#undef EPP_LAUNCH_V5B
+#undef EPP_LAUNCH_V5
+        return launch_error(MINDIST ? "epp_check_states_mindist" : "epp_check_states");
+    }
+    if ((impl == 4 || impl == 5) && (reinterpret_cast<uintptr_t>(xyz) & 15) == 0 && (reinterpret_cast<uintptr_t>(valid) & 1) == 0 &&
         n / 2 < 0xFFFFFFFFll && !tl) {
         const uint32_t sb = w.off_bitmap - w.off_aos;
         const bool stg = v4_stage(w);
@@ -1239,7 +1507,7 @@ epp_status launch_states(const WorldView& w, const WorldView* dw, const double* 
 #undef EPP_LAUNCH_V4
         return launch_error(MINDIST ? "epp_check_states_mindist" : "epp_check_states");
     }
-    if ((impl == 3 || impl == 4) && (reinterpret_cast<uintptr_t>(xyz) & 15) == 0 && (reinterpret_cast<uintptr_t>(valid) & 1) == 0) {
+    if ((impl >= 3) && (reinterpret_cast<uintptr_t>(xyz) & 15) == 0 && (reinterpret_cast<uintptr_t>(valid) & 1) == 0) {
         const uint32_t sb = w.off_bitmap - w.off_aos;
         const bool stg = v3_stage(w);
         const int g3 = v3_grid(w, n);
@@ -1325,8 +1593,15 @@ epp_status epp_dbg_states_timeline(const epp_world* world, const double* xyz, in
     const bool lds = w.front_bytes + kScratchBytes <= kLdsBudget && !env_int("EPP_NO_LDS", 0);
     const uint32_t full_cap = (uint32_t)env_int("EPP_STAGE_FULL_MAX", 40 * 1024);
     const uint32_t stage = !lds ? 0u : (w.blob_bytes <= full_cap ? w.blob_bytes : w.front_bytes);
-    const int impl = env_int("EPP_STATES_IMPL", 4);
-    if (impl == 3 || impl == 4)  // (the timeline runs k_states_v3 for impl 4 too)
+    const int impl = env_int("EPP_STATES_IMPL", 5);
+    if (impl == 5 && v5_fits(w) && (reinterpret_cast<uintptr_t>(xyz) & 15) == 0 &&
+        (reinterpret_cast<uintptr_t>(valid) & 3) == 0)
+        *grid_waves = [&] {
+            const int64_t g5 = n / 4;
+            const int bs = v5_block(g5 <= (int64_t)v5_cap() * 1024 ? 1024 : 512);
+            return (int)std::max<int64_t>(1, std::min<int64_t>((g5 + bs - 1) / bs, v5_cap())) * (bs / 64);
+        }();
+    else if (impl >= 3)  // (the timeline runs k_states_v3 for impl 4 too)
         *grid_waves = v3_grid(w, n) * (kBlock3 / 64);
     else
         *grid_waves = (impl == 1 ? bm_grid(w, std::max<int64_t>(1, n / 4))

@@ -45,6 +45,9 @@ constexpr int kRecDoubles = 17;
 constexpr int R_META = 16;
 
 constexpr size_t kListMaxLen = 4095;  // OBBs per fine-cell list (12-bit count)
+// LDS bytes k_states_v5 may spend on the staged world (records, lists, class table);
+// the rest of the 160 KB holds its wave queues
+constexpr size_t kStageBudget = 96 * 1024;
 
 constexpr uint32_t META_FILLING = 1u;
 constexpr uint32_t META_GATE = 2u;
@@ -79,18 +82,21 @@ struct WorldView {
     uint32_t off_bitmap;      // cls[] (u16 per fine cell)
     uint32_t bm_words;        // index of the zero sentinel class
     int32_t bnx, bny, bnz;    // cells per axis
-    float bofx, bofy, bofz;   // origin (float)
+    float bofx, bofy, bofz;   // offset: cell coordinate f = fmaf((float)p, bi, bof)
     float bix, biy, biz;      // 1 / cell size (float)
 };
 
-// Bitmap cell index along one axis: the same float operations on host and device, so
-// the host marks exactly the cells the kernels look up; monotone in p.  Values
-// outside [0, n) mean "outside every AABB".
+// Class-grid cell index along one axis: f = fmaf((float)p, inv, off), truncated.  The
+// same float operations on host and device, so the host marks exactly the cells the
+// kernels look up; monotone in p.  The grid keeps an empty margin cell at both ends of
+// every axis (every AABB corner maps to [1, n-2]), so a kernel may clamp an
+// out-of-range index to [0, n-1] (hardware cvt: NaN -> 0, saturating) instead of
+// testing bounds: such states land in an empty cell, exactly like "outside".
 #if defined(__HIPCC__)
 __host__ __device__
 #endif
-inline int bm_axis(double p, float o, float inv) {
-    float f = ((float)p - o) * inv;
+inline int bm_axis(double p, float off, float inv) {
+    float f = fmaf((float)p, inv, off);
     f = fminf(fmaxf(f, -1.0f), 16777216.0f);  // NaN -> -1 (outside); keeps (int) defined
     return (int)f;                             // truncation toward zero
 }

@@ -155,7 +155,7 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
     std::vector<uint32_t> hdr;    // per list: start << 12 | count
     std::vector<uint16_t> flat;   // the lists' OBB ids
     const char* env_bits = std::getenv("EPP_BITMAP_BITS");
-    double setenv_target = env_bits && *env_bits ? std::max(64.0, std::atof(env_bits)) : double(1 << 16);
+    double setenv_target = env_bits && *env_bits ? std::max(64.0, std::atof(env_bits)) : double(1 << 14);
     for (;;) {
         const double target = setenv_target;
         int bd[3] = {1, 1, 1};
@@ -170,16 +170,17 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
             for (int pass = 0;; ++pass) {
                 bool ok = true;
                 for (int k = 0; k < 3; ++k) {
-                    bd[k] = std::min(4096, (int)std::ceil(ext[k] / h) + 2 + pass);
-                    bo[k] = (float)(g0[k] - h);
+                    bd[k] = std::min(4096, (int)std::ceil(ext[k] / h) + 4 + pass);
                     bi[k] = (float)(1.0 / h);
+                    bo[k] = (float)(-(g0[k] - 1.5 * h) * (double)bi[k]);  // origin 1.5 cells below g0
                 }
-                // every AABB corner must map inside the grid (else widen and retry)
+                // every AABB corner must map to [1, n-2]: the first and last cell of each
+                // axis stay empty (else widen and retry)
                 for (int i = 0; i < n && ok; ++i)
                     for (int k = 0; k < 3; ++k) {
                         const int lo_i = bm_axis(hw.aabbs[(size_t)i * 6 + k], bo[k], bi[k]);
                         const int hi_i = bm_axis(hw.aabbs[(size_t)i * 6 + 3 + k], bo[k], bi[k]);
-                        if (lo_i < 0 || hi_i >= bd[k]) ok = false;
+                        if (lo_i < 1 || hi_i > bd[k] - 2) ok = false;
                     }
                 if (ok) break;
                 if (pass > 8) h *= 1.1;
@@ -227,6 +228,14 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
                 return false;
             }
             setenv_target = target / 8;
+            continue;
+        }
+        // k_states_v5 stages records + lists + class table into LDS: keep that part
+        // within kStageBudget by coarsening the class grid (down to 4096 cells)
+        const size_t staged = align16((size_t)n * kRecDoubles * 8) + align16(hdr.size() * 4 + flat.size() * 2) +
+                              align16(cls.size() * 2);
+        if (!env_bits && staged > kStageBudget && target > 4096.0) {
+            setenv_target = target / 2;
             continue;
         }
         v.bnx = bd[0]; v.bny = bd[1]; v.bnz = bd[2];

@@ -41,7 +41,12 @@ def main():
     dv = capi.DeviceBuffer(N)
     res = {}
 
+    import re
+    pat = re.compile(sys.argv[1]) if len(sys.argv) > 1 else None
+
     def run(name, world, buf, env=None):
+        if pat and not pat.search(name):
+            return
         for k, v in (env or {}).items():
             os.environ[k] = str(v)
         f = lambda r: world.check_states_dev(buf.ptr + (r % NB) * N * 24, N, 0, dv.ptr, stream=st)  # noqa
@@ -69,6 +74,8 @@ def main():
         print(f"stream_mode{mode}_16M", res[f"stream_mode{mode}_16M"], flush=True)
 
     def big(name, world, env=None):
+        if pat and not pat.search(name):
+            return
         for k, v in (env or {}).items():
             os.environ[k] = str(v)
         f = lambda r: world.check_states_dev(d.ptr, NB * N, 0, dbig.ptr, stream=st)  # noqa
@@ -79,21 +86,29 @@ def main():
         res[name] = {"us": ms * 1e3, "GBs": 25 * NB * N / (ms * 1e-3) / 1e9}
         print(name, res[name], flush=True)
 
-    for impl in (0, 1, 3, 4):
+    for impl in (0, 1, 3, 4, 5):
         e = {"EPP_STATES_IMPL": impl}
         run(f"c2_impl{impl}", w2, d, e)
         big(f"c2_impl{impl}_16M", w2, e)
         run(f"c2_impl{impl}_empty_world", w0, d, e)
+    run("c2_impl5_b512", w2, d, {"EPP_STATES_IMPL": 5, "EPP_V5_BLOCK": 512})
+    big("c2_impl5_b1024_16M", w2, {"EPP_STATES_IMPL": 5, "EPP_V5_BLOCK": 1024})
+    run("c2_impl5_b256", w2, d, {"EPP_STATES_IMPL": 5, "EPP_V5_BLOCK": 256})
+    big("c2_impl5_b256_16M", w2, {"EPP_STATES_IMPL": 5, "EPP_V5_BLOCK": 256})
+    run("c2_impl5_ablate_exact", w2, d, {"EPP_STATES_IMPL": 5, "EPP_V5_PAIRS": 2})
+    big("c2_impl5_ablate_exact_16M", w2, {"EPP_STATES_IMPL": 5, "EPP_V5_PAIRS": 2})
+    run("c2_impl5_walk", w2, d, {"EPP_STATES_IMPL": 5, "EPP_V5_PAIRS": 0})
+    big("c2_impl5_walk_16M", w2, {"EPP_STATES_IMPL": 5, "EPP_V5_PAIRS": 0})
     for impl in (3, 4):
-        for k in (2, 3, 4):
+        for k in (3,):
             e = {"EPP_STATES_IMPL": impl, "EPP_WG_PER_CU": k}
             run(f"c2_impl{impl}_wg_per_cu_{k}", w2, d, e)
             big(f"c2_impl{impl}_wg_per_cu_{k}_16M", w2, e)
-    for bits in (1 << 14, 1 << 17):
+    for bits in (1 << 12, 1 << 14, 1 << 15):
         os.environ["EPP_BITMAP_BITS"] = str(bits)
         wb = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
         del os.environ["EPP_BITMAP_BITS"]
-        for impl in (3, 4):
+        for impl in (4, 5):
             run(f"c2_impl{impl}_cells_{bits}", wb, d, {"EPP_STATES_IMPL": impl})
             big(f"c2_impl{impl}_cells_{bits}_16M", wb, {"EPP_STATES_IMPL": impl})
         wb.close()

@@ -91,6 +91,30 @@ def test_states_mindist(geom, worlds, name):
         assert np.array_equal(got, exp), md
 
 
+@pytest.mark.parametrize("impl", ["0", "1", "3", "4", "5", "5walk", "5b512"])
+@pytest.mark.parametrize("name", ["c2", "c3"])
+def test_states_every_kernel_variant(geom, worlds, name, impl, monkeypatch):
+    """Each k_states variant (EPP_STATES_IMPL; 5 = default, falls back when its staged
+    world does not fit LDS; "5walk" = v5 with per-state list walks instead of pairs) on
+    plain, compacting and minDistance launches, ragged n."""
+    monkeypatch.setenv("EPP_STATES_IMPL", impl[0])
+    monkeypatch.setenv("EPP_V5_PAIRS", "0" if impl.endswith("walk") else "1")
+    monkeypatch.setenv("EPP_V5_BLOCK", "512" if impl.endswith("b512") else "1024")
+    impl = int(impl[0])
+    rg, ro, ws = worlds
+    gates, obstacles, (lo, hi) = ws[name]
+    ref = O.world_build(geom, gates, obstacles, rg, ro)
+    w = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
+    pts = np.vstack([synth.sample_states(31 + impl, lo, hi, 150_001), _adversarial_points(ref)])
+    exp = O.check_states(ref, rg, ro, pts, False, threads=8)
+    assert np.array_equal(w.check_states(pts, False), exp)
+    valid, idx = w.check_states(pts, False, compact=True)
+    assert np.array_equal(valid, exp) and np.array_equal(np.sort(idx), np.flatnonzero(exp))
+    for n in (1, 2, 3, 5, 4097):
+        assert np.array_equal(w.check_states(pts[:n], False), exp[:n]), n
+    assert np.array_equal(w.check_states_mindist(pts, 0.15), O.check_states_mindist(ref, pts, 0.15))
+
+
 def test_compaction(geom, worlds):
     rg, ro, ws = worlds
     gates, obstacles, (lo, hi) = ws["c2"]
