@@ -21,15 +21,19 @@ tail -3 gpurun_out/smoke.log; stop_on_fault $rc smoke
 echo "== bench"
 timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?
 tail -c 1500 gpurun_out/bench.json; tail -3 gpurun_out/bench.err; stop_on_fault $rc bench
-echo "== rocprofv3 kernel trace of the bench"
-rm -rf gpurun_out/prof
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu > gpurun_out/prof_bench.json 2> gpurun_out/prof.err; rc=$?
+echo "== rocprofv3 kernel trace of the bench headline (no plan / side legs: one launch shape)"
+rm -rf gpurun_out/prof gpurun_out/prof_full
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu --no-plan --no-side > gpurun_out/prof_bench.json 2> gpurun_out/prof.err; rc=$?
 tail -3 gpurun_out/prof.err; stop_on_fault $rc rocprof
+echo "== rocprofv3 kernel trace of the whole bench (plan + side legs)"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_full -o run -- python3 bench.py --no-cpu > gpurun_out/prof_full_bench.json 2> gpurun_out/prof_full.err; rc=$?
+tail -3 gpurun_out/prof_full.err; stop_on_fault $rc rocprof_full
 for c in FETCH_SIZE WRITE_SIZE; do
   echo "== rocprofv3 --pmc $c"
   rm -rf gpurun_out/pmc_$c
   timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_$c -o run -- python3 bench.py --no-cpu --no-side --no-plan > gpurun_out/pmc_$c.json 2> gpurun_out/pmc_$c.err; rc=$?
   tail -2 gpurun_out/pmc_$c.err; stop_on_fault $rc pmc_$c
 done
-python3 scripts/profile_summary.py gpurun_out r01 > gpurun_out/profile_summary.log 2>&1; cat gpurun_out/profile_summary.log
+python3 scripts/profile_summary.py gpurun_out ${TAG:-r01} > gpurun_out/profile_summary.log 2>&1; cat gpurun_out/profile_summary.log
+cp gpurun_out/bench.json profiles/${TAG:-r01}_bench.json
 echo done

@@ -1,6 +1,8 @@
 """Summarise a gpu_check.sh session into profiles/<tag>_*.{csv,json} (committed).
 
-  <tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary of `python3 bench.py --no-cpu`
+  <tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary of the bench headline
+                           (`python3 bench.py --no-cpu --no-plan --no-side`: one launch shape)
+  <tag>_kernel_stats_full.csv  the same over the whole bench (`--no-cpu`: plan + side legs)
   <tag>_traffic.json       HBM bytes per k_states launch from the FETCH_SIZE / WRITE_SIZE passes,
                            corrected as MI355X_MICROARCH.md prescribes: FETCH_SIZE counts half the
                            bytes of a wide (16 B/lane) streaming read on gfx950 -> x2; both in KB.
@@ -17,12 +19,14 @@ root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 prof = os.path.join(root, "profiles")
 os.makedirs(prof, exist_ok=True)
 
-stats = glob.glob(os.path.join(out_dir, "prof", "**", "*kernel_stats.csv"), recursive=True)
-if stats:
-    shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
-    rows = list(csv.DictReader(open(stats[0])))
-    for r in rows[:12]:
-        print(r.get("Name", "")[:70], r.get("Calls"), r.get("AverageNs"))
+for sub, suffix in (("prof", "kernel_stats"), ("prof_full", "kernel_stats_full")):
+    stats = glob.glob(os.path.join(out_dir, sub, "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], os.path.join(prof, f"{tag}_{suffix}.csv"))
+        rows = list(csv.DictReader(open(stats[0])))
+        print(f"-- {suffix}")
+        for r in rows[:12]:
+            print(r.get("Name", "")[:70], r.get("Calls"), r.get("AverageNs"))
 
 
 def per_kernel(counter):
