@@ -1096,7 +1096,7 @@ __device__ __forceinline__ uint32_t cell_axis5(double p, float off, float inv, u
 // single-pass launches (e.g. 1M states on 256 CUs) drop the second buffer's registers.
 template <bool MINDIST, bool COMPACT, bool TL, int BLOCK, bool PREFETCH>
 __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict__ wv,
-                                                     const double* __restrict__ xyz, int64_t groups, int64_t n,
+                                                     const double* xyz, int64_t groups, int64_t n,
                                                      int can_pass, double md, uint8_t* __restrict__ valid,
                                                      int32_t* __restrict__ compact_idx,
                                                      unsigned long long* __restrict__ n_valid, uint32_t stage_bytes,
@@ -1118,9 +1118,12 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
     const int64_t gfirst = (int64_t)blockIdx.x * BLOCK;
     int64_t g = gfirst + threadIdx.x;
     double va[12], vb[12];
+    // (no full group: loads read the WorldView instead, >= 96 bytes, ignored)
+    const double* xyzb = groups > 0 ? xyz : reinterpret_cast<const double*>(wv);
     auto load = [&](int64_t grp, double (&dst)[12]) {
         grp = grp < groups ? grp : groups - 1;
-        const double2* q = reinterpret_cast<const double2*>(xyz) + 6 * grp;
+        grp = grp < 0 ? 0 : grp;
+        const double2* q = reinterpret_cast<const double2*>(xyzb) + 6 * grp;
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
             const double2 t = q[k];
@@ -1128,11 +1131,36 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
             dst[2 * k + 1] = t.y;
         }
     };
-    if (gfirst < groups) load(g, va);
-    // [off_aos, blob_bytes): records, list headers, list ids, class table, copied while
-    // the group's loads are in flight.  (LDS-DMA variants were tried: hipcc then drains
-    // vmcnt at the first use of any group, prefetched ones included.)
-    stage_copy(lds_blob, wv->blob + wv->off_aos, stage_bytes, BLOCK);
+    // [off_aos, blob_bytes): records, list headers, list ids, class table.  The copy's
+    // loads are issued BEFORE the group's loads and stored after them, so the stores
+    // wait on a counted vmcnt that leaves the group's HBM loads in flight, and the
+    // barrier below never waits on HBM.  Every lane loads and stores every chunk slot
+    // (clamped source; out-of-range chunks go to a dummy LDS slot): no branches.  xyz
+    // is not __restrict__ so its loads cannot be sunk past the LDS stores.
+    // (LDS-DMA variants were tried: hipcc then drains vmcnt at the first use of any
+    // group, prefetched ones included.)
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // (HIP's uint4 struct ends up on the stack)
+    constexpr int kStageChunks = (int)(kStageBudget / (BLOCK * 16));
+    u32x4 stg[kStageChunks];
+    const uint32_t n16 = stage_bytes / 16u;  // >= 1 (the class table's sentinel)
+#if defined(__HIP_DEVICE_COMPILE__)  // global (not flat) loads: flat ones would also count lgkmcnt and force vmcnt(0)
+    typedef const __attribute__((address_space(1))) u32x4* gptr_stage;
+    const gptr_stage ssrc = (gptr_stage)(wv->blob + wv->off_aos);
+#else
+    const u32x4* ssrc = reinterpret_cast<const u32x4*>(wv->blob + wv->off_aos);
+#endif
+#pragma unroll
+    for (int i = 0; i < kStageChunks; ++i) {
+        const uint32_t o = (uint32_t)(i * BLOCK) + threadIdx.x;
+        stg[i] = ssrc[o < n16 ? o : n16 - 1u];
+    }
+    load(g, va);  // unconditional (clamped): a branch here would make hipcc's vmcnt counts conservative
+#pragma unroll
+    for (int i = 0; i < kStageChunks; ++i) {
+        const uint32_t o = (uint32_t)(i * BLOCK) + threadIdx.x;
+        // (the launch allocates 16 spare bytes after the copy: the dummy slot)
+        *reinterpret_cast<u32x4*>(lds_blob + 16u * (o < n16 ? o : n16)) = stg[i];
+    }
     const uint32_t lists_off = wv->off_lists - wv->off_aos, ids_off = wv->off_ids - wv->off_aos;
     const uint16_t* cls_tab = reinterpret_cast<const uint16_t*>(lds_blob + (wv->off_bitmap - wv->off_aos));
     const uint32_t* hdrs = reinterpret_cast<const uint32_t*>(lds_blob + lists_off);
@@ -1391,7 +1419,8 @@ int v5_block(int dflt) {
 }
 bool v5_fits(const WorldView& w) {
     const uint32_t q = queue5_bytes<1024>();
-    return (w.blob_bytes - w.off_aos) + q <= 160u * 1024u && !env_int("EPP_NO_LDS", 0);
+    return (w.blob_bytes - w.off_aos) + 16u + q <= 160u * 1024u && (w.blob_bytes - w.off_aos) <= kStageBudget &&
+           !env_int("EPP_NO_LDS", 0);
 }
 int v5_cap() { return cu_count() * std::max(1, env_int("EPP_WG_PER_CU5", 1)); }
 bool v4_stage(const WorldView& w) {
@@ -1463,7 +1492,7 @@ epp_status launch_states(const WorldView& w, const WorldView* dw, const double* 
 #define EPP_LAUNCH_V5(C, T, B, P)                                                                                \
     do {                                                                                                         \
         allow_lds(k_states_v5<MINDIST, C, T, B, P>, queue5_bytes<B>());                                          \
-        hipLaunchKernelGGL((k_states_v5<MINDIST, C, T, B, P>), dim3(grid), dim3(B), sb, st, dw, xyz, g5, n,       \
+        hipLaunchKernelGGL((k_states_v5<MINDIST, C, T, B, P>), dim3(grid), dim3(B), sb + 16, st, dw, xyz, g5, n,  \
                            can_pass, md, valid, compact_idx, nv, sb, fast, tl);                                  \
     } while (0)
 #define EPP_LAUNCH_V5B(B)                                          \

@@ -45,9 +45,10 @@ constexpr int kRecDoubles = 17;
 constexpr int R_META = 16;
 
 constexpr size_t kListMaxLen = 4095;  // OBBs per fine-cell list (12-bit count)
-// LDS bytes k_states_v5 may spend on the staged world (records, lists, class table);
-// the rest of the 160 KB holds its wave queues
-constexpr size_t kStageBudget = 96 * 1024;
+// LDS bytes k_states_v5 stages per workgroup (records, lists, class table): the class
+// grid is coarsened until the world fits; the copy is register-staged, so this also
+// bounds its per-lane registers (4 x 16 B at 1024 threads)
+constexpr size_t kStageBudget = 64 * 1024;
 
 constexpr uint32_t META_FILLING = 1u;
 constexpr uint32_t META_GATE = 2u;
