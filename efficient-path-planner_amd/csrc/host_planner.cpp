@@ -77,8 +77,11 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     const double hi[3] = {wp.upperBound.x, wp.upperBound.y, wp.upperBound.z};
     check(epp_sample_uniform(seed, lo, hi, samples, 0, d_s, st), "sample");
     check(epp_check_states(w, d_s, samples, canPass ? 1 : 0, d_v, nullptr, nullptr, st), "state check");
-    std::vector<double> xyz(n_s * 3);
-    std::vector<uint8_t> valid(n_s);
+    // per-thread host staging, reused across calls (no per-call zero fill of MBs)
+    thread_local std::vector<double> xyz;
+    thread_local std::vector<uint8_t> valid;
+    xyz.resize(n_s * 3);
+    valid.resize(n_s);
     check(epp_memcpy_d2h(xyz.data(), d_s, n_s * 24, st), "download");
     check(epp_memcpy_d2h(valid.data(), d_v, n_s, st), "download");
     // nodes: start, goal, then the valid samples in sample order
@@ -101,34 +104,21 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     check(epp_knn_ws(d_nodes, n, k, 0.0, d_nbr, d_ws, ws_bytes, st), "knn");
     check(epp_knn_edges(d_nodes, d_nbr, n, k, d_e1, d_e2, st), "edges");
     check(epp_check_motions(w, d_e1, d_e2, (int64_t)m, canPass ? 1 : 0, 0, d_ev, st), "motion check");
-    std::vector<int32_t> nbr(m);
-    std::vector<uint8_t> ev(m);
+    thread_local std::vector<int32_t> nbr;
+    thread_local std::vector<uint8_t> ev;
+    nbr.resize(m);
+    ev.resize(m);
     check(epp_memcpy_d2h(nbr.data(), d_nbr, m * 4, st), "download");
     check(epp_memcpy_d2h(ev.data(), d_ev, m, st), "download");
     const auto t_dev1 = std::chrono::steady_clock::now();
-    // ---- 3. shortest path over the valid edges (undirected), start = 0, goal = 1 ------
-    // CSR of the symmetrised valid k-NN edges, then A* with the Euclidean distance to
-    // the goal (admissible and consistent for Euclidean edge costs: an optimal path).
-    std::vector<int32_t> deg(n + 1, 0);
+    // ---- 3. shortest path over the valid edges, start = 0, goal = 1 ----------------------
+    // A* with the Euclidean distance to the goal (admissible and consistent for Euclidean
+    // edge costs: an optimal path of the graph searched).  First over the forward k-NN
+    // edges alone, read straight from the k-NN table (no graph build: A* touches only
+    // the nodes it expands); only if the goal is not reached that way, again over the
+    // symmetrised graph (reverse edges added as a CSR).
     int64_t n_valid_edges = 0;
-    for (size_t e = 0; e < m; ++e) {
-        const int j = nbr[e];
-        if (j < 0 || !ev[e]) continue;
-        ++deg[e / k];
-        ++deg[j];
-        ++n_valid_edges;
-    }
-    std::vector<int32_t> off(n + 1, 0);
-    for (int i = 0; i < n; ++i) off[i + 1] = off[i] + deg[i];
-    std::vector<int32_t> adj(off[n]);
-    for (int i = 0; i < n; ++i) deg[i] = off[i];
-    for (size_t e = 0; e < m; ++e) {
-        const int j = nbr[e];
-        if (j < 0 || !ev[e]) continue;
-        const int i = (int)(e / k);
-        adj[deg[i]++] = j;
-        adj[deg[j]++] = i;
-    }
+    for (size_t e = 0; e < m; ++e) n_valid_edges += (nbr[e] >= 0 && ev[e]) ? 1 : 0;
     {
         std::lock_guard<std::mutex> lk(g_stats_mu);
         stats_.states_sampled += samples;
@@ -138,30 +128,57 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     }
     auto node = [&](int v) { return Vec3(nodes[3 * v], nodes[3 * v + 1], nodes[3 * v + 2]); };
     const Vec3 gp = node(1);
-    std::vector<double> dist(n, std::numeric_limits<double>::infinity());
-    std::vector<int> prev(n, -1);
-    std::vector<uint8_t> closed(n, 0);
+    std::vector<double> dist(n);
+    std::vector<int> prev(n);
+    std::vector<uint8_t> closed(n);
+    std::vector<int32_t> roff, radj;  // reverse edges (second pass only)
     using QE = std::pair<double, int>;  // (g + h, node)
-    std::priority_queue<QE, std::vector<QE>, std::greater<QE>> q;
-    dist[0] = 0.0;
-    q.push({(node(0) - gp).norm(), 0});
-    while (!q.empty()) {
-        const int u = q.top().second;
-        q.pop();
-        if (closed[u]) continue;
-        closed[u] = 1;
-        if (u == 1) break;
-        const Vec3 pu = node(u);
-        for (int32_t a = off[u]; a < off[u + 1]; ++a) {
-            const int v = adj[a];
-            if (closed[v]) continue;
+    auto astar = [&](bool with_reverse) {
+        std::fill(dist.begin(), dist.end(), std::numeric_limits<double>::infinity());
+        std::fill(prev.begin(), prev.end(), -1);
+        std::fill(closed.begin(), closed.end(), 0);
+        std::priority_queue<QE, std::vector<QE>, std::greater<QE>> q;
+        dist[0] = 0.0;
+        q.push({(node(0) - gp).norm(), 0});
+        auto relax = [&](int u, const Vec3& pu, int v) {
+            if (closed[v]) return;
             const double nd = dist[u] + (node(v) - pu).norm();
             if (nd < dist[v]) {
                 dist[v] = nd;
                 prev[v] = u;
                 q.push({nd + (node(v) - gp).norm(), v});
             }
+        };
+        while (!q.empty()) {
+            const int u = q.top().second;
+            q.pop();
+            if (closed[u]) continue;
+            closed[u] = 1;
+            if (u == 1) return true;
+            const Vec3 pu = node(u);
+            const size_t e0 = (size_t)u * k;
+            for (int c = 0; c < k; ++c) {
+                const int v = nbr[e0 + c];
+                if (v >= 0 && ev[e0 + c]) relax(u, pu, v);
+            }
+            if (with_reverse)
+                for (int32_t r = roff[u]; r < roff[u + 1]; ++r) relax(u, pu, radj[r]);
         }
+        return false;
+    };
+    if (!astar(false)) {
+        roff.assign(n + 1, 0);
+        for (size_t e = 0; e < m; ++e)
+            if (nbr[e] >= 0 && ev[e]) ++roff[nbr[e] + 1];
+        for (int i = 0; i < n; ++i) roff[i + 1] += roff[i];
+        radj.resize(roff[n]);
+        std::vector<int32_t> fill(roff.begin(), roff.end() - 1);
+        for (int i = 0; i < n; ++i)
+            for (int c = 0; c < k; ++c) {
+                const size_t e = (size_t)i * k + c;
+                if (nbr[e] >= 0 && ev[e]) radj[fill[nbr[e]]++] = i;
+            }
+        astar(true);
     }
     auto account = [&] {
         const auto t_end = std::chrono::steady_clock::now();

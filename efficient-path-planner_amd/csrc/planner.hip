@@ -10,6 +10,7 @@
 // (collision.hip); the host runs the shortest-path search over the valid edges.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <mutex>
 #include <string>
@@ -111,12 +112,15 @@ struct KnnGrid {
 };
 
 constexpr int kBoundsThreads = 1024;
+constexpr int kBoundsBlocks = 64;
+constexpr double kNodesPerCell = 3.0;  // mean nodes per grid cell (EPP_KNN_NPC overrides; tuning)
 
-__global__ __launch_bounds__(kBoundsThreads) void k_knn_bounds(const double* __restrict__ nodes, int n,
-                                                               int cell_cap, KnnGrid* __restrict__ g) {
+// Per-block min/max of the node coordinates: part[6 * block] = (min xyz, max xyz).
+__global__ __launch_bounds__(kBoundsThreads) void k_knn_bounds_part(const double* __restrict__ nodes, int n,
+                                                                    double* __restrict__ part) {
     __shared__ double smin[3][kBoundsThreads / 64], smax[3][kBoundsThreads / 64];
     double mn[3] = {1e308, 1e308, 1e308}, mx[3] = {-1e308, -1e308, -1e308};
-    for (int i = threadIdx.x; i < n; i += kBoundsThreads)
+    for (int i = blockIdx.x * kBoundsThreads + threadIdx.x; i < n; i += gridDim.x * kBoundsThreads)
         for (int d = 0; d < 3; ++d) {
             const double v = nodes[3 * i + d];
             mn[d] = fmin(mn[d], v);
@@ -140,34 +144,50 @@ __global__ __launch_bounds__(kBoundsThreads) void k_knn_bounds(const double* __r
                 mn[d] = fmin(mn[d], smin[d][w]);
                 mx[d] = fmax(mx[d], smax[d][w]);
             }
-        double ext[3], vol = 1.0, emax = 0.0;
         for (int d = 0; d < 3; ++d) {
-            ext[d] = mx[d] - mn[d];
-            emax = fmax(emax, ext[d]);
+            part[6 * blockIdx.x + d] = mn[d];
+            part[6 * blockIdx.x + 3 + d] = mx[d];
         }
-        const double floor_ext = fmax(emax, 1e-9) * 1e-3;  // flat point sets: thin slabs
-        for (int d = 0; d < 3; ++d) vol *= fmax(ext[d], floor_ext);
-        double h = cbrt(3.0 * vol / (double)max(n, 1));
-        h = fmax(h, 1e-12);
-        int dims[3];
-        long long cells;
-        for (;;) {
-            cells = 1;
-            for (int d = 0; d < 3; ++d) {
-                dims[d] = (int)fmin(ext[d] / h, 1023.0) + 1;
-                cells *= dims[d];
-            }
-            if (cells <= cell_cap) break;
-            h *= 1.25;
-        }
-        for (int d = 0; d < 3; ++d) {
-            g->lo[d] = mn[d];
-            g->dims[d] = dims[d];
-        }
-        g->h = h;
-        g->inv_h = 1.0 / h;
-        g->ncell = (int)cells;
     }
+}
+
+// Grid shape from the block partials (one thread).
+__global__ void k_knn_setup(const double* __restrict__ part, int nparts, int n, int cell_cap, double npc,
+                            KnnGrid* __restrict__ g) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double mn[3] = {1e308, 1e308, 1e308}, mx[3] = {-1e308, -1e308, -1e308};
+    for (int b = 0; b < nparts; ++b)
+        for (int d = 0; d < 3; ++d) {
+            mn[d] = fmin(mn[d], part[6 * b + d]);
+            mx[d] = fmax(mx[d], part[6 * b + 3 + d]);
+        }
+    double ext[3], vol = 1.0, emax = 0.0;
+    for (int d = 0; d < 3; ++d) {
+        ext[d] = mx[d] - mn[d];
+        emax = fmax(emax, ext[d]);
+    }
+    const double floor_ext = fmax(emax, 1e-9) * 1e-3;  // flat point sets: thin slabs
+    for (int d = 0; d < 3; ++d) vol *= fmax(ext[d], floor_ext);
+    double h = cbrt(npc * vol / (double)max(n, 1));
+    h = fmax(h, 1e-12);
+    int dims[3];
+    long long cells;
+    for (;;) {
+        cells = 1;
+        for (int d = 0; d < 3; ++d) {
+            dims[d] = (int)fmin(ext[d] / h, 1023.0) + 1;
+            cells *= dims[d];
+        }
+        if (cells <= cell_cap) break;
+        h *= 1.25;
+    }
+    for (int d = 0; d < 3; ++d) {
+        g->lo[d] = mn[d];
+        g->dims[d] = dims[d];
+    }
+    g->h = h;
+    g->inv_h = 1.0 / h;
+    g->ncell = (int)cells;
 }
 
 __device__ __forceinline__ int knn_cell_axis(double v, const KnnGrid& g, int d) {
@@ -187,33 +207,33 @@ __global__ void k_knn_count(const double* __restrict__ nodes, int n, const KnnGr
     atomicAdd(&cnt[c], 1);
 }
 
-// exclusive scan of cnt[0..ncell) into start[0..ncell], one block
+// exclusive scan of cnt[0..ncell) into start[0..ncell], one block: per-thread chunk sums,
+// wave scans (shuffles), wave totals in LDS
 __global__ __launch_bounds__(kBoundsThreads) void k_knn_scan(const KnnGrid* __restrict__ gp,
                                                              const int* __restrict__ cnt,
                                                              int* __restrict__ start) {
-    __shared__ int part[kBoundsThreads];
+    __shared__ int wsum[kBoundsThreads / 64];
     const int nc = gp->ncell;
     const int per = (nc + kBoundsThreads - 1) / kBoundsThreads;
     const int b = threadIdx.x * per, e = min(nc, b + per);
     int s = 0;
     for (int c = b; c < e; ++c) s += cnt[c];
-    part[threadIdx.x] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int acc = 0;
-        for (int t = 0; t < kBoundsThreads; ++t) {
-            const int v = part[t];
-            part[t] = acc;
-            acc += v;
-        }
-        start[nc] = acc;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int incl = s;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
     }
+    if (lane == 63) wsum[wv] = incl;
     __syncthreads();
-    int acc = part[threadIdx.x];
+    int wbase = 0;
+    for (int w = 0; w < wv; ++w) wbase += wsum[w];
+    int acc = wbase + incl - s;
     for (int c = b; c < e; ++c) {
         start[c] = acc;
         acc += cnt[c];
     }
+    if (threadIdx.x == kBoundsThreads - 1) start[nc] = acc;
 }
 
 __global__ void k_knn_scatter(const double* __restrict__ nodes, int n, const int* __restrict__ cell_of,
@@ -324,17 +344,18 @@ __global__ void k_knn_edges(const double* __restrict__ nodes, const int32_t* __r
     }
 }
 
-// Scratch of the grid k-NN, every part 256-byte aligned: grid params | cell_of[n] |
+// Scratch of the grid k-NN, every part 256-byte aligned: grid params | bounds partials | cell_of[n] |
 // sidx[n] | sxyz[3n] | cnt[cap+1] | fill[cap+1] | start[cap+1]   (cap = max(64, n))
 struct KnnLayout {
-    size_t cell, sidx, sxyz, cnt, start, fill, bytes;
+    size_t part, cell, sidx, sxyz, cnt, start, fill, bytes;
     int cap;
 };
 KnnLayout knn_layout(int n) {
     auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
     KnnLayout L;
     L.cap = max(64, n);
-    L.cell = 256;
+    L.part = 256;                                   // kBoundsBlocks x 6 doubles (3 KB)
+    L.cell = L.part + al((size_t)kBoundsBlocks * 48);
     L.sidx = L.cell + al((size_t)n * 4);
     L.sxyz = L.sidx + al((size_t)n * 4);
     L.cnt = L.sxyz + al((size_t)n * 24);
@@ -363,7 +384,12 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
     }
     const double r2 = max_dist > 0 ? max_dist * max_dist : 1e300;
     const dim3 g256((n + 255) / 256), b256(256);
-    hipLaunchKernelGGL(k_knn_bounds, dim3(1), dim3(kBoundsThreads), 0, s, nodes, n, L.cap, g);
+    const int nb = std::max(1, std::min(kBoundsBlocks, (n + kBoundsThreads - 1) / kBoundsThreads));
+    double* part = reinterpret_cast<double*>(buf + L.part);
+    hipLaunchKernelGGL(k_knn_bounds_part, dim3(nb), dim3(kBoundsThreads), 0, s, nodes, n, part);
+    const char* npc_env = std::getenv("EPP_KNN_NPC");
+    const double npc = npc_env && *npc_env ? std::max(0.5, std::atof(npc_env)) : kNodesPerCell;
+    hipLaunchKernelGGL(k_knn_setup, dim3(1), dim3(64), 0, s, part, nb, n, L.cap, npc, g);
     hipLaunchKernelGGL(k_knn_count, g256, b256, 0, s, nodes, n, g, cell_of, cnt);
     hipLaunchKernelGGL(k_knn_scan, dim3(1), dim3(kBoundsThreads), 0, s, g, cnt, start);
     hipLaunchKernelGGL(k_knn_scatter, g256, b256, 0, s, nodes, n, cell_of, start, fill, sxyz, sidx);
