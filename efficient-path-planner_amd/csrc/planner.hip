@@ -113,7 +113,7 @@ struct KnnGrid {
 
 constexpr int kBoundsThreads = 1024;
 constexpr int kBoundsBlocks = 64;
-constexpr double kNodesPerCell = 3.0;  // mean nodes per grid cell (EPP_KNN_NPC overrides; tuning)
+constexpr double kNodesPerCell = 2.0;  // mean nodes per grid cell (EPP_KNN_NPC overrides; tuning)
 
 // Per-block min/max of the node coordinates: part[6 * block] = (min xyz, max xyz).
 __global__ __launch_bounds__(kBoundsThreads) void k_knn_bounds_part(const double* __restrict__ nodes, int n,
@@ -285,24 +285,36 @@ __global__ __launch_bounds__(256) void k_knn_grid(const KnnGrid* __restrict__ gp
                     if (x < 0 || x >= g.dims[0]) continue;
                     const int cell = (z * g.dims[1] + y) * g.dims[0] + x;
                     const int e = start[cell + 1];
-                    for (int q = start[cell]; q < e; ++q) {
-                        const int j = sidx[q];
-                        const double ddx = sxyz[3 * q] - px, ddy = sxyz[3 * q + 1] - py, ddz = sxyz[3 * q + 2] - pz;
-                        const double d = (ddx * ddx + ddy * ddy) + ddz * ddz;
-                        if (j == self || !(d < bd[K - 1] || (d == bd[K - 1] && j < bi[K - 1]))) continue;
-                        double vd = d;
-                        int vi = j;
-                        bool shift = false;
+                    // candidates four at a time: their loads are in flight together
+                    for (int q0 = start[cell]; q0 < e; q0 += 4) {
+                        double dd[4];
+                        int jj[4];
 #pragma unroll
-                        for (int k = 0; k < K; ++k) {
-                            shift = shift || vd < bd[k] || (vd == bd[k] && vi < bi[k]);
-                            if (shift) {
-                                const double td = bd[k];
-                                const int ti = bi[k];
-                                bd[k] = vd;
-                                bi[k] = vi;
-                                vd = td;
-                                vi = ti;
+                        for (int u = 0; u < 4; ++u) {
+                            const int q = min(q0 + u, e - 1);
+                            jj[u] = q0 + u < e ? sidx[q] : self;  // past the cell: skipped below
+                            const double ddx = sxyz[3 * q] - px, ddy = sxyz[3 * q + 1] - py, ddz = sxyz[3 * q + 2] - pz;
+                            dd[u] = (ddx * ddx + ddy * ddy) + ddz * ddz;
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const double d = dd[u];
+                            const int j = jj[u];
+                            if (j == self || !(d < bd[K - 1] || (d == bd[K - 1] && j < bi[K - 1]))) continue;
+                            double vd = d;
+                            int vi = j;
+                            bool shift = false;
+#pragma unroll
+                            for (int k = 0; k < K; ++k) {
+                                shift = shift || vd < bd[k] || (vd == bd[k] && vi < bi[k]);
+                                if (shift) {
+                                    const double td = bd[k];
+                                    const int ti = bi[k];
+                                    bd[k] = vd;
+                                    bi[k] = vi;
+                                    vd = td;
+                                    vi = ti;
+                                }
                             }
                         }
                     }

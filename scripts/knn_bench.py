@@ -19,7 +19,7 @@ nodes = synth.sample_states(5, [-6, -6, 0], [6, 6, 2], 63000)
 d_n = capi.DeviceBuffer.from_array(nodes)
 d_k = capi.DeviceBuffer(4 * 16 * len(nodes))
 ref = capi.knn(nodes, 16, method="brute")
-for npc in ("2", "3", "4"):
+for npc in ("1.5", "2", "3"):
     os.environ["EPP_KNN_NPC"] = npc
     f = lambda r: capi.check(L.epp_knn_grid(d_n.ptr, len(nodes), 16, 0.0, d_k.ptr, st))  # noqa: E731
     f(0)
