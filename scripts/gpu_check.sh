@@ -34,6 +34,6 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_$c -o run -- python3 bench.py --no-cpu --no-side --no-plan > gpurun_out/pmc_$c.json 2> gpurun_out/pmc_$c.err; rc=$?
   tail -2 gpurun_out/pmc_$c.err; stop_on_fault $rc pmc_$c
 done
-python3 scripts/profile_summary.py gpurun_out ${TAG:-r01} > gpurun_out/profile_summary.log 2>&1; cat gpurun_out/profile_summary.log
-cp gpurun_out/bench.json profiles/${TAG:-r01}_bench.json
+# (summaries are written locally afterwards — only gpurun_out/ comes back from the box:
+#   python3 scripts/profile_summary.py gpurun_out rNN && cp gpurun_out/bench.json profiles/rNN_bench.json)
 echo done
