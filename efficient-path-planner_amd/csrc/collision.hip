@@ -1074,7 +1074,7 @@ __global__ __launch_bounds__(kBlock4) void k_states_v4(const WorldView* __restri
 constexpr int kBlock5 = 1024;  // threads per workgroup (BLOCK template default)
 struct WaveQueue5 {
     double x[64], y[64], z[64];
-    uint32_t pair[64];  // queue slot << 20 | index into the list ids
+    uint32_t pair[128];  // segment heads of the (state, candidate) pairs
     uint16_t cls[64];
     uint8_t hit[64];
 };
@@ -1094,7 +1094,10 @@ __device__ __forceinline__ uint32_t cell_axis5(double p, float off, float inv, u
 // XCC_ID | needy states << 32)
 // PREFETCH: groups per lane > 1 (the next group's loads overlap this one's work);
 // single-pass launches (e.g. 1M states on 256 CUs) drop the second buffer's registers.
-template <bool MINDIST, bool COMPACT, bool TL, int BLOCK, bool PREFETCH>
+// SPL: states per lane and group (4: 96 B = six 16-B loads, 8: 192 B = twelve); one
+// flag store of SPL bytes.  More states per lane = fewer waves, i.e. fewer executions
+// of the per-wave fixed costs (setup, staging, the exact path).
+template <bool MINDIST, bool COMPACT, bool TL, int BLOCK, bool PREFETCH, int SPL>
 __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict__ wv,
                                                      const double* xyz, int64_t groups, int64_t n,
                                                      int can_pass, double md, uint8_t* __restrict__ valid,
@@ -1117,15 +1120,16 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
     const int64_t stride = (int64_t)gridDim.x * BLOCK;
     const int64_t gfirst = (int64_t)blockIdx.x * BLOCK;
     int64_t g = gfirst + threadIdx.x;
-    double va[12], vb[12];
+    constexpr int NV = 3 * SPL;  // doubles per group
+    double va[NV], vb[NV];
     // (no full group: loads read the WorldView instead, >= 96 bytes, ignored)
     const double* xyzb = groups > 0 ? xyz : reinterpret_cast<const double*>(wv);
-    auto load = [&](int64_t grp, double (&dst)[12]) {
+    auto load = [&](int64_t grp, double (&dst)[NV]) {
         grp = grp < groups ? grp : groups - 1;
         grp = grp < 0 ? 0 : grp;
-        const double2* q = reinterpret_cast<const double2*>(xyzb) + 6 * grp;
+        const double2* q = reinterpret_cast<const double2*>(xyzb) + (NV / 2) * grp;
 #pragma unroll
-        for (int k = 0; k < 6; ++k) {
+        for (int k = 0; k < NV / 2; ++k) {
             const double2 t = q[k];
             dst[2 * k] = t.x;
             dst[2 * k + 1] = t.y;
@@ -1177,16 +1181,16 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
                        cz = cell_axis5(pz, oz, iz, nz - 1);
         return (uint32_t)cls_tab[__umul24(__umul24(cz, ny) + cy, nx) + cx];
     };
-    auto process = [&](int64_t gg, const double (&v)[12]) {
+    auto process = [&](int64_t gg, const double (&v)[NV]) {
         const bool live = gg < groups;
-        uint32_t c[4];
-        bool needy[4];
-        unsigned long long b[4];
-        uint32_t base[4], total = 0;
+        uint32_t c[SPL];
+        bool needy[SPL];
+        unsigned long long b[SPL];
+        uint32_t base[SPL], total = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) c[k] = cls_of(v[3 * k], v[3 * k + 1], v[3 * k + 2]);
+        for (int k = 0; k < SPL; ++k) c[k] = cls_of(v[3 * k], v[3 * k + 1], v[3 * k + 2]);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < SPL; ++k) {
             needy[k] = live & (c[k] != 0u);
             b[k] = __ballot(needy[k]);
             base[k] = total;
@@ -1199,15 +1203,15 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
         uint32_t hits = 0;
         if (fast == 2) {  // ablation (diagnostics only, wrong answers): needy states count as hits
 #pragma unroll
-            for (int k = 0; k < 4; ++k) hits |= needy[k] ? 1u << k : 0u;
+            for (int k = 0; k < SPL; ++k) hits |= needy[k] ? 1u << k : 0u;
         } else if (total > 0) {  // wave-uniform
-            uint32_t pos[4];
+            uint32_t pos[SPL];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) pos[k] = base[k] + lanes_below(b[k]);
+            for (int k = 0; k < SPL; ++k) pos[k] = base[k] + lanes_below(b[k]);
             // queue the needy states (slot = rank in the wave), rounds of 64
             for (uint32_t r0 = 0; r0 < total; r0 += 64) {
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
+                for (int k = 0; k < SPL; ++k) {
                     const uint32_t slot = pos[k] - r0;
                     if (needy[k] && slot < 64u) {
                         qu->x[slot] = v[3 * k];
@@ -1225,22 +1229,37 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
                 uint32_t ptot;
                 const uint32_t poff = wave_excl_scan(cnt, lane, ptot);
                 bool hit_e = false;
-                if (fast && ptot <= 64u) {
-                    // one (state, candidate) pair per lane: lane q finds its state as the
-                    // max-scan of segment heads (state e marks position poff_e)
+                if (fast && ptot <= 128u) {
+                    // one (state, candidate) pair per lane and round (two rounds at most):
+                    // pair q finds its state as the max-scan of segment heads (state e
+                    // marks position poff_e); hits come back by ballot
                     qu->pair[lane] = 0u;
+                    qu->pair[64 + lane] = 0u;
                     if (act) qu->pair[poff] = (uint32_t)lane;  // cnt >= 1 for queued states
                     wave_lds_sync();
-                    const uint32_t e = dpp_incl_max(qu->pair[lane]);
-                    const uint32_t pe = (uint32_t)__shfl((int)poff, (int)e, 64);
-                    const uint32_t fe = (uint32_t)__shfl((int)first, (int)e, 64);
-                    bool h = false;
-                    if ((uint32_t)lane < ptot)
-                        h = rec_hit<MINDIST>(recs + (size_t)ids_all[fe + (uint32_t)lane - pe] * kRecDoubles, rg, ro,
-                                             qu->x[e], qu->y[e], qu->z[e], can_pass != 0, md);
-                    const unsigned long long m = __ballot(h);
-                    const unsigned long long msk = cnt >= 64u ? ~0ull : ((1ull << cnt) - 1ull);
-                    hit_e = act && ((m >> poff) & msk) != 0ull;
+                    const uint32_t e0 = dpp_incl_max(qu->pair[lane]);
+                    auto test = [&](uint32_t e, uint32_t q) {
+                        const uint32_t pe = (uint32_t)__shfl((int)poff, (int)e, 64);
+                        const uint32_t fe = (uint32_t)__shfl((int)first, (int)e, 64);
+                        return q < ptot && rec_hit<MINDIST>(recs + (size_t)ids_all[fe + q - pe] * kRecDoubles, rg, ro,
+                                                            qu->x[e], qu->y[e], qu->z[e], can_pass != 0, md);
+                    };
+                    const unsigned long long m0 = __ballot(test(e0, (uint32_t)lane));
+                    unsigned long long m1 = 0ull;
+                    if (ptot > 64u) {  // wave-uniform
+                        const uint32_t carry = (uint32_t)__builtin_amdgcn_readlane((int)e0, 63);
+                        const uint32_t e1 = max(dpp_incl_max(qu->pair[64 + lane]), carry);
+                        m1 = __ballot(test(e1, 64u + (uint32_t)lane));
+                    }
+                    // any hit among this state's pairs [poff, poff + cnt) of the 128-bit mask
+                    auto bits = [](unsigned long long m, uint32_t from, uint32_t len) {
+                        const unsigned long long msk = len >= 64u ? ~0ull : ((1ull << len) - 1ull);
+                        return ((m >> from) & msk) != 0ull;
+                    };
+                    const uint32_t end = poff + cnt;
+                    const bool lo = poff < 64u && bits(m0, poff, min(end, 64u) - poff);
+                    const bool hi = end > 64u && bits(m1, poff > 64u ? poff - 64u : 0u, end - max(poff, 64u));
+                    hit_e = act && (lo || hi);
                 } else if (act) {  // long lists: each queued state walks its own
                     hit_e = states_exact_rec<MINDIST>(lds_blob, lists_off, ids_off, rg, ro, qu->x[lane], qu->y[lane],
                                                       qu->z[lane], qu->cls[lane], can_pass, md);
@@ -1248,7 +1267,7 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
                 // back to the owners: state slot r0 + e lives on lane e
                 const unsigned long long hm = __ballot(hit_e);
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
+                for (int k = 0; k < SPL; ++k) {
                     const uint32_t slot = pos[k] - r0;
                     if (needy[k] && slot < 64u && ((hm >> slot) & 1ull)) hits |= 1u << k;
                 }
@@ -1257,10 +1276,18 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
             if (TL && tl_item == 0) mark(5);
         }
         if (TL) ++tl_item;
-        const uint32_t fl = live ? (~hits & 15u) : 0u;  // bit k: state 4 gg + k valid
-        if (live)
-            *reinterpret_cast<uint32_t*>(valid + 4 * gg) =
-                (fl & 1u) | ((fl & 2u) << 7) | ((fl & 4u) << 14) | ((fl & 8u) << 21);
+        const uint32_t fl = live ? (~hits & ((1u << SPL) - 1u)) : 0u;  // bit k: state SPL gg + k valid
+        if (live) {
+            if (SPL == 4) {
+                *reinterpret_cast<uint32_t*>(valid + 4 * gg) =
+                    (fl & 1u) | ((fl & 2u) << 7) | ((fl & 4u) << 14) | ((fl & 8u) << 21);
+            } else {
+                unsigned long long w = 0ull;
+#pragma unroll
+                for (int k = 0; k < SPL; ++k) w |= (unsigned long long)((fl >> k) & 1u) << (8 * k);
+                *reinterpret_cast<unsigned long long*>(valid + SPL * gg) = w;
+            }
+        }
         if (COMPACT) {  // wave-ballot compaction
             const uint32_t cnt = (uint32_t)__popc(fl);
             uint32_t ctot;
@@ -1270,8 +1297,8 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
             wbase = __shfl(wbase, 0, 64);
             uint64_t p = wbase + cex;
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if ((fl >> k) & 1u) compact_idx[p++] = (int32_t)(4 * gg + k);
+            for (int k = 0; k < SPL; ++k)
+                if ((fl >> k) & 1u) compact_idx[p++] = (int32_t)(SPL * gg + k);
         }
     };
     // block-uniform trip count; the next group's loads are issued before this one is
@@ -1300,8 +1327,8 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
             tl[gwave * 8 + 7] = xcc | ((unsigned long long)tl_needy << 32);
         }
     }
-    if (blockIdx.x == 0 && threadIdx.x < (int)(n - 4 * groups)) {  // tail: the last n % 4 states
-        const int64_t i = 4 * groups + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < (int)(n - SPL * groups)) {  // tail: the last n % SPL states
+        const int64_t i = SPL * groups + threadIdx.x;
         const double px = xyz[3 * i], py = xyz[3 * i + 1], pz = xyz[3 * i + 2];
         const uint32_t c = cls_of(px, py, pz);
         const bool ok = !(c != 0u && states_exact_rec<MINDIST>(lds_blob, lists_off, ids_off, rg, ro, px, py, pz, c,
@@ -1481,35 +1508,47 @@ epp_status launch_states(const WorldView& w, const WorldView* dw, const double* 
     const int impl = env_int("EPP_STATES_IMPL", 5);
     if (impl == 5 && v5_fits(w) && (reinterpret_cast<uintptr_t>(xyz) & 15) == 0 &&
         (reinterpret_cast<uintptr_t>(valid) & 3) == 0) {
-        const int64_t g5 = n / 4;
         const uint32_t sb = w.blob_bytes - w.off_aos;
         const int fast = env_int("EPP_V5_PAIRS", 1);
-        // single pass: 1024-thread workgroups; multi-pass (prefetching): 512 (VGPR budget)
-        const bool single = g5 <= (int64_t)v5_cap() * 1024;
-        const int bs = v5_block(single ? 1024 : 512);
-        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((g5 + bs - 1) / bs, v5_cap()));
-        const bool pf = g5 > (int64_t)grid * bs;  // more than one group per lane
-#define EPP_LAUNCH_V5(C, T, B, P)                                                                                \
-    do {                                                                                                         \
-        allow_lds(k_states_v5<MINDIST, C, T, B, P>, queue5_bytes<B>());                                          \
-        hipLaunchKernelGGL((k_states_v5<MINDIST, C, T, B, P>), dim3(grid), dim3(B), sb + 16, st, dw, xyz, g5, n,  \
-                           can_pass, md, valid, compact_idx, nv, sb, fast, tl);                                  \
+        // single pass over the states: 8 states per lane in 512-thread workgroups (half
+        // the waves of 4 per lane: fewer executions of the per-wave fixed costs); more
+        // than one pass: 4 per lane with the next group prefetched
+        const int64_t cap = v5_cap();
+        const bool spl8 = env_int("EPP_V5_SPL", 4) == 8 && (reinterpret_cast<uintptr_t>(valid) & 7) == 0 &&
+                          n / 8 <= cap * 512;
+        const int spl = spl8 ? 8 : 4;
+        const int64_t gN = n / spl;
+        const bool single = gN <= cap * (spl8 ? 512 : 1024);
+        const int bs = v5_block(spl8 ? 512 : (single ? 1024 : 512));
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((gN + bs - 1) / bs, cap));
+        const bool pf = gN > (int64_t)grid * bs;  // more than one group per lane
+#define EPP_LAUNCH_V5(C, T, B, P, S)                                                                              \
+    do {                                                                                                          \
+        allow_lds(k_states_v5<MINDIST, C, T, B, P, S>, queue5_bytes<B>());                                        \
+        hipLaunchKernelGGL((k_states_v5<MINDIST, C, T, B, P, S>), dim3(grid), dim3(B), sb + 16, st, dw, xyz, gN, n, \
+                           can_pass, md, valid, compact_idx, nv, sb, fast, tl);                                   \
     } while (0)
-#define EPP_LAUNCH_V5B(B)                                          \
-    do {                                                           \
-        if (pf) {                                                  \
-            if (tl) EPP_LAUNCH_V5(false, true, B, true);           \
-            else if (compact_idx) EPP_LAUNCH_V5(true, false, B, true); \
-            else EPP_LAUNCH_V5(false, false, B, true);             \
-        } else {                                                   \
-            if (tl) EPP_LAUNCH_V5(false, true, B, false);          \
-            else if (compact_idx) EPP_LAUNCH_V5(true, false, B, false); \
-            else EPP_LAUNCH_V5(false, false, B, false);            \
-        }                                                          \
+#define EPP_LAUNCH_V5B(B, S)                                          \
+    do {                                                              \
+        if (pf) {                                                     \
+            if (tl) EPP_LAUNCH_V5(false, true, B, true, S);           \
+            else if (compact_idx) EPP_LAUNCH_V5(true, false, B, true, S); \
+            else EPP_LAUNCH_V5(false, false, B, true, S);             \
+        } else {                                                      \
+            if (tl) EPP_LAUNCH_V5(false, true, B, false, S);          \
+            else if (compact_idx) EPP_LAUNCH_V5(true, false, B, false, S); \
+            else EPP_LAUNCH_V5(false, false, B, false, S);            \
+        }                                                             \
     } while (0)
-        if (bs == 256) EPP_LAUNCH_V5B(256);
-        else if (bs == 512) EPP_LAUNCH_V5B(512);
-        else EPP_LAUNCH_V5B(1024);
+        if (spl8) {
+            EPP_LAUNCH_V5B(512, 8);
+        } else if (bs == 256) {
+            EPP_LAUNCH_V5B(256, 4);
+        } else if (bs == 512) {
+            EPP_LAUNCH_V5B(512, 4);
+        } else {
+            EPP_LAUNCH_V5B(1024, 4);
+        }
 #undef EPP_LAUNCH_V5B
 #undef EPP_LAUNCH_V5
         return launch_error(MINDIST ? "epp_check_states_mindist" : "epp_check_states");
@@ -1626,9 +1665,12 @@ epp_status epp_dbg_states_timeline(const epp_world* world, const double* xyz, in
     if (impl == 5 && v5_fits(w) && (reinterpret_cast<uintptr_t>(xyz) & 15) == 0 &&
         (reinterpret_cast<uintptr_t>(valid) & 3) == 0)
         *grid_waves = [&] {
-            const int64_t g5 = n / 4;
-            const int bs = v5_block(g5 <= (int64_t)v5_cap() * 1024 ? 1024 : 512);
-            return (int)std::max<int64_t>(1, std::min<int64_t>((g5 + bs - 1) / bs, v5_cap())) * (bs / 64);
+            const int64_t cap = v5_cap();
+            const bool spl8 = env_int("EPP_V5_SPL", 4) == 8 && (reinterpret_cast<uintptr_t>(valid) & 7) == 0 &&
+                              n / 8 <= cap * 512;
+            const int64_t gN = n / (spl8 ? 8 : 4);
+            const int bs = v5_block(spl8 ? 512 : (gN <= cap * 1024 ? 1024 : 512));
+            return (int)std::max<int64_t>(1, std::min<int64_t>((gN + bs - 1) / bs, cap)) * (bs / 64);
         }();
     else if (impl >= 3)  // (the timeline runs k_states_v3 for impl 4 too)
         *grid_waves = v3_grid(w, n) * (kBlock3 / 64);

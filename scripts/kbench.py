@@ -91,6 +91,7 @@ def main():
         run(f"c2_impl{impl}", w2, d, e)
         big(f"c2_impl{impl}_16M", w2, e)
         run(f"c2_impl{impl}_empty_world", w0, d, e)
+    run("c2_impl5_spl8", w2, d, {"EPP_STATES_IMPL": 5, "EPP_V5_SPL": 8})
     run("c2_impl5_b512", w2, d, {"EPP_STATES_IMPL": 5, "EPP_V5_BLOCK": 512})
     big("c2_impl5_b1024_16M", w2, {"EPP_STATES_IMPL": 5, "EPP_V5_BLOCK": 1024})
     run("c2_impl5_b256", w2, d, {"EPP_STATES_IMPL": 5, "EPP_V5_BLOCK": 256})

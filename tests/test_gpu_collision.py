@@ -91,7 +91,7 @@ def test_states_mindist(geom, worlds, name):
         assert np.array_equal(got, exp), md
 
 
-@pytest.mark.parametrize("impl", ["0", "1", "3", "4", "5", "5walk", "5b512"])
+@pytest.mark.parametrize("impl", ["0", "1", "3", "4", "5", "5walk", "5b512", "5spl8"])
 @pytest.mark.parametrize("name", ["c2", "c3"])
 def test_states_every_kernel_variant(geom, worlds, name, impl, monkeypatch):
     """Each k_states variant (EPP_STATES_IMPL; 5 = default, falls back when its staged
@@ -100,6 +100,7 @@ def test_states_every_kernel_variant(geom, worlds, name, impl, monkeypatch):
     monkeypatch.setenv("EPP_STATES_IMPL", impl[0])
     monkeypatch.setenv("EPP_V5_PAIRS", "0" if impl.endswith("walk") else "1")
     monkeypatch.setenv("EPP_V5_BLOCK", "512" if impl.endswith("b512") else "1024")
+    monkeypatch.setenv("EPP_V5_SPL", "8" if impl.endswith("spl8") else "4")
     impl = int(impl[0])
     rg, ro, ws = worlds
     gates, obstacles, (lo, hi) = ws[name]
