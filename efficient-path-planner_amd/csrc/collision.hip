@@ -1368,6 +1368,168 @@ __global__ __launch_bounds__(kBlock) void k_motions(WorldView w, const double* _
     }
 }
 
+// ---- k_motions_v2: motion checks out of LDS ----------------------------------------
+// The coarse grid (occupancy masks, cell starts, cell lists) and the AoS OBB records are
+// staged into LDS once per persistent workgroup; one edge per lane per iteration.  Every
+// candidate test is branch-free on LDS data: all record fields are read up front, so a
+// candidate costs one LDS round trip instead of the short-circuit chain of dependent
+// global loads of k_motions.  Same candidate order, de-duplication (first common cell)
+// and predicates as ray_valid / ray_valid_d32 (src/World.cpp:130-162, src/OBB.cpp:10-91).
+constexpr int kBlockM = 512;
+
+// OBB::checkCollisionWithRay (src/OBB.cpp:10-61) on one AoS record, branch-free.  `r` is
+// the owner's inflation radius; the endpoint tests inflate only collision OBBs (:13-14),
+// the slab test always (:28).  Axes are processed in order with the reference's min /
+// max selects; an axis after a rejection cannot undo it, so evaluating every axis and
+// combining the rejections gives the reference's early-return answer.
+__device__ __forceinline__ bool rec_ray_hit(const double* rec, const double s[3], const double e[3], double r) {
+    double f[kRecDoubles];
+#pragma unroll
+    for (int k = 0; k <= F_HZ; ++k) f[k] = rec[k];
+    f[R_META] = rec[R_META];
+    const uint32_t m = (uint32_t)__double_as_longlong(f[R_META]);
+    const bool fill = (m & META_FILLING) != 0u;
+    const double c = f[F_COS], sn = f[F_SIN];
+    const double cx = f[F_CX], cy = f[F_CY], cz = f[F_CZ];
+    const double h[3] = {f[F_HX], f[F_HY], f[F_HZ]};
+    // endpoint tests  :13-18 (OBB::checkCollisionWithPoint, inflated iff collision)
+    const double ph0 = fill ? h[0] : h[0] + r, ph1 = fill ? h[1] : h[1] + r, ph2 = fill ? h[2] : h[2] + r;
+    double ls[3], ld[3];
+    bool end_hit;
+    {
+        const double dx = s[0] - cx, dy = s[1] - cy, dz = s[2] - cz;
+        ls[0] = c * dx + sn * dy;
+        ls[1] = c * dy - sn * dx;
+        ls[2] = dz;
+        const double ex = e[0] - cx, ey = e[1] - cy, ez = e[2] - cz;
+        const double le0 = c * ex + sn * ey, le1 = c * ey - sn * ex;
+        end_hit = ((fabs(ls[0]) <= ph0) & (fabs(ls[1]) <= ph1) & (fabs(dz) <= ph2)) |
+                  ((fabs(le0) <= ph0) & (fabs(le1) <= ph1) & (fabs(ez) <= ph2));
+        ld[0] = le0 - ls[0];  // localEnd - localStart  :23
+        ld[1] = le1 - ls[1];
+        ld[2] = ez - ls[2];
+    }
+    double tMin = 0.0, tMax = 1.0;
+    bool rejected = false;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double ih = h[k] + r;  // always inflated  :28
+        const double bmin = -ih, bmax = ih;
+        const bool par = fabs(ld[k]) < 1e-6;  // :34
+        const bool outside = (ls[k] < bmin) | (ls[k] > bmax);
+        const double invD = 1.0 / ld[k];  // :44 (unused when par)
+        const double t1 = (bmin - ls[k]) * invD;
+        const double t2 = (bmax - ls[k]) * invD;
+        const double tEntry = (t2 < t1) ? t2 : t1;  // std::min
+        const double tExit = (t1 < t2) ? t2 : t1;   // std::max
+        const double nMin = (tMin < tEntry) ? tEntry : tMin;
+        const double nMax = (tExit < tMax) ? tExit : tMax;
+        rejected = rejected | (par & outside) | (!par & (nMin > nMax));
+        tMin = par ? tMin : nMin;
+        tMax = par ? tMax : nMax;
+    }
+    const bool slab_hit = !rejected & (0 <= tMin) & (tMin <= 1) & (0 <= tMax) & (tMax <= 1);  // :60
+    return end_hit | slab_hit;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlockM) void k_motions_v2(const WorldView* __restrict__ wv, const double* __restrict__ s1,
+                                                        const double* __restrict__ s2, int64_t n, int can_pass,
+                                                        uint8_t* __restrict__ valid, uint32_t front_bytes,
+                                                        uint32_t rec_bytes) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    // [0, front_bytes): masks, cell starts, cell lists (the blob up to `meta`);
+    // [front_bytes, + rec_bytes): the AoS records
+    {
+        const uint4* src0 = reinterpret_cast<const uint4*>(wv->blob);
+        const uint4* src1 = reinterpret_cast<const uint4*>(wv->blob + wv->off_aos);
+        uint4* dst = reinterpret_cast<uint4*>(lds);
+        for (uint32_t o = threadIdx.x; o < front_bytes / 16; o += kBlockM) dst[o] = src0[o];
+        uint4* dst1 = reinterpret_cast<uint4*>(lds + front_bytes);
+        for (uint32_t o = threadIdx.x; o < rec_bytes / 16; o += kBlockM) dst1[o] = src1[o];
+    }
+    const unsigned long long* mask = reinterpret_cast<const unsigned long long*>(lds + wv->off_cell_mask);
+    const uint32_t* cs = reinterpret_cast<const uint32_t*>(lds + wv->off_cell_start);
+    const uint16_t* co = reinterpret_cast<const uint16_t*>(lds + wv->off_cell_obb);
+    const double* recs = reinterpret_cast<const double*>(lds + front_bytes);
+    const int nx = wv->nx, ny = wv->ny, nz = wv->nz;
+    const double gx0 = wv->gx0, gy0 = wv->gy0, gz0 = wv->gz0, gx1 = wv->gx1, gy1 = wv->gy1, gz1 = wv->gz1;
+    const float ofx = wv->ofx, ofy = wv->ofy, ofz = wv->ofz, i4x = wv->i4x, i4y = wv->i4y, i4z = wv->i4z;
+    const float limx = wv->limx, limy = wv->limy, limz = wv->limz;
+    const float fmx = wv->fmaxx, fmy = wv->fmaxy, fmz = wv->fmaxz;
+    const double rg = wv->r_gate, ro = wv->r_obst;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * kBlockM;
+    for (int64_t i = (int64_t)blockIdx.x * kBlockM + threadIdx.x; i < n; i += stride) {
+        const double s[3] = {s1[3 * i], s1[3 * i + 1], s1[3 * i + 2]};
+        const double e[3] = {s2[3 * i], s2[3 * i + 1], s2[3 * i + 2]};
+        bool ok = true;
+        if (MODE == 0) {
+            // World::checkRayValid — rtree intersects(rayBox): closed AABB overlap
+            double lo[3], hi[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = (e[k] < s[k]) ? e[k] : s[k];
+                hi[k] = (s[k] < e[k]) ? e[k] : s[k];
+            }
+            if (!(hi[0] < gx0 || gx1 < lo[0] || hi[1] < gy0 || gy1 < lo[1] || hi[2] < gz0 || gz1 < lo[2])) {
+                const int x0 = fine_index(fine_coord(lo[0], ofx, i4x), nx) >> 2;
+                const int x1 = fine_index(fine_coord(hi[0], ofx, i4x), nx) >> 2;
+                const int y0 = fine_index(fine_coord(lo[1], ofy, i4y), ny) >> 2;
+                const int y1 = fine_index(fine_coord(hi[1], ofy, i4y), ny) >> 2;
+                const int z0 = fine_index(fine_coord(lo[2], ofz, i4z), nz) >> 2;
+                const int z1 = fine_index(fine_coord(hi[2], ofz, i4z), nz) >> 2;
+                for (int z = z0; z <= z1 && ok; ++z)
+                    for (int y = y0; y <= y1 && ok; ++y)
+                        for (int x = x0; x <= x1 && ok; ++x) {
+                            const int cell = (z * ny + y) * nx + x;
+                            const uint32_t b = cs[cell], en = cs[cell + 1];
+                            for (uint32_t k = b; k < en; ++k) {
+                                const double* rec = recs + (size_t)co[k] * kRecDoubles;
+                                const uint32_t m = (uint32_t)__double_as_longlong(rec[R_META]);
+                                const int ox = (m >> 8) & 255, oy = (m >> 16) & 255, oz = m >> 24;
+                                // tested once: in the first cell its and the ray's ranges share
+                                const bool first = x == (ox > x0 ? ox : x0) && y == (oy > y0 ? oy : y0) &&
+                                                   z == (oz > z0 ? oz : z0);
+                                const bool overlap = !(rec[F_HIX] < lo[0] || hi[0] < rec[F_LOX] || rec[F_HIY] < lo[1] ||
+                                                       hi[1] < rec[F_LOY] || rec[F_HIZ] < lo[2] || hi[2] < rec[F_LOZ]);
+                                const bool skip = (m & META_FILLING) && can_pass;  // :150-153
+                                if (first && overlap && !skip &&
+                                    rec_ray_hit(rec, s, e, (m & META_GATE) ? rg : ro)) {
+                                    ok = false;
+                                    break;
+                                }
+                            }
+                        }
+            }
+        } else {
+            // discrete32: x = s + (e - s) * (k/32), k = 1..32 (World::checkPointValidity each)
+            for (int k = 1; k <= 32 && ok; ++k) {
+                const double t = (double)k / 32.0;
+                const double px = s[0] + (e[0] - s[0]) * t;
+                const double py = s[1] + (e[1] - s[1]) * t;
+                const double pz = s[2] + (e[2] - s[2]) * t;
+                const float fx = fine_coord(px, ofx, i4x), fy = fine_coord(py, ofy, i4y), fz = fine_coord(pz, ofz, i4z);
+                const bool in = (fx >= 0.0f) & (fx <= limx) & (fy >= 0.0f) & (fy <= limy) & (fz >= 0.0f) & (fz <= limz);
+                const int ix = (int)fminf(fmaxf(fx, 0.0f), fmx);
+                const int iy = (int)fminf(fmaxf(fy, 0.0f), fmy);
+                const int iz = (int)fminf(fmaxf(fz, 0.0f), fmz);
+                const int cell = ((iz >> 2) * ny + (iy >> 2)) * nx + (ix >> 2);
+                const uint32_t bit = (uint32_t)((((iz & 3) << 2) + (iy & 3)) * 4 + (ix & 3));
+                const bool occ = in && ((mask[cell] >> bit) & 1ull);
+                if (!occ) continue;
+                const uint32_t b = cs[cell], en = cs[cell + 1];
+                for (uint32_t q = b; q < en; ++q)
+                    if (rec_hit<false>(recs + (size_t)co[q] * kRecDoubles, rg, ro, px, py, pz, can_pass != 0, 0.0)) {
+                        ok = false;
+                        break;
+                    }
+            }
+        }
+        valid[i] = ok ? 1 : 0;
+    }
+}
+
 struct DevInfo {
     int cus = 256;
     bool init = false;
@@ -1689,6 +1851,28 @@ epp_status epp_check_motions(const epp_world* world, const double* s1, const dou
     }
     if (n == 0) return EPP_OK;
     const WorldView& w = world_view(world);
+    hipStream_t st0 = (hipStream_t)stream;
+    {
+        // LDS-resident variant: coarse grid + lists (blob up to `meta`) and the records
+        const uint32_t front = w.off_meta;
+        const uint32_t recb = (uint32_t)(((size_t)w.n_obb * kRecDoubles * 8 + 15) & ~size_t(15));
+        if (env_int("EPP_MOTIONS_IMPL", 2) == 2 && front % 16 == 0 && front + recb <= 160u * 1024u &&
+            !env_int("EPP_NO_LDS", 0)) {
+            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + kBlockM - 1) / kBlockM, (int64_t)cu_count() *
+                                                    std::max(1, (int)((160u * 1024u) / (front + recb)))));
+            const WorldView* dw = world_dview(world);
+            if (mode == 0) {
+                allow_lds(k_motions_v2<0>);
+                hipLaunchKernelGGL((k_motions_v2<0>), dim3(grid), dim3(kBlockM), front + recb, st0, dw, s1, s2, n,
+                                   can_pass_gate, valid, front, recb);
+            } else {
+                allow_lds(k_motions_v2<1>);
+                hipLaunchKernelGGL((k_motions_v2<1>), dim3(grid), dim3(kBlockM), front + recb, st0, dw, s1, s2, n,
+                                   can_pass_gate, valid, front, recb);
+            }
+            return launch_error("epp_check_motions");
+        }
+    }
     const int aligned =
         ((reinterpret_cast<uintptr_t>(s1) | reinterpret_cast<uintptr_t>(s2)) & 15) == 0;
     const int64_t groups = (n + 3) / 4;

@@ -128,9 +128,13 @@ def test_compaction(geom, worlds):
     assert np.array_equal(np.sort(idx), np.flatnonzero(exp))
 
 
+@pytest.mark.parametrize("impl", ["2", "1"])
 @pytest.mark.parametrize("name", ["c1", "c2", "c3"])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_motions_bit_exact(geom, worlds, name, mode):
+def test_motions_bit_exact(geom, worlds, name, mode, impl, monkeypatch):
+    """k_motions_v2 (LDS-resident, default) and k_motions (EPP_MOTIONS_IMPL=1) vs the
+    oracle; includes edges parallel to an axis within the 1e-6 threshold."""
+    monkeypatch.setenv("EPP_MOTIONS_IMPL", impl)
     rg, ro, ws = worlds
     gates, obstacles, (lo, hi) = ws[name]
     ref = O.world_build(geom, gates, obstacles, rg, ro)
