@@ -68,48 +68,45 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     ThreadScratch& ts = ThreadScratch::get();
     void* st = ts.stream();
     const auto t_dev0 = std::chrono::steady_clock::now();
-    // ---- 1. sample + validate states (StateValidator::isValid) --------------------------
+    // ---- 1. sample + validate states (StateValidator::isValid), all on the device ------
+    // nodes = start, goal, then the valid samples in sample order (ordered compaction)
     const size_t n_s = (size_t)samples;
-    ts.reset(ThreadScratch::rounded(n_s * 24) + ThreadScratch::rounded(n_s));
+    const size_t max_nodes = n_s + 2;
+    const size_t m_max = max_nodes * (size_t)k;
+    const size_t ws_bytes = (size_t)epp_knn_workspace_size((int32_t)max_nodes);
+    ts.reset(ThreadScratch::rounded(n_s * 24) + ThreadScratch::rounded(n_s) + ThreadScratch::rounded(max_nodes * 24) +
+             ThreadScratch::rounded(8) + ThreadScratch::rounded(m_max * 4) + 2 * ThreadScratch::rounded(m_max * 24) +
+             ThreadScratch::rounded(m_max) + ThreadScratch::rounded(ws_bytes));
     double* d_s = static_cast<double*>(ts.carve(n_s * 24));
     uint8_t* d_v = static_cast<uint8_t*>(ts.carve(n_s));
+    double* d_nodes = static_cast<double*>(ts.carve(max_nodes * 24));
+    int64_t* d_cnt = static_cast<int64_t*>(ts.carve(8));
+    int32_t* d_nbr = static_cast<int32_t*>(ts.carve(m_max * 4));
+    double* d_e1 = static_cast<double*>(ts.carve(m_max * 24));
+    double* d_e2 = static_cast<double*>(ts.carve(m_max * 24));
+    uint8_t* d_ev = static_cast<uint8_t*>(ts.carve(m_max));
+    void* d_ws = ts.carve(ws_bytes);
     const double lo[3] = {wp.lowerBound.x, wp.lowerBound.y, wp.lowerBound.z};
     const double hi[3] = {wp.upperBound.x, wp.upperBound.y, wp.upperBound.z};
+    const double ends[6] = {start.x, start.y, start.z, goal.x, goal.y, goal.z};
     check(epp_sample_uniform(seed, lo, hi, samples, 0, d_s, st), "sample");
     check(epp_check_states(w, d_s, samples, canPass ? 1 : 0, d_v, nullptr, nullptr, st), "state check");
-    // per-thread host staging, reused across calls (no per-call zero fill of MBs)
-    thread_local std::vector<double> xyz;
-    thread_local std::vector<uint8_t> valid;
-    xyz.resize(n_s * 3);
-    valid.resize(n_s);
-    check(epp_memcpy_d2h(xyz.data(), d_s, n_s * 24, st), "download");
-    check(epp_memcpy_d2h(valid.data(), d_v, n_s, st), "download");
-    // nodes: start, goal, then the valid samples in sample order
-    std::vector<double> nodes = {start.x, start.y, start.z, goal.x, goal.y, goal.z};
-    for (size_t i = 0; i < n_s; ++i)
-        if (valid[i]) nodes.insert(nodes.end(), &xyz[3 * i], &xyz[3 * i + 3]);
-    const int32_t n = (int32_t)(nodes.size() / 3);
+    check(epp_compact_states(d_s, d_v, samples, d_nodes + 6, d_cnt, st), "compact");
+    check(epp_memcpy_h2d(d_nodes, ends, sizeof(ends), st), "upload");  // (synchronises the stream)
+    int64_t n_valid_states = 0;
+    check(epp_memcpy_d2h(&n_valid_states, d_cnt, 8, st), "download");
+    const int32_t n = (int32_t)(n_valid_states + 2);
     // ---- 2. k-NN graph + batched motion checks (MotionValidator::checkMotion) --------
     const size_t m = (size_t)n * k;
-    const size_t ws_bytes = (size_t)epp_knn_workspace_size(n);
-    ts.reset(ThreadScratch::rounded((size_t)n * 24) + ThreadScratch::rounded(m * 4) +
-             2 * ThreadScratch::rounded(m * 24) + ThreadScratch::rounded(m) + ThreadScratch::rounded(ws_bytes));
-    double* d_nodes = static_cast<double*>(ts.carve((size_t)n * 24));
-    int32_t* d_nbr = static_cast<int32_t*>(ts.carve(m * 4));
-    double* d_e1 = static_cast<double*>(ts.carve(m * 24));
-    double* d_e2 = static_cast<double*>(ts.carve(m * 24));
-    uint8_t* d_ev = static_cast<uint8_t*>(ts.carve(m));
-    void* d_ws = ts.carve(ws_bytes);
-    check(epp_memcpy_h2d(d_nodes, nodes.data(), (uint64_t)n * 24, st), "upload");
     check(epp_knn_ws(d_nodes, n, k, 0.0, d_nbr, d_ws, ws_bytes, st), "knn");
     check(epp_knn_edges(d_nodes, d_nbr, n, k, d_e1, d_e2, st), "edges");
     check(epp_check_motions(w, d_e1, d_e2, (int64_t)m, canPass ? 1 : 0, 0, d_ev, st), "motion check");
-    thread_local std::vector<int32_t> nbr;
-    thread_local std::vector<uint8_t> ev;
-    nbr.resize(m);
-    ev.resize(m);
-    check(epp_memcpy_d2h(nbr.data(), d_nbr, m * 4, st), "download");
-    check(epp_memcpy_d2h(ev.data(), d_ev, m, st), "download");
+    check(epp_mask_edges(d_nbr, d_ev, (int64_t)m, st), "mask edges");  // failed motions -> -1
+    // node coordinates and the masked k-NN table into pinned host staging
+    const double* nodes = static_cast<const double*>(ts.pinned(0, (size_t)n * 24));
+    const int32_t* nbr = static_cast<const int32_t*>(ts.pinned(1, m * 4));
+    check(epp_memcpy_d2h(const_cast<double*>(nodes), d_nodes, (uint64_t)n * 24, st), "download");
+    check(epp_memcpy_d2h(const_cast<int32_t*>(nbr), d_nbr, m * 4, st), "download");
     const auto t_dev1 = std::chrono::steady_clock::now();
     // ---- 3. shortest path over the valid edges, start = 0, goal = 1 ----------------------
     // A* with the Euclidean distance to the goal (admissible and consistent for Euclidean
@@ -118,7 +115,7 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     // the nodes it expands); only if the goal is not reached that way, again over the
     // symmetrised graph (reverse edges added as a CSR).
     int64_t n_valid_edges = 0;
-    for (size_t e = 0; e < m; ++e) n_valid_edges += (nbr[e] >= 0 && ev[e]) ? 1 : 0;
+    for (size_t e = 0; e < m; ++e) n_valid_edges += nbr[e] >= 0 ? 1 : 0;
     {
         std::lock_guard<std::mutex> lk(g_stats_mu);
         stats_.states_sampled += samples;
@@ -159,7 +156,7 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
             const size_t e0 = (size_t)u * k;
             for (int c = 0; c < k; ++c) {
                 const int v = nbr[e0 + c];
-                if (v >= 0 && ev[e0 + c]) relax(u, pu, v);
+                if (v >= 0) relax(u, pu, v);
             }
             if (with_reverse)
                 for (int32_t r = roff[u]; r < roff[u + 1]; ++r) relax(u, pu, radj[r]);
@@ -169,14 +166,14 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     if (!astar(false)) {
         roff.assign(n + 1, 0);
         for (size_t e = 0; e < m; ++e)
-            if (nbr[e] >= 0 && ev[e]) ++roff[nbr[e] + 1];
+            if (nbr[e] >= 0) ++roff[nbr[e] + 1];
         for (int i = 0; i < n; ++i) roff[i + 1] += roff[i];
         radj.resize(roff[n]);
         std::vector<int32_t> fill(roff.begin(), roff.end() - 1);
         for (int i = 0; i < n; ++i)
             for (int c = 0; c < k; ++c) {
                 const size_t e = (size_t)i * k + c;
-                if (nbr[e] >= 0 && ev[e]) radj[fill[nbr[e]]++] = i;
+                if (nbr[e] >= 0) radj[fill[nbr[e]]++] = i;
             }
         astar(true);
     }

@@ -8,6 +8,8 @@
 #include <stdexcept>
 #include <string>
 
+#include <hip/hip_runtime_api.h>
+
 #include "epp.h"
 
 namespace epp {
@@ -51,8 +53,25 @@ public:
         return p;
     }
     static size_t rounded(size_t bytes) { return (bytes + 255) & ~size_t(255); }
+    // Pinned (page-locked) host staging of at least `bytes`, slot 0 or 1: device-to-host
+    // copies into it run at DMA speed instead of through a pageable bounce buffer.
+    void* pinned(int slot, size_t bytes) {
+        if (bytes > pcap_[slot]) {
+            if (pin_[slot]) (void)hipHostFree(pin_[slot]);
+            pin_[slot] = nullptr;
+            pcap_[slot] = 0;
+            if (hipHostMalloc(&pin_[slot], bytes, hipHostMallocDefault) != hipSuccess) {
+                pin_[slot] = nullptr;
+                throw std::runtime_error("pinned host staging: hipHostMalloc failed");
+            }
+            pcap_[slot] = bytes;
+        }
+        return pin_[slot];
+    }
     ~ThreadScratch() {
         if (buf_) epp_free(buf_);
+        for (void* p : pin_)
+            if (p) (void)hipHostFree(p);
         if (stream_) epp_stream_destroy(stream_);
     }
 
@@ -60,6 +79,8 @@ private:
     void* stream_ = nullptr;
     void* buf_ = nullptr;
     size_t cap_ = 0, used_ = 0;
+    void* pin_[2] = {nullptr, nullptr};
+    size_t pcap_[2] = {0, 0};
 };
 
 }  // namespace epp

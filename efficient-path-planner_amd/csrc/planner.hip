@@ -422,6 +422,81 @@ struct CachedWs {
     bool used = false;
 };
 CachedWs g_knn_ws[64];
+CachedWs g_compact_ws[64];
+
+// ---- ordered compaction of the valid states ----------------------------------------
+// Chunks of kCompactChunk states per block: (1) per-block counts, (2) one block scans the
+// counts, (3) every block writes its valid states at its offset in index order (wave
+// ballots + per-wave counts in LDS).  Deterministic: the planner's node order (and with
+// it k-NN tie breaks and the search) does not depend on scheduling.
+constexpr int kCompactThreads = 256;
+constexpr int kCompactChunk = 4096;
+
+__global__ __launch_bounds__(kCompactThreads) void k_compact_count(const uint8_t* __restrict__ valid, int64_t n,
+                                                                   int* __restrict__ counts) {
+    __shared__ int ws[kCompactThreads / 64];
+    const int64_t b0 = (int64_t)blockIdx.x * kCompactChunk;
+    int c = 0;
+    for (int j = threadIdx.x; j < kCompactChunk; j += kCompactThreads) {
+        const int64_t i = b0 + j;
+        c += (i < n && valid[i]) ? 1 : 0;
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int w = 0; w < kCompactThreads / 64; ++w) t += ws[w];
+        counts[blockIdx.x] = t;
+    }
+}
+
+__global__ void k_compact_scan(int* __restrict__ counts, int nb, int64_t* __restrict__ n_out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    int64_t acc = 0;
+    for (int b = 0; b < nb; ++b) {
+        const int c = counts[b];
+        counts[b] = (int)acc;
+        acc += c;
+    }
+    *n_out = acc;
+}
+
+__global__ __launch_bounds__(kCompactThreads) void k_compact_scatter(const double* __restrict__ xyz,
+                                                                     const uint8_t* __restrict__ valid, int64_t n,
+                                                                     const int* __restrict__ offsets,
+                                                                     double* __restrict__ out) {
+    __shared__ int wcnt[kCompactThreads / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t b0 = (int64_t)blockIdx.x * kCompactChunk;
+    int64_t base = offsets[blockIdx.x];
+    for (int j0 = 0; j0 < kCompactChunk; j0 += kCompactThreads) {  // block-uniform rounds, index order
+        const int64_t i = b0 + j0 + threadIdx.x;
+        const bool v = i < n && valid[i];
+        const unsigned long long bal = __ballot(v);
+        if (lane == 0) wcnt[wv] = __popcll(bal);
+        __syncthreads();
+        int before = 0, total = 0;
+        for (int w = 0; w < kCompactThreads / 64; ++w) {
+            before += w < wv ? wcnt[w] : 0;
+            total += wcnt[w];
+        }
+        if (v) {
+            const int64_t p = base + before + (int64_t)__builtin_amdgcn_mbcnt_hi(
+                                                     (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            out[3 * p] = xyz[3 * i];
+            out[3 * p + 1] = xyz[3 * i + 1];
+            out[3 * p + 2] = xyz[3 * i + 2];
+        }
+        base += total;
+        __syncthreads();  // wcnt is rewritten next round
+    }
+}
+
+__global__ void k_mask_edges(int32_t* __restrict__ nbr, const uint8_t* __restrict__ valid, int64_t m) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < m && !valid[e]) nbr[e] = -1;
+}
 
 epp_status last(const char* what) {
     hipError_t e = hipGetLastError();
@@ -535,6 +610,54 @@ epp_status epp_knn_grid(const double* nodes, int32_t n, int32_t k, double max_di
     const epp_status rc = knn_grid_launch(nodes, n, k, max_dist, nbr, static_cast<char*>(c.buf), L, s);
     if (hipEventRecord(c.done, s) == hipSuccess) c.used = true;
     return rc;
+}
+
+epp_status epp_compact_states(const double* xyz, const uint8_t* valid, int64_t n, double* out, int64_t* n_out,
+                              void* stream) {
+    if (n < 0 || !n_out || (n > 0 && (!xyz || !valid || !out))) {
+        set_error("epp_compact_states: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    const int nb = (int)std::max<int64_t>(1, (n + kCompactChunk - 1) / kCompactChunk);
+    int* counts = nullptr;
+    // the per-block counts live in the cached k-NN workspace's device (small, stream-ordered use)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    CachedWs& c = g_compact_ws[dev & 63];
+    std::lock_guard<std::mutex> lk(c.mu);
+    hipError_t e = hipSuccess;
+    if (!c.done) e = hipEventCreateWithFlags(&c.done, hipEventDisableTiming);
+    if (e == hipSuccess && c.used) e = hipStreamWaitEvent(s, c.done, 0);
+    if (e == hipSuccess && (size_t)nb * 4 > c.cap) {
+        if (c.buf) e = hipFree(c.buf);
+        c.buf = nullptr;
+        c.cap = 0;
+        if (e == hipSuccess) e = hipMalloc(&c.buf, (size_t)nb * 4);
+        if (e == hipSuccess) c.cap = (size_t)nb * 4;
+    }
+    if (e != hipSuccess) {
+        set_error(std::string("epp_compact_states: workspace: ") + hipGetErrorString(e));
+        return EPP_ERR_HIP;
+    }
+    counts = static_cast<int*>(c.buf);
+    hipLaunchKernelGGL(k_compact_count, dim3(nb), dim3(kCompactThreads), 0, s, valid, n, counts);
+    hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(64), 0, s, counts, nb, n_out);
+    hipLaunchKernelGGL(k_compact_scatter, dim3(nb), dim3(kCompactThreads), 0, s, xyz, valid, n, counts, out);
+    const epp_status rc = last("epp_compact_states");
+    if (hipEventRecord(c.done, s) == hipSuccess) c.used = true;
+    return rc;
+}
+
+epp_status epp_mask_edges(int32_t* nbr, const uint8_t* valid, int64_t m, void* stream) {
+    if (m < 0 || (m > 0 && (!nbr || !valid))) {
+        set_error("epp_mask_edges: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    if (m == 0) return EPP_OK;
+    hipLaunchKernelGGL(k_mask_edges, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, (hipStream_t)stream, nbr,
+                       valid, m);
+    return last("epp_mask_edges");
 }
 
 epp_status epp_knn_edges(const double* nodes, const int32_t* nbr, int32_t n, int32_t k, double* s1,

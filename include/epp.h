@@ -173,6 +173,12 @@ epp_status epp_knn_grid_ws(const double* nodes, int32_t n, int32_t k, double max
  * (s2 = s1 for a missing neighbour).  s1, s2: n k x 3. */
 epp_status epp_knn_edges(const double* nodes, const int32_t* nbr, int32_t n, int32_t k, double* s1,
                          double* s2, void* stream);
+/* Ordered stream compaction of the valid states (planner node list): out = xyz[i] for
+ * valid[i] != 0, in index order; *n_out (device int64) = their count.  out holds n x 3. */
+epp_status epp_compact_states(const double* xyz, const uint8_t* valid, int64_t n, double* out, int64_t* n_out,
+                              void* stream);
+/* nbr[e] = -1 where valid[e] == 0 (edges that failed the motion check), in place. */
+epp_status epp_mask_edges(int32_t* nbr, const uint8_t* valid, int64_t m, void* stream);
 
 /* ---- host-buffer convenience (synchronous; used by the C++ API shims) ------------- */
 /* generateTrajectory for one track with host buffers.  Returns the row count in

@@ -411,3 +411,19 @@ def test_vector_and_matrix_helpers():
     assert np.array_equal(np.asarray(v), [1, 2, 3])
     m = ot.MatrixXd(np.arange(6.0).reshape(2, 3))
     assert m.shape == (2, 3) and np.array_equal(np.asarray(m), np.arange(6.0).reshape(2, 3))
+
+
+@pytest.mark.parametrize("n", [1, 4095, 4096, 65536, 100_003])
+def test_compact_states_ordered(n):
+    """Ordered compaction (the planner's node list): same rows, same order as numpy."""
+    xyz = synth.sample_states(12, [-6, -6, 0], [6, 6, 2], n)
+    valid = (np.random.RandomState(n).rand(n) < 0.9).astype(np.uint8)
+    assert np.array_equal(capi.compact_states(xyz, valid), xyz[valid.astype(bool)])
+    assert len(capi.compact_states(xyz, np.zeros(n, np.uint8))) == 0
+
+
+def test_mask_edges():
+    rs = np.random.RandomState(3)
+    nbr = rs.randint(-1, 1000, (777, 16)).astype(np.int32)
+    valid = (rs.rand(777, 16) < 0.7).astype(np.uint8)
+    assert np.array_equal(capi.mask_edges(nbr, valid), np.where(valid.astype(bool), nbr, -1))
