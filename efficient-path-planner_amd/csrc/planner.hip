@@ -12,6 +12,8 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <vector>
+#include <cstdio>
 #include <mutex>
 #include <string>
 
@@ -109,6 +111,7 @@ struct KnnGrid {
     double h, inv_h;
     int dims[3];
     int ncell;
+    int next;  // k_knn_tile's block queue
 };
 
 constexpr int kBoundsThreads = 1024;
@@ -188,6 +191,7 @@ __global__ void k_knn_setup(const double* __restrict__ part, int nparts, int n, 
     g->h = h;
     g->inv_h = 1.0 / h;
     g->ncell = (int)cells;
+    g->next = 0;
 }
 
 __device__ __forceinline__ int knn_cell_axis(double v, const KnnGrid& g, int d) {
@@ -214,26 +218,39 @@ __global__ __launch_bounds__(kBoundsThreads) void k_knn_scan(const KnnGrid* __re
                                                              int* __restrict__ start) {
     __shared__ int wsum[kBoundsThreads / 64];
     const int nc = gp->ncell;
-    const int per = (nc + kBoundsThreads - 1) / kBoundsThreads;
-    const int b = threadIdx.x * per, e = min(nc, b + per);
-    int s = 0;
-    for (int c = b; c < e; ++c) s += cnt[c];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int incl = s;
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
+    // tiles of 4 cells per thread, coalesced; the carry runs across tiles
+    int carry = 0;
+    for (int t0 = 0; t0 < nc; t0 += 4 * kBoundsThreads) {  // block-uniform
+        const int b = t0 + 4 * threadIdx.x;
+        int v[4], s = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            v[u] = b + u < nc ? cnt[b + u] : 0;
+            s += v[u];
+        }
+        int incl = s;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += t;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        int wbase = 0, tile = 0;
+        for (int w = 0; w < kBoundsThreads / 64; ++w) {
+            wbase += w < wv ? wsum[w] : 0;
+            tile += wsum[w];
+        }
+        int acc = carry + wbase + incl - s;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (b + u < nc) start[b + u] = acc;
+            acc += v[u];
+        }
+        carry += tile;
+        __syncthreads();  // wsum is rewritten by the next tile
     }
-    if (lane == 63) wsum[wv] = incl;
-    __syncthreads();
-    int wbase = 0;
-    for (int w = 0; w < wv; ++w) wbase += wsum[w];
-    int acc = wbase + incl - s;
-    for (int c = b; c < e; ++c) {
-        start[c] = acc;
-        acc += cnt[c];
-    }
-    if (threadIdx.x == kBoundsThreads - 1) start[nc] = acc;
+    if (threadIdx.x == 0) start[nc] = carry;
 }
 
 __global__ void k_knn_scatter(const double* __restrict__ nodes, int n, const int* __restrict__ cell_of,
@@ -250,28 +267,59 @@ __global__ void k_knn_scatter(const double* __restrict__ nodes, int n, const int
     sxyz[3 * pos + 2] = nodes[3 * i + 2];
 }
 
+// Insert candidate (d, j) into the sorted top-K (distance, then index): ties keep the
+// lower index first, so the visiting order never changes the result.
 template <int K>
-__global__ __launch_bounds__(256) void k_knn_grid(const KnnGrid* __restrict__ gp, int n, double r2max,
-                                                  const double* __restrict__ sxyz,
-                                                  const int* __restrict__ sidx,
-                                                  const int* __restrict__ start,
-                                                  int32_t* __restrict__ nbr) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;  // queries in cell order: coherent walks
-    if (t >= n) return;
-    const KnnGrid g = *gp;
-    const int self = sidx[t];
-    const double px = sxyz[3 * t], py = sxyz[3 * t + 1], pz = sxyz[3 * t + 2];
-    const int c[3] = {knn_cell_axis(px, g, 0), knn_cell_axis(py, g, 1), knn_cell_axis(pz, g, 2)};
-    const double p[3] = {px, py, pz};
-    double bd[K];
-    int bi[K];
+__device__ __forceinline__ void knn_insert(double (&bd)[K], int (&bi)[K], double d, int j) {
+    if (!(d < bd[K - 1] || (d == bd[K - 1] && j < bi[K - 1]))) return;
+    double vd = d;
+    int vi = j;
+    bool shift = false;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        bd[k] = r2max;
-        bi[k] = 0x7fffffff;
+        shift = shift || vd < bd[k] || (vd == bd[k] && vi < bi[k]);
+        if (shift) {
+            const double td = bd[k];
+            const int ti = bi[k];
+            bd[k] = vd;
+            bi[k] = vi;
+            vd = td;
+            vi = ti;
+        }
     }
+}
+
+// Exact stopping rule after shell r: the K-th best squared distance is below the squared
+// distance from p to the nearest face of the searched (2r+1)^3 block that has cells
+// beyond it (minus a rounding margin).  Also true when no cells are left.
+template <int K>
+__device__ __forceinline__ bool knn_done(const KnnGrid& g, const int (&c)[3], const double (&p)[3], int r,
+                                         const double (&bd)[K]) {
+    double dmin = 1e300;
+    bool all = true;
+    for (int d = 0; d < 3; ++d) {
+        if (c[d] - r > 0) {
+            dmin = fmin(dmin, p[d] - (g.lo[d] + (double)(c[d] - r) * g.h));
+            all = false;
+        }
+        if (c[d] + r < g.dims[d] - 1) {
+            dmin = fmin(dmin, (g.lo[d] + (double)(c[d] + r + 1) * g.h) - p[d]);
+            all = false;
+        }
+    }
+    if (all) return true;
+    dmin -= g.h * 1e-6;  // cell assignment rounds; stay conservative
+    return dmin > 0 && bd[K - 1] < dmin * dmin;
+}
+
+// Shells r_from, r_from + 1, ... from global memory until knn_done (candidates BATCH
+// at a time: their loads are in flight together).
+template <int K, int BATCH = 4>
+__device__ void knn_walk(const KnnGrid& g, const int (&c)[3], const double (&p)[3], int self, double (&bd)[K],
+                         int (&bi)[K], const double* __restrict__ sxyz, const int* __restrict__ sidx,
+                         const int* __restrict__ start, int r_from) {
     const int rmax = max(g.dims[0], max(g.dims[1], g.dims[2]));
-    for (int r = 0; r <= rmax; ++r) {
+    for (int r = r_from; r <= rmax; ++r) {
         for (int dz = -r; dz <= r; ++dz) {
             const int z = c[2] + dz;
             if (z < 0 || z >= g.dims[2]) continue;
@@ -285,61 +333,322 @@ __global__ __launch_bounds__(256) void k_knn_grid(const KnnGrid* __restrict__ gp
                     if (x < 0 || x >= g.dims[0]) continue;
                     const int cell = (z * g.dims[1] + y) * g.dims[0] + x;
                     const int e = start[cell + 1];
-                    // candidates four at a time: their loads are in flight together
-                    for (int q0 = start[cell]; q0 < e; q0 += 4) {
-                        double dd[4];
-                        int jj[4];
+                    for (int q0 = start[cell]; q0 < e; q0 += BATCH) {
+                        double dd[BATCH];
+                        int jj[BATCH];
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) {
+                        for (int u = 0; u < BATCH; ++u) {
                             const int q = min(q0 + u, e - 1);
                             jj[u] = q0 + u < e ? sidx[q] : self;  // past the cell: skipped below
-                            const double ddx = sxyz[3 * q] - px, ddy = sxyz[3 * q + 1] - py, ddz = sxyz[3 * q + 2] - pz;
+                            const double ddx = sxyz[3 * q] - p[0], ddy = sxyz[3 * q + 1] - p[1], ddz = sxyz[3 * q + 2] - p[2];
                             dd[u] = (ddx * ddx + ddy * ddy) + ddz * ddz;
                         }
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const double d = dd[u];
-                            const int j = jj[u];
-                            if (j == self || !(d < bd[K - 1] || (d == bd[K - 1] && j < bi[K - 1]))) continue;
-                            double vd = d;
-                            int vi = j;
-                            bool shift = false;
-#pragma unroll
-                            for (int k = 0; k < K; ++k) {
-                                shift = shift || vd < bd[k] || (vd == bd[k] && vi < bi[k]);
-                                if (shift) {
-                                    const double td = bd[k];
-                                    const int ti = bi[k];
-                                    bd[k] = vd;
-                                    bi[k] = vi;
-                                    vd = td;
-                                    vi = ti;
-                                }
-                            }
-                        }
+                        for (int u = 0; u < BATCH; ++u)
+                            if (jj[u] != self) knn_insert<K>(bd, bi, dd[u], jj[u]);
                     }
                 }
             }
         }
-        // distance from p to the nearest face of the searched block that has cells beyond it
-        double dmin = 1e300;
-        bool all = true;
-        for (int d = 0; d < 3; ++d) {
-            if (c[d] - r > 0) {
-                dmin = fmin(dmin, p[d] - (g.lo[d] + (double)(c[d] - r) * g.h));
-                all = false;
-            }
-            if (c[d] + r < g.dims[d] - 1) {
-                dmin = fmin(dmin, (g.lo[d] + (double)(c[d] + r + 1) * g.h) - p[d]);
-                all = false;
-            }
-        }
-        if (all) break;
-        dmin -= g.h * 1e-6;  // cell assignment rounds; stay conservative
-        if (dmin > 0 && bd[K - 1] < dmin * dmin) break;
+        if (knn_done<K>(g, c, p, r, bd)) break;
     }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_knn_grid(const KnnGrid* __restrict__ gp, int n, double r2max,
+                                                  const double* __restrict__ sxyz,
+                                                  const int* __restrict__ sidx,
+                                                  const int* __restrict__ start,
+                                                  int32_t* __restrict__ nbr) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;  // queries in cell order: coherent walks
+    if (t >= n) return;
+    const KnnGrid g = *gp;
+    const int self = sidx[t];
+    const double p[3] = {sxyz[3 * t], sxyz[3 * t + 1], sxyz[3 * t + 2]};
+    const int c[3] = {knn_cell_axis(p[0], g, 0), knn_cell_axis(p[1], g, 1), knn_cell_axis(p[2], g, 2)};
+    double bd[K];
+    int bi[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        bd[k] = r2max;
+        bi[k] = 0x7fffffff;
+    }
+    knn_walk<K>(g, c, p, self, bd, bi, sxyz, sidx, start, 0);
 #pragma unroll
     for (int k = 0; k < K; ++k) nbr[(int64_t)self * K + k] = bi[k] == 0x7fffffff ? -1 : bi[k];
+}
+
+// ---- tiled grid k-NN ----------------------------------------------------------------
+// A workgroup takes a block of kTileB^3 cells: the block plus a kTileH-cell halo is
+// copied into LDS (coordinates, ids, per-cell offsets) and every query of the block
+// looks at the kTileW^3 cube of cells around its own (shells 0..kTileH) out of LDS; only
+// if the exact stopping rule does not hold after shell kTileH does it continue from
+// global memory (knn_walk from shell kTileH+1).  The per-query walk of k_knn_grid is
+// bound by dependent global round trips; here they are LDS reads.
+//
+// The sorted top-K insert costs ~K*12 VALU per candidate, and a wave pays it whenever
+// any of its lanes inserts -- nearly always.  So the cube is scanned twice instead:
+// pass 1 histograms the candidates' squared distances into kTileNB bins (quarter octaves
+// of d / t0, LDS counters); the bin where the running count reaches K gives a cut;
+// pass 2 lists the candidates at or below the cut (<= kTileL per query); only those go
+// through the insert.  The bin key is monotone in d, so every unlisted candidate is
+// strictly farther than every listed one and, with >= K listed, the result is exact.  A
+// query whose list would be short or overflow inserts its whole cube instead (rare).
+//
+// Lanes per query: a block holds ~64..160 queries at ~2 nodes per cell; with fewer
+// queries than threads, 2 or 4 adjacent lanes share one query (cube rows split between
+// them; the histogram and the list are shared through LDS atomics), so blocks take about
+// the same time whatever their query count.
+constexpr int kTileB = 4, kTileH = 2, kTileE = kTileB + 2 * kTileH, kTileCells = kTileE * kTileE * kTileE;
+constexpr int kTileW = 2 * kTileH + 1;  // cube edge around the query's cell
+constexpr int kTileRows = kTileW * kTileW;
+constexpr int kTileCap = 1344;          // candidates a halo may hold (else the block walks from global)
+constexpr int kTileThreads = 256;
+constexpr int kTileL = 32;              // per-query list length
+constexpr int kTileNB = 16;             // histogram bins (16-bit counters, two per word)
+
+// Bin key of a squared distance: exponent and two mantissa bits of d * inv_t0 (float),
+// i.e. quarter-octave bins; monotone non-decreasing in d.
+__device__ __forceinline__ int tile_key(double d, float inv_t0) {
+    return (int)(__float_as_uint((float)d * inv_t0) >> 21) - (127 << 2);
+}
+
+// Visits the candidates of cube rows row0, row0 + rstep, ... around a query (a row =
+// kTileW consecutive halo cells along x, one contiguous LDS range), four candidates at a
+// time so their LDS reads are in flight together.  f(q, d, id, valid).
+template <class F>
+__device__ __forceinline__ void tile_rows(const int* cst, const double* cx, const double* cy, const double* cz,
+                                          const int* cid, int h0, int row0, int rstep, const double (&p)[3], F&& f) {
+    for (int row = row0; row < kTileRows; row += rstep) {
+        const int a = h0 + ((row / kTileW) * kTileE + row % kTileW) * kTileE;
+        const int q1 = cst[a + kTileW];
+        for (int q = cst[a]; q < q1; q += 4) {
+            double d[4];
+            int j[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int qq = min(q + u, q1 - 1);
+                const double ddx = cx[qq] - p[0], ddy = cy[qq] - p[1], ddz = cz[qq] - p[2];
+                d[u] = (ddx * ddx + ddy * ddy) + ddz * ddz;
+                j[u] = cid[qq];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) f(min(q + u, q1 - 1), d[u], j[u], q + u < q1);
+        }
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void knn_store(int32_t* __restrict__ nbr, int self, const int (&bi)[K]) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) nbr[(int64_t)self * K + k] = bi[k] == 0x7fffffff ? -1 : bi[k];
+}
+
+template <int K>
+__global__ __launch_bounds__(kTileThreads) void k_knn_tile(KnnGrid* __restrict__ gp, double r2max,
+                                                           const double* __restrict__ sxyz,
+                                                           const int* __restrict__ sidx,
+                                                           const int* __restrict__ start,
+                                                           int32_t* __restrict__ nbr, int mode,
+                                                           unsigned long long* __restrict__ dbg) {
+    __shared__ double cx[kTileCap], cy[kTileCap], cz[kTileCap];
+    __shared__ int cid[kTileCap];
+    __shared__ uint16_t qh[kTileCap];                      // the block's queries (LDS positions)
+    __shared__ int cst[kTileCells + 1];                    // halo cell -> LDS offset
+    __shared__ uint32_t hist[kTileNB / 2][kTileThreads];   // [bin pair][query slot]
+    __shared__ uint16_t lst[kTileL][kTileThreads];         // [entry][query slot]
+    __shared__ int nls[kTileThreads];                      // list lengths
+    __shared__ int wsum[kTileThreads / 64];
+    __shared__ int s_nq, s_b;
+    const KnnGrid g = *gp;
+    const int nbx = (g.dims[0] + kTileB - 1) / kTileB, nby = (g.dims[1] + kTileB - 1) / kTileB,
+              nbz = (g.dims[2] + kTileB - 1) / kTileB;
+    const int nblocks = nbx * nby * nbz;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    constexpr int kPer = kTileCells / kTileThreads;  // halo cells per thread
+    static_assert(kTileCells % kTileThreads == 0, "");
+    // histogram origin: bins span d in [t0, 16 t0), t0 ~ a quarter of the expected K-th
+    // squared distance at ~2 nodes per cell (~(K/16)^(2/3) * 1.5 h^2)
+    const float kscale = K <= 4 ? 0.40f : K <= 8 ? 0.63f : 1.0f;
+    const float inv_t0 = 1.0f / ((float)(g.h * g.h) * 0.35f * kscale);
+    for (;;) {
+        // blocks from a queue: whichever workgroup is free takes the next one (block
+        // costs differ by ~3x: query counts, the grid's boundary)
+        if (threadIdx.x == 0) s_b = atomicAdd(&gp->next, 1);
+        __syncthreads();
+        const int b = s_b;  // block-uniform
+        if (b >= nblocks) break;
+        const int bx = b % nbx, by = (b / nbx) % nby, bz = b / (nbx * nby);
+        const int ox = bx * kTileB - kTileH, oy = by * kTileB - kTileH, oz = bz * kTileB - kTileH;
+        const unsigned long long t_begin = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
+        // 1. halo cell sizes -> exclusive scan (thread t owns halo cells kPer*t ..)
+        int cnt[kPer], cell0[kPer], tot = 0;
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int t = kPer * threadIdx.x + u;
+            const int x = ox + t % kTileE, y = oy + (t / kTileE) % kTileE, z = oz + t / (kTileE * kTileE);
+            const bool in = x >= 0 && x < g.dims[0] && y >= 0 && y < g.dims[1] && z >= 0 && z < g.dims[2];
+            const int cell = in ? (z * g.dims[1] + y) * g.dims[0] + x : 0;
+            const int s0 = start[cell], s1 = start[cell + 1];
+            cnt[u] = in ? s1 - s0 : 0;
+            cell0[u] = s0;
+            tot += cnt[u];
+        }
+        int incl = tot;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        int base = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < kTileThreads / 64; ++w) {
+            base += w < wv ? wsum[w] : 0;
+            total += wsum[w];
+        }
+        base += incl - tot;
+        {
+            int acc = base;
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) {
+                cst[kPer * threadIdx.x + u] = acc;
+                acc += cnt[u];
+            }
+        }
+        if (threadIdx.x == 0) {
+            cst[kTileCells] = total;
+            s_nq = 0;
+        }
+        __syncthreads();
+        if (total <= kTileCap) {  // block-uniform
+            // 2. copy the halo's candidates; list the block's own nodes as queries
+            int acc = base;
+#pragma unroll
+            for (int u = 0; u < kPer; ++u) {
+                const int t = kPer * threadIdx.x + u;
+                const int hx = t % kTileE, hy = (t / kTileE) % kTileE, hz = t / (kTileE * kTileE);
+                const bool inner = hx >= kTileH && hx < kTileH + kTileB && hy >= kTileH && hy < kTileH + kTileB &&
+                                   hz >= kTileH && hz < kTileH + kTileB;
+                const int q0 = (inner && cnt[u]) ? atomicAdd(&s_nq, cnt[u]) : 0;
+                for (int q = 0; q < cnt[u]; ++q) {
+                    const int sg = cell0[u] + q;
+                    cx[acc + q] = sxyz[3 * sg];
+                    cy[acc + q] = sxyz[3 * sg + 1];
+                    cz[acc + q] = sxyz[3 * sg + 2];
+                    cid[acc + q] = sidx[sg];
+                    if (inner) qh[q0 + q] = (uint16_t)(acc + q);
+                }
+                acc += cnt[u];
+            }
+            __syncthreads();
+            // 3. queries, lpq adjacent lanes per query
+            const int nq = mode == 4 ? 0 : s_nq;  // mode 4..6: timing ablations (inexact)
+            const int lpq = nq <= kTileThreads / 4 ? 4 : nq <= kTileThreads / 2 ? 2 : 1;  // block-uniform
+            const int slot = threadIdx.x / lpq, sub = threadIdx.x % lpq;
+            for (int qb = 0; qb < nq; qb += kTileThreads / lpq) {  // block-uniform
+                const int qi = qb + slot;
+                const bool live = qi < nq;
+                if (sub == 0) {
+#pragma unroll
+                    for (int w = 0; w < kTileNB / 2; ++w) hist[w][slot] = 0u;
+                    nls[slot] = 0;
+                }
+                const int me = live ? qh[qi] : 0;
+                const int self = cid[me];
+                const double p[3] = {cx[me], cy[me], cz[me]};
+                const int c[3] = {knn_cell_axis(p[0], g, 0), knn_cell_axis(p[1], g, 1), knn_cell_axis(p[2], g, 2)};
+                const int h0 = ((c[2] - oz - kTileH) * kTileE + (c[1] - oy - kTileH)) * kTileE + (c[0] - ox - kTileH);
+                __syncthreads();  // cleared counters visible to the query's lanes
+                // pass 1: histogram of bin keys
+                if (live)
+                    tile_rows(cst, cx, cy, cz, cid, h0, sub, lpq, p, [&](int, double d, int j, bool valid) {
+                        const int kb = max(tile_key(d, inv_t0), 0);
+                        if (valid && j != self && kb < kTileNB) atomicAdd(&hist[kb >> 1][slot], 1u << ((kb & 1) << 4));
+                    });
+                __syncthreads();
+                int cut = 0x7fffffff, run = 0;
+#pragma unroll
+                for (int w = 0; w < kTileNB / 2; ++w) {
+                    const uint32_t hv = hist[w][slot];
+                    run += hv & 0xffff;
+                    if (run >= K && cut == 0x7fffffff) cut = 2 * w;
+                    run += hv >> 16;
+                    if (run >= K && cut == 0x7fffffff) cut = 2 * w + 1;
+                }
+                if (mode == 5) {
+                    if (live && sub == 0) nbr[(int64_t)self * K] = cut + run;
+                    continue;
+                }
+                // pass 2: list the candidates at or below the cut
+                if (live)
+                    tile_rows(cst, cx, cy, cz, cid, h0, sub, lpq, p, [&](int q, double d, int j, bool valid) {
+                        if (valid && j != self && tile_key(d, inv_t0) <= cut) {
+                            const int at = atomicAdd(&nls[slot], 1);
+                            if (at < kTileL) lst[at][slot] = (uint16_t)q;
+                        }
+                    });
+                __syncthreads();
+                if (!live || sub != 0) continue;
+                const int nl = nls[slot];
+                if (mode == 6) {
+                    nbr[(int64_t)self * K] = nl;
+                    continue;
+                }
+                double bd[K];
+                int bi[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    bd[k] = r2max;
+                    bi[k] = 0x7fffffff;
+                }
+                if (nl >= K && nl <= kTileL) {
+                    for (int i = 0; i < nl; ++i) {
+                        const int q = lst[i][slot];
+                        const double ddx = cx[q] - p[0], ddy = cy[q] - p[1], ddz = cz[q] - p[2];
+                        knn_insert<K>(bd, bi, (ddx * ddx + ddy * ddy) + ddz * ddz, cid[q]);
+                    }
+                } else {  // short or overflowing list: insert the whole cube
+                    tile_rows(cst, cx, cy, cz, cid, h0, 0, 1, p, [&](int, double d, int j, bool valid) {
+                        if (valid && j != self) knn_insert<K>(bd, bi, d, j);
+                    });
+                }
+                if (mode != 2 && !knn_done<K>(g, c, p, kTileH, bd))
+                    knn_walk<K, 1>(g, c, p, self, bd, bi, sxyz, sidx, start, kTileH + 1);
+                knn_store<K>(nbr, self, bi);
+            }
+        } else {
+            // crowded halo: the block's queries walk from global memory
+            for (int t2 = threadIdx.x; t2 < kTileB * kTileB * kTileB; t2 += kTileThreads) {
+                const int x = bx * kTileB + t2 % kTileB, y = by * kTileB + (t2 / kTileB) % kTileB,
+                          z = bz * kTileB + t2 / (kTileB * kTileB);
+                if (x >= g.dims[0] || y >= g.dims[1] || z >= g.dims[2]) continue;
+                const int cell = (z * g.dims[1] + y) * g.dims[0] + x;
+                for (int t = start[cell]; t < start[cell + 1]; ++t) {
+                    const int self = sidx[t];
+                    const double p[3] = {sxyz[3 * t], sxyz[3 * t + 1], sxyz[3 * t + 2]};
+                    const int c[3] = {x, y, z};
+                    double bd[K];
+                    int bi[K];
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        bd[k] = r2max;
+                        bi[k] = 0x7fffffff;
+                    }
+                    knn_walk<K, 1>(g, c, p, self, bd, bi, sxyz, sidx, start, 0);
+                    knn_store<K>(nbr, self, bi);
+                }
+            }
+        }
+        __syncthreads();  // the LDS tile is rewritten by the next block
+        if (dbg && threadIdx.x == 0) {  // diagnostics: per-block timing (EPP_KNN_TILE_DBG)
+            const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+            dbg[4 * b] = t_begin;
+            dbg[4 * b + 1] = t_end;
+            dbg[4 * b + 2] = (unsigned long long)s_nq;
+            dbg[4 * b + 3] = blockIdx.x;
+        }
+    }
 }
 
 __global__ void k_knn_edges(const double* __restrict__ nodes, const int32_t* __restrict__ nbr, int64_t m,
@@ -405,11 +714,40 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
     hipLaunchKernelGGL(k_knn_count, g256, b256, 0, s, nodes, n, g, cell_of, cnt);
     hipLaunchKernelGGL(k_knn_scan, dim3(1), dim3(kBoundsThreads), 0, s, g, cnt, start);
     hipLaunchKernelGGL(k_knn_scatter, g256, b256, 0, s, nodes, n, cell_of, start, fill, sxyz, sidx);
-    switch (k) {
-        case 4: hipLaunchKernelGGL(k_knn_grid<4>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
-        case 8: hipLaunchKernelGGL(k_knn_grid<8>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
-        case 16: hipLaunchKernelGGL(k_knn_grid<16>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
-        default: hipLaunchKernelGGL(k_knn_grid<32>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
+    const char* tile_env = std::getenv("EPP_KNN_TILE");
+    if ((!tile_env || std::atoi(tile_env) != 0) && (k == 4 || k == 8 || k == 16)) {
+        // persistent: the block count is only known on the device (grid shape)
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const dim3 gt((unsigned)std::max(1, cus * 2)), bt(kTileThreads);
+        const int mode = tile_env ? std::atoi(tile_env) : 1;  // 2, 4..6: ablations (inexact)
+        static unsigned long long* dbg = nullptr;           // diagnostics only
+        if (std::getenv("EPP_KNN_TILE_DBG") && !dbg && hipMalloc(&dbg, 4 * 8 * 65536) != hipSuccess) dbg = nullptr;
+        unsigned long long* d = std::getenv("EPP_KNN_TILE_DBG") ? dbg : nullptr;
+        if (d) (void)hipMemsetAsync(d, 0, 4 * 8 * 65536, s);
+        if (k == 4) hipLaunchKernelGGL(k_knn_tile<4>, gt, bt, 0, s, g, r2, sxyz, sidx, start, nbr, mode, d);
+        else if (k == 8) hipLaunchKernelGGL(k_knn_tile<8>, gt, bt, 0, s, g, r2, sxyz, sidx, start, nbr, mode, d);
+        else hipLaunchKernelGGL(k_knn_tile<16>, gt, bt, 0, s, g, r2, sxyz, sidx, start, nbr, mode, d);
+        if (d) {
+            std::vector<unsigned long long> h(4 * 65536);
+            (void)hipStreamSynchronize(s);
+            (void)hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost);
+            unsigned long long t0 = ~0ull, t1 = 0;
+            for (int i = 0; i < 65536; ++i)
+                if (h[4 * i + 1]) t0 = std::min(t0, h[4 * i]), t1 = std::max(t1, h[4 * i + 1]);
+            std::fprintf(stderr, "knn_tile blocks (start_us end_us nq wg):\n");
+            for (int i = 0; i < 65536; ++i)
+                if (h[4 * i + 1])
+                    std::fprintf(stderr, "%d %.2f %.2f %llu %llu\n", i, (h[4 * i] - t0) / 100.0, (h[4 * i + 1] - t0) / 100.0,
+                                 h[4 * i + 2], h[4 * i + 3]);
+        }
+    } else {
+        switch (k) {
+            case 4: hipLaunchKernelGGL(k_knn_grid<4>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
+            case 8: hipLaunchKernelGGL(k_knn_grid<8>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
+            case 16: hipLaunchKernelGGL(k_knn_grid<16>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
+            default: hipLaunchKernelGGL(k_knn_grid<32>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
+        }
     }
     return last("epp_knn_grid");
 }

@@ -19,10 +19,14 @@ nodes = synth.sample_states(5, [-6, -6, 0], [6, 6, 2], 63000)
 d_n = capi.DeviceBuffer.from_array(nodes)
 d_k = capi.DeviceBuffer(4 * 16 * len(nodes))
 ref = capi.knn(nodes, 16, method="brute")
-for npc in ("1.5", "2", "3"):
+cfgs = (("0", "2"), ("1", "2"), ("2", "2"), ("1", "1.5"), ("1", "2.5"))
+if len(sys.argv) > 1:  # e.g. "1:2" -> tile 1, npc 2 only
+    cfgs = [tuple(a.split(":")) for a in sys.argv[1:]]
+for tile, npc in cfgs:
+    os.environ["EPP_KNN_TILE"] = tile
     os.environ["EPP_KNN_NPC"] = npc
     f = lambda r: capi.check(L.epp_knn_grid(d_n.ptr, len(nodes), 16, 0.0, d_k.ptr, st))  # noqa: E731
     f(0)
     ms = timed_kernel_ms(capi, st, f, 10)
     ok = np.array_equal(d_k.download(np.int32, 16 * len(nodes)).reshape(-1, 16), ref)
-    print(f"npc {npc}: {ms * 1e3:.1f} us per call, exact={ok}", flush=True)
+    print(f"tile {tile} npc {npc}: {ms * 1e3:.1f} us per call, exact={ok}", flush=True)

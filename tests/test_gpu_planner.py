@@ -75,10 +75,13 @@ def test_knn_vs_bruteforce(k, method):
     assert np.array_equal(got, _knn_ref(nodes, k))
 
 
-@pytest.mark.parametrize("k", [4, 16, 32])
-def test_knn_grid_large(k):
+@pytest.mark.parametrize("tile", ["1", "0"])
+@pytest.mark.parametrize("k", [4, 8, 16, 32])
+def test_knn_grid_large(k, tile, monkeypatch):
     """Grid k-NN (used above 2048 nodes) vs the all-pairs kernel and numpy: clustered,
-    duplicated and lattice (many exact ties) nodes."""
+    duplicated and lattice (many exact ties) nodes; with the tiled LDS kernel (k 8/16)
+    and with the per-query walk."""
+    monkeypatch.setenv("EPP_KNN_TILE", tile)
     rs = np.random.RandomState(k)
     nodes = synth.sample_states(100 + k, [-6, -6, 0], [6, 6, 2], 4000)
     nodes[:300] = rs.normal(0, 0.05, (300, 3)) + [1, 1, 1]          # a dense cluster
@@ -91,6 +94,17 @@ def test_knn_grid_large(k):
     assert np.array_equal(capi.knn(nodes, k), got)                   # auto -> grid
     assert np.array_equal(capi.knn(nodes, k, method="ws"), got)      # caller workspace
     assert np.array_equal(capi.knn(nodes, k, method="grid_ws"), got)
+
+
+@pytest.mark.parametrize("k", [8, 16])
+def test_knn_tile_crowded_halo(k):
+    """A cluster far denser than the grid's cell size: the tiles around it overflow their
+    LDS capacity and walk from global memory; the answer stays exact."""
+    rs = np.random.RandomState(3)
+    nodes = synth.sample_states(200 + k, [-6, -6, 0], [6, 6, 2], 6000)
+    nodes[:3000] = rs.normal(0, 0.02, (3000, 3)) + [0.5, -0.5, 1]
+    got = capi.knn(nodes, k, method="grid")
+    assert np.array_equal(got, capi.knn(nodes, k, method="brute"))
 
 
 def test_knn_grid_back_to_back_streams():
