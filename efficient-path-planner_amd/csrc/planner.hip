@@ -111,7 +111,9 @@ struct KnnGrid {
     double h, inv_h;
     int dims[3];
     int ncell;
-    int next;  // k_knn_tile's block queue
+    int next;    // k_knn_tile's block queue
+    int nretry;  // k_knn_tile's retry list length
+    int why[4];  // retry causes (diagnostics): list overflow, K-th beyond Dcut, shell rule, crowded
 };
 
 constexpr int kBoundsThreads = 1024;
@@ -157,13 +159,20 @@ __global__ __launch_bounds__(kBoundsThreads) void k_knn_bounds_part(const double
 // Grid shape from the block partials (one thread).
 __global__ void k_knn_setup(const double* __restrict__ part, int nparts, int n, int cell_cap, double npc,
                             KnnGrid* __restrict__ g) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (threadIdx.x >= 64 || blockIdx.x != 0) return;
+    // one wave folds the partials (all loads in flight at once), lane 0 does the rest
     double mn[3] = {1e308, 1e308, 1e308}, mx[3] = {-1e308, -1e308, -1e308};
-    for (int b = 0; b < nparts; ++b)
+    for (int b = threadIdx.x; b < nparts; b += 64)
         for (int d = 0; d < 3; ++d) {
             mn[d] = fmin(mn[d], part[6 * b + d]);
             mx[d] = fmax(mx[d], part[6 * b + 3 + d]);
         }
+    for (int d = 0; d < 3; ++d)
+        for (int o = 32; o > 0; o >>= 1) {
+            mn[d] = fmin(mn[d], __shfl_xor(mn[d], o, 64));
+            mx[d] = fmax(mx[d], __shfl_xor(mx[d], o, 64));
+        }
+    if (threadIdx.x != 0) return;
     double ext[3], vol = 1.0, emax = 0.0;
     for (int d = 0; d < 3; ++d) {
         ext[d] = mx[d] - mn[d];
@@ -192,6 +201,8 @@ __global__ void k_knn_setup(const double* __restrict__ part, int nparts, int n, 
     g->inv_h = 1.0 / h;
     g->ncell = (int)cells;
     g->next = 0;
+    g->nretry = 0;
+    for (int i = 0; i < 4; ++i) g->why[i] = 0;
 }
 
 __device__ __forceinline__ int knn_cell_axis(double v, const KnnGrid& g, int d) {
@@ -216,17 +227,27 @@ __global__ void k_knn_count(const double* __restrict__ nodes, int n, const KnnGr
 __global__ __launch_bounds__(kBoundsThreads) void k_knn_scan(const KnnGrid* __restrict__ gp,
                                                              const int* __restrict__ cnt,
                                                              int* __restrict__ start) {
+    constexpr int kScanPer = 16;  // cells per thread per tile
+    constexpr int kScanTile = kScanPer * kBoundsThreads;
+    __shared__ int tile_v[kScanTile + kScanTile / 32];  // padded: i -> i + i / 32
     __shared__ int wsum[kBoundsThreads / 64];
     const int nc = gp->ncell;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    // tiles of 4 cells per thread, coalesced; the carry runs across tiles
+    // tiles staged through LDS: coalesced loads and stores, kScanPer consecutive cells
+    // per thread for the scan; the carry runs across tiles
     int carry = 0;
-    for (int t0 = 0; t0 < nc; t0 += 4 * kBoundsThreads) {  // block-uniform
-        const int b = t0 + 4 * threadIdx.x;
-        int v[4], s = 0;
+    for (int t0 = 0; t0 < nc; t0 += kScanTile) {  // block-uniform
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            v[u] = b + u < nc ? cnt[b + u] : 0;
+        for (int u = 0; u < kScanPer; ++u) {
+            const int i = u * kBoundsThreads + threadIdx.x;
+            tile_v[i + (i >> 5)] = t0 + i < nc ? cnt[t0 + i] : 0;
+        }
+        __syncthreads();
+        int v[kScanPer], s = 0;
+#pragma unroll
+        for (int u = 0; u < kScanPer; ++u) {
+            const int i = kScanPer * threadIdx.x + u;
+            v[u] = tile_v[i + (i >> 5)];
             s += v[u];
         }
         int incl = s;
@@ -243,12 +264,19 @@ __global__ __launch_bounds__(kBoundsThreads) void k_knn_scan(const KnnGrid* __re
         }
         int acc = carry + wbase + incl - s;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (b + u < nc) start[b + u] = acc;
+        for (int u = 0; u < kScanPer; ++u) {
+            const int i = kScanPer * threadIdx.x + u;
+            tile_v[i + (i >> 5)] = acc;
             acc += v[u];
         }
         carry += tile;
-        __syncthreads();  // wsum is rewritten by the next tile
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kScanPer; ++u) {
+            const int i = u * kBoundsThreads + threadIdx.x;
+            if (t0 + i < nc) start[t0 + i] = tile_v[i + (i >> 5)];
+        }
+        __syncthreads();  // tile_v and wsum are rewritten by the next tile
     }
     if (threadIdx.x == 0) start[nc] = carry;
 }
@@ -292,9 +320,8 @@ __device__ __forceinline__ void knn_insert(double (&bd)[K], int (&bi)[K], double
 // Exact stopping rule after shell r: the K-th best squared distance is below the squared
 // distance from p to the nearest face of the searched (2r+1)^3 block that has cells
 // beyond it (minus a rounding margin).  Also true when no cells are left.
-template <int K>
-__device__ __forceinline__ bool knn_done(const KnnGrid& g, const int (&c)[3], const double (&p)[3], int r,
-                                         const double (&bd)[K]) {
+// knn_bound returns that squared distance (+inf: no cells left; 0: never).
+__device__ __forceinline__ double knn_bound(const KnnGrid& g, const int (&c)[3], const double (&p)[3], int r) {
     double dmin = 1e300;
     bool all = true;
     for (int d = 0; d < 3; ++d) {
@@ -307,9 +334,16 @@ __device__ __forceinline__ bool knn_done(const KnnGrid& g, const int (&c)[3], co
             all = false;
         }
     }
-    if (all) return true;
+    if (all) return INFINITY;
     dmin -= g.h * 1e-6;  // cell assignment rounds; stay conservative
-    return dmin > 0 && bd[K - 1] < dmin * dmin;
+    return dmin > 0 ? dmin * dmin : 0.0;
+}
+
+template <int K>
+__device__ __forceinline__ bool knn_done(const KnnGrid& g, const int (&c)[3], const double (&p)[3], int r,
+                                         const double (&bd)[K]) {
+    const double b = knn_bound(g, c, p, r);
+    return b == INFINITY || bd[K - 1] < b;
 }
 
 // Shells r_from, r_from + 1, ... from global memory until knn_done (candidates BATCH
@@ -380,60 +414,54 @@ __global__ __launch_bounds__(256) void k_knn_grid(const KnnGrid* __restrict__ gp
 
 // ---- tiled grid k-NN ----------------------------------------------------------------
 // A workgroup takes a block of kTileB^3 cells: the block plus a kTileH-cell halo is
-// copied into LDS (coordinates, ids, per-cell offsets) and every query of the block
-// looks at the kTileW^3 cube of cells around its own (shells 0..kTileH) out of LDS; only
-// if the exact stopping rule does not hold after shell kTileH does it continue from
-// global memory (knn_walk from shell kTileH+1).  The per-query walk of k_knn_grid is
+// copied into LDS and every query of the block looks at the kTileW^3 cube of cells
+// around its own (shells 0..kTileH) out of LDS.  The per-query walk of k_knn_grid is
 // bound by dependent global round trips; here they are LDS reads.
 //
-// The sorted top-K insert costs ~K*12 VALU per candidate, and a wave pays it whenever
-// any of its lanes inserts -- nearly always.  So the cube is scanned twice instead:
-// pass 1 histograms the candidates' squared distances into kTileNB bins (quarter octaves
-// of d / t0, LDS counters); the bin where the running count reaches K gives a cut;
-// pass 2 lists the candidates at or below the cut (<= kTileL per query); only those go
-// through the insert.  The bin key is monotone in d, so every unlisted candidate is
-// strictly farther than every listed one and, with >= K listed, the result is exact.  A
-// query whose list would be short or overflow inserts its whole cube instead (rare).
+// Selection.  The sorted top-K insert costs ~K*12 VALU per candidate, and a wave pays
+// it whenever any of its lanes inserts -- nearly always.  So the cube is scanned twice
+// on float coordinates (relative to the block centre, one 16-byte LDS record per
+// candidate): pass 1 histograms the squared distances into kTileNB quarter-octave bins;
+// the bin where the running count reaches K gives a bound Dcut; pass 2 lists the
+// candidates with float distance below Dcut + 2*delta (<= kTileL per query).  Only the
+// listed candidates get an exact (double, from global memory) distance and the insert.
+// delta bounds the float error of a squared distance within a halo (<= ~1e-4 h^2; 1e-3
+// h^2 is used), so every candidate with exact d <= Dcut is listed; if the exact K-th
+// distance is <= Dcut the result is therefore exact.  Queries where that check, the
+// list size or the exact stopping rule after shell kTileH fails -- and all queries of a
+// halo over capacity -- go to a retry list that k_knn_retry walks from global memory.
 //
 // Lanes per query: a block holds ~64..160 queries at ~2 nodes per cell; with fewer
 // queries than threads, 2 or 4 adjacent lanes share one query (cube rows split between
 // them; the histogram and the list are shared through LDS atomics), so blocks take about
-// the same time whatever their query count.
+// the same time whatever their query count.  Blocks come from a queue (costs differ).
 constexpr int kTileB = 4, kTileH = 2, kTileE = kTileB + 2 * kTileH, kTileCells = kTileE * kTileE * kTileE;
 constexpr int kTileW = 2 * kTileH + 1;  // cube edge around the query's cell
 constexpr int kTileRows = kTileW * kTileW;
-constexpr int kTileCap = 1344;          // candidates a halo may hold (else the block walks from global)
+constexpr int kTileCap = 1344;          // candidates a halo may hold (else its queries retry)
 constexpr int kTileThreads = 256;
 constexpr int kTileL = 32;              // per-query list length
 constexpr int kTileNB = 16;             // histogram bins (16-bit counters, two per word)
-
-// Bin key of a squared distance: exponent and two mantissa bits of d * inv_t0 (float),
-// i.e. quarter-octave bins; monotone non-decreasing in d.
-__device__ __forceinline__ int tile_key(double d, float inv_t0) {
-    return (int)(__float_as_uint((float)d * inv_t0) >> 21) - (127 << 2);
-}
+constexpr double kTileDelta = 1e-3;     // float error allowance, in h^2
 
 // Visits the candidates of cube rows row0, row0 + rstep, ... around a query (a row =
 // kTileW consecutive halo cells along x, one contiguous LDS range), four candidates at a
-// time so their LDS reads are in flight together.  f(q, d, id, valid).
+// time so their LDS reads are in flight together.  f(q, d_float, id, valid).
 template <class F>
-__device__ __forceinline__ void tile_rows(const int* cst, const double* cx, const double* cy, const double* cz,
-                                          const int* cid, int h0, int row0, int rstep, const double (&p)[3], F&& f) {
+__device__ __forceinline__ void tile_rows(const int* cst, const float4* cand, int h0, int row0, int rstep,
+                                          const float4& pf, F&& f) {
     for (int row = row0; row < kTileRows; row += rstep) {
         const int a = h0 + ((row / kTileW) * kTileE + row % kTileW) * kTileE;
         const int q1 = cst[a + kTileW];
         for (int q = cst[a]; q < q1; q += 4) {
-            double d[4];
-            int j[4];
+            float4 c[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) c[u] = cand[min(q + u, q1 - 1)];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int qq = min(q + u, q1 - 1);
-                const double ddx = cx[qq] - p[0], ddy = cy[qq] - p[1], ddz = cz[qq] - p[2];
-                d[u] = (ddx * ddx + ddy * ddy) + ddz * ddz;
-                j[u] = cid[qq];
+                const float dx = c[u].x - pf.x, dy = c[u].y - pf.y, dz = c[u].z - pf.z;
+                f(min(q + u, q1 - 1), (dx * dx + dy * dy) + dz * dz, __float_as_int(c[u].w), q + u < q1);
             }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) f(min(q + u, q1 - 1), d[u], j[u], q + u < q1);
         }
     }
 }
@@ -444,15 +472,109 @@ __device__ __forceinline__ void knn_store(int32_t* __restrict__ nbr, int self, c
     for (int k = 0; k < K; ++k) nbr[(int64_t)self * K + k] = bi[k] == 0x7fffffff ? -1 : bi[k];
 }
 
+// Queries the tile pass could not settle (rare: sparse corners, crowded halos), one
+// wave per query so a single far walk does not serialise on dependent global loads:
+// lanes take x-rows of cells (each one contiguous range of the cell-sorted nodes) and
+// keep their own top-K.  First the cube of radius kTileH + 1, then one shell at a time
+// until the stopping rule holds -- tested cheaply as ">= K listed candidates below the
+// bound" over all lanes -- then K rounds of a wave-wide (distance, index) arg-min merge
+// the lane lists; lane 0 writes the result.  Called by whole waves.
 template <int K>
-__global__ __launch_bounds__(kTileThreads) void k_knn_tile(KnnGrid* __restrict__ gp, double r2max,
+__device__ void knn_retry_wave(const KnnGrid& g, double r2max, const double* __restrict__ nodes,
+                               const double* __restrict__ sxyz, const int* __restrict__ sidx,
+                               const int* __restrict__ start, int self, int32_t* __restrict__ nbr) {
+    const int lane = threadIdx.x & 63;
+    const int rmax = max(g.dims[0], max(g.dims[1], g.dims[2]));
+    const double p[3] = {nodes[3 * (int64_t)self], nodes[3 * (int64_t)self + 1], nodes[3 * (int64_t)self + 2]};
+    const int c[3] = {knn_cell_axis(p[0], g, 0), knn_cell_axis(p[1], g, 1), knn_cell_axis(p[2], g, 2)};
+    double bd[K];
+    int bi[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        bd[k] = r2max;
+        bi[k] = 0x7fffffff;
+    }
+    // candidates of cells [xa, xb] of row (y, z) into the lane's list
+    auto scan = [&](int y, int z, int xa, int xb) {
+        const int a = (z * g.dims[1] + y) * g.dims[0];
+        const int e = start[a + xb + 1];
+        for (int q0 = start[a + xa]; q0 < e; q0 += 4) {
+            double dd[4];
+            int jj[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int q = min(q0 + u, e - 1);
+                jj[u] = q0 + u < e ? sidx[q] : self;  // past the row: skipped below
+                const double ddx = sxyz[3 * q] - p[0], ddy = sxyz[3 * q + 1] - p[1], ddz = sxyz[3 * q + 2] - p[2];
+                dd[u] = (ddx * ddx + ddy * ddy) + ddz * ddz;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (jj[u] != self) knn_insert<K>(bd, bi, dd[u], jj[u]);
+        }
+    };
+    for (int R = kTileH + 1;; ++R) {  // wave-uniform
+        // rows of shell R (the whole cube the first time)
+        const bool cube = R == kTileH + 1;
+        const int w = 2 * R + 1;
+        for (int row = lane; row < w * w; row += 64) {
+            const int dz = row / w - R, dy = row % w - R;
+            const int z = c[2] + dz, y = c[1] + dy;
+            if (z < 0 || z >= g.dims[2] || y < 0 || y >= g.dims[1]) continue;
+            const int xa = max(c[0] - R, 0), xb = min(c[0] + R, g.dims[0] - 1);
+            if (cube || dz == -R || dz == R || dy == -R || dy == R) {
+                scan(y, z, xa, xb);
+            } else {  // inner rows: only the shell's two end cells
+                if (c[0] - R >= 0) scan(y, z, c[0] - R, c[0] - R);
+                if (c[0] + R < g.dims[0]) scan(y, z, c[0] + R, c[0] + R);
+            }
+        }
+        const double bound = knn_bound(g, c, p, R);
+        if (bound != INFINITY && R < rmax && !(r2max < bound)) {  // (radius below it: done)
+            int below = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) below += (bi[k] != 0x7fffffff && bd[k] < bound) ? 1 : 0;
+            for (int o = 32; o > 0; o >>= 1) below += __shfl_xor(below, o, 64);
+            if (below < K) continue;
+        }
+        break;
+    }
+    // merge: K rounds of arg-min over the lane list heads
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        double md = bd[0];
+        int mi = bi[0];
+        for (int o = 32; o > 0; o >>= 1) {
+            const double od = __shfl_xor(md, o, 64);
+            const int oi = __shfl_xor(mi, o, 64);
+            if (od < md || (od == md && oi < mi)) {
+                md = od;
+                mi = oi;
+            }
+        }
+        if (lane == 0) nbr[(int64_t)self * K + k] = mi == 0x7fffffff ? -1 : mi;
+        if (mi != 0x7fffffff && bi[0] == mi) {  // the winning lane drops its head
+#pragma unroll
+            for (int t = 0; t + 1 < K; ++t) {
+                bd[t] = bd[t + 1];
+                bi[t] = bi[t + 1];
+            }
+            bd[K - 1] = r2max;
+            bi[K - 1] = 0x7fffffff;
+        }
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restrict__ gp, double r2max,
+                                                           const double* __restrict__ nodes,
                                                            const double* __restrict__ sxyz,
                                                            const int* __restrict__ sidx,
                                                            const int* __restrict__ start,
+                                                           int* __restrict__ retry,
                                                            int32_t* __restrict__ nbr, int mode,
                                                            unsigned long long* __restrict__ dbg) {
-    __shared__ double cx[kTileCap], cy[kTileCap], cz[kTileCap];
-    __shared__ int cid[kTileCap];
+    __shared__ float4 cand[kTileCap];                      // x, y, z (block-centre relative), id
     __shared__ uint16_t qh[kTileCap];                      // the block's queries (LDS positions)
     __shared__ int cst[kTileCells + 1];                    // halo cell -> LDS offset
     __shared__ uint32_t hist[kTileNB / 2][kTileThreads];   // [bin pair][query slot]
@@ -470,16 +592,18 @@ __global__ __launch_bounds__(kTileThreads) void k_knn_tile(KnnGrid* __restrict__
     // histogram origin: bins span d in [t0, 16 t0), t0 ~ a quarter of the expected K-th
     // squared distance at ~2 nodes per cell (~(K/16)^(2/3) * 1.5 h^2)
     const float kscale = K <= 4 ? 0.40f : K <= 8 ? 0.63f : 1.0f;
-    const float inv_t0 = 1.0f / ((float)(g.h * g.h) * 0.35f * kscale);
+    const double t0 = g.h * g.h * 0.35 * kscale;
+    const float inv_t0 = (float)(1.0 / t0);
+    const double delta = kTileDelta * g.h * g.h;
     for (;;) {
-        // blocks from a queue: whichever workgroup is free takes the next one (block
-        // costs differ by ~3x: query counts, the grid's boundary)
         if (threadIdx.x == 0) s_b = atomicAdd(&gp->next, 1);
         __syncthreads();
         const int b = s_b;  // block-uniform
         if (b >= nblocks) break;
         const int bx = b % nbx, by = (b / nbx) % nby, bz = b / (nbx * nby);
         const int ox = bx * kTileB - kTileH, oy = by * kTileB - kTileH, oz = bz * kTileB - kTileH;
+        const double cen[3] = {g.lo[0] + (ox + 0.5 * kTileE) * g.h, g.lo[1] + (oy + 0.5 * kTileE) * g.h,
+                               g.lo[2] + (oz + 0.5 * kTileE) * g.h};
         const unsigned long long t_begin = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
         // 1. halo cell sizes -> exclusive scan (thread t owns halo cells kPer*t ..)
         int cnt[kPer], cell0[kPer], tot = 0;
@@ -533,17 +657,15 @@ __global__ __launch_bounds__(kTileThreads) void k_knn_tile(KnnGrid* __restrict__
                 const int q0 = (inner && cnt[u]) ? atomicAdd(&s_nq, cnt[u]) : 0;
                 for (int q = 0; q < cnt[u]; ++q) {
                     const int sg = cell0[u] + q;
-                    cx[acc + q] = sxyz[3 * sg];
-                    cy[acc + q] = sxyz[3 * sg + 1];
-                    cz[acc + q] = sxyz[3 * sg + 2];
-                    cid[acc + q] = sidx[sg];
+                    cand[acc + q] = make_float4((float)(sxyz[3 * sg] - cen[0]), (float)(sxyz[3 * sg + 1] - cen[1]),
+                                                (float)(sxyz[3 * sg + 2] - cen[2]), __int_as_float(sidx[sg]));
                     if (inner) qh[q0 + q] = (uint16_t)(acc + q);
                 }
                 acc += cnt[u];
             }
             __syncthreads();
             // 3. queries, lpq adjacent lanes per query
-            const int nq = mode == 4 ? 0 : s_nq;  // mode 4..6: timing ablations (inexact)
+            const int nq = mode == 4 ? 0 : s_nq;  // mode 4: timing ablation (inexact)
             const int lpq = nq <= kTileThreads / 4 ? 4 : nq <= kTileThreads / 2 ? 2 : 1;  // block-uniform
             const int slot = threadIdx.x / lpq, sub = threadIdx.x % lpq;
             for (int qb = 0; qb < nq; qb += kTileThreads / lpq) {  // block-uniform
@@ -555,35 +677,36 @@ __global__ __launch_bounds__(kTileThreads) void k_knn_tile(KnnGrid* __restrict__
                     nls[slot] = 0;
                 }
                 const int me = live ? qh[qi] : 0;
-                const int self = cid[me];
-                const double p[3] = {cx[me], cy[me], cz[me]};
+                const float4 pf = cand[me];
+                const int self = __float_as_int(pf.w);
+                // exact coordinates and cell (the row offsets; the final distances)
+                const double p[3] = {nodes[3 * (int64_t)self], nodes[3 * (int64_t)self + 1], nodes[3 * (int64_t)self + 2]};
                 const int c[3] = {knn_cell_axis(p[0], g, 0), knn_cell_axis(p[1], g, 1), knn_cell_axis(p[2], g, 2)};
                 const int h0 = ((c[2] - oz - kTileH) * kTileE + (c[1] - oy - kTileH)) * kTileE + (c[0] - ox - kTileH);
                 __syncthreads();  // cleared counters visible to the query's lanes
-                // pass 1: histogram of bin keys
+                // pass 1: histogram of bin keys (exponent + two mantissa bits of d / t0)
                 if (live)
-                    tile_rows(cst, cx, cy, cz, cid, h0, sub, lpq, p, [&](int, double d, int j, bool valid) {
-                        const int kb = max(tile_key(d, inv_t0), 0);
+                    tile_rows(cst, cand, h0, sub, lpq, pf, [&](int, float d, int j, bool valid) {
+                        const int kb = max((int)(__float_as_uint(d * inv_t0) >> 21) - (127 << 2), 0);
                         if (valid && j != self && kb < kTileNB) atomicAdd(&hist[kb >> 1][slot], 1u << ((kb & 1) << 4));
                     });
                 __syncthreads();
-                int cut = 0x7fffffff, run = 0;
+                int cut = -1, run = 0;
 #pragma unroll
                 for (int w = 0; w < kTileNB / 2; ++w) {
                     const uint32_t hv = hist[w][slot];
                     run += hv & 0xffff;
-                    if (run >= K && cut == 0x7fffffff) cut = 2 * w;
+                    if (run >= K && cut < 0) cut = 2 * w;
                     run += hv >> 16;
-                    if (run >= K && cut == 0x7fffffff) cut = 2 * w + 1;
+                    if (run >= K && cut < 0) cut = 2 * w + 1;
                 }
-                if (mode == 5) {
-                    if (live && sub == 0) nbr[(int64_t)self * K] = cut + run;
-                    continue;
-                }
-                // pass 2: list the candidates at or below the cut
+                // Dcut: upper edge of bin `cut` (none reached K: no bound)
+                const double dcut = cut < 0 ? INFINITY : (double)__uint_as_float((uint32_t)(cut + 1 + (127 << 2)) << 21) * t0;
+                const float dlist = (float)(dcut + 2.0 * delta);
+                // pass 2: list the candidates below Dcut + 2 delta
                 if (live)
-                    tile_rows(cst, cx, cy, cz, cid, h0, sub, lpq, p, [&](int q, double d, int j, bool valid) {
-                        if (valid && j != self && tile_key(d, inv_t0) <= cut) {
+                    tile_rows(cst, cand, h0, sub, lpq, pf, [&](int q, float d, int j, bool valid) {
+                        if (valid && j != self && d < dlist) {
                             const int at = atomicAdd(&nls[slot], 1);
                             if (at < kTileL) lst[at][slot] = (uint16_t)q;
                         }
@@ -591,43 +714,8 @@ __global__ __launch_bounds__(kTileThreads) void k_knn_tile(KnnGrid* __restrict__
                 __syncthreads();
                 if (!live || sub != 0) continue;
                 const int nl = nls[slot];
-                if (mode == 6) {
-                    nbr[(int64_t)self * K] = nl;
-                    continue;
-                }
-                double bd[K];
-                int bi[K];
-#pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    bd[k] = r2max;
-                    bi[k] = 0x7fffffff;
-                }
-                if (nl >= K && nl <= kTileL) {
-                    for (int i = 0; i < nl; ++i) {
-                        const int q = lst[i][slot];
-                        const double ddx = cx[q] - p[0], ddy = cy[q] - p[1], ddz = cz[q] - p[2];
-                        knn_insert<K>(bd, bi, (ddx * ddx + ddy * ddy) + ddz * ddz, cid[q]);
-                    }
-                } else {  // short or overflowing list: insert the whole cube
-                    tile_rows(cst, cx, cy, cz, cid, h0, 0, 1, p, [&](int, double d, int j, bool valid) {
-                        if (valid && j != self) knn_insert<K>(bd, bi, d, j);
-                    });
-                }
-                if (mode != 2 && !knn_done<K>(g, c, p, kTileH, bd))
-                    knn_walk<K, 1>(g, c, p, self, bd, bi, sxyz, sidx, start, kTileH + 1);
-                knn_store<K>(nbr, self, bi);
-            }
-        } else {
-            // crowded halo: the block's queries walk from global memory
-            for (int t2 = threadIdx.x; t2 < kTileB * kTileB * kTileB; t2 += kTileThreads) {
-                const int x = bx * kTileB + t2 % kTileB, y = by * kTileB + (t2 / kTileB) % kTileB,
-                          z = bz * kTileB + t2 / (kTileB * kTileB);
-                if (x >= g.dims[0] || y >= g.dims[1] || z >= g.dims[2]) continue;
-                const int cell = (z * g.dims[1] + y) * g.dims[0] + x;
-                for (int t = start[cell]; t < start[cell + 1]; ++t) {
-                    const int self = sidx[t];
-                    const double p[3] = {sxyz[3 * t], sxyz[3 * t + 1], sxyz[3 * t + 2]};
-                    const int c[3] = {x, y, z};
+                bool ok = nl <= kTileL;
+                if (ok) {
                     double bd[K];
                     int bi[K];
 #pragma unroll
@@ -635,9 +723,47 @@ __global__ __launch_bounds__(kTileThreads) void k_knn_tile(KnnGrid* __restrict__
                         bd[k] = r2max;
                         bi[k] = 0x7fffffff;
                     }
-                    knn_walk<K, 1>(g, c, p, self, bd, bi, sxyz, sidx, start, 0);
-                    knn_store<K>(nbr, self, bi);
+                    // exact distances of the listed candidates, kLoads at a time in flight
+                    constexpr int kLoads = 4;
+                    for (int i0 = 0; i0 < nl; i0 += kLoads) {
+                        double dd[kLoads];
+                        int jj[kLoads];
+#pragma unroll
+                        for (int u = 0; u < kLoads; ++u) {
+                            const int i = min(i0 + u, nl - 1);
+                            jj[u] = __float_as_int(cand[lst[i][slot]].w);
+                        }
+#pragma unroll
+                        for (int u = 0; u < kLoads; ++u) {
+                            const double ddx = nodes[3 * (int64_t)jj[u]] - p[0], ddy = nodes[3 * (int64_t)jj[u] + 1] - p[1],
+                                         ddz = nodes[3 * (int64_t)jj[u] + 2] - p[2];
+                            dd[u] = (ddx * ddx + ddy * ddy) + ddz * ddz;
+                        }
+#pragma unroll
+                        for (int u = 0; u < kLoads; ++u)
+                            if (i0 + u < nl) knn_insert<K>(bd, bi, dd[u], jj[u]);
+                    }
+                    // exact when the K-th distance is within the listed range and the cube
+                    // suffices (stopping rule after shell kTileH)
+                    const bool in_range = bd[K - 1] <= dcut;
+                    ok = in_range && knn_done<K>(g, c, p, kTileH, bd);
+                    if (ok) knn_store<K>(nbr, self, bi);
+                    else atomicAdd(&gp->why[in_range ? 2 : 1], 1);
+                } else {
+                    atomicAdd(&gp->why[0], 1);
                 }
+                if (!ok) retry[atomicAdd(&gp->nretry, 1)] = self;
+            }
+        } else {
+            // crowded halo: the block's queries retry from global memory
+            for (int t2 = threadIdx.x; t2 < kTileB * kTileB * kTileB; t2 += kTileThreads) {
+                const int x = bx * kTileB + t2 % kTileB, y = by * kTileB + (t2 / kTileB) % kTileB,
+                          z = bz * kTileB + t2 / (kTileB * kTileB);
+                if (x >= g.dims[0] || y >= g.dims[1] || z >= g.dims[2]) continue;
+                const int cell = (z * g.dims[1] + y) * g.dims[0] + x;
+                const int e = start[cell + 1];
+                for (int t = start[cell]; t < e; ++t) retry[atomicAdd(&gp->nretry, 1)] = sidx[t];
+                if (e > start[cell]) atomicAdd(&gp->why[3], e - start[cell]);
             }
         }
         __syncthreads();  // the LDS tile is rewritten by the next block
@@ -649,6 +775,21 @@ __global__ __launch_bounds__(kTileThreads) void k_knn_tile(KnnGrid* __restrict__
             dbg[4 * b + 3] = blockIdx.x;
         }
     }
+}
+
+// Retry list of k_knn_tile: one wave per query (knn_retry_wave).
+template <int K>
+__global__ __launch_bounds__(256) void k_knn_retry(const KnnGrid* __restrict__ gp, double r2max,
+                                                   const double* __restrict__ nodes,
+                                                   const double* __restrict__ sxyz,
+                                                   const int* __restrict__ sidx,
+                                                   const int* __restrict__ start,
+                                                   const int* __restrict__ retry,
+                                                   int32_t* __restrict__ nbr) {
+    const KnnGrid g = *gp;
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (int i = wave; i < g.nretry; i += nwaves)  // wave-uniform
+        knn_retry_wave<K>(g, r2max, nodes, sxyz, sidx, start, retry[i], nbr);
 }
 
 __global__ void k_knn_edges(const double* __restrict__ nodes, const int32_t* __restrict__ nbr, int64_t m,
@@ -719,15 +860,20 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
         // persistent: the block count is only known on the device (grid shape)
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const dim3 gt((unsigned)std::max(1, cus * 2)), bt(kTileThreads);
+        const dim3 gt((unsigned)std::max(1, cus * 3)), bt(kTileThreads);
         const int mode = tile_env ? std::atoi(tile_env) : 1;  // 2, 4..6: ablations (inexact)
         static unsigned long long* dbg = nullptr;           // diagnostics only
         if (std::getenv("EPP_KNN_TILE_DBG") && !dbg && hipMalloc(&dbg, 4 * 8 * 65536) != hipSuccess) dbg = nullptr;
         unsigned long long* d = std::getenv("EPP_KNN_TILE_DBG") ? dbg : nullptr;
         if (d) (void)hipMemsetAsync(d, 0, 4 * 8 * 65536, s);
-        if (k == 4) hipLaunchKernelGGL(k_knn_tile<4>, gt, bt, 0, s, g, r2, sxyz, sidx, start, nbr, mode, d);
-        else if (k == 8) hipLaunchKernelGGL(k_knn_tile<8>, gt, bt, 0, s, g, r2, sxyz, sidx, start, nbr, mode, d);
-        else hipLaunchKernelGGL(k_knn_tile<16>, gt, bt, 0, s, g, r2, sxyz, sidx, start, nbr, mode, d);
+        int* retry = cell_of;  // free once the scatter has run
+        if (k == 4) hipLaunchKernelGGL(k_knn_tile<4>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr, mode, d);
+        else if (k == 8) hipLaunchKernelGGL(k_knn_tile<8>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr, mode, d);
+        else hipLaunchKernelGGL(k_knn_tile<16>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr, mode, d);
+        const dim3 gr(64), br(256);  // 256 waves: one per retried query
+        if (k == 4) hipLaunchKernelGGL(k_knn_retry<4>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr);
+        else if (k == 8) hipLaunchKernelGGL(k_knn_retry<8>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr);
+        else hipLaunchKernelGGL(k_knn_retry<16>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr);
         if (d) {
             std::vector<unsigned long long> h(4 * 65536);
             (void)hipStreamSynchronize(s);
@@ -735,8 +881,14 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
             unsigned long long t0 = ~0ull, t1 = 0;
             for (int i = 0; i < 65536; ++i)
                 if (h[4 * i + 1]) t0 = std::min(t0, h[4 * i]), t1 = std::max(t1, h[4 * i + 1]);
-            std::fprintf(stderr, "knn_tile blocks (start_us end_us nq wg):\n");
-            for (int i = 0; i < 65536; ++i)
+            KnnGrid hg;
+            (void)hipMemcpy(&hg, g, sizeof(hg), hipMemcpyDeviceToHost);
+            std::fprintf(stderr, "knn_tile n %d dims %d %d %d h %g retries %d (list %d range %d shell %d crowded %d) span_us %.1f\n",
+                         n, hg.dims[0], hg.dims[1], hg.dims[2], hg.h, hg.nretry, hg.why[0], hg.why[1], hg.why[2], hg.why[3],
+                         (t1 - t0) / 100.0);
+            const bool list = std::atoi(std::getenv("EPP_KNN_TILE_DBG")) == 1;
+            if (list) std::fprintf(stderr, "knn_tile blocks (start_us end_us nq wg):\n");
+            for (int i = 0; list && i < 65536; ++i)
                 if (h[4 * i + 1])
                     std::fprintf(stderr, "%d %.2f %.2f %llu %llu\n", i, (h[4 * i] - t0) / 100.0, (h[4 * i + 1] - t0) / 100.0,
                                  h[4 * i + 2], h[4 * i + 3]);
