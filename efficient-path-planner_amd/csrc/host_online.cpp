@@ -9,6 +9,7 @@
 #include <stdexcept>
 
 #include "epp/OnlineTrajGenerator.h"
+#include "epp/OptimalTimeParametrizer.h"
 #include "epp/trajectory_generator.h"
 
 namespace epp {
@@ -71,16 +72,21 @@ bool OnlineTrajGenerator::getGateCenterAndNormal(const std::vector<double>& g, V
     return true;
 }
 
-Matrix OnlineTrajGenerator::generate(const std::vector<Vec3>& path, double t0, const Vec3& v0, const Vec3& a0) const {
+// trajectory of the given type through `path` (src/OnlineTrajGenerator.cpp:95-119 and
+// :375-410); `pre` = the "optimal" type's re-simulated lead-in points
+Matrix OnlineTrajGenerator::generate(const std::vector<Vec3>& path, double t0, const Vec3& v0, const Vec3& a0,
+                                     const std::vector<Vec3>& pre) const {
     const auto& tg = configParser->getTrajectoryGeneratorProperties();
     if (tg.type == "snap") {
         Matrix traj;
         poly_traj::generateTrajectory(path, tg.maxVelocity, tg.maxAcceleration, tg.samplingInterval, t0, v0, a0, traj);
         return traj;
     }
-    if (tg.type == "spline" || tg.type == "optimal")
-        throw std::runtime_error("Trajectory type '" + tg.type +
-                                 "' is not part of this build (only \"snap\", the min-snap path, is)");
+    if (tg.type == "optimal")
+        return OptimalTimeParametrizer::calculateTrajectory(path, pre, tg.maxVelocity, tg.maxAcceleration, t0,
+                                                            tg.samplingInterval, tg.maxTrajDivergence);
+    if (tg.type == "spline")
+        throw std::runtime_error("Trajectory type 'spline' is not part of this build (\"snap\" and \"optimal\" are)");
     std::cerr << "Trajectory type not supported" << std::endl;
     throw std::runtime_error("Trajectory type not supported");
 }
@@ -239,7 +245,15 @@ void OnlineTrajGenerator::recomputeTraj(int gateId, const Vec3& /*dronePos*/, do
     pathSegments[segPost] = post;
     std::vector<std::vector<Vec3>> slice(pathSegments.begin() + segPre, pathSegments.end());
     const std::vector<Vec3> filled = pathPlanner.includeGates2(slice);
-    const Matrix postTraj = generate(filled, advancedTime, velA, accA);
+    std::vector<Vec3> lead;  // "optimal": the last prepend_traj_time seconds, re-simulated
+    if (configParser->getTrajectoryGeneratorProperties().type == "optimal") {
+        const double from = std::max(0.0, advancedTime - configParser->getTrajectoryGeneratorProperties().prependTrajTime);
+        for (double t = from; t < advancedTime; t += 0.1) {
+            const double* r = traj.row(nearestRow(traj, t));
+            lead.emplace_back(r[0], r[3], r[6]);
+        }
+    }
+    const Matrix postTraj = generate(filled, advancedTime, velA, accA, lead);
     Matrix merged(startAdv + postTraj.rows, traj.cols);
     for (size_t i = 0; i < startAdv; ++i)
         for (size_t c = 0; c < traj.cols; ++c) merged(i, c) = traj(i, c);
@@ -250,21 +264,26 @@ void OnlineTrajGenerator::recomputeTraj(int gateId, const Vec3& /*dronePos*/, do
     waypoints = filled;
 }
 
-// src/OnlineTrajGenerator.cpp:423-439
-std::vector<double> OnlineTrajGenerator::sampleTraj(double currentTime) const {
-    std::lock_guard<std::mutex> lk(trajMu);
-    if (plannedTraj.rows == 0) throw std::runtime_error("No trajectory data available.");
-    const size_t tc = plannedTraj.cols - 1;
+// the row whose time (last column) is nearest to t, first on ties (src/OnlineTrajGenerator.cpp:423-439)
+size_t OnlineTrajGenerator::nearestRow(const Matrix& traj, double t) {
+    const size_t tc = traj.cols - 1;
     size_t best_i = 0;
     double best = std::numeric_limits<double>::infinity();
-    for (size_t i = 0; i < plannedTraj.rows; ++i) {
-        const double d = std::abs(plannedTraj(i, tc) - currentTime);
+    for (size_t i = 0; i < traj.rows; ++i) {
+        const double d = std::abs(traj(i, tc) - t);
         if (d < best) {
             best = d;
             best_i = i;
         }
     }
-    return std::vector<double>(plannedTraj.row(best_i), plannedTraj.row(best_i) + plannedTraj.cols);
+    return best_i;
+}
+
+std::vector<double> OnlineTrajGenerator::sampleTraj(double currentTime) const {
+    std::lock_guard<std::mutex> lk(trajMu);
+    if (plannedTraj.rows == 0) throw std::runtime_error("No trajectory data available.");
+    const size_t i = nearestRow(plannedTraj, currentTime);
+    return std::vector<double>(plannedTraj.row(i), plannedTraj.row(i) + plannedTraj.cols);
 }
 
 std::vector<Vec3> OnlineTrajGenerator::getWaypoints() const {

@@ -71,6 +71,8 @@ def lib() -> C.CDLL:
             "epp_sample_batch": (i32, [vp, vp, vp, i32, dp, vp, vp, vp, vp]),
             "epp_generate_trajectory_host": (i32, [vp, i32, dp, dp, dp, dp, vp, vp,
                                                    C.POINTER(C.POINTER(C.c_double)), C.POINTER(i64)]),
+            "epp_optimal_trajectory_host": (i32, [vp, i32, vp, i32, dp, dp, dp, dp, dp,
+                                                  C.POINTER(C.POINTER(C.c_double)), C.POINTER(i64)]),
             "epp_host_free": (None, [vp]),
             "epp_sample_uniform": (i32, [C.c_uint64, vp, vp, i64, i64, vp, vp]),
             "epp_knn": (i32, [vp, i32, i32, dp, vp, vp]),
@@ -101,7 +103,7 @@ EXPORTED = [
     "epp_check_states_mindist", "epp_check_motions", "epp_minsnap_batch", "epp_sample_count",
     "epp_sample_batch", "epp_generate_trajectory_host", "epp_host_free", "epp_sample_uniform", "epp_knn",
     "epp_knn_bruteforce", "epp_knn_grid", "epp_knn_workspace_size", "epp_knn_ws", "epp_knn_grid_ws",
-    "epp_knn_edges", "epp_compact_states", "epp_mask_edges",
+    "epp_knn_edges", "epp_compact_states", "epp_mask_edges", "epp_optimal_trajectory_host",
 ]
 
 
@@ -298,6 +300,24 @@ def generate_trajectory(waypoints, v_max, a_max, dt, t0=0.0, v0=(0, 0, 0), a0=(0
     if n.value == 0:
         return np.zeros((0, 10))
     out = np.ctypeslib.as_array(rows, shape=(n.value * 10,)).copy().reshape(-1, 10)
+    lib().epp_host_free(C.cast(rows, C.c_void_p))
+    return out
+
+
+def optimal_trajectory(waypoints, v_max, a_max, dt, t0=0.0, max_deviation=0.1, pre_waypoints=()) -> np.ndarray:
+    """OptimalTimeParametrizer::calculateTrajectory (the "optimal" type; host code,
+    external/time_parametrization/src/OptimalTimeParametrizer.cpp:11-108): rows x 11."""
+    wp = np.ascontiguousarray(np.asarray(waypoints, np.float64).reshape(-1, 3))
+    pre = np.ascontiguousarray(np.asarray(pre_waypoints, np.float64).reshape(-1, 3))
+    rows = C.POINTER(C.c_double)()
+    n = C.c_int64(0)
+    check(lib().epp_optimal_trajectory_host(_ptr(wp), len(wp), _ptr(pre) if len(pre) else None, len(pre),
+                                            float(v_max), float(a_max), float(dt), float(t0), float(max_deviation),
+                                            C.byref(rows), C.byref(n)))
+    if n.value == 0:
+        lib().epp_host_free(C.cast(rows, C.c_void_p))
+        return np.zeros((0, 11))
+    out = np.ctypeslib.as_array(rows, shape=(n.value * 11,)).copy().reshape(-1, 11)
     lib().epp_host_free(C.cast(rows, C.c_void_p))
     return out
 

@@ -186,6 +186,15 @@ epp_status epp_mask_edges(int32_t* nbr, const uint8_t* valid, int64_t m, void* s
 epp_status epp_generate_trajectory_host(const double* wp, int32_t n_wp, double v_max, double a_max,
                                         double dt, double t0, const double v0[3], const double a0[3],
                                         double** rows, int64_t* n_rows);
+/* The "optimal" trajectory type (OptimalTimeParametrizer::calculateTrajectory,
+ * external/time_parametrization/src/OptimalTimeParametrizer.cpp:11-108; host code: one
+ * sequential phase-plane integration).  wp: n_wp x 3, pre: n_pre x 3 lead-in points
+ * (may be NULL when n_pre = 0).  rows: *n_rows x 11 [x vx ax y vy ay z vz az yaw t+t0],
+ * malloc'd, release with epp_host_free.  EPP_ERR_RUNTIME "Trajectory is not valid" when
+ * the integration fails. */
+epp_status epp_optimal_trajectory_host(const double* wp, int32_t n_wp, const double* pre, int32_t n_pre,
+                                       double v_max, double a_max, double dt, double t0, double max_deviation,
+                                       double** rows, int64_t* n_rows);
 void epp_host_free(void* p);
 
 #ifdef __cplusplus

@@ -46,7 +46,9 @@ private:
     bool getGateCenterAndNormal(const std::vector<double>& gate, Vec3& center, Vec3& normal) const;
     bool checkGatePassed(const Vec3& p1, const Vec3& p2, int gateId) const;
     void recomputeTraj(int gateId, const Vec3& dronePos, double flightTime);
-    Matrix generate(const std::vector<Vec3>& path, double t0, const Vec3& v0, const Vec3& a0) const;
+    Matrix generate(const std::vector<Vec3>& path, double t0, const Vec3& v0, const Vec3& a0,
+                    const std::vector<Vec3>& pre = {}) const;
+    static size_t nearestRow(const Matrix& traj, double t);
     std::vector<double> gateRow(int gateId) const;
 
     std::shared_ptr<ConfigParser> configParser;

@@ -408,6 +408,40 @@ def test_online_async_update(track):
     assert not np.array_equal(otg.get_planned_traj(), before)
 
 
+def test_online_optimal_type(tmp_path, track):
+    """type "optimal" (src/OnlineTrajGenerator.cpp:108-114, :385-406): 11 columns, the
+    planned rows equal the oracle's time-optimal parametrisation of the same waypoints,
+    and a gate update re-simulates the lead-in and keeps the prefix."""
+    import timeopt  # oracle/ (test infrastructure)
+    path, c, gates, obstacles, start, goal = track
+    c2 = json.loads(json.dumps(c))
+    tg = c2["trajectory_generator_properties"]
+    tg["type"] = "optimal"
+    p2 = tmp_path / "c_opt.json"
+    p2.write_text(json.dumps(c2))
+    otg = _ot().OnlineTrajGenerator(start, goal, gates, obstacles, str(p2))
+    otg.pre_compute_traj(1.5)
+    traj = otg.get_planned_traj()
+    assert traj.shape[1] == 11 and len(traj) > 50
+    exp = np.array(timeopt.calculate_trajectory(np.asarray(otg.get_waypoints()), [], tg["max_velocity"],
+                                                tg["max_acceleration"], 1.5, tg["sampling_interval"],
+                                                tg["max_traj_divergence"]))
+    assert np.array_equal(traj, exp)
+    assert len(otg.sample_traj(2.0)) == 11 and otg.get_traj_end_time() == traj[-1, 10]
+    np.testing.assert_allclose(traj[0, [0, 3, 6]], start, atol=1e-12)
+    before = traj
+    gid = 2
+    t_fly = 2.0
+    i = int(np.argmin(np.abs(before[:, 10] - t_fly)))
+    replanned = otg.update_gate_pos(gid, _lateral(gates[gid], 0.3), before[i, [0, 3, 6]], True, t_fly)
+    after = otg.get_planned_traj()
+    assert after.shape[1] == 11
+    adv = t_fly + c["path_planner_properties"]["time_limit_online"] + 0.01
+    k = int(np.argmax(before[:, 10] > adv))
+    assert np.array_equal(after[:k], before[:k])
+    assert replanned == (not np.array_equal(after, before))
+
+
 def test_trajectory_type_not_supported(tmp_path, track):
     path, c, gates, obstacles, start, goal = track
     c2 = json.loads(json.dumps(c))
