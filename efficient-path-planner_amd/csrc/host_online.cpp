@@ -10,6 +10,7 @@
 
 #include "epp/OnlineTrajGenerator.h"
 #include "epp/OptimalTimeParametrizer.h"
+#include "epp/TrajInterpolation.h"
 #include "epp/trajectory_generator.h"
 
 namespace epp {
@@ -45,8 +46,12 @@ std::vector<double> OnlineTrajGenerator::gateRow(int gateId) const {
                                nominalGatePositionAndType.row(gateId) + nominalGatePositionAndType.cols);
 }
 
-// checkpoints — src/OnlineTrajGenerator.cpp:32-47
+// debug dumps + checkpoints — src/OnlineTrajGenerator.cpp:20-47
 void OnlineTrajGenerator::init(const Vec3& start, const Vec3& goal) {
+    for (size_t i = 0; i < nominalGatePositionAndType.rows; ++i) pathWriter.updateGatePos((int)i, gateRow((int)i));
+    for (size_t i = 0; i < nominalObstaclePosition.rows; ++i)
+        pathWriter.updateObstaclePos((int)i, std::vector<double>(nominalObstaclePosition.row(i),
+                                                                 nominalObstaclePosition.row(i) + nominalObstaclePosition.cols));
     checkpoints.push_back(start);
     const double offset = configParser->getPathPlannerProperties().checkpointGateOffset;
     for (size_t i = 0; i < nominalGatePositionAndType.rows; ++i) {
@@ -56,6 +61,7 @@ void OnlineTrajGenerator::init(const Vec3& start, const Vec3& goal) {
         checkpoints.push_back(center + normal * offset);
     }
     checkpoints.push_back(goal);
+    pathWriter.writeCheckpoints(checkpoints);
 }
 
 // src/OnlineTrajGenerator.cpp:50-70
@@ -85,8 +91,7 @@ Matrix OnlineTrajGenerator::generate(const std::vector<Vec3>& path, double t0, c
     if (tg.type == "optimal")
         return OptimalTimeParametrizer::calculateTrajectory(path, pre, tg.maxVelocity, tg.maxAcceleration, t0,
                                                             tg.samplingInterval, tg.maxTrajDivergence);
-    if (tg.type == "spline")
-        throw std::runtime_error("Trajectory type 'spline' is not part of this build (\"snap\" and \"optimal\" are)");
+    if (tg.type == "spline") return TrajInterpolation().interpolateTraj(path, tg.maxTime, t0, tg.samplingInterval);
     std::cerr << "Trajectory type not supported" << std::endl;
     throw std::runtime_error("Trajectory type not supported");
 }
@@ -103,6 +108,7 @@ void OnlineTrajGenerator::preComputeTraj(double takeoffTime) {
         pathSegments.push_back(path);
     }
     const std::vector<Vec3> pruned = pathPlanner.includeGates2(pathSegments);
+    pathWriter.writePath(pruned);
     Matrix traj = generate(pruned, takeoffTime, Vec3(0, 0, 0), Vec3(0, 0, 0));
     std::lock_guard<std::mutex> lk(trajMu);
     plannedTraj = std::move(traj);
@@ -137,6 +143,7 @@ bool OnlineTrajGenerator::updateGatePos(int gateId, const std::vector<double>& n
     gatesObservedWithinRange.insert(gateId);
     for (int k = 0; k < 6; ++k) nominalGatePositionAndType(gateId, k) = newPose[k];
     pathPlanner.parseGatesAndObstacles(nominalGatePositionAndType, nominalObstaclePosition);
+    pathWriter.updateGatePos(gateId, gateRow(gateId));
 
     Matrix traj;
     {
@@ -207,6 +214,7 @@ void OnlineTrajGenerator::recomputeTraj(int gateId, const Vec3& /*dronePos*/, do
     getGateCenterAndNormal(gateRow(segPre), center, normal);
     checkpoints[cpPre] = center - normal * pp.checkpointGateOffset;
     checkpoints[cpPost] = center + normal * pp.checkpointGateOffset;
+    pathWriter.writeCheckpoints(checkpoints);
 
     double advancedTime = flightTime;
     if (pp.advanceForCalculation) advancedTime += pp.timeLimitOnline + 0.01;
@@ -245,6 +253,7 @@ void OnlineTrajGenerator::recomputeTraj(int gateId, const Vec3& /*dronePos*/, do
     pathSegments[segPost] = post;
     std::vector<std::vector<Vec3>> slice(pathSegments.begin() + segPre, pathSegments.end());
     const std::vector<Vec3> filled = pathPlanner.includeGates2(slice);
+    pathWriter.writePath(filled);
     std::vector<Vec3> lead;  // "optimal": the last prepend_traj_time seconds, re-simulated
     if (configParser->getTrajectoryGeneratorProperties().type == "optimal") {
         const double from = std::max(0.0, advancedTime - configParser->getTrajectoryGeneratorProperties().prependTrajTime);

@@ -73,6 +73,8 @@ def lib() -> C.CDLL:
                                                    C.POINTER(C.POINTER(C.c_double)), C.POINTER(i64)]),
             "epp_optimal_trajectory_host": (i32, [vp, i32, vp, i32, dp, dp, dp, dp, dp,
                                                   C.POINTER(C.POINTER(C.c_double)), C.POINTER(i64)]),
+            "epp_spline_trajectory_host": (i32, [vp, i32, dp, dp, dp, C.POINTER(C.POINTER(C.c_double)),
+                                                 C.POINTER(i64)]),
             "epp_host_free": (None, [vp]),
             "epp_sample_uniform": (i32, [C.c_uint64, vp, vp, i64, i64, vp, vp]),
             "epp_knn": (i32, [vp, i32, i32, dp, vp, vp]),
@@ -104,6 +106,7 @@ EXPORTED = [
     "epp_sample_batch", "epp_generate_trajectory_host", "epp_host_free", "epp_sample_uniform", "epp_knn",
     "epp_knn_bruteforce", "epp_knn_grid", "epp_knn_workspace_size", "epp_knn_ws", "epp_knn_grid_ws",
     "epp_knn_edges", "epp_compact_states", "epp_mask_edges", "epp_optimal_trajectory_host",
+    "epp_spline_trajectory_host",
 ]
 
 
@@ -318,6 +321,19 @@ def optimal_trajectory(waypoints, v_max, a_max, dt, t0=0.0, max_deviation=0.1, p
         lib().epp_host_free(C.cast(rows, C.c_void_p))
         return np.zeros((0, 11))
     out = np.ctypeslib.as_array(rows, shape=(n.value * 11,)).copy().reshape(-1, 11)
+    lib().epp_host_free(C.cast(rows, C.c_void_p))
+    return out
+
+
+def spline_trajectory(waypoints, max_t, dt, t0=0.0) -> np.ndarray:
+    """TrajInterpolation::interpolateTraj (the "spline" type; host code,
+    src/TrajInterpolation.cpp:44-68): rows x 10."""
+    wp = np.ascontiguousarray(np.asarray(waypoints, np.float64).reshape(-1, 3))
+    rows = C.POINTER(C.c_double)()
+    n = C.c_int64(0)
+    check(lib().epp_spline_trajectory_host(_ptr(wp), len(wp), float(max_t), float(t0), float(dt),
+                                           C.byref(rows), C.byref(n)))
+    out = np.ctypeslib.as_array(rows, shape=(n.value * 10,)).copy().reshape(-1, 10) if n.value else np.zeros((0, 10))
     lib().epp_host_free(C.cast(rows, C.c_void_p))
     return out
 

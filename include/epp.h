@@ -195,6 +195,12 @@ epp_status epp_generate_trajectory_host(const double* wp, int32_t n_wp, double v
 epp_status epp_optimal_trajectory_host(const double* wp, int32_t n_wp, const double* pre, int32_t n_pre,
                                        double v_max, double a_max, double dt, double t0, double max_deviation,
                                        double** rows, int64_t* n_rows);
+/* The "spline" trajectory type (TrajInterpolation::interpolateTraj,
+ * src/TrajInterpolation.cpp:44-68): cubic B-spline through wp (n_wp >= 4) at chord-length
+ * parameters, int((max_t - t0) / dt) + 1 rows [x 0 0 y 0 0 z 0 0 t], t = i dt + t0;
+ * malloc'd, release with epp_host_free. */
+epp_status epp_spline_trajectory_host(const double* wp, int32_t n_wp, double max_t, double t0, double dt,
+                                      double** rows, int64_t* n_rows);
 void epp_host_free(void* p);
 
 #ifdef __cplusplus

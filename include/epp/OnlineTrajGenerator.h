@@ -15,6 +15,7 @@
 
 #include "epp/ConfigParser.h"
 #include "epp/PathPlanner.h"
+#include "epp/PathWriter.h"
 #include "epp/types.h"
 
 namespace epp {
@@ -63,6 +64,7 @@ private:
     mutable std::mutex trajMu;
     bool trajectoryCurrentlyUpdating = false;
     std::future<void> pending;
+    PathWriter pathWriter{"path_segments"};  // include/OnlineTrajGenerator.h:132
 };
 
 }  // namespace epp

@@ -442,6 +442,34 @@ def test_online_optimal_type(tmp_path, track):
     assert replanned == (not np.array_equal(after, before))
 
 
+def test_online_spline_type_and_path_writer(tmp_path, track, monkeypatch):
+    """type "spline" (src/OnlineTrajGenerator.cpp:102-107: TrajInterpolation through the
+    waypoints, sampled up to max_time) and the PathWriter dumps the reference writes to
+    ./path_segments (src/PathWriter.cpp, src/OnlineTrajGenerator.cpp:20-47, :90)."""
+    import spline_np  # oracle/ (test infrastructure)
+    path, c, gates, obstacles, start, goal = track
+    c2 = json.loads(json.dumps(c))
+    tg = c2["trajectory_generator_properties"]
+    tg["type"] = "spline"
+    p2 = tmp_path / "c_spline.json"
+    p2.write_text(json.dumps(c2))
+    monkeypatch.chdir(tmp_path)
+    otg = _ot().OnlineTrajGenerator(start, goal, gates, obstacles, str(p2))
+    otg.pre_compute_traj(1.5)
+    traj = otg.get_planned_traj()
+    wp = np.asarray(otg.get_waypoints())
+    exp = spline_np.interpolate_traj(wp, tg["max_time"], 1.5, tg["sampling_interval"])
+    assert traj.shape == exp.shape and traj.shape[1] == 10
+    np.testing.assert_allclose(traj, exp, rtol=0, atol=1e-9)
+    out = tmp_path / "path_segments"
+    assert sorted(os.listdir(out)) == ["checkpoints.txt", "gates.txt", "obstacles.txt", "path_0.txt"]
+    assert len((out / "gates.txt").read_text().splitlines()) == len(gates)
+    assert len((out / "obstacles.txt").read_text().splitlines()) == len(obstacles)
+    pts = np.loadtxt(out / "path_0.txt")
+    np.testing.assert_allclose(pts, wp, rtol=1e-5, atol=1e-5)  # default stream precision (6 digits)
+    assert (out / "gates.txt").read_text().splitlines()[0].startswith("id: 0 info: ")
+
+
 def test_trajectory_type_not_supported(tmp_path, track):
     path, c, gates, obstacles, start, goal = track
     c2 = json.loads(json.dumps(c))
