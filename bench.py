@@ -70,7 +70,7 @@ def main():
     ap.add_argument("--no-side", action="store_true", help="skip the side measurements")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-plan", action="store_true", help="skip the full-plan (C4) leg")
-    ap.add_argument("--plan-reps", type=int, default=3)
+    ap.add_argument("--plan-reps", type=int, default=5)
     args = ap.parse_args()
 
     from eppamd.dist import Dist, env

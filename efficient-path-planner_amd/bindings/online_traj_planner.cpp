@@ -137,6 +137,28 @@ PYBIND11_MODULE(online_traj_planner, m) {
             py::arg("start"), py::arg("end"), py::arg("canPassGate") = false)
         .def("update_gate_pos",
              [](epp::PathPlanner& self, int gateId, const std::vector<double>& pose) { self.updateGatePos(gateId, pose); })
+        .def(
+            "plan_paths",  // concurrent planPath over independent (start, goal) pairs
+            [](const epp::PathPlanner& self, const std::vector<std::pair<py::object, py::object>>& problems,
+               double timeLimit) {
+                std::vector<std::pair<Vec3, Vec3>> pr;
+                for (const auto& p : problems) pr.emplace_back(to_vec3(p.first), to_vec3(p.second));
+                std::vector<std::vector<Vec3>> paths;
+                std::vector<char> ok;
+                {
+                    py::gil_scoped_release release;
+                    self.planPaths(pr, timeLimit, paths, ok);
+                }
+                py::list out;
+                for (size_t i = 0; i < pr.size(); ++i) {
+                    py::array_t<double> a({(py::ssize_t)paths[i].size(), (py::ssize_t)3});
+                    for (size_t j = 0; j < paths[i].size(); ++j)
+                        for (int k = 0; k < 3; ++k) a.mutable_data()[j * 3 + k] = paths[i][j][k];
+                    out.append(py::make_tuple((bool)ok[i], a));
+                }
+                return out;
+            },
+            py::arg("problems"), py::arg("timeLimit"))
         .def("set_seed", &epp::PathPlanner::setSeed)
         .def("set_neighbours", &epp::PathPlanner::setNeighbours)
         .def("last_stats", [](const epp::PathPlanner& self) {

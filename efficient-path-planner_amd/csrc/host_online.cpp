@@ -101,11 +101,16 @@ void OnlineTrajGenerator::preComputeTraj(double takeoffTime) {
     waitForUpdate();
     const double timeLimit = configParser->getPathPlannerProperties().timeLimitOffline;
     pathSegments.clear();
-    for (size_t i = 0; i + 1 < checkpoints.size(); i += 2) {
-        std::vector<Vec3> path;
-        if (!pathPlanner.planPath(checkpoints[i], checkpoints[i + 1], timeLimit, path))
-            throw std::runtime_error("Path not found");
-        pathSegments.push_back(path);
+    // the gate-to-gate segments are independent: planned concurrently (the reference
+    // loops over them); the first failure in segment order throws, as in the loop
+    std::vector<std::pair<Vec3, Vec3>> problems;
+    for (size_t i = 0; i + 1 < checkpoints.size(); i += 2) problems.emplace_back(checkpoints[i], checkpoints[i + 1]);
+    std::vector<std::vector<Vec3>> paths;
+    std::vector<char> ok;
+    pathPlanner.planPaths(problems, timeLimit, paths, ok);
+    for (size_t s = 0; s < problems.size(); ++s) {
+        if (!ok[s]) throw std::runtime_error("Path not found");
+        pathSegments.push_back(paths[s]);
     }
     const std::vector<Vec3> pruned = pathPlanner.includeGates2(pathSegments);
     pathWriter.writePath(pruned);
@@ -237,10 +242,15 @@ void OnlineTrajGenerator::recomputeTraj(int gateId, const Vec3& /*dronePos*/, do
         return;
     }
     if (cpNext >= checkpoints.size()) throw std::runtime_error("Post segment path not found. Exiting");
-    // the two segments are planned back to back; each is one batched GPU pass
-    std::vector<Vec3> pre, post;
-    const bool okPre = pathPlanner.planPath(posA, checkpoints[cpPre], pp.timeLimitOnline, pre);
-    const bool okPost = pathPlanner.planPath(checkpoints[cpPost], checkpoints[cpNext], pp.timeLimitOnline, post);
+    // the two segments are planned concurrently, like the reference's two threads
+    // (src/OnlineTrajGenerator.cpp:324-340)
+    std::vector<std::vector<Vec3>> two;
+    std::vector<char> okTwo;
+    pathPlanner.planPaths({{posA, checkpoints[cpPre]}, {checkpoints[cpPost], checkpoints[cpNext]}}, pp.timeLimitOnline,
+                          two, okTwo);
+    const std::vector<Vec3>& pre = two[0];
+    const std::vector<Vec3>& post = two[1];
+    const bool okPre = okTwo[0] != 0, okPost = okTwo[1] != 0;
     if (!okPre) {
         std::cerr << "Pre path not found. Exiting" << std::endl;
         throw std::runtime_error("Pre path not found. Exiting");

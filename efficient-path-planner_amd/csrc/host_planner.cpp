@@ -8,8 +8,15 @@
 #include <limits>
 #include <mutex>
 #include <queue>
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
 #include <stdexcept>
+#include <thread>
 #include <utility>
+
+#include <hip/hip_runtime_api.h>
 
 #include "epp/PathPlanner.h"
 #include "host_scratch.h"
@@ -18,6 +25,46 @@ namespace epp {
 
 namespace {
 std::mutex g_stats_mu;
+
+// Worker threads for PathPlanner::planPaths.  Grown on demand and never torn down (the
+// process exit ends them; their thread-local device scratch is then left to the runtime
+// rather than freed after it).
+class PlanPool {
+public:
+    void submit(std::function<void()> job) {
+        std::lock_guard<std::mutex> lk(mu_);
+        q_.push_back(std::move(job));
+        // a waiting thread per queued job, else one more thread
+        if (idle_ < (int)q_.size()) std::thread([this] { loop(); }).detach();
+        else cv_.notify_one();
+    }
+
+private:
+    void loop() {
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            while (q_.empty()) {
+                ++idle_;
+                cv_.wait(lk);
+                --idle_;
+            }
+            std::function<void()> job = std::move(q_.front());
+            q_.pop_front();
+            lk.unlock();
+            job();
+            lk.lock();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+    int idle_ = 0;
+};
+
+PlanPool& plan_pool() {
+    static PlanPool* pool = new PlanPool();  // intentionally leaked (see above)
+    return *pool;
+}
 
 uint64_t mix(uint64_t a, uint64_t b) {
     uint64_t x = a ^ (b + 0x9E3779B97F4A7C15ull + (a << 6) + (a >> 2));
@@ -74,9 +121,10 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     const size_t max_nodes = n_s + 2;
     const size_t m_max = max_nodes * (size_t)k;
     const size_t ws_bytes = (size_t)epp_knn_workspace_size((int32_t)max_nodes);
+    const size_t cws_bytes = (size_t)epp_compact_workspace_size((int64_t)n_s);
     ts.reset(ThreadScratch::rounded(n_s * 24) + ThreadScratch::rounded(n_s) + ThreadScratch::rounded(max_nodes * 24) +
              ThreadScratch::rounded(8) + ThreadScratch::rounded(m_max * 4) + 2 * ThreadScratch::rounded(m_max * 24) +
-             ThreadScratch::rounded(m_max) + ThreadScratch::rounded(ws_bytes));
+             ThreadScratch::rounded(m_max) + ThreadScratch::rounded(ws_bytes) + ThreadScratch::rounded(cws_bytes));
     double* d_s = static_cast<double*>(ts.carve(n_s * 24));
     uint8_t* d_v = static_cast<uint8_t*>(ts.carve(n_s));
     double* d_nodes = static_cast<double*>(ts.carve(max_nodes * 24));
@@ -86,12 +134,13 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     double* d_e2 = static_cast<double*>(ts.carve(m_max * 24));
     uint8_t* d_ev = static_cast<uint8_t*>(ts.carve(m_max));
     void* d_ws = ts.carve(ws_bytes);
+    void* d_cws = ts.carve(cws_bytes);
     const double lo[3] = {wp.lowerBound.x, wp.lowerBound.y, wp.lowerBound.z};
     const double hi[3] = {wp.upperBound.x, wp.upperBound.y, wp.upperBound.z};
     const double ends[6] = {start.x, start.y, start.z, goal.x, goal.y, goal.z};
     check(epp_sample_uniform(seed, lo, hi, samples, 0, d_s, st), "sample");
     check(epp_check_states(w, d_s, samples, canPass ? 1 : 0, d_v, nullptr, nullptr, st), "state check");
-    check(epp_compact_states(d_s, d_v, samples, d_nodes + 6, d_cnt, st), "compact");
+    check(epp_compact_states_ws(d_s, d_v, samples, d_nodes + 6, d_cnt, d_cws, cws_bytes, st), "compact");
     check(epp_memcpy_h2d(d_nodes, ends, sizeof(ends), st), "upload");  // (synchronises the stream)
     int64_t n_valid_states = 0;
     check(epp_memcpy_d2h(&n_valid_states, d_cnt, 8, st), "download");
@@ -244,25 +293,110 @@ bool PathPlanner::planPath(const Vec3& start, const Vec3& goal, double timeLimit
         std::lock_guard<std::mutex> lk(g_stats_mu);
         stats_ = PlannerStats();
     }
-    int64_t samples = pp.samplesFMT > 0 ? pp.samplesFMT : 4096;
     const uint64_t call = __atomic_fetch_add(&calls_, 1, __ATOMIC_RELAXED);
+    int attempts = 0;
+    const bool ok = planCall(start, goal, timeLimit, call, resultPath, attempts);
+    {
+        std::lock_guard<std::mutex> lk(g_stats_mu);
+        stats_.attempts = attempts;
+        stats_.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return ok;
+}
+
+// One planPath problem with its call number (the seed): up to 4 attempts with doubled
+// samples while inside timeLimit (the role of solve(timeLimit), src/PathPlanner.cpp:126-136)
+bool PathPlanner::planCall(const Vec3& start, const Vec3& goal, double timeLimit, uint64_t call,
+                           std::vector<Vec3>& out, int& attempts) const {
+    const auto t0 = std::chrono::steady_clock::now();
+    const auto& pp = configParser->getPathPlannerProperties();
+    int64_t samples = pp.samplesFMT > 0 ? pp.samplesFMT : 4096;
     uint64_t seed = mix(seed_, call);
     for (int d = 0; d < 3; ++d) seed = mix(mix(seed, bits_of(start[d])), bits_of(goal[d]));
     bool ok = false;
-    int attempt = 0;
-    for (; attempt < 4 && !ok; ++attempt) {
-        ok = planOnce(start, goal, samples, mix(seed, attempt), resultPath);
+    attempts = 0;
+    for (; attempts < 4 && !ok; ++attempts) {
+        ok = planOnce(start, goal, samples, mix(seed, attempts), out);
         const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        if (!ok && el > timeLimit) break;  // out of time: give up like solve(timeLimit)
+        if (!ok && el > timeLimit) {  // out of time: give up like solve(timeLimit)
+            ++attempts;
+            break;
+        }
         samples *= 2;
     }
+    if (!ok) out.clear();
+    return ok;
+}
+
+void PathPlanner::planPaths(const std::vector<std::pair<Vec3, Vec3>>& problems, double timeLimit,
+                            std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const {
+    const auto& pp = configParser->getPathPlannerProperties();
+    if (pp.planner != "rrt" && pp.planner != "fmt") {
+        std::cerr << "Unknown planner" << std::endl;
+        throw std::runtime_error("Unknown planner");
+    }
+    const size_t n = problems.size();
+    paths.assign(n, {});
+    ok.assign(n, 0);
+    if (n == 0) return;
+    const auto t0 = std::chrono::steady_clock::now();
     {
         std::lock_guard<std::mutex> lk(g_stats_mu);
-        stats_.attempts = attempt;
-        stats_.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        stats_ = PlannerStats();
     }
-    if (!ok) resultPath.clear();
-    return ok;
+    const uint64_t base = __atomic_fetch_add(&calls_, (uint64_t)n, __ATOMIC_RELAXED);
+    std::vector<int> attempts(n, 0);
+    std::vector<std::exception_ptr> err(n);
+    auto run = [&](size_t i) {
+        try {
+            ok[i] = planCall(problems[i].first, problems[i].second, timeLimit, base + i, paths[i], attempts[i]) ? 1 : 0;
+        } catch (...) {
+            err[i] = std::current_exception();
+        }
+    };
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    (void)worldPtr->device();  // build the device world once, before the threads share it
+    // problems 1.. on persistent pool threads (their ThreadScratch -- stream, device and
+    // pinned buffers -- survives between calls), problem 0 on the calling thread
+    std::mutex done_mu;
+    std::condition_variable done_cv;
+    const char* conc = std::getenv("EPP_PLAN_CONCURRENT");  // 0: one after the other (A/B)
+    if (conc && std::atoi(conc) == 0) {
+        for (size_t i = 0; i < n; ++i) run(i);
+        std::lock_guard<std::mutex> lk(g_stats_mu);
+        stats_.attempts = *std::max_element(attempts.begin(), attempts.end());
+        stats_.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        for (const auto& e : err)
+            if (e) std::rethrow_exception(e);
+        return;
+    }
+    // W concurrent planners (the caller + W-1 pool threads) pull problems in order: more
+    // than the hardware queues a process gets (4) only adds host contention
+    const char* thr = std::getenv("EPP_PLAN_THREADS");
+    const size_t W = std::min(n, (size_t)std::max(1, thr ? std::atoi(thr) : 4));
+    std::atomic<size_t> next{0};
+    auto drain = [&] {
+        for (size_t i = next++; i < n; i = next++) run(i);
+    };
+    size_t pending = W - 1;
+    for (size_t w = 1; w < W; ++w)
+        plan_pool().submit([&, dev] {
+            (void)hipSetDevice(dev);
+            drain();
+            std::lock_guard<std::mutex> lk(done_mu);
+            if (--pending == 0) done_cv.notify_all();
+        });
+    drain();
+    {
+        std::unique_lock<std::mutex> lk(done_mu);
+        done_cv.wait(lk, [&] { return pending == 0; });
+    }
+    for (const auto& e : err)
+        if (e) std::rethrow_exception(e);
+    std::lock_guard<std::mutex> lk(g_stats_mu);
+    stats_.attempts = *std::max_element(attempts.begin(), attempts.end());
+    stats_.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 // PathPlanner::includeGates2 — src/PathPlanner.cpp:175-230

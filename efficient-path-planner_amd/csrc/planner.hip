@@ -1131,12 +1131,28 @@ epp_status epp_compact_states(const double* xyz, const uint8_t* valid, int64_t n
         return EPP_ERR_HIP;
     }
     counts = static_cast<int*>(c.buf);
+    const epp_status rc = epp_compact_states_ws(xyz, valid, n, out, n_out, counts, c.cap, stream);
+    if (hipEventRecord(c.done, s) == hipSuccess) c.used = true;
+    return rc;
+}
+
+uint64_t epp_compact_workspace_size(int64_t n) {
+    return n <= 0 ? 4 : (uint64_t)((n + kCompactChunk - 1) / kCompactChunk) * 4;
+}
+
+epp_status epp_compact_states_ws(const double* xyz, const uint8_t* valid, int64_t n, double* out, int64_t* n_out,
+                                 void* ws, uint64_t ws_bytes, void* stream) {
+    if (n < 0 || !n_out || (n > 0 && (!xyz || !valid || !out)) || !ws || ws_bytes < epp_compact_workspace_size(n)) {
+        set_error("epp_compact_states: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    const int nb = (int)std::max<int64_t>(1, (n + kCompactChunk - 1) / kCompactChunk);
+    int* counts = static_cast<int*>(ws);
     hipLaunchKernelGGL(k_compact_count, dim3(nb), dim3(kCompactThreads), 0, s, valid, n, counts);
     hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(64), 0, s, counts, nb, n_out);
     hipLaunchKernelGGL(k_compact_scatter, dim3(nb), dim3(kCompactThreads), 0, s, xyz, valid, n, counts, out);
-    const epp_status rc = last("epp_compact_states");
-    if (hipEventRecord(c.done, s) == hipSuccess) c.used = true;
-    return rc;
+    return last("epp_compact_states");
 }
 
 epp_status epp_mask_edges(int32_t* nbr, const uint8_t* valid, int64_t m, void* stream) {

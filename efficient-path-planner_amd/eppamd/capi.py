@@ -85,6 +85,8 @@ def lib() -> C.CDLL:
             "epp_knn_grid_ws": (i32, [vp, i32, i32, dp, vp, vp, C.c_uint64, vp]),
             "epp_knn_edges": (i32, [vp, vp, i32, i32, vp, vp, vp]),
             "epp_compact_states": (i32, [vp, vp, i64, vp, vp, vp]),
+            "epp_compact_workspace_size": (C.c_uint64, [i64]),
+            "epp_compact_states_ws": (i32, [vp, vp, i64, vp, vp, vp, C.c_uint64, vp]),
             "epp_mask_edges": (i32, [vp, vp, i64, vp]),
         }
         for name, (res, args) in sig.items():
@@ -106,7 +108,7 @@ EXPORTED = [
     "epp_sample_batch", "epp_generate_trajectory_host", "epp_host_free", "epp_sample_uniform", "epp_knn",
     "epp_knn_bruteforce", "epp_knn_grid", "epp_knn_workspace_size", "epp_knn_ws", "epp_knn_grid_ws",
     "epp_knn_edges", "epp_compact_states", "epp_mask_edges", "epp_optimal_trajectory_host",
-    "epp_spline_trajectory_host",
+    "epp_spline_trajectory_host", "epp_compact_workspace_size", "epp_compact_states_ws",
 ]
 
 
@@ -367,14 +369,19 @@ def knn(nodes: np.ndarray, k: int, max_dist: float = 0.0, method: str = "auto") 
     return d_k.download(np.int32, n * k).reshape(n, k)
 
 
-def compact_states(xyz: np.ndarray, valid: np.ndarray) -> np.ndarray:
-    """epp_compact_states: the valid rows of xyz, in index order."""
+def compact_states(xyz: np.ndarray, valid: np.ndarray, ws: bool = False) -> np.ndarray:
+    """epp_compact_states (ws: epp_compact_states_ws, caller workspace): the valid rows of
+    xyz, in index order."""
     xyz = np.ascontiguousarray(np.asarray(xyz, np.float64).reshape(-1, 3))
     valid = np.ascontiguousarray(np.asarray(valid, np.uint8))
     n = len(xyz)
     d_x, d_v = DeviceBuffer.from_array(xyz), DeviceBuffer.from_array(valid)
     d_o, d_c = DeviceBuffer(24 * max(n, 1)), DeviceBuffer(8)
-    check(lib().epp_compact_states(d_x.ptr, d_v.ptr, n, d_o.ptr, d_c.ptr, None))
+    if ws:
+        d_w = DeviceBuffer(int(lib().epp_compact_workspace_size(n)))
+        check(lib().epp_compact_states_ws(d_x.ptr, d_v.ptr, n, d_o.ptr, d_c.ptr, d_w.ptr, d_w.nbytes, None))
+    else:
+        check(lib().epp_compact_states(d_x.ptr, d_v.ptr, n, d_o.ptr, d_c.ptr, None))
     sync()
     cnt = int(d_c.download(np.int64, 1)[0])
     return d_o.download(np.float64, 3 * cnt).reshape(cnt, 3) if cnt else np.zeros((0, 3))

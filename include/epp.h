@@ -177,6 +177,12 @@ epp_status epp_knn_edges(const double* nodes, const int32_t* nbr, int32_t n, int
  * valid[i] != 0, in index order; *n_out (device int64) = their count.  out holds n x 3. */
 epp_status epp_compact_states(const double* xyz, const uint8_t* valid, int64_t n, double* out, int64_t* n_out,
                               void* stream);
+/* Caller-workspace variant (ws: >= epp_compact_workspace_size(n) device bytes that no
+ * other stream uses until this call's kernels completed); epp_compact_states uses a
+ * cached per-device workspace ordered by an event (serialising concurrent streams). */
+uint64_t epp_compact_workspace_size(int64_t n);
+epp_status epp_compact_states_ws(const double* xyz, const uint8_t* valid, int64_t n, double* out, int64_t* n_out,
+                                 void* ws, uint64_t ws_bytes, void* stream);
 /* nbr[e] = -1 where valid[e] == 0 (edges that failed the motion check), in place. */
 epp_status epp_mask_edges(int32_t* nbr, const uint8_t* valid, int64_t m, void* stream);
 

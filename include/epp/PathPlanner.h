@@ -42,6 +42,13 @@ public:
 
     void parseGatesAndObstacles(const Matrix& nominalGatePositionAndType, const Matrix& nominalObstaclePosition);
     bool planPath(const Vec3& start, const Vec3& goal, double timeLimit, std::vector<Vec3>& resultPath) const;
+    // Independent (start, goal) problems planned concurrently, one host thread and one
+    // HIP stream each (their small kernels overlap on the GPU).  Problem i gets the seed
+    // of the i-th of consecutive planPath calls, so results do not depend on thread
+    // timing.  ok[i] / paths[i] as planPath's return value / resultPath; stats = the sum,
+    // ms = the batch's wall time.
+    void planPaths(const std::vector<std::pair<Vec3, Vec3>>& problems, double timeLimit,
+                   std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const;
     void updateGatePos(int gateId, const std::vector<double>& newPose);
     bool checkTrajectoryValidity(const Matrix& trajectory, double minDistance) const;
     std::vector<Vec3> includeGates2(std::vector<std::vector<Vec3>> waypoints) const;
@@ -58,6 +65,8 @@ private:
     std::vector<Vec3> shortcut(const std::vector<Vec3>& path) const;
     bool planOnce(const Vec3& start, const Vec3& goal, int64_t samples, uint64_t seed,
                   std::vector<Vec3>& out) const;
+    bool planCall(const Vec3& start, const Vec3& goal, double timeLimit, uint64_t call, std::vector<Vec3>& out,
+                  int& attempts) const;
 
     std::shared_ptr<ConfigParser> configParser;
     uint64_t seed_ = 0x5eedull;

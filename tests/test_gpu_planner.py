@@ -195,6 +195,25 @@ def test_plan_path_seeded_is_deterministic(c1):
     assert np.array_equal(pa, pb)
 
 
+def test_plan_paths_concurrent_matches_sequential(c1):
+    """planPaths (one host thread + stream per problem) gives problem i exactly what the
+    i-th of consecutive planPath calls gives, failures included, whatever the timing."""
+    g, o, start, goal, w, rg, ro = c1
+    blocked = np.array([1.0, 0.5, 0.5])  # inside an obstacle
+    problems = [(start, goal), (goal, start), (start, blocked), (start, (start + goal) / 2), (goal, start)]
+    a = _ot().PathPlanner(g, o, CONFIG)
+    seq = [a.plan_path(s, t, 0.5) for s, t in problems]
+    for rep in range(2):
+        b = _ot().PathPlanner(g, o, CONFIG)
+        con = b.plan_paths(problems, 0.5)
+        assert len(con) == len(problems)
+        for (ok, path), ref in zip(con, seq):
+            assert ok == (ref is not None)
+            if ok:
+                assert np.array_equal(path, ref)
+                _path_valid(path, w, rg, ro, False)
+
+
 def test_plan_path_blocked_goal(c1):
     g, o, start, _, *_ = c1
     pp = _ot().PathPlanner(g, o, CONFIG)
@@ -495,6 +514,7 @@ def test_compact_states_ordered(n):
     xyz = synth.sample_states(12, [-6, -6, 0], [6, 6, 2], n)
     valid = (np.random.RandomState(n).rand(n) < 0.9).astype(np.uint8)
     assert np.array_equal(capi.compact_states(xyz, valid), xyz[valid.astype(bool)])
+    assert np.array_equal(capi.compact_states(xyz, valid, ws=True), xyz[valid.astype(bool)])
     assert len(capi.compact_states(xyz, np.zeros(n, np.uint8))) == 0
 
 
