@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -44,7 +45,7 @@ struct SegScratch {  // per-segment scratch: A^-1 (100), H (100), Q 6x6 block (3
     static constexpr int kAinv = 0, kH = 100, kQ = 200, kW = 236, kL = 252, kSize = 268;
 };
 
-__device__ __forceinline__ double nfabian(const double* p, const double* q, double vmax,
+__host__ __device__ __forceinline__ double nfabian(const double* p, const double* q, double vmax,
                                           double amax) {
     // estimateSegmentTimesNfabian — src/vertex.cpp:272-289 (magic 6.5)
     const double d0 = q[0] - p[0], d1 = q[1] - p[1], d2 = q[2] - p[2];
@@ -77,43 +78,59 @@ __device__ void invert_mapping(double T, double* Ai /* 10x10 row-major */) {
             D[k][j] = row[j + HALF];
         }
     }
-    // D^-1 by LU with partial pivoting (Eigen's 5x5 inverse path)
+    // D^-1 by LU with partial pivoting (Eigen's 5x5 inverse path).  Every loop is fully
+    // unrolled and the row swap is a select, so all indices are static and the arrays
+    // stay in registers (a data-dependent row index would put them in scratch memory).
     int perm[HALF];
 #pragma unroll
     for (int i = 0; i < HALF; ++i) perm[i] = i;
+#pragma unroll
     for (int k = 0; k < HALF; ++k) {
         int p = k;
         double best = fabs(D[k][k]);
+#pragma unroll
         for (int r = k + 1; r < HALF; ++r)
             if (fabs(D[r][k]) > best) {
                 best = fabs(D[r][k]);
                 p = r;
             }
-        if (p != k) {
+#pragma unroll
+        for (int r = k + 1; r < HALF; ++r) {
+            const bool sw = (r == p);
+#pragma unroll
             for (int c = 0; c < HALF; ++c) {
                 const double t = D[k][c];
-                D[k][c] = D[p][c];
-                D[p][c] = t;
+                D[k][c] = sw ? D[r][c] : t;
+                D[r][c] = sw ? t : D[r][c];
             }
             const int t = perm[k];
-            perm[k] = perm[p];
-            perm[p] = t;
+            perm[k] = sw ? perm[r] : t;
+            perm[r] = sw ? t : perm[r];
         }
+#pragma unroll
         for (int r = k + 1; r < HALF; ++r) {
             D[r][k] = D[r][k] / D[k][k];
+#pragma unroll
             for (int c = k + 1; c < HALF; ++c) D[r][c] = D[r][c] - D[r][k] * D[k][c];
         }
     }
     double Dinv[HALF][HALF];
+#pragma unroll
     for (int col = 0; col < HALF; ++col) {
         double x[HALF];
+#pragma unroll
         for (int i = 0; i < HALF; ++i) x[i] = (perm[i] == col) ? 1.0 : 0.0;
+#pragma unroll
         for (int i = 0; i < HALF; ++i)
+#pragma unroll
             for (int j = 0; j < i; ++j) x[i] = x[i] - D[i][j] * x[j];
+#pragma unroll
         for (int i = HALF - 1; i >= 0; --i) {
+#pragma unroll
             for (int j = i + 1; j < HALF; ++j) x[i] = x[i] - D[i][j] * x[j];
             x[i] = x[i] / D[i][i];
         }
+#pragma unroll
         for (int i = 0; i < HALF; ++i) Dinv[i][col] = x[i];
     }
     for (int i = 0; i < N * N; ++i) Ai[i] = 0.0;
@@ -366,11 +383,13 @@ __global__ __launch_bounds__(kWave) void k_minsnap(const double* __restrict__ wp
     if (lane == 0 && status) status[track] = 0;
 }
 
+constexpr int kRowChunk = 512;  // samples per k_sample_rows round
+
 // Trajectory::evaluateRange control flow — src/trajectory.cpp:81-141.
 struct RangeIter {
     const double* T;
     int M, i;
-    double t_end, acc, tis;
+    double t_end, acc, tis, Ti;  // Ti = T[i], kept in a register (one LDS read per segment)
     __device__ void init(const double* T_, int M_) {
         T = T_;
         M = M_;
@@ -384,14 +403,16 @@ struct RangeIter {
         if (i >= M) i = M - 1;
         acc = acc - T[i];
         tis = 0.0 - acc;
+        Ti = T[i];
     }
     // Advances to the next sample; returns false when the loop ends.
     __device__ bool next(int& seg, double& t_in, double& t_acc) {
         while (acc < t_end) {
-            if (tis > T[i]) {
-                tis = tis - T[i];
+            if (tis > Ti) {
+                tis = tis - Ti;
                 i++;
                 if (i >= M) return false;
+                Ti = T[i];
                 continue;
             }
             seg = i;
@@ -454,8 +475,10 @@ __global__ __launch_bounds__(kWave) void k_sample_rows(const double* __restrict_
                                                        int n_tracks, double dt,
                                                        const double* __restrict__ t0,
                                                        const int64_t* __restrict__ row_off,
-                                                       double* __restrict__ rows) {
-    // one dynamic LDS array (Guideline 17): [T (M) | tin (64) | tac (64) | seg (64) | cnt, done]
+                                                       double* __restrict__ rows, int64_t cap_rows) {
+    // one dynamic LDS array (Guideline 17): [T (M) | tin | tac | seg (kRowChunk each) | cnt, done]
+    // lane 0 runs the sequential time recurrence for kRowChunk samples at a time, then the
+    // wave evaluates them (fewer barriers / coefficient-load round trips than 64 a round)
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int t = blockIdx.x;
     if (t >= n_tracks) return;
@@ -465,10 +488,10 @@ __global__ __launch_bounds__(kWave) void k_sample_rows(const double* __restrict_
     const int seg0 = wp_off[t] - t;
     double* sT = sm;
     double* s_tin = sT + ((M + 1) & ~1);
-    double* s_tac = s_tin + kWave;
-    int* s_seg = reinterpret_cast<int*>(s_tac + kWave);
-    int& s_cnt = s_seg[kWave];
-    int& s_done = s_seg[kWave + 1];
+    double* s_tac = s_tin + kRowChunk;
+    int* s_seg = reinterpret_cast<int*>(s_tac + kRowChunk);
+    int& s_cnt = s_seg[kRowChunk];
+    int& s_done = s_seg[kRowChunk + 1];
     for (int i = lane; i < M; i += kWave) sT[i] = seg_times[seg0 + i];
     const double toff = t0 ? t0[t] : 0.0;
     double* out = rows + (row_off ? row_off[t] : 0) * 10;
@@ -484,7 +507,7 @@ __global__ __launch_bounds__(kWave) void k_sample_rows(const double* __restrict_
             int c = 0;
             int seg;
             double tin, tac;
-            while (c < kWave) {
+            while (c < kRowChunk) {
                 if (!it.next(seg, tin, tac)) {
                     s_done = 1;
                     break;
@@ -499,13 +522,13 @@ __global__ __launch_bounds__(kWave) void k_sample_rows(const double* __restrict_
         }
         __syncthreads();
         const int cnt = s_cnt, done = s_done;
-        if (lane < cnt) {
-            const double* cs = coeffs + (size_t)(seg0 + s_seg[lane]) * 30;
-            const double tin = s_tin[lane];
-            double* row = out + (base + lane) * 10;
+        for (int j = lane; j < cnt && base + j < cap_rows; j += kWave) {  // (cap: single-track host path)
+            const double* cs = coeffs + (size_t)(seg0 + s_seg[j]) * 30;
+            const double tin = s_tin[j];
+            double* row = out + (base + j) * 10;
             for (int d = 0; d < 3; ++d)
                 for (int k = 0; k < 3; ++k) row[3 * d + k] = poly_eval(cs + d * N, tin, k);
-            row[9] = s_tac[lane] + toff;  // sampling_times[i] + startTimeOffset
+            row[9] = s_tac[j] + toff;  // sampling_times[i] + startTimeOffset
         }
         base += cnt;
         __syncthreads();
@@ -665,9 +688,9 @@ epp_status epp_sample_batch(const double* seg_times, const double* coeffs, const
     if (st) return st;
     int max_m = 0;
     if (max_segments(wp_offsets, n_tracks, (hipStream_t)stream, &max_m)) return EPP_ERR_HIP;
-    const size_t shm = ((size_t)((max_m + 1) & ~1) + 3 * kWave + 2) * 8;
+    const size_t shm = ((size_t)((max_m + 1) & ~1) + 3 * kRowChunk + 2) * 8;
     hipLaunchKernelGGL(k_sample_rows, dim3(n_tracks), dim3(kWave), shm, (hipStream_t)stream, seg_times,
-                       coeffs, wp_offsets, n_tracks, dt, t0, row_offsets, rows);
+                       coeffs, wp_offsets, n_tracks, dt, t0, row_offsets, rows, (int64_t)INT64_MAX);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         set_error(std::string("epp_sample_batch: ") + hipGetErrorString(e));
@@ -677,6 +700,11 @@ epp_status epp_sample_batch(const double* seg_times, const double* coeffs, const
 }
 
 // poly_traj::generateTrajectory with host buffers (src/trajectory_generator.cpp:12-100).
+// Latency path (one track, e.g. the 50 Hz refit): per-thread cached device / pinned
+// buffers and stream, one upload, the three kernels back to back (the host knows the
+// segment count, so no offset read-backs), one download.  The row buffer is sized from
+// the segment times recomputed on the host (+16 rows of slack; the kernel never writes
+// past it, and a short buffer is detected and redone).
 epp_status epp_generate_trajectory_host(const double* wp, int32_t n_wp, double v_max, double a_max,
                                         double dt, double t0, const double v0[3],
                                         const double a0[3], double** rows_out, int64_t* n_rows) {
@@ -690,73 +718,123 @@ epp_status epp_generate_trajectory_host(const double* wp, int32_t n_wp, double v
         set_error("At least two waypoints are required");  // trajectory_generator.cpp:24
         return EPP_ERR_INVALID_ARGUMENT;
     }
+    epp_status rc = ensure_consts();
+    if (rc) return rc;
     const int M = n_wp - 1;
-    // one device allocation: wp | v0 a0 | T | coeffs | t0 | offsets | counts/row_off | status
-    const size_t n_d = (size_t)n_wp * 3 + 6 + M + (size_t)M * 30 + 1;
-    char* d = nullptr;
-    const size_t bytes = n_d * 8 + 2 * 8 + 2 * 8 + 8 + 64;
-    if (hipMalloc(&d, bytes) != hipSuccess) {
-        set_error("generateTrajectory: hipMalloc failed");
-        return EPP_ERR_HIP;
-    }
-    double* d_wp = (double*)d;
-    double* d_va = d_wp + (size_t)n_wp * 3;
-    double* d_T = d_va + 6;
-    double* d_C = d_T + M;
-    double* d_t0 = d_C + (size_t)M * 30;
-    int32_t* d_off = (int32_t*)(d_t0 + 1);
-    int64_t* d_cnt = (int64_t*)(d_off + 2);
-    int64_t* d_roff = d_cnt + 1;
-    int32_t* d_status = (int32_t*)(d_roff + 1);
-    double va[6] = {v0 ? v0[0] : 0.0, v0 ? v0[1] : 0.0, v0 ? v0[2] : 0.0,
-                    a0 ? a0[0] : 0.0, a0 ? a0[1] : 0.0, a0 ? a0[2] : 0.0};
-    const int32_t off[2] = {0, n_wp};
-    const int64_t zero = 0;
-    epp_status rc = EPP_OK;
-    int32_t status = 0;
-    int64_t count = 0;
-    double* host_rows = nullptr;
-    double* d_rows = nullptr;
-    hipStream_t s = nullptr;
-    auto fail = [&](epp_status code, const char* msg) {
-        if (msg) set_error(msg);
-        rc = code;
+    double t_end = 0.0;  // host estimate of the duration (capacity only)
+    for (int i = 0; i < M; ++i) t_end += nfabian(wp + 3 * i, wp + 3 * (i + 1), v_max, a_max);
+    int64_t cap = (dt > 0 && std::isfinite(t_end)) ? (int64_t)(t_end / dt) + 16 : 16;
+    struct Cache {
+        char* d = nullptr;
+        size_t dcap = 0;
+        char* h = nullptr;
+        size_t hcap = 0;
+        hipStream_t s = nullptr;
     };
-    if (hipMemcpy(d_wp, wp, (size_t)n_wp * 24, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(d_va, va, 48, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(d_t0, &t0, 8, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(d_off, off, 8, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(d_roff, &zero, 8, hipMemcpyHostToDevice) != hipSuccess) {
-        fail(EPP_ERR_HIP, "generateTrajectory: upload failed");
-    }
-    if (!rc) rc = epp_minsnap_batch(d_wp, d_off, 1, v_max, a_max, d_va, d_va + 3, d_T, d_C, d_status, s);
-    if (!rc) rc = epp_sample_count(d_T, d_off, 1, dt, d_cnt, s);
-    if (!rc && (hipMemcpy(&status, d_status, 4, hipMemcpyDeviceToHost) != hipSuccess ||
-                hipMemcpy(&count, d_cnt, 8, hipMemcpyDeviceToHost) != hipSuccess))
-        fail(EPP_ERR_HIP, "generateTrajectory: download failed");
-    if (!rc && status != 0)
-        fail(EPP_ERR_RUNTIME, status == -2 ? "Segment times need to be greater than zero"
-                                           : "min-snap solve failed");
-    if (!rc && count > 0) {
-        if (hipMalloc(&d_rows, (size_t)count * 80) != hipSuccess) {
-            fail(EPP_ERR_HIP, "generateTrajectory: hipMalloc rows failed");
-        } else {
-            rc = epp_sample_batch(d_T, d_C, d_off, 1, dt, d_t0, d_roff, d_rows, s);
-            host_rows = (double*)std::malloc((size_t)count * 80);
-            if (!rc && (!host_rows ||
-                        hipMemcpy(host_rows, d_rows, (size_t)count * 80, hipMemcpyDeviceToHost) != hipSuccess))
-                fail(EPP_ERR_HIP, "generateTrajectory: download rows failed");
+    static thread_local Cache c;
+    auto a16 = [](size_t x) { return (x + 15) & ~size_t(15); };
+    const bool lds = M <= kMaxLdsSeg;
+    for (int pass = 0; pass < 2; ++pass) {
+        // device: [in: wp | va | t0 | off(2 i32) | goff | roff] [T | C | scratch] [rows (cap) | cnt | status]
+        const size_t in_b = a16((size_t)n_wp * 24 + 48 + 8 + 8 + 8 + 8);
+        const size_t mid_b = a16((size_t)M * 8) + a16((size_t)M * 240) + (lds ? 0 : a16((size_t)M * SegScratch::kSize * 8));
+        const size_t out_b = (size_t)cap * 80 + 16;
+        const size_t need = in_b + mid_b + out_b;
+        if (!c.s && hipStreamCreateWithFlags(&c.s, hipStreamNonBlocking) != hipSuccess) {
+            set_error("generateTrajectory: stream");
+            return EPP_ERR_HIP;
         }
+        if (need > c.dcap) {
+            if (c.d) (void)hipFree(c.d);
+            c.d = nullptr;
+            c.dcap = 0;
+            if (hipMalloc(&c.d, need) != hipSuccess) {
+                set_error("generateTrajectory: hipMalloc failed");
+                return EPP_ERR_HIP;
+            }
+            c.dcap = need;
+        }
+        const size_t hneed = std::max(in_b, out_b);
+        if (hneed > c.hcap) {
+            if (c.h) (void)hipHostFree(c.h);
+            c.h = nullptr;
+            c.hcap = 0;
+            if (hipHostMalloc(&c.h, hneed, 0) != hipSuccess) {
+                set_error("generateTrajectory: hipHostMalloc failed");
+                return EPP_ERR_HIP;
+            }
+            c.hcap = hneed;
+        }
+        // inputs, staged in pinned memory
+        double* h_wp = (double*)c.h;
+        std::memcpy(h_wp, wp, (size_t)n_wp * 24);
+        double* h_va = h_wp + (size_t)n_wp * 3;
+        for (int k = 0; k < 3; ++k) {
+            h_va[k] = v0 ? v0[k] : 0.0;
+            h_va[3 + k] = a0 ? a0[k] : 0.0;
+        }
+        h_va[6] = t0;
+        int32_t* h_off = (int32_t*)(h_va + 7);
+        h_off[0] = 0;
+        h_off[1] = n_wp;
+        int64_t* h_goff = (int64_t*)(h_off + 2);
+        h_goff[0] = 0;  // global scratch offset of the track
+        h_goff[1] = 0;  // row offset
+        double* d_wp = (double*)c.d;
+        double* d_va = d_wp + (size_t)n_wp * 3;
+        double* d_t0 = d_va + 6;
+        int32_t* d_off = (int32_t*)(d_va + 7);
+        int64_t* d_goff = (int64_t*)(d_off + 2);
+        int64_t* d_roff = d_goff + 1;
+        double* d_T = (double*)(c.d + in_b);
+        double* d_C = (double*)(c.d + in_b + a16((size_t)M * 8));
+        double* d_scr = (double*)(c.d + in_b + a16((size_t)M * 8) + a16((size_t)M * 240));
+        double* d_rows = (double*)(c.d + in_b + mid_b);
+        int64_t* d_cnt = (int64_t*)(d_rows + (size_t)cap * 10);
+        int32_t* d_status = (int32_t*)(d_cnt + 1);
+        hipStream_t s = c.s;
+        hipError_t e = hipMemcpyAsync(c.d, c.h, in_b, hipMemcpyHostToDevice, s);
+        const size_t vert_doubles = (size_t)(M + 1) * (15 + 12) + M;
+        if (lds) {
+            const size_t shm = ((size_t)M * SegScratch::kSize + vert_doubles + 2) * sizeof(double);
+            hipLaunchKernelGGL((k_minsnap<true>), dim3(1), dim3(kWave), shm, s, d_wp, d_off, 1, v_max, a_max, d_va,
+                               d_va + 3, d_T, d_C, d_status, nullptr, nullptr);
+        } else {
+            hipLaunchKernelGGL((k_minsnap<false>), dim3(1), dim3(kWave), (vert_doubles + 2) * sizeof(double), s,
+                               d_wp, d_off, 1, v_max, a_max, d_va, d_va + 3, d_T, d_C, d_status, d_scr, d_goff);
+        }
+        hipLaunchKernelGGL(k_sample_count, dim3(1), dim3(kWave), (size_t)(M + 2) * 8, s, d_T, d_off, 1, dt, d_cnt);
+        hipLaunchKernelGGL(k_sample_rows, dim3(1), dim3(kWave), ((size_t)((M + 1) & ~1) + 3 * kRowChunk + 2) * 8, s,
+                           d_T, d_C, d_off, 1, dt, d_t0, d_roff, d_rows, cap);
+        if (e == hipSuccess) e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemcpyAsync(c.h, d_rows, out_b, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) {
+            set_error(std::string("generateTrajectory: ") + hipGetErrorString(e));
+            return EPP_ERR_HIP;
+        }
+        const int64_t count = *(const int64_t*)(c.h + (size_t)cap * 80);
+        const int32_t status = *(const int32_t*)(c.h + (size_t)cap * 80 + 8);
+        if (status != 0) {
+            set_error(status == -2 ? "Segment times need to be greater than zero" : "min-snap solve failed");
+            return EPP_ERR_RUNTIME;
+        }
+        if (count > cap) {  // host estimate short: once more with the exact size
+            cap = count + 16;
+            continue;
+        }
+        double* host_rows = (double*)std::malloc((size_t)std::max<int64_t>(count, 1) * 80);
+        if (!host_rows) {
+            set_error("generateTrajectory: out of host memory");
+            return EPP_ERR_RUNTIME;
+        }
+        if (count > 0) std::memcpy(host_rows, c.h, (size_t)count * 80);
+        *rows_out = host_rows;
+        *n_rows = count;
+        return EPP_OK;
     }
-    if (d_rows) (void)hipFree(d_rows);
-    (void)hipFree(d);
-    if (rc) {
-        std::free(host_rows);
-        return rc;
-    }
-    *rows_out = host_rows;
-    *n_rows = count;
-    return EPP_OK;
+    set_error("generateTrajectory: row count");
+    return EPP_ERR_RUNTIME;
 }
 
 }  // extern "C"

@@ -88,6 +88,25 @@ def test_generate_trajectory_vs_oracle(seed):
     np.testing.assert_allclose(got[0, [2, 5, 8]], a0, atol=1e-9)
 
 
+@pytest.mark.parametrize("n,dt", [(40, 0.1), (26, 0.01), (9, 0.003)])
+def test_generate_trajectory_long_tracks(n, dt):
+    """The single-track latency path: more than 24 segments (global scratch), many rows
+    (row buffer sized from host-side segment times)."""
+    wp = synth.random_track_waypoints(900 + n, n)
+    got = capi.generate_trajectory(wp, 1.5, 2.5, dt, 0.5)
+    exp = O.generate_trajectory(wp, 1.5, 2.5, dt, 0.5)
+    assert got.shape == exp.shape
+    assert np.array_equal(got[:, 9], exp[:, 9])
+    assert np.abs(got[:, :9] - exp[:, :9]).max() < 1e-6
+
+
+def test_generate_trajectory_zero_segment():
+    wp = np.array([[0.0, 0.0, 0.5], [1.0, 2.0, 1.5], [1.0, 2.0, 1.5], [2.0, 0.0, 1.0]])
+    with pytest.raises(capi.EppError) as e:
+        capi.generate_trajectory(wp, 1.0, 2.0, 0.1)
+    assert "Segment times need to be greater than zero" in str(e.value)
+
+
 def test_generate_trajectory_two_waypoints_and_errors():
     wp = np.array([[0.0, 0.0, 0.5], [1.0, 2.0, 1.5]])
     got = capi.generate_trajectory(wp, 1.0, 2.0, 0.05)
