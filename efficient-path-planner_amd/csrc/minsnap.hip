@@ -147,40 +147,54 @@ __device__ void invert_mapping(double T, double* Ai /* 10x10 row-major */) {
         }
 }
 
-// 4x4 Cholesky of a symmetric block (lower factor in place).  Returns false if not SPD.
-__device__ bool chol4(double* L) {
+// 4x4 Cholesky (lower factor in place; false if not SPD) and the two triangular solves
+// with MC right-hand sides (b: 4 x MC, row-major), on register arrays: fully unrolled so
+// the indices are static.  The serial block solve runs on one lane, where every LDS round
+// trip in a dependent chain would be exposed latency.
+__device__ __forceinline__ bool chol4r(double (&L)[16]) {
+    bool ok = true;
+#pragma unroll
     for (int j = 0; j < 4; ++j) {
         double d = L[j * 4 + j];
+#pragma unroll
         for (int k = 0; k < j; ++k) d = d - L[j * 4 + k] * L[j * 4 + k];
-        if (!(d > 0.0)) return false;
+        ok = ok && (d > 0.0);
         d = sqrt(d);
         L[j * 4 + j] = d;
+#pragma unroll
         for (int i = j + 1; i < 4; ++i) {
             double s = L[i * 4 + j];
+#pragma unroll
             for (int k = 0; k < j; ++k) s = s - L[i * 4 + k] * L[j * 4 + k];
             L[i * 4 + j] = s / d;
         }
+#pragma unroll
         for (int i = 0; i < j; ++i) L[i * 4 + j] = 0.0;
     }
-    return true;
+    return ok;
 }
-
-// solve L x = b in place (b: 4 x m, row-major with stride m)
-__device__ void lsolve4(const double* L, double* b, int m) {
-    for (int c = 0; c < m; ++c)
+template <int MC>
+__device__ __forceinline__ void lsolve4r(const double (&L)[16], double (&b)[4 * MC]) {
+#pragma unroll
+    for (int c = 0; c < MC; ++c)
+#pragma unroll
         for (int i = 0; i < 4; ++i) {
-            double s = b[i * m + c];
-            for (int k = 0; k < i; ++k) s = s - L[i * 4 + k] * b[k * m + c];
-            b[i * m + c] = s / L[i * 4 + i];
+            double s = b[i * MC + c];
+#pragma unroll
+            for (int k = 0; k < i; ++k) s = s - L[i * 4 + k] * b[k * MC + c];
+            b[i * MC + c] = s / L[i * 4 + i];
         }
 }
-// solve L^T x = b in place
-__device__ void ltsolve4(const double* L, double* b, int m) {
-    for (int c = 0; c < m; ++c)
+template <int MC>
+__device__ __forceinline__ void ltsolve4r(const double (&L)[16], double (&b)[4 * MC]) {
+#pragma unroll
+    for (int c = 0; c < MC; ++c)
+#pragma unroll
         for (int i = 3; i >= 0; --i) {
-            double s = b[i * m + c];
-            for (int k = i + 1; k < 4; ++k) s = s - L[k * 4 + i] * b[k * m + c];
-            b[i * m + c] = s / L[i * 4 + i];
+            double s = b[i * MC + c];
+#pragma unroll
+            for (int k = i + 1; k < 4; ++k) s = s - L[k * 4 + i] * b[k * MC + c];
+            b[i * MC + c] = s / L[i * 4 + i];
         }
 }
 
@@ -317,47 +331,92 @@ __global__ __launch_bounds__(kWave) void k_minsnap(const double* __restrict__ wp
     __syncthreads();
     // ---- phase 4: block Cholesky solve (one lane; 4x4 blocks, 3 right-hand sides) ---
     if (lane == 0 && nin > 0) {
+        // the carried blocks (W_{v-1}, z_{v-1}; x_{v+1} on the way back) stay in registers
         bool ok = true;
-        for (int v = 1; v <= nin && ok; ++v) {
-            double* L = scr + (size_t)(v - 1) * SegScratch::kSize + SegScratch::kL;
+        double Wp[16], zp[12];
+        for (int v = 1; v <= nin; ++v) {
+            double* Ls = scr + (size_t)(v - 1) * SegScratch::kSize + SegScratch::kL;
+            double L[16], b[12];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) L[i] = Ls[i];
+#pragma unroll
+            for (int i = 0; i < 12; ++i) b[i] = rhs[(size_t)v * 12 + i];
             if (v > 1) {  // S_v = D_v - W_{v-1}^T W_{v-1},  W_{v-1} = L_{v-1}^-1 E_{v-1}
-                const double* Wp = scr + (size_t)(v - 2) * SegScratch::kSize + SegScratch::kW;
+#pragma unroll
                 for (int p = 0; p < 4; ++p)
+#pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         double s = 0.0;
+#pragma unroll
                         for (int k = 0; k < 4; ++k) s = s + Wp[k * 4 + p] * Wp[k * 4 + q];
                         L[p * 4 + q] = L[p * 4 + q] - s;
                     }
                 // z_v = b_v - W_{v-1}^T z_{v-1}
-                double* bp = rhs + (size_t)(v - 1) * 12;
-                double* b = rhs + (size_t)v * 12;
+#pragma unroll
                 for (int p = 0; p < 4; ++p)
+#pragma unroll
                     for (int d = 0; d < 3; ++d) {
                         double s = 0.0;
-                        for (int k = 0; k < 4; ++k) s = s + Wp[k * 4 + p] * bp[k * 3 + d];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) s = s + Wp[k * 4 + p] * zp[k * 3 + d];
                         b[p * 3 + d] = b[p * 3 + d] - s;
                     }
             }
-            ok = chol4(L);
+            ok = chol4r(L);
             if (!ok) break;
-            lsolve4(L, rhs + (size_t)v * 12, 3);
-            if (v < nin) lsolve4(L, scr + (size_t)(v - 1) * SegScratch::kSize + SegScratch::kW, 4);
+            lsolve4r<3>(L, b);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) Ls[i] = L[i];
+#pragma unroll
+            for (int i = 0; i < 12; ++i) {
+                rhs[(size_t)v * 12 + i] = b[i];
+                zp[i] = b[i];
+            }
+            if (v < nin) {
+                double* Ws = scr + (size_t)(v - 1) * SegScratch::kSize + SegScratch::kW;
+                double W[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) W[i] = Ws[i];
+                lsolve4r<4>(L, W);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    Ws[i] = W[i];
+                    Wp[i] = W[i];
+                }
+            }
         }
         if (ok) {
+            double xn[12];
             for (int v = nin; v >= 1; --v) {
-                double* x = rhs + (size_t)v * 12;
+                double x[12], L[16];
+#pragma unroll
+                for (int i = 0; i < 12; ++i) x[i] = rhs[(size_t)v * 12 + i];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) L[i] = scr[(size_t)(v - 1) * SegScratch::kSize + SegScratch::kL + i];
                 if (v < nin) {  // z_v - W_v x_{v+1}
                     const double* Wv = scr + (size_t)(v - 1) * SegScratch::kSize + SegScratch::kW;
-                    const double* xn = rhs + (size_t)(v + 1) * 12;
+                    double W[16];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) W[i] = Wv[i];
+#pragma unroll
                     for (int p = 0; p < 4; ++p)
+#pragma unroll
                         for (int d = 0; d < 3; ++d) {
                             double s = 0.0;
-                            for (int k = 0; k < 4; ++k) s = s + Wv[p * 4 + k] * xn[k * 3 + d];
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) s = s + W[p * 4 + k] * xn[k * 3 + d];
                             x[p * 3 + d] = x[p * 3 + d] - s;
                         }
                 }
-                ltsolve4(scr + (size_t)(v - 1) * SegScratch::kSize + SegScratch::kL, x, 3);
+                ltsolve4r<3>(L, x);
+#pragma unroll
+                for (int i = 0; i < 12; ++i) {
+                    rhs[(size_t)v * 12 + i] = x[i];
+                    xn[i] = x[i];
+                }
+#pragma unroll
                 for (int p = 0; p < 4; ++p)
+#pragma unroll
                     for (int d = 0; d < 3; ++d) dv[(v * HALF + 1 + p) * 3 + d] = x[p * 3 + d];
             }
         } else {
@@ -426,6 +485,24 @@ struct RangeIter {
         tis = tis + dt;
         acc = acc + dt;
     }
+    // The next 8 samples at once when none of them rolls over into the next segment or
+    // reaches the end (the same additions, in the same order, as 8 next/advance steps;
+    // acc and tis only grow, so checking the 8th sample covers all).  False: nothing
+    // consumed, take single steps.
+    __device__ bool fast8(double dt, double (&tin)[8], double (&tac)[8]) {
+        double t = tis, a = acc;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            tin[k] = t;
+            tac[k] = a;
+            t = t + dt;
+            a = a + dt;
+        }
+        if (!(tac[7] < t_end) || tin[7] > Ti) return false;
+        tis = t;
+        acc = a;
+        return true;
+    }
 };
 
 // One wavefront per track: the lanes stage the segment times in LDS, lane 0 runs the
@@ -450,8 +527,13 @@ __global__ __launch_bounds__(kWave) void k_sample_count(const double* __restrict
         it.init(sT, M);
         int64_t n = 0;
         int seg;
-        double tin, tac;
-        while (it.next(seg, tin, tac)) {
+        double tin, tac, tin8[8], tac8[8];
+        for (;;) {
+            if (it.fast8(dt, tin8, tac8)) {
+                n += 8;
+                continue;
+            }
+            if (!it.next(seg, tin, tac)) break;
             ++n;
             it.advance(dt);
         }
@@ -506,8 +588,18 @@ __global__ __launch_bounds__(kWave) void k_sample_rows(const double* __restrict_
         if (lane == 0) {
             int c = 0;
             int seg;
-            double tin, tac;
+            double tin, tac, tin8[8], tac8[8];
             while (c < kRowChunk) {
+                if (c + 8 <= kRowChunk && it.fast8(dt, tin8, tac8)) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        s_seg[c + k] = it.i;
+                        s_tin[c + k] = tin8[k];
+                        s_tac[c + k] = tac8[k];
+                    }
+                    c += 8;
+                    continue;
+                }
                 if (!it.next(seg, tin, tac)) {
                     s_done = 1;
                     break;
