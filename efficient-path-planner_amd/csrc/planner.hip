@@ -118,7 +118,7 @@ struct KnnGrid {
 
 constexpr int kBoundsThreads = 1024;
 constexpr int kBoundsBlocks = 64;
-constexpr double kNodesPerCell = 2.0;  // mean nodes per grid cell (EPP_KNN_NPC overrides; tuning)
+constexpr double kNodesPerCell = 1.5;  // mean nodes per grid cell (EPP_KNN_NPC overrides; tuned for k_knn_tile: ~90 queries per 4^3 block -> 2 lanes each)
 
 // Per-block min/max of the node coordinates: part[6 * block] = (min xyz, max xyz).
 __global__ __launch_bounds__(kBoundsThreads) void k_knn_bounds_part(const double* __restrict__ nodes, int n,
@@ -466,6 +466,44 @@ __device__ __forceinline__ void tile_rows(const int* cst, const float4* cand, in
     }
 }
 
+// tile_rows restricted to the cells that can hold a candidate with squared distance
+// <= thr: a row is skipped when its (y, z) gap alone exceeds thr, else trimmed to the x
+// cells within reach (still one contiguous LDS range).  fr = the query's offset inside its
+// own cell per axis; gaps are shrunk by a hair, so the culling only ever keeps too much.
+__device__ __forceinline__ double tile_gap(int off, double fr, double h) {
+    const double g = off < 0 ? fr + (double)(-off - 1) * h : (off > 0 ? (h - fr) + (double)(off - 1) * h : 0.0);
+    return fmax(g - 1e-6 * h, 0.0);
+}
+
+template <class F>
+__device__ __forceinline__ void tile_rows_near(const int* cst, const float4* cand, int h0, int row0, int rstep,
+                                               const float4& pf, const double (&fr)[3], double h, double thr, F&& f) {
+    const double gx1 = tile_gap(1, fr[0], h), gx2 = tile_gap(2, fr[0], h);
+    const double gxm1 = tile_gap(-1, fr[0], h), gxm2 = tile_gap(-2, fr[0], h);
+    for (int row = row0; row < kTileRows; row += rstep) {
+        const int rz = row / kTileW, ry = row % kTileW;
+        const double gy = tile_gap(ry - kTileH, fr[1], h), gz = tile_gap(rz - kTileH, fr[2], h);
+        const double gyz = gy * gy + gz * gz;
+        if (gyz > thr) continue;
+        const double rem = thr - gyz;
+        const int xa = gxm2 * gxm2 <= rem ? 0 : (gxm1 * gxm1 <= rem ? 1 : 2);
+        const int xb = gx2 * gx2 <= rem ? 4 : (gx1 * gx1 <= rem ? 3 : 2);
+        const int a = h0 + (rz * kTileE + ry) * kTileE;
+        const int q1 = cst[a + xb + 1];
+        for (int q = cst[a + xa]; q < q1; q += 4) {
+            float4 c[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) c[u] = cand[min(q + u, q1 - 1)];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float dx = c[u].x - pf.x, dy = c[u].y - pf.y, dz = c[u].z - pf.z;
+                f(min(q + u, q1 - 1), (dx * dx + dy * dy) + dz * dz, __float_as_int(c[u].w), q + u < q1);
+            }
+        }
+    }
+}
+static_assert(kTileW == 5 && kTileH == 2, "tile_rows_near trims rows of 5 cells");
+
 template <int K>
 __device__ __forceinline__ void knn_store(int32_t* __restrict__ nbr, int self, const int (&bi)[K]) {
 #pragma unroll
@@ -703,14 +741,20 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                 // Dcut: upper edge of bin `cut` (none reached K: no bound)
                 const double dcut = cut < 0 ? INFINITY : (double)__uint_as_float((uint32_t)(cut + 1 + (127 << 2)) << 21) * t0;
                 const float dlist = (float)(dcut + 2.0 * delta);
-                // pass 2: list the candidates below Dcut + 2 delta
-                if (live)
-                    tile_rows(cst, cand, h0, sub, lpq, pf, [&](int q, float d, int j, bool valid) {
+                // pass 2: list the candidates below Dcut + 2 delta, visiting only the cells
+                // within Dcut + 3 delta (a candidate's float distance is within delta of
+                // its exact one, which is at least its cell's distance)
+                if (live) {
+                    const double fr[3] = {p[0] - (g.lo[0] + (double)c[0] * g.h), p[1] - (g.lo[1] + (double)c[1] * g.h),
+                                          p[2] - (g.lo[2] + (double)c[2] * g.h)};
+                    const double thr2 = cut < 0 ? INFINITY : dcut + 3.0 * delta;
+                    tile_rows_near(cst, cand, h0, sub, lpq, pf, fr, g.h, thr2, [&](int q, float d, int j, bool valid) {
                         if (valid && j != self && d < dlist) {
                             const int at = atomicAdd(&nls[slot], 1);
                             if (at < kTileL) lst[at][slot] = (uint16_t)q;
                         }
                     });
+                }
                 __syncthreads();
                 if (!live || sub != 0) continue;
                 const int nl = nls[slot];
