@@ -1375,7 +1375,7 @@ __global__ __launch_bounds__(kBlock) void k_motions(WorldView w, const double* _
 // candidate costs one LDS round trip instead of the short-circuit chain of dependent
 // global loads of k_motions.  Same candidate order, de-duplication (first common cell)
 // and predicates as ray_valid / ray_valid_d32 (src/World.cpp:130-162, src/OBB.cpp:10-91).
-constexpr int kBlockM = 512;
+constexpr int kBlockM = 512;  // default k_motions_v2 block (EPP_MOTIONS_BLOCK=512)
 
 // OBB::checkCollisionWithRay (src/OBB.cpp:10-61) on one AoS record, branch-free.  `r` is
 // the owner's inflation radius; the endpoint tests inflate only collision OBBs (:13-14),
@@ -1432,8 +1432,8 @@ __device__ __forceinline__ bool rec_ray_hit(const double* rec, const double s[3]
     return end_hit | slab_hit;
 }
 
-template <int MODE>
-__global__ __launch_bounds__(kBlockM) void k_motions_v2(const WorldView* __restrict__ wv, const double* __restrict__ s1,
+template <int MODE, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_motions_v2(const WorldView* __restrict__ wv, const double* __restrict__ s1,
                                                         const double* __restrict__ s2, int64_t n, int can_pass,
                                                         uint8_t* __restrict__ valid, uint32_t front_bytes,
                                                         uint32_t rec_bytes) {
@@ -1444,9 +1444,9 @@ __global__ __launch_bounds__(kBlockM) void k_motions_v2(const WorldView* __restr
         const uint4* src0 = reinterpret_cast<const uint4*>(wv->blob);
         const uint4* src1 = reinterpret_cast<const uint4*>(wv->blob + wv->off_aos);
         uint4* dst = reinterpret_cast<uint4*>(lds);
-        for (uint32_t o = threadIdx.x; o < front_bytes / 16; o += kBlockM) dst[o] = src0[o];
+        for (uint32_t o = threadIdx.x; o < front_bytes / 16; o += BLOCK) dst[o] = src0[o];
         uint4* dst1 = reinterpret_cast<uint4*>(lds + front_bytes);
-        for (uint32_t o = threadIdx.x; o < rec_bytes / 16; o += kBlockM) dst1[o] = src1[o];
+        for (uint32_t o = threadIdx.x; o < rec_bytes / 16; o += BLOCK) dst1[o] = src1[o];
     }
     const unsigned long long* mask = reinterpret_cast<const unsigned long long*>(lds + wv->off_cell_mask);
     const uint32_t* cs = reinterpret_cast<const uint32_t*>(lds + wv->off_cell_start);
@@ -1459,8 +1459,8 @@ __global__ __launch_bounds__(kBlockM) void k_motions_v2(const WorldView* __restr
     const float fmx = wv->fmaxx, fmy = wv->fmaxy, fmz = wv->fmaxz;
     const double rg = wv->r_gate, ro = wv->r_obst;
     __syncthreads();
-    const int64_t stride = (int64_t)gridDim.x * kBlockM;
-    for (int64_t i = (int64_t)blockIdx.x * kBlockM + threadIdx.x; i < n; i += stride) {
+    const int64_t stride = (int64_t)gridDim.x * BLOCK;
+    for (int64_t i = (int64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
         const double s[3] = {s1[3 * i], s1[3 * i + 1], s1[3 * i + 2]};
         const double e[3] = {s2[3 * i], s2[3 * i + 1], s2[3 * i + 2]};
         bool ok = true;
@@ -1527,6 +1527,247 @@ __global__ __launch_bounds__(kBlockM) void k_motions_v2(const WorldView* __restr
             }
         }
         valid[i] = ok ? 1 : 0;
+    }
+}
+
+// ---- k_motions_v3: analytic motion checks with a per-wave candidate queue ------------
+// k_motions_v2's analytic mode pays the divergent per-lane walk AND, whenever any lane of
+// the wave reaches a surviving candidate, the ~200-instruction slab test with most lanes
+// idle (C3: ~0.9 candidates per edge on average, ~5 for the wave's worst lane).  Here the
+// walk only filters (first common cell, closed AABB overlap, filling skip — the rtree
+// prefilter of src/World.cpp:143-153) and pushes (lane, OBB) pairs into the wave's LDS
+// queue; the wave then runs the exact test over the queue 64 pairs at a time with every
+// lane busy, the pair's edge fetched from its owner lane by ds_bpermute.  Any hit clears
+// the owner's flag.  An edge is invalid iff some candidate hits, so testing every
+// candidate (no early exit) gives the reference's answer.  A full queue makes the
+// pushing lane test inline (same predicate).
+constexpr int kQueueM = 256;  // queued pairs per wave
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_motions_v3(const WorldView* __restrict__ wv, const double* __restrict__ s1,
+                                                      const double* __restrict__ s2, int64_t n, int can_pass,
+                                                      uint8_t* __restrict__ valid, uint32_t front_bytes,
+                                                      uint32_t rec_bytes) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    {
+        const uint4* src0 = reinterpret_cast<const uint4*>(wv->blob);
+        const uint4* src1 = reinterpret_cast<const uint4*>(wv->blob + wv->off_aos);
+        uint4* dst = reinterpret_cast<uint4*>(lds);
+        for (uint32_t o = threadIdx.x; o < front_bytes / 16; o += BLOCK) dst[o] = src0[o];
+        uint4* dst1 = reinterpret_cast<uint4*>(lds + front_bytes);
+        for (uint32_t o = threadIdx.x; o < rec_bytes / 16; o += BLOCK) dst1[o] = src1[o];
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t* queue = reinterpret_cast<uint32_t*>(lds + front_bytes + rec_bytes) + wave * (kQueueM + 1);
+    uint32_t* qcount = queue + kQueueM;
+    uint8_t* flags = lds + front_bytes + rec_bytes + (BLOCK / 64) * (kQueueM + 1) * 4 + wave * 64;
+    const uint32_t* cs = reinterpret_cast<const uint32_t*>(lds + wv->off_cell_start);
+    const uint16_t* co = reinterpret_cast<const uint16_t*>(lds + wv->off_cell_obb);
+    const double* recs = reinterpret_cast<const double*>(lds + front_bytes);
+    const int nx = wv->nx, ny = wv->ny, nz = wv->nz;
+    const double gx0 = wv->gx0, gy0 = wv->gy0, gz0 = wv->gz0, gx1 = wv->gx1, gy1 = wv->gy1, gz1 = wv->gz1;
+    const float ofx = wv->ofx, ofy = wv->ofy, ofz = wv->ofz, i4x = wv->i4x, i4y = wv->i4y, i4z = wv->i4z;
+    const double rg = wv->r_gate, ro = wv->r_obst;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * BLOCK;
+    // wave-uniform loop: every lane of the wave runs every iteration (ds_bpermute below)
+    for (int64_t i0 = (int64_t)blockIdx.x * BLOCK + wave * 64; i0 < n; i0 += stride) {
+        const int64_t i = i0 + lane;
+        const bool act = i < n;
+        double s[3] = {0.0, 0.0, 0.0}, e[3] = {0.0, 0.0, 0.0};
+        if (act) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                s[k] = s1[3 * i + k];
+                e[k] = s2[3 * i + k];
+            }
+        }
+        if (lane == 0) *qcount = 0u;
+        flags[lane] = 1;
+        wave_lds_sync();
+        bool ok = true;
+        double lo[3], hi[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = (e[k] < s[k]) ? e[k] : s[k];
+            hi[k] = (s[k] < e[k]) ? e[k] : s[k];
+        }
+        // World::checkRayValid — rtree intersects(rayBox): closed AABB overlap
+        if (act && !(hi[0] < gx0 || gx1 < lo[0] || hi[1] < gy0 || gy1 < lo[1] || hi[2] < gz0 || gz1 < lo[2])) {
+            const int x0 = fine_index(fine_coord(lo[0], ofx, i4x), nx) >> 2;
+            const int x1 = fine_index(fine_coord(hi[0], ofx, i4x), nx) >> 2;
+            const int y0 = fine_index(fine_coord(lo[1], ofy, i4y), ny) >> 2;
+            const int y1 = fine_index(fine_coord(hi[1], ofy, i4y), ny) >> 2;
+            const int z0 = fine_index(fine_coord(lo[2], ofz, i4z), nz) >> 2;
+            const int z1 = fine_index(fine_coord(hi[2], ofz, i4z), nz) >> 2;
+            for (int z = z0; z <= z1; ++z)
+                for (int y = y0; y <= y1; ++y)
+                    for (int x = x0; x <= x1; ++x) {
+                        const int cell = (z * ny + y) * nx + x;
+                        const uint32_t b = cs[cell], en = cs[cell + 1];
+                        for (uint32_t k = b; k < en; ++k) {
+                            const uint32_t id = co[k];
+                            const double* rec = recs + (size_t)id * kRecDoubles;
+                            const uint32_t m = (uint32_t)__double_as_longlong(rec[R_META]);
+                            const int ox = (m >> 8) & 255, oy = (m >> 16) & 255, oz = m >> 24;
+                            const bool first = (x == (ox > x0 ? ox : x0)) & (y == (oy > y0 ? oy : y0)) &
+                                               (z == (oz > z0 ? oz : z0));
+                            const bool overlap = !((rec[F_HIX] < lo[0]) | (hi[0] < rec[F_LOX]) | (rec[F_HIY] < lo[1]) |
+                                                   (hi[1] < rec[F_LOY]) | (rec[F_HIZ] < lo[2]) | (hi[2] < rec[F_LOZ]));
+                            const bool skip = (m & META_FILLING) && can_pass;  // :150-153
+                            if (first & overlap & !skip) {
+                                const uint32_t slot = atomicAdd(qcount, 1u);
+                                if (slot < (uint32_t)kQueueM)
+                                    queue[slot] = (id << 6) | (uint32_t)lane;
+                                else if (rec_ray_hit(rec, s, e, (m & META_GATE) ? rg : ro))
+                                    ok = false;
+                            }
+                        }
+                    }
+        }
+        wave_lds_sync();
+        const uint32_t total = min(*qcount, (uint32_t)kQueueM);
+        for (uint32_t base = 0; base < total; base += 64) {
+            const uint32_t j = base + lane;
+            const bool has = j < total;
+            const uint32_t q = has ? queue[j] : 0u;
+            const int owner = (int)(q & 63u);
+            double ps[3], pe[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                ps[k] = __shfl(s[k], owner);
+                pe[k] = __shfl(e[k], owner);
+            }
+            if (has) {
+                const double* rec = recs + (size_t)(q >> 6) * kRecDoubles;
+                const uint32_t m = (uint32_t)__double_as_longlong(rec[R_META]);
+                if (rec_ray_hit(rec, ps, pe, (m & META_GATE) ? rg : ro)) flags[owner] = 0;
+            }
+        }
+        wave_lds_sync();
+        if (act) valid[i] = (ok && flags[lane]) ? 1 : 0;
+        wave_lds_sync();  // flags / count are reset by the next iteration
+    }
+}
+
+// ---- k_motions_d32q: discrete32 motion checks with a per-wave candidate queue ---------
+// The 32 points s + (e - s)·k/32 (k = 1..32) are stepped wave-uniformly.  At each k a
+// lane whose point lies in an occupied fine cell walks its coarse cell's list and pushes
+// the OBBs whose AABB strictly contains the point (the rtree `contains` of
+// src/World.cpp:83) as (lane, k, OBB) triples; when the queue holds kFlushD32 or more
+// (and after k = 32) the wave runs OBB::checkCollisionWithPoint (src/OBB.cpp:63-91, via
+// rec_hit) on 64 triples at a time, the point recomputed from the owner's endpoints with
+// the same arithmetic as k_motions_v2.  Lanes already invalid stop pushing.  A push past
+// the queue's end is tested inline.
+constexpr int kQueueD32 = 512;
+constexpr uint32_t kFlushD32 = 256;
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_motions_d32q(const WorldView* __restrict__ wv,
+                                                        const double* __restrict__ s1, const double* __restrict__ s2,
+                                                        int64_t n, int can_pass, uint8_t* __restrict__ valid,
+                                                        uint32_t front_bytes, uint32_t rec_bytes) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    {
+        const uint4* src0 = reinterpret_cast<const uint4*>(wv->blob);
+        const uint4* src1 = reinterpret_cast<const uint4*>(wv->blob + wv->off_aos);
+        uint4* dst = reinterpret_cast<uint4*>(lds);
+        for (uint32_t o = threadIdx.x; o < front_bytes / 16; o += BLOCK) dst[o] = src0[o];
+        uint4* dst1 = reinterpret_cast<uint4*>(lds + front_bytes);
+        for (uint32_t o = threadIdx.x; o < rec_bytes / 16; o += BLOCK) dst1[o] = src1[o];
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t* queue = reinterpret_cast<uint32_t*>(lds + front_bytes + rec_bytes) + wave * (kQueueD32 + 1);
+    uint32_t* qcount = queue + kQueueD32;
+    uint8_t* flags = lds + front_bytes + rec_bytes + (BLOCK / 64) * (kQueueD32 + 1) * 4 + wave * 64;
+    const unsigned long long* mask = reinterpret_cast<const unsigned long long*>(lds + wv->off_cell_mask);
+    const uint32_t* cs = reinterpret_cast<const uint32_t*>(lds + wv->off_cell_start);
+    const uint16_t* co = reinterpret_cast<const uint16_t*>(lds + wv->off_cell_obb);
+    const double* recs = reinterpret_cast<const double*>(lds + front_bytes);
+    const int nx = wv->nx, ny = wv->ny;
+    const float ofx = wv->ofx, ofy = wv->ofy, ofz = wv->ofz, i4x = wv->i4x, i4y = wv->i4y, i4z = wv->i4z;
+    const float limx = wv->limx, limy = wv->limy, limz = wv->limz;
+    const float fmx = wv->fmaxx, fmy = wv->fmaxy, fmz = wv->fmaxz;
+    const double rg = wv->r_gate, ro = wv->r_obst;
+    const bool cp = can_pass != 0;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * BLOCK;
+    for (int64_t i0 = (int64_t)blockIdx.x * BLOCK + wave * 64; i0 < n; i0 += stride) {
+        const int64_t i = i0 + lane;
+        const bool act = i < n;
+        double s[3] = {0.0, 0.0, 0.0}, e[3] = {0.0, 0.0, 0.0};
+        if (act) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                s[k] = s1[3 * i + k];
+                e[k] = s2[3 * i + k];
+            }
+        }
+        if (lane == 0) *qcount = 0u;
+        flags[lane] = act ? 1 : 0;
+        wave_lds_sync();
+        bool ok = true;
+        for (int k = 1; k <= 32; ++k) {
+            const double t = (double)k / 32.0;
+            const double px = s[0] + (e[0] - s[0]) * t;
+            const double py = s[1] + (e[1] - s[1]) * t;
+            const double pz = s[2] + (e[2] - s[2]) * t;
+            const float fx = fine_coord(px, ofx, i4x), fy = fine_coord(py, ofy, i4y), fz = fine_coord(pz, ofz, i4z);
+            const bool in = (fx >= 0.0f) & (fx <= limx) & (fy >= 0.0f) & (fy <= limy) & (fz >= 0.0f) & (fz <= limz);
+            const int ix = (int)fminf(fmaxf(fx, 0.0f), fmx);
+            const int iy = (int)fminf(fmaxf(fy, 0.0f), fmy);
+            const int iz = (int)fminf(fmaxf(fz, 0.0f), fmz);
+            const int cell = ((iz >> 2) * ny + (iy >> 2)) * nx + (ix >> 2);
+            const uint32_t bit = (uint32_t)((((iz & 3) << 2) + (iy & 3)) * 4 + (ix & 3));
+            const bool live = ok && flags[lane];
+            if (live && in && ((mask[cell] >> bit) & 1ull)) {
+                const uint32_t b = cs[cell], en = cs[cell + 1];
+                for (uint32_t q = b; q < en; ++q) {
+                    const uint32_t id = co[q];
+                    const double* rec = recs + (size_t)id * kRecDoubles;
+                    // rtree contains(point): strict  src/World.cpp:83 (rec_hit re-tests it)
+                    const bool inside = (rec[F_LOX] < px) & (px < rec[F_HIX]) & (rec[F_LOY] < py) &
+                                        (py < rec[F_HIY]) & (rec[F_LOZ] < pz) & (pz < rec[F_HIZ]);
+                    if (inside) {
+                        const uint32_t slot = atomicAdd(qcount, 1u);
+                        if (slot < (uint32_t)kQueueD32)
+                            queue[slot] = (id << 11) | ((uint32_t)(k - 1) << 6) | (uint32_t)lane;
+                        else if (rec_hit<false>(rec, rg, ro, px, py, pz, cp, 0.0))
+                            ok = false;
+                    }
+                }
+            }
+            wave_lds_sync();
+            const uint32_t cnt = *qcount;  // wave-uniform
+            if (cnt >= kFlushD32 || k == 32) {
+                const uint32_t total = min(cnt, (uint32_t)kQueueD32);
+                for (uint32_t base = 0; base < total; base += 64) {
+                    const uint32_t j = base + lane;
+                    const bool has = j < total;
+                    const uint32_t qe = has ? queue[j] : 0u;
+                    const int owner = (int)(qe & 63u);
+                    double ps[3], pe[3];
+#pragma unroll
+                    for (int d = 0; d < 3; ++d) {
+                        ps[d] = __shfl(s[d], owner);
+                        pe[d] = __shfl(e[d], owner);
+                    }
+                    if (has) {
+                        const double tq = (double)(((qe >> 6) & 31u) + 1u) / 32.0;
+                        const double qx = ps[0] + (pe[0] - ps[0]) * tq;
+                        const double qy = ps[1] + (pe[1] - ps[1]) * tq;
+                        const double qz = ps[2] + (pe[2] - ps[2]) * tq;
+                        if (rec_hit<false>(recs + (size_t)(qe >> 11) * kRecDoubles, rg, ro, qx, qy, qz, cp, 0.0))
+                            flags[owner] = 0;
+                    }
+                }
+                wave_lds_sync();
+                if (lane == 0) *qcount = 0u;
+                wave_lds_sync();
+            }
+        }
+        if (act) valid[i] = (ok && flags[lane]) ? 1 : 0;
+        wave_lds_sync();
     }
 }
 
@@ -1856,20 +2097,40 @@ epp_status epp_check_motions(const epp_world* world, const double* s1, const dou
         // LDS-resident variant: coarse grid + lists (blob up to `meta`) and the records
         const uint32_t front = w.off_meta;
         const uint32_t recb = (uint32_t)(((size_t)w.n_obb * kRecDoubles * 8 + 15) & ~size_t(15));
-        if (env_int("EPP_MOTIONS_IMPL", 2) == 2 && front % 16 == 0 && front + recb <= 160u * 1024u &&
+        const int impl = env_int("EPP_MOTIONS_IMPL", 3);
+        // pair-queue kernels (v3 analytic, d32q discrete32) unless v2 is asked for
+        const bool v3 = impl == 3;
+        // 1024-thread blocks: the staged world (~95 KB at 512 OBBs) allows one block per
+        // CU, so 1024 threads double the waves that hide the LDS walk latency
+        const int block = env_int("EPP_MOTIONS_BLOCK", 1024) == 512 ? 512 : 1024;
+        const uint32_t extra =
+            v3 ? (uint32_t)((block / 64) * (((mode == 0 ? kQueueM : kQueueD32) + 1) * 4 + 64)) : 0u;
+        if ((impl == 2 || impl == 3) && front % 16 == 0 && front + recb + extra <= 160u * 1024u &&
             !env_int("EPP_NO_LDS", 0)) {
-            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + kBlockM - 1) / kBlockM, (int64_t)cu_count() *
-                                                    std::max(1, (int)((160u * 1024u) / (front + recb)))));
+            const uint32_t shm = front + recb + extra;
+            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + block - 1) / block, (int64_t)cu_count() *
+                                                    std::max(1, (int)((160u * 1024u) / shm))));
             const WorldView* dw = world_dview(world);
-            if (mode == 0) {
-                allow_lds(k_motions_v2<0>);
-                hipLaunchKernelGGL((k_motions_v2<0>), dim3(grid), dim3(kBlockM), front + recb, st0, dw, s1, s2, n,
-                                   can_pass_gate, valid, front, recb);
+#define EPP_LAUNCH_M(KERNEL)                                                                                  \
+    do {                                                                                                      \
+        allow_lds(KERNEL);                                                                                    \
+        hipLaunchKernelGGL(KERNEL, dim3(grid), dim3(block), shm, st0, dw, s1, s2, n, can_pass_gate, valid, front, \
+                           recb);                                                                             \
+    } while (0)
+            if (v3 && mode == 0) {
+                if (block == 1024) EPP_LAUNCH_M((k_motions_v3<1024>));
+                else EPP_LAUNCH_M((k_motions_v3<512>));
+            } else if (v3) {
+                if (block == 1024) EPP_LAUNCH_M((k_motions_d32q<1024>));
+                else EPP_LAUNCH_M((k_motions_d32q<512>));
+            } else if (mode == 0) {
+                if (block == 1024) EPP_LAUNCH_M((k_motions_v2<0, 1024>));
+                else EPP_LAUNCH_M((k_motions_v2<0, 512>));
             } else {
-                allow_lds(k_motions_v2<1>);
-                hipLaunchKernelGGL((k_motions_v2<1>), dim3(grid), dim3(kBlockM), front + recb, st0, dw, s1, s2, n,
-                                   can_pass_gate, valid, front, recb);
+                if (block == 1024) EPP_LAUNCH_M((k_motions_v2<1, 1024>));
+                else EPP_LAUNCH_M((k_motions_v2<1, 512>));
             }
+#undef EPP_LAUNCH_M
             return launch_error("epp_check_motions");
         }
     }

@@ -128,13 +128,16 @@ def test_compaction(geom, worlds):
     assert np.array_equal(np.sort(idx), np.flatnonzero(exp))
 
 
-@pytest.mark.parametrize("impl", ["2", "1"])
+@pytest.mark.parametrize("impl", ["3", "2", "1", "3/512", "2/512"])
 @pytest.mark.parametrize("name", ["c1", "c2", "c3"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_motions_bit_exact(geom, worlds, name, mode, impl, monkeypatch):
-    """k_motions_v2 (LDS-resident, default) and k_motions (EPP_MOTIONS_IMPL=1) vs the
-    oracle; includes edges parallel to an axis within the 1e-6 threshold."""
+    """k_motions_v3 (analytic pair queue, default), k_motions_v2 (LDS-resident; discrete32
+    default) and k_motions (EPP_MOTIONS_IMPL=1) vs the oracle, at 1024- and 512-thread
+    blocks; includes edges parallel to an axis within the 1e-6 threshold."""
+    impl, _, block = impl.partition("/")
     monkeypatch.setenv("EPP_MOTIONS_IMPL", impl)
+    monkeypatch.setenv("EPP_MOTIONS_BLOCK", block or "1024")
     rg, ro, ws = worlds
     gates, obstacles, (lo, hi) = ws[name]
     ref = O.world_build(geom, gates, obstacles, rg, ro)
@@ -152,6 +155,24 @@ def test_motions_bit_exact(geom, worlds, name, mode, impl, monkeypatch):
         got = w.check_motions(s1, s2, cp, mode)
         exp = O.check_motions(ref, rg, ro, s1, s2, cp, mode, threads=8)
         assert exp.min() == 0 and exp.max() == 1
+        assert np.array_equal(got, exp), (cp, np.flatnonzero(got != exp)[:10])
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("impl", ["3", "2"])
+def test_motions_queue_overflow(geom, worlds, impl, mode, monkeypatch):
+    """Long edges through the 512-OBB world: analytic mode overflows the v3 queue (256
+    pairs per wave, overflow lanes test inline); discrete32 flushes its queue many times
+    per wave.  Answers still match the oracle."""
+    monkeypatch.setenv("EPP_MOTIONS_IMPL", impl)
+    rg, ro, ws = worlds
+    gates, obstacles, (lo, hi) = ws["c3"]
+    ref = O.world_build(geom, gates, obstacles, rg, ro)
+    w = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
+    s1, s2 = synth.edges(61, 62, lo, hi, 20_000, max_len=6.0)
+    for cp in (0, 1):
+        got = w.check_motions(s1, s2, cp, mode)
+        exp = O.check_motions(ref, rg, ro, s1, s2, cp, mode, threads=8)
         assert np.array_equal(got, exp), (cp, np.flatnonzero(got != exp)[:10])
 
 
