@@ -1853,6 +1853,38 @@ bool v5_fits(const WorldView& w) {
            !env_int("EPP_NO_LDS", 0);
 }
 int v5_cap() { return cu_count() * std::max(1, env_int("EPP_WG_PER_CU5", 1)); }
+
+// Launch shape of k_states_v5.  Single pass (every lane one group): by default two
+// 512-thread workgroups per CU when two staged copies fit in LDS (1M states: 8.3-8.4 us
+// vs 8.7-8.8 us for one 1024-thread workgroup — each half of the CU syncs and stages on
+// its own), else one 1024-thread workgroup.  More than one pass: 512 threads, the next
+// group prefetched.  EPP_WG_PER_CU5 / EPP_V5_BLOCK / EPP_V5_SPL override (diagnostics).
+struct V5Shape {
+    bool spl8;
+    int64_t gN;
+    int bs, grid;
+    bool pf;
+};
+V5Shape v5_shape(int64_t n, const uint8_t* valid, uint32_t sb) {
+    V5Shape r{};
+    const bool forced = env_int("EPP_WG_PER_CU5", 0) > 0 || env_int("EPP_V5_BLOCK", 0) > 0;
+    const int64_t cap = v5_cap();
+    r.spl8 = env_int("EPP_V5_SPL", 4) == 8 && (reinterpret_cast<uintptr_t>(valid) & 7) == 0 && n / 8 <= cap * 512;
+    r.gN = n / (r.spl8 ? 8 : 4);
+    const bool two = !forced && !r.spl8 && 2u * (sb + 16u + queue5_bytes<512>()) <= 160u * 1024u &&
+                     r.gN <= 2 * (int64_t)cu_count() * 512;
+    if (two) {
+        r.bs = 512;
+        r.grid = (int)std::max<int64_t>(1, (r.gN + 511) / 512);
+        r.pf = false;
+        return r;
+    }
+    const bool single = r.gN <= cap * (r.spl8 ? 512 : 1024);
+    r.bs = v5_block(r.spl8 ? 512 : (single ? 1024 : 512));
+    r.grid = (int)std::max<int64_t>(1, std::min<int64_t>((r.gN + r.bs - 1) / r.bs, cap));
+    r.pf = r.gN > (int64_t)r.grid * r.bs;  // more than one group per lane
+    return r;
+}
 bool v4_stage(const WorldView& w) {
     return (w.off_bitmap - w.off_aos) + sizeof(StateQueue4) <= 160u * 1024u && !env_int("EPP_NO_LDS", 0);
 }
@@ -1916,19 +1948,17 @@ epp_status launch_states(const WorldView& w, const WorldView* dw, const double* 
         // single pass over the states: 8 states per lane in 512-thread workgroups (half
         // the waves of 4 per lane: fewer executions of the per-wave fixed costs); more
         // than one pass: 4 per lane with the next group prefetched
-        const int64_t cap = v5_cap();
-        const bool spl8 = env_int("EPP_V5_SPL", 4) == 8 && (reinterpret_cast<uintptr_t>(valid) & 7) == 0 &&
-                          n / 8 <= cap * 512;
-        const int spl = spl8 ? 8 : 4;
-        const int64_t gN = n / spl;
-        const bool single = gN <= cap * (spl8 ? 512 : 1024);
-        const int bs = v5_block(spl8 ? 512 : (single ? 1024 : 512));
-        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((gN + bs - 1) / bs, cap));
-        const bool pf = gN > (int64_t)grid * bs;  // more than one group per lane
+        const V5Shape sh = v5_shape(n, valid, sb);
+        const bool spl8 = sh.spl8, pf = sh.pf;
+        const int64_t gN = sh.gN;
+        const int bs = sh.bs, grid = sh.grid;
+        // dynamic LDS: the staged world, optionally padded (EPP_V5_LDS_MIN bytes) so that
+        // no more than the intended number of workgroups can share a CU
+        const uint32_t dyn = std::max<uint32_t>(sb + 16, (uint32_t)std::max(0, env_int("EPP_V5_LDS_MIN", 0)));
 #define EPP_LAUNCH_V5(C, T, B, P, S)                                                                              \
     do {                                                                                                          \
         allow_lds(k_states_v5<MINDIST, C, T, B, P, S>, queue5_bytes<B>());                                        \
-        hipLaunchKernelGGL((k_states_v5<MINDIST, C, T, B, P, S>), dim3(grid), dim3(B), sb + 16, st, dw, xyz, gN, n, \
+        hipLaunchKernelGGL((k_states_v5<MINDIST, C, T, B, P, S>), dim3(grid), dim3(B), dyn, st, dw, xyz, gN, n,     \
                            can_pass, md, valid, compact_idx, nv, sb, fast, tl);                                   \
     } while (0)
 #define EPP_LAUNCH_V5B(B, S)                                          \
@@ -2068,12 +2098,8 @@ epp_status epp_dbg_states_timeline(const epp_world* world, const double* xyz, in
     if (impl == 5 && v5_fits(w) && (reinterpret_cast<uintptr_t>(xyz) & 15) == 0 &&
         (reinterpret_cast<uintptr_t>(valid) & 3) == 0)
         *grid_waves = [&] {
-            const int64_t cap = v5_cap();
-            const bool spl8 = env_int("EPP_V5_SPL", 4) == 8 && (reinterpret_cast<uintptr_t>(valid) & 7) == 0 &&
-                              n / 8 <= cap * 512;
-            const int64_t gN = n / (spl8 ? 8 : 4);
-            const int bs = v5_block(spl8 ? 512 : (gN <= cap * 1024 ? 1024 : 512));
-            return (int)std::max<int64_t>(1, std::min<int64_t>((gN + bs - 1) / bs, cap)) * (bs / 64);
+            const V5Shape sh = v5_shape(n, valid, w.blob_bytes - w.off_aos);
+            return sh.grid * (sh.bs / 64);
         }();
     else if (impl >= 3)  // (the timeline runs k_states_v3 for impl 4 too)
         *grid_waves = v3_grid(w, n) * (kBlock3 / 64);

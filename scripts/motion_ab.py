@@ -12,11 +12,13 @@ from eppamd import capi, config, synth  # noqa: E402
 cfg = config.load(os.path.join(ROOT, "configs", "config.json"))
 geom = config.geometry(cfg)
 rg, ro = config.inflate_radii(cfg)
-g3, o3 = synth.track_world(42, n_obstacles=472)
+# argv[1] == "c2": the planner's case (C4 track world, 64 OBBs, short k-NN-like edges)
+c2 = len(sys.argv) > 1 and sys.argv[1] == "c2"
+g3, o3 = synth.track_world(100) if c2 else synth.track_world(42, n_obstacles=472)
 w3 = capi.World(capi.build_obbs(geom, g3, o3), rg, ro)
 lo, hi = synth.C2_BOUNDS
 n = 1 << 20
-s1, s2 = synth.edges(43, 8, lo, hi, n)
+s1, s2 = synth.edges(43, 8, lo, hi, n, max_len=0.25 if c2 else 0.5)
 import ctypes as C  # noqa: E402
 st = C.c_void_p()
 capi.check(capi.lib().epp_stream_create(C.byref(st)))

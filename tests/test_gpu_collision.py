@@ -91,15 +91,17 @@ def test_states_mindist(geom, worlds, name):
         assert np.array_equal(got, exp), md
 
 
-@pytest.mark.parametrize("impl", ["0", "1", "3", "4", "5", "5walk", "5b512", "5spl8"])
+@pytest.mark.parametrize("impl", ["0", "1", "3", "4", "5", "5walk", "5b512", "5b1024", "5spl8"])
 @pytest.mark.parametrize("name", ["c2", "c3"])
 def test_states_every_kernel_variant(geom, worlds, name, impl, monkeypatch):
     """Each k_states variant (EPP_STATES_IMPL; 5 = default, falls back when its staged
     world does not fit LDS; "5walk" = v5 with per-state list walks instead of pairs) on
-    plain, compacting and minDistance launches, ragged n."""
+    plain, compacting and minDistance launches, ragged n.  "5" runs the default launch
+    shape (two 512-thread workgroups per CU for a single pass), "5b512"/"5b1024" force
+    one workgroup shape."""
     monkeypatch.setenv("EPP_STATES_IMPL", impl[0])
     monkeypatch.setenv("EPP_V5_PAIRS", "0" if impl.endswith("walk") else "1")
-    monkeypatch.setenv("EPP_V5_BLOCK", "512" if impl.endswith("b512") else "1024")
+    monkeypatch.setenv("EPP_V5_BLOCK", "512" if impl.endswith("b512") else ("1024" if impl.endswith("b1024") else ""))
     monkeypatch.setenv("EPP_V5_SPL", "8" if impl.endswith("spl8") else "4")
     impl = int(impl[0])
     rg, ro, ws = worlds
@@ -114,6 +116,18 @@ def test_states_every_kernel_variant(geom, worlds, name, impl, monkeypatch):
     for n in (1, 2, 3, 5, 4097):
         assert np.array_equal(w.check_states(pts[:n], False), exp[:n]), n
     assert np.array_equal(w.check_states_mindist(pts, 0.15), O.check_states_mindist(ref, pts, 0.15))
+
+
+@pytest.mark.parametrize("n", [1 << 20, (1 << 20) + 4 * 256 * 512 + 7, 5 << 20])
+def test_states_full_size(geom, worlds, n):
+    """BASELINE C2 size (1,048,576 states: the single-pass two-workgroups-per-CU shape),
+    just past it, and 5M states (prefetching multi-pass shape), bit-exact vs the oracle."""
+    rg, ro, ws = worlds
+    gates, obstacles, (lo, hi) = ws["c2"]
+    ref = O.world_build(geom, gates, obstacles, rg, ro)
+    w = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
+    pts = synth.sample_states(7, lo, hi, n)
+    assert np.array_equal(w.check_states(pts, False), O.check_states(ref, rg, ro, pts, False, threads=8))
 
 
 def test_compaction(geom, worlds):
