@@ -25,9 +25,9 @@ capi.check(capi.lib().epp_stream_create(C.byref(st)))
 d1, d2 = capi.DeviceBuffer.from_array(s1, st), capi.DeviceBuffer.from_array(s2, st)
 dv = capi.DeviceBuffer(n)
 out = {}
-for impl, block in [("2", "512"), ("2", "1024"), ("3", "512"), ("3", "1024")]:
+for impl, block in [tuple(x.split(":")) for x in os.environ.get("AB_CFGS", "2:512,2:1024,3:512,3:1024").split(",")]:
     os.environ["EPP_MOTIONS_IMPL"], os.environ["EPP_MOTIONS_BLOCK"] = impl, block
-    for mode in (0, 1):
+    for mode in [int(m) for m in os.environ.get("AB_MODES", "0,1").split(",")]:
         f = lambda r: w3.check_motions_dev(d1.ptr, d2.ptr, n, 0, mode, dv.ptr, stream=st)  # noqa: E731
         f(0)
         ms = bench.timed_kernel_ms(capi, st, f, 20)

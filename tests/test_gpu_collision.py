@@ -142,16 +142,18 @@ def test_compaction(geom, worlds):
     assert np.array_equal(np.sort(idx), np.flatnonzero(exp))
 
 
-@pytest.mark.parametrize("impl", ["3", "2", "1", "3/512", "2/512"])
+@pytest.mark.parametrize("impl", ["4", "3", "2", "1", "4/512", "3/512", "2/512", "4/1024", "3/1024", "2/1024"])
 @pytest.mark.parametrize("name", ["c1", "c2", "c3"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_motions_bit_exact(geom, worlds, name, mode, impl, monkeypatch):
-    """k_motions_v3 (analytic pair queue, default), k_motions_v2 (LDS-resident; discrete32
-    default) and k_motions (EPP_MOTIONS_IMPL=1) vs the oracle, at 1024- and 512-thread
-    blocks; includes edges parallel to an axis within the 1e-6 threshold."""
+    """k_motions_v4 (analytic, lane-balanced walk; default) / k_motions_d32q (discrete32
+    default, impl 3 and 4), k_motions_v3 (analytic per-lane walk), k_motions_v2
+    (LDS-resident) and k_motions (EPP_MOTIONS_IMPL=1) vs the oracle, at the default block
+    size and forced 512/1024-thread blocks; includes edges parallel to an axis within the
+    1e-6 threshold."""
     impl, _, block = impl.partition("/")
     monkeypatch.setenv("EPP_MOTIONS_IMPL", impl)
-    monkeypatch.setenv("EPP_MOTIONS_BLOCK", block or "1024")
+    monkeypatch.setenv("EPP_MOTIONS_BLOCK", block)  # "" = by LDS fit (the default)
     rg, ro, ws = worlds
     gates, obstacles, (lo, hi) = ws[name]
     ref = O.world_build(geom, gates, obstacles, rg, ro)
@@ -173,7 +175,7 @@ def test_motions_bit_exact(geom, worlds, name, mode, impl, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("impl", ["3", "2"])
+@pytest.mark.parametrize("impl", ["4", "3", "2"])
 def test_motions_queue_overflow(geom, worlds, impl, mode, monkeypatch):
     """Long edges through the 512-OBB world: analytic mode overflows the v3 queue (256
     pairs per wave, overflow lanes test inline); discrete32 flushes its queue many times
