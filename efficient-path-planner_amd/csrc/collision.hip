@@ -1997,6 +1997,149 @@ __global__ __launch_bounds__(BLOCK) void k_motions_d32q(const WorldView* __restr
     }
 }
 
+// ---- k_motions_d32b: discrete32, lane-balanced list walk ------------------------------
+// As k_motions_d32q (wave-uniform steps k = 1..32, queued (lane, k, OBB) triples, the
+// exact OBB::checkCollisionWithPoint on flush), but at each step the occupied lanes'
+// cell lists are expanded over the whole wave (exclusive scan of the list lengths,
+// segment heads, DPP max-scan) instead of each lane walking its own list: the wave pays
+// ceil(sum of lengths / 64) rounds instead of the longest list.  The entry filter is the
+// rtree `contains` (src/World.cpp:83) against the outward-rounded float AABB (a superset
+// of the strict double test, which rec_hit repeats).  The queue is flushed before it
+// could overflow.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_motions_d32b(const WorldView* __restrict__ wv,
+                                                        const double* __restrict__ s1, const double* __restrict__ s2,
+                                                        int64_t n, int can_pass, uint8_t* __restrict__ valid,
+                                                        uint32_t front_bytes, uint32_t rec_bytes) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    {
+        const uint4* src0 = reinterpret_cast<const uint4*>(wv->blob);
+        const uint4* src1 = reinterpret_cast<const uint4*>(wv->blob + wv->off_aos);
+        uint4* dst = reinterpret_cast<uint4*>(lds);
+        for (uint32_t o = threadIdx.x; o < front_bytes / 16; o += BLOCK) dst[o] = src0[o];
+        uint4* dst1 = reinterpret_cast<uint4*>(lds + front_bytes);
+        for (uint32_t o = threadIdx.x; o < rec_bytes / 16; o += BLOCK) dst1[o] = src1[o];
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    constexpr uint32_t kWaveBytes = (kQueueD32 + 1) * 4 + 64 + 256;
+    unsigned char* wbase = lds + front_bytes + rec_bytes + wave * kWaveBytes;
+    uint32_t* queue = reinterpret_cast<uint32_t*>(wbase);
+    uint32_t* qcount = queue + kQueueD32;
+    uint8_t* flags = wbase + (kQueueD32 + 1) * 4;
+    uint32_t* heads = reinterpret_cast<uint32_t*>(wbase + (kQueueD32 + 1) * 4 + 64);
+    float4* filt = reinterpret_cast<float4*>(lds + front_bytes + rec_bytes + (BLOCK / 64) * kWaveBytes);
+    const unsigned long long* mask = reinterpret_cast<const unsigned long long*>(lds + wv->off_cell_mask);
+    const uint32_t* cs = reinterpret_cast<const uint32_t*>(lds + wv->off_cell_start);
+    const uint16_t* co = reinterpret_cast<const uint16_t*>(lds + wv->off_cell_obb);
+    const double* recs = reinterpret_cast<const double*>(lds + front_bytes);
+    __syncthreads();  // records staged
+    for (int o = threadIdx.x; o < wv->n_obb; o += BLOCK) {
+        const double* r = recs + (size_t)o * kRecDoubles;
+        filt[2 * o] = make_float4(__double2float_rd(r[F_LOX]), __double2float_rd(r[F_LOY]), __double2float_rd(r[F_LOZ]),
+                                  0.0f);
+        filt[2 * o + 1] = make_float4(__double2float_ru(r[F_HIX]), __double2float_ru(r[F_HIY]),
+                                      __double2float_ru(r[F_HIZ]), 0.0f);
+    }
+    const int nx = wv->nx, ny = wv->ny;
+    const float ofx = wv->ofx, ofy = wv->ofy, ofz = wv->ofz, i4x = wv->i4x, i4y = wv->i4y, i4z = wv->i4z;
+    const float limx = wv->limx, limy = wv->limy, limz = wv->limz;
+    const float fmx = wv->fmaxx, fmy = wv->fmaxy, fmz = wv->fmaxz;
+    const double rg = wv->r_gate, ro = wv->r_obst;
+    const bool cp = can_pass != 0;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * BLOCK;
+    for (int64_t i0 = (int64_t)blockIdx.x * BLOCK + wave * 64; i0 < n; i0 += stride) {
+        const int64_t i = i0 + lane;
+        const bool act = i < n;
+        double s[3] = {0.0, 0.0, 0.0}, e[3] = {0.0, 0.0, 0.0};
+        if (act) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                s[k] = s1[3 * i + k];
+                e[k] = s2[3 * i + k];
+            }
+        }
+        if (lane == 0) *qcount = 0u;
+        flags[lane] = act ? 1 : 0;
+        wave_lds_sync();
+        auto flush = [&]() {
+            const uint32_t total = *qcount;
+            for (uint32_t base = 0; base < total; base += 64) {
+                const uint32_t j = base + lane;
+                const bool has = j < total;
+                const uint32_t qe = has ? queue[j] : 0u;
+                const int owner = (int)(qe & 63u);
+                double ps[3], pe[3];
+#pragma unroll
+                for (int d = 0; d < 3; ++d) {
+                    ps[d] = __shfl(s[d], owner);
+                    pe[d] = __shfl(e[d], owner);
+                }
+                if (has) {
+                    const double tq = (double)(((qe >> 6) & 31u) + 1u) / 32.0;
+                    const double qx = ps[0] + (pe[0] - ps[0]) * tq;
+                    const double qy = ps[1] + (pe[1] - ps[1]) * tq;
+                    const double qz = ps[2] + (pe[2] - ps[2]) * tq;
+                    if (rec_hit<false>(recs + (size_t)(qe >> 11) * kRecDoubles, rg, ro, qx, qy, qz, cp, 0.0))
+                        flags[owner] = 0;
+                }
+            }
+            wave_lds_sync();
+            if (lane == 0) *qcount = 0u;
+            wave_lds_sync();
+        };
+        for (int k = 1; k <= 32; ++k) {
+            const double t = (double)k / 32.0;
+            const double px = s[0] + (e[0] - s[0]) * t;
+            const double py = s[1] + (e[1] - s[1]) * t;
+            const double pz = s[2] + (e[2] - s[2]) * t;
+            const float fx = fine_coord(px, ofx, i4x), fy = fine_coord(py, ofy, i4y), fz = fine_coord(pz, ofz, i4z);
+            const bool in = (fx >= 0.0f) & (fx <= limx) & (fy >= 0.0f) & (fy <= limy) & (fz >= 0.0f) & (fz <= limz);
+            const int ix = (int)fminf(fmaxf(fx, 0.0f), fmx);
+            const int iy = (int)fminf(fmaxf(fy, 0.0f), fmy);
+            const int iz = (int)fminf(fmaxf(fz, 0.0f), fmz);
+            const int cell = ((iz >> 2) * ny + (iy >> 2)) * nx + (ix >> 2);
+            const uint32_t bit = (uint32_t)((((iz & 3) << 2) + (iy & 3)) * 4 + (ix & 3));
+            const bool live = flags[lane] != 0;
+            const bool occ = live && in && ((mask[cell] >> bit) & 1ull);
+            const uint32_t b = occ ? cs[cell] : 0u;
+            const uint32_t len = occ ? cs[cell + 1] - b : 0u;
+            uint32_t total_e;
+            const uint32_t offe = wave_excl_scan(len, lane, total_e);
+            uint32_t carry_s = 0u;
+            for (uint32_t eb = 0; eb < total_e; eb += 64) {
+                if (*qcount > (uint32_t)(kQueueD32 - 64)) flush();
+                heads[lane] = 0u;
+                wave_lds_sync();
+                if (len > 0u && offe >= eb && offe < eb + 64u) heads[offe - eb] = (uint32_t)lane + 1u;
+                wave_lds_sync();
+                const uint32_t hs = dpp_incl_max(heads[lane]);
+                const uint32_t own = hs ? hs - 1u : carry_s;
+                carry_s = (uint32_t)__builtin_amdgcn_readlane((int)own, 63);
+                const bool has = eb + (uint32_t)lane < total_e;
+                const uint32_t sb = (uint32_t)__shfl((int)b, (int)own);
+                const uint32_t soff = (uint32_t)__shfl((int)offe, (int)own);
+                const double qx = __shfl(px, (int)own), qy = __shfl(py, (int)own), qz = __shfl(pz, (int)own);
+                if (has) {
+                    const uint32_t id = co[sb + (eb + (uint32_t)lane - soff)];
+                    const float4 fa = filt[2 * id], fb = filt[2 * id + 1];
+                    const bool may = ((double)fa.x < qx) & (qx < (double)fb.x) & ((double)fa.y < qy) &
+                                     (qy < (double)fb.y) & ((double)fa.z < qz) & (qz < (double)fb.z);
+                    if (may) {
+                        const uint32_t slot = atomicAdd(qcount, 1u);
+                        queue[slot] = (id << 11) | ((uint32_t)(k - 1) << 6) | own;
+                    }
+                }
+                wave_lds_sync();
+            }
+            if (*qcount >= kFlushD32) flush();
+        }
+        flush();
+        if (act) valid[i] = flags[lane] ? 1 : 0;
+        wave_lds_sync();
+    }
+}
+
 struct DevInfo {
     int cus = 256;
     bool init = false;
@@ -2349,12 +2492,14 @@ epp_status epp_check_motions(const epp_world* world, const double* s1, const dou
         // LDS-resident variant: coarse grid + lists (blob up to `meta`) and the records
         const uint32_t front = w.off_meta;
         const uint32_t recb = (uint32_t)(((size_t)w.n_obb * kRecDoubles * 8 + 15) & ~size_t(15));
-        const int impl = env_int("EPP_MOTIONS_IMPL", 4);
+        const int impl = env_int("EPP_MOTIONS_IMPL", 5);  // 5: v4 analytic + d32b discrete32
         // pair-queue kernels (v3/v4 analytic, d32q discrete32) unless v2 is asked for
-        const bool v3 = impl == 3 || impl == 4;
-        const bool v4 = impl == 4 && mode == 0;
+        const bool v3 = impl == 3 || impl == 4 || impl == 5;
+        const bool v4 = (impl == 4 || impl == 5) && mode == 0;
+        const bool d32b = impl == 5 && mode == 1;  // (analytic under impl 5: v4)
         auto extra_for = [&](int blk) -> uint32_t {
-            return v4   ? (uint32_t)((blk / 64) * ((kQueueM + 1) * 4 + 64 + 256) + (uint32_t)w.n_obb * 32u)
+            return v4     ? (uint32_t)((blk / 64) * ((kQueueM + 1) * 4 + 64 + 256) + (uint32_t)w.n_obb * 32u)
+                   : d32b ? (uint32_t)((blk / 64) * ((kQueueD32 + 1) * 4 + 64 + 256) + (uint32_t)w.n_obb * 32u)
                    : v3 ? (uint32_t)((blk / 64) * (((mode == 0 ? kQueueM : kQueueD32) + 1) * 4 + 64) +
                                      (mode == 0 ? (uint32_t)w.n_obb * 32u : 0u))
                         : 0u;
@@ -2381,6 +2526,9 @@ epp_status epp_check_motions(const epp_world* world, const double* s1, const dou
             if (v4) {
                 if (block == 1024) EPP_LAUNCH_M((k_motions_v4<1024>));
                 else EPP_LAUNCH_M((k_motions_v4<512>));
+            } else if (d32b) {
+                if (block == 1024) EPP_LAUNCH_M((k_motions_d32b<1024>));
+                else EPP_LAUNCH_M((k_motions_d32b<512>));
             } else if (v3 && mode == 0) {
                 if (block == 1024) EPP_LAUNCH_M((k_motions_v3<1024>));
                 else EPP_LAUNCH_M((k_motions_v3<512>));

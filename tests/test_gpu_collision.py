@@ -142,12 +142,12 @@ def test_compaction(geom, worlds):
     assert np.array_equal(np.sort(idx), np.flatnonzero(exp))
 
 
-@pytest.mark.parametrize("impl", ["4", "3", "2", "1", "4/512", "3/512", "2/512", "4/1024", "3/1024", "2/1024"])
+@pytest.mark.parametrize("impl", ["5", "4", "3", "2", "1", "5/512", "4/512", "3/512", "2/512", "5/1024", "4/1024", "3/1024", "2/1024"])
 @pytest.mark.parametrize("name", ["c1", "c2", "c3"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_motions_bit_exact(geom, worlds, name, mode, impl, monkeypatch):
-    """k_motions_v4 (analytic, lane-balanced walk; default) / k_motions_d32q (discrete32
-    default, impl 3 and 4), k_motions_v3 (analytic per-lane walk), k_motions_v2
+    """impl 5 (default): k_motions_v4 (analytic, lane-balanced walk) + k_motions_d32b
+    (discrete32, lane-balanced); impl 4: v4 + k_motions_d32q; impl 3: k_motions_v3 (analytic per-lane walk), k_motions_v2
     (LDS-resident) and k_motions (EPP_MOTIONS_IMPL=1) vs the oracle, at the default block
     size and forced 512/1024-thread blocks; includes edges parallel to an axis within the
     1e-6 threshold."""
@@ -175,7 +175,7 @@ def test_motions_bit_exact(geom, worlds, name, mode, impl, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("impl", ["4", "3", "2"])
+@pytest.mark.parametrize("impl", ["5", "4", "3", "2"])
 def test_motions_queue_overflow(geom, worlds, impl, mode, monkeypatch):
     """Long edges through the 512-OBB world: analytic mode overflows the v3 queue (256
     pairs per wave, overflow lanes test inline); discrete32 flushes its queue many times
