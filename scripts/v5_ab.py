@@ -29,7 +29,7 @@ for b in range(B):
     pts = synth.sample_states(7, lo, hi, N, start=b * N)
     capi.check(L.epp_memcpy_h2d(d.ptr + b * N * 24, pts.ctypes.data, pts.nbytes, st))
 dv = capi.DeviceBuffer(N)
-keys = ["EPP_V5_BLOCK", "EPP_WG_PER_CU5", "EPP_V5_LDS_MIN", "EPP_V5_SPL", "EPP_BITMAP_BITS"]
+keys = ["EPP_V5_BLOCK", "EPP_WG_PER_CU5", "EPP_V5_LDS_MIN", "EPP_V5_SPL", "EPP_BITMAP_BITS", "EPP_V5_PAIRS"]
 res = {c: [] for c in cfgs}
 
 
