@@ -65,8 +65,8 @@ def timed_kernel_ms(capi, stream, fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=2000)  # ~17 ms timed: host hiccups amortised
+    ap.add_argument("--warmup", type=int, default=200)  # ~2 ms of GPU work: clocks settle
     ap.add_argument("--no-side", action="store_true", help="skip the side measurements")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-plan", action="store_true", help="skip the full-plan (C4) leg")
@@ -110,17 +110,27 @@ def main():
     capi.check(L.epp_stream_sync(stream))
     dist.barrier()
     capi.check(L.epp_stream_sync(stream))
+    ev0, ev1 = C.c_void_p(), C.c_void_p()
+    capi.check(L.epp_event_create(C.byref(ev0)))
+    capi.check(L.epp_event_create(C.byref(ev1)))
     t0 = time.perf_counter()
+    capi.check(L.epp_event_record(ev0, stream))
     for i in range(args.steps):
         step(i)
+    capi.check(L.epp_event_record(ev1, stream))
     capi.check(L.epp_stream_sync(stream))
     dist.barrier()
     t1 = time.perf_counter()
     elapsed = dist.max(t1 - t0)
     value = ws * N_STATES * args.steps / elapsed
 
-    # dominant kernel's average launch time, HIP events on the launch stream
-    kms = timed_kernel_ms(capi, stream, step, max(10, min(args.steps, 50)))
+    # dominant kernel's average launch time: HIP events on the launch stream bracketing
+    # the timed region's K back-to-back launches (the only kernel in it)
+    evms = C.c_float()
+    capi.check(L.epp_event_elapsed_ms(ev0, ev1, C.byref(evms)))
+    L.epp_event_destroy(ev0)
+    L.epp_event_destroy(ev1)
+    kms = evms.value / args.steps
     achieved = BYTES_PER_STATE * N_STATES / (kms * 1e-3) / 1e9
     n_valid = int(d_valid.download(np.uint8, N_STATES).sum())
 
