@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-plan", action="store_true", help="skip the full-plan (C4) leg")
     ap.add_argument("--plan-reps", type=int, default=5)
+    ap.add_argument("--host-loop", action="store_true",
+                    help="launch the timed steps from a host loop instead of replaying a captured HIP graph")
     args = ap.parse_args()
 
     from eppamd.dist import Dist, env
@@ -108,6 +110,30 @@ def main():
     for i in range(args.warmup):
         step(i)
     capi.check(L.epp_stream_sync(stream))
+    # The K timed steps (the same K launches the host loop would make) are captured once
+    # into a HIP graph and replayed, so the kernels dispatch back to back whatever the
+    # host launch path costs (an ~8 us kernel is about one host-side launch; under
+    # rocprofv3's kernel trace a host loop runs at ~11 us per launch).
+    graph = None
+    if not args.host_loop:
+        g = C.c_void_p()
+        try:
+            capi.check(L.epp_graph_begin(stream))
+            for i in range(args.steps):
+                step(i)
+            capi.check(L.epp_graph_end(stream, C.byref(g)))
+            graph = g.value
+        except capi.EppError as e:
+            print(f"bench: graph capture failed ({e}); timing the host loop", file=sys.stderr)
+        capi.check(L.epp_stream_sync(stream))
+
+    def run_steps():
+        if graph is not None:
+            capi.check(L.epp_graph_launch(graph, stream))
+        else:
+            for i in range(args.steps):
+                step(i)
+
     dist.barrier()
     capi.check(L.epp_stream_sync(stream))
     ev0, ev1 = C.c_void_p(), C.c_void_p()
@@ -115,8 +141,7 @@ def main():
     capi.check(L.epp_event_create(C.byref(ev1)))
     t0 = time.perf_counter()
     capi.check(L.epp_event_record(ev0, stream))
-    for i in range(args.steps):
-        step(i)
+    run_steps()
     capi.check(L.epp_event_record(ev1, stream))
     capi.check(L.epp_stream_sync(stream))
     dist.barrier()
@@ -131,6 +156,8 @@ def main():
     L.epp_event_destroy(ev0)
     L.epp_event_destroy(ev1)
     kms = evms.value / args.steps
+    if graph is not None:
+        capi.check(L.epp_graph_destroy(graph))
     achieved = BYTES_PER_STATE * N_STATES / (kms * 1e-3) / 1e9
     n_valid = int(d_valid.download(np.uint8, N_STATES).sum())
 
@@ -165,7 +192,8 @@ def main():
             "config": {"workload": "C2: 1 track, 8 gates, 64 OBBs, 1,048,576 sampled states per step",
                        "states_per_step_per_gpu": N_STATES, "obbs": int(len(obbs)),
                        "can_pass_gate": False, "valid_fraction": n_valid / N_STATES,
-                       "parallelism": f"replicas x{ws} (independent samplers)"},
+                       "parallelism": f"replicas x{ws} (independent samplers)",
+                       "launch": "hip graph of the K steps" if graph is not None else "host loop"},
             "roofline": {"bound": "hbm", "kernel": "k_states_v5", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "traffic_unit": "bytes per launch",

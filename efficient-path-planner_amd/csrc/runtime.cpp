@@ -100,4 +100,32 @@ epp_status epp_event_elapsed_ms(void* start, void* stop, float* ms) {
 }
 void epp_host_free(void* p) { std::free(p); }
 
+// Stream capture into a HIP graph: a captured sequence of stream-ordered epp_* calls is
+// replayed with one host call (the kernels dispatch back to back, no per-launch host
+// work in between).  Relaxed mode keeps the launchers' host-side queries legal.
+epp_status epp_graph_begin(void* stream) {
+    EPP_HIP_RET(hipStreamBeginCapture((hipStream_t)stream, hipStreamCaptureModeRelaxed));
+    return EPP_OK;
+}
+epp_status epp_graph_end(void* stream, void** exec) {
+    if (!exec) return EPP_ERR_INVALID_ARGUMENT;
+    hipGraph_t g = nullptr;
+    EPP_HIP_RET(hipStreamEndCapture((hipStream_t)stream, &g));
+    hipGraphExec_t e = nullptr;
+    const hipError_t err = hipGraphInstantiate(&e, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    EPP_HIP_RET(err);
+    EPP_HIP_RET(hipGraphUpload(e, (hipStream_t)stream));
+    *exec = e;
+    return EPP_OK;
+}
+epp_status epp_graph_launch(void* exec, void* stream) {
+    EPP_HIP_RET(hipGraphLaunch((hipGraphExec_t)exec, (hipStream_t)stream));
+    return EPP_OK;
+}
+epp_status epp_graph_destroy(void* exec) {
+    if (exec) EPP_HIP_RET(hipGraphExecDestroy((hipGraphExec_t)exec));
+    return EPP_OK;
+}
+
 }  // extern "C"

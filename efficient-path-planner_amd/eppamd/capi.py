@@ -57,6 +57,10 @@ def lib() -> C.CDLL:
             "epp_event_destroy": (i32, [vp]),
             "epp_event_record": (i32, [vp, vp]),
             "epp_event_elapsed_ms": (i32, [vp, vp, C.POINTER(C.c_float)]),
+            "epp_graph_begin": (i32, [vp]),
+            "epp_graph_end": (i32, [vp, C.POINTER(vp)]),
+            "epp_graph_launch": (i32, [vp, vp]),
+            "epp_graph_destroy": (i32, [vp]),
             "epp_build_obbs": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, i32, vp, i32, C.POINTER(i32)]),
             "epp_world_create": (i32, [vp, i32, dp, dp, C.POINTER(vp)]),
             "epp_world_update": (i32, [vp, vp, i32]),
@@ -109,6 +113,7 @@ EXPORTED = [
     "epp_knn_bruteforce", "epp_knn_grid", "epp_knn_workspace_size", "epp_knn_ws", "epp_knn_grid_ws",
     "epp_knn_edges", "epp_compact_states", "epp_mask_edges", "epp_optimal_trajectory_host",
     "epp_spline_trajectory_host", "epp_compact_workspace_size", "epp_compact_states_ws",
+    "epp_graph_begin", "epp_graph_end", "epp_graph_launch", "epp_graph_destroy",
 ]
 
 

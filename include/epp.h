@@ -86,6 +86,13 @@ epp_status epp_event_create(void** event);
 epp_status epp_event_destroy(void* event);
 epp_status epp_event_record(void* event, void* stream);
 epp_status epp_event_elapsed_ms(void* start, void* stop, float* ms);
+/* Stream capture of stream-ordered epp_* calls into an instantiated HIP graph and its
+ * replay (no counterpart in the reference: launch-overhead tool for batched callers,
+ * e.g. bench.py's timed steps). */
+epp_status epp_graph_begin(void* stream);
+epp_status epp_graph_end(void* stream, void** exec);
+epp_status epp_graph_launch(void* exec, void* stream);
+epp_status epp_graph_destroy(void* exec);
 
 /* ---- world ------------------------------------------------------------------------ */
 /* World::addGate / World::addObstacle (src/World.cpp:13-55) via
