@@ -125,6 +125,9 @@ def main():
             graph = g.value
         except capi.EppError as e:
             print(f"bench: graph capture failed ({e}); timing the host loop", file=sys.stderr)
+            if L.epp_graph_end(stream, C.byref(g)) == 0:  # leave capture mode if still in it
+                L.epp_graph_destroy(g)
+            graph = None
         capi.check(L.epp_stream_sync(stream))
 
     def run_steps():
