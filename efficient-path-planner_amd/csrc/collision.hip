@@ -1071,7 +1071,6 @@ __global__ __launch_bounds__(kBlock4) void k_states_v4(const WorldView* __restri
 // queued state walks its own list.  One 32-bit store writes a lane's four flags.
 // The per-state VALU count matters: at 1M states/launch the kernel's critical path is
 // the last-arriving data plus the VALU work behind it (PMC: SQ_INSTS_VALU).
-constexpr int kBlock5 = 1024;  // threads per workgroup (BLOCK template default)
 struct WaveQueue5 {
     double x[64], y[64], z[64];
     uint32_t pair[128];  // segment heads of the (state, candidate) pairs
@@ -1375,7 +1374,6 @@ __global__ __launch_bounds__(kBlock) void k_motions(WorldView w, const double* _
 // candidate costs one LDS round trip instead of the short-circuit chain of dependent
 // global loads of k_motions.  Same candidate order, de-duplication (first common cell)
 // and predicates as ray_valid / ray_valid_d32 (src/World.cpp:130-162, src/OBB.cpp:10-91).
-constexpr int kBlockM = 512;  // default k_motions_v2 block (EPP_MOTIONS_BLOCK=512)
 
 // OBB::checkCollisionWithRay (src/OBB.cpp:10-61) on one AoS record, branch-free.  `r` is
 // the owner's inflation radius; the endpoint tests inflate only collision OBBs (:13-14),
