@@ -73,10 +73,20 @@ def main():
     ap.add_argument("--plan-reps", type=int, default=5)
     ap.add_argument("--host-loop", action="store_true",
                     help="launch the timed steps from a host loop instead of replaying a captured HIP graph")
+    ap.add_argument("--launcher-check", action="store_true",
+                    help="CPU-only: run the rank launch + gloo exchange plumbing and print one JSON line")
     args = ap.parse_args()
 
-    from eppamd.dist import Dist, env
+    from eppamd.dist import Dist, env, spawn_ranks
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `bench.py --gpus N` without a launcher: one child process per GPU (rank = local
+        # rank = GPU index), started before this process touches the GPU
+        sys.exit(spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
     ws, rank, local = env()
+    if ws != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws} (launch one process per GPU)")
+    if args.launcher_check:
+        return launcher_check(ws, rank, local)
     dist = Dist(ws, rank, local, "nccl")
     import ctypes as C
 
@@ -210,6 +220,22 @@ def main():
         }
         print(json.dumps(out))
     capi.check(L.epp_stream_destroy(stream))
+    dist.close()
+
+
+def launcher_check(ws, rank, local):
+    """The multi-rank plumbing of this bench without a GPU (gloo): the same launch, env,
+    barrier, max-over-ranks reduction and ragged waypoint all-gather as the GPU run."""
+    from eppamd.dist import Dist
+    dist = Dist(ws, rank, local, "gloo")
+    dist.barrier()
+    wp = np.arange(3 * (5 + rank), dtype=np.float64).reshape(-1, 3) + 1000 * rank
+    sets = dist.all_gather_waypoints(wp)
+    t = dist.max(float(rank + 1))
+    if rank == 0:
+        print(json.dumps({"n_gpus": ws, "ranks_seen": [int(s[0, 0] // 1000) for s in sets],
+                          "waypoints_per_track": [len(s) for s in sets], "max_over_ranks": t,
+                          "local_rank": local}))
     dist.close()
 
 

@@ -1,0 +1,456 @@
+// motions.hip — batched motion (edge) validity checks for gfx950 (MI355X).
+//
+//   World::checkRayValid(s, e, canPassGate)  src/World.cpp:130-162, via
+//   OBB::checkCollisionWithRay               src/OBB.cpp:10-61        (mode 0, analytic)
+//   32-step discretised check                BASELINE config 3         (mode 1; points
+//   s + (e - s) k/32, k = 1..32, each World::checkPointValidity(p, canPassGate))
+//
+// Kernels, chosen by what fits (epp_check_motions):
+//   k_motions_v4   analytic, coarse grid + records in LDS, lane-balanced list walk;
+//   k_motions_d32b discrete32, same staging, lane-balanced list walk per step;
+//   k_motions      generic (worlds too large for LDS): one lane per edge, L2-resident world.
+#include "collision_common.h"
+
+namespace epp {
+namespace {
+
+// Generic kernel (worlds whose coarse grid + records exceed LDS): one lane per edge, four
+// edges per lane and iteration, the world read through L1/L2.
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_motions(WorldView w, const double* __restrict__ s1,
+                                                    const double* __restrict__ s2, int64_t n,
+                                                    int can_pass, uint8_t* __restrict__ valid,
+                                                    int aligned) {
+    const Acc a = make_acc(w.blob, w.blob, w);
+    const int64_t groups = (n + 3) / 4;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x; g < groups; g += stride) {
+        const int64_t first = 4 * g;
+        double vs[12], ve[12];
+        load4(s1, first, n, aligned != 0, vs);
+        load4(s2, first, n, aligned != 0, ve);
+        uint32_t f[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (first + k < n) {
+                const double* s = vs + 3 * k;
+                const double* e = ve + 3 * k;
+                f[k] = (MODE == 0 ? ray_valid(a, w, s, e, can_pass != 0)
+                                  : ray_valid_d32(a, w, s, e, can_pass != 0))
+                           ? 1u
+                           : 0u;
+            }
+        store4(valid, first, n, f);
+    }
+}
+
+constexpr int kQueueM = 256;  // queued (edge, OBB) pairs per wave  // queued pairs per wave
+
+// ---- k_motions_v4: analytic motion checks, lane-balanced candidate walk ---------------
+// v3's walk is per lane, so a wave pays its worst lane's list length (C3: 28.5 entries
+// against a wave average of 6.7).  v4 expands the work over the whole wave in two
+// levels, all in wave-uniform control flow:
+//   1. (edge, coarse cell) pairs: each lane's cell box has nc cells; an exclusive scan of
+//      nc lays the pairs out, 64 per chunk; a lane finds the pair's owner edge by a DPP
+//      max-scan of segment heads (LDS `heads`) and decodes the cell from the owner's box;
+//   2. (pair, list entry): the chunk's list lengths are scanned the same way; each lane
+//      takes one entry, reads the OBB's 32-byte filter record (outward-rounded float
+//      AABB + meta) and applies the first-common-cell rule, the overlap test and the
+//      filling skip (src/World.cpp:143-153); survivors go to the wave's queue.
+// The queue is flushed (exact double overlap + OBB::checkCollisionWithRay on 64 pairs at
+// a time, as in v3) whenever it could not take another chunk, and at the end, so it never
+// overflows.  Same answers as the reference: an edge is invalid iff some candidate hits.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_motions_v4(const WorldView* __restrict__ wv, const double* __restrict__ s1,
+                                                      const double* __restrict__ s2, int64_t n, int can_pass,
+                                                      uint8_t* __restrict__ valid, uint32_t front_bytes,
+                                                      uint32_t rec_bytes) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    {
+        const uint4* src0 = reinterpret_cast<const uint4*>(wv->blob);
+        const uint4* src1 = reinterpret_cast<const uint4*>(wv->blob + wv->off_aos);
+        uint4* dst = reinterpret_cast<uint4*>(lds);
+        for (uint32_t o = threadIdx.x; o < front_bytes / 16; o += BLOCK) dst[o] = src0[o];
+        uint4* dst1 = reinterpret_cast<uint4*>(lds + front_bytes);
+        for (uint32_t o = threadIdx.x; o < rec_bytes / 16; o += BLOCK) dst1[o] = src1[o];
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // per wave: queue[kQueueM], count, flags[64] (bytes), heads[64] (u32)
+    constexpr uint32_t kWaveBytes = (kQueueM + 1) * 4 + 64 + 256;
+    unsigned char* wbase = lds + front_bytes + rec_bytes + wave * kWaveBytes;
+    uint32_t* queue = reinterpret_cast<uint32_t*>(wbase);
+    uint32_t* qcount = queue + kQueueM;
+    uint8_t* flags = wbase + (kQueueM + 1) * 4;
+    uint32_t* heads = reinterpret_cast<uint32_t*>(wbase + (kQueueM + 1) * 4 + 64);
+    float4* filt = reinterpret_cast<float4*>(lds + front_bytes + rec_bytes + (BLOCK / 64) * kWaveBytes);
+    const uint32_t* cs = reinterpret_cast<const uint32_t*>(lds + wv->off_cell_start);
+    const uint16_t* co = reinterpret_cast<const uint16_t*>(lds + wv->off_cell_obb);
+    const double* recs = reinterpret_cast<const double*>(lds + front_bytes);
+    __syncthreads();  // records staged
+    for (int o = threadIdx.x; o < wv->n_obb; o += BLOCK) {
+        const double* r = recs + (size_t)o * kRecDoubles;
+        filt[2 * o] = make_float4(__double2float_rd(r[F_LOX]), __double2float_rd(r[F_LOY]), __double2float_rd(r[F_LOZ]),
+                                  __uint_as_float((uint32_t)__double_as_longlong(r[R_META])));
+        filt[2 * o + 1] = make_float4(__double2float_ru(r[F_HIX]), __double2float_ru(r[F_HIY]),
+                                      __double2float_ru(r[F_HIZ]), 0.0f);
+    }
+    const int nx = wv->nx, ny = wv->ny, nz = wv->nz;
+    const double gx0 = wv->gx0, gy0 = wv->gy0, gz0 = wv->gz0, gx1 = wv->gx1, gy1 = wv->gy1, gz1 = wv->gz1;
+    const float ofx = wv->ofx, ofy = wv->ofy, ofz = wv->ofz, i4x = wv->i4x, i4y = wv->i4y, i4z = wv->i4z;
+    const double rg = wv->r_gate, ro = wv->r_obst;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * BLOCK;
+    for (int64_t i0 = (int64_t)blockIdx.x * BLOCK + wave * 64; i0 < n; i0 += stride) {
+        const int64_t i = i0 + lane;
+        const bool act = i < n;
+        double s[3] = {0.0, 0.0, 0.0}, e[3] = {0.0, 0.0, 0.0};
+        if (act) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                s[k] = s1[3 * i + k];
+                e[k] = s2[3 * i + k];
+            }
+        }
+        if (lane == 0) *qcount = 0u;
+        flags[lane] = 1;
+        double lo[3], hi[3];
+        float flo[3], fhi[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = (e[k] < s[k]) ? e[k] : s[k];
+            hi[k] = (s[k] < e[k]) ? e[k] : s[k];
+            flo[k] = __double2float_rd(lo[k]);
+            fhi[k] = __double2float_ru(hi[k]);
+        }
+        // World::checkRayValid — rtree intersects(rayBox): closed AABB overlap with the grid
+        const bool in = act && !(hi[0] < gx0 || gx1 < lo[0] || hi[1] < gy0 || gy1 < lo[1] || hi[2] < gz0 || gz1 < lo[2]);
+        const int x0 = fine_index(fine_coord(lo[0], ofx, i4x), nx) >> 2;
+        const int x1 = fine_index(fine_coord(hi[0], ofx, i4x), nx) >> 2;
+        const int y0 = fine_index(fine_coord(lo[1], ofy, i4y), ny) >> 2;
+        const int y1 = fine_index(fine_coord(hi[1], ofy, i4y), ny) >> 2;
+        const int z0 = fine_index(fine_coord(lo[2], ofz, i4z), nz) >> 2;
+        const int z1 = fine_index(fine_coord(hi[2], ofz, i4z), nz) >> 2;
+        const uint32_t wx = (uint32_t)(x1 - x0 + 1), wy = (uint32_t)(y1 - y0 + 1);
+        const uint32_t nc = in ? wx * wy * (uint32_t)(z1 - z0 + 1) : 0u;
+        const uint32_t box0 = (uint32_t)x0 | ((uint32_t)y0 << 8) | ((uint32_t)z0 << 16);
+        const uint32_t boxw = wx | (wy << 8);
+        uint32_t total_c;
+        const uint32_t offc = wave_excl_scan(nc, lane, total_c);
+        wave_lds_sync();
+
+        // exact tests of the queued pairs (wave-uniform call sites only)
+        auto flush = [&]() {
+            const uint32_t total = *qcount;
+            for (uint32_t base = 0; base < total; base += 64) {
+                const uint32_t j = base + lane;
+                const bool has = j < total;
+                const uint32_t q = has ? queue[j] : 0u;
+                const int owner = (int)(q & 63u);
+                double ps[3], pe[3];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    ps[k] = __shfl(s[k], owner);
+                    pe[k] = __shfl(e[k], owner);
+                }
+                if (has) {
+                    const double* rec = recs + (size_t)(q >> 6) * kRecDoubles;
+                    const uint32_t m = (uint32_t)__double_as_longlong(rec[R_META]);
+                    double plo[3], phi[3];
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        plo[k] = (pe[k] < ps[k]) ? pe[k] : ps[k];
+                        phi[k] = (ps[k] < pe[k]) ? pe[k] : ps[k];
+                    }
+                    const bool overlap = !((rec[F_HIX] < plo[0]) | (phi[0] < rec[F_LOX]) | (rec[F_HIY] < plo[1]) |
+                                           (phi[1] < rec[F_LOY]) | (rec[F_HIZ] < plo[2]) | (phi[2] < rec[F_LOZ]));
+                    if (overlap && rec_ray_hit(rec, ps, pe, (m & META_GATE) ? rg : ro)) flags[owner] = 0;
+                }
+            }
+            wave_lds_sync();
+            if (lane == 0) *qcount = 0u;
+            wave_lds_sync();
+        };
+
+        uint32_t carry_owner = 0u;
+        for (uint32_t cb = 0; cb < total_c; cb += 64) {
+            // level 1: lane -> (owner edge, cell)
+            heads[lane] = 0u;
+            wave_lds_sync();
+            if (nc > 0u && offc >= cb && offc < cb + 64u) heads[offc - cb] = (uint32_t)lane + 1u;
+            wave_lds_sync();
+            const uint32_t hm = dpp_incl_max(heads[lane]);
+            const uint32_t owner = hm ? hm - 1u : carry_owner;
+            carry_owner = (uint32_t)__builtin_amdgcn_readlane((int)owner, 63);
+            const bool has_c = cb + (uint32_t)lane < total_c;
+            const uint32_t ooff = (uint32_t)__shfl((int)offc, (int)owner);
+            const uint32_t ob = (uint32_t)__shfl((int)box0, (int)owner);
+            const uint32_t ow = (uint32_t)__shfl((int)boxw, (int)owner);
+            const uint32_t c = cb + (uint32_t)lane - ooff;
+            const uint32_t owx = ow & 255u, owy = ow >> 8;
+            const uint32_t cx = c % owx, t = c / owx, cy = t % owy, cz = t / owy;
+            const uint32_t x = (ob & 255u) + cx, y = ((ob >> 8) & 255u) + cy, z = (ob >> 16) + cz;
+            const int cell = ((int)z * ny + (int)y) * nx + (int)x;
+            const uint32_t b = has_c ? cs[cell] : 0u;
+            const uint32_t len = has_c ? cs[cell + 1] - b : 0u;
+            const uint32_t seg = x | (y << 8) | (z << 16) | (owner << 24);
+            uint32_t total_e;
+            const uint32_t offe = wave_excl_scan(len, lane, total_e);
+            // level 2: lane -> (segment, list entry)
+            uint32_t carry_s = 0u;
+            for (uint32_t eb = 0; eb < total_e; eb += 64) {
+                if (*qcount > (uint32_t)(kQueueM - 64)) flush();
+                heads[lane] = 0u;
+                wave_lds_sync();
+                if (len > 0u && offe >= eb && offe < eb + 64u) heads[offe - eb] = (uint32_t)lane + 1u;
+                wave_lds_sync();
+                const uint32_t hs = dpp_incl_max(heads[lane]);
+                const uint32_t sidx = hs ? hs - 1u : carry_s;
+                carry_s = (uint32_t)__builtin_amdgcn_readlane((int)sidx, 63);
+                const bool has = eb + (uint32_t)lane < total_e;
+                const uint32_t sb = (uint32_t)__shfl((int)b, (int)sidx);
+                const uint32_t soff = (uint32_t)__shfl((int)offe, (int)sidx);
+                const uint32_t sp = (uint32_t)__shfl((int)seg, (int)sidx);
+                const int own = (int)(sp >> 24);
+                const uint32_t obox = (uint32_t)__shfl((int)box0, own);
+                float ol[3], oh[3];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    ol[k] = __shfl(flo[k], own);
+                    oh[k] = __shfl(fhi[k], own);
+                }
+                if (has) {
+                    const uint32_t id = co[sb + (eb + (uint32_t)lane - soff)];
+                    const float4 fa = filt[2 * id], fb = filt[2 * id + 1];
+                    const uint32_t m = __float_as_uint(fa.w);
+                    const uint32_t ox = (m >> 8) & 255u, oy = (m >> 16) & 255u, oz = m >> 24;
+                    const uint32_t ex0 = obox & 255u, ey0 = (obox >> 8) & 255u, ez0 = obox >> 16;
+                    const bool first = ((sp & 255u) == max(ox, ex0)) & (((sp >> 8) & 255u) == max(oy, ey0)) &
+                                       (((sp >> 16) & 255u) == max(oz, ez0));
+                    const bool may = !((fb.x < ol[0]) | (oh[0] < fa.x) | (fb.y < ol[1]) | (oh[1] < fa.y) |
+                                       (fb.z < ol[2]) | (oh[2] < fa.z));
+                    const bool skip = (m & META_FILLING) && can_pass;  // :150-153
+                    if (first & may & !skip) {
+                        const uint32_t slot = atomicAdd(qcount, 1u);
+                        queue[slot] = (id << 6) | (uint32_t)own;
+                    }
+                }
+                wave_lds_sync();
+            }
+        }
+        flush();
+        if (act) valid[i] = flags[lane] ? 1 : 0;
+        wave_lds_sync();
+    }
+}
+
+constexpr int kQueueD32 = 512;
+constexpr uint32_t kFlushD32 = 256;
+
+// ---- k_motions_d32b: discrete32, lane-balanced list walk ------------------------------
+// As k_motions_d32q (wave-uniform steps k = 1..32, queued (lane, k, OBB) triples, the
+// exact OBB::checkCollisionWithPoint on flush), but at each step the occupied lanes'
+// cell lists are expanded over the whole wave (exclusive scan of the list lengths,
+// segment heads, DPP max-scan) instead of each lane walking its own list: the wave pays
+// ceil(sum of lengths / 64) rounds instead of the longest list.  The entry filter is the
+// rtree `contains` (src/World.cpp:83) against the outward-rounded float AABB (a superset
+// of the strict double test, which rec_hit repeats).  The queue is flushed before it
+// could overflow.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_motions_d32b(const WorldView* __restrict__ wv,
+                                                        const double* __restrict__ s1, const double* __restrict__ s2,
+                                                        int64_t n, int can_pass, uint8_t* __restrict__ valid,
+                                                        uint32_t front_bytes, uint32_t rec_bytes) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    {
+        const uint4* src0 = reinterpret_cast<const uint4*>(wv->blob);
+        const uint4* src1 = reinterpret_cast<const uint4*>(wv->blob + wv->off_aos);
+        uint4* dst = reinterpret_cast<uint4*>(lds);
+        for (uint32_t o = threadIdx.x; o < front_bytes / 16; o += BLOCK) dst[o] = src0[o];
+        uint4* dst1 = reinterpret_cast<uint4*>(lds + front_bytes);
+        for (uint32_t o = threadIdx.x; o < rec_bytes / 16; o += BLOCK) dst1[o] = src1[o];
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    constexpr uint32_t kWaveBytes = (kQueueD32 + 1) * 4 + 64 + 256;
+    unsigned char* wbase = lds + front_bytes + rec_bytes + wave * kWaveBytes;
+    uint32_t* queue = reinterpret_cast<uint32_t*>(wbase);
+    uint32_t* qcount = queue + kQueueD32;
+    uint8_t* flags = wbase + (kQueueD32 + 1) * 4;
+    uint32_t* heads = reinterpret_cast<uint32_t*>(wbase + (kQueueD32 + 1) * 4 + 64);
+    float4* filt = reinterpret_cast<float4*>(lds + front_bytes + rec_bytes + (BLOCK / 64) * kWaveBytes);
+    const unsigned long long* mask = reinterpret_cast<const unsigned long long*>(lds + wv->off_cell_mask);
+    const uint32_t* cs = reinterpret_cast<const uint32_t*>(lds + wv->off_cell_start);
+    const uint16_t* co = reinterpret_cast<const uint16_t*>(lds + wv->off_cell_obb);
+    const double* recs = reinterpret_cast<const double*>(lds + front_bytes);
+    __syncthreads();  // records staged
+    for (int o = threadIdx.x; o < wv->n_obb; o += BLOCK) {
+        const double* r = recs + (size_t)o * kRecDoubles;
+        filt[2 * o] = make_float4(__double2float_rd(r[F_LOX]), __double2float_rd(r[F_LOY]), __double2float_rd(r[F_LOZ]),
+                                  0.0f);
+        filt[2 * o + 1] = make_float4(__double2float_ru(r[F_HIX]), __double2float_ru(r[F_HIY]),
+                                      __double2float_ru(r[F_HIZ]), 0.0f);
+    }
+    const int nx = wv->nx, ny = wv->ny;
+    const float ofx = wv->ofx, ofy = wv->ofy, ofz = wv->ofz, i4x = wv->i4x, i4y = wv->i4y, i4z = wv->i4z;
+    const float limx = wv->limx, limy = wv->limy, limz = wv->limz;
+    const float fmx = wv->fmaxx, fmy = wv->fmaxy, fmz = wv->fmaxz;
+    const double rg = wv->r_gate, ro = wv->r_obst;
+    const bool cp = can_pass != 0;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * BLOCK;
+    for (int64_t i0 = (int64_t)blockIdx.x * BLOCK + wave * 64; i0 < n; i0 += stride) {
+        const int64_t i = i0 + lane;
+        const bool act = i < n;
+        double s[3] = {0.0, 0.0, 0.0}, e[3] = {0.0, 0.0, 0.0};
+        if (act) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                s[k] = s1[3 * i + k];
+                e[k] = s2[3 * i + k];
+            }
+        }
+        if (lane == 0) *qcount = 0u;
+        flags[lane] = act ? 1 : 0;
+        wave_lds_sync();
+        auto flush = [&]() {
+            const uint32_t total = *qcount;
+            for (uint32_t base = 0; base < total; base += 64) {
+                const uint32_t j = base + lane;
+                const bool has = j < total;
+                const uint32_t qe = has ? queue[j] : 0u;
+                const int owner = (int)(qe & 63u);
+                double ps[3], pe[3];
+#pragma unroll
+                for (int d = 0; d < 3; ++d) {
+                    ps[d] = __shfl(s[d], owner);
+                    pe[d] = __shfl(e[d], owner);
+                }
+                if (has) {
+                    const double tq = (double)(((qe >> 6) & 31u) + 1u) / 32.0;
+                    const double qx = ps[0] + (pe[0] - ps[0]) * tq;
+                    const double qy = ps[1] + (pe[1] - ps[1]) * tq;
+                    const double qz = ps[2] + (pe[2] - ps[2]) * tq;
+                    if (rec_hit<false>(recs + (size_t)(qe >> 11) * kRecDoubles, rg, ro, qx, qy, qz, cp, 0.0))
+                        flags[owner] = 0;
+                }
+            }
+            wave_lds_sync();
+            if (lane == 0) *qcount = 0u;
+            wave_lds_sync();
+        };
+        for (int k = 1; k <= 32; ++k) {
+            const double t = (double)k / 32.0;
+            const double px = s[0] + (e[0] - s[0]) * t;
+            const double py = s[1] + (e[1] - s[1]) * t;
+            const double pz = s[2] + (e[2] - s[2]) * t;
+            const float fx = fine_coord(px, ofx, i4x), fy = fine_coord(py, ofy, i4y), fz = fine_coord(pz, ofz, i4z);
+            const bool in = (fx >= 0.0f) & (fx <= limx) & (fy >= 0.0f) & (fy <= limy) & (fz >= 0.0f) & (fz <= limz);
+            const int ix = (int)fminf(fmaxf(fx, 0.0f), fmx);
+            const int iy = (int)fminf(fmaxf(fy, 0.0f), fmy);
+            const int iz = (int)fminf(fmaxf(fz, 0.0f), fmz);
+            const int cell = ((iz >> 2) * ny + (iy >> 2)) * nx + (ix >> 2);
+            const uint32_t bit = (uint32_t)((((iz & 3) << 2) + (iy & 3)) * 4 + (ix & 3));
+            const bool live = flags[lane] != 0;
+            const bool occ = live && in && ((mask[cell] >> bit) & 1ull);
+            const uint32_t b = occ ? cs[cell] : 0u;
+            const uint32_t len = occ ? cs[cell + 1] - b : 0u;
+            uint32_t total_e;
+            const uint32_t offe = wave_excl_scan(len, lane, total_e);
+            uint32_t carry_s = 0u;
+            for (uint32_t eb = 0; eb < total_e; eb += 64) {
+                if (*qcount > (uint32_t)(kQueueD32 - 64)) flush();
+                heads[lane] = 0u;
+                wave_lds_sync();
+                if (len > 0u && offe >= eb && offe < eb + 64u) heads[offe - eb] = (uint32_t)lane + 1u;
+                wave_lds_sync();
+                const uint32_t hs = dpp_incl_max(heads[lane]);
+                const uint32_t own = hs ? hs - 1u : carry_s;
+                carry_s = (uint32_t)__builtin_amdgcn_readlane((int)own, 63);
+                const bool has = eb + (uint32_t)lane < total_e;
+                const uint32_t sb = (uint32_t)__shfl((int)b, (int)own);
+                const uint32_t soff = (uint32_t)__shfl((int)offe, (int)own);
+                const double qx = __shfl(px, (int)own), qy = __shfl(py, (int)own), qz = __shfl(pz, (int)own);
+                if (has) {
+                    const uint32_t id = co[sb + (eb + (uint32_t)lane - soff)];
+                    const float4 fa = filt[2 * id], fb = filt[2 * id + 1];
+                    const bool may = ((double)fa.x < qx) & (qx < (double)fb.x) & ((double)fa.y < qy) &
+                                     (qy < (double)fb.y) & ((double)fa.z < qz) & (qz < (double)fb.z);
+                    if (may) {
+                        const uint32_t slot = atomicAdd(qcount, 1u);
+                        queue[slot] = (id << 11) | ((uint32_t)(k - 1) << 6) | own;
+                    }
+                }
+                wave_lds_sync();
+            }
+            if (*qcount >= kFlushD32) flush();
+        }
+        flush();
+        if (act) valid[i] = flags[lane] ? 1 : 0;
+        wave_lds_sync();
+    }
+}
+
+}  // namespace
+}  // namespace epp
+
+using namespace epp;
+
+extern "C" {
+
+// Kernel choice: the LDS kernels (k_motions_v4 analytic, k_motions_d32b discrete32) when the
+// coarse grid, the records and the wave queues fit a CU's LDS, else k_motions.  Test hooks
+// (not for production use): EPP_MOTIONS_KERNEL=generic forces k_motions, EPP_MOTIONS_BLOCK =
+// 512 | 1024 forces the LDS kernels' workgroup size.
+epp_status epp_check_motions(const epp_world* world, const double* s1, const double* s2, int64_t n,
+                             int32_t can_pass_gate, int32_t mode, uint8_t* valid, void* stream) {
+    if (!world || n < 0 || (n > 0 && (!s1 || !s2 || !valid)) || (mode != 0 && mode != 1)) {
+        set_error("epp_check_motions: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    if (n == 0) return EPP_OK;
+    const WorldView& w = world_view(world);
+    hipStream_t st = (hipStream_t)stream;
+    const char* forced = std::getenv("EPP_MOTIONS_KERNEL");
+    const bool generic = forced && std::string(forced) == "generic";
+    // LDS: coarse grid + lists (blob up to `meta`), the records, per-wave queue/flags/heads,
+    // and a 32-byte float filter record per OBB
+    const uint32_t front = w.off_meta;
+    const uint32_t recb = (uint32_t)(((size_t)w.n_obb * kRecDoubles * 8 + 15) & ~size_t(15));
+    auto extra_for = [&](int blk) -> uint32_t {
+        const uint32_t q = mode == 0 ? (uint32_t)kQueueM : (uint32_t)kQueueD32;
+        return (uint32_t)((blk / 64) * ((q + 1) * 4 + 64 + 256) + (uint32_t)w.n_obb * 32u);
+    };
+    // Block size: 512 threads when two such blocks fit a CU's LDS (small worlds: C4's 64
+    // OBBs, v4 28 vs 32 us per 1M edges), else 1024 (C3's 512 OBBs stage ~95 KB, one block
+    // per CU, and 1024 threads double the waves behind the LDS walk: v4 52 vs 69 us)
+    const int eb = env_int("EPP_MOTIONS_BLOCK", 0);
+    const int block = eb == 512 ? 512 : eb == 1024 ? 1024 : (2u * (front + recb + extra_for(512)) <= 160u * 1024u ? 512 : 1024);
+    const uint32_t shm = front + recb + extra_for(block);
+    if (!generic && front % 16 == 0 && shm <= 160u * 1024u) {
+        const int grid = (int)std::max<int64_t>(
+            1, std::min<int64_t>((n + block - 1) / block, (int64_t)cu_count() * std::max(1, (int)((160u * 1024u) / shm))));
+        const WorldView* dw = world_dview(world);
+#define EPP_LAUNCH_M(KERNEL)                                                                                           \
+    do {                                                                                                               \
+        allow_lds(KERNEL);                                                                                             \
+        hipLaunchKernelGGL(KERNEL, dim3(grid), dim3(block), shm, st, dw, s1, s2, n, can_pass_gate, valid, front, recb); \
+    } while (0)
+        if (mode == 0) {
+            if (block == 1024) EPP_LAUNCH_M((k_motions_v4<1024>));
+            else EPP_LAUNCH_M((k_motions_v4<512>));
+        } else {
+            if (block == 1024) EPP_LAUNCH_M((k_motions_d32b<1024>));
+            else EPP_LAUNCH_M((k_motions_d32b<512>));
+        }
+#undef EPP_LAUNCH_M
+        return launch_error("epp_check_motions");
+    }
+    const int aligned = ((reinterpret_cast<uintptr_t>(s1) | reinterpret_cast<uintptr_t>(s2)) & 15) == 0;
+    const int grid = grid_for((n + 3) / 4, 0);
+    if (mode == 0)
+        hipLaunchKernelGGL((k_motions<0>), dim3(grid), dim3(kBlock), 0, st, w, s1, s2, n, can_pass_gate, valid, aligned);
+    else
+        hipLaunchKernelGGL((k_motions<1>), dim3(grid), dim3(kBlock), 0, st, w, s1, s2, n, can_pass_gate, valid, aligned);
+    return launch_error("epp_check_motions");
+}
+
+}  // extern "C"

@@ -154,10 +154,9 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
     std::vector<uint16_t> cls;
     std::vector<uint32_t> hdr;    // per list: start << 12 | count
     std::vector<uint16_t> flat;   // the lists' OBB ids
-    const char* env_bits = std::getenv("EPP_BITMAP_BITS");
-    double setenv_target = env_bits && *env_bits ? std::max(64.0, std::atof(env_bits)) : double(1 << 14);
+    double cls_target = double(1 << 14);  // fine cells to start from (coarsened below if needed)
     for (;;) {
-        const double target = setenv_target;
+        const double target = cls_target;
         int bd[3] = {1, 1, 1};
         float bo[3] = {0, 0, 0}, bi[3] = {1, 1, 1};
         if (n > 0) {
@@ -227,15 +226,15 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
                 set_error("epp_world: candidate list table overflow");
                 return false;
             }
-            setenv_target = target / 8;
+            cls_target = target / 8;
             continue;
         }
         // k_states_v5 stages records + lists + class table into LDS: keep that part
         // within kStageBudget by coarsening the class grid (down to 4096 cells)
         const size_t staged = align16((size_t)n * kRecDoubles * 8) + align16(hdr.size() * 4 + flat.size() * 2) +
                               align16(cls.size() * 2);
-        if (!env_bits && staged > kStageBudget && target > 4096.0) {
-            setenv_target = target / 2;
+        if (staged > kStageBudget && target > 4096.0) {
+            cls_target = target / 2;
             continue;
         }
         v.bnx = bd[0]; v.bny = bd[1]; v.bnz = bd[2];
@@ -399,7 +398,7 @@ epp_status epp_world_get_aabbs(const epp_world* w, double* lo_hi) {
 
 }  // extern "C"
 
-// Accessor for the kernels' launchers (collision.hip).
+// Accessor for the kernels' launchers (states.hip, motions.hip, planner.hip).
 namespace epp {
 const WorldView& world_view(const epp_world* w) { return w->view; }
 const WorldView* world_dview(const epp_world* w) { return w->d_view; }

@@ -7,6 +7,9 @@ code on CPU tensors (used by the world_size-2 tests in this container).
 from __future__ import annotations
 
 import os
+import socket
+import subprocess
+import sys
 
 import numpy as np
 
@@ -15,6 +18,32 @@ def env():
     """(world_size, rank, local_rank) from the torchrun environment."""
     return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
             int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: list[str], extra_env: dict | None = None) -> int:
+    """Runs `argv` as n processes, one per GPU of this node (RANK = LOCAL_RANK = i,
+    WORLD_SIZE = n, rendezvous on 127.0.0.1), and returns the first non-zero exit code
+    (0 if every rank succeeded).  The caller must not have initialised the GPU: the
+    children each bind their own device."""
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        e = dict(os.environ)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                  "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": port})
+        e.update(extra_env or {})
+        procs.append(subprocess.Popen(argv, env=e))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        print(f"spawn_ranks: exit codes {rcs}", file=sys.stderr)
+    return bad[0] if bad else 0
 
 
 class Dist:

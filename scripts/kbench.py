@@ -58,6 +58,9 @@ def main():
         res[name] = {"us": ms * 1e3, "GBs": 25 * N / (ms * 1e-3) / 1e9}
         print(name, res[name], flush=True)
 
+    if not os.path.exists(os.path.join(ROOT, "scripts", "libdiag.so")):
+        os.system(f"/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -shared -fPIC -o {ROOT}/scripts/libdiag.so "
+                  f"{ROOT}/scripts/diag_stream.hip")
     diag = C.CDLL(os.path.join(ROOT, "scripts", "libdiag.so"))
     diag.diag_stream.argtypes = [C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_void_p]
     dbig = capi.DeviceBuffer(NB * N)
@@ -86,33 +89,13 @@ def main():
         res[name] = {"us": ms * 1e3, "GBs": 25 * NB * N / (ms * 1e-3) / 1e9}
         print(name, res[name], flush=True)
 
-    for impl in (0, 1, 3, 4, 5):
-        e = {"EPP_STATES_IMPL": impl}
-        run(f"c2_impl{impl}", w2, d, e)
-        big(f"c2_impl{impl}_16M", w2, e)
-        run(f"c2_impl{impl}_empty_world", w0, d, e)
-    run("c2_impl5_spl8", w2, d, {"EPP_STATES_IMPL": 5, "EPP_V5_SPL": 8})
-    run("c2_impl5_b512", w2, d, {"EPP_STATES_IMPL": 5, "EPP_V5_BLOCK": 512})
-    big("c2_impl5_b1024_16M", w2, {"EPP_STATES_IMPL": 5, "EPP_V5_BLOCK": 1024})
-    run("c2_impl5_b256", w2, d, {"EPP_STATES_IMPL": 5, "EPP_V5_BLOCK": 256})
-    big("c2_impl5_b256_16M", w2, {"EPP_STATES_IMPL": 5, "EPP_V5_BLOCK": 256})
-    run("c2_impl5_ablate_exact", w2, d, {"EPP_STATES_IMPL": 5, "EPP_V5_PAIRS": 2})
-    big("c2_impl5_ablate_exact_16M", w2, {"EPP_STATES_IMPL": 5, "EPP_V5_PAIRS": 2})
-    run("c2_impl5_walk", w2, d, {"EPP_STATES_IMPL": 5, "EPP_V5_PAIRS": 0})
-    big("c2_impl5_walk_16M", w2, {"EPP_STATES_IMPL": 5, "EPP_V5_PAIRS": 0})
-    for impl in (3, 4):
-        for k in (3,):
-            e = {"EPP_STATES_IMPL": impl, "EPP_WG_PER_CU": k}
-            run(f"c2_impl{impl}_wg_per_cu_{k}", w2, d, e)
-            big(f"c2_impl{impl}_wg_per_cu_{k}_16M", w2, e)
-    for bits in (1 << 12, 1 << 14, 1 << 15):
-        os.environ["EPP_BITMAP_BITS"] = str(bits)
-        wb = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
-        del os.environ["EPP_BITMAP_BITS"]
-        for impl in (4, 5):
-            run(f"c2_impl{impl}_cells_{bits}", wb, d, {"EPP_STATES_IMPL": impl})
-            big(f"c2_impl{impl}_cells_{bits}_16M", wb, {"EPP_STATES_IMPL": impl})
-        wb.close()
+    for kern in ("v5", "v4", "generic"):
+        e = {"EPP_STATES_KERNEL": kern}
+        run(f"c2_{kern}", w2, d, e)
+        big(f"c2_{kern}_16M", w2, e)
+        run(f"c2_{kern}_empty_world", w0, d, e)
+    run("c2_v5_b1024", w2, d, {"EPP_V5_BLOCK": 1024})
+    big("c2_v5_b1024_16M", w2, {"EPP_V5_BLOCK": 1024})
     # motions, C3
     g3, o3 = synth.track_world(42, n_obstacles=472)
     w3 = capi.World(capi.build_obbs(geom, g3, o3), rg, ro)

@@ -54,3 +54,32 @@ def test_all_gather_waypoints_gloo_ws2():
             exp = np.arange(3 * (4 + 3 * r), dtype=np.float64).reshape(-1, 3) + 100 * r
             assert np.array_equal(np.array(sets[r]), exp)
         assert empty == [0, 7]
+
+
+def test_bench_spawns_ranks_gloo_ws2():
+    """`bench.py --gpus 2` without a launcher spawns one process per rank (RANK/LOCAL_RANK/
+    WORLD_SIZE set before any device call) and reports n_gpus = 2 from rank 0; the
+    --launcher-check mode runs that plumbing with gloo instead of the GPU work."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--launcher-check"],
+                         env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["ranks_seen"] == [0, 1] and r["waypoints_per_track"] == [5, 6]
+    assert r["max_over_ranks"] == 2.0 and r["local_rank"] == 0
+
+
+def test_bench_rejects_mismatched_world_size():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--launcher-check"],
+                         env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr

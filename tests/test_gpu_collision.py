@@ -91,24 +91,22 @@ def test_states_mindist(geom, worlds, name):
         assert np.array_equal(got, exp), md
 
 
-@pytest.mark.parametrize("impl", ["0", "1", "3", "4", "5", "5walk", "5b512", "5b1024", "5spl8"])
+@pytest.mark.parametrize("impl", ["v5", "v5b512", "v5b1024", "v4", "generic"])
 @pytest.mark.parametrize("name", ["c2", "c3"])
 def test_states_every_kernel_variant(geom, worlds, name, impl, monkeypatch):
-    """Each k_states variant (EPP_STATES_IMPL; 5 = default, falls back when its staged
-    world does not fit LDS; "5walk" = v5 with per-state list walks instead of pairs) on
-    plain, compacting and minDistance launches, ragged n.  "5" runs the default launch
-    shape (two 512-thread workgroups per CU for a single pass), "5b512"/"5b1024" force
-    one workgroup shape."""
-    monkeypatch.setenv("EPP_STATES_IMPL", impl[0])
-    monkeypatch.setenv("EPP_V5_PAIRS", "0" if impl.endswith("walk") else "1")
-    monkeypatch.setenv("EPP_V5_BLOCK", "512" if impl.endswith("b512") else ("1024" if impl.endswith("b1024") else ""))
-    monkeypatch.setenv("EPP_V5_SPL", "8" if impl.endswith("spl8") else "4")
-    impl = int(impl[0])
+    """Each state kernel (k_states_v5 = default, k_states_v4 = fallback for worlds whose
+    staged part exceeds LDS, e.g. C3; k_states = generic) on plain, compacting and
+    minDistance launches, ragged n.  "v5" runs the default launch shape (two 512-thread
+    workgroups per CU for a single pass), "v5b512"/"v5b1024" force one workgroup shape
+    (test hooks EPP_STATES_KERNEL / EPP_V5_BLOCK)."""
+    monkeypatch.setenv("EPP_STATES_KERNEL", impl[:2] if impl.startswith("v") else impl)
+    monkeypatch.setenv("EPP_V5_BLOCK", impl[3:] if impl.startswith("v5b") else "")
+    seed = 31 + len(impl)
     rg, ro, ws = worlds
     gates, obstacles, (lo, hi) = ws[name]
     ref = O.world_build(geom, gates, obstacles, rg, ro)
     w = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
-    pts = np.vstack([synth.sample_states(31 + impl, lo, hi, 150_001), _adversarial_points(ref)])
+    pts = np.vstack([synth.sample_states(seed, lo, hi, 150_001), _adversarial_points(ref)])
     exp = O.check_states(ref, rg, ro, pts, False, threads=8)
     assert np.array_equal(w.check_states(pts, False), exp)
     valid, idx = w.check_states(pts, False, compact=True)
@@ -142,17 +140,15 @@ def test_compaction(geom, worlds):
     assert np.array_equal(np.sort(idx), np.flatnonzero(exp))
 
 
-@pytest.mark.parametrize("impl", ["5", "4", "3", "2", "1", "5/512", "4/512", "3/512", "2/512", "5/1024", "4/1024", "3/1024", "2/1024"])
+@pytest.mark.parametrize("impl", ["lds", "lds/512", "lds/1024", "generic"])
 @pytest.mark.parametrize("name", ["c1", "c2", "c3"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_motions_bit_exact(geom, worlds, name, mode, impl, monkeypatch):
-    """impl 5 (default): k_motions_v4 (analytic, lane-balanced walk) + k_motions_d32b
-    (discrete32, lane-balanced); impl 4: v4 + k_motions_d32q; impl 3: k_motions_v3 (analytic per-lane walk), k_motions_v2
-    (LDS-resident) and k_motions (EPP_MOTIONS_IMPL=1) vs the oracle, at the default block
-    size and forced 512/1024-thread blocks; includes edges parallel to an axis within the
-    1e-6 threshold."""
+    """The LDS kernels (k_motions_v4 analytic, k_motions_d32b discrete32) at the default
+    block size and forced 512/1024-thread blocks, and the generic k_motions, vs the
+    oracle; includes edges parallel to an axis within the 1e-6 threshold."""
     impl, _, block = impl.partition("/")
-    monkeypatch.setenv("EPP_MOTIONS_IMPL", impl)
+    monkeypatch.setenv("EPP_MOTIONS_KERNEL", impl)
     monkeypatch.setenv("EPP_MOTIONS_BLOCK", block)  # "" = by LDS fit (the default)
     rg, ro, ws = worlds
     gates, obstacles, (lo, hi) = ws[name]
@@ -175,12 +171,11 @@ def test_motions_bit_exact(geom, worlds, name, mode, impl, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("impl", ["5", "4", "3", "2"])
+@pytest.mark.parametrize("impl", ["lds", "generic"])
 def test_motions_queue_overflow(geom, worlds, impl, mode, monkeypatch):
-    """Long edges through the 512-OBB world: analytic mode overflows the v3 queue (256
-    pairs per wave, overflow lanes test inline); discrete32 flushes its queue many times
-    per wave.  Answers still match the oracle."""
-    monkeypatch.setenv("EPP_MOTIONS_IMPL", impl)
+    """Long edges through the 512-OBB world: both LDS kernels flush their wave queues many
+    times per wave.  Answers still match the oracle."""
+    monkeypatch.setenv("EPP_MOTIONS_KERNEL", impl)
     rg, ro, ws = worlds
     gates, obstacles, (lo, hi) = ws["c3"]
     ref = O.world_build(geom, gates, obstacles, rg, ro)
