@@ -67,7 +67,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)  # ~17 ms timed: host hiccups amortised
     ap.add_argument("--warmup", type=int, default=200)  # ~2 ms of GPU work: clocks settle
-    ap.add_argument("--no-side", action="store_true", help="skip the side measurements")
+    ap.add_argument("--no-side", action="store_true", help="skip the side measurements (C3, C5)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-plan", action="store_true", help="skip the full-plan (C4) leg")
     ap.add_argument("--plan-reps", type=int, default=5)
@@ -105,6 +105,12 @@ def main():
     obbs = capi.build_obbs(geom, gates, obstacles)
     world = capi.World(obbs, rg, ro)
     lo, hi = synth.C2_BOUNDS
+
+    # ---- the metric's second half and the side legs (before the headline's timed region)
+    plan = full_plan(dist, rank, args.plan_reps) if not args.no_plan else None
+    side, c5_inputs = {}, None
+    if not args.no_side and rank == 0:
+        side, c5_inputs = side_measurements(capi, L, stream, geom, cfg, rg, ro)
 
     # ---- resident inputs: 16 fresh 1M-state batches per rank ------------------------
     d_states = capi.DeviceBuffer(N_BATCHES * N_STATES * 24)
@@ -174,19 +180,13 @@ def main():
     achieved = BYTES_PER_STATE * N_STATES / (kms * 1e-3) / 1e9
     n_valid = int(d_valid.download(np.uint8, N_STATES).sum())
 
-    plan = None
-    if not args.no_plan:
-        plan = full_plan(dist, rank, args.plan_reps)
-
     traffic, traffic_src = committed_traffic()
-
-    side = {}
-    if not args.no_side and rank == 0:
-        side = side_measurements(capi, L, stream, geom, cfg, rg, ro)
 
     cpu = None
     if not args.no_cpu and rank == 0 and ws == 1:
-        cpu = cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi)
+        cpu = cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs)
+    if c5_inputs:
+        os.unlink(c5_inputs["cfg_path"])
 
     if rank == 0:
         out = {
@@ -343,21 +343,172 @@ def side_measurements(capi, L, stream, geom, cfg, rg, ro):
     ms = timed_kernel_ms(capi, stream, ms_fn, 10)
     res["c5_minsnap_batch"] = {"problems_per_s": nt / (ms * 1e-3), "ms_per_launch": ms, "problems": nt,
                                "segments": 12}
-    # C5 single refit latency (host buffers in/out, includes sampling at dt=0.1)
+    # C5 single refit latency (host buffers in/out, includes sampling at dt=0.1): the
+    # C++ entry through ctypes, 200 calls
     wp1 = tracks[0]
-    t = time.perf_counter()
-    for _ in range(20):
+    lat = np.zeros(200)
+    for r in range(len(lat)):
+        t = time.perf_counter()
         capi.generate_trajectory(wp1, 1.0, 2.0, 0.1)
-    res["c5_refit_latency_ms"] = (time.perf_counter() - t) / 20 * 1e3
-    return res
+        lat[r] = time.perf_counter() - t
+    res["c5_refit"] = _pct(lat[20:] * 1e6)
+    # C5 online replanning loop (1000 steps of gate update + A11 + refit + sampling)
+    tg = cfg["trajectory_generator_properties"]
+    c5cfg, c5path, c5geom, c5g, c5o, wp, window = c5_setup()
+    lat = c5_online(c5path, c5geom, c5g, c5o, wp, window, tg["max_velocity"], tg["max_acceleration"],
+                    tg["sampling_interval"], cfg["path_planner_properties"]["min_dist_check_traj_collision"])
+    res["c5_online"] = dict(_pct(lat), workload="C5: 1000 steps of gate-pose perturbation (+-0.1 m, +-0.1 rad) -> "
+                            "World update -> A11 check of 100 lookahead rows -> 12-segment min-snap refit (W = 13) "
+                            "-> sampling at dt = 0.1", waypoints=int(len(wp)), window_gates=[g for g, _ in window])
+    # the same loop's inputs for the CPU leg
+    c5_inputs = dict(cfg_path=c5path, geom=c5geom, gates=c5g, obstacles=c5o, wp=wp, window=window,
+                     vmax=tg["max_velocity"], amax=tg["max_acceleration"], dt=tg["sampling_interval"],
+                     md=cfg["path_planner_properties"]["min_dist_check_traj_collision"])
+    return res, c5_inputs
 
 
-def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi):
-    """CPU oracle (a port of the reference's World semantics, 1 thread like OMPL's
-    one-query-at-a-time plugin calls) on a bounded sample of the same workload."""
+C5_STEPS = 1000
+
+
+def _track_config(samples=PLAN_SAMPLES):
+    """configs/config.json with the C2/C4 track bounds [-6,6]^2 x [0,2] (a temp file)."""
+    import tempfile
+
+    from eppamd import config
+    cfg = config.load(os.path.join(ROOT, "configs", "config.json"))
+    cfg["world_properties"]["lower_bound"] = [-6, -6, 0]
+    cfg["world_properties"]["upper_bound"] = [6, 6, 2]
+    cfg["path_planner_properties"]["samples_fmt"] = samples
+    fd, path = tempfile.mkstemp(suffix=".json")
+    with os.fdopen(fd, "w") as f:
+        json.dump(cfg, f)
+    return cfg, path
+
+
+def c5_setup(seed=42):
+    """The C5 track: the C2 world (8 gates, 24 obstacles), planned once end to end; the
+    refit window is its first 13 waypoints (12 segments), which include the centres of the
+    first gates (includeGates2 inserts them)."""
+    import online_traj_planner as otp
+    from eppamd import config, synth
+    cfg, path = _track_config()
+    geom = config.geometry(cfg)
+    gates, obstacles = synth.track_world(seed)
+    cps = synth.gate_checkpoints(gates, geom.gate_height, 0.55)
+    otg = otp.OnlineTrajGenerator(cps[0], cps[-1], gates, obstacles, path)
+    otg.pre_compute_traj(0.0)
+    wp = np.ascontiguousarray(otg.get_waypoints()[:13])
+    centres = gates[:, :3] + np.stack([np.zeros(len(gates)), np.zeros(len(gates)),
+                                       geom.gate_height[gates[:, 6].astype(int)]], 1)
+    window = []  # (gate, waypoint index) of the gates whose centre is a window waypoint
+    for g, c in enumerate(centres):
+        d = np.linalg.norm(wp - c, axis=1)
+        if d.min() < 1e-9:
+            window.append((g, int(d.argmin())))
+    return cfg, path, geom, gates, obstacles, wp, window
+
+
+def c5_online(cfg_path, geom, gates, obstacles, wp, window, vmax, amax, dt, md, steps=C5_STEPS, cpu=False):
+    """C5 (BASELINE configs[4]): the 50 Hz online replanning step, `steps` times.  Per
+    step: one window gate gets a perturbed pose (+-0.1 m in x, y; +-0.1 rad yaw around its
+    nominal pose) -> World update (World::updateGatePosition, src/World.cpp:20-27) -> A11
+    re-check of the 100 lookahead rows (PathPlanner::checkTrajectoryValidity with
+    min_dist_check_traj_collision, src/PathPlanner.cpp:267-280) -> 12-segment min-snap refit
+    (W = 13, the gate's centre waypoint moved) from the current state -> sampled at dt
+    (poly_traj::generateTrajectory).  The GPU step runs the product (PathPlanner /
+    polynomial_trajectory modules); cpu=True runs the same step on the CPU oracle (world
+    rebuild, minDistance check, min-snap + sampling).  Returns per-step microseconds."""
+    rs = np.random.RandomState(5)
+    gates = np.array(gates, float)
+    perturb = [(window[s % len(window)], rs.uniform(-0.1, 0.1, 3)) for s in range(steps)]
+    v0, a0 = np.array([0.4, -0.2, 0.1]), np.array([0.0, 0.3, 0.0])
+    lat = np.zeros(steps)
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        rg, ro = float(cfg_json(cfg_path)["world_properties"]["inflate_radius"]["gate"]), \
+            float(cfg_json(cfg_path)["world_properties"]["inflate_radius"]["obstacle"])
+        rows = O.generate_trajectory(wp, vmax, amax, dt, 0.0, v0, a0)
+        for s, ((g, wi), d) in enumerate(perturb):
+            t = time.perf_counter()
+            gs = gates.copy()
+            gs[g, 0] += d[0]
+            gs[g, 1] += d[1]
+            gs[g, 5] += d[2]
+            w = O.world_build(geom, gs, obstacles, rg, ro)
+            O.check_states_mindist(w, rows[:100][:, [0, 3, 6]], md)
+            wp2 = wp.copy()
+            wp2[wi, :2] = gs[g, :2]
+            rows = O.generate_trajectory(wp2, vmax, amax, dt, 0.0, v0, a0)
+            lat[s] = time.perf_counter() - t
+        return lat * 1e6
+    import online_traj_planner as otp
+    import polynomial_trajectory as pt
+    pp = otp.PathPlanner(gates, obstacles, cfg_path)
+    rows = pt.generate_trajectory(wp, vmax, amax, dt, 0.0, v0, a0)
+    pp.check_trajectory_validity(rows[:100], md)  # first upload of the world
+    for s, ((g, wi), d) in enumerate(perturb):
+        t = time.perf_counter()
+        pose = gates[g, :6].copy()
+        pose[0] += d[0]
+        pose[1] += d[1]
+        pose[5] += d[2]
+        pp.update_gate_pos(g, pose)
+        pp.check_trajectory_validity(rows[:100], md)
+        wp2 = wp.copy()
+        wp2[wi, :2] = pose[:2]
+        rows = pt.generate_trajectory(wp2, vmax, amax, dt, 0.0, v0, a0)
+        lat[s] = time.perf_counter() - t
+    return lat * 1e6
+
+
+def cfg_json(path):
+    with open(path) as f:
+        return json.load(f)
+
+
+def _pct(lat):
+    return {"p50_us": float(np.percentile(lat, 50)), "p99_us": float(np.percentile(lat, 99)),
+            "mean_us": float(lat.mean()), "steps": int(len(lat))}
+
+
+def host_info():
+    """The host the CPU legs ran on: logical CPUs of the machine, the CPUs this process
+    may run on, and the CPU model (/proc/cpuinfo, as lscpu reports it)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count()
+    return {"nproc": os.cpu_count(), "affinity_cpus": affinity, "cpu_model": model}
+
+
+# host threads for the all-cores legs: the box's CPU share of one GPU (16; the machine
+# reports more logical CPUs than a one-GPU job may use)
+CPU_SHARE_THREADS = 16
+
+
+def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None):
+    """The CPU oracle (a port of the reference's World / min-snap semantics, kind "port") on
+    bounded samples of the same workloads, ~15 s in total:
+
+    * value: state validity checks/s on 1 thread (OMPL calls the plugins one query at a
+      time) over the C2 batch; all_cores_value: the same on CPU_SHARE_THREADS threads;
+    * c3_*: C3 motion checks (512 OBBs) analytic / discrete32 on CPU_SHARE_THREADS threads;
+    * c5_online: the C5 loop on the oracle (world rebuild, minDistance check, min-snap +
+      sampling), per-step latency, 1 thread."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from eppamd import synth
+    nt = min(CPU_SHARE_THREADS, host_info()["affinity_cpus"] or 1)
     w = O.world_build(geom, gates, obstacles, rg, ro)
     pts = synth.sample_states(7, lo, hi, N_STATES)
     reps = 0
@@ -365,16 +516,38 @@ def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi):
     while True:
         O.check_states(w, rg, ro, pts, False, threads=1)
         reps += 1
-        if time.perf_counter() - t > 10.0:
+        if time.perf_counter() - t > 6.0:
             break
     dt = time.perf_counter() - t
     t2 = time.perf_counter()
-    nt = min(16, os.cpu_count() or 1)
-    O.check_states(w, rg, ro, pts, False, threads=nt)
-    dt2 = time.perf_counter() - t2
-    return {"value": reps * N_STATES / dt, "unit": "state validity checks/s", "cores": 1, "kind": "port",
-            "sample": f"{reps} passes over the same 1,048,576-state C2 batch ({reps * N_STATES} checks, {dt:.1f} s)",
-            "all_cores_value": N_STATES / dt2, "all_cores_threads": nt}
+    for _ in range(3):
+        O.check_states(w, rg, ro, pts, False, threads=nt)
+    dt2 = (time.perf_counter() - t2) / 3
+    out = {"value": reps * N_STATES / dt, "unit": "state validity checks/s", "cores": 1, "kind": "port",
+           "sample": f"{reps} passes over the same 1,048,576-state C2 batch ({reps * N_STATES} checks, {dt:.1f} s)",
+           "all_cores_value": N_STATES / dt2, "all_cores_threads": nt, "host": host_info()}
+    # C3 motions: 512 OBBs, the same edge generator as the GPU leg (bounded edge counts)
+    g3, o3 = synth.track_world(42, n_obstacles=472)
+    w3 = O.world_build(geom, g3, o3, rg, ro)
+    for mode, key, n in ((0, "c3_motion_analytic", 1 << 18), (1, "c3_motion_discrete32", 1 << 16)):
+        s1, s2 = synth.edges(43, 8, lo, hi, n)
+        t = time.perf_counter()
+        O.check_motions(w3, rg, ro, s1, s2, False, mode, threads=nt)
+        el = time.perf_counter() - t
+        out[key] = {"edges_per_s": n / el, "threads": nt, "edges": n}
+    if c5_inputs:
+        c = c5_inputs
+        lat = c5_online(c["cfg_path"], c["geom"], c["gates"], c["obstacles"], c["wp"], c["window"], c["vmax"],
+                        c["amax"], c["dt"], c["md"], cpu=True)
+        out["c5_online"] = dict(_pct(lat), threads=1)
+        wp1 = synth.random_track_waypoints(10_000, 12)
+        lat = np.zeros(200)
+        for r in range(len(lat)):
+            t = time.perf_counter()
+            O.generate_trajectory(wp1, 1.0, 2.0, 0.1)
+            lat[r] = time.perf_counter() - t
+        out["c5_refit"] = dict(_pct(lat[20:] * 1e6), threads=1)
+    return out
 
 
 if __name__ == "__main__":

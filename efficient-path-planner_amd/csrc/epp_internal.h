@@ -26,6 +26,8 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+
 #include "epp.h"
 
 namespace epp {
@@ -110,6 +112,10 @@ struct HostWorld {
     void* d_blob = nullptr;
     const WorldView* d_view = nullptr;  // device copy of `view` (after the blob)
     size_t d_capacity = 0;
+    void* h_stage = nullptr;            // pinned staging of the upload
+    size_t h_capacity = 0;
+    hipStream_t stream = nullptr;       // the upload's stream
+    uint64_t generation = 0;            // uploads so far (epp_world_generation)
     std::string blob;            // host image of the device blob
     std::vector<double> aabbs;   // n x 6
 };

@@ -36,7 +36,19 @@ OnlineTrajGenerator::~OnlineTrajGenerator() {
 }
 
 void OnlineTrajGenerator::waitForUpdate() {
-    if (pending.valid()) pending.get();
+    if (pending.valid()) pending.wait();
+    collectUpdate();
+}
+
+// Takes the finished online recomputation's result; its failure (e.g. "Pre path not
+// found. Exiting") is reported here, named as the previous update's.
+void OnlineTrajGenerator::collectUpdate() {
+    if (!pending.valid()) return;
+    try {
+        pending.get();
+    } catch (const std::exception& e) {
+        throw std::runtime_error(std::string("previous trajectory update failed: ") + e.what());
+    }
 }
 
 std::vector<double> OnlineTrajGenerator::gateRow(int gateId) const {
@@ -144,7 +156,17 @@ bool OnlineTrajGenerator::updateGatePos(int gateId, const std::vector<double>& n
     if (gatesObservedWithinRange.count(gateId)) return false;
     if (!pathPlanner.worldPtr->checkPointValidity(dronePos, false)) return false;
     if (newPose.size() < 6) throw std::invalid_argument("newPose needs 6 values");
-    waitForUpdate();
+    // An online recomputation (recalculate_online) still running: the reference throws
+    // when it gets here (src/OnlineTrajGenerator.cpp:208-212).  Here the check comes
+    // before the world is rebuilt, since the running recomputation plans on that world
+    // (the reference rebuilds it under the planning threads' feet).
+    if (pending.valid()) {
+        if (pending.wait_for(std::chrono::seconds(0)) != std::future_status::ready) {
+            std::cerr << "Call to update trajectory, while previous update is still going on";
+            throw std::runtime_error("Call to update trajectory, while previous update is still going on");
+        }
+        collectUpdate();
+    }
     gatesObservedWithinRange.insert(gateId);
     for (int k = 0; k < 6; ++k) nominalGatePositionAndType(gateId, k) = newPose[k];
     pathPlanner.parseGatesAndObstacles(nominalGatePositionAndType, nominalObstaclePosition);
@@ -191,7 +213,7 @@ bool OnlineTrajGenerator::updateGatePos(int gateId, const std::vector<double>& n
     if (passing)
         valid = pathPlanner.checkTrajectoryValidity(look, configParser->getPathPlannerProperties().minDistCheckTrajCollision);
     if (valid && passing) return false;
-    if (trajectoryCurrentlyUpdating) {
+    if (trajectoryCurrentlyUpdating.load()) {
         std::cerr << "Call to update trajectory, while previous update is still going on";
         throw std::runtime_error("Call to update trajectory, while previous update is still going on");
     }
@@ -209,7 +231,7 @@ bool OnlineTrajGenerator::updateGatePos(int gateId, const std::vector<double>& n
 // OnlineTrajGenerator::recomputeTraj — src/OnlineTrajGenerator.cpp:258-421
 void OnlineTrajGenerator::recomputeTraj(int gateId, const Vec3& /*dronePos*/, double flightTime) {
     struct Reset {
-        bool& f;
+        std::atomic<bool>& f;
         ~Reset() { f = false; }
     } reset{trajectoryCurrentlyUpdating};
     const auto& pp = configParser->getPathPlannerProperties();

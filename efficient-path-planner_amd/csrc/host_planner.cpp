@@ -277,17 +277,33 @@ std::vector<Vec3> PathPlanner::shortcut(const std::vector<Vec3>& p) const {
     return out;
 }
 
+// The planner choice of src/PathPlanner.cpp:106-123.  "rrt" cannot be honoured (OMPL's
+// RRT* is third-party and not part of this build; its `range` has no counterpart): it
+// runs the same batch planner as "fmt", and says so once per process.  The reference
+// itself never reads optimality_threshold_percentage (getStraightLineObjective,
+// src/PathPlanner.cpp:160-168, is never called), so neither does this build.
+static void checkPlannerConfig(const PathPlannerProperties& pp) {
+    if (pp.planner != "rrt" && pp.planner != "fmt") {
+        std::cerr << "Unknown planner" << std::endl;
+        throw std::runtime_error("Unknown planner");  // :121-123
+    }
+    if (pp.planner == "rrt") {
+        static std::once_flag once;
+        std::call_once(once, [] {
+            std::cerr << "PathPlanner: planner \"rrt\" runs the batch sampling planner of this build (OMPL's RRT* "
+                         "is not available); path_planner_properties.range is not used"
+                      << std::endl;
+        });
+    }
+}
+
 // PathPlanner::planPath — src/PathPlanner.cpp:80-158
 bool PathPlanner::planPath(const Vec3& start, const Vec3& goal, double timeLimit, std::vector<Vec3>& resultPath) const {
     if (!resultPath.empty()) {
         resultPath.clear();
         std::cerr << "Result path not empty, clearing it" << std::endl;
     }
-    const auto& pp = configParser->getPathPlannerProperties();
-    if (pp.planner != "rrt" && pp.planner != "fmt") {
-        std::cerr << "Unknown planner" << std::endl;
-        throw std::runtime_error("Unknown planner");  // :121-123
-    }
+    checkPlannerConfig(configParser->getPathPlannerProperties());
     const auto t0 = std::chrono::steady_clock::now();
     {
         std::lock_guard<std::mutex> lk(g_stats_mu);
@@ -330,11 +346,7 @@ bool PathPlanner::planCall(const Vec3& start, const Vec3& goal, double timeLimit
 
 void PathPlanner::planPaths(const std::vector<std::pair<Vec3, Vec3>>& problems, double timeLimit,
                             std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const {
-    const auto& pp = configParser->getPathPlannerProperties();
-    if (pp.planner != "rrt" && pp.planner != "fmt") {
-        std::cerr << "Unknown planner" << std::endl;
-        throw std::runtime_error("Unknown planner");
-    }
+    checkPlannerConfig(configParser->getPathPlannerProperties());
     const size_t n = problems.size();
     paths.assign(n, {});
     ok.assign(n, 0);

@@ -45,13 +45,20 @@ void World::addObject(int id, bool gate, const std::vector<double>& c, bool upda
     std::vector<epp_obb_desc> gd, od;
     std::vector<int32_t> off = {0, 0};
     std::vector<double> row;
+    int type = -1;
     if (gate) {
-        if (c.size() < 7) throw std::invalid_argument("gate coordinates need 7 values");
-        const int type = (int)c[6];  // World.cpp:18
+        if (c.size() >= 7) {
+            type = (int)c[6];  // World.cpp:18
+        } else if (update && c.size() == 6) {  // a pose only: the gate keeps its type
+            std::lock_guard<std::mutex> lk(mu_);
+            for (const auto& e : entries_)
+                if (e.gate && e.id == id) type = e.type;
+        }
+        if (type < 0) throw std::invalid_argument("gate coordinates need 7 values");
         gd = descs_of(config_->getGateGeometryByTypeId(type));
         off[1] = (int32_t)gd.size();
-        row.assign(c.begin(), c.begin() + 7);
-        row[6] = 0;  // descriptors passed as type 0
+        row.assign(c.begin(), c.begin() + 6);
+        row.push_back(0);  // descriptors passed as type 0
     } else {
         if (c.size() < 6) throw std::invalid_argument("obstacle coordinates need 6 values");
         od = descs_of(config_->getObstacleGeometry());
@@ -70,11 +77,12 @@ void World::addObject(int id, bool gate, const std::vector<double>& c, bool upda
         for (auto& e : entries_)
             if (e.gate == gate && e.id == id) {
                 e.obbs = out;
+                e.type = type;
                 dirty_ = true;
                 return;
             }
     }
-    entries_.push_back({id, gate, out});
+    entries_.push_back({id, gate, type, out});
     dirty_ = true;
 }
 
@@ -107,45 +115,62 @@ const epp_world* World::device() const {
     return dev_;
 }
 
+// Host-array queries.  Small batches (the reference's one-at-a-time validator calls,
+// checkTrajectoryValidity's few hundred rows) run zero-copy: the kernel reads the query
+// from and writes the flags to pinned host memory, so a call is one launch and one
+// stream synchronisation.  Large batches are staged through HBM by DMA.
+namespace {
+constexpr int64_t kZeroCopyMax = 16384;  // queries per call read straight from host memory
+}
+
 void World::checkPoints(const double* xyz, int64_t n, bool canPassGate, uint8_t* out) const {
-    if (n <= 0) return;
-    const epp_world* w = device();
-    ThreadScratch& ts = ThreadScratch::get();
-    void* st = ts.stream();
-    ts.reset(ThreadScratch::rounded((size_t)n * 24) + ThreadScratch::rounded((size_t)n));
-    double* d_xyz = static_cast<double*>(ts.carve((size_t)n * 24));
-    uint8_t* d_out = static_cast<uint8_t*>(ts.carve((size_t)n));
-    check(epp_memcpy_h2d(d_xyz, xyz, (uint64_t)n * 24, st), "upload");
-    check(epp_check_states(w, d_xyz, n, canPassGate ? 1 : 0, d_out, nullptr, nullptr, st), "checkPoints");
-    check(epp_memcpy_d2h(out, d_out, (uint64_t)n, st), "download");
+    query(n, 1, [&](const double* const* in, uint8_t* flags, void* st) {
+        check(epp_check_states(device(), in[0], n, canPassGate ? 1 : 0, flags, nullptr, nullptr, st), "checkPoints");
+    }, &xyz, out);
 }
 
 void World::checkPointsMinDistance(const double* xyz, int64_t n, double minDistance, uint8_t* out) const {
-    if (n <= 0) return;
-    const epp_world* w = device();
-    ThreadScratch& ts = ThreadScratch::get();
-    void* st = ts.stream();
-    ts.reset(ThreadScratch::rounded((size_t)n * 24) + ThreadScratch::rounded((size_t)n));
-    double* d_xyz = static_cast<double*>(ts.carve((size_t)n * 24));
-    uint8_t* d_out = static_cast<uint8_t*>(ts.carve((size_t)n));
-    check(epp_memcpy_h2d(d_xyz, xyz, (uint64_t)n * 24, st), "upload");
-    check(epp_check_states_mindist(w, d_xyz, n, minDistance, d_out, st), "checkPointsMinDistance");
-    check(epp_memcpy_d2h(out, d_out, (uint64_t)n, st), "download");
+    query(n, 1, [&](const double* const* in, uint8_t* flags, void* st) {
+        check(epp_check_states_mindist(device(), in[0], n, minDistance, flags, st), "checkPointsMinDistance");
+    }, &xyz, out);
 }
 
 void World::checkRays(const double* s1, const double* s2, int64_t n, bool canPassGate, uint8_t* out,
                       int mode) const {
+    const double* in[2] = {s1, s2};
+    query(n, 2, [&](const double* const* d, uint8_t* flags, void* st) {
+        check(epp_check_motions(device(), d[0], d[1], n, canPassGate ? 1 : 0, mode, flags, st), "checkRays");
+    }, in, out);
+}
+
+template <typename Launch>
+void World::query(int64_t n, int n_in, Launch&& launch, const double* const* in, uint8_t* out) const {
     if (n <= 0) return;
-    const epp_world* w = device();
+    (void)device();  // upload a changed world before the launch (not inside it)
     ThreadScratch& ts = ThreadScratch::get();
     void* st = ts.stream();
-    ts.reset(2 * ThreadScratch::rounded((size_t)n * 24) + ThreadScratch::rounded((size_t)n));
-    double* d1 = static_cast<double*>(ts.carve((size_t)n * 24));
-    double* d2 = static_cast<double*>(ts.carve((size_t)n * 24));
+    const size_t in_b = (size_t)n * 24;
+    const double* d_in[2] = {nullptr, nullptr};
+    if (n <= kZeroCopyMax) {
+        char* h = static_cast<char*>(ts.pinned(0, n_in * ThreadScratch::rounded(in_b) + ThreadScratch::rounded((size_t)n)));
+        for (int k = 0; k < n_in; ++k) {
+            std::memcpy(h + k * ThreadScratch::rounded(in_b), in[k], in_b);
+            d_in[k] = reinterpret_cast<const double*>(h + k * ThreadScratch::rounded(in_b));
+        }
+        uint8_t* flags = reinterpret_cast<uint8_t*>(h + n_in * ThreadScratch::rounded(in_b));
+        launch(d_in, flags, st);
+        check(epp_stream_sync(st), "query");
+        std::memcpy(out, flags, (size_t)n);
+        return;
+    }
+    ts.reset(n_in * ThreadScratch::rounded(in_b) + ThreadScratch::rounded((size_t)n));
+    for (int k = 0; k < n_in; ++k) {
+        double* d = static_cast<double*>(ts.carve(in_b));
+        check(epp_memcpy_h2d(d, in[k], (uint64_t)in_b, st), "upload");
+        d_in[k] = d;
+    }
     uint8_t* d_out = static_cast<uint8_t*>(ts.carve((size_t)n));
-    check(epp_memcpy_h2d(d1, s1, (uint64_t)n * 24, st), "upload");
-    check(epp_memcpy_h2d(d2, s2, (uint64_t)n * 24, st), "upload");
-    check(epp_check_motions(w, d1, d2, n, canPassGate ? 1 : 0, mode, d_out, st), "checkRays");
+    launch(d_in, d_out, st);
     check(epp_memcpy_d2h(out, d_out, (uint64_t)n, st), "download");
 }
 

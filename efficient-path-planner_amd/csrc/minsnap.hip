@@ -28,6 +28,7 @@
 #include <string>
 #include <vector>
 
+#include "cached_ws.h"
 #include "epp_internal.h"
 
 namespace epp {
@@ -36,14 +37,23 @@ namespace {
 constexpr int N = 10;
 constexpr int HALF = 5;
 constexpr int kWave = 64;
-constexpr int kMaxLdsSeg = 24;  // tracks with more segments use the global scratch path
 
 // falling factorials: B[k][j] = j! / (j-k)!  (src/polynomial.cpp:145-160)
 __constant__ double cB[N][N];
 
-struct SegScratch {  // per-segment scratch: A^-1 (100), H (100), Q 6x6 block (36), W (16), L (16)
-    static constexpr int kAinv = 0, kH = 100, kQ = 200, kW = 236, kL = 252, kSize = 268;
-};
+// Phase timeline of the fused refit (diagnostics builds only: -DEPP_REFIT_TL, see
+// scripts/refit_timeline.py): thread 0 of each workgroup stamps s_memrealtime (100 MHz).
+#ifdef EPP_REFIT_TL
+__device__ unsigned long long g_refit_tl[2][16];
+#define EPP_TL(k)                                                                         \
+    do {                                                                                  \
+        if (threadIdx.x == 0) g_refit_tl[blockIdx.x & 1][k] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define EPP_TL(k) \
+    do {          \
+    } while (0)
+#endif
 
 __host__ __device__ __forceinline__ double nfabian(const double* p, const double* q, double vmax,
                                           double amax) {
@@ -52,6 +62,23 @@ __host__ __device__ __forceinline__ double nfabian(const double* p, const double
     const double distance = sqrt((d0 * d0 + d1 * d1) + d2 * d2);
     return distance / vmax * 2 * (1.0 + 6.5 * vmax / amax * exp(-distance / vmax * 2));
 }
+
+// Reciprocal and reciprocal square root: the hardware estimates (v_rcp_f64, v_rsq_f64:
+// ~5e-8 relative error, measured) refined by two Newton steps to ~1e-16, in 6 dependent
+// instructions instead of the ~10-20 of an IEEE division / square root.
+__device__ __forceinline__ double rcp_nr(double x) {
+    double y = __builtin_amdgcn_rcp(x);
+    y = fma(y, fma(-x, y, 1.0), y);
+    return fma(y, fma(-x, y, 1.0), y);
+}
+__device__ __forceinline__ double rsq_nr(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    y = fma(0.5 * y, fma(-(x * y), y, 1.0), y);
+    return fma(0.5 * y, fma(-(x * y), y, 1.0), y);
+}
+
+// 1 / r! for r = 0..4 (the same roundings as dividing at run time)
+__device__ constexpr double kInvFact[HALF] = {1.0, 1.0, 1.0 / 2.0, 1.0 / 6.0, 1.0 / 24.0};
 
 // setupMappingMatrix + invertMappingMatrix (Schur complement), one lane per segment.
 __device__ void invert_mapping(double T, double* Ai /* 10x10 row-major */) {
@@ -82,6 +109,7 @@ __device__ void invert_mapping(double T, double* Ai /* 10x10 row-major */) {
     // unrolled and the row swap is a select, so all indices are static and the arrays
     // stay in registers (a data-dependent row index would put them in scratch memory).
     int perm[HALF];
+    double piv_inv[HALF];
 #pragma unroll
     for (int i = 0; i < HALF; ++i) perm[i] = i;
 #pragma unroll
@@ -107,9 +135,13 @@ __device__ void invert_mapping(double T, double* Ai /* 10x10 row-major */) {
             perm[k] = sw ? perm[r] : t;
             perm[r] = sw ? t : perm[r];
         }
+        // one reciprocal per pivot instead of a division per entry (a division is a
+        // ~10-instruction dependent sequence on CDNA): results within an ulp or two
+        const double ip = rcp_nr(D[k][k]);
+        piv_inv[k] = ip;
 #pragma unroll
         for (int r = k + 1; r < HALF; ++r) {
-            D[r][k] = D[r][k] / D[k][k];
+            D[r][k] = D[r][k] * ip;
 #pragma unroll
             for (int c = k + 1; c < HALF; ++c) D[r][c] = D[r][c] - D[r][k] * D[k][c];
         }
@@ -128,14 +160,14 @@ __device__ void invert_mapping(double T, double* Ai /* 10x10 row-major */) {
         for (int i = HALF - 1; i >= 0; --i) {
 #pragma unroll
             for (int j = i + 1; j < HALF; ++j) x[i] = x[i] - D[i][j] * x[j];
-            x[i] = x[i] / D[i][i];
+            x[i] = x[i] * piv_inv[i];
         }
 #pragma unroll
         for (int i = 0; i < HALF; ++i) Dinv[i][col] = x[i];
     }
     for (int i = 0; i < N * N; ++i) Ai[i] = 0.0;
     for (int r = 0; r < HALF; ++r) {
-        const double adinv = 1.0 / cB[r][r];  // A_diag.cwiseInverse()
+        const double adinv = kInvFact[r];  // A_diag.cwiseInverse(): 1 / B[r][r] = 1 / r!
         Ai[r * N + r] = adinv;
         for (int c = 0; c < HALF; ++c) Ai[(r + HALF) * N + c + HALF] = Dinv[r][c];
     }
@@ -143,174 +175,104 @@ __device__ void invert_mapping(double T, double* Ai /* 10x10 row-major */) {
         for (int c = 0; c < HALF; ++c) {
             double s = 0.0;
             for (int k = 0; k < HALF; ++k) s = s + Dinv[r][k] * C[k][c];
-            Ai[(r + HALF) * N + c] = -s * (1.0 / cB[c][c]);  // -D^-1 C A_diag^-1
+            Ai[(r + HALF) * N + c] = -s * kInvFact[c];  // -D^-1 C A_diag^-1
         }
 }
 
-// 4x4 Cholesky (lower factor in place; false if not SPD) and the two triangular solves
-// with MC right-hand sides (b: 4 x MC, row-major), on register arrays: fully unrolled so
-// the indices are static.  The serial block solve runs on one lane, where every LDS round
-// trip in a dependent chain would be exposed latency.
-__device__ __forceinline__ bool chol4r(double (&L)[16]) {
-    bool ok = true;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        double d = L[j * 4 + j];
-#pragma unroll
-        for (int k = 0; k < j; ++k) d = d - L[j * 4 + k] * L[j * 4 + k];
-        ok = ok && (d > 0.0);
-        d = sqrt(d);
-        L[j * 4 + j] = d;
-#pragma unroll
-        for (int i = j + 1; i < 4; ++i) {
-            double s = L[i * 4 + j];
-#pragma unroll
-            for (int k = 0; k < j; ++k) s = s - L[i * 4 + k] * L[j * 4 + k];
-            L[i * 4 + j] = s / d;
-        }
-#pragma unroll
-        for (int i = 0; i < j; ++i) L[i * 4 + j] = 0.0;
-    }
-    return ok;
-}
-template <int MC>
-__device__ __forceinline__ void lsolve4r(const double (&L)[16], double (&b)[4 * MC]) {
-#pragma unroll
-    for (int c = 0; c < MC; ++c)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            double s = b[i * MC + c];
-#pragma unroll
-            for (int k = 0; k < i; ++k) s = s - L[i * 4 + k] * b[k * MC + c];
-            b[i * MC + c] = s / L[i * 4 + i];
-        }
-}
-template <int MC>
-__device__ __forceinline__ void ltsolve4r(const double (&L)[16], double (&b)[4 * MC]) {
-#pragma unroll
-    for (int c = 0; c < MC; ++c)
-#pragma unroll
-        for (int i = 3; i >= 0; --i) {
-            double s = b[i * MC + c];
-#pragma unroll
-            for (int k = i + 1; k < 4; ++k) s = s - L[k * 4 + i] * b[k * MC + c];
-            b[i * MC + c] = s / L[i * 4 + i];
-        }
-}
+// Per-segment scratch (doubles): A^-1 (10x10), H (10x10), the 6x6 snap block Q of Q_i,
+// G = Q * (rows 4..9 of A^-1) (6x10), and the R_pp blocks: W (coupling to the next inner
+// vertex) and L (diagonal block, then its Cholesky factor), I (1 / diagonal of the factor).
+struct Seg {
+    static constexpr int kAinv = 0, kH = 100, kQ = 200, kG = 236, kW = 296, kL = 312, kI = 328, kSize = 332;
+};
+// Per track, besides the segment scratch: (M+1) x 5 x 3 vertex values, (M+1) x 4 x 3
+// right-hand sides, M segment times.
+__host__ __device__ constexpr size_t vertex_doubles(int M) { return (size_t)(M + 1) * 27 + (size_t)M; }
+// Tracks with up to this many segments keep the segment scratch in LDS (~114 KB at 40).
+constexpr int kMaxLdsSeg = 40;
 
-// One workgroup (= one wavefront) per track.  scratch: per segment SegScratch::kSize
-// doubles (LDS when the track has <= kMaxLdsSeg segments, else the global workspace),
-// plus per vertex 5x3 derivative values and 4x3 rhs.
-template <bool LDS>
-__global__ __launch_bounds__(kWave) void k_minsnap(const double* __restrict__ wp,
-                                                   const int32_t* __restrict__ wp_off, int n_tracks,
-                                                   double vmax, double amax,
-                                                   const double* __restrict__ v0,
-                                                   const double* __restrict__ a0,
-                                                   double* __restrict__ seg_times,
-                                                   double* __restrict__ coeffs,
-                                                   int32_t* __restrict__ status,
-                                                   double* __restrict__ gscratch,
-                                                   const int64_t* __restrict__ gscratch_off) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    // all LDS in the one dynamic array (no static __shared__ in front of it:
-    // cdna_hip_programming.md Guideline 17); the first 16 bytes hold the error flag
-    int& s_err = *reinterpret_cast<int*>(smem);
-    double* sm = smem + 2;
-    const int track = blockIdx.x;
-    if (track >= n_tracks) return;
-    const int lane = threadIdx.x;
-    const int w0 = wp_off[track];
-    const int W = wp_off[track + 1] - w0;
-    const int M = W - 1;
-    const int seg0 = w0 - track;
-    if (lane == 0) s_err = 0;
-    if (W < 2) {
-        if (lane == 0 && status) status[track] = -1;  // std::invalid_argument
-        return;
-    }
-    double* scr;   // M * kSize
-    double* dv;    // (M+1) * 5 * 3 vertex derivative values
-    double* rhs;   // (M+1) * 4 * 3
-    double* Tm;    // M
-    if (LDS) {
-        scr = sm;
-        dv = scr + (size_t)M * SegScratch::kSize;
-    } else {
-        scr = gscratch + gscratch_off[track];
-        dv = sm;
-    }
-    rhs = dv + (size_t)(M + 1) * 15;
-    Tm = rhs + (size_t)(M + 1) * 12;
-    const double* P = wp + (size_t)w0 * 3;
-    __syncthreads();
-
+// The min-snap solve of one track by one workgroup of BLOCK threads (every thread calls
+// it; it contains barriers).  P: W x 3 waypoints; v0/a0: the start vertex's velocity and
+// acceleration (NULL = 0); times_in: caller segment times (NULL = Nfabian).  scr: M x
+// Seg::kSize, dv/rhs/Tm: vertex_doubles(M) (LDS or global).  *s_err must be 0 and
+// visible to every thread on entry.  Writes T_out (M, may be NULL) and C_out (M x 3 x 10,
+// increasing powers).  Returns 0, -2 (a segment time <= 0: the reference's
+// CHECK_GT(segment_time, 0), impl :297) or -3 (R_pp not SPD).
+template <int BLOCK>
+__device__ __forceinline__ int solve_track(const double* __restrict__ P, int M, double vmax, double amax,
+                                           const double* v0, const double* a0, const double* times_in,
+                                           double* scr, double* dv, double* rhs, double* Tm, int* s_err,
+                                           double* T_out, double* C_out) {
+    const int tid = threadIdx.x;
     // ---- phase 1: segment times, mapping inverses, fixed vertex values ----------
-    for (int i = lane; i < M; i += kWave) {
-        const double T = nfabian(P + 3 * i, P + 3 * (i + 1), vmax, amax);
+    for (int i = tid; i < M; i += BLOCK) {
+        const double T = times_in ? times_in[i] : nfabian(P + 3 * i, P + 3 * (i + 1), vmax, amax);
         Tm[i] = T;
-        seg_times[seg0 + i] = T;
-        if (!(T > 0)) atomicOr(&s_err, 1);  // CHECK_GT(segment_time, 0)  impl :297
-        else invert_mapping(T, scr + (size_t)i * SegScratch::kSize + SegScratch::kAinv);
+        if (T_out) T_out[i] = T;
+        if (!(T > 0)) atomicOr(s_err, 1);  // CHECK_GT(segment_time, 0)  impl :297
+        else invert_mapping(T, scr + (size_t)i * Seg::kSize + Seg::kAinv);
     }
-    for (int e = lane; e < (M + 1) * 15; e += kWave) {
+    // start vertex {p0, v0, a0, 0, 0}, inner {p}, end {p, 0, 0, 0, 0}: makeStartOrEnd
+    // (src/vertex.cpp:146-170) and trajectory_generator.cpp:28-50
+    for (int e = tid; e < (M + 1) * 15; e += BLOCK) {
         const int v = e / 15, k = (e % 15) / 3, d = e % 3;
         double val = 0.0;  // free values are overwritten by the solve
-        if (k == 0) val = P[3 * v + d];                       // position, every vertex
-        else if (v == 0 && k == 1) val = v0 ? v0[3 * track + d] : 0.0;  // makeStartOrEnd
-        else if (v == 0 && k == 2) val = a0 ? a0[3 * track + d] : 0.0;
+        if (k == 0) val = P[3 * v + d];
+        else if (v == 0 && k == 1) val = v0 ? v0[d] : 0.0;
+        else if (v == 0 && k == 2) val = a0 ? a0[d] : 0.0;
         dv[e] = val;
     }
     __syncthreads();
-    if (s_err) {
-        if (lane == 0 && status) status[track] = -2;
-        return;
-    }
-    // ---- phase 2: Q (6x6 snap block) and H = A^-T Q A^-1 --------------------------
-    for (int e = lane; e < M * 36; e += kWave) {
+    EPP_TL(1);
+    if (*s_err) return -2;
+    // ---- phase 2: Q (6x6 snap block), G = Q A^-1, H = A^-T G ------------------------
+    // computeQuadraticCostJacobian (impl :567-583): Q[9-r][9-c] = B[4][9-r] B[4][9-c] t^e 2/e
+    for (int e = tid; e < M * 36; e += BLOCK) {
         const int i = e / 36, a = 4 + (e % 36) / 6, b = 4 + e % 6;
-        const double ex = (double)(a + b - 7);  // (N-1-4)*2+1-row-col with row=9-a, col=9-b
-        scr[(size_t)i * SegScratch::kSize + SegScratch::kQ + (a - 4) * 6 + (b - 4)] =
-            cB[4][a] * cB[4][b] * pow(Tm[i], ex) * 2.0 / ex;
+        const double ex = (double)(a + b - 7);
+        scr[(size_t)i * Seg::kSize + Seg::kQ + (a - 4) * 6 + (b - 4)] = cB[4][a] * cB[4][b] * pow(Tm[i], ex) * 2.0 / ex;
     }
     __syncthreads();
-    // All 100 entries are computed (no mirroring of a triangle): each row then keeps
-    // the exact translation invariance H[r][0] == -H[r][5] that the reference's full
-    // product has; mirroring breaks it and costs ~1e-6 on long, stiff tracks.
-    for (int e = lane; e < M * 100; e += kWave) {
+    EPP_TL(2);
+    for (int e = tid; e < M * 60; e += BLOCK) {
+        const int i = e / 60, a = (e % 60) / 10, c = e % 10;
+        double* S = scr + (size_t)i * Seg::kSize;
+        double g = 0.0;
+#pragma unroll
+        for (int b = 0; b < 6; ++b) g = g + S[Seg::kQ + a * 6 + b] * S[Seg::kAinv + (b + 4) * N + c];
+        S[Seg::kG + a * 10 + c] = g;
+    }
+    __syncthreads();
+    EPP_TL(3);
+    // All 100 entries (no mirrored triangle): every row keeps the exact translation
+    // invariance H[r][0] == -H[r][5] that the reference's full product has.
+    for (int e = tid; e < M * 100; e += BLOCK) {
         const int i = e / 100, r = (e % 100) / 10, c = e % 10;
-        const double* S = scr + (size_t)i * SegScratch::kSize;
-        const double* Ai = S + SegScratch::kAinv;
-        const double* Q = S + SegScratch::kQ;
+        double* S = scr + (size_t)i * Seg::kSize;
         double h = 0.0;
-        for (int a = 4; a < N; ++a) {
-            double qa = 0.0;
-            for (int b = 4; b < N; ++b) qa = qa + Q[(a - 4) * 6 + (b - 4)] * Ai[b * N + c];
-            h = h + Ai[a * N + r] * qa;
-        }
-        double* H = const_cast<double*>(S) + SegScratch::kH;
-        H[r * N + c] = h;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) h = h + S[Seg::kAinv + (a + 4) * N + r] * S[Seg::kG + a * 10 + c];
+        S[Seg::kH + r * N + c] = h;
     }
     __syncthreads();
+    EPP_TL(4);
     // ---- phase 3: block-tridiagonal system over the inner vertices ----------------
     // free variable (v, p): vertex v in 1..M-1, derivative p+1.  Diagonal block D_v is
     // kept in the L slot of segment v-1, the coupling E_v (v -> v+1) in the W slot.
     const int nin = M - 1;
-    for (int e = lane; e < nin * 16; e += kWave) {
+    for (int e = tid; e < nin * 16; e += BLOCK) {
         const int v = 1 + e / 16, p = (e % 16) / 4, q = e % 4;
-        const double* Hm = scr + (size_t)(v - 1) * SegScratch::kSize + SegScratch::kH;
-        const double* Hp = scr + (size_t)v * SegScratch::kSize + SegScratch::kH;
-        scr[(size_t)(v - 1) * SegScratch::kSize + SegScratch::kL + p * 4 + q] =
-            Hm[(6 + p) * N + 6 + q] + Hp[(1 + p) * N + 1 + q];
-        scr[(size_t)(v - 1) * SegScratch::kSize + SegScratch::kW + p * 4 + q] =
-            (v < nin) ? Hp[(1 + p) * N + 6 + q] : 0.0;
+        const double* Hm = scr + (size_t)(v - 1) * Seg::kSize + Seg::kH;
+        const double* Hp = scr + (size_t)v * Seg::kSize + Seg::kH;
+        scr[(size_t)(v - 1) * Seg::kSize + Seg::kL + p * 4 + q] = Hm[(6 + p) * N + 6 + q] + Hp[(1 + p) * N + 1 + q];
+        scr[(size_t)(v - 1) * Seg::kSize + Seg::kW + p * 4 + q] = (v < nin) ? Hp[(1 + p) * N + 6 + q] : 0.0;
     }
-    for (int e = lane; e < nin * 12; e += kWave) {
+    for (int e = tid; e < nin * 12; e += BLOCK) {
         const int v = 1 + e / 12, p = (e % 12) / 3, d = e % 3;
         double s = 0.0;
         // segment v-1: rows 0..4 = vertex v-1, rows 5..9 = vertex v; row of (v,p+1) = 6+p
         {
-            const double* H = scr + (size_t)(v - 1) * SegScratch::kSize + SegScratch::kH;
+            const double* H = scr + (size_t)(v - 1) * Seg::kSize + Seg::kH;
             for (int r = 0; r < N; ++r) {
                 const int vv = (r < HALF) ? v - 1 : v, k = r % HALF;
                 const bool fixed = (k == 0) || vv == 0 || vv == M;
@@ -319,7 +281,7 @@ __global__ __launch_bounds__(kWave) void k_minsnap(const double* __restrict__ wp
         }
         // segment v: rows 0..4 = vertex v (row of (v,p+1) = 1+p), rows 5..9 = vertex v+1
         {
-            const double* H = scr + (size_t)v * SegScratch::kSize + SegScratch::kH;
+            const double* H = scr + (size_t)v * Seg::kSize + Seg::kH;
             for (int r = 0; r < N; ++r) {
                 const int vv = (r < HALF) ? v : v + 1, k = r % HALF;
                 const bool fixed = (k == 0) || vv == 0 || vv == M;
@@ -329,117 +291,193 @@ __global__ __launch_bounds__(kWave) void k_minsnap(const double* __restrict__ wp
         rhs[(v * 4 + p) * 3 + d] = -s;
     }
     __syncthreads();
-    // ---- phase 4: block Cholesky solve (one lane; 4x4 blocks, 3 right-hand sides) ---
-    if (lane == 0 && nin > 0) {
-        // the carried blocks (W_{v-1}, z_{v-1}; x_{v+1} on the way back) stay in registers
+    EPP_TL(5);
+    // ---- phase 4: block Cholesky solve (4x4 blocks, 3 right-hand sides) ---------------
+    // The inner vertices are eliminated in order (block Thomas) by one lane with every
+    // carried block in registers: per step v the Schur complement S_v = D_v - W_{v-1}^T
+    // W_{v-1}, z_v = b_v - W_{v-1}^T z_{v-1}, the Cholesky factor L_v of S_v and the
+    // forward solves z_v <- L_v^-1 z_v, W_v = L_v^-1 E_v; then x_v = L_v^-T (z_v - W_v
+    // x_{v+1}) backwards.  The step's inputs are loaded before the previous step's
+    // results are stored, FMAs throughout and Newton-refined reciprocals instead of
+    // divisions / square roots (within ~1e-15 of them): the chain is issue-bound, and a
+    // wave64 fp64 instruction costs the same whatever the active lanes.
+    if (tid == 0 && nin > 0) {
         bool ok = true;
         double Wp[16], zp[12];
-        for (int v = 1; v <= nin; ++v) {
-            double* Ls = scr + (size_t)(v - 1) * SegScratch::kSize + SegScratch::kL;
-            double L[16], b[12];
+        double D[16], E[16], b[12];
+        auto load = [&](int v) {
+            const double* Sg = scr + (size_t)(v - 1) * Seg::kSize;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) L[i] = Ls[i];
+            for (int i = 0; i < 16; ++i) D[i] = Sg[Seg::kL + i];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) E[i] = Sg[Seg::kW + i];
 #pragma unroll
             for (int i = 0; i < 12; ++i) b[i] = rhs[(size_t)v * 12 + i];
-            if (v > 1) {  // S_v = D_v - W_{v-1}^T W_{v-1},  W_{v-1} = L_{v-1}^-1 E_{v-1}
+        };
+        load(1);
+        for (int v = 1; v <= nin; ++v) {
+            double L[16], inv[4], z[12], Wn[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) L[i] = D[i];
+#pragma unroll
+            for (int i = 0; i < 12; ++i) z[i] = b[i];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) Wn[i] = E[i];
+            if (v < nin) load(v + 1);  // independent of this step: in flight meanwhile
+            if (v > 1) {
 #pragma unroll
                 for (int p = 0; p < 4; ++p)
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        double s = 0.0;
+                    for (int q = 0; q <= p; ++q)
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) s = s + Wp[k * 4 + p] * Wp[k * 4 + q];
-                        L[p * 4 + q] = L[p * 4 + q] - s;
-                    }
-                // z_v = b_v - W_{v-1}^T z_{v-1}
+                        for (int k = 0; k < 4; ++k) L[p * 4 + q] = fma(-Wp[k * 4 + p], Wp[k * 4 + q], L[p * 4 + q]);
 #pragma unroll
                 for (int p = 0; p < 4; ++p)
 #pragma unroll
-                    for (int d = 0; d < 3; ++d) {
-                        double s = 0.0;
+                    for (int d = 0; d < 3; ++d)
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) s = s + Wp[k * 4 + p] * zp[k * 3 + d];
-                        b[p * 3 + d] = b[p * 3 + d] - s;
-                    }
+                        for (int k = 0; k < 4; ++k) z[p * 3 + d] = fma(-Wp[k * 4 + p], zp[k * 3 + d], z[p * 3 + d]);
             }
-            ok = chol4r(L);
-            if (!ok) break;
-            lsolve4r<3>(L, b);
+            // Cholesky (lower triangle of L)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) Ls[i] = L[i];
+            for (int j = 0; j < 4; ++j) {
+                double dd = L[j * 5];
+#pragma unroll
+                for (int k = 0; k < j; ++k) dd = fma(-L[j * 4 + k], L[j * 4 + k], dd);
+                ok = ok && (dd > 0.0);
+                const double r = rsq_nr(dd);
+                inv[j] = r;
+                L[j * 5] = dd * r;
+#pragma unroll
+                for (int i = j + 1; i < 4; ++i) {
+                    double t = L[i * 4 + j];
+#pragma unroll
+                    for (int k = 0; k < j; ++k) t = fma(-L[i * 4 + k], L[j * 4 + k], t);
+                    L[i * 4 + j] = t * r;
+                }
+            }
+            if (!ok) break;
+            // forward solves: z (3 columns) and, but for the last vertex, W (4 columns)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    double t = z[i * 3 + c];
+#pragma unroll
+                    for (int k = 0; k < i; ++k) t = fma(-L[i * 4 + k], z[k * 3 + c], t);
+                    z[i * 3 + c] = t * inv[i];
+                }
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    double t = Wn[i * 4 + c];
+#pragma unroll
+                    for (int k = 0; k < i; ++k) t = fma(-L[i * 4 + k], Wn[k * 4 + c], t);
+                    Wn[i * 4 + c] = t * inv[i];
+                }
+            }
+            double* Sg = scr + (size_t)(v - 1) * Seg::kSize;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) Sg[Seg::kL + i] = L[i];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) Sg[Seg::kI + i] = inv[i];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                Sg[Seg::kW + i] = Wn[i];
+                Wp[i] = Wn[i];
+            }
 #pragma unroll
             for (int i = 0; i < 12; ++i) {
-                rhs[(size_t)v * 12 + i] = b[i];
-                zp[i] = b[i];
-            }
-            if (v < nin) {
-                double* Ws = scr + (size_t)(v - 1) * SegScratch::kSize + SegScratch::kW;
-                double W[16];
-#pragma unroll
-                for (int i = 0; i < 16; ++i) W[i] = Ws[i];
-                lsolve4r<4>(L, W);
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    Ws[i] = W[i];
-                    Wp[i] = W[i];
-                }
+                rhs[(size_t)v * 12 + i] = z[i];
+                zp[i] = z[i];
             }
         }
         if (ok) {
             double xn[12];
             for (int v = nin; v >= 1; --v) {
-                double x[12], L[16];
+                const double* Sg = scr + (size_t)(v - 1) * Seg::kSize;
+                double x[12];
 #pragma unroll
                 for (int i = 0; i < 12; ++i) x[i] = rhs[(size_t)v * 12 + i];
-#pragma unroll
-                for (int i = 0; i < 16; ++i) L[i] = scr[(size_t)(v - 1) * SegScratch::kSize + SegScratch::kL + i];
                 if (v < nin) {  // z_v - W_v x_{v+1}
-                    const double* Wv = scr + (size_t)(v - 1) * SegScratch::kSize + SegScratch::kW;
-                    double W[16];
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) W[i] = Wv[i];
 #pragma unroll
                     for (int p = 0; p < 4; ++p)
 #pragma unroll
-                        for (int d = 0; d < 3; ++d) {
-                            double s = 0.0;
+                        for (int d = 0; d < 3; ++d)
 #pragma unroll
-                            for (int k = 0; k < 4; ++k) s = s + W[p * 4 + k] * xn[k * 3 + d];
-                            x[p * 3 + d] = x[p * 3 + d] - s;
-                        }
+                            for (int k = 0; k < 4; ++k) x[p * 3 + d] = fma(-Sg[Seg::kW + p * 4 + k], xn[k * 3 + d], x[p * 3 + d]);
                 }
-                ltsolve4r<3>(L, x);
 #pragma unroll
-                for (int i = 0; i < 12; ++i) {
-                    rhs[(size_t)v * 12 + i] = x[i];
-                    xn[i] = x[i];
-                }
+                for (int i = 3; i >= 0; --i)
+#pragma unroll
+                    for (int d = 0; d < 3; ++d) {
+                        double t = x[i * 3 + d];
+#pragma unroll
+                        for (int k = i + 1; k < 4; ++k) t = fma(-Sg[Seg::kL + k * 4 + i], x[k * 3 + d], t);
+                        x[i * 3 + d] = t * Sg[Seg::kI + i];
+                    }
+#pragma unroll
+                for (int i = 0; i < 12; ++i) xn[i] = x[i];
 #pragma unroll
                 for (int p = 0; p < 4; ++p)
 #pragma unroll
                     for (int d = 0; d < 3; ++d) dv[(v * HALF + 1 + p) * 3 + d] = x[p * 3 + d];
             }
         } else {
-            s_err = 1;
+            *s_err = 1;
         }
     }
     __syncthreads();
-    if (s_err) {
-        if (lane == 0 && status) status[track] = -3;
-        return;
-    }
+    EPP_TL(6);
+    if (*s_err) return -3;
     // ---- phase 5: p_i = A_i^-1 [d_i ; d_{i+1}] -------------------------------------
-    for (int e = lane; e < M * 30; e += kWave) {
+    for (int e = tid; e < M * 30; e += BLOCK) {
         const int i = e / 30, d = (e % 30) / 10, r = e % 10;
-        const double* Ai = scr + (size_t)i * SegScratch::kSize + SegScratch::kAinv;
+        const double* Ai = scr + (size_t)i * Seg::kSize + Seg::kAinv;
         double s = 0.0;
         for (int k = 0; k < N; ++k) {
             const int v = i + (k >= HALF ? 1 : 0);
             s = s + Ai[r * N + k] * dv[(v * HALF + (k % HALF)) * 3 + d];
         }
-        coeffs[((size_t)(seg0 + i) * 3 + d) * N + r] = s;
+        C_out[((size_t)i * 3 + d) * N + r] = s;
     }
-    if (lane == 0 && status) status[track] = 0;
+    return 0;
+}
+
+// Batch: one workgroup (BLOCK threads) per track.  Track k owns waypoints
+// [wp_off[k], wp_off[k+1]) and segments [wp_off[k]-k, wp_off[k+1]-k-1).  LDS: the segment
+// scratch (when LDS) and the vertex values; else the segment scratch lives in gscratch
+// at the track's first segment (Σ M x Seg::kSize doubles).
+template <int BLOCK, bool LDS>
+__global__ __launch_bounds__(BLOCK) void k_minsnap(const double* __restrict__ wp, const int32_t* __restrict__ wp_off,
+                                                   int n_tracks, double vmax, double amax, const double* __restrict__ v0,
+                                                   const double* __restrict__ a0, const double* __restrict__ times_in,
+                                                   double* __restrict__ seg_times, double* __restrict__ coeffs,
+                                                   int32_t* __restrict__ status, double* __restrict__ gscratch) {
+    // one dynamic LDS array (cdna_hip_programming.md Guideline 17); the first 16 bytes
+    // hold the error flag
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    int* s_err = reinterpret_cast<int*>(smem);
+    double* sm = smem + 2;
+    const int track = blockIdx.x;
+    if (track >= n_tracks) return;
+    const int w0 = wp_off[track];
+    const int W = wp_off[track + 1] - w0;
+    const int M = W - 1;
+    const int seg0 = w0 - track;
+    if (W < 2) {
+        if (threadIdx.x == 0 && status) status[track] = -1;  // std::invalid_argument
+        return;
+    }
+    if (threadIdx.x == 0) *s_err = 0;
+    double* scr = LDS ? sm : gscratch + (size_t)seg0 * Seg::kSize;
+    double* dv = LDS ? sm + (size_t)M * Seg::kSize : sm;
+    double* rhs = dv + (size_t)(M + 1) * 15;
+    double* Tm = rhs + (size_t)(M + 1) * 12;
+    __syncthreads();
+    const int st = solve_track<BLOCK>(wp + (size_t)w0 * 3, M, vmax, amax, v0 ? v0 + 3 * track : nullptr,
+                                      a0 ? a0 + 3 * track : nullptr, times_in ? times_in + seg0 : nullptr, scr, dv, rhs,
+                                      Tm, s_err, seg_times + seg0, coeffs + (size_t)seg0 * 30);
+    if (threadIdx.x == 0 && status) status[track] = st;
 }
 
 constexpr int kRowChunk = 512;  // samples per k_sample_rows round
@@ -449,7 +487,7 @@ struct RangeIter {
     const double* T;
     int M, i;
     double t_end, acc, tis, Ti;  // Ti = T[i], kept in a register (one LDS read per segment)
-    __device__ void init(const double* T_, int M_) {
+    __host__ __device__ void init(const double* T_, int M_) {
         T = T_;
         M = M_;
         t_end = 0.0;  // max_time_ += segment.getTime()  trajectory.h:63-70
@@ -465,7 +503,7 @@ struct RangeIter {
         Ti = T[i];
     }
     // Advances to the next sample; returns false when the loop ends.
-    __device__ bool next(int& seg, double& t_in, double& t_acc) {
+    __host__ __device__ bool next(int& seg, double& t_in, double& t_acc) {
         while (acc < t_end) {
             if (tis > Ti) {
                 tis = tis - Ti;
@@ -481,7 +519,7 @@ struct RangeIter {
         }
         return false;
     }
-    __device__ void advance(double dt) {
+    __host__ __device__ void advance(double dt) {
         tis = tis + dt;
         acc = acc + dt;
     }
@@ -542,12 +580,11 @@ __global__ __launch_bounds__(kWave) void k_sample_count(const double* __restrict
 }
 
 // Polynomial::evaluate(t, k) — polynomial.h:136-149
+// (Horner with fused multiply-adds: the sampled values are compared at 1e-6, the time
+// column, which does not go through here, exactly)
 __device__ __forceinline__ double poly_eval(const double* c, double t, int k) {
     double r = cB[k][N - 1] * c[N - 1];
-    for (int j = N - 2; j >= k; --j) {
-        r = r * t;
-        r = r + cB[k][j] * c[j];
-    }
+    for (int j = N - 2; j >= k; --j) r = fma(r, t, cB[k][j] * c[j]);
     return r;
 }
 
@@ -628,14 +665,96 @@ __global__ __launch_bounds__(kWave) void k_sample_rows(const double* __restrict_
     }
 }
 
-struct Workspace {
-    double* d = nullptr;
-    size_t cap = 0;
-    int64_t* off = nullptr;
-    size_t off_cap = 0;
+// ---- single-track fused refit (the 50 Hz latency path) --------------------------------
+// poly_traj::generateTrajectory for one track in ONE launch of one workgroup, reading its
+// inputs from and writing the rows to pinned host memory (no copies).  The host has
+// already run the two sequential parts, which a GPU lane runs slowly (~65 ns per dependent
+// step): the segment times (Nfabian with the host's libm, as the reference) and
+// Trajectory::evaluateRange's `acc += dt` recurrence (sample times and segments, exact).
+// The workgroup solves the min-snap problem with those times (solve_track) and
+// evaluates the rows (Polynomial::evaluate).
+constexpr int kRefitArgW = 41;  // tracks up to this many waypoints pass wp, v0, a0, T as kernel arguments
+struct RefitArgs {
+    const double* in;  // host-mapped: [wp (W x 3) | v0 (3) | a0 (3) | T (M)] | t_in (R) | t (R) | segment (R, int32)
+    int32_t W;
+    int32_t R;         // rows
+    int32_t rows_lds;  // 1: stage the sample data in LDS with the inputs
+    double t0;         // startTimeOffset
+    double* out;       // host-mapped: R x 10 rows
+    int64_t* info;     // host-mapped: [status]
+    double* scratch;   // device: segment scratch (tracks longer than kMaxLdsSeg)
+    double small[3 * kRefitArgW + 6 + kRefitArgW - 1];  // wp | v0 | a0 | T when W <= kRefitArgW
 };
-Workspace g_ws[64];
+constexpr int kRefitBlock = 256;
+__host__ __device__ inline size_t refit_in_doubles(int W, int R) {
+    return (size_t)3 * W + 6 + (W - 1) + 2 * (size_t)R + ((size_t)R + 1) / 2;
+}
+// LDS doubles: flag (2) | wp, v0, a0, T | solve scratch | coefficients | [sample data]
+__host__ __device__ inline size_t refit_lds_doubles(int M, bool lds, int rows_in_lds) {
+    return 2 + (((size_t)3 * (M + 1) + 6 + M + 1) & ~size_t(1)) + (lds ? (size_t)M * Seg::kSize : 0) +
+           vertex_doubles(M) + (size_t)M * 30 + (size_t)rows_in_lds * 2 + ((size_t)rows_in_lds + 1) / 2;
+}
+
+template <bool LDS>
+__global__ __launch_bounds__(kRefitBlock) void k_refit(RefitArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    int* s_err = reinterpret_cast<int*>(smem);
+    const int tid = threadIdx.x, W = a.W, M = W - 1, R = a.R;
+    EPP_TL(0);
+    const double* h_tin = a.in + 3 * W + 6 + M;
+    const double* h_tac = h_tin + R;
+    const int32_t* h_seg = reinterpret_cast<const int32_t*>(h_tac + R);
+    double* P = smem + 2;  // wp | v0 | a0 | T
+    const int nin = 3 * W + 6 + M;
+    const double* src = W <= kRefitArgW ? a.small : a.in;  // kernel arguments or host memory
+    for (int e = tid; e < nin; e += kRefitBlock) P[e] = src[e];
+    if (tid == 0) *s_err = 0;
+    double* rest = smem + 2 + (((size_t)nin + 1) & ~size_t(1));
+    double* scr = LDS ? rest : a.scratch;
+    double* dv = LDS ? rest + (size_t)M * Seg::kSize : rest;
+    double* rhs = dv + (size_t)(M + 1) * 15;
+    double* Tm = rhs + (size_t)(M + 1) * 12;
+    double* C = Tm + M;  // coefficients (M x 3 x 10)
+    // the sample data: one round of host reads now (in LDS) instead of after the solve
+    double* s_tin = C + (size_t)M * 30;
+    double* s_tac = s_tin + R;
+    int32_t* s_seg = reinterpret_cast<int32_t*>(s_tac + R);
+    if (a.rows_lds) {
+        for (int e = tid; e < R; e += kRefitBlock) {
+            s_tin[e] = h_tin[e];
+            s_tac[e] = h_tac[e];
+            s_seg[e] = h_seg[e];
+        }
+    }
+    __syncthreads();
+    const int st = solve_track<kRefitBlock>(P, M, 0.0, 0.0, P + 3 * W, P + 3 * W + 3, P + 3 * W + 6, scr, dv, rhs, Tm,
+                                            s_err, nullptr, C);
+    EPP_TL(7);
+    if (st == 0) {
+        __syncthreads();  // coefficients complete
+        auto row = [&](int j, double tin, double tac, int seg) {
+            const double* cs = C + (size_t)seg * 30;
+            double r[10];
+#pragma unroll
+            for (int d = 0; d < 3; ++d)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) r[3 * d + q] = poly_eval(cs + d * N, tin, q);
+            r[9] = tac + a.t0;  // sampling_times[i] + startTimeOffset
+            double2* o = reinterpret_cast<double2*>(a.out + (size_t)j * 10);
+#pragma unroll
+            for (int q = 0; q < 5; ++q) o[q] = make_double2(r[2 * q], r[2 * q + 1]);
+        };
+        if (a.rows_lds)
+            for (int j = tid; j < R; j += kRefitBlock) row(j, s_tin[j], s_tac[j], s_seg[j]);
+        else
+            for (int j = tid; j < R; j += kRefitBlock) row(j, h_tin[j], h_tac[j], h_seg[j]);
+    }
+    EPP_TL(11);
+    if (tid == 0) a.info[0] = st;
+}
+
 bool g_consts_ready[64];
+CachedWs g_minsnap_ws[64];
 
 epp_status ensure_consts() {
     int dev = 0;
@@ -658,20 +777,134 @@ epp_status ensure_consts() {
     return EPP_OK;
 }
 
-// Largest segment count of a batch (the offsets live on the device).
-int max_segments(const int32_t* d_off, int n_tracks, hipStream_t s, int* out) {
+// The track offsets of a batch (they live on the device; the launchers need the largest
+// segment count to size LDS and the total for the global scratch).
+epp_status read_offsets(const int32_t* d_off, int n_tracks, hipStream_t s, const char* what, int* max_m,
+                        int64_t* total_m) {
     std::vector<int32_t> off(n_tracks + 1);
     hipError_t e = hipMemcpyAsync(off.data(), d_off, off.size() * 4, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) {
-        set_error(std::string("epp: reading track offsets: ") + hipGetErrorString(e));
-        return -1;
+        set_error(std::string(what) + ": reading track offsets: " + hipGetErrorString(e));
+        return EPP_ERR_HIP;
     }
     int m = 1;
-    for (int t = 0; t < n_tracks; ++t) m = std::max(m, off[t + 1] - off[t] - 1);
-    *out = m;
-    return 0;
+    int64_t tot = 0;
+    for (int t = 0; t < n_tracks; ++t) {
+        const int mt = off[t + 1] - off[t] - 1;
+        m = std::max(m, mt);
+        tot += std::max(0, mt);
+    }
+    *max_m = m;
+    if (total_m) *total_m = tot;
+    return EPP_OK;
 }
+
+epp_status launch_error(const char* what) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_error(std::string(what) + ": " + hipGetErrorString(e));
+        return EPP_ERR_HIP;
+    }
+    return EPP_OK;
+}
+
+epp_status minsnap_batch(const double* wp, const int32_t* wp_offsets, int32_t n_tracks, double v_max, double a_max,
+                         const double* v0, const double* a0, const double* times_in, double* seg_times, double* coeffs,
+                         int32_t* status, void* stream, const char* what) {
+    if (n_tracks < 0 || (n_tracks > 0 && (!wp || !wp_offsets || !seg_times || !coeffs))) {
+        set_error(std::string(what) + ": invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    if (n_tracks == 0) return EPP_OK;
+    epp_status st = ensure_consts();
+    if (st) return st;
+    hipStream_t s = (hipStream_t)stream;
+    int max_m = 0;
+    int64_t total_m = 0;
+    if ((st = read_offsets(wp_offsets, n_tracks, s, what, &max_m, &total_m))) return st;
+    constexpr int kB = 64;  // one wavefront per track: the batch is throughput-bound
+    if (max_m <= kMaxLdsSeg) {
+        const size_t shm = ((size_t)max_m * Seg::kSize + vertex_doubles(max_m) + 2) * sizeof(double);
+        hipLaunchKernelGGL((k_minsnap<kB, true>), dim3(n_tracks), dim3(kB), shm, s, wp, wp_offsets, n_tracks, v_max,
+                           a_max, v0, a0, times_in, seg_times, coeffs, status, nullptr);
+        return launch_error(what);
+    }
+    // long tracks: segment scratch in a per-device workspace whose reuse by another stream
+    // waits for this launch (CachedWs)
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    CachedWs& ws = g_minsnap_ws[dev & 63];
+    std::lock_guard<std::mutex> lk(ws.mu);
+    const hipError_t e = ws.acquire(s, (size_t)std::max<int64_t>(total_m, 1) * Seg::kSize * sizeof(double));
+    if (e != hipSuccess) {
+        set_error(std::string(what) + ": workspace: " + hipGetErrorString(e));
+        return EPP_ERR_HIP;
+    }
+    const size_t shm = (vertex_doubles(max_m) + 2) * sizeof(double);
+    hipLaunchKernelGGL((k_minsnap<kB, false>), dim3(n_tracks), dim3(kB), shm, s, wp, wp_offsets, n_tracks, v_max, a_max,
+                       v0, a0, times_in, seg_times, coeffs, status, static_cast<double*>(ws.buf));
+    st = launch_error(what);
+    ws.release(s);
+    return st;
+}
+
+// Per-host-thread state of the single-track latency path: a stream, pinned host buffers
+// the kernel reads / writes directly, and the device segment scratch of long tracks.
+struct RefitCache {
+    hipStream_t s = nullptr;
+    int dev = -1;
+    double* h_in = nullptr;
+    size_t in_cap = 0;
+    char* h_out = nullptr;
+    size_t out_cap = 0;
+    double* d_scr = nullptr;
+    size_t scr_cap = 0;
+    std::vector<double> T, tin, tac;  // host side of the refit: times and samples
+    std::vector<int32_t> seg;
+    void release() {
+        if (h_in) (void)hipHostFree(h_in);
+        if (h_out) (void)hipHostFree(h_out);
+        if (d_scr) (void)hipFree(d_scr);
+        if (s) (void)hipStreamDestroy(s);
+        h_in = nullptr;
+        h_out = nullptr;
+        d_scr = nullptr;
+        s = nullptr;
+        in_cap = out_cap = scr_cap = 0;
+    }
+    ~RefitCache() { release(); }
+    epp_status ensure(size_t in_b, size_t out_b, size_t scr_b) {
+        int d = 0;
+        (void)hipGetDevice(&d);
+        if (d != dev) release();  // bound to another device: start over
+        dev = d;
+        hipError_t e = hipSuccess;
+        if (!s) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+        auto grow_host = [&](auto*& p, size_t& cap, size_t need) {
+            if (e != hipSuccess || need <= cap) return;
+            if (p) (void)hipHostFree(p);
+            p = nullptr;
+            cap = 0;
+            e = hipHostMalloc(reinterpret_cast<void**>(&p), need, hipHostMallocDefault);
+            if (e == hipSuccess) cap = need;
+        };
+        grow_host(h_in, in_cap, in_b);
+        grow_host(h_out, out_cap, out_b);
+        if (e == hipSuccess && scr_b > scr_cap) {
+            if (d_scr) (void)hipFree(d_scr);
+            d_scr = nullptr;
+            scr_cap = 0;
+            e = hipMalloc(reinterpret_cast<void**>(&d_scr), scr_b);
+            if (e == hipSuccess) scr_cap = scr_b;
+        }
+        if (e != hipSuccess) {
+            set_error(std::string("generateTrajectory: buffers: ") + hipGetErrorString(e));
+            return EPP_ERR_HIP;
+        }
+        return EPP_OK;
+    }
+};
 
 }  // namespace
 }  // namespace epp
@@ -680,98 +913,43 @@ using namespace epp;
 
 extern "C" {
 
-epp_status epp_minsnap_batch(const double* wp, const int32_t* wp_offsets, int32_t n_tracks,
-                             double v_max, double a_max, const double* v0, const double* a0,
-                             double* seg_times, double* coeffs, int32_t* status, void* stream) {
-    if (n_tracks < 0 || (n_tracks > 0 && (!wp || !wp_offsets || !seg_times || !coeffs))) {
-        set_error("epp_minsnap_batch: invalid argument");
-        return EPP_ERR_INVALID_ARGUMENT;
-    }
-    if (n_tracks == 0) return EPP_OK;
-    epp_status st = ensure_consts();
-    if (st) return st;
-    hipStream_t s = (hipStream_t)stream;
-    // The offsets live on the device; the launcher needs the largest segment count to
-    // size LDS, so read them back (n_tracks + 1 ints).
-    std::vector<int32_t> off(n_tracks + 1);
-    hipError_t e = hipMemcpyAsync(off.data(), wp_offsets, off.size() * 4, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) {
-        set_error(std::string("epp_minsnap_batch: offsets: ") + hipGetErrorString(e));
-        return EPP_ERR_HIP;
-    }
-    int max_m = 0;
-    for (int t = 0; t < n_tracks; ++t) max_m = std::max(max_m, off[t + 1] - off[t] - 1);
-    if (max_m < 1) max_m = 1;
-    const size_t vert_doubles = (size_t)(max_m + 1) * (15 + 12) + max_m;
-    if (max_m <= kMaxLdsSeg) {
-        const size_t shm = ((size_t)max_m * SegScratch::kSize + vert_doubles + 2) * sizeof(double);
-        hipLaunchKernelGGL((k_minsnap<true>), dim3(n_tracks), dim3(kWave), shm, s, wp, wp_offsets,
-                           n_tracks, v_max, a_max, v0, a0, seg_times, coeffs, status, nullptr,
-                           nullptr);
-    } else {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        Workspace& ws = g_ws[dev & 63];
-        std::vector<int64_t> goff(n_tracks);
-        size_t total = 0;
-        for (int t = 0; t < n_tracks; ++t) {
-            goff[t] = (int64_t)total;
-            total += (size_t)std::max(1, off[t + 1] - off[t] - 1) * SegScratch::kSize;
-        }
-        if (total > ws.cap) {
-            if (ws.d) (void)hipFree(ws.d);
-            ws.d = nullptr;
-            ws.cap = 0;
-            if (hipMalloc(&ws.d, total * sizeof(double)) != hipSuccess) return EPP_ERR_HIP;
-            ws.cap = total;
-        }
-        if ((size_t)n_tracks > ws.off_cap) {
-            if (ws.off) (void)hipFree(ws.off);
-            ws.off = nullptr;
-            ws.off_cap = 0;
-            if (hipMalloc(&ws.off, (size_t)n_tracks * 8) != hipSuccess) return EPP_ERR_HIP;
-            ws.off_cap = n_tracks;
-        }
-        e = hipMemcpyAsync(ws.off, goff.data(), (size_t)n_tracks * 8, hipMemcpyHostToDevice, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) return EPP_ERR_HIP;
-        const size_t shm = (vert_doubles + 2) * sizeof(double);
-        hipLaunchKernelGGL((k_minsnap<false>), dim3(n_tracks), dim3(kWave), shm, s, wp, wp_offsets,
-                           n_tracks, v_max, a_max, v0, a0, seg_times, coeffs, status, ws.d, ws.off);
-    }
-    e = hipGetLastError();
-    if (e != hipSuccess) {
-        set_error(std::string("epp_minsnap_batch: ") + hipGetErrorString(e));
-        return EPP_ERR_HIP;
-    }
-    return EPP_OK;
+epp_status epp_minsnap_batch(const double* wp, const int32_t* wp_offsets, int32_t n_tracks, double v_max,
+                             double a_max, const double* v0, const double* a0, double* seg_times, double* coeffs,
+                             int32_t* status, void* stream) {
+    return minsnap_batch(wp, wp_offsets, n_tracks, v_max, a_max, v0, a0, nullptr, seg_times, coeffs, status, stream,
+                         "epp_minsnap_batch");
 }
 
-epp_status epp_sample_count(const double* seg_times, const int32_t* wp_offsets, int32_t n_tracks,
-                            double dt, int64_t* row_counts, void* stream) {
+epp_status epp_minsnap_batch_times(const double* wp, const int32_t* wp_offsets, int32_t n_tracks, const double* v0,
+                                   const double* a0, const double* seg_times_in, double* coeffs, int32_t* status,
+                                   void* stream) {
+    if (n_tracks > 0 && !seg_times_in) {
+        set_error("epp_minsnap_batch_times: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    // the kernel copies the caller's times to seg_times: in place is fine (same index)
+    return minsnap_batch(wp, wp_offsets, n_tracks, 0.0, 0.0, v0, a0, seg_times_in, const_cast<double*>(seg_times_in),
+                         coeffs, status, stream, "epp_minsnap_batch_times");
+}
+
+epp_status epp_sample_count(const double* seg_times, const int32_t* wp_offsets, int32_t n_tracks, double dt,
+                            int64_t* row_counts, void* stream) {
     if (n_tracks < 0 || (n_tracks > 0 && (!seg_times || !wp_offsets || !row_counts))) {
         set_error("epp_sample_count: invalid argument");
         return EPP_ERR_INVALID_ARGUMENT;
     }
     if (n_tracks == 0) return EPP_OK;
     int max_m = 0;
-    if (max_segments(wp_offsets, n_tracks, (hipStream_t)stream, &max_m)) return EPP_ERR_HIP;
-    hipLaunchKernelGGL(k_sample_count, dim3(n_tracks), dim3(kWave), (size_t)(max_m + 2) * 8,
-                       (hipStream_t)stream, seg_times, wp_offsets, n_tracks, dt, row_counts);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        set_error(std::string("epp_sample_count: ") + hipGetErrorString(e));
-        return EPP_ERR_HIP;
-    }
-    return EPP_OK;
+    epp_status st = read_offsets(wp_offsets, n_tracks, (hipStream_t)stream, "epp_sample_count", &max_m, nullptr);
+    if (st) return st;
+    hipLaunchKernelGGL(k_sample_count, dim3(n_tracks), dim3(kWave), (size_t)(max_m + 2) * 8, (hipStream_t)stream,
+                       seg_times, wp_offsets, n_tracks, dt, row_counts);
+    return launch_error("epp_sample_count");
 }
 
-epp_status epp_sample_batch(const double* seg_times, const double* coeffs, const int32_t* wp_offsets,
-                            int32_t n_tracks, double dt, const double* t0, const int64_t* row_offsets,
-                            double* rows, void* stream) {
-    if (n_tracks < 0 ||
-        (n_tracks > 0 && (!seg_times || !coeffs || !wp_offsets || !row_offsets || !rows))) {
+epp_status epp_sample_batch(const double* seg_times, const double* coeffs, const int32_t* wp_offsets, int32_t n_tracks,
+                            double dt, const double* t0, const int64_t* row_offsets, double* rows, void* stream) {
+    if (n_tracks < 0 || (n_tracks > 0 && (!seg_times || !coeffs || !wp_offsets || !row_offsets || !rows))) {
         set_error("epp_sample_batch: invalid argument");
         return EPP_ERR_INVALID_ARGUMENT;
     }
@@ -779,27 +957,21 @@ epp_status epp_sample_batch(const double* seg_times, const double* coeffs, const
     epp_status st = ensure_consts();
     if (st) return st;
     int max_m = 0;
-    if (max_segments(wp_offsets, n_tracks, (hipStream_t)stream, &max_m)) return EPP_ERR_HIP;
+    if ((st = read_offsets(wp_offsets, n_tracks, (hipStream_t)stream, "epp_sample_batch", &max_m, nullptr))) return st;
     const size_t shm = ((size_t)((max_m + 1) & ~1) + 3 * kRowChunk + 2) * 8;
-    hipLaunchKernelGGL(k_sample_rows, dim3(n_tracks), dim3(kWave), shm, (hipStream_t)stream, seg_times,
-                       coeffs, wp_offsets, n_tracks, dt, t0, row_offsets, rows, (int64_t)INT64_MAX);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        set_error(std::string("epp_sample_batch: ") + hipGetErrorString(e));
-        return EPP_ERR_HIP;
-    }
-    return EPP_OK;
+    hipLaunchKernelGGL(k_sample_rows, dim3(n_tracks), dim3(kWave), shm, (hipStream_t)stream, seg_times, coeffs,
+                       wp_offsets, n_tracks, dt, t0, row_offsets, rows, (int64_t)INT64_MAX);
+    return launch_error("epp_sample_batch");
 }
 
 // poly_traj::generateTrajectory with host buffers (src/trajectory_generator.cpp:12-100).
-// Latency path (one track, e.g. the 50 Hz refit): per-thread cached device / pinned
-// buffers and stream, one upload, the three kernels back to back (the host knows the
-// segment count, so no offset read-backs), one download.  The row buffer is sized from
-// the segment times recomputed on the host (+16 rows of slack; the kernel never writes
-// past it, and a short buffer is detected and redone).
-epp_status epp_generate_trajectory_host(const double* wp, int32_t n_wp, double v_max, double a_max,
-                                        double dt, double t0, const double v0[3],
-                                        const double a0[3], double** rows_out, int64_t* n_rows) {
+// The host computes the segment times (estimateSegmentTimesNfabian with its libm, as the
+// reference, or the caller's) and runs Trajectory::evaluateRange's sample recurrence
+// (src/trajectory.cpp:81-141: exact count, times and segments); one launch of k_refit then
+// solves and writes the rows straight into pinned memory; one stream synchronisation.
+epp_status generate_trajectory(const double* wp, int32_t n_wp, const double* times, double v_max, double a_max,
+                               double dt, double t0, const double v0[3], const double a0[3], double** rows_out,
+                               int64_t* n_rows) {
     if (!rows_out || !n_rows || (n_wp > 0 && !wp)) {
         set_error("generateTrajectory: invalid argument");
         return EPP_ERR_INVALID_ARGUMENT;
@@ -812,121 +984,104 @@ epp_status epp_generate_trajectory_host(const double* wp, int32_t n_wp, double v
     }
     epp_status rc = ensure_consts();
     if (rc) return rc;
+    static thread_local RefitCache c;
     const int M = n_wp - 1;
-    double t_end = 0.0;  // host estimate of the duration (capacity only)
-    for (int i = 0; i < M; ++i) t_end += nfabian(wp + 3 * i, wp + 3 * (i + 1), v_max, a_max);
-    int64_t cap = (dt > 0 && std::isfinite(t_end)) ? (int64_t)(t_end / dt) + 16 : 16;
-    struct Cache {
-        char* d = nullptr;
-        size_t dcap = 0;
-        char* h = nullptr;
-        size_t hcap = 0;
-        hipStream_t s = nullptr;
-    };
-    static thread_local Cache c;
-    auto a16 = [](size_t x) { return (x + 15) & ~size_t(15); };
-    const bool lds = M <= kMaxLdsSeg;
-    for (int pass = 0; pass < 2; ++pass) {
-        // device: [in: wp | va | t0 | off(2 i32) | goff | roff] [T | C | scratch] [rows (cap) | cnt | status]
-        const size_t in_b = a16((size_t)n_wp * 24 + 48 + 8 + 8 + 8 + 8);
-        const size_t mid_b = a16((size_t)M * 8) + a16((size_t)M * 240) + (lds ? 0 : a16((size_t)M * SegScratch::kSize * 8));
-        const size_t out_b = (size_t)cap * 80 + 16;
-        const size_t need = in_b + mid_b + out_b;
-        if (!c.s && hipStreamCreateWithFlags(&c.s, hipStreamNonBlocking) != hipSuccess) {
-            set_error("generateTrajectory: stream");
-            return EPP_ERR_HIP;
-        }
-        if (need > c.dcap) {
-            if (c.d) (void)hipFree(c.d);
-            c.d = nullptr;
-            c.dcap = 0;
-            if (hipMalloc(&c.d, need) != hipSuccess) {
-                set_error("generateTrajectory: hipMalloc failed");
-                return EPP_ERR_HIP;
-            }
-            c.dcap = need;
-        }
-        const size_t hneed = std::max(in_b, out_b);
-        if (hneed > c.hcap) {
-            if (c.h) (void)hipHostFree(c.h);
-            c.h = nullptr;
-            c.hcap = 0;
-            if (hipHostMalloc(&c.h, hneed, 0) != hipSuccess) {
-                set_error("generateTrajectory: hipHostMalloc failed");
-                return EPP_ERR_HIP;
-            }
-            c.hcap = hneed;
-        }
-        // inputs, staged in pinned memory
-        double* h_wp = (double*)c.h;
-        std::memcpy(h_wp, wp, (size_t)n_wp * 24);
-        double* h_va = h_wp + (size_t)n_wp * 3;
-        for (int k = 0; k < 3; ++k) {
-            h_va[k] = v0 ? v0[k] : 0.0;
-            h_va[3 + k] = a0 ? a0[k] : 0.0;
-        }
-        h_va[6] = t0;
-        int32_t* h_off = (int32_t*)(h_va + 7);
-        h_off[0] = 0;
-        h_off[1] = n_wp;
-        int64_t* h_goff = (int64_t*)(h_off + 2);
-        h_goff[0] = 0;  // global scratch offset of the track
-        h_goff[1] = 0;  // row offset
-        double* d_wp = (double*)c.d;
-        double* d_va = d_wp + (size_t)n_wp * 3;
-        double* d_t0 = d_va + 6;
-        int32_t* d_off = (int32_t*)(d_va + 7);
-        int64_t* d_goff = (int64_t*)(d_off + 2);
-        int64_t* d_roff = d_goff + 1;
-        double* d_T = (double*)(c.d + in_b);
-        double* d_C = (double*)(c.d + in_b + a16((size_t)M * 8));
-        double* d_scr = (double*)(c.d + in_b + a16((size_t)M * 8) + a16((size_t)M * 240));
-        double* d_rows = (double*)(c.d + in_b + mid_b);
-        int64_t* d_cnt = (int64_t*)(d_rows + (size_t)cap * 10);
-        int32_t* d_status = (int32_t*)(d_cnt + 1);
-        hipStream_t s = c.s;
-        hipError_t e = hipMemcpyAsync(c.d, c.h, in_b, hipMemcpyHostToDevice, s);
-        const size_t vert_doubles = (size_t)(M + 1) * (15 + 12) + M;
-        if (lds) {
-            const size_t shm = ((size_t)M * SegScratch::kSize + vert_doubles + 2) * sizeof(double);
-            hipLaunchKernelGGL((k_minsnap<true>), dim3(1), dim3(kWave), shm, s, d_wp, d_off, 1, v_max, a_max, d_va,
-                               d_va + 3, d_T, d_C, d_status, nullptr, nullptr);
-        } else {
-            hipLaunchKernelGGL((k_minsnap<false>), dim3(1), dim3(kWave), (vert_doubles + 2) * sizeof(double), s,
-                               d_wp, d_off, 1, v_max, a_max, d_va, d_va + 3, d_T, d_C, d_status, d_scr, d_goff);
-        }
-        hipLaunchKernelGGL(k_sample_count, dim3(1), dim3(kWave), (size_t)(M + 2) * 8, s, d_T, d_off, 1, dt, d_cnt);
-        hipLaunchKernelGGL(k_sample_rows, dim3(1), dim3(kWave), ((size_t)((M + 1) & ~1) + 3 * kRowChunk + 2) * 8, s,
-                           d_T, d_C, d_off, 1, dt, d_t0, d_roff, d_rows, cap);
-        if (e == hipSuccess) e = hipGetLastError();
-        if (e == hipSuccess) e = hipMemcpyAsync(c.h, d_rows, out_b, hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) {
-            set_error(std::string("generateTrajectory: ") + hipGetErrorString(e));
-            return EPP_ERR_HIP;
-        }
-        const int64_t count = *(const int64_t*)(c.h + (size_t)cap * 80);
-        const int32_t status = *(const int32_t*)(c.h + (size_t)cap * 80 + 8);
-        if (status != 0) {
-            set_error(status == -2 ? "Segment times need to be greater than zero" : "min-snap solve failed");
+    c.T.resize(M);
+    for (int i = 0; i < M; ++i) {
+        c.T[i] = times ? times[i] : nfabian(wp + 3 * i, wp + 3 * (i + 1), v_max, a_max);
+        if (!(c.T[i] > 0)) {  // CHECK_GT(segment_time, 0)  impl :297
+            set_error("Segment times need to be greater than zero");
             return EPP_ERR_RUNTIME;
         }
-        if (count > cap) {  // host estimate short: once more with the exact size
-            cap = count + 16;
-            continue;
-        }
-        double* host_rows = (double*)std::malloc((size_t)std::max<int64_t>(count, 1) * 80);
-        if (!host_rows) {
-            set_error("generateTrajectory: out of host memory");
-            return EPP_ERR_RUNTIME;
-        }
-        if (count > 0) std::memcpy(host_rows, c.h, (size_t)count * 80);
-        *rows_out = host_rows;
-        *n_rows = count;
-        return EPP_OK;
     }
-    set_error("generateTrajectory: row count");
-    return EPP_ERR_RUNTIME;
+    c.tin.clear();
+    c.tac.clear();
+    c.seg.clear();
+    if (dt > 0) {
+        RangeIter it;
+        it.init(c.T.data(), M);
+        int sg;
+        double ti, ta;
+        while (it.next(sg, ti, ta)) {
+            c.seg.push_back(sg);
+            c.tin.push_back(ti);
+            c.tac.push_back(ta);
+            it.advance(dt);
+        }
+    }
+    const int R = (int)c.tin.size();
+    const bool lds = M <= kMaxLdsSeg;
+    if ((rc = c.ensure(refit_in_doubles(n_wp, R) * 8, (size_t)R * 80 + 16, lds ? 0 : (size_t)M * Seg::kSize * 8))) return rc;
+    double* in = c.h_in;
+    std::memcpy(in, wp, (size_t)n_wp * 24);
+    for (int k = 0; k < 3; ++k) {
+        in[3 * n_wp + k] = v0 ? v0[k] : 0.0;
+        in[3 * n_wp + 3 + k] = a0 ? a0[k] : 0.0;
+    }
+    std::memcpy(in + 3 * n_wp + 6, c.T.data(), (size_t)M * 8);
+    double* ins = in + 3 * n_wp + 6 + M;
+    if (R) {
+        std::memcpy(ins, c.tin.data(), (size_t)R * 8);
+        std::memcpy(ins + R, c.tac.data(), (size_t)R * 8);
+        std::memcpy(ins + 2 * R, c.seg.data(), (size_t)R * 4);
+    }
+    RefitArgs a;
+    a.in = in;
+    a.W = n_wp;
+    a.R = R;
+    a.t0 = t0;
+    if (n_wp <= kRefitArgW) std::memcpy(a.small, in, (size_t)(3 * n_wp + 6 + M) * 8);
+    // stage the sample data in LDS when it fits next to the solve's scratch
+    a.rows_lds = refit_lds_doubles(M, lds, R) * 8 <= 160u * 1024u ? 1 : 0;
+    a.out = reinterpret_cast<double*>(c.h_out + 16);
+    a.info = reinterpret_cast<int64_t*>(c.h_out);
+    a.scratch = c.d_scr;
+    a.info[0] = -100;
+    const size_t shm = refit_lds_doubles(M, lds, a.rows_lds ? R : 0) * sizeof(double);
+    if (lds) hipLaunchKernelGGL(k_refit<true>, dim3(1), dim3(kRefitBlock), shm, c.s, a);
+    else hipLaunchKernelGGL(k_refit<false>, dim3(1), dim3(kRefitBlock), shm, c.s, a);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(c.s);
+    if (e != hipSuccess) {
+        set_error(std::string("generateTrajectory: ") + hipGetErrorString(e));
+        return EPP_ERR_HIP;
+    }
+    if (a.info[0] != 0) {
+        set_error(a.info[0] == -2 ? "Segment times need to be greater than zero" : "min-snap solve failed");
+        return EPP_ERR_RUNTIME;
+    }
+    double* host_rows = (double*)std::malloc((size_t)std::max(R, 1) * 80);
+    if (!host_rows) {
+        set_error("generateTrajectory: out of host memory");
+        return EPP_ERR_RUNTIME;
+    }
+    if (R) std::memcpy(host_rows, a.out, (size_t)R * 80);
+    *rows_out = host_rows;
+    *n_rows = R;
+    return EPP_OK;
 }
+
+epp_status epp_generate_trajectory_host(const double* wp, int32_t n_wp, double v_max, double a_max, double dt,
+                                        double t0, const double v0[3], const double a0[3], double** rows_out,
+                                        int64_t* n_rows) {
+    return generate_trajectory(wp, n_wp, nullptr, v_max, a_max, dt, t0, v0, a0, rows_out, n_rows);
+}
+
+epp_status epp_generate_trajectory_times_host(const double* wp, int32_t n_wp, const double* seg_times, double dt,
+                                              double t0, const double v0[3], const double a0[3], double** rows_out,
+                                              int64_t* n_rows) {
+    if (n_wp >= 2 && !seg_times) {
+        set_error("generateTrajectory: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    return generate_trajectory(wp, n_wp, seg_times, 0.0, 0.0, dt, t0, v0, a0, rows_out, n_rows);
+}
+
+#ifdef EPP_REFIT_TL
+// diagnostics builds only: the last refit's phase timeline (2 workgroups x 16 stamps)
+epp_status epp_dbg_refit_tl(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_refit_tl), sizeof(g_refit_tl)) == hipSuccess ? EPP_OK : EPP_ERR_HIP;
+}
+#endif
 
 }  // extern "C"

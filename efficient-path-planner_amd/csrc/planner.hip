@@ -17,6 +17,7 @@
 #include <mutex>
 #include <string>
 
+#include "cached_ws.h"
 #include "epp_internal.h"
 
 namespace epp {
@@ -948,13 +949,6 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
     return last("epp_knn_grid");
 }
 
-struct CachedWs {
-    std::mutex mu;
-    void* buf = nullptr;
-    size_t cap = 0;
-    hipEvent_t done = nullptr;
-    bool used = false;
-};
 CachedWs g_knn_ws[64];
 CachedWs g_compact_ws[64];
 
@@ -1128,21 +1122,13 @@ epp_status epp_knn_grid(const double* nodes, int32_t n, int32_t k, double max_di
     hipStream_t s = (hipStream_t)stream;
     const KnnLayout L = knn_layout(n);
     hipError_t e = hipSuccess;
-    if (!c.done) e = hipEventCreateWithFlags(&c.done, hipEventDisableTiming);
-    if (e == hipSuccess && c.used) e = hipStreamWaitEvent(s, c.done, 0);
-    if (e == hipSuccess && L.bytes > c.cap) {
-        if (c.buf) e = hipFree(c.buf);
-        c.buf = nullptr;
-        c.cap = 0;
-        if (e == hipSuccess) e = hipMalloc(&c.buf, L.bytes);
-        if (e == hipSuccess) c.cap = L.bytes;
-    }
+    e = c.acquire(s, L.bytes);
     if (e != hipSuccess) {
         set_error(std::string("epp_knn_grid: workspace: ") + hipGetErrorString(e));
         return EPP_ERR_HIP;
     }
     const epp_status rc = knn_grid_launch(nodes, n, k, max_dist, nbr, static_cast<char*>(c.buf), L, s);
-    if (hipEventRecord(c.done, s) == hipSuccess) c.used = true;
+    c.release(s);
     return rc;
 }
 
@@ -1161,22 +1147,14 @@ epp_status epp_compact_states(const double* xyz, const uint8_t* valid, int64_t n
     CachedWs& c = g_compact_ws[dev & 63];
     std::lock_guard<std::mutex> lk(c.mu);
     hipError_t e = hipSuccess;
-    if (!c.done) e = hipEventCreateWithFlags(&c.done, hipEventDisableTiming);
-    if (e == hipSuccess && c.used) e = hipStreamWaitEvent(s, c.done, 0);
-    if (e == hipSuccess && (size_t)nb * 4 > c.cap) {
-        if (c.buf) e = hipFree(c.buf);
-        c.buf = nullptr;
-        c.cap = 0;
-        if (e == hipSuccess) e = hipMalloc(&c.buf, (size_t)nb * 4);
-        if (e == hipSuccess) c.cap = (size_t)nb * 4;
-    }
+    e = c.acquire(s, (size_t)nb * 4);
     if (e != hipSuccess) {
         set_error(std::string("epp_compact_states: workspace: ") + hipGetErrorString(e));
         return EPP_ERR_HIP;
     }
     counts = static_cast<int*>(c.buf);
     const epp_status rc = epp_compact_states_ws(xyz, valid, n, out, n_out, counts, c.cap, stream);
-    if (hipEventRecord(c.done, s) == hipSuccess) c.used = true;
+    c.release(s);
     return rc;
 }
 

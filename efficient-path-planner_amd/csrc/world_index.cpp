@@ -12,7 +12,6 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
-#include <map>
 #include <cstring>
 #include <new>
 #include <string>
@@ -123,8 +122,8 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
     v.limz = (float)(4 * nd[2]) * (1.0f + 0x1.0p-20f);
     v.fmaxx = (float)(4 * nd[0] - 1); v.fmaxy = (float)(4 * nd[1] - 1); v.fmaxz = (float)(4 * nd[2] - 1);
     const int ncell = nd[0] * nd[1] * nd[2];
-    std::vector<std::vector<uint16_t>> cells(ncell);
     std::vector<uint64_t> mask(ncell, 0);
+    std::vector<int> cbox((size_t)n * 6);  // per OBB: first / last coarse cell per axis
     for (int i = 0; i < n; ++i) {
         const double* lo = &hw.aabbs[(size_t)i * 6];
         const double* hi = lo + 3;
@@ -132,19 +131,32 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
         for (int k = 0; k < 3; ++k) {
             f0[k] = fine_index(fine_coord(lo[k], of[k], i4[k]), nd[k]);
             f1[k] = fine_index(fine_coord(hi[k], of[k], i4[k]), nd[k]);
+            cbox[(size_t)i * 6 + k] = f0[k] >> 2;
+            cbox[(size_t)i * 6 + 3 + k] = f1[k] >> 2;
         }
         meta[i] |= ((uint32_t)(f0[0] >> 2) << 8) | ((uint32_t)(f0[1] >> 2) << 16) |
                    ((uint32_t)(f0[2] >> 2) << 24);
-        for (int z = f0[2] >> 2; z <= f1[2] >> 2; ++z)
-            for (int y = f0[1] >> 2; y <= f1[1] >> 2; ++y)
-                for (int x = f0[0] >> 2; x <= f1[0] >> 2; ++x)
-                    cells[((size_t)z * nd[1] + y) * nd[0] + x].push_back((uint16_t)i);
         for (int z = f0[2]; z <= f1[2]; ++z)
             for (int y = f0[1]; y <= f1[1]; ++y)
                 for (int x = f0[0]; x <= f1[0]; ++x) {
                     const size_t c = ((size_t)(z >> 2) * nd[1] + (y >> 2)) * nd[0] + (x >> 2);
                     mask[c] |= 1ull << (((z & 3) * 4 + (y & 3)) * 4 + (x & 3));
                 }
+    }
+    // coarse cell lists (CSR, ascending OBB id): count, scan, scatter
+    std::vector<uint32_t> cell_start(ncell + 1, 0);
+    auto for_coarse = [&](int i, auto&& fn) {
+        const int* b = &cbox[(size_t)i * 6];
+        for (int z = b[2]; z <= b[5]; ++z)
+            for (int y = b[1]; y <= b[4]; ++y)
+                for (int x = b[0]; x <= b[3]; ++x) fn(((size_t)z * nd[1] + y) * nd[0] + x);
+    };
+    for (int i = 0; i < n; ++i) for_coarse(i, [&](size_t c) { ++cell_start[c + 1]; });
+    for (int c = 0; c < ncell; ++c) cell_start[c + 1] += cell_start[c];
+    std::vector<uint16_t> cell_obb(cell_start[ncell]);
+    {
+        std::vector<uint32_t> fill(cell_start.begin(), cell_start.end() - 1);
+        for (int i = 0; i < n; ++i) for_coarse(i, [&](size_t c) { cell_obb[fill[c]++] = (uint16_t)i; });
     }
     // ---- fine cell classes (k_states fast path) ------------------------------------
     // Per fine cell a u16 class: 0 = no inflated AABB reaches it (valid, no test), else
@@ -186,39 +198,77 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
             }
         }
         const size_t cells = (size_t)bd[0] * bd[1] * bd[2];
-        std::vector<std::vector<uint16_t>> sets(cells);
-        for (int i = 0; i < n; ++i) {
-            int lo_i[3], hi_i[3];
-            for (int k = 0; k < 3; ++k) {
-                lo_i[k] = bm_axis(hw.aabbs[(size_t)i * 6 + k], bo[k], bi[k]);
-                hi_i[k] = bm_axis(hw.aabbs[(size_t)i * 6 + 3 + k], bo[k], bi[k]);
-            }
-            for (int z = lo_i[2]; z <= hi_i[2]; ++z)
-                for (int y = lo_i[1]; y <= hi_i[1]; ++y)
-                    for (int x = lo_i[0]; x <= hi_i[0]; ++x)
-                        sets[((size_t)z * bd[1] + y) * bd[0] + x].push_back((uint16_t)i);
+        // the records and the class table alone already exceed the staging budget: coarsen
+        // before building any list
+        if (align16((size_t)n * kRecDoubles * 8) + align16((cells + 1) * 2) > kStageBudget && target > 4096.0) {
+            cls_target = target / 2;
+            continue;
         }
+        // Per-cell candidate lists (ascending OBB id) as CSR: count, scan, scatter — the
+        // OBBs are visited in id order, so every list comes out sorted.
+        std::vector<uint32_t> cstart(cells + 1, 0);
+        std::vector<int> box((size_t)n * 6);
+        for (int i = 0; i < n; ++i)
+            for (int k = 0; k < 3; ++k) {
+                box[(size_t)i * 6 + k] = bm_axis(hw.aabbs[(size_t)i * 6 + k], bo[k], bi[k]);
+                box[(size_t)i * 6 + 3 + k] = bm_axis(hw.aabbs[(size_t)i * 6 + 3 + k], bo[k], bi[k]);
+            }
+        auto for_cells = [&](int i, auto&& fn) {
+            const int* b = &box[(size_t)i * 6];
+            for (int z = b[2]; z <= b[5]; ++z)
+                for (int y = b[1]; y <= b[4]; ++y) {
+                    const size_t row = ((size_t)z * bd[1] + y) * bd[0];
+                    for (int x = b[0]; x <= b[3]; ++x) fn(row + x);
+                }
+        };
+        for (int i = 0; i < n; ++i) for_cells(i, [&](size_t c) { ++cstart[c + 1]; });
+        for (size_t c = 0; c < cells; ++c) cstart[c + 1] += cstart[c];
+        std::vector<uint16_t> cid(cstart[cells]);
+        {
+            std::vector<uint32_t> fill(cstart.begin(), cstart.end() - 1);
+            for (int i = 0; i < n; ++i) for_cells(i, [&](size_t c) { cid[fill[c]++] = (uint16_t)i; });
+        }
+        // Equal lists share one id (first occurrence in cell order), found through an
+        // open-addressing hash table over the lists.
         cls.assign(cells + 1, 0);  // + the zero sentinel (out-of-grid lookups)
-        std::map<std::vector<uint16_t>, uint16_t> ids;
-        hdr.assign(1, 0u);  // list 0: unused (class 0 = free)
+        hdr.assign(1, 0u);         // list 0: unused (class 0 = free)
         flat.clear();
+        std::vector<uint32_t> slot_cell;  // per table slot: 1 + the cell holding the list (0 = empty)
+        std::vector<uint16_t> slot_id;
+        size_t occupied = 0;
+        for (size_t c = 0; c < cells; ++c) occupied += cstart[c + 1] != cstart[c];
+        size_t tsize = 64;
+        while (tsize < 2 * occupied) tsize <<= 1;
+        slot_cell.assign(tsize, 0u);
+        slot_id.assign(tsize, 0);
         bool full = false;
         for (size_t c = 0; c < cells && !full; ++c) {
-            if (sets[c].empty()) continue;
-            auto it = ids.find(sets[c]);
-            if (it != ids.end()) {
-                cls[c] = it->second;
-                continue;
+            const uint32_t b0 = cstart[c], m = cstart[c + 1] - b0;
+            if (m == 0) continue;
+            uint64_t h = 1469598103934665603ull;  // FNV-1a over the ids
+            for (uint32_t j = 0; j < m; ++j) h = (h ^ cid[b0 + j]) * 1099511628211ull;
+            size_t t = (size_t)(h ^ (h >> 29)) & (tsize - 1);
+            bool found = false;
+            while (slot_cell[t]) {
+                const size_t o = slot_cell[t] - 1;
+                const uint32_t ob = cstart[o], om = cstart[o + 1] - ob;
+                if (om == m && std::equal(&cid[b0], &cid[b0] + m, &cid[ob])) {
+                    cls[c] = slot_id[t];
+                    found = true;
+                    break;
+                }
+                t = (t + 1) & (tsize - 1);
             }
-            const size_t m = sets[c].size();
+            if (found) continue;
             if (hdr.size() >= 65535 || flat.size() + m >= (size_t(1) << 20) || m > kListMaxLen) {
                 full = true;
                 break;
             }
             const uint16_t id = (uint16_t)hdr.size();
-            hdr.push_back((uint32_t)(flat.size() << 12) | (uint32_t)m);  // start : 20, count : 12
-            flat.insert(flat.end(), sets[c].begin(), sets[c].end());
-            ids.emplace(sets[c], id);
+            hdr.push_back((uint32_t)(flat.size() << 12) | m);  // start : 20, count : 12
+            flat.insert(flat.end(), &cid[b0], &cid[b0] + m);
+            slot_cell[t] = (uint32_t)c + 1;
+            slot_id[t] = id;
             cls[c] = id;
         }
         if (full) {  // more distinct lists than a u16 class can name: a coarser grid
@@ -244,8 +294,6 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
         v.n_lists = (uint32_t)hdr.size();
         break;
     }
-    std::vector<uint32_t> cell_start(ncell + 1, 0);
-    for (int c = 0; c < ncell; ++c) cell_start[c + 1] = cell_start[c] + (uint32_t)cells[c].size();
     const size_t n_entries = cell_start[ncell];
     // ---- pack (layout in epp_internal.h) ---------------------------------------
     const size_t off_mask = 0;
@@ -277,11 +325,7 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
     char* b = &hw.blob[0];
     std::memcpy(b + off_mask, mask.data(), mask.size() * 8);
     std::memcpy(b + off_cs, cell_start.data(), cell_start.size() * 4);
-    size_t pos = off_co;
-    for (int c = 0; c < ncell; ++c) {
-        if (!cells[c].empty()) std::memcpy(b + pos, cells[c].data(), cells[c].size() * 2);
-        pos += cells[c].size() * 2;
-    }
+    if (n_entries) std::memcpy(b + off_co, cell_obb.data(), n_entries * 2);
     std::memcpy(b + off_meta, meta.data(), meta.size() * 4);
     std::memcpy(b + off_soa, soa.data(), soa.size() * sizeof(double));
     if (!aos.empty()) std::memcpy(b + off_aos, aos.data(), aos.size() * sizeof(double));
@@ -304,30 +348,43 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
 
 // The device allocation holds the blob followed by a copy of the WorldView (kernels
 // that keep only a pointer to it read the fields they need through the scalar cache).
+// The upload goes through a pinned staging buffer on the world's own stream (one DMA,
+// no pageable bounce); the caller has made sure no kernel still reads the old blob.
 bool upload(HostWorld& hw) {
     const size_t bytes = hw.blob.size();
     const size_t view_off = (bytes + 255) & ~size_t(255);
     const size_t need = view_off + sizeof(WorldView);
-    if (need > hw.d_capacity) {
+    hipError_t e = hipSuccess;
+    if (!hw.stream) e = hipStreamCreateWithFlags(&hw.stream, hipStreamNonBlocking);
+    if (e == hipSuccess && need > hw.d_capacity) {
         if (hw.d_blob) (void)hipFree(hw.d_blob);
         hw.d_blob = nullptr;
         hw.d_capacity = 0;
-        hipError_t e = hipMalloc(&hw.d_blob, need);
-        if (e != hipSuccess) {
-            set_error(std::string("epp_world: hipMalloc: ") + hipGetErrorString(e));
-            return false;
-        }
-        hw.d_capacity = need;
+        e = hipMalloc(&hw.d_blob, need);
+        if (e == hipSuccess) hw.d_capacity = need;
+    }
+    if (e == hipSuccess && need > hw.h_capacity) {
+        if (hw.h_stage) (void)hipHostFree(hw.h_stage);
+        hw.h_stage = nullptr;
+        hw.h_capacity = 0;
+        e = hipHostMalloc(&hw.h_stage, need, hipHostMallocDefault);
+        if (e == hipSuccess) hw.h_capacity = need;
+    }
+    if (e != hipSuccess) {
+        set_error(std::string("epp_world: allocation: ") + hipGetErrorString(e));
+        return false;
     }
     hw.view.blob = (const unsigned char*)hw.d_blob;
     hw.d_view = reinterpret_cast<const WorldView*>(static_cast<char*>(hw.d_blob) + view_off);
-    hipError_t e = hipMemcpy(hw.d_blob, hw.blob.data(), bytes, hipMemcpyHostToDevice);
-    if (e == hipSuccess)
-        e = hipMemcpy(static_cast<char*>(hw.d_blob) + view_off, &hw.view, sizeof(WorldView), hipMemcpyHostToDevice);
+    std::memcpy(hw.h_stage, hw.blob.data(), bytes);
+    std::memcpy(static_cast<char*>(hw.h_stage) + view_off, &hw.view, sizeof(WorldView));
+    e = hipMemcpyAsync(hw.d_blob, hw.h_stage, need, hipMemcpyHostToDevice, hw.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(hw.stream);
     if (e != hipSuccess) {
-        set_error(std::string("epp_world: hipMemcpy: ") + hipGetErrorString(e));
+        set_error(std::string("epp_world: upload: ") + hipGetErrorString(e));
         return false;
     }
+    ++hw.generation;
     return true;
 }
 
@@ -380,7 +437,18 @@ epp_status epp_world_update(epp_world* w, const epp_obb* obbs, int32_t n) {
 epp_status epp_world_destroy(epp_world* w) {
     if (!w) return EPP_OK;
     if (w->d_blob) (void)hipFree(w->d_blob);
+    if (w->h_stage) (void)hipHostFree(w->h_stage);
+    if (w->stream) (void)hipStreamDestroy(w->stream);
     delete w;
+    return EPP_OK;
+}
+
+epp_status epp_world_generation(const epp_world* w, uint64_t* generation) {
+    if (!w || !generation) {
+        epp::set_error("epp_world_generation: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    *generation = w->generation;
     return EPP_OK;
 }
 

@@ -67,14 +67,18 @@ def lib() -> C.CDLL:
             "epp_world_destroy": (i32, [vp]),
             "epp_world_num_obbs": (i32, [vp, C.POINTER(i32)]),
             "epp_world_get_aabbs": (i32, [vp, vp]),
+            "epp_world_generation": (i32, [vp, C.POINTER(C.c_uint64)]),
             "epp_check_states": (i32, [vp, vp, i64, i32, vp, vp, vp, vp]),
             "epp_check_states_mindist": (i32, [vp, vp, i64, dp, vp, vp]),
             "epp_check_motions": (i32, [vp, vp, vp, i64, i32, i32, vp, vp]),
             "epp_minsnap_batch": (i32, [vp, vp, i32, dp, dp, vp, vp, vp, vp, vp, vp]),
+            "epp_minsnap_batch_times": (i32, [vp, vp, i32, vp, vp, vp, vp, vp, vp]),
             "epp_sample_count": (i32, [vp, vp, i32, dp, vp, vp]),
             "epp_sample_batch": (i32, [vp, vp, vp, i32, dp, vp, vp, vp, vp]),
             "epp_generate_trajectory_host": (i32, [vp, i32, dp, dp, dp, dp, vp, vp,
                                                    C.POINTER(C.POINTER(C.c_double)), C.POINTER(i64)]),
+            "epp_generate_trajectory_times_host": (i32, [vp, i32, vp, dp, dp, vp, vp,
+                                                         C.POINTER(C.POINTER(C.c_double)), C.POINTER(i64)]),
             "epp_optimal_trajectory_host": (i32, [vp, i32, vp, i32, dp, dp, dp, dp, dp,
                                                   C.POINTER(C.POINTER(C.c_double)), C.POINTER(i64)]),
             "epp_spline_trajectory_host": (i32, [vp, i32, dp, dp, dp, C.POINTER(C.POINTER(C.c_double)),
@@ -113,7 +117,8 @@ EXPORTED = [
     "epp_knn_bruteforce", "epp_knn_grid", "epp_knn_workspace_size", "epp_knn_ws", "epp_knn_grid_ws",
     "epp_knn_edges", "epp_compact_states", "epp_mask_edges", "epp_optimal_trajectory_host",
     "epp_spline_trajectory_host", "epp_compact_workspace_size", "epp_compact_states_ws",
-    "epp_graph_begin", "epp_graph_end", "epp_graph_launch", "epp_graph_destroy",
+    "epp_graph_begin", "epp_graph_end", "epp_graph_launch", "epp_graph_destroy", "epp_minsnap_batch_times",
+    "epp_generate_trajectory_times_host", "epp_world_generation",
 ]
 
 
@@ -205,6 +210,11 @@ class World:
         obbs = np.ascontiguousarray(obbs, dtype=OBB_DTYPE)
         check(lib().epp_world_update(self.handle, _ptr(obbs) if len(obbs) else None, len(obbs)))
         self.n = len(obbs)
+
+    def generation(self) -> int:
+        g = C.c_uint64(0)
+        check(lib().epp_world_generation(self.handle, C.byref(g)))
+        return g.value
 
     def aabbs(self) -> np.ndarray:
         out = np.zeros((max(self.n, 1), 6))
@@ -298,6 +308,47 @@ def minsnap_batch(tracks, v_max, a_max, v0=None, a0=None):
     return Ts, Cs, st
 
 
+def minsnap_batch_times(tracks, times, v0=None, a0=None):
+    """epp_minsnap_batch_times: as minsnap_batch with the caller's segment times (a list
+    of (W_k - 1) arrays; setupFromVertices(vertices, segment_times)).  Returns (coeffs
+    list, status array)."""
+    wp = np.ascontiguousarray(np.concatenate([np.asarray(t, np.float64).reshape(-1, 3) for t in tracks]))
+    off = np.zeros(len(tracks) + 1, np.int32)
+    off[1:] = np.cumsum([len(t) for t in tracks])
+    nt = len(tracks)
+    nseg = int(off[-1]) - nt
+    T = np.ascontiguousarray(np.concatenate([np.asarray(t, np.float64).ravel() for t in times]))
+    assert len(T) == nseg
+    d_wp, d_off, d_T = DeviceBuffer.from_array(wp), DeviceBuffer.from_array(off), DeviceBuffer.from_array(T)
+    d_v0 = DeviceBuffer.from_array(np.ascontiguousarray(v0, np.float64)) if v0 is not None else None
+    d_a0 = DeviceBuffer.from_array(np.ascontiguousarray(a0, np.float64)) if a0 is not None else None
+    d_C, d_st = DeviceBuffer(240 * max(nseg, 1)), DeviceBuffer(4 * nt)
+    check(lib().epp_minsnap_batch_times(d_wp.ptr, d_off.ptr, nt, d_v0.ptr if d_v0 else None,
+                                        d_a0.ptr if d_a0 else None, d_T.ptr, d_C.ptr, d_st.ptr, None))
+    sync()
+    Cf = d_C.download(np.float64, nseg * 30).reshape(nseg, 3, 10)
+    st = d_st.download(np.int32, nt)
+    return [Cf[int(off[k]) - k:int(off[k + 1]) - k - 1] for k in range(nt)], st
+
+
+def generate_trajectory_times(waypoints, seg_times, dt, t0=0.0, v0=(0, 0, 0), a0=(0, 0, 0)) -> np.ndarray:
+    """generateTrajectory with the caller's segment times (epp_generate_trajectory_times_host)."""
+    wp = np.ascontiguousarray(np.asarray(waypoints, np.float64).reshape(-1, 3))
+    T = np.ascontiguousarray(seg_times, np.float64)
+    v0 = np.ascontiguousarray(v0, np.float64)
+    a0 = np.ascontiguousarray(a0, np.float64)
+    rows = C.POINTER(C.c_double)()
+    n = C.c_int64(0)
+    check(lib().epp_generate_trajectory_times_host(_ptr(wp), len(wp), _ptr(T), float(dt), float(t0), _ptr(v0),
+                                                   _ptr(a0), C.byref(rows), C.byref(n)))
+    if n.value == 0:
+        lib().epp_host_free(C.cast(rows, C.c_void_p))
+        return np.zeros((0, 10))
+    out = np.ctypeslib.as_array(rows, shape=(n.value * 10,)).copy().reshape(-1, 10)
+    lib().epp_host_free(C.cast(rows, C.c_void_p))
+    return out
+
+
 def generate_trajectory(waypoints, v_max, a_max, dt, t0=0.0, v0=(0, 0, 0), a0=(0, 0, 0)) -> np.ndarray:
     """poly_traj::generateTrajectory (src/trajectory_generator.cpp:12-100) on the GPU."""
     wp = np.ascontiguousarray(np.asarray(waypoints, np.float64).reshape(-1, 3))
@@ -308,6 +359,7 @@ def generate_trajectory(waypoints, v_max, a_max, dt, t0=0.0, v0=(0, 0, 0), a0=(0
     check(lib().epp_generate_trajectory_host(_ptr(wp), len(wp), float(v_max), float(a_max), float(dt), float(t0),
                                              _ptr(v0), _ptr(a0), C.byref(rows), C.byref(n)))
     if n.value == 0:
+        lib().epp_host_free(C.cast(rows, C.c_void_p))
         return np.zeros((0, 10))
     out = np.ctypeslib.as_array(rows, shape=(n.value * 10,)).copy().reshape(-1, 10)
     lib().epp_host_free(C.cast(rows, C.c_void_p))

@@ -3,7 +3,9 @@
  *
  * Plain pointers and sizes only; no torch / Eigen / OMPL types.  Every compute
  * entry point is stream-ordered on the hipStream_t passed as `void* stream`
- * (NULL = the null stream) and takes DEVICE pointers for bulk data.  All
+ * (NULL = the null stream) and takes DEVICE pointers for bulk data (pinned host memory
+ * from hipHostMalloc also works: the kernels then read / write it over the bus, which
+ * the host-array paths use for small batches).  All
  * functions return an epp_status (0 = ok, < 0 = error); the message of the last
  * error on the calling thread is available from epp_last_error().
  *
@@ -113,8 +115,13 @@ epp_status epp_build_obbs(const epp_obb_desc* gate_desc, const int32_t* gate_des
  * uploads both to the current device.  obbs is a HOST array. */
 epp_status epp_world_create(const epp_obb* obbs, int32_t n_obbs, double r_gate, double r_obst,
                             epp_world** out);
-/* Replaces the OBB set (gate-pose update = full rebuild, src/OnlineTrajGenerator.cpp:146). */
+/* Replaces the OBB set (gate-pose update = full rebuild, src/OnlineTrajGenerator.cpp:146).
+ * Waits for every kernel on the device first (they may read the old index), then
+ * uploads.  HIP graphs that captured launches on this world must be re-captured
+ * afterwards: launch shapes depend on the index size (epp_world_generation changes). */
 epp_status epp_world_update(epp_world* w, const epp_obb* obbs, int32_t n_obbs);
+/* Number of uploads of this world so far (create = 1, every update + 1). */
+epp_status epp_world_generation(const epp_world* w, uint64_t* generation);
 epp_status epp_world_destroy(epp_world* w);
 epp_status epp_world_num_obbs(const epp_world* w, int32_t* n);
 /* Host copy of the AABBs computed for the index (lo[3], hi[3] per OBB). */
@@ -144,6 +151,14 @@ epp_status epp_check_motions(const epp_world* w, const double* s1, const double*
 epp_status epp_minsnap_batch(const double* wp, const int32_t* wp_offsets, int32_t n_tracks,
                              double v_max, double a_max, const double* v0, const double* a0,
                              double* seg_times, double* coeffs, int32_t* status, void* stream);
+/* As epp_minsnap_batch with the caller's segment times instead of
+ * estimateSegmentTimesNfabian: PolynomialOptimization<10>::setupFromVertices(vertices,
+ * segment_times) (impl/polynomial_optimization_linear_impl.h:56-109), as the reference's
+ * own tests call it (external/poly_traj/test/test_polynomial_optimization.cpp:765-769).
+ * seg_times_in: total segments (device).  status -2 for a segment time <= 0. */
+epp_status epp_minsnap_batch_times(const double* wp, const int32_t* wp_offsets, int32_t n_tracks, const double* v0,
+                                   const double* a0, const double* seg_times_in, double* coeffs, int32_t* status,
+                                   void* stream);
 /* Number of rows Trajectory::evaluateRange produces for every track (device int64 out). */
 epp_status epp_sample_count(const double* seg_times, const int32_t* wp_offsets, int32_t n_tracks,
                             double dt, int64_t* row_counts, void* stream);
@@ -194,11 +209,20 @@ epp_status epp_compact_states_ws(const double* xyz, const uint8_t* valid, int64_
 epp_status epp_mask_edges(int32_t* nbr, const uint8_t* valid, int64_t m, void* stream);
 
 /* ---- host-buffer convenience (synchronous; used by the C++ API shims) ------------- */
-/* generateTrajectory for one track with host buffers.  Returns the row count in
- * *n_rows; rows is (re)allocated with malloc and must be released with epp_host_free. */
+/* generateTrajectory for one track with host buffers (poly_traj::generateTrajectory,
+ * external/poly_traj/src/trajectory_generator.cpp:12-100): one fused launch (min-snap
+ * solve + evaluateRange sampling) reading and writing pinned host memory.  Returns the row
+ * count in *n_rows; rows is allocated with malloc and must be released with
+ * epp_host_free.  EPP_ERR_INVALID_ARGUMENT "At least two waypoints are required";
+ * EPP_ERR_RUNTIME "Segment times need to be greater than zero" (the reference's glog
+ * CHECK). */
 epp_status epp_generate_trajectory_host(const double* wp, int32_t n_wp, double v_max, double a_max,
                                         double dt, double t0, const double v0[3], const double a0[3],
                                         double** rows, int64_t* n_rows);
+/* The same with the caller's segment times (n_wp - 1 of them) instead of Nfabian's. */
+epp_status epp_generate_trajectory_times_host(const double* wp, int32_t n_wp, const double* seg_times, double dt,
+                                              double t0, const double v0[3], const double a0[3], double** rows,
+                                              int64_t* n_rows);
 /* The "optimal" trajectory type (OptimalTimeParametrizer::calculateTrajectory,
  * external/time_parametrization/src/OptimalTimeParametrizer.cpp:11-108; host code: one
  * sequential phase-plane integration).  wp: n_wp x 3, pre: n_pre x 3 lead-in points

@@ -4,8 +4,11 @@
 // Concurrency: the reference recomputes on a detached std::thread and writes the
 // trajectory while Python may read it.  Here every access to the planned
 // trajectory goes through one mutex; with recalculate_online the recomputation runs on
-// a worker thread whose completion is awaited by the next update or the destructor.
+// a worker thread.  An update arriving while it runs throws the reference's
+// "Call to update trajectory, while previous update is still going on" before touching
+// the world; the destructor and wait_for_update() wait for it.
 #pragma once
+#include <atomic>
 #include <future>
 #include <memory>
 #include <mutex>
@@ -39,7 +42,8 @@ public:
     // waypoints of the last (re)planned trajectory, after includeGates2
     std::vector<Vec3> getWaypoints() const;
     PathPlanner& planner() { return pathPlanner; }
-    // waits for an in-flight online recomputation (recalculate_online)
+    // waits for an in-flight online recomputation (recalculate_online); rethrows its
+    // failure as std::runtime_error("previous trajectory update failed: ...")
     void waitForUpdate();
 
 private:
@@ -47,6 +51,7 @@ private:
     bool getGateCenterAndNormal(const std::vector<double>& gate, Vec3& center, Vec3& normal) const;
     bool checkGatePassed(const Vec3& p1, const Vec3& p2, int gateId) const;
     void recomputeTraj(int gateId, const Vec3& dronePos, double flightTime);
+    void collectUpdate();
     Matrix generate(const std::vector<Vec3>& path, double t0, const Vec3& v0, const Vec3& a0,
                     const std::vector<Vec3>& pre = {}) const;
     static size_t nearestRow(const Matrix& traj, double t);
@@ -62,7 +67,7 @@ private:
     Matrix plannedTraj;
     std::vector<Vec3> waypoints;  // guarded by trajMu
     mutable std::mutex trajMu;
-    bool trajectoryCurrentlyUpdating = false;
+    std::atomic<bool> trajectoryCurrentlyUpdating{false};
     std::future<void> pending;
     PathWriter pathWriter{"path_segments"};  // include/OnlineTrajGenerator.h:132
 };

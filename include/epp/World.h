@@ -29,6 +29,8 @@ public:
     void resetWorld();
     // coordinates: (x, y, z, roll, pitch, yaw, type); z is forced to 0 (World.cpp:16)
     void addGate(int gateId, const std::vector<double>& coordinates);
+    // coordinates: (x, y, z, roll, pitch, yaw, type), or the 6-value pose alone (the gate
+    // keeps its type; the reference reads coordinates(6), src/World.cpp:18)
     void updateGatePosition(int gateId, const std::vector<double>& coordinates);
     // coordinates: (x, y, z, roll, pitch, yaw)
     void addObstacle(int obstacleId, const std::vector<double>& coordinates);
@@ -56,10 +58,13 @@ private:
     struct Entry {
         int id;
         bool gate;
+        int type;  // gate type (-1 for obstacles)
         std::vector<epp_obb> obbs;
     };
     void addObject(int id, bool gate, const std::vector<double>& coordinates, bool update);
     void sync() const;
+    template <typename Launch>
+    void query(int64_t n, int n_in, Launch&& launch, const double* const* in, uint8_t* out) const;
 
     std::shared_ptr<ConfigParser> config_;
     double rGate_, rObst_;

@@ -1,0 +1,44 @@
+"""Phase timeline of the fused single-track refit (k_refit): builds a diagnostics copy of
+libepp.so with -DEPP_REFIT_TL into scripts/dbg/ (not the product library), runs 50
+refits and prints the median time of every phase boundary (s_memrealtime, 100 MHz)
+relative to the kernel's first stamp.  Stamps: 0 entry, 1 inputs + A^-1, 2 Q, 3 G, 4 H,
+5 assembly, 6 block Cholesky, 7 coefficients, 11 rows written."""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "efficient-path-planner_amd")]
+from eppamd import synth  # noqa: E402
+
+out = os.path.join(ROOT, "scripts", "dbg")  # built here (make below), shipped with the tree
+os.makedirs(out, exist_ok=True)
+pkg = os.path.join(ROOT, "efficient-path-planner_amd")
+subprocess.run(["make", "-s", "-j16", "-C", pkg, f"BUILD={out}/build", f"LIB={out}/libepp_tl.so",
+                "EXTRA=-DEPP_REFIT_TL", f"{out}/libepp_tl.so"], check=True)
+L = C.CDLL(os.path.join(out, "libepp_tl.so"))
+wp = np.ascontiguousarray(synth.random_track_waypoints(10_000, 12))
+v = np.zeros(3)
+rows = C.POINTER(C.c_double)()
+n = C.c_int64()
+tl = np.zeros(32, np.uint64)
+stamps = []
+for r in range(60):
+    rc = L.epp_generate_trajectory_host(C.c_void_p(wp.ctypes.data), len(wp), C.c_double(1.0), C.c_double(2.0),
+                                        C.c_double(0.1), C.c_double(0.0), C.c_void_p(v.ctypes.data),
+                                        C.c_void_p(v.ctypes.data), C.byref(rows), C.byref(n))
+    assert rc == 0
+    L.epp_host_free(C.cast(rows, C.c_void_p))
+    L.epp_dbg_refit_tl(C.c_void_p(tl.ctypes.data))
+    stamps.append(tl.astype(np.int64).copy())
+st = np.array(stamps[10:]).reshape(-1, 2, 16)
+t0 = st[:, :, 0].min(axis=1)
+for wg in range(2):
+    for k in range(12):
+        d = (st[:, wg, k] - t0) * 10  # ns
+        if (st[:, wg, k] > 0).all():
+            print(f"wg{wg} stamp {k:2d}: median {np.median(d) / 1000:7.2f} us")
+print("rows", n.value)

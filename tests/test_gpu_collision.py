@@ -255,3 +255,161 @@ def test_global_memory_path_large_world(cfg, geom):
     assert np.array_equal(w.check_states(pts), O.check_states(ref, rg, ro, pts, threads=8))
     s1, s2 = synth.edges(1, 2, *synth.C2_BOUNDS, 20_000)
     assert np.array_equal(w.check_motions(s1, s2), O.check_motions(ref, rg, ro, s1, s2, threads=8))
+
+
+# ---- worlds with "filling" OBBs (configs/config_filling.json: one per gate, the portal
+# opening).  Reference semantics: a filling OBB is skipped by the state and ray checks when
+# canPassGate (src/World.cpp:92-95, :150-153), always by the minDistance check (:116-119);
+# its AABB is not inflated (src/OBB.cpp:117-121) and its point test is not inflated
+# (src/OBB.h:54-57), but the ray slab test always inflates (src/OBB.cpp:28).
+FILLING_CONFIG = os.path.join(os.path.dirname(GOLDEN), "..", "configs", "config_filling.json")
+
+
+@pytest.fixture(scope="module")
+def fworlds():
+    cfg = config.load(FILLING_CONFIG)
+    fgeom = config.geometry(cfg)
+    assert fgeom.gate_desc["filling"].sum() == 2
+    rg, ro, ws = _worlds(cfg, fgeom)
+    return fgeom, rg, ro, ws
+
+
+def _gate_openings(gates, geom, n_per_gate=400, seed=3):
+    """States in and around every gate opening (the filling boxes), in world coordinates."""
+    rs = np.random.RandomState(seed)
+    out = []
+    for g in gates:
+        h = geom.gate_height[int(g[6])]
+        loc = rs.uniform([-0.3, -0.05, -0.3], [0.3, 0.05, 0.3], size=(n_per_gate, 3))
+        c, s = np.cos(g[5]), np.sin(g[5])
+        out.append(np.stack([g[0] + c * loc[:, 0] - s * loc[:, 1], g[1] + s * loc[:, 0] + c * loc[:, 1],
+                             h + loc[:, 2]], 1))
+    return np.vstack(out)
+
+
+@pytest.mark.parametrize("kernel", ["v5", "v4", "generic"])
+@pytest.mark.parametrize("name", ["c1", "c2", "c3"])
+def test_filling_states_bit_exact(fworlds, name, kernel, monkeypatch):
+    monkeypatch.setenv("EPP_STATES_KERNEL", kernel)
+    fgeom, rg, ro, ws = fworlds
+    gates, obstacles, (lo, hi) = ws[name]
+    ref = O.world_build(fgeom, gates, obstacles, rg, ro)
+    assert sum(int(o["filling"]) for o in ref) == len(gates)
+    w = capi.World(capi.build_obbs(fgeom, gates, obstacles), rg, ro)
+    pts = np.vstack([synth.sample_states(17, lo, hi, 100_003), _gate_openings(gates, fgeom),
+                     _adversarial_points(ref)])
+    res = {}
+    for cp in (0, 1):
+        got = w.check_states(pts, cp)
+        exp = O.check_states(ref, rg, ro, pts, cp, threads=8)
+        assert exp.min() == 0 and exp.max() == 1
+        assert np.array_equal(got, exp), (cp, np.flatnonzero(got != exp)[:10])
+        res[cp] = exp
+    # the filling boxes decide: states in an opening are invalid unless the gate may be passed
+    assert (res[1] >= res[0]).all() and (res[1] > res[0]).sum() >= 20
+    for md in (0.0, 0.1, 0.3):  # minDistance skips every filling OBB
+        assert np.array_equal(w.check_states_mindist(pts, md), O.check_states_mindist(ref, pts, md)), md
+
+
+@pytest.mark.parametrize("kernel", ["lds", "generic"])
+@pytest.mark.parametrize("name", ["c1", "c2", "c3"])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_filling_motions_bit_exact(fworlds, name, mode, kernel, monkeypatch):
+    monkeypatch.setenv("EPP_MOTIONS_KERNEL", kernel)
+    fgeom, rg, ro, ws = fworlds
+    gates, obstacles, (lo, hi) = ws[name]
+    ref = O.world_build(fgeom, gates, obstacles, rg, ro)
+    w = capi.World(capi.build_obbs(fgeom, gates, obstacles), rg, ro)
+    n = 60_000 if mode == 0 else 15_000
+    s1, s2 = synth.edges(45, 9, lo, hi, n, max_len=0.5 if name != "c1" else 1.5)
+    # edges through the openings, along the gate normal (the way a drone passes a gate)
+    a = _gate_openings(gates, fgeom, 300, seed=5)
+    yaw = np.repeat(gates[:, 5], 300)
+    nrm = np.stack([-np.sin(yaw), np.cos(yaw), np.zeros_like(yaw)], 1)
+    s1, s2 = np.vstack([s1, a - 0.4 * nrm]), np.vstack([s2, a + 0.4 * nrm])
+    res = {}
+    for cp in (0, 1):
+        got = w.check_motions(s1, s2, cp, mode)
+        exp = O.check_motions(ref, rg, ro, s1, s2, cp, mode, threads=8)
+        assert exp.min() == 0 and exp.max() == 1
+        assert np.array_equal(got, exp), (cp, np.flatnonzero(got != exp)[:10])
+        res[cp] = exp
+    assert (res[1] >= res[0]).all() and (res[1] > res[0]).sum() >= 20
+
+
+@pytest.mark.parametrize("n", [1 << 20, 5 << 20])
+def test_filling_states_full_size(fworlds, n):
+    """BASELINE C2 size with filling OBBs, both can_pass_gate outcomes, bit-exact."""
+    fgeom, rg, ro, ws = fworlds
+    gates, obstacles, (lo, hi) = ws["c2"]
+    ref = O.world_build(fgeom, gates, obstacles, rg, ro)
+    w = capi.World(capi.build_obbs(fgeom, gates, obstacles), rg, ro)
+    pts = synth.sample_states(7, lo, hi, n)
+    e0 = O.check_states(ref, rg, ro, pts, False, threads=8)
+    e1 = O.check_states(ref, rg, ro, pts, True, threads=8)
+    assert (e1 > e0).sum() > 0
+    assert np.array_equal(w.check_states(pts, False), e0)
+    assert np.array_equal(w.check_states(pts, True), e1)
+
+
+def test_graph_replay_matches_direct_launch(geom, worlds):
+    """bench.py times replayed HIP graphs of epp_check_states: K captured launches over
+    rotating batches give the same flags as direct launches and as the oracle."""
+    import ctypes as C
+    L = capi.lib()
+    rg, ro, ws = worlds
+    gates, obstacles, (lo, hi) = ws["c2"]
+    ref = O.world_build(geom, gates, obstacles, rg, ro)
+    w = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
+    n, nb = 200_000, 3
+    pts = [synth.sample_states(77 + b, lo, hi, n) for b in range(nb)]
+    d_in = [capi.DeviceBuffer.from_array(p) for p in pts]
+    d_out = [capi.DeviceBuffer(n) for _ in range(nb)]
+    s = C.c_void_p()
+    capi.check(L.epp_stream_create(C.byref(s)))
+    g = C.c_void_p()
+    gen0 = w.generation()
+    capi.check(L.epp_graph_begin(s.value))
+    for k in range(2 * nb):
+        w.check_states_dev(d_in[k % nb].ptr, n, 0, d_out[k % nb].ptr, stream=s.value)
+    capi.check(L.epp_graph_end(s.value, C.byref(g)))
+    for b in range(nb):
+        d_out[b].zero()
+    capi.sync()
+    capi.check(L.epp_graph_launch(g.value, s.value))
+    capi.check(L.epp_stream_sync(s.value))
+    for b in range(nb):
+        got = d_out[b].download(np.uint8, n)
+        assert np.array_equal(got, w.check_states(pts[b]))
+        assert np.array_equal(got, O.check_states(ref, rg, ro, pts[b], False, threads=8))
+    capi.check(L.epp_graph_destroy(g.value))
+    L.epp_stream_destroy(s.value)
+    # an update is a new upload: captured graphs must be re-captured (epp.h)
+    w.update(capi.build_obbs(geom, gates, obstacles))
+    assert w.generation() == gen0 + 1
+
+
+def test_world_update_small_queries_zero_copy(cfg, geom, worlds):
+    """The C++ World's host-array queries (zero-copy below 16384 queries, DMA above) after
+    gate-pose updates agree with the oracle rebuilt from the same poses."""
+    import online_traj_planner as otp
+    rg, ro, ws = worlds
+    gates, obstacles, (lo, hi) = ws["c2"]
+    from conftest import CONFIG
+    pp = otp.PathPlanner(gates, obstacles, CONFIG)
+    rs = np.random.RandomState(0)
+    g = np.array(gates, float)
+    for step in range(6):
+        k = step % len(g)
+        g[k, 0] += rs.uniform(-0.1, 0.1)
+        g[k, 5] += rs.uniform(-0.1, 0.1)
+        pp.update_gate_pos(k, list(g[k, :6]))
+        ref = O.world_build(geom, g, obstacles, rg, ro)
+        for n in (1, 100, 20_000):
+            pts = synth.sample_states(300 + step, lo, hi, n)
+            rows = np.zeros((n, 10))
+            rows[:, [0, 3, 6]] = pts
+            exp = O.check_states_mindist(ref, pts, 0.1)
+            assert pp.check_trajectory_validity(rows, 0.1) == bool(exp.all())
+            for p, e in zip(pts[:50], O.check_states(ref, rg, ro, pts[:50], False)):
+                assert pp.check_point_validity(p, False) == bool(e)

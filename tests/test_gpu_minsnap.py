@@ -134,3 +134,191 @@ def test_large_batch_property():
                     assert abs(a - b) < 1e-6
         np.testing.assert_allclose([O.poly_eval(Cf[-1, d], T[-1], 0) for d in range(3)], tracks[k][-1],
                                    atol=1e-6)
+
+
+# ---- pinned directly to the reference's own vectors ---------------------------------
+# external/poly_traj/test/test_polynomial_optimization.cpp (fixtures in
+# tests/golden/reference_minsnap.json): the GPU is compared with the reference's numbers,
+# not only with the oracle.
+REF = json.load(open(os.path.join(GOLDEN, "reference_minsnap.json")))
+
+
+def _embed3(wp):
+    wp = np.asarray(wp, np.float64)
+    out = np.zeros((len(wp), 3))
+    out[:, :wp.shape[1]] = wp
+    return out
+
+
+def test_two_vertices_setup_reference_golden():
+    """TwoVerticesSetup (:743-787): rest-to-rest 0 -> 5 m in T = 5 s, snap; the
+    reference's MATLAB coefficients at 1e-12, embedded in 3-D (y, z at rest at 0), via
+    setupFromVertices(vertices, segment_times) = epp_minsnap_batch_times and the fused
+    single-track path."""
+    c = REF["two_vertices_setup"]
+    wp = np.array([[c["start_x"], 0.0, 0.0], [c["goal_x"], 0.0, 0.0]])
+    Cs, st = capi.minsnap_batch_times([wp], [[c["segment_time"]]])
+    assert st[0] == 0
+    np.testing.assert_allclose(Cs[0][0, 0], c["matlab_coeffs"], rtol=0, atol=c["tolerance"])
+    assert np.abs(Cs[0][0, 1:]).max() == 0.0
+    rows = capi.generate_trajectory_times(wp, [c["segment_time"]], 0.05)
+    t = rows[:, 9]
+    x = np.polyval(np.asarray(c["matlab_coeffs"])[::-1], t)
+    np.testing.assert_allclose(rows[:, 0], x, rtol=0, atol=1e-9)  # (golden rounded to ~1e-15 per coefficient)
+    # sample times follow evaluateRange exactly (they depend on the segment time only)
+    assert np.array_equal(t, O.sample_traj([c["segment_time"]], Cs[0], 0.05)[:, 9])
+
+
+def _check_path(times, coeffs, wp, D, tol):
+    """checkPath (:113-174): vertex constraints met (positions; start/end derivatives 1..4
+    zero) and C0..C4 continuity at every inner vertex."""
+    M = len(times)
+    for i in range(M):
+        for d in range(3):
+            for k in range(5):
+                beg = O.poly_eval(coeffs[i, d], 0.0, k)
+                end = O.poly_eval(coeffs[i, d], times[i], k)
+                if k == 0:
+                    assert abs(beg - (wp[i, d] if d < D else 0.0)) < tol
+                    assert abs(end - (wp[i + 1, d] if d < D else 0.0)) < tol
+                if i == 0 and k > 0:
+                    assert abs(beg) < tol
+                if i == M - 1 and k > 0:
+                    assert abs(end) < tol
+                if i > 0:
+                    assert abs(O.poly_eval(coeffs[i - 1, d], times[i - 1], k) - beg) < tol
+
+
+SNAP_SETS = [p for p in REF["parameter_sets"] if p["deriv"] == 4]
+
+
+@pytest.mark.parametrize("ps", SNAP_SETS, ids=lambda p: p["name"])
+def test_reference_parameter_sets(ps):
+    """The reference's snap parameter sets segment_{1,10,50}_dim_{1,3} (:790-879):
+    createRandomVertices (std::mt19937, src/vertex.cpp:27-82) -> estimateSegmentTimes
+    (Nfabian) -> solve, checked with checkPath at the reference's 1e-6, and against the
+    oracle's coefficients at 1e-6.  50 segments run the global-scratch kernel."""
+    D = ps["D"]
+    wp = _embed3(O.random_vertices(ps["segments"], D, -ps["pos"], ps["pos"], ps["seed"]))
+    Ts, Cs, st = capi.minsnap_batch([wp], ps["v_max"], ps["a_max"])
+    assert st[0] == 0
+    T_ref = O.segment_times(wp[:, :D], ps["v_max"], ps["a_max"])
+    np.testing.assert_allclose(Ts[0], T_ref, rtol=1e-12)
+    _check_path(Ts[0], Cs[0], wp, D, REF["check_path_tolerance"]["tol"])
+    mask = np.zeros((len(wp), 5), np.uint8)
+    mask[:, 0] = 1
+    mask[0, :] = mask[-1, :] = 1
+    val = np.zeros((len(wp), 5, D))
+    val[:, 0] = wp[:, :D]
+    ref = O.minsnap_solve(mask, val, T_ref, D, 4)
+    assert np.abs(Cs[0][:, :D] - ref).max() < COEF_TOL
+    # the same with the caller's times (setupFromVertices(vertices, times))
+    Ct, st2 = capi.minsnap_batch_times([wp], [T_ref])
+    assert st2[0] == 0 and np.abs(Ct[0][:, :D] - ref).max() < COEF_TOL
+
+
+@pytest.mark.parametrize("D", [1, 3])
+def test_constraint_packing_reference(D):
+    """ConstraintPacking (:505-564): 5 setups of 10 segments (seeds 12345..12349,
+    positions +-50): A_i p_i reproduces the vertex values and is continuous (1e-6)."""
+    c = REF["constraint_packing"]
+    tracks = [_embed3(O.random_vertices(10, D, -c["pos"], c["pos"], c["seed"] + k)) for k in range(c["setups"])]
+    Ts, Cs, st = capi.minsnap_batch(tracks, c["v_max"], c["a_max"])
+    assert (st == 0).all()
+    for wp, T, Cf in zip(tracks, Ts, Cs):
+        for i in range(len(T)):
+            A = O.mapping_matrix(T[i])
+            for d in range(3):
+                dd = A @ Cf[i, d]
+                if i > 0:  # derivatives 0..4 at the shared vertex
+                    prev = O.mapping_matrix(T[i - 1]) @ Cf[i - 1, d]
+                    np.testing.assert_allclose(dd[:5], prev[5:], atol=c["tol"])
+                np.testing.assert_allclose(dd[0], wp[i, d], atol=c["tol"])
+                np.testing.assert_allclose(dd[5], wp[i + 1, d], atol=c["tol"])
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_generate_trajectory_times_vs_oracle(seed):
+    rs = np.random.RandomState(seed)
+    wp = synth.random_track_waypoints(700 + seed, 4 + 3 * seed)
+    T = O.segment_times(wp, 1.0, 2.0) * rs.uniform(0.7, 1.4, len(wp) - 1)  # caller times near Nfabian's
+    got = capi.generate_trajectory_times(wp, T, 0.1, 1.5, (0.2, 0.0, -0.1), (0.0, 0.3, 0.0))
+    mask = np.zeros((len(wp), 5), np.uint8)
+    mask[:, 0] = 1
+    mask[0, :] = mask[-1, :] = 1
+    val = np.zeros((len(wp), 5, 3))
+    val[:, 0] = wp
+    val[0, 1], val[0, 2] = (0.2, 0.0, -0.1), (0.0, 0.3, 0.0)
+    exp = O.sample_traj(T, O.minsnap_solve(mask, val, T, 3, 4), 0.1, 1.5)
+    assert got.shape == exp.shape
+    assert np.array_equal(got[:, 9], exp[:, 9])
+    assert np.abs(got[:, :9] - exp[:, :9]).max() < 1e-6
+    with pytest.raises(capi.EppError) as e:
+        capi.generate_trajectory_times(wp, np.where(np.arange(len(T)) == 1, 0.0, T), 0.1)
+    assert "Segment times need to be greater than zero" in str(e.value)
+
+
+def test_long_tracks_two_streams_back_to_back():
+    """Tracks longer than the LDS limit use the per-device workspace; two streams issuing
+    batches back to back must not share it while the first still runs (event-ordered
+    reuse), answers equal the oracle's."""
+    import ctypes as C
+    L = capi.lib()
+    batches = [[synth.random_track_waypoints(4000 + 50 * b + k, 45 + k % 7) for k in range(24)] for b in range(2)]
+    streams = []
+    for _ in batches:
+        s = C.c_void_p()
+        capi.check(L.epp_stream_create(C.byref(s)))
+        streams.append(s.value)
+    bufs, outs = [], []
+    for tracks, s in zip(batches, streams):
+        wp = np.ascontiguousarray(np.concatenate(tracks))
+        off = np.zeros(len(tracks) + 1, np.int32)
+        off[1:] = np.cumsum([len(t) for t in tracks])
+        nseg = int(off[-1]) - len(tracks)
+        d = [capi.DeviceBuffer.from_array(wp), capi.DeviceBuffer.from_array(off), capi.DeviceBuffer(8 * nseg),
+             capi.DeviceBuffer(240 * nseg), capi.DeviceBuffer(4 * len(tracks))]
+        bufs.append(d)
+        outs.append((off, nseg))
+    for (dwp, doff, dT, dC, dst), tracks, s in zip(bufs, batches, streams):  # back to back, no sync between
+        capi.check(L.epp_minsnap_batch(dwp.ptr, doff.ptr, len(tracks), 1.0, 2.0, None, None, dT.ptr, dC.ptr,
+                                       dst.ptr, s))
+    capi.sync()
+    for (dwp, doff, dT, dC, dst), tracks, (off, nseg) in zip(bufs, batches, outs):
+        Cf = dC.download(np.float64, nseg * 30).reshape(nseg, 3, 10)
+        assert (dst.download(np.int32, len(tracks)) == 0).all()
+        for k, wp in enumerate(tracks):
+            _, ref = O.minsnap_track(wp, 1.0, 2.0)
+            assert np.abs(Cf[int(off[k]) - k:int(off[k + 1]) - k - 1] - ref).max() < COEF_TOL
+    for s in streams:
+        L.epp_stream_destroy(s)
+
+
+# ---- the polynomial_trajectory pybind surface (external/poly_traj/README.md:79) -------
+@pytest.mark.parametrize("seed", range(3))
+def test_polynomial_trajectory_module(seed):
+    """polynomial_trajectory.generate_trajectory(waypoints, v_max, a_max,
+    sampling_intervall) with the README's arguments vs the oracle: same shape, time
+    column exact, 1e-6 elsewhere; start time offset and initial state keywords."""
+    import polynomial_trajectory as pt
+    wp = synth.random_track_waypoints(800 + seed, 5 + 4 * seed)
+    got = pt.generate_trajectory(wp, 1.0, 2.0, 0.1)
+    exp = O.generate_trajectory(wp, 1.0, 2.0, 0.1)
+    assert got.shape == exp.shape and got.shape[1] == 10
+    assert np.array_equal(got[:, 9], exp[:, 9])
+    assert np.abs(got[:, :9] - exp[:, :9]).max() < 1e-6
+    got = pt.generate_trajectory(wp, 1.5, 2.5, 0.05, startTimeOffset=2.0, initialVel=[0.1, 0.2, 0.0],
+                                 initialAcc=[0.0, 0.0, 0.3])
+    exp = O.generate_trajectory(wp, 1.5, 2.5, 0.05, 2.0, (0.1, 0.2, 0.0), (0.0, 0.0, 0.3))
+    assert got.shape == exp.shape and np.array_equal(got[:, 9], exp[:, 9])
+    assert np.abs(got[:, :9] - exp[:, :9]).max() < 1e-6
+
+
+def test_polynomial_trajectory_errors():
+    import polynomial_trajectory as pt
+    with pytest.raises(ValueError, match="At least two waypoints are required"):
+        pt.generate_trajectory(np.zeros((1, 3)), 1.0, 2.0, 0.1)
+    with pytest.raises(ValueError):
+        pt.generate_trajectory(np.zeros((4, 2)), 1.0, 2.0, 0.1)  # not (n, 3)
+    with pytest.raises(RuntimeError, match="Segment times need to be greater than zero"):
+        pt.generate_trajectory(np.array([[0, 0, 1.0], [0, 0, 1.0], [1, 0, 1.0]]), 1.0, 2.0, 0.1)

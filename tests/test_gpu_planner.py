@@ -523,3 +523,47 @@ def test_mask_edges():
     nbr = rs.randint(-1, 1000, (777, 16)).astype(np.int32)
     valid = (rs.rand(777, 16) < 0.7).astype(np.uint8)
     assert np.array_equal(capi.mask_edges(nbr, valid), np.where(valid.astype(bool), nbr, -1))
+
+
+def test_online_update_while_replanning_throws(track):
+    """An update arriving while the online recomputation (recalculate_online) still runs
+    gets the reference's runtime_error (src/OnlineTrajGenerator.cpp:208-212), raised
+    before the world is touched; wait_for_update() then completes the first one."""
+    path, c, gates, obstacles, start, goal = track
+    c2 = json.loads(json.dumps(c))
+    c2["path_planner_properties"]["recalculate_online"] = True
+    c2["path_planner_properties"]["samples_fmt"] = 1 << 20  # a replan of ~10 ms
+    p2 = os.path.join(os.path.dirname(path), "config_async_busy.json")
+    open(p2, "w").write(json.dumps(c2))
+    otg = _ot().OnlineTrajGenerator(start, goal, gates, obstacles, p2)
+    otg.pre_compute_traj(0.0)
+    before = otg.get_planned_traj()
+    i = int(np.argmin(np.abs(before[:, 9] - 5.0)))
+    drone = before[i, [0, 3, 6]]
+    assert otg.update_gate_pos(4, _lateral(gates[4], 0.3), drone, True, 5.0) is True
+    with pytest.raises(RuntimeError, match="while previous update is still going on"):
+        otg.update_gate_pos(5, _lateral(gates[5], 0.3), drone, True, 5.0)
+    otg.wait_for_update()
+    assert not np.array_equal(otg.get_planned_traj(), before)
+
+
+def test_c1_plumbing_end_to_end(tmp_path, c1, geom):
+    """BASELINE config 1 (single gate + 4 obstacles, bounds [-2,2]^2 x [0,2]) end to end:
+    OnlineTrajGenerator plans start -> gate -> goal, its waypoints are valid under the
+    oracle's validators, and its trajectory equals polynomial_trajectory's
+    generate_trajectory of those waypoints and the oracle's within 1e-6 (time column
+    exact)."""
+    import polynomial_trajectory as pt
+    g, o, start, goal, w, rg, ro = c1
+    otg = _ot().OnlineTrajGenerator(start, goal, g, o, CONFIG)
+    otg.pre_compute_traj(0.0)
+    wp = otg.get_waypoints()
+    traj = otg.get_planned_traj()
+    centre = g[0, :3] + [0, 0, geom.gate_height[0]]
+    assert min(np.linalg.norm(wp - centre, axis=1)) < 1e-12  # includeGates2 inserts the gate centre
+    _path_valid(wp, w, rg, ro, False)
+    rows = pt.generate_trajectory(wp, 1.0, 2.0, 0.1)
+    assert np.array_equal(rows, traj)
+    exp = O.generate_trajectory(wp, 1.0, 2.0, 0.1)
+    assert rows.shape == exp.shape and np.array_equal(rows[:, 9], exp[:, 9])
+    assert np.abs(rows[:, :9] - exp[:, :9]).max() < 1e-6

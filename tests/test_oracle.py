@@ -228,7 +228,12 @@ def test_obb_boundary_known_answers():
         assert got == c["valid"], c
 
 
-def test_oracle_vs_pure_python_track_world(cfg, geom):
+@pytest.mark.parametrize("cfg_name", ["config.json", "config_filling.json"])
+def test_oracle_vs_pure_python_track_world(cfg_name):
+    """Two independent restatements agree; config_filling.json adds a filling OBB per gate
+    (the opening), so the can_pass_gate skips are exercised too."""
+    cfg = config.load(os.path.join(os.path.dirname(GOLDEN), "..", "configs", cfg_name))
+    geom = config.geometry(cfg)
     rg, ro = config.inflate_radii(cfg)
     gates, obstacles = synth.track_world(42)
     w = O.world_build(geom, gates, obstacles, rg, ro)
@@ -240,16 +245,27 @@ def test_oracle_vs_pure_python_track_world(cfg, geom):
         assert list(o["center"]) == pw[k]["center"]
     lo, hi = synth.C2_BOUNDS
     pts = synth.sample_states(11, lo, np.array([6.0, 6.0, 1.6]), 1500)
+    # plus states in and around the gate openings (gate frame offsets, rotated by the yaw)
+    rs = np.random.RandomState(1)
+    loc = rs.uniform([-0.3, -0.05, -0.3], [0.3, 0.05, 0.3], size=(len(gates), 60, 3))
+    c, s = np.cos(gates[:, 5])[:, None], np.sin(gates[:, 5])[:, None]
+    h = geom.gate_height[gates[:, 6].astype(int)][:, None]
+    op = np.stack([gates[:, :1] + c * loc[..., 0] - s * loc[..., 1], gates[:, 1:2] + s * loc[..., 0] + c * loc[..., 1],
+                   h + loc[..., 2]], -1).reshape(-1, 3)
+    pts = np.vstack([pts, op])
+    if cfg_name == "config_filling.json":
+        assert (O.check_states(w, rg, ro, op, 1) > O.check_states(w, rg, ro, op, 0)).sum() > 20
     for cp in (0, 1):
         got = O.check_states(w, rg, ro, pts, cp)
         ref = np.array([pyref_obb.point_valid(pw, rg, ro, list(p), cp) for p in pts], np.uint8)
         assert (got == ref).all()
     s1, s2 = synth.edges(12, 13, lo, np.array([6.0, 6.0, 1.6]), 600, max_len=1.5)
     for mode in (0, 1):
-        got = O.check_motions(w, rg, ro, s1, s2, False, mode)
-        fn = pyref_obb.ray_valid if mode == 0 else pyref_obb.ray_valid_d32
-        ref = np.array([fn(pw, rg, ro, list(a), list(b), False) for a, b in zip(s1, s2)], np.uint8)
-        assert (got == ref).all()
+        for cp in (0, 1):
+            got = O.check_motions(w, rg, ro, s1, s2, cp, mode)
+            fn = pyref_obb.ray_valid if mode == 0 else pyref_obb.ray_valid_d32
+            ref = np.array([fn(pw, rg, ro, list(a), list(b), cp) for a, b in zip(s1, s2)], np.uint8)
+            assert (got == ref).all()
     md = O.check_states_mindist(w, pts, 0.3)
     ref = np.array([pyref_obb.point_valid_mindist(pw, list(p), 0.3) for p in pts], np.uint8)
     assert (md == ref).all()
