@@ -503,6 +503,8 @@ def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None):
     * value: state validity checks/s on 1 thread (OMPL calls the plugins one query at a
       time) over the C2 batch; all_cores_value: the same on CPU_SHARE_THREADS threads;
     * c3_*: C3 motion checks (512 OBBs) analytic / discrete32 on CPU_SHARE_THREADS threads;
+    * full_plan_ms_per_track: the C4 track planned by the CPU restatement of the same batch
+      planner (paths equal to the GPU's, tests/test_gpu_planner.py), CPU_SHARE_THREADS threads;
     * c5_online: the C5 loop on the oracle (world rebuild, minDistance check, min-snap +
       sampling), per-step latency, 1 thread."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -524,7 +526,7 @@ def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None):
         O.check_states(w, rg, ro, pts, False, threads=nt)
     dt2 = (time.perf_counter() - t2) / 3
     out = {"value": reps * N_STATES / dt, "unit": "state validity checks/s", "cores": 1, "kind": "port",
-           "sample": f"{reps} passes over the same 1,048,576-state C2 batch ({reps * N_STATES} checks, {dt:.1f} s)",
+           "sample": f"{reps} passes over the same {N_STATES:,}-state C2 batch ({reps * N_STATES} checks, {dt:.1f} s)",
            "all_cores_value": N_STATES / dt2, "all_cores_threads": nt, "host": host_info()}
     # C3 motions: 512 OBBs, the same edge generator as the GPU leg (bounded edge counts)
     g3, o3 = synth.track_world(42, n_obstacles=472)
@@ -535,6 +537,27 @@ def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None):
         O.check_motions(w3, rg, ro, s1, s2, False, mode, threads=nt)
         el = time.perf_counter() - t
         out[key] = {"edges_per_s": n / el, "threads": nt, "edges": n}
+    # C4 full plan on the CPU: the same batch planner restated (oracle/track_planner.py):
+    # 9 gate-to-gate plans (65,536 samples, k = 16; each plan's checks and k-NN on nt
+    # threads) + includeGates2 + min-snap + sampling, the rank-0 track (seed 100)
+    import track_planner as TP
+    from eppamd import config as cfgmod
+    c4, c4path = _track_config()
+    os.unlink(c4path)
+    g4, o4 = synth.track_world(100)
+    w4 = O.world_build(geom, g4, o4, rg, ro)
+    ends = synth.gate_checkpoints(g4, geom.gate_height, 0.55)
+    cps = np.vstack([ends[0], synth.gate_checkpoints(g4, geom.gate_height,
+                                                     c4["path_planner_properties"]["checkpoint_gate_offset"]), ends[-1]])
+    tg = c4["trajectory_generator_properties"]
+    lo4, hi4 = cfgmod.bounds(c4)
+    t = time.perf_counter()
+    wp4, rows4 = TP.plan_track(w4, rg, ro, lo4, hi4, cps, PLAN_SAMPLES, tg["max_velocity"], tg["max_acceleration"],
+                               tg["sampling_interval"], threads=nt)
+    out["full_plan_ms_per_track"] = (time.perf_counter() - t) * 1e3
+    out["full_plan"] = {"threads": nt, "tracks": 1, "waypoints": int(len(wp4)), "traj_rows": int(len(rows4)),
+                        "workload": "C4 rank-0 track: 9 batch plans (65,536 samples, k=16) + includeGates2 + "
+                                    "min-snap + sampling, the planner restated on the CPU (oracle/track_planner.py)"}
     if c5_inputs:
         c = c5_inputs
         lat = c5_online(c["cfg_path"], c["geom"], c["gates"], c["obstacles"], c["wp"], c["window"], c["vmax"],

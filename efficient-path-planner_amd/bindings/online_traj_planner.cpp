@@ -159,6 +159,24 @@ PYBIND11_MODULE(online_traj_planner, m) {
                 return out;
             },
             py::arg("problems"), py::arg("timeLimit"))
+        .def(
+            "plan_once",  // one batch-planner attempt with an explicit sample count and seed
+            [](const epp::PathPlanner& self, const py::object& start, const py::object& goal, int64_t samples,
+               uint64_t seed) -> py::object {
+                Vec3 s = to_vec3(start), g = to_vec3(goal);
+                std::vector<Vec3> path;
+                bool ok;
+                {
+                    py::gil_scoped_release release;
+                    ok = self.planOnce(s, g, samples, seed, path);
+                }
+                if (!ok) return py::none();
+                py::array_t<double> out({(py::ssize_t)path.size(), (py::ssize_t)3});
+                for (size_t i = 0; i < path.size(); ++i)
+                    for (int k = 0; k < 3; ++k) out.mutable_data()[i * 3 + k] = path[i][k];
+                return out;
+            },
+            py::arg("start"), py::arg("goal"), py::arg("samples"), py::arg("seed"))
         .def("set_seed", &epp::PathPlanner::setSeed)
         .def("set_neighbours", &epp::PathPlanner::setNeighbours)
         .def("last_stats", [](const epp::PathPlanner& self) {

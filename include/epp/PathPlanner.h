@@ -57,14 +57,16 @@ public:
     void setSeed(uint64_t seed) { seed_ = seed; }
     void setNeighbours(int k) { k_ = k; }
     const PlannerStats& lastStats() const { return stats_; }
+    // One batch-planner attempt with an explicit sample count and RNG seed (planPath makes
+    // up to 4 of them); public for the CPU restatement's path-equality tests and baselines.
+    bool planOnce(const Vec3& start, const Vec3& goal, int64_t samples, uint64_t seed,
+                  std::vector<Vec3>& out) const;
 
     std::shared_ptr<World> worldPtr;
 
 private:
     std::vector<Vec3> pruneWaypoints(const std::vector<Vec3>& waypoints) const;
     std::vector<Vec3> shortcut(const std::vector<Vec3>& path) const;
-    bool planOnce(const Vec3& start, const Vec3& goal, int64_t samples, uint64_t seed,
-                  std::vector<Vec3>& out) const;
     bool planCall(const Vec3& start, const Vec3& goal, double timeLimit, uint64_t call, std::vector<Vec3>& out,
                   int& attempts) const;
 

@@ -52,6 +52,7 @@ def lib() -> C.CDLL:
             "or_invert_mapping": (None, [vp, vp]),
             "or_poly_eval": (dp, [vp, dp, i32]),
             "or_random_vertices": (None, [i32, i32, dp, dp, u64, vp]),
+            "or_plan_once": (i32, [vp, i32, dp, dp, vp, vp, vp, vp, i64, u64, i32, i32, i32, vp, i32, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(l, name)
@@ -185,3 +186,19 @@ def random_vertices(n_segments, dim, pos_min, pos_max, seed):
     out = np.zeros((n_segments + 1, dim))
     lib().or_random_vertices(n_segments, dim, pos_min, pos_max, seed, _p(out))
     return out
+
+
+def plan_once(w, r_gate, r_obst, lo, hi, start, goal, samples, seed, k=16, can_pass_gate=False, threads=1):
+    """CPU restatement of PathPlanner::planOnce (this build's batch planner): the path as an
+    (L, 3) array, or None; plus (samples, valid samples, edges, valid edges)."""
+    lo, hi = np.ascontiguousarray(lo, np.float64), np.ascontiguousarray(hi, np.float64)
+    start, goal = np.ascontiguousarray(start, np.float64), np.ascontiguousarray(goal, np.float64)
+    cap = 4096
+    path = np.zeros((cap, 3))
+    stats = np.zeros(4, np.int64)
+    n = lib().or_plan_once(_p(w), len(w), r_gate, r_obst, _p(lo), _p(hi), _p(start), _p(goal), int(samples),
+                           int(seed) & 0xFFFFFFFFFFFFFFFF, int(k), int(bool(can_pass_gate)), int(threads), _p(path),
+                           cap, _p(stats))
+    if n < 0:
+        raise ValueError("or_plan_once: path buffer too small")
+    return (path[:n].copy() if n > 0 else None), stats

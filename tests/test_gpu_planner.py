@@ -567,3 +567,58 @@ def test_c1_plumbing_end_to_end(tmp_path, c1, geom):
     exp = O.generate_trajectory(wp, 1.0, 2.0, 0.1)
     assert rows.shape == exp.shape and np.array_equal(rows[:, 9], exp[:, 9])
     assert np.abs(rows[:, :9] - exp[:, :9]).max() < 1e-6
+
+
+# ---- the planner against its CPU restatement (oracle/epp_oracle.cpp or_plan_once) ------
+# Same counter-RNG samples, exact k-NN with the same tie rule, the same A* and shortcut:
+# the GPU pipeline must give the SAME path, not just a valid one.
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_plan_once_equals_cpu_restatement(c1, seed):
+    g, o, start, goal, w, rg, ro = c1
+    pp = _ot().PathPlanner(g, o, CONFIG)
+    lo, hi = synth.C1_BOUNDS
+    for samples in (1000, 4096, 20_000):
+        got = pp.plan_once(start, goal, samples, seed)
+        exp, st = O.plan_once(w, rg, ro, lo, hi, start, goal, samples, seed, 16, False, 8)
+        assert (got is None) == (exp is None)
+        if got is not None:
+            assert np.array_equal(got, exp), (samples, got, exp)
+    blocked = np.array([1.0, 0.5, 0.5])
+    assert pp.plan_once(start, blocked, 4096, seed) is None
+    assert O.plan_once(w, rg, ro, lo, hi, start, blocked, 4096, seed, 16, False, 4)[0] is None
+
+
+def test_plan_once_equals_cpu_restatement_track(track, geom):
+    """Every gate-to-gate segment of the C2 track (65,536 samples, the C4 size) equal on
+    GPU and CPU."""
+    path, c, gates, obstacles, start, goal = track
+    pp = _ot().PathPlanner(gates, obstacles, path)
+    rg, ro = config.inflate_radii(c)
+    w = O.world_build(geom, gates, obstacles, rg, ro)
+    lo, hi = np.array(c["world_properties"]["lower_bound"], float), np.array(c["world_properties"]["upper_bound"], float)
+    cps = synth.gate_checkpoints(gates, geom.gate_height, c["path_planner_properties"]["checkpoint_gate_offset"])
+    cps = np.vstack([start, cps, goal])
+    for s in range(0, len(cps) - 1, 2):
+        got = pp.plan_once(cps[s], cps[s + 1], 65536, 1000 + s)
+        exp, _ = O.plan_once(w, rg, ro, lo, hi, cps[s], cps[s + 1], 65536, 1000 + s, 16, False, 16)
+        assert got is not None and np.array_equal(got, exp), s
+
+
+def test_precompute_traj_equals_cpu_track(track, geom):
+    """OnlineTrajGenerator::preComputeTraj (9 concurrent GPU plans + includeGates2 +
+    min-snap) equals the CPU restatement of the whole track (oracle/track_planner.py):
+    identical waypoints, trajectory within 1e-6 with the time column exact."""
+    import track_planner as TP
+    path, c, gates, obstacles, start, goal = track
+    otg = _ot().OnlineTrajGenerator(start, goal, gates, obstacles, path)
+    otg.pre_compute_traj(0.0)
+    rg, ro = config.inflate_radii(c)
+    w = O.world_build(geom, gates, obstacles, rg, ro)
+    lo, hi = np.array(c["world_properties"]["lower_bound"], float), np.array(c["world_properties"]["upper_bound"], float)
+    tg, pp = c["trajectory_generator_properties"], c["path_planner_properties"]
+    wp, rows = TP.plan_track(w, rg, ro, lo, hi, otg.get_checkpoints(), pp["samples_fmt"], tg["max_velocity"],
+                             tg["max_acceleration"], tg["sampling_interval"], threads=8)
+    assert np.array_equal(otg.get_waypoints(), wp)
+    traj = otg.get_planned_traj()
+    assert traj.shape == rows.shape and np.array_equal(traj[:, 9], rows[:, 9])
+    assert np.abs(traj[:, :9] - rows[:, :9]).max() < 1e-6

@@ -291,3 +291,27 @@ def test_counter_sampler_matches_oracle():
     a = synth.sample_states(7, lo, hi, 5000)
     b = O.sample_states(7, lo, hi, 5000)
     assert np.array_equal(a, b)
+
+
+def test_cpu_planner_restatement_basic(cfg, geom):
+    """or_plan_once (the CPU restatement of the batch planner): deterministic, thread-count
+    independent, valid paths under the oracle's validators, None for a blocked goal; the
+    k-NN inside matches brute force (ties to the lower index)."""
+    rg, ro = config.inflate_radii(cfg)
+    g, o, start, goal = synth.c1_world()
+    w = O.world_build(geom, g, o, rg, ro)
+    lo, hi = synth.C1_BOUNDS
+    a, sa = O.plan_once(w, rg, ro, lo, hi, start, goal, 3000, 7, 16, False, 1)
+    b, sb = O.plan_once(w, rg, ro, lo, hi, start, goal, 3000, 7, 16, False, 5)
+    assert a is not None and np.array_equal(a, b) and np.array_equal(sa, sb)
+    assert np.array_equal(a[0], start) and np.array_equal(a[-1], goal)
+    assert O.check_motions(w, rg, ro, a[:-1], a[1:]).all()
+    assert O.plan_once(w, rg, ro, lo, hi, start, np.array([1.0, 0.5, 0.5]), 3000, 7)[0] is None
+
+
+def test_track_planner_seed_derivation():
+    """track_planner.mix / call_seed restate host_planner.cpp's 64-bit mixing (spot values
+    computed with the C++ expression)."""
+    import track_planner as TP
+    assert TP.mix(0, 0) == 0xE220A8397B1DCDAF
+    assert TP.mix(0x5EED, 12345678901234) == 0x15220C2B70B99518
