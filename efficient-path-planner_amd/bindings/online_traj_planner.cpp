@@ -10,6 +10,7 @@
 #include <stdexcept>
 #include <string>
 
+#include "epp/MultiTrackPlanner.h"
 #include "epp/OnlineTrajGenerator.h"
 
 namespace py = pybind11;
@@ -192,6 +193,34 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["ms_search"] = s.ms_search;
             return d;
         });
+
+    // planTracks (include/epp/MultiTrackPlanner.h): independent tracks across GPUs of this
+    // node, one host thread per device, waypoint sets all-gathered over RCCL
+    m.def(
+        "plan_tracks",
+        [](const py::list& problems, const std::string& configPath, const std::vector<int>& devices,
+           double takeoffTime) {
+            std::vector<epp::TrackProblem> tp;
+            for (const auto& item : problems) {
+                py::tuple t = py::reinterpret_borrow<py::tuple>(item);
+                if (t.size() != 4) throw std::invalid_argument("problems: (start, goal, gates, obstacles) tuples");
+                tp.push_back({to_vec3(t[0]), to_vec3(t[1]), to_matrix(t[2]), to_matrix(t[3])});
+            }
+            std::vector<epp::TrackResult> res;
+            {
+                py::gil_scoped_release release;
+                res = epp::planTracks(tp, configPath, devices, takeoffTime);
+            }
+            py::list out;
+            for (const auto& r : res) {
+                py::array_t<double> wp({(py::ssize_t)r.waypoints.size(), (py::ssize_t)3});
+                for (size_t i = 0; i < r.waypoints.size(); ++i)
+                    for (int k = 0; k < 3; ++k) wp.mutable_data()[i * 3 + k] = r.waypoints[i][k];
+                out.append(py::make_tuple(wp, from_matrix(r.trajectory), r.device));
+            }
+            return out;
+        },
+        py::arg("problems"), py::arg("configPath"), py::arg("devices"), py::arg("takeoffTime") = 0.0);
 
     py::class_<epp::OnlineTrajGenerator>(m, "OnlineTrajGenerator")
         .def(py::init([](const py::object& start, const py::object& goal, const py::object& gates,

@@ -1,0 +1,228 @@
+// comm.cpp — the multi-track path's one exchange step over RCCL (xGMI): every rank plans
+// its own track, then the final waypoint sets are all-gathered (the
+// reference has no multi-GPU code).  RCCL is opened at first use (dlopen of
+// librccl.so.1: the one already in the process, e.g. PyTorch's, or ROCm's), so the
+// library does not depend on it unless the exchange is used.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "epp_internal.h"
+
+namespace epp {
+namespace {
+
+struct Rccl {
+    void* h = nullptr;
+    decltype(&ncclGetUniqueId) getUniqueId = nullptr;
+    decltype(&ncclCommInitRank) commInitRank = nullptr;
+    decltype(&ncclCommInitAll) commInitAll = nullptr;
+    decltype(&ncclCommDestroy) commDestroy = nullptr;
+    decltype(&ncclAllGather) allGather = nullptr;
+    decltype(&ncclGetErrorString) errorString = nullptr;
+};
+
+const Rccl* rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+            r.h = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+            if (r.h) break;
+        }
+        if (!r.h) return;
+        r.getUniqueId = reinterpret_cast<decltype(r.getUniqueId)>(dlsym(r.h, "ncclGetUniqueId"));
+        r.commInitRank = reinterpret_cast<decltype(r.commInitRank)>(dlsym(r.h, "ncclCommInitRank"));
+        r.commInitAll = reinterpret_cast<decltype(r.commInitAll)>(dlsym(r.h, "ncclCommInitAll"));
+        r.commDestroy = reinterpret_cast<decltype(r.commDestroy)>(dlsym(r.h, "ncclCommDestroy"));
+        r.allGather = reinterpret_cast<decltype(r.allGather)>(dlsym(r.h, "ncclAllGather"));
+        r.errorString = reinterpret_cast<decltype(r.errorString)>(dlsym(r.h, "ncclGetErrorString"));
+    });
+    if (!r.h || !r.getUniqueId || !r.commInitRank || !r.commInitAll || !r.commDestroy || !r.allGather ||
+        !r.errorString) {
+        set_error("epp_comm: RCCL (librccl.so.1) is not available");
+        return nullptr;
+    }
+    return &r;
+}
+
+epp_status nccl_error(const Rccl* r, ncclResult_t e, const char* what) {
+    set_error(std::string(what) + ": " + r->errorString(e));
+    return EPP_ERR_RUNTIME;
+}
+
+}  // namespace
+}  // namespace epp
+
+struct epp_comm {
+    ncclComm_t comm = nullptr;
+    int n_ranks = 0, rank = 0, device = 0;
+    char* d_buf = nullptr;  // counts (n_ranks + 1 int32, padded) | send set | gathered sets
+    size_t cap = 0;
+    hipStream_t stream = nullptr;
+};
+
+using namespace epp;
+
+extern "C" {
+
+epp_status epp_comm_unique_id(uint8_t id[128]) {
+    if (!id) {
+        set_error("epp_comm_unique_id: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    const Rccl* r = rccl();
+    if (!r) return EPP_ERR_UNSUPPORTED;
+    ncclUniqueId u;
+    const ncclResult_t e = r->getUniqueId(&u);
+    if (e != ncclSuccess) return nccl_error(r, e, "ncclGetUniqueId");
+    static_assert(sizeof(u) == 128, "ncclUniqueId is 128 bytes");
+    std::memcpy(id, &u, 128);
+    return EPP_OK;
+}
+
+epp_status epp_comm_init(const uint8_t id[128], int32_t n_ranks, int32_t rank, epp_comm** out) {
+    if (!id || !out || n_ranks < 1 || rank < 0 || rank >= n_ranks) {
+        set_error("epp_comm_init: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    const Rccl* r = rccl();
+    if (!r) return EPP_ERR_UNSUPPORTED;
+    ncclUniqueId u;
+    std::memcpy(&u, id, 128);
+    epp_comm* c = new epp_comm();
+    c->n_ranks = n_ranks;
+    c->rank = rank;
+    (void)hipGetDevice(&c->device);
+    const ncclResult_t e = r->commInitRank(&c->comm, n_ranks, u, rank);
+    if (e != ncclSuccess) {
+        delete c;
+        return nccl_error(r, e, "ncclCommInitRank");
+    }
+    *out = c;
+    return EPP_OK;
+}
+
+epp_status epp_comm_init_all(int32_t n_devices, const int32_t* devices, epp_comm** out) {
+    if (n_devices < 1 || !devices || !out) {
+        set_error("epp_comm_init_all: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    const Rccl* r = rccl();
+    if (!r) return EPP_ERR_UNSUPPORTED;
+    std::vector<ncclComm_t> comms(n_devices);
+    std::vector<int> devs(devices, devices + n_devices);
+    const ncclResult_t e = r->commInitAll(comms.data(), n_devices, devs.data());
+    if (e != ncclSuccess) return nccl_error(r, e, "ncclCommInitAll");
+    for (int i = 0; i < n_devices; ++i) {
+        out[i] = new epp_comm();
+        out[i]->comm = comms[i];
+        out[i]->n_ranks = n_devices;
+        out[i]->rank = i;
+        out[i]->device = devices[i];
+    }
+    return EPP_OK;
+}
+
+epp_status epp_comm_destroy(epp_comm* c) {
+    if (!c) return EPP_OK;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(c->device);
+    if (c->d_buf) (void)hipFree(c->d_buf);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    const Rccl* r = rccl();
+    if (r && c->comm) r->commDestroy(c->comm);
+    (void)hipSetDevice(prev);
+    delete c;
+    return EPP_OK;
+}
+
+epp_status epp_comm_rank(const epp_comm* c, int32_t* rank, int32_t* n_ranks) {
+    if (!c || !rank || !n_ranks) return EPP_ERR_INVALID_ARGUMENT;
+    *rank = c->rank;
+    *n_ranks = c->n_ranks;
+    return EPP_OK;
+}
+
+epp_status epp_comm_allgather_waypoints(epp_comm* c, const double* wp, int32_t n, int32_t cap, double* out,
+                                        int32_t* counts) {
+    if (!c || n < 0 || cap < 0 || (n > 0 && !wp) || !counts || (cap > 0 && !out)) {
+        set_error("epp_comm_allgather_waypoints: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    const Rccl* r = rccl();
+    if (!r) return EPP_ERR_UNSUPPORTED;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(c->device);
+    struct Restore {
+        int d;
+        ~Restore() { (void)hipSetDevice(d); }
+    } restore{prev};
+    const int R = c->n_ranks;
+    const size_t cnt_b = ((size_t)(R + 1) * 4 + 255) & ~size_t(255);
+    hipError_t he = hipSuccess;
+    if (!c->stream) he = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    auto grow = [&](size_t need) {
+        if (he != hipSuccess || need <= c->cap) return;
+        if (c->d_buf) (void)hipFree(c->d_buf);
+        c->d_buf = nullptr;
+        c->cap = 0;
+        he = hipMalloc(&c->d_buf, need);
+        if (he == hipSuccess) c->cap = need;
+    };
+    grow(cnt_b);
+    // 1. the counts
+    if (he == hipSuccess) he = hipMemcpyAsync(c->d_buf, &n, 4, hipMemcpyHostToDevice, c->stream);
+    if (he != hipSuccess) {
+        set_error(std::string("epp_comm_allgather_waypoints: ") + hipGetErrorString(he));
+        return EPP_ERR_HIP;
+    }
+    ncclResult_t e = r->allGather(c->d_buf, c->d_buf + 4, 1, ncclInt32, c->comm, c->stream);
+    if (e != ncclSuccess) return nccl_error(r, e, "ncclAllGather (counts)");
+    he = hipMemcpyAsync(counts, c->d_buf + 4, (size_t)R * 4, hipMemcpyDeviceToHost, c->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(c->stream);
+    if (he != hipSuccess) {
+        set_error(std::string("epp_comm_allgather_waypoints: ") + hipGetErrorString(he));
+        return EPP_ERR_HIP;
+    }
+    int32_t maxw = 0;
+    for (int i = 0; i < R; ++i) maxw = std::max(maxw, counts[i]);
+    if (maxw > cap) {
+        set_error("epp_comm_allgather_waypoints: a rank has more waypoints than cap (counts filled)");
+        return EPP_ERR_CAPACITY;
+    }
+    if (maxw == 0) return EPP_OK;
+    // 2. the sets, padded to the longest (zeros after a rank's own points)
+    const size_t set_b = (size_t)maxw * 24;
+    grow(cnt_b + set_b * (R + 1));
+    char* d_send = c->d_buf + cnt_b;
+    char* d_recv = d_send + set_b;
+    if (he == hipSuccess) he = hipMemsetAsync(d_send, 0, set_b, c->stream);
+    if (he == hipSuccess && n > 0) he = hipMemcpyAsync(d_send, wp, (size_t)n * 24, hipMemcpyHostToDevice, c->stream);
+    if (he != hipSuccess) {
+        set_error(std::string("epp_comm_allgather_waypoints: ") + hipGetErrorString(he));
+        return EPP_ERR_HIP;
+    }
+    e = r->allGather(d_send, d_recv, (size_t)maxw * 3, ncclFloat64, c->comm, c->stream);
+    if (e != ncclSuccess) return nccl_error(r, e, "ncclAllGather (waypoints)");
+    for (int i = 0; i < R && he == hipSuccess; ++i)
+        if (counts[i] > 0)
+            he = hipMemcpyAsync(out + (size_t)i * cap * 3, d_recv + (size_t)i * set_b, (size_t)counts[i] * 24,
+                                hipMemcpyDeviceToHost, c->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(c->stream);
+    if (he != hipSuccess) {
+        set_error(std::string("epp_comm_allgather_waypoints: ") + hipGetErrorString(he));
+        return EPP_ERR_HIP;
+    }
+    return EPP_OK;
+}
+
+}  // extern "C"

@@ -68,6 +68,12 @@ def lib() -> C.CDLL:
             "epp_world_num_obbs": (i32, [vp, C.POINTER(i32)]),
             "epp_world_get_aabbs": (i32, [vp, vp]),
             "epp_world_generation": (i32, [vp, C.POINTER(C.c_uint64)]),
+            "epp_comm_unique_id": (i32, [vp]),
+            "epp_comm_init": (i32, [vp, i32, i32, C.POINTER(vp)]),
+            "epp_comm_init_all": (i32, [i32, vp, vp]),
+            "epp_comm_destroy": (i32, [vp]),
+            "epp_comm_rank": (i32, [vp, C.POINTER(i32), C.POINTER(i32)]),
+            "epp_comm_allgather_waypoints": (i32, [vp, vp, i32, i32, vp, vp]),
             "epp_check_states": (i32, [vp, vp, i64, i32, vp, vp, vp, vp]),
             "epp_check_states_mindist": (i32, [vp, vp, i64, dp, vp, vp]),
             "epp_check_motions": (i32, [vp, vp, vp, i64, i32, i32, vp, vp]),
@@ -118,7 +124,8 @@ EXPORTED = [
     "epp_knn_edges", "epp_compact_states", "epp_mask_edges", "epp_optimal_trajectory_host",
     "epp_spline_trajectory_host", "epp_compact_workspace_size", "epp_compact_states_ws",
     "epp_graph_begin", "epp_graph_end", "epp_graph_launch", "epp_graph_destroy", "epp_minsnap_batch_times",
-    "epp_generate_trajectory_times_host", "epp_world_generation",
+    "epp_generate_trajectory_times_host", "epp_world_generation", "epp_comm_unique_id", "epp_comm_init",
+    "epp_comm_init_all", "epp_comm_destroy", "epp_comm_rank", "epp_comm_allgather_waypoints",
 ]
 
 
@@ -464,3 +471,49 @@ def knn_edges(nodes: np.ndarray, nbr: np.ndarray):
     check(lib().epp_knn_edges(d_n.ptr, d_k.ptr, n, k, d_1.ptr, d_2.ptr, None))
     sync()
     return d_1.download(np.float64, 3 * n * k).reshape(-1, 3), d_2.download(np.float64, 3 * n * k).reshape(-1, 3)
+
+
+class Comm:
+    """RCCL communicator of the multi-track plan's exchange step (epp_comm_*).
+
+    One process per GPU: Comm(unique_id, n_ranks, rank) on the rank's device, with the
+    id from Comm.unique_id() on rank 0 shared out of band."""
+
+    def __init__(self, uid: bytes, n_ranks: int, rank: int, handle=None):
+        if handle is not None:
+            self.handle = handle
+        else:
+            assert len(uid) == 128
+            buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+            h = C.c_void_p()
+            check(lib().epp_comm_init(C.cast(buf, C.c_void_p), n_ranks, rank, C.byref(h)))
+            self.handle = h.value
+        r, n = C.c_int32(), C.c_int32()
+        check(lib().epp_comm_rank(self.handle, C.byref(r), C.byref(n)))
+        self.rank, self.n_ranks = r.value, n.value
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * 128)()
+        check(lib().epp_comm_unique_id(C.cast(buf, C.c_void_p)))
+        return bytes(buf)
+
+    @classmethod
+    def init_all(cls, devices) -> list["Comm"]:
+        devs = np.ascontiguousarray(devices, np.int32)
+        hs = (C.c_void_p * len(devs))()
+        check(lib().epp_comm_init_all(len(devs), _ptr(devs), C.cast(hs, C.c_void_p)))
+        return [cls(b"", 0, 0, handle=h) for h in hs]
+
+    def allgather_waypoints(self, wp: np.ndarray, cap: int = 4096) -> list[np.ndarray]:
+        wp = np.ascontiguousarray(np.asarray(wp, np.float64).reshape(-1, 3))
+        out = np.zeros((self.n_ranks, cap, 3))
+        counts = np.zeros(self.n_ranks, np.int32)
+        check(lib().epp_comm_allgather_waypoints(self.handle, _ptr(wp) if len(wp) else None, len(wp), cap,
+                                                 _ptr(out), _ptr(counts)))
+        return [out[r, :counts[r]].copy() for r in range(self.n_ranks)]
+
+    def close(self) -> None:
+        if self.handle:
+            lib().epp_comm_destroy(self.handle)
+            self.handle = None

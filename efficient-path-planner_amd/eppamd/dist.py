@@ -79,6 +79,17 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
 
+    def broadcast_bytes(self, b: bytes | None, n: int) -> bytes:
+        """Rank 0's n bytes on every rank (bootstraps the product's RCCL communicator)."""
+        if self.ws == 1:
+            return b
+        torch = self.torch
+        t = torch.zeros(n, dtype=torch.uint8, device=self.device)
+        if self.rank == 0:
+            t.copy_(torch.frombuffer(bytearray(b), dtype=torch.uint8))
+        self.dist.broadcast(t, 0)
+        return bytes(t.cpu().numpy().tobytes())
+
     def all_gather_waypoints(self, wp: np.ndarray) -> list[np.ndarray]:
         """All-gather of every rank's (W_r, 3) float64 waypoint set: the counts first, then
         the sets padded to max W (two collectives, a few KB each)."""

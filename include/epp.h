@@ -208,6 +208,27 @@ epp_status epp_compact_states_ws(const double* xyz, const uint8_t* valid, int64_
 /* nbr[e] = -1 where valid[e] == 0 (edges that failed the motion check), in place. */
 epp_status epp_mask_edges(int32_t* nbr, const uint8_t* valid, int64_t m, void* stream);
 
+/* ---- multi-GPU: the multi-track plan's exchange step (RCCL over xGMI) --------------- */
+/* BASELINE config 4 / SURVEY §8e: every rank (one GPU) plans its own track; the final
+ * waypoint sets are then all-gathered.  No reference counterpart (the reference is
+ * single-threaded CPU code).  RCCL is loaded at first use (librccl.so.1); without it these
+ * return EPP_ERR_UNSUPPORTED.
+ * One process per GPU: rank 0 calls epp_comm_unique_id and shares the 128 bytes out of
+ * band (e.g. torch.distributed, MPI); every rank calls epp_comm_init on its device.
+ * One process, several GPUs: epp_comm_init_all (one communicator per device; use each
+ * from its own host thread). */
+typedef struct epp_comm epp_comm;
+epp_status epp_comm_unique_id(uint8_t id[128]);
+epp_status epp_comm_init(const uint8_t id[128], int32_t n_ranks, int32_t rank, epp_comm** out);
+epp_status epp_comm_init_all(int32_t n_devices, const int32_t* devices, epp_comm** out /* n_devices */);
+epp_status epp_comm_destroy(epp_comm* comm);
+epp_status epp_comm_rank(const epp_comm* comm, int32_t* rank, int32_t* n_ranks);
+/* All-gather of every rank's waypoint set (wp: n x 3 HOST doubles): counts[r] = rank r's
+ * count (n_ranks entries), out + r * cap * 3 = its points (HOST, n_ranks x cap x 3).  Every
+ * rank must call it.  EPP_ERR_CAPACITY (counts filled) if a rank has more than cap. */
+epp_status epp_comm_allgather_waypoints(epp_comm* comm, const double* wp, int32_t n, int32_t cap, double* out,
+                                        int32_t* counts);
+
 /* ---- host-buffer convenience (synchronous; used by the C++ API shims) ------------- */
 /* generateTrajectory for one track with host buffers (poly_traj::generateTrajectory,
  * external/poly_traj/src/trajectory_generator.cpp:12-100): one fused launch (min-snap

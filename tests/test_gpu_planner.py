@@ -622,3 +622,41 @@ def test_precompute_traj_equals_cpu_track(track, geom):
     traj = otg.get_planned_traj()
     assert traj.shape == rows.shape and np.array_equal(traj[:, 9], rows[:, 9])
     assert np.abs(traj[:, :9] - rows[:, :9]).max() < 1e-6
+
+
+# ---- multi-GPU: the exchange step (RCCL) and planTracks -----------------------------
+def test_comm_single_rank_allgather():
+    """epp_comm_* on one rank (the box has one GPU): the all-gather returns the rank's own
+    ragged set, an empty set, and EPP_ERR_CAPACITY with the counts when a set exceeds cap."""
+    uid = capi.Comm.unique_id()
+    assert len(uid) == 128
+    c = capi.Comm(uid, 1, 0)
+    assert (c.rank, c.n_ranks) == (0, 1)
+    wp = synth.sample_states(3, [-6, -6, 0], [6, 6, 2], 37)
+    sets = c.allgather_waypoints(wp, cap=64)
+    assert len(sets) == 1 and np.array_equal(sets[0], wp)
+    assert c.allgather_waypoints(np.zeros((0, 3)), cap=8)[0].shape == (0, 3)
+    with pytest.raises(capi.EppError) as e:
+        c.allgather_waypoints(wp, cap=10)
+    assert e.value.code == capi.EPP_ERR_CAPACITY
+    c.close()
+    (ca,) = capi.Comm.init_all([0])
+    assert np.array_equal(ca.allgather_waypoints(wp[:5])[0], wp[:5])
+    ca.close()
+
+
+def test_plan_tracks_across_devices(track, geom):
+    """planTracks (include/epp/MultiTrackPlanner.h) over this box's GPU: every track's
+    all-gathered waypoints and trajectory equal a standalone OnlineTrajGenerator's."""
+    path, c, gates, obstacles, start, goal = track
+    g2, o2 = synth.track_world(101)
+    cps2 = synth.gate_checkpoints(g2, geom.gate_height, 0.55)
+    problems = [(start, goal, gates, obstacles), (cps2[0], cps2[-1], g2, o2), (start, goal, gates, obstacles)]
+    res = _ot().plan_tracks(problems, path, [0])
+    assert len(res) == 3
+    for (wp, traj, dev), (s, gl, g, o) in zip(res, problems):
+        otg = _ot().OnlineTrajGenerator(s, gl, g, o, path)
+        otg.pre_compute_traj(0.0)
+        assert dev == 0
+        assert np.array_equal(wp, otg.get_waypoints())
+        assert np.array_equal(traj, otg.get_planned_traj())
