@@ -13,6 +13,8 @@
 //   double  aos[n_obb][17]       the OBB table again as 136-byte records (exact path)
 //   uint32  hdr[n_lists]         candidate lists of the fine cells: start << 12 | count
 //   uint16  ids[...]             the lists' OBB ids
+//   uint8   cls8[ncells+1]       the fine-cell classes as bytes, when n_lists <= 256 (what
+//                                k_states_v5 stages; else it stages the u16 cls[])
 //   -------------------------    (everything above: staged into LDS by k_states_bm)
 //   uint16  cls[ncells+1]        fine-cell class over the padded union box: 0 = outside
 //                                every inflated AABB, else list index; the extra last
@@ -84,6 +86,7 @@ struct WorldView {
     uint32_t n_lists;
     uint32_t off_bitmap;      // cls[] (u16 per fine cell)
     uint32_t bm_words;        // index of the zero sentinel class
+    uint32_t off_cls8;        // the same classes as bytes (0: more than 255 lists, none)
     int32_t bnx, bny, bnz;    // cells per axis
     float bofx, bofy, bofz;   // offset: cell coordinate f = fmaf((float)p, bi, bof)
     float bix, biy, biz;      // 1 / cell size (float)

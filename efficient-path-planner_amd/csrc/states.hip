@@ -327,8 +327,7 @@ __global__ __launch_bounds__(kBlock4) void k_states_v4(const WorldView* __restri
 struct WaveQueue5 {
     double x[64], y[64], z[64];
     uint32_t pair[128];  // segment heads of the (state, candidate) pairs
-    uint16_t cls[64];
-    uint8_t hit[64];
+    uint32_t hdr[64];  // the queued states' list headers (start << 12 | count)
 };
 template <int BLOCK>
 constexpr uint32_t queue5_bytes() { return (BLOCK / 64) * sizeof(WaveQueue5); }
@@ -341,12 +340,32 @@ __device__ __forceinline__ uint32_t cell_axis5(double p, float off, float inv, u
     return min((uint32_t)i, nm1);  // negative -> huge -> last (empty) cell
 }
 
+// Per-wave timeline of k_states_v5 (diagnostics builds only: -DEPP_STATES_TL, see
+// scripts/states_timeline.py): lane 0 stamps s_memrealtime (100 MHz) at entry, after the
+// staging barrier, after the first group's classification (its data arrived), after its
+// exact path, at the end; plus HW_ID.
+#ifdef EPP_STATES_TL
+constexpr int kTlWaves = 1 << 16;
+__device__ unsigned long long g_states_tl[kTlWaves][6];
+#define EPP_STL(k)                                                                                  \
+    do {                                                                                            \
+        const int w_ = (int)((blockIdx.x * BLOCK + threadIdx.x) >> 6);                             \
+        const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                             \
+        if ((threadIdx.x & 63) == 0 && w_ < kTlWaves) g_states_tl[w_][k] = t_;                      \
+    } while (0)
+#else
+#define EPP_STL(k) \
+    do {           \
+    } while (0)
+#endif
+
 // PREFETCH: groups per lane > 1 (the next group's loads overlap this one's work);
 // single-pass launches (e.g. 1M states on 256 CUs) drop the second buffer's registers.
 // SPL: states per lane and group (4: 96 B = six 16-B loads, 8: 192 B = twelve); one
 // flag store of SPL bytes.  More states per lane = fewer waves, i.e. fewer executions
 // of the per-wave fixed costs (setup, staging, the exact path).
-template <bool MINDIST, bool COMPACT, int BLOCK, bool PREFETCH, int SPL>
+// SC: staging chunks (16 B) per lane: enough for the staged bytes (launcher's choice).
+template <bool MINDIST, bool COMPACT, int BLOCK, bool PREFETCH, int SPL, bool C8, int SC>
 __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict__ wv,
                                                      const double* xyz, int64_t groups, int64_t n,
                                                      int can_pass, double md, uint8_t* __restrict__ valid,
@@ -355,6 +374,7 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
     __shared__ WaveQueue5 queues[BLOCK / 64];
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_blob[];
     const int lane = threadIdx.x & 63;
+    EPP_STL(0);
     WaveQueue5* qu = &queues[threadIdx.x >> 6];
     const int64_t stride = (int64_t)gridDim.x * BLOCK;
     const int64_t gfirst = (int64_t)blockIdx.x * BLOCK;
@@ -383,7 +403,7 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
     // (LDS-DMA variants were tried: hipcc then drains vmcnt at the first use of any
     // group, prefetched ones included.)
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));  // (HIP's uint4 struct ends up on the stack)
-    constexpr int kStageChunks = (int)(kStageBudget / (BLOCK * 16));
+    constexpr int kStageChunks = SC;
     u32x4 stg[kStageChunks];
     const uint32_t n16 = stage_bytes / 16u;  // >= 1 (the class table's sentinel)
 #if defined(__HIP_DEVICE_COMPILE__)  // global (not flat) loads: flat ones would also count lgkmcnt and force vmcnt(0)
@@ -405,7 +425,8 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
         *reinterpret_cast<u32x4*>(lds_blob + 16u * (o < n16 ? o : n16)) = stg[i];
     }
     const uint32_t lists_off = wv->off_lists - wv->off_aos, ids_off = wv->off_ids - wv->off_aos;
-    const uint16_t* cls_tab = reinterpret_cast<const uint16_t*>(lds_blob + (wv->off_bitmap - wv->off_aos));
+    // the class table: bytes (C8, staged right after the lists) or u16
+    const unsigned char* cls_base = lds_blob + ((C8 ? wv->off_cls8 : wv->off_bitmap) - wv->off_aos);
     const uint32_t* hdrs = reinterpret_cast<const uint32_t*>(lds_blob + lists_off);
     const uint16_t* ids_all = reinterpret_cast<const uint16_t*>(lds_blob + ids_off);
     const double* recs = reinterpret_cast<const double*>(lds_blob);
@@ -413,10 +434,12 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
     const uint32_t nx = (uint32_t)wv->bnx, ny = (uint32_t)wv->bny, nz = (uint32_t)wv->bnz;
     const double rg = wv->r_gate, ro = wv->r_obst;
     __syncthreads();
+    EPP_STL(1);
     auto cls_of = [&](double px, double py, double pz) -> uint32_t {
         const uint32_t cx = cell_axis5(px, ox, ix, nx - 1), cy = cell_axis5(py, oy, iy, ny - 1),
                        cz = cell_axis5(pz, oz, iz, nz - 1);
-        return (uint32_t)cls_tab[__umul24(__umul24(cz, ny) + cy, nx) + cx];
+        const uint32_t idx = __umul24(__umul24(cz, ny) + cy, nx) + cx;
+        return C8 ? (uint32_t)cls_base[idx] : (uint32_t)reinterpret_cast<const uint16_t*>(cls_base)[idx];
     };
     auto process = [&](int64_t gg, const double (&v)[NV]) {
         const bool live = gg < groups;
@@ -433,8 +456,20 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
             base[k] = total;
             total += (uint32_t)__popcll(b[k]);
         }
+        EPP_STL(2);
+        // the needy states' list headers, read now (one LDS round trip for all four,
+        // overlapping the ballot arithmetic) and queued with the state
+        uint32_t hd[SPL];
+#pragma unroll
+        for (int k = 0; k < SPL; ++k) hd[k] = hdrs[needy[k] ? c[k] : 0u];  // list 0 is empty
         uint32_t hits = 0;
+#ifdef EPP_STATES_NOEXACT  // diagnostics builds only (wrong answers): the cost of the exact path
+#pragma unroll
+        for (int k = 0; k < SPL; ++k) hits |= needy[k] ? 1u << k : 0u;
+        if (false) {
+#else
         if (total > 0) {  // wave-uniform
+#endif
             uint32_t pos[SPL];
 #pragma unroll
             for (int k = 0; k < SPL; ++k) pos[k] = base[k] + lanes_below(b[k]);
@@ -447,15 +482,15 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
                         qu->x[slot] = v[3 * k];
                         qu->y[slot] = v[3 * k + 1];
                         qu->z[slot] = v[3 * k + 2];
-                        qu->cls[slot] = (uint16_t)c[k];
+                        qu->hdr[slot] = hd[k];
                     }
                 }
                 wave_lds_sync();
                 const uint32_t tq = min(total - r0, 64u);
                 // lane e < tq owns queued state e: its candidate list
                 const bool act = (uint32_t)lane < tq;
-                const uint32_t hd = hdrs[act ? (uint32_t)qu->cls[lane] : 0u];  // list 0 is empty
-                const uint32_t cnt = hd & 4095u, first = hd >> 12;
+                const uint32_t hq = act ? qu->hdr[lane] : 0u;
+                const uint32_t cnt = hq & 4095u, first = hq >> 12;
                 uint32_t ptot;
                 const uint32_t poff = wave_excl_scan(cnt, lane, ptot);
                 bool hit_e = false;
@@ -491,8 +526,12 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
                     const bool hi = end > 64u && bits(m1, poff > 64u ? poff - 64u : 0u, end - max(poff, 64u));
                     hit_e = act && (lo || hi);
                 } else if (act) {  // long lists: each queued state walks its own
-                    hit_e = states_exact_rec<MINDIST>(lds_blob, lists_off, ids_off, rg, ro, qu->x[lane], qu->y[lane],
-                                                      qu->z[lane], qu->cls[lane], can_pass, md);
+                    const double* rc = reinterpret_cast<const double*>(lds_blob);
+                    const uint16_t* idl = reinterpret_cast<const uint16_t*>(lds_blob + ids_off) + first;
+                    const double px = qu->x[lane], py = qu->y[lane], pz = qu->z[lane];
+                    for (uint32_t j = 0; j < cnt; ++j)
+                        hit_e |= rec_hit<MINDIST>(rc + (size_t)idl[j] * kRecDoubles, rg, ro, px, py, pz, can_pass != 0,
+                                                  md);
                 }
                 // back to the owners: state slot r0 + e lives on lane e
                 const unsigned long long hm = __ballot(hit_e);
@@ -504,6 +543,7 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
                 wave_lds_sync();  // the queue is rewritten next
             }
         }
+        EPP_STL(3);
         const uint32_t fl = live ? (~hits & ((1u << SPL) - 1u)) : 0u;  // bit k: state SPL gg + k valid
         if (live) {
             if (SPL == 4) {
@@ -545,6 +585,15 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
             process(g, va);
         }
     }
+#ifdef EPP_STATES_TL
+    EPP_STL(4);
+    if (lane == 0) {
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        const int w_ = (int)((blockIdx.x * BLOCK + threadIdx.x) >> 6);
+        if (w_ < kTlWaves) g_states_tl[w_][5] = hw;
+    }
+#endif
     if (blockIdx.x == 0 && threadIdx.x < (int)(n - SPL * groups)) {  // tail: the last n % SPL states
         const int64_t i = SPL * groups + threadIdx.x;
         const double px = xyz[3 * i], py = xyz[3 * i + 1], pz = xyz[3 * i + 2];
@@ -570,9 +619,14 @@ StatesKernel forced_kernel() {
     return k == "generic" ? StatesKernel::Generic : k == "v4" ? StatesKernel::V4 : StatesKernel::V5;
 }
 
-// k_states_v5 stages [off_aos, blob_bytes) next to its wave queues
+// k_states_v5 stages records, lists and the class table (bytes when there are, else u16):
+// [off_aos, end of the byte table) or [off_aos, blob_bytes)
+uint32_t v5_staged(const WorldView& w) {
+    const uint32_t cells = w.bm_words + 1;
+    return (w.off_cls8 ? ((w.off_cls8 + cells + 15u) & ~15u) : w.blob_bytes) - w.off_aos;
+}
 bool v5_fits(const WorldView& w) {
-    const uint32_t sb = w.blob_bytes - w.off_aos;
+    const uint32_t sb = v5_staged(w);
     return sb <= kStageBudget && sb + 16u + queue5_bytes<1024>() <= 160u * 1024u;
 }
 
@@ -625,14 +679,26 @@ epp_status launch_states(const WorldView& w, const WorldView* dw, const double* 
     const StatesKernel want = forced_kernel();
     const bool x16 = (reinterpret_cast<uintptr_t>(xyz) & 15) == 0;
     if (want == StatesKernel::V5 && v5_fits(w) && x16 && (reinterpret_cast<uintptr_t>(valid) & 3) == 0) {
-        const uint32_t sb = w.blob_bytes - w.off_aos;
+        const uint32_t sb = v5_staged(w);
         const V5Shape sh = v5_shape(n, sb);
         const uint32_t dyn = sb + 16u;  // the staged world + the dummy slot of the copy
-#define EPP_LAUNCH_V5(C, B, P)                                                                                  \
-    do {                                                                                                        \
-        allow_lds(k_states_v5<MINDIST, C, B, P, 4>, queue5_bytes<B>());                                         \
-        hipLaunchKernelGGL((k_states_v5<MINDIST, C, B, P, 4>), dim3(sh.grid), dim3(B), dyn, st, dw, xyz, sh.gN, n, \
-                           can_pass, md, valid, compact_idx, nv, sb);                                           \
+#define EPP_LAUNCH_V5S(C, B, P, C8, SC)                                                                              \
+    do {                                                                                                             \
+        allow_lds(k_states_v5<MINDIST, C, B, P, 4, C8, SC>, queue5_bytes<B>());                                      \
+        hipLaunchKernelGGL((k_states_v5<MINDIST, C, B, P, 4, C8, SC>), dim3(sh.grid), dim3(B), dyn, st, dw, xyz, sh.gN, \
+                           n, can_pass, md, valid, compact_idx, nv, sb);                                             \
+    } while (0)
+        // staging chunks per lane: half the budget's when the staged bytes fit in it
+        const bool half_stage = sb <= (uint32_t)kStageBudget / 2;
+#define EPP_LAUNCH_V5C(C, B, P, C8)                                                              \
+    do {                                                                                         \
+        if (half_stage) EPP_LAUNCH_V5S(C, B, P, C8, (int)(kStageBudget / 2 / (B * 16)));         \
+        else EPP_LAUNCH_V5S(C, B, P, C8, (int)(kStageBudget / (B * 16)));                        \
+    } while (0)
+#define EPP_LAUNCH_V5(C, B, P)                                 \
+    do {                                                       \
+        if (w.off_cls8) EPP_LAUNCH_V5C(C, B, P, true);          \
+        else EPP_LAUNCH_V5C(C, B, P, false);                    \
     } while (0)
 #define EPP_LAUNCH_V5B(B)                                \
     do {                                                 \
@@ -648,6 +714,8 @@ epp_status launch_states(const WorldView& w, const WorldView* dw, const double* 
         else EPP_LAUNCH_V5B(1024);
 #undef EPP_LAUNCH_V5B
 #undef EPP_LAUNCH_V5
+#undef EPP_LAUNCH_V5C
+#undef EPP_LAUNCH_V5S
         return launch_error(what);
     }
     if (want != StatesKernel::Generic && x16 && (reinterpret_cast<uintptr_t>(valid) & 1) == 0 &&
@@ -713,6 +781,15 @@ epp_status epp_check_states(const epp_world* world, const double* xyz, int64_t n
     return launch_states<false>(world_view(world), world_dview(world), xyz, n, can_pass_gate, 0.0, valid,
                                 compact_idx, n_valid, stream);
 }
+
+#ifdef EPP_STATES_TL
+// diagnostics builds only: the per-wave timeline of the last k_states_v5 launch
+epp_status epp_dbg_states_tl(unsigned long long* out, int64_t waves) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_states_tl), (size_t)std::min<int64_t>(waves, kTlWaves) * 48) == hipSuccess
+               ? EPP_OK
+               : EPP_ERR_HIP;
+}
+#endif
 
 epp_status epp_check_states_mindist(const epp_world* world, const double* xyz, int64_t n, double min_distance,
                                     uint8_t* valid, void* stream) {

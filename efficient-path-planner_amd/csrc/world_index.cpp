@@ -315,7 +315,10 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
     const size_t off_aos = align16(off_soa + soa.size() * sizeof(double));
     const size_t off_lists = align16(off_aos + aos.size() * sizeof(double));
     const size_t off_ids = off_lists + hdr.size() * 4;
-    const size_t off_bm = align16(off_ids + flat.size() * 2);
+    // byte classes (k_states_v5 stages them instead of the u16 table) when the lists fit
+    const bool c8 = hdr.size() <= 256;
+    const size_t off_c8 = align16(off_ids + flat.size() * 2);
+    const size_t off_bm = c8 ? align16(off_c8 + cls.size()) : off_c8;
     const size_t total = align16(off_bm + cls.size() * 2);
     if (total > 0xFFFFFFFFull) {
         set_error("epp_world: index too large");
@@ -334,6 +337,9 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
     v.off_ids = (uint32_t)off_ids;
     v.off_aos = (uint32_t)off_aos;
     std::memcpy(b + off_bm, cls.data(), cls.size() * 2);
+    if (c8)
+        for (size_t c = 0; c < cls.size(); ++c) b[off_c8 + c] = (char)(uint8_t)cls[c];
+    v.off_cls8 = c8 ? (uint32_t)off_c8 : 0u;
     v.off_lists = (uint32_t)off_lists;
     v.off_bitmap = (uint32_t)off_bm;
     v.blob_bytes = (uint32_t)total;
