@@ -44,7 +44,34 @@ __global__ __launch_bounds__(kBlock) void k_motions(WorldView w, const double* _
     }
 }
 
-constexpr int kQueueM = 256;  // queued (edge, OBB) pairs per wave  // queued pairs per wave
+constexpr int kQueueM = 256;  // queued (edge, OBB) pairs per wave
+
+// Per-wave time split of k_motions_v4 (diagnostics builds only: -DEPP_MOTIONS_TL, see
+// scripts/motions_timeline.py): shader-clock cycles spent in the level-1/2 walk, in the
+// flushes, and in total, plus the pairs walked / queued.
+#ifdef EPP_MOTIONS_TL
+constexpr int kMtlWaves = 1 << 16;
+__device__ unsigned long long g_motions_tl[kMtlWaves][6];
+#define EPP_MTL_DECL unsigned long long tl_walk = 0, tl_flush = 0, tl_t0 = __builtin_readcyclecounter(), tl_e = 0, tl_q = 0, tl_c = 0
+#define EPP_MTL_ADD(v, t) v += __builtin_readcyclecounter() - (t)
+#define EPP_MTL_NOW(t) const unsigned long long t = __builtin_readcyclecounter()
+#define EPP_MTL_CNT(v, x) v += (x)
+#define EPP_MTL_END                                                                                   \
+    do {                                                                                              \
+        const int w_ = (int)((blockIdx.x * BLOCK + threadIdx.x) >> 6);                               \
+        if (lane == 0 && w_ < kMtlWaves) {                                                           \
+            g_motions_tl[w_][0] = tl_walk; g_motions_tl[w_][1] = tl_flush;                            \
+            g_motions_tl[w_][2] = __builtin_readcyclecounter() - tl_t0; g_motions_tl[w_][3] = tl_e;   \
+            g_motions_tl[w_][4] = tl_q; g_motions_tl[w_][5] = tl_c;                                   \
+        }                                                                                             \
+    } while (0)
+#else
+#define EPP_MTL_DECL
+#define EPP_MTL_ADD(v, t)
+#define EPP_MTL_NOW(t)
+#define EPP_MTL_CNT(v, x)
+#define EPP_MTL_END
+#endif
 
 // ---- k_motions_v4: analytic motion checks, lane-balanced candidate walk ---------------
 // v3's walk is per lane, so a wave pays its worst lane's list length (C3: 28.5 entries
@@ -99,6 +126,7 @@ __global__ __launch_bounds__(BLOCK) void k_motions_v4(const WorldView* __restric
     const float ofx = wv->ofx, ofy = wv->ofy, ofz = wv->ofz, i4x = wv->i4x, i4y = wv->i4y, i4z = wv->i4z;
     const double rg = wv->r_gate, ro = wv->r_obst;
     __syncthreads();
+    EPP_MTL_DECL;
     const int64_t stride = (int64_t)gridDim.x * BLOCK;
     for (int64_t i0 = (int64_t)blockIdx.x * BLOCK + wave * 64; i0 < n; i0 += stride) {
         const int64_t i = i0 + lane;
@@ -140,7 +168,9 @@ __global__ __launch_bounds__(BLOCK) void k_motions_v4(const WorldView* __restric
 
         // exact tests of the queued pairs (wave-uniform call sites only)
         auto flush = [&]() {
+            EPP_MTL_NOW(tf);
             const uint32_t total = *qcount;
+            EPP_MTL_CNT(tl_q, total);
             for (uint32_t base = 0; base < total; base += 64) {
                 const uint32_t j = base + lane;
                 const bool has = j < total;
@@ -169,8 +199,11 @@ __global__ __launch_bounds__(BLOCK) void k_motions_v4(const WorldView* __restric
             wave_lds_sync();
             if (lane == 0) *qcount = 0u;
             wave_lds_sync();
+            EPP_MTL_ADD(tl_flush, tf);
         };
 
+        EPP_MTL_NOW(tw);
+        EPP_MTL_CNT(tl_c, total_c);
         uint32_t carry_owner = 0u;
         for (uint32_t cb = 0; cb < total_c; cb += 64) {
             // level 1: lane -> (owner edge, cell)
@@ -195,6 +228,7 @@ __global__ __launch_bounds__(BLOCK) void k_motions_v4(const WorldView* __restric
             const uint32_t seg = x | (y << 8) | (z << 16) | (owner << 24);
             uint32_t total_e;
             const uint32_t offe = wave_excl_scan(len, lane, total_e);
+            EPP_MTL_CNT(tl_e, total_e);
             // level 2: lane -> (segment, list entry)
             uint32_t carry_s = 0u;
             for (uint32_t eb = 0; eb < total_e; eb += 64) {
@@ -237,10 +271,12 @@ __global__ __launch_bounds__(BLOCK) void k_motions_v4(const WorldView* __restric
                 wave_lds_sync();
             }
         }
+        EPP_MTL_ADD(tl_walk, tw);
         flush();
         if (act) valid[i] = flags[lane] ? 1 : 0;
         wave_lds_sync();
     }
+    EPP_MTL_END;
 }
 
 constexpr int kQueueD32 = 512;
@@ -452,5 +488,15 @@ epp_status epp_check_motions(const epp_world* world, const double* s1, const dou
         hipLaunchKernelGGL((k_motions<1>), dim3(grid), dim3(kBlock), 0, st, w, s1, s2, n, can_pass_gate, valid, aligned);
     return launch_error("epp_check_motions");
 }
+
+#ifdef EPP_MOTIONS_TL
+// diagnostics builds only: the per-wave time split of the last k_motions_v4 launch
+epp_status epp_dbg_motions_tl(unsigned long long* out, int64_t waves) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_motions_tl), (size_t)std::min<int64_t>(waves, kMtlWaves) * 48) ==
+                   hipSuccess
+               ? EPP_OK
+               : EPP_ERR_HIP;
+}
+#endif
 
 }  // extern "C"
