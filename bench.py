@@ -62,6 +62,15 @@ def timed_kernel_ms(capi, stream, fn, reps):
     return ms.value / reps
 
 
+def json_stdout():
+    """stdout carries only the one JSON line: everything else written to fd 1 from here on
+    (the library's own messages, e.g. PathWriter's "Folder created") goes to stderr."""
+    sys.stdout.flush()
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(fd, "w")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -82,11 +91,12 @@ def main():
         # `bench.py --gpus N` without a launcher: one child process per GPU (rank = local
         # rank = GPU index), started before this process touches the GPU
         sys.exit(spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
+    out_stream = json_stdout()
     ws, rank, local = env()
     if ws != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws} (launch one process per GPU)")
     if args.launcher_check:
-        return launcher_check(ws, rank, local)
+        return launcher_check(ws, rank, local, out_stream)
     dist = Dist(ws, rank, local, "nccl")
     import ctypes as C
 
@@ -218,12 +228,12 @@ def main():
             "cpu_baseline": cpu,
             "side": side,
         }
-        print(json.dumps(out))
+        print(json.dumps(out), file=out_stream, flush=True)
     capi.check(L.epp_stream_destroy(stream))
     dist.close()
 
 
-def launcher_check(ws, rank, local):
+def launcher_check(ws, rank, local, out_stream):
     """The multi-rank plumbing of this bench without a GPU (gloo): the same launch, env,
     barrier, max-over-ranks reduction and ragged waypoint all-gather as the GPU run."""
     from eppamd.dist import Dist
@@ -235,7 +245,7 @@ def launcher_check(ws, rank, local):
     if rank == 0:
         print(json.dumps({"n_gpus": ws, "ranks_seen": [int(s[0, 0] // 1000) for s in sets],
                           "waypoints_per_track": [len(s) for s in sets], "max_over_ranks": t,
-                          "local_rank": local}))
+                          "local_rank": local}), file=out_stream, flush=True)
     dist.close()
 
 

@@ -19,6 +19,16 @@
 //   uint16  cls[ncells+1]        fine-cell class over the padded union box: 0 = outside
 //                                every inflated AABB, else list index; the extra last
 //                                entry is 0 (out-of-range lookups)
+//   uint32  tiles[T*T][...]      motion filter (k_motions_v5): the xy extent split into
+//                                T x T tiles, each with the OBBs whose slab-rounded AABB
+//                                reaches it (<= 32 W, bit j = the tile's j-th OBB) and, per
+//                                axis k and local slab s (S per tile and axis; z is not
+//                                tiled), rows LE (bit set iff the OBB's AABB starts in a
+//                                slab <= s) and GE (ends in a slab >= s), W words each, W+1
+//                                words apart (an odd stride spreads a wave's row reads over
+//                                the LDS banks); then rows FX / FY (the OBB's first tile
+//                                along x / y is this one) and FILL (filling OBBs), and the
+//                                tile's OBB ids (u16); tile_words words per tile
 //
 // n_pad rounds n_obbs up to a multiple of 4; every array starts 16-byte aligned.
 #pragma once
@@ -90,7 +100,31 @@ struct WorldView {
     int32_t bnx, bny, bnz;    // cells per axis
     float bofx, bofy, bofz;   // offset: cell coordinate f = fmaf((float)p, bi, bof)
     float bix, biy, biz;      // 1 / cell size (float)
+    // motion tile filter (slab_n = 0: none)
+    uint32_t off_slab;
+    int32_t slab_n;           // S = 1 << slab_log: local slabs per tile and axis
+    int32_t slab_log;
+    int32_t slab_w;           // W words of OBB bits per row (a power of two, <= 32)
+    int32_t tile_n;           // T tiles per axis (x, y)
+    uint32_t tile_words;      // words per tile (a multiple of 4)
+    float sofx, sofy, sofz;   // global slab = (int)fmaf((float)p, si, sof), clamped to
+    float six, siy, siz;      // [0, G-1], G = T S (x, y) or S (z); tile = slab >> slab_log
 };
+
+constexpr int kSlabMaxWords = 32;              // tiles of up to 1024 OBBs
+constexpr size_t kSlabBudget = 40 * 1024;      // bytes of tile tables
+
+// Global slab index along one axis: the same float operations on host and device, monotone in p
+// (fmaf is correctly rounded), so an AABB overlap in doubles implies an overlap of the
+// slab ranges (the filter is a superset of the rtree query).  NaN -> 0.
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline int slab_axis(double p, float off, float inv, int S) {
+    float f = fmaf((float)p, inv, off);
+    f = fminf(fmaxf(f, 0.0f), (float)(S - 1));
+    return (int)f;
+}
 
 // Class-grid cell index along one axis: f = fmaf((float)p, inv, off), truncated.  The
 // same float operations on host and device, so the host marks exactly the cells the

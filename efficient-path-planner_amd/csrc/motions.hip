@@ -425,6 +425,270 @@ __global__ __launch_bounds__(BLOCK) void k_motions_d32b(const WorldView* __restr
     }
 }
 
+// ---- k_motions_v5: tile/slab-filtered motion checks ------------------------------------
+// The candidate set of an edge is a bit set over a tile's OBBs, computed without walking
+// any cell list.  Per axis k the edge's box [lo_k, hi_k] maps to global slabs [a_k, b_k]
+// (slab_axis: monotone, so an AABB overlap in doubles implies a slab overlap); x and y
+// slabs group into T x T tiles of S slabs.  In each tile the box reaches,
+//   cand = AND_k  LE_k[b_k] & GE_k[a_k]        (local slabs, clamped into the tile)
+// are the tile's OBBs whose slab-rounded AABB overlaps the edge's — together a superset of
+// the rtree query of World::checkRayValid (src/World.cpp:130-162).  An OBB in several of
+// those tiles is kept only in the first one along each axis (FX / FY rows), with
+// can_pass_gate the filling OBBs are masked out (:150-153).  The (edge, OBB) pairs go to
+// the wave's queue at offsets from a wave scan of the lanes' popcounts and are tested 64
+// at a time:
+//   MODE 0  exact closed AABB overlap in doubles + OBB::checkCollisionWithRay (src/OBB.cpp:10-61);
+//   MODE 1  the points s + (e - s) k/32, k = 1..32, through the rtree's strict containment
+//           and OBB::checkCollisionWithPoint (src/World.cpp:80-128, src/OBB.cpp:63-91).  The
+//           range of k that can hit is bounded first: every test is |a + b t| <= h (or
+//           lo < a + b t < hi) along the edge, so t lies in an interval, computed here
+//           with a slack eta (1e-6 m + 1e-12 of the coordinates' magnitude) far above the
+//           rounding of the points and of the interval; only the k inside it are tested
+//           exactly, in order, until one hits.  The slab range is widened by one slab per
+//           side, so points rounded past the edge's box stay covered.
+// An edge is invalid iff some pair hits — the reference's answer.
+constexpr int kQueueV5 = 256;
+
+template <int W, int MODE>
+__global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict__ wv, const double* __restrict__ s1,
+                                                     const double* __restrict__ s2, int64_t n, int can_pass,
+                                                     uint8_t* __restrict__ valid, uint32_t rec_bytes,
+                                                     uint32_t tile_bytes) {
+    constexpr int BLOCK = 1024;
+    constexpr int STRIDE = W + 1;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    EPP_MTL_DECL;
+    {
+        const uint4* src0 = reinterpret_cast<const uint4*>(wv->blob + wv->off_aos);
+        const uint4* src1 = reinterpret_cast<const uint4*>(wv->blob + wv->off_slab);
+        uint4* dst0 = reinterpret_cast<uint4*>(lds);
+        uint4* dst1 = reinterpret_cast<uint4*>(lds + rec_bytes);
+        for (uint32_t o = threadIdx.x; o < rec_bytes / 16; o += BLOCK) dst0[o] = src0[o];
+        for (uint32_t o = threadIdx.x; o < tile_bytes / 16; o += BLOCK) dst1[o] = src1[o];
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const double* recs = reinterpret_cast<const double*>(lds);
+    const uint32_t* tiles = reinterpret_cast<const uint32_t*>(lds + rec_bytes);
+    constexpr uint32_t kWaveBytes = kQueueV5 * 4 + 64;
+    unsigned char* wbase = lds + rec_bytes + tile_bytes + wave * kWaveBytes;
+    uint32_t* queue = reinterpret_cast<uint32_t*>(wbase);
+    uint8_t* flags = wbase + kQueueV5 * 4;
+    const int S = wv->slab_n, SL = wv->slab_log, T = wv->tile_n;
+    const uint32_t TW = wv->tile_words;
+    const int G[3] = {T * S, T * S, S};
+    const float sof[3] = {wv->sofx, wv->sofy, wv->sofz}, sinv[3] = {wv->six, wv->siy, wv->siz};
+    const double rg = wv->r_gate, ro = wv->r_obst;
+    const bool cp = can_pass != 0;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * BLOCK;
+    for (int64_t i0 = (int64_t)blockIdx.x * BLOCK + wave * 64; i0 < n; i0 += stride) {
+        const int64_t i = i0 + lane;
+        const bool act = i < n;
+        double s[3] = {0.0, 0.0, 0.0}, e[3] = {0.0, 0.0, 0.0};
+        if (act) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                s[k] = s1[3 * i + k];
+                e[k] = s2[3 * i + k];
+            }
+        }
+        flags[lane] = 1;
+        EPP_MTL_NOW(tl_b);
+        int ga[3], gb[3];
+        double blo[3], bhi[3];  // the edge's box (rtree query box, World.cpp:137-141)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const double lo = (e[k] < s[k]) ? e[k] : s[k];
+            const double hi = (s[k] < e[k]) ? e[k] : s[k];
+            blo[k] = MODE == 1 ? lo - (1e-9 + 1e-12 * fabs(lo)) : lo;
+            bhi[k] = MODE == 1 ? hi + (1e-9 + 1e-12 * fabs(hi)) : hi;
+            ga[k] = slab_axis(lo, sof[k], sinv[k], G[k]);
+            gb[k] = slab_axis(hi, sof[k], sinv[k], G[k]);
+            if (MODE == 1) {
+                ga[k] = ga[k] > 0 ? ga[k] - 1 : 0;
+                gb[k] = gb[k] < G[k] - 1 ? gb[k] + 1 : G[k] - 1;
+            }
+        }
+        const int tx0 = ga[0] >> SL, ty0 = ga[1] >> SL;
+        const int ntx = (gb[0] >> SL) - tx0 + 1;
+        const int ntiles = act ? ntx * ((gb[1] >> SL) - ty0 + 1) : 0;
+        uint32_t qn = 0;  // queued pairs (wave-uniform)
+        auto flush = [&]() {
+            EPP_MTL_NOW(tl_f);
+            for (uint32_t base = 0; base < qn; base += 64) {
+                const uint32_t jq = base + lane;
+                const bool has = jq < qn;
+                const uint32_t q = has ? queue[jq] : 0u;
+                const int owner = (int)(q & 63u);
+                double ps[3], pe[3];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    ps[k] = __shfl(s[k], owner);
+                    pe[k] = __shfl(e[k], owner);
+                }
+                if (has) {
+                    const double* rec = recs + (size_t)(q >> 6) * kRecDoubles;
+                    bool hit;
+                    if (MODE == 0) {  // (the AABB overlap was tested before queueing)
+                        const uint32_t m = (uint32_t)__double_as_longlong(rec[R_META]);
+                        hit = rec_ray_hit(rec, ps, pe, (m & META_GATE) ? rg : ro);
+                    } else {
+                        double rr[kRecDoubles];  // the record in registers
+#pragma unroll
+                        for (int k = 0; k <= F_HZ; ++k) rr[k] = rec[k];
+                        rr[R_META] = rec[R_META];
+                        const uint32_t m = (uint32_t)__double_as_longlong(rr[R_META]);
+                        const bool fillb = (m & META_FILLING) != 0u;
+                        const double r = (m & META_GATE) ? rg : ro;
+                        const double d[3] = {pe[0] - ps[0], pe[1] - ps[1], pe[2] - ps[2]};
+                        const double mag = fmax(fmax(fmax(fabs(ps[0]), fabs(ps[1])), fmax(fabs(ps[2]), fabs(pe[0]))),
+                                                fmax(fmax(fabs(pe[1]), fabs(pe[2])),
+                                                     fmax(fmax(fabs(rr[F_CX]), fabs(rr[F_CY])), fabs(rr[F_CZ]))));
+                        const double eta = 1e-6 + 1e-12 * mag;
+                        double t0 = 0.0, t1 = 1.0;
+                        // lo - eta <= a + b t <= hi + eta
+                        auto clip = [&](double a, double b, double lo, double hi) {
+                            const double u0 = lo - eta - a, u1 = hi + eta - a;
+                            if (b == 0.0) {
+                                if (!(u0 <= 0.0 && 0.0 <= u1)) t1 = -1.0;
+                            } else {
+                                const double v0 = u0 / b, v1 = u1 / b;
+                                t0 = fmax(t0, fmin(v0, v1));
+                                t1 = fmin(t1, fmax(v0, v1));
+                            }
+                        };
+                        // rtree contains (strict)  src/World.cpp:83
+                        clip(ps[0], d[0], rr[F_LOX], rr[F_HIX]);
+                        clip(ps[1], d[1], rr[F_LOY], rr[F_HIY]);
+                        clip(ps[2], d[2], rr[F_LOZ], rr[F_HIZ]);
+                        // OBB::checkCollisionWithPoint in the OBB frame  src/OBB.cpp:63-91
+                        const double c = rr[F_COS], sn = rr[F_SIN];
+                        const double ax = ps[0] - rr[F_CX], ay = ps[1] - rr[F_CY];
+                        const double tx = fillb ? rr[F_HX] : rr[F_HX] + r, ty = fillb ? rr[F_HY] : rr[F_HY] + r,
+                                     tz = fillb ? rr[F_HZ] : rr[F_HZ] + r;
+                        clip(c * ax + sn * ay, c * d[0] + sn * d[1], -tx, tx);
+                        clip(c * ay - sn * ax, c * d[1] - sn * d[0], -ty, ty);
+                        clip(ps[2] - rr[F_CZ], d[2], -tz, tz);
+                        int k0 = 33, k1 = 0;
+                        if (t0 <= t1) {  // (NaN bounds: fmax/fmin drop them -> the whole edge)
+                            k0 = max(1, (int)ceil(32.0 * t0));
+                            k1 = min(32, (int)floor(32.0 * t1));
+                        }
+                        hit = false;
+                        for (int k = k0; k <= k1 && !hit; ++k) {
+                            const double t = (double)k / 32.0;
+                            const double qx = ps[0] + (pe[0] - ps[0]) * t;
+                            const double qy = ps[1] + (pe[1] - ps[1]) * t;
+                            const double qz = ps[2] + (pe[2] - ps[2]) * t;
+                            hit = rec_hit<false>(rr, rg, ro, qx, qy, qz, cp, 0.0);
+                        }
+                    }
+                    if (hit) flags[owner] = 0;
+                }
+            }
+            wave_lds_sync();
+            qn = 0;
+            EPP_MTL_ADD(tl_flush, tl_f);
+        };
+        // the tiles the edges' boxes reach (wave-uniform loop; mostly one)
+        for (int j = 0;; ++j) {
+            const bool has_t = j < ntiles;
+            if (!__builtin_amdgcn_ballot_w64(has_t)) break;
+            uint32_t cand[W];
+#pragma unroll
+            for (int w = 0; w < W; ++w) cand[w] = 0u;
+            const uint16_t* ids = nullptr;
+            if (has_t) {
+                const int tx = tx0 + j % ntx, ty = ty0 + j / ntx;
+                const uint32_t* tile = tiles + (size_t)(ty * T + tx) * TW;
+                const int la[3] = {min(max(ga[0] - (tx << SL), 0), S - 1), min(max(ga[1] - (ty << SL), 0), S - 1), ga[2]};
+                const int lb[3] = {min(max(gb[0] - (tx << SL), 0), S - 1), min(max(gb[1] - (ty << SL), 0), S - 1), gb[2]};
+#pragma unroll
+                for (int w = 0; w < W; ++w) cand[w] = ~0u;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const uint32_t* le = tile + ((2 * k) * S + lb[k]) * STRIDE;
+                    const uint32_t* ge = tile + ((2 * k + 1) * S + la[k]) * STRIDE;
+#pragma unroll
+                    for (int w = 0; w < W; ++w) cand[w] &= le[w] & ge[w];
+                }
+                const uint32_t* tail = tile + 6 * S * STRIDE;
+                if (tx > tx0) {
+#pragma unroll
+                    for (int w = 0; w < W; ++w) cand[w] &= tail[w];
+                }
+                if (ty > ty0) {
+#pragma unroll
+                    for (int w = 0; w < W; ++w) cand[w] &= tail[W + w];
+                }
+                if (cp) {
+#pragma unroll
+                    for (int w = 0; w < W; ++w) cand[w] &= ~tail[2 * W + w];
+                }
+                ids = reinterpret_cast<const uint16_t*>(tail + 3 * W);
+            }
+            EPP_MTL_NOW(tl_p);
+            if (has_t) {
+                // exact prefilter: drop the candidates whose AABB misses the edge's box in
+                // doubles (closed, as the rtree query; MODE 1: the box widened by a hair,
+                // since a rounded point may sit an ulp past it), so only true rtree hits
+                // (MODE 0) reach the queue
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    uint32_t m = cand[w];
+                    while (m) {
+                        const uint32_t bit = (uint32_t)__builtin_ctz(m);
+                        m &= m - 1u;
+                        const double* rec = recs + (size_t)ids[32 * w + bit] * kRecDoubles;
+                        const bool overlap = !((rec[F_HIX] < blo[0]) | (bhi[0] < rec[F_LOX]) | (rec[F_HIY] < blo[1]) |
+                                               (bhi[1] < rec[F_LOY]) | (rec[F_HIZ] < blo[2]) | (bhi[2] < rec[F_LOZ]));
+                        if (!overlap) cand[w] &= ~(1u << bit);
+                    }
+                }
+            }
+#ifdef EPP_MOTIONS_TL
+            __builtin_amdgcn_wave_barrier();
+#endif
+            EPP_MTL_ADD(tl_e, tl_p);
+            EPP_MTL_NOW(tl_u);
+            uint32_t cnt = 0;
+#pragma unroll
+            for (int w = 0; w < W; ++w) cnt += __popc(cand[w]);
+            uint32_t total;
+            const uint32_t off = wave_excl_scan(cnt, lane, total);
+            EPP_MTL_CNT(tl_q, total);
+            // append in windows that fit the queue (one unless the edges are very long)
+            for (uint32_t done = 0; done < total;) {
+                if (qn == (uint32_t)kQueueV5) flush();
+                const uint32_t take = min((uint32_t)kQueueV5 - qn, total - done);
+                if (cnt && off < done + take && off + cnt > done) {
+                    uint32_t jj = off;
+#pragma unroll
+                    for (int w = 0; w < W; ++w) {
+                        uint32_t m = cand[w];
+                        while (m) {
+                            const uint32_t bit = (uint32_t)__builtin_ctz(m);
+                            m &= m - 1u;
+                            if (jj >= done && jj < done + take)
+                                queue[qn + jj - done] = (uint32_t)ids[32 * w + bit] << 6 | (uint32_t)lane;
+                            ++jj;
+                        }
+                    }
+                }
+                wave_lds_sync();
+                qn += take;
+                done += take;
+            }
+            EPP_MTL_ADD(tl_c, tl_u);
+        }
+        EPP_MTL_ADD(tl_walk, tl_b);
+        flush();
+        if (act) valid[i] = flags[lane];
+        wave_lds_sync();
+    }
+    EPP_MTL_END;
+}
+
 }  // namespace
 }  // namespace epp
 
@@ -432,10 +696,12 @@ using namespace epp;
 
 extern "C" {
 
-// Kernel choice: the LDS kernels (k_motions_v4 analytic, k_motions_d32b discrete32) when the
-// coarse grid, the records and the wave queues fit a CU's LDS, else k_motions.  Test hooks
-// (not for production use): EPP_MOTIONS_KERNEL=generic forces k_motions, EPP_MOTIONS_BLOCK =
-// 512 | 1024 forces the LDS kernels' workgroup size.
+// Kernel choice: k_motions_v5 (slab filter) for worlds of <= 1024 OBBs whose records and
+// slab rows fit a CU's LDS; else the cell-list LDS kernels (k_motions_v4 analytic,
+// k_motions_d32b discrete32) when the coarse grid, the records and the wave queues fit;
+// else k_motions.  Test hooks (not for production use): EPP_MOTIONS_KERNEL=generic forces
+// k_motions, =v4 skips k_motions_v5; EPP_MOTIONS_BLOCK = 512 | 1024 forces the cell-list
+// kernels' workgroup size.
 epp_status epp_check_motions(const epp_world* world, const double* s1, const double* s2, int64_t n,
                              int32_t can_pass_gate, int32_t mode, uint8_t* valid, void* stream) {
     if (!world || n < 0 || (n > 0 && (!s1 || !s2 || !valid)) || (mode != 0 && mode != 1)) {
@@ -458,6 +724,41 @@ epp_status epp_check_motions(const epp_world* world, const double* s1, const dou
     // Block size: 512 threads when two such blocks fit a CU's LDS (small worlds: C4's 64
     // OBBs, v4 28 vs 32 us per 1M edges), else 1024 (C3's 512 OBBs stage ~95 KB, one block
     // per CU, and 1024 threads double the waves behind the LDS walk: v4 52 vs 69 us)
+    // k_motions_v5 when the world has tile tables and they, the records and the queues fit
+    const bool force_v4 = forced && std::string(forced) == "v4";
+    if (!generic && !force_v4 && w.slab_n > 0) {
+        const uint32_t recb5 = (uint32_t)(((size_t)w.n_obb * kRecDoubles * 8 + 15) & ~size_t(15));
+        const uint32_t tileb = (uint32_t)((size_t)w.tile_n * w.tile_n * w.tile_words * 4);
+        const uint32_t shm5 = recb5 + tileb + 16u * (kQueueV5 * 4 + 64);
+        if (shm5 <= kLdsBudget) {
+            const int per_cu = std::max(1, std::min(2, (int)((160u * 1024u) / shm5)));
+            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + 1023) / 1024, (int64_t)cu_count() * per_cu));
+            const WorldView* dw = world_dview(world);
+#define EPP_LAUNCH_M5(WW, MM)                                                                                   \
+    do {                                                                                                        \
+        allow_lds(k_motions_v5<WW, MM>);                                                                        \
+        hipLaunchKernelGGL((k_motions_v5<WW, MM>), dim3(grid), dim3(1024), shm5, st, dw, s1, s2, n, can_pass_gate, \
+                           valid, recb5, tileb);                                                                \
+    } while (0)
+#define EPP_LAUNCH_M5W(MM)                                    \
+    switch (w.slab_w) {                                       \
+        case 1: EPP_LAUNCH_M5(1, MM); break;                  \
+        case 2: EPP_LAUNCH_M5(2, MM); break;                  \
+        case 4: EPP_LAUNCH_M5(4, MM); break;                  \
+        case 8: EPP_LAUNCH_M5(8, MM); break;                  \
+        case 16: EPP_LAUNCH_M5(16, MM); break;                \
+        default: EPP_LAUNCH_M5(32, MM); break;                \
+    }
+            if (mode == 0) {
+                EPP_LAUNCH_M5W(0)
+            } else {
+                EPP_LAUNCH_M5W(1)
+            }
+#undef EPP_LAUNCH_M5W
+#undef EPP_LAUNCH_M5
+            return launch_error("epp_check_motions");
+        }
+    }
     const int eb = env_int("EPP_MOTIONS_BLOCK", 0);
     const int block = eb == 512 ? 512 : eb == 1024 ? 1024 : (2u * (front + recb + extra_for(512)) <= 160u * 1024u ? 512 : 1024);
     const uint32_t shm = front + recb + extra_for(block);

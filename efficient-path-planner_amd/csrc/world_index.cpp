@@ -319,7 +319,105 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
     const bool c8 = hdr.size() <= 256;
     const size_t off_c8 = align16(off_ids + flat.size() * 2);
     const size_t off_bm = c8 ? align16(off_c8 + cls.size()) : off_c8;
-    const size_t total = align16(off_bm + cls.size() * 2);
+    // ---- motion tile filter (k_motions_v5) ------------------------------------------
+    // The smallest row width W (words of OBB bits), then the fewest tiles per axis T,
+    // for which every tile holds <= 32 W OBBs; S local slabs per tile and axis as many as
+    // fit kSlabBudget (4..64, a power of two).
+    std::vector<uint32_t> slab;
+    int S = 0, SL = 0, W = 0, T = 0;
+    uint32_t tw = 0;
+    float so[3] = {0, 0, 0}, si[3] = {0, 0, 0};
+    std::vector<int> gsl((size_t)n * 6);  // per OBB: global slab lo / hi per axis
+    auto tile_words = [](int s_, int w_) {
+        return (uint32_t)((6 * s_ * (w_ + 1) + 3 * w_ + 16 * w_ + 3) & ~3);
+    };
+    auto place = [&](int t_, int sl_) {  // slab ranges for (T, S); returns the largest tile population
+        const int s_ = 1 << sl_;
+        for (int k = 0; k < 3; ++k) {
+            const int G = k < 2 ? t_ * s_ : s_;
+            const double ext = std::max(g1[k] - g0[k], 1e-6);
+            si[k] = (float)(G / ext);
+            so[k] = (float)(-g0[k] * (G / ext));
+            for (int i = 0; i < n; ++i) {
+                const double* lo = &hw.aabbs[(size_t)i * 6];
+                gsl[(size_t)i * 6 + k] = slab_axis(lo[k], so[k], si[k], G);
+                gsl[(size_t)i * 6 + 3 + k] = slab_axis(lo[3 + k], so[k], si[k], G);
+            }
+        }
+        std::vector<int> pop((size_t)t_ * t_, 0);
+        for (int i = 0; i < n; ++i) {
+            const int* g = &gsl[(size_t)i * 6];
+            for (int ty = g[1] >> sl_; ty <= g[4] >> sl_; ++ty)
+                for (int tx = g[0] >> sl_; tx <= g[3] >> sl_; ++tx) ++pop[(size_t)ty * t_ + tx];
+        }
+        return *std::max_element(pop.begin(), pop.end());
+    };
+    // first with >= 16 local slabs (the filter's resolution sets how many pairs reach the
+    // exact test), then with >= 4
+    for (int min_sl = 4; n > 0 && !W && min_sl >= 2; min_sl -= 2)
+        for (int w_ = 1; w_ <= kSlabMaxWords && !W; w_ *= 2)
+            for (int t_ = 1; t_ <= 16 && !W; ++t_) {
+                int sl_ = 6;
+                while (sl_ >= min_sl && (size_t)t_ * t_ * tile_words(1 << sl_, w_) * 4 > kSlabBudget) --sl_;
+                if (sl_ < min_sl) break;
+                if (place(t_, sl_) <= 32 * w_) {
+                    W = w_;
+                    T = t_;
+                    SL = sl_;
+                }
+            }
+    if (W) {
+        S = 1 << SL;
+        place(T, SL);
+        tw = tile_words(S, W);
+        const int stride = W + 1;
+        slab.assign((size_t)T * T * tw, 0u);
+        std::vector<int> fill_n((size_t)T * T, 0);
+        for (int i = 0; i < n; ++i) {
+            const int* g = &gsl[(size_t)i * 6];
+            const int tx0 = g[0] >> SL, ty0 = g[1] >> SL;
+            for (int ty = ty0; ty <= g[4] >> SL; ++ty)
+                for (int tx = tx0; tx <= g[3] >> SL; ++tx) {
+                    const size_t t = (size_t)ty * T + tx;
+                    uint32_t* tile = &slab[t * tw];
+                    const int j = fill_n[t]++;
+                    const uint32_t bit = 1u << (j & 31);
+                    const int wd = j >> 5;
+                    // local slab of the OBB's ends (clamped into the tile; z is not tiled)
+                    const int l[3] = {std::min(std::max(g[0] - (tx << SL), 0), S - 1),
+                                      std::min(std::max(g[1] - (ty << SL), 0), S - 1), g[2]};
+                    const int h[3] = {std::min(std::max(g[3] - (tx << SL), 0), S - 1),
+                                      std::min(std::max(g[4] - (ty << SL), 0), S - 1), g[5]};
+                    for (int k = 0; k < 3; ++k) {
+                        tile[((size_t)(2 * k) * S + l[k]) * stride + wd] |= bit;
+                        tile[((size_t)(2 * k + 1) * S + h[k]) * stride + wd] |= bit;
+                    }
+                    uint32_t* tail = tile + (size_t)6 * S * stride;
+                    if (tx == tx0) tail[wd] |= bit;                        // FX
+                    if (ty == ty0) tail[W + wd] |= bit;                    // FY
+                    if (meta[i] & META_FILLING) tail[2 * W + wd] |= bit;   // FILL
+                    reinterpret_cast<uint16_t*>(tail + 3 * W)[j] = (uint16_t)i;
+                }
+        }
+        for (size_t t = 0; t < (size_t)T * T; ++t)
+            for (int k = 0; k < 3; ++k) {  // marks -> prefix ORs: LE up, GE down
+                uint32_t* le = &slab[t * tw + (size_t)(2 * k) * S * stride];
+                uint32_t* ge = &slab[t * tw + (size_t)(2 * k + 1) * S * stride];
+                for (int s_ = 1; s_ < S; ++s_)
+                    for (int w_ = 0; w_ < W; ++w_) le[(size_t)s_ * stride + w_] |= le[(size_t)(s_ - 1) * stride + w_];
+                for (int s_ = S - 2; s_ >= 0; --s_)
+                    for (int w_ = 0; w_ < W; ++w_) ge[(size_t)s_ * stride + w_] |= ge[(size_t)(s_ + 1) * stride + w_];
+            }
+    }
+    v.slab_n = S;
+    v.slab_log = SL;
+    v.slab_w = W;
+    v.tile_n = T;
+    v.tile_words = tw;
+    v.sofx = so[0]; v.sofy = so[1]; v.sofz = so[2];
+    v.six = si[0]; v.siy = si[1]; v.siz = si[2];
+    const size_t off_slab = align16(off_bm + cls.size() * 2);
+    const size_t total = align16(off_slab + slab.size() * 4);
     if (total > 0xFFFFFFFFull) {
         set_error("epp_world: index too large");
         return false;
@@ -337,6 +435,8 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
     v.off_ids = (uint32_t)off_ids;
     v.off_aos = (uint32_t)off_aos;
     std::memcpy(b + off_bm, cls.data(), cls.size() * 2);
+    if (!slab.empty()) std::memcpy(b + off_slab, slab.data(), slab.size() * 4);
+    v.off_slab = (uint32_t)off_slab;
     if (c8)
         for (size_t c = 0; c < cls.size(); ++c) b[off_c8 + c] = (char)(uint8_t)cls[c];
     v.off_cls8 = c8 ? (uint32_t)off_c8 : 0u;

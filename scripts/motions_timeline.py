@@ -1,4 +1,4 @@
-"""Per-wave time split of k_motions_v4 on C3 (512 OBBs, 1M analytic edges): builds a
+"""Per-wave time split of the motion kernels on C3 (512 OBBs, 1M analytic edges): builds a
 diagnostics copy of libepp.so with -DEPP_MOTIONS_TL into scripts/dbg/ (not the product),
 runs the launch, and prints per-wave shader-clock cycles in the candidate walk, in the
 flushes (exact tests) and in total, with the pairs walked / queued per wave."""
@@ -30,7 +30,12 @@ N = 1 << 20
 s1, s2 = synth.edges(43, 8, *synth.C2_BOUNDS, N)
 d1, d2 = capi.DeviceBuffer.from_array(s1), capi.DeviceBuffer.from_array(s2)
 dv = capi.DeviceBuffer(N)
-for mode in (0,):
+kernel = sys.argv[1] if len(sys.argv) > 1 else "v5"
+if kernel == "v4":
+    os.environ["EPP_MOTIONS_KERNEL"] = "v4"
+names = (("walk cycles", "flush cycles", "total cycles", "entries", "queued", "cell pairs") if kernel == "v4" else
+         ("filter+queue", "flush cycles", "total cycles", "prefilter", "pairs", "push"))
+for mode in (0, 1):
     for r in range(20):
         w.check_motions_dev(d1.ptr, d2.ptr, N, 0, mode, dv.ptr)
     capi.sync()
@@ -41,8 +46,8 @@ for mode in (0,):
     live = tl[:, 2] > 0
     tl = tl[live]
     print(f"waves with work: {len(tl)}")
-    for name, k in (("walk cycles", 0), ("flush cycles", 1), ("total cycles", 2), ("entries", 3), ("queued", 4),
-                    ("cell pairs", 5)):
+    print(f"-- {kernel} mode {mode}")
+    for k, name in enumerate(names):
         v = tl[:, k]
         print(f"{name:14s} p10 {np.percentile(v, 10):9.0f} p50 {np.percentile(v, 50):9.0f} p90 {np.percentile(v, 90):9.0f}"
               f" max {v.max():9.0f} mean {v.mean():9.0f}")

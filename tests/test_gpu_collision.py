@@ -140,13 +140,14 @@ def test_compaction(geom, worlds):
     assert np.array_equal(np.sort(idx), np.flatnonzero(exp))
 
 
-@pytest.mark.parametrize("impl", ["lds", "lds/512", "lds/1024", "generic"])
+@pytest.mark.parametrize("impl", ["lds", "v4", "v4/512", "v4/1024", "generic"])
 @pytest.mark.parametrize("name", ["c1", "c2", "c3"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_motions_bit_exact(geom, worlds, name, mode, impl, monkeypatch):
-    """The LDS kernels (k_motions_v4 analytic, k_motions_d32b discrete32) at the default
-    block size and forced 512/1024-thread blocks, and the generic k_motions, vs the
-    oracle; includes edges parallel to an axis within the 1e-6 threshold."""
+    """The default slab-filter kernel (k_motions_v5, both modes), the cell-list kernels
+    (k_motions_v4 analytic, k_motions_d32b discrete32) at the default block size and forced
+    512/1024-thread blocks, and the generic k_motions, vs the oracle; includes edges
+    parallel to an axis within the 1e-6 threshold."""
     impl, _, block = impl.partition("/")
     monkeypatch.setenv("EPP_MOTIONS_KERNEL", impl)
     monkeypatch.setenv("EPP_MOTIONS_BLOCK", block)  # "" = by LDS fit (the default)
@@ -171,10 +172,11 @@ def test_motions_bit_exact(geom, worlds, name, mode, impl, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("impl", ["lds", "generic"])
+@pytest.mark.parametrize("impl", ["lds", "v4", "generic"])
 def test_motions_queue_overflow(geom, worlds, impl, mode, monkeypatch):
-    """Long edges through the 512-OBB world: both LDS kernels flush their wave queues many
-    times per wave.  Answers still match the oracle."""
+    """Long edges through the 512-OBB world: the LDS kernels flush their wave queues many
+    times per wave (k_motions_v5: several queue windows per wave).  Answers still match
+    the oracle."""
     monkeypatch.setenv("EPP_MOTIONS_KERNEL", impl)
     rg, ro, ws = worlds
     gates, obstacles, (lo, hi) = ws["c3"]
@@ -184,6 +186,30 @@ def test_motions_queue_overflow(geom, worlds, impl, mode, monkeypatch):
     for cp in (0, 1):
         got = w.check_motions(s1, s2, cp, mode)
         exp = O.check_motions(ref, rg, ro, s1, s2, cp, mode, threads=8)
+        assert np.array_equal(got, exp), (cp, np.flatnonzero(got != exp)[:10])
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_motions_outside_and_across(geom, worlds, mode):
+    """Edges beyond the world's box on every side (slab indices clamp to the end slabs),
+    edges across the whole world, zero-length edges and edges touching AABB faces, through
+    the default kernel vs the oracle."""
+    rg, ro, ws = worlds
+    gates, obstacles, (lo, hi) = ws["c3"]
+    ref = O.world_build(geom, gates, obstacles, rg, ro)
+    w = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
+    rs = np.random.RandomState(17)
+    lo, hi = np.asarray(lo, float), np.asarray(hi, float)
+    far = rs.uniform(lo - 20, hi + 20, size=(20_000, 3))
+    across = np.stack([rs.uniform(lo, hi, size=(5000, 3)), rs.uniform(lo, hi, size=(5000, 3))])
+    bl, bh = ref["aabb_lo"], ref["aabb_hi"]
+    face = np.where(rs.rand(5000, 1) < 0.5, bl[rs.randint(0, len(ref), 5000)], bh[rs.randint(0, len(ref), 5000)])
+    s1 = np.vstack([far[:10_000], across[0], face, face])
+    s2 = np.vstack([far[10_000:], across[1], face + rs.normal(size=(5000, 3)) * 0.2, face])
+    for cp in (0, 1):
+        got = w.check_motions(s1, s2, cp, mode)
+        exp = O.check_motions(ref, rg, ro, s1, s2, cp, mode, threads=8)
+        assert exp.min() == 0 and exp.max() == 1
         assert np.array_equal(got, exp), (cp, np.flatnonzero(got != exp)[:10])
 
 
@@ -311,7 +337,7 @@ def test_filling_states_bit_exact(fworlds, name, kernel, monkeypatch):
         assert np.array_equal(w.check_states_mindist(pts, md), O.check_states_mindist(ref, pts, md)), md
 
 
-@pytest.mark.parametrize("kernel", ["lds", "generic"])
+@pytest.mark.parametrize("kernel", ["lds", "v4", "generic"])
 @pytest.mark.parametrize("name", ["c1", "c2", "c3"])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_filling_motions_bit_exact(fworlds, name, mode, kernel, monkeypatch):
