@@ -21,6 +21,22 @@
 namespace epp {
 const WorldView& world_view(const epp_world* w);
 const WorldView* world_dview(const epp_world* w);
+epp_status ensure_index(const epp_world* w);  // rebuild + upload a stale index (world_index.cpp)
+SmallWorld small_world(const epp_world* w);
+
+// small.hip: brute-force kernels for small queries (no index needed)
+constexpr int64_t kSmallStates = 4096;   // states per call
+constexpr int64_t kSmallMotions = 1024;  // edges per call
+constexpr int kSmallMaxObbs = 256;       // OBBs (records staged in LDS: 34 KB)
+bool small_states(const SmallWorld& sw, int64_t n);
+bool small_motions(const SmallWorld& sw, int64_t n);
+// done != NULL: each workgroup publishes seq in done[blockIdx.x] when its flags are visible
+epp_status launch_states_small(const SmallWorld& sw, bool mindist, const double* xyz, int64_t n, int32_t can_pass,
+                               double md, uint8_t* valid, int32_t* compact_idx, int64_t* n_valid, hipStream_t st,
+                               uint32_t* done = nullptr, uint32_t seq = 0);
+epp_status launch_motions_small(const SmallWorld& sw, int32_t mode, const double* s1, const double* s2, int64_t n,
+                                int32_t can_pass, uint8_t* valid, hipStream_t st, uint32_t* done = nullptr,
+                                uint32_t seq = 0);
 
 namespace {
 
@@ -367,6 +383,65 @@ __device__ __forceinline__ bool rec_hit(const double* rec, double rg, double ro,
     const double ix = f[F_HX] + r, iy = f[F_HY] + r, iz = f[F_HZ] + r;  // shouldBeInflated()
     const double tx = fill ? f[F_HX] : ix, ty = fill ? f[F_HY] : iy, tz = fill ? f[F_HZ] : iz;
     return in & !skip & (fabs(lx) <= tx) & (fabs(ly) <= ty) & (fabs(dz) <= tz);
+}
+
+// The 32-step discretised motion check against ONE OBB record: does some point
+// s + (e - s) k/32, k = 1..32, lie strictly inside the OBB's AABB (rtree contains,
+// src/World.cpp:83) and collide with it (OBB::checkCollisionWithPoint, src/OBB.cpp:63-91;
+// filling boxes skipped with can_pass, :92-95)?  Every one of those tests is |a + b t| <= h
+// (or lo < a + b t < hi) along the edge, so the t that can hit lie in an interval; it is
+// computed with a slack eta (1e-6 m + 1e-12 of the coordinates' magnitude) far above the
+// rounding of the points and of the interval itself, and only the k inside it are tested
+// exactly (the reference's point evaluation), in order, until one hits.
+__device__ __forceinline__ bool d32_pair_hit(const double* rec, const double ps[3], const double pe[3], double rg,
+                                             double ro, bool cp) {
+    double rr[kRecDoubles];  // the record in registers
+#pragma unroll
+    for (int k = 0; k <= F_HZ; ++k) rr[k] = rec[k];
+    rr[R_META] = rec[R_META];
+    const uint32_t m = (uint32_t)__double_as_longlong(rr[R_META]);
+    const bool fillb = (m & META_FILLING) != 0u;
+    const double r = (m & META_GATE) ? rg : ro;
+    const double d[3] = {pe[0] - ps[0], pe[1] - ps[1], pe[2] - ps[2]};
+    const double mag = fmax(fmax(fmax(fabs(ps[0]), fabs(ps[1])), fmax(fabs(ps[2]), fabs(pe[0]))),
+                            fmax(fmax(fabs(pe[1]), fabs(pe[2])), fmax(fmax(fabs(rr[F_CX]), fabs(rr[F_CY])), fabs(rr[F_CZ]))));
+    const double eta = 1e-6 + 1e-12 * mag;
+    double t0 = 0.0, t1 = 1.0;
+    // lo - eta <= a + b t <= hi + eta
+    auto clip = [&](double a, double b, double lo, double hi) {
+        const double u0 = lo - eta - a, u1 = hi + eta - a;
+        if (b == 0.0) {
+            if (!(u0 <= 0.0 && 0.0 <= u1)) t1 = -1.0;
+        } else {
+            const double v0 = u0 / b, v1 = u1 / b;
+            t0 = fmax(t0, fmin(v0, v1));
+            t1 = fmin(t1, fmax(v0, v1));
+        }
+    };
+    clip(ps[0], d[0], rr[F_LOX], rr[F_HIX]);  // rtree contains (strict)
+    clip(ps[1], d[1], rr[F_LOY], rr[F_HIY]);
+    clip(ps[2], d[2], rr[F_LOZ], rr[F_HIZ]);
+    const double c = rr[F_COS], sn = rr[F_SIN];  // the OBB frame
+    const double ax = ps[0] - rr[F_CX], ay = ps[1] - rr[F_CY];
+    const double tx = fillb ? rr[F_HX] : rr[F_HX] + r, ty = fillb ? rr[F_HY] : rr[F_HY] + r,
+                 tz = fillb ? rr[F_HZ] : rr[F_HZ] + r;
+    clip(c * ax + sn * ay, c * d[0] + sn * d[1], -tx, tx);
+    clip(c * ay - sn * ax, c * d[1] - sn * d[0], -ty, ty);
+    clip(ps[2] - rr[F_CZ], d[2], -tz, tz);
+    int k0 = 33, k1 = 0;
+    if (t0 <= t1) {  // (NaN bounds: fmax/fmin drop them -> the whole edge)
+        k0 = max(1, (int)ceil(32.0 * t0));
+        k1 = min(32, (int)floor(32.0 * t1));
+    }
+    bool hit = false;
+    for (int k = k0; k <= k1 && !hit; ++k) {
+        const double t = (double)k / 32.0;
+        const double qx = ps[0] + (pe[0] - ps[0]) * t;
+        const double qy = ps[1] + (pe[1] - ps[1]) * t;
+        const double qz = ps[2] + (pe[2] - ps[2]) * t;
+        hit = rec_hit<false>(rr, rg, ro, qx, qy, qz, cp, 0.0);
+    }
+    return hit;
 }
 
 // Exact test on the AoS records + the cell's candidate list (no early exit: the lists

@@ -35,6 +35,7 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -142,8 +143,16 @@ inline int bm_axis(double p, float off, float inv) {
 }
 
 // Host-side world: the upload plus host copies (for AABB introspection and rebuilds).
+// epp_world_update only rebuilds the OBB records (into pinned host memory, which the
+// small-query kernels read directly) and marks the device index stale; the index is
+// rebuilt and uploaded by the first call that needs it (ensure_index).
 struct HostWorld {
     WorldView view{};
+    std::vector<epp_obb> obbs;          // the OBBs of the current version
+    double* h_recs = nullptr;           // pinned: n x kRecDoubles records of the current version
+    size_t h_recs_cap = 0;
+    bool index_stale = false;           // the device blob is an older version
+    std::mutex mu;                      // guards the lazy index rebuild
     double r_gate = 0, r_obst = 0;
     int device = 0;
     void* d_blob = nullptr;
@@ -180,5 +189,13 @@ inline int fine_index(float f, int n) {
 }
 
 void set_error(const std::string& msg);
+
+// The OBB records of a world for the small-query kernels (brute force over every OBB):
+// the device blob's when the index is current, else the pinned host copy (zero-copy).
+struct SmallWorld {
+    const double* recs;
+    int32_t n_obb;
+    double r_gate, r_obst;
+};
 
 }  // namespace epp

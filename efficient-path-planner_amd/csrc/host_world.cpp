@@ -7,6 +7,7 @@
 
 #include "epp/World.h"
 #include "host_scratch.h"
+#include "small_sync.h"
 
 namespace epp {
 
@@ -123,15 +124,27 @@ namespace {
 constexpr int64_t kZeroCopyMax = 16384;  // queries per call read straight from host memory
 }
 
+// (the small-query lambdas run the synchronous brute-force path of small.hip when the
+// query qualifies and report whether they did)
 void World::checkPoints(const double* xyz, int64_t n, bool canPassGate, uint8_t* out) const {
     query(n, 1, [&](const double* const* in, uint8_t* flags, void* st) {
         check(epp_check_states(device(), in[0], n, canPassGate ? 1 : 0, flags, nullptr, nullptr, st), "checkPoints");
+    }, [&](const double* const* in, uint8_t* flags, void* st) {
+        bool handled = false;
+        check(states_small_sync(device(), false, in[0], n, canPassGate ? 1 : 0, 0.0, flags, (hipStream_t)st, &handled),
+              "checkPoints");
+        return handled;
     }, &xyz, out);
 }
 
 void World::checkPointsMinDistance(const double* xyz, int64_t n, double minDistance, uint8_t* out) const {
     query(n, 1, [&](const double* const* in, uint8_t* flags, void* st) {
         check(epp_check_states_mindist(device(), in[0], n, minDistance, flags, st), "checkPointsMinDistance");
+    }, [&](const double* const* in, uint8_t* flags, void* st) {
+        bool handled = false;
+        check(states_small_sync(device(), true, in[0], n, 0, minDistance, flags, (hipStream_t)st, &handled),
+              "checkPointsMinDistance");
+        return handled;
     }, &xyz, out);
 }
 
@@ -140,11 +153,16 @@ void World::checkRays(const double* s1, const double* s2, int64_t n, bool canPas
     const double* in[2] = {s1, s2};
     query(n, 2, [&](const double* const* d, uint8_t* flags, void* st) {
         check(epp_check_motions(device(), d[0], d[1], n, canPassGate ? 1 : 0, mode, flags, st), "checkRays");
+    }, [&](const double* const* d, uint8_t* flags, void* st) {
+        bool handled = false;
+        check(motions_small_sync(device(), mode, d[0], d[1], n, canPassGate ? 1 : 0, flags, (hipStream_t)st, &handled),
+              "checkRays");
+        return handled;
     }, in, out);
 }
 
-template <typename Launch>
-void World::query(int64_t n, int n_in, Launch&& launch, const double* const* in, uint8_t* out) const {
+template <typename Launch, typename Small>
+void World::query(int64_t n, int n_in, Launch&& launch, Small&& small, const double* const* in, uint8_t* out) const {
     if (n <= 0) return;
     (void)device();  // upload a changed world before the launch (not inside it)
     ThreadScratch& ts = ThreadScratch::get();
@@ -158,8 +176,10 @@ void World::query(int64_t n, int n_in, Launch&& launch, const double* const* in,
             d_in[k] = reinterpret_cast<const double*>(h + k * ThreadScratch::rounded(in_b));
         }
         uint8_t* flags = reinterpret_cast<uint8_t*>(h + n_in * ThreadScratch::rounded(in_b));
-        launch(d_in, flags, st);
-        check(epp_stream_sync(st), "query");
+        if (!small(d_in, flags, st)) {
+            launch(d_in, flags, st);
+            check(epp_stream_sync(st), "query");
+        }
         std::memcpy(out, flags, (size_t)n);
         return;
     }

@@ -20,6 +20,7 @@
 // one lane runs the sequential `acc += dt` / segment roll-over recurrence (so sample
 // times and counts are bit-identical), and the wavefront evaluates the rows.
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <cmath>
@@ -63,14 +64,9 @@ __host__ __device__ __forceinline__ double nfabian(const double* p, const double
     return distance / vmax * 2 * (1.0 + 6.5 * vmax / amax * exp(-distance / vmax * 2));
 }
 
-// Reciprocal and reciprocal square root: the hardware estimates (v_rcp_f64, v_rsq_f64:
-// ~5e-8 relative error, measured) refined by two Newton steps to ~1e-16, in 6 dependent
-// instructions instead of the ~10-20 of an IEEE division / square root.
-__device__ __forceinline__ double rcp_nr(double x) {
-    double y = __builtin_amdgcn_rcp(x);
-    y = fma(y, fma(-x, y, 1.0), y);
-    return fma(y, fma(-x, y, 1.0), y);
-}
+// Reciprocal square root: the hardware estimate (v_rsq_f64: ~5e-8 relative error,
+// measured) refined by two Newton steps to ~1e-16, in 6 dependent instructions instead of
+// the ~10-20 of an IEEE square root and division.
 __device__ __forceinline__ double rsq_nr(double x) {
     double y = __builtin_amdgcn_rsq(x);
     y = fma(0.5 * y, fma(-(x * y), y, 1.0), y);
@@ -80,103 +76,26 @@ __device__ __forceinline__ double rsq_nr(double x) {
 // 1 / r! for r = 0..4 (the same roundings as dividing at run time)
 __device__ constexpr double kInvFact[HALF] = {1.0, 1.0, 1.0 / 2.0, 1.0 / 6.0, 1.0 / 24.0};
 
-// setupMappingMatrix + invertMappingMatrix (Schur complement), one lane per segment.
-__device__ void invert_mapping(double T, double* Ai /* 10x10 row-major */) {
-    // A rows 5+k = baseCoeffsWithTime(N, k, T): [k] = B[k][k], [j>k] = B[k][j] * T^(j-k)
-    // with the power built by repeated multiplication (polynomial.h:213-218).
-    double C[HALF][HALF], D[HALF][HALF];
-#pragma unroll
-    for (int k = 0; k < HALF; ++k) {
-        double row[N];
-#pragma unroll
-        for (int j = 0; j < N; ++j) row[j] = 0.0;
-        row[k] = cB[k][k];
-        if (fabs(T) >= 2.220446049250313e-16) {
-            double tp = T;
-#pragma unroll
-            for (int j = k + 1; j < N; ++j) {
-                row[j] = cB[k][j] * tp;
-                tp = tp * T;
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < HALF; ++j) {
-            C[k][j] = row[j];
-            D[k][j] = row[j + HALF];
-        }
-    }
-    // D^-1 by LU with partial pivoting (Eigen's 5x5 inverse path).  Every loop is fully
-    // unrolled and the row swap is a select, so all indices are static and the arrays
-    // stay in registers (a data-dependent row index would put them in scratch memory).
-    int perm[HALF];
-    double piv_inv[HALF];
-#pragma unroll
-    for (int i = 0; i < HALF; ++i) perm[i] = i;
-#pragma unroll
-    for (int k = 0; k < HALF; ++k) {
-        int p = k;
-        double best = fabs(D[k][k]);
-#pragma unroll
-        for (int r = k + 1; r < HALF; ++r)
-            if (fabs(D[r][k]) > best) {
-                best = fabs(D[r][k]);
-                p = r;
-            }
-#pragma unroll
-        for (int r = k + 1; r < HALF; ++r) {
-            const bool sw = (r == p);
-#pragma unroll
-            for (int c = 0; c < HALF; ++c) {
-                const double t = D[k][c];
-                D[k][c] = sw ? D[r][c] : t;
-                D[r][c] = sw ? t : D[r][c];
-            }
-            const int t = perm[k];
-            perm[k] = sw ? perm[r] : t;
-            perm[r] = sw ? t : perm[r];
-        }
-        // one reciprocal per pivot instead of a division per entry (a division is a
-        // ~10-instruction dependent sequence on CDNA): results within an ulp or two
-        const double ip = rcp_nr(D[k][k]);
-        piv_inv[k] = ip;
-#pragma unroll
-        for (int r = k + 1; r < HALF; ++r) {
-            D[r][k] = D[r][k] * ip;
-#pragma unroll
-            for (int c = k + 1; c < HALF; ++c) D[r][c] = D[r][c] - D[r][k] * D[k][c];
-        }
-    }
-    double Dinv[HALF][HALF];
-#pragma unroll
-    for (int col = 0; col < HALF; ++col) {
-        double x[HALF];
-#pragma unroll
-        for (int i = 0; i < HALF; ++i) x[i] = (perm[i] == col) ? 1.0 : 0.0;
-#pragma unroll
-        for (int i = 0; i < HALF; ++i)
-#pragma unroll
-            for (int j = 0; j < i; ++j) x[i] = x[i] - D[i][j] * x[j];
-#pragma unroll
-        for (int i = HALF - 1; i >= 0; --i) {
-#pragma unroll
-            for (int j = i + 1; j < HALF; ++j) x[i] = x[i] - D[i][j] * x[j];
-            x[i] = x[i] * piv_inv[i];
-        }
-#pragma unroll
-        for (int i = 0; i < HALF; ++i) Dinv[i][col] = x[i];
-    }
-    for (int i = 0; i < N * N; ++i) Ai[i] = 0.0;
-    for (int r = 0; r < HALF; ++r) {
-        const double adinv = kInvFact[r];  // A_diag.cwiseInverse(): 1 / B[r][r] = 1 / r!
-        Ai[r * N + r] = adinv;
-        for (int c = 0; c < HALF; ++c) Ai[(r + HALF) * N + c + HALF] = Dinv[r][c];
-    }
-    for (int r = 0; r < HALF; ++r)
-        for (int c = 0; c < HALF; ++c) {
-            double s = 0.0;
-            for (int k = 0; k < HALF; ++k) s = s + Dinv[r][k] * C[k][c];
-            Ai[(r + HALF) * N + c] = -s * kInvFact[c];  // -D^-1 C A_diag^-1
-        }
+// setupMappingMatrix + invertMappingMatrix (impl :111-121, :142-179) in closed form.  The
+// mapping matrix is A = [[diag(k!), 0], [C, D]] with C[k][j] = B[k][j] T^(j-k) and
+// D[k][j] = B[k][j+5] T^(j+5-k), i.e. D = diag(T^-k) B5 diag(T^(j+5)) for the constant
+// B5[k][j] = B[k][j+5].  So
+//   A^-1 = [[diag(1/k!), 0], [-D^-1 C diag(1/k!), D^-1]],
+//   D^-1[r][c] = B5^-1[r][c] T^(c-r-5),   (-D^-1 C diag(1/k!))[r][c] = K[r][c] T^(c-r-5)
+// with constant B5^-1 and K[r][c] = -sum_{k<=c} B5^-1[r][k] B[k][c] / c!: every entry is
+// a constant times a power of 1/T, so the 100 entries are independent (one thread each)
+// instead of a 5x5 LU per segment on one lane.  The reference's LU with partial pivoting
+// gives the same matrix to rounding (the parity target of the solve is 1e-6).
+__constant__ double cB5inv[HALF][HALF];
+__constant__ double cK[HALF][HALF];
+
+__device__ __forceinline__ double ainv_entry(double invT, int r, int c) {
+    if (r < HALF) return r == c ? kInvFact[r] : 0.0;
+    const int rr = r - HALF;
+    const int ex = (c < HALF ? c : c - HALF) - rr - HALF;  // in [-9, -1]
+    double p = invT;
+    for (int k = 1; k < -ex; ++k) p = p * invT;
+    return (c < HALF ? cK[rr][c] : cB5inv[rr][c - HALF]) * p;
 }
 
 // Per-segment scratch (doubles): A^-1 (10x10), H (10x10), the 6x6 snap block Q of Q_i,
@@ -210,8 +129,22 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ P, int M, 
         Tm[i] = T;
         if (T_out) T_out[i] = T;
         if (!(T > 0)) atomicOr(s_err, 1);  // CHECK_GT(segment_time, 0)  impl :297
-        else invert_mapping(T, scr + (size_t)i * Seg::kSize + Seg::kAinv);
     }
+    __syncthreads();
+    for (int e = tid; e < M * N * N; e += BLOCK) {
+        const int i = e / (N * N), r = (e % (N * N)) / N, c = e % N;
+        // 1/T: the hardware reciprocal refined by two Newton steps (~1e-16; a division
+        // per entry would cost ~10 dependent instructions)
+        const double T = Tm[i];
+        double it = __builtin_amdgcn_rcp(T);
+        it = fma(it, fma(-T, it, 1.0), it);
+        it = fma(it, fma(-T, it, 1.0), it);
+        scr[(size_t)i * Seg::kSize + Seg::kAinv + r * N + c] = ainv_entry(it, r, c);
+    }
+#ifdef EPP_REFIT_TL
+    __syncthreads();
+    EPP_TL(9);
+#endif
     // start vertex {p0, v0, a0, 0, 0}, inner {p}, end {p, 0, 0, 0, 0}: makeStartOrEnd
     // (src/vertex.cpp:146-170) and trajectory_generator.cpp:28-50
     for (int e = tid; e < (M + 1) * 15; e += BLOCK) {
@@ -666,91 +599,151 @@ __global__ __launch_bounds__(kWave) void k_sample_rows(const double* __restrict_
 }
 
 // ---- single-track fused refit (the 50 Hz latency path) --------------------------------
-// poly_traj::generateTrajectory for one track in ONE launch of one workgroup, reading its
-// inputs from and writing the rows to pinned host memory (no copies).  The host has
-// already run the two sequential parts, which a GPU lane runs slowly (~65 ns per dependent
-// step): the segment times (Nfabian with the host's libm, as the reference) and
-// Trajectory::evaluateRange's `acc += dt` recurrence (sample times and segments, exact).
-// The workgroup solves the min-snap problem with those times (solve_track) and
-// evaluates the rows (Polynomial::evaluate).
+// poly_traj::generateTrajectory for one track in ONE launch, reading its inputs from and
+// writing the rows to pinned host memory (no copies).  The host has already run the two
+// sequential parts, which a GPU lane runs slowly (~65 ns per dependent step): the segment
+// times (Nfabian with the host's libm, as the reference) and Trajectory::evaluateRange's
+// `acc += dt` recurrence (sample times and segments, exact).
+//   workgroup 0        solves the min-snap problem with those times (solve_track) and
+//                      publishes the coefficients (device memory) and its status;
+//   workgroups 1..G    each own a slice of the rows: they fetch its sample data from the
+//                      host while workgroup 0 solves, wait for the coefficients, evaluate
+//                      the rows (Polynomial::evaluate) and write them to the host — G CUs
+//                      writing in parallel instead of one (one CU's PCIe writes are slow).
+// Completion is published in host memory (workgroup 0: the status; writers: their slot)
+// and polled by the host instead of synchronising the stream.
 constexpr int kRefitArgW = 41;  // tracks up to this many waypoints pass wp, v0, a0, T as kernel arguments
+constexpr int kRefitMaxWriters = 16;
 struct RefitArgs {
     const double* in;  // host-mapped: [wp (W x 3) | v0 (3) | a0 (3) | T (M)] | t_in (R) | t (R) | segment (R, int32)
     int32_t W;
     int32_t R;         // rows
-    int32_t rows_lds;  // 1: stage the sample data in LDS with the inputs
+    int32_t writers;   // G
+    uint32_t seq;      // this call's number (completion words hold it)
     double t0;         // startTimeOffset
     double* out;       // host-mapped: R x 10 rows
     int64_t* info;     // host-mapped: [status]
+    uint32_t* done;    // host-mapped: the writers' completion slots
+    double* coef;      // device: M x 30 coefficients (workgroup 0 -> writers)
+    uint32_t* flag;    // device: [seq of the published coefficients, status]
     double* scratch;   // device: segment scratch (tracks longer than kMaxLdsSeg)
     double small[3 * kRefitArgW + 6 + kRefitArgW - 1];  // wp | v0 | a0 | T when W <= kRefitArgW
 };
 constexpr int kRefitBlock = 256;
+constexpr int kRefitRowChunk = 128;  // rows per writer round (LDS staged)
 __host__ __device__ inline size_t refit_in_doubles(int W, int R) {
     return (size_t)3 * W + 6 + (W - 1) + 2 * (size_t)R + ((size_t)R + 1) / 2;
 }
-// LDS doubles: flag (2) | wp, v0, a0, T | solve scratch | coefficients | [sample data]
-__host__ __device__ inline size_t refit_lds_doubles(int M, bool lds, int rows_in_lds) {
-    return 2 + (((size_t)3 * (M + 1) + 6 + M + 1) & ~size_t(1)) + (lds ? (size_t)M * Seg::kSize : 0) +
-           vertex_doubles(M) + (size_t)M * 30 + (size_t)rows_in_lds * 2 + ((size_t)rows_in_lds + 1) / 2;
+// LDS doubles of the solver: flag (2) | wp, v0, a0, T | solve scratch | coefficients; of a
+// writer: coefficients | sample chunk (t_in, t, segment) | row chunk
+__host__ __device__ inline size_t refit_lds_doubles(int M, bool lds) {
+    const size_t solver = 2 + (((size_t)3 * (M + 1) + 6 + M + 1) & ~size_t(1)) + (lds ? (size_t)M * Seg::kSize : 0) +
+                          vertex_doubles(M) + (size_t)M * 30;
+    const size_t writer = (size_t)M * 30 + 2 + (size_t)kRefitRowChunk * 3 + (size_t)kRefitRowChunk * 10;
+    return solver > writer ? solver : writer;
 }
 
 template <bool LDS>
 __global__ __launch_bounds__(kRefitBlock) void k_refit(RefitArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    int* s_err = reinterpret_cast<int*>(smem);
     const int tid = threadIdx.x, W = a.W, M = W - 1, R = a.R;
-    EPP_TL(0);
     const double* h_tin = a.in + 3 * W + 6 + M;
     const double* h_tac = h_tin + R;
     const int32_t* h_seg = reinterpret_cast<const int32_t*>(h_tac + R);
-    double* P = smem + 2;  // wp | v0 | a0 | T
-    const int nin = 3 * W + 6 + M;
-    const double* src = W <= kRefitArgW ? a.small : a.in;  // kernel arguments or host memory
-    for (int e = tid; e < nin; e += kRefitBlock) P[e] = src[e];
-    if (tid == 0) *s_err = 0;
-    double* rest = smem + 2 + (((size_t)nin + 1) & ~size_t(1));
-    double* scr = LDS ? rest : a.scratch;
-    double* dv = LDS ? rest + (size_t)M * Seg::kSize : rest;
-    double* rhs = dv + (size_t)(M + 1) * 15;
-    double* Tm = rhs + (size_t)(M + 1) * 12;
-    double* C = Tm + M;  // coefficients (M x 3 x 10)
-    // the sample data: one round of host reads now (in LDS) instead of after the solve
-    double* s_tin = C + (size_t)M * 30;
-    double* s_tac = s_tin + R;
-    int32_t* s_seg = reinterpret_cast<int32_t*>(s_tac + R);
-    if (a.rows_lds) {
-        for (int e = tid; e < R; e += kRefitBlock) {
-            s_tin[e] = h_tin[e];
-            s_tac[e] = h_tac[e];
-            s_seg[e] = h_seg[e];
+    if (blockIdx.x == 0) {  // ---- the solver ----
+        int* s_err = reinterpret_cast<int*>(smem);
+        EPP_TL(0);
+        double* P = smem + 2;  // wp | v0 | a0 | T
+        const int nin = 3 * W + 6 + M;
+        const double* src = W <= kRefitArgW ? a.small : a.in;  // kernel arguments or host memory
+        for (int e = tid; e < nin; e += kRefitBlock) P[e] = src[e];
+        if (tid == 0) *s_err = 0;
+        double* rest = smem + 2 + (((size_t)nin + 1) & ~size_t(1));
+        double* scr = LDS ? rest : a.scratch;
+        double* dv = LDS ? rest + (size_t)M * Seg::kSize : rest;
+        double* rhs = dv + (size_t)(M + 1) * 15;
+        double* Tm = rhs + (size_t)(M + 1) * 12;
+        double* C = Tm + M;  // coefficients (M x 3 x 10)
+        __syncthreads();
+        const int st = solve_track<kRefitBlock>(P, M, 0.0, 0.0, P + 3 * W, P + 3 * W + 3, P + 3 * W + 6, scr, dv,
+                                                rhs, Tm, s_err, nullptr, C);
+        EPP_TL(7);
+        __syncthreads();  // coefficients complete
+        for (int e = tid; e < M * 30; e += kRefitBlock) a.coef[e] = C[e];
+        __threadfence();  // (every storing wave) -> the barrier -> the release below
+        __syncthreads();
+        if (tid == 0) {
+            a.flag[1] = (uint32_t)st;
+            __hip_atomic_store(a.flag, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.info, (int64_t)st, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+        EPP_TL(11);
+        return;
+    }
+    // ---- a row writer: rows [r0, r1) ----
+    const int g = blockIdx.x - 1;
+    const int per = (R + a.writers - 1) / a.writers;
+    const int r0 = min(R, g * per), r1 = min(R, r0 + per);
+    double* C = smem;
+    double* s_tin = C + (size_t)M * 30 + 2;
+    double* s_tac = s_tin + kRefitRowChunk;
+    int32_t* s_seg = reinterpret_cast<int32_t*>(s_tac + kRefitRowChunk);
+    double* rbuf = reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(s_tac + 2 * kRefitRowChunk) + 15) &
+                                             ~uintptr_t(15));
+    auto fetch = [&](int c0, int cnt) {  // sample data of rows [c0, c0 + cnt) (host reads)
+        if (tid < cnt) {
+            s_tin[tid] = h_tin[c0 + tid];
+            s_tac[tid] = h_tac[c0 + tid];
+            s_seg[tid] = h_seg[c0 + tid];
+        }
+    };
+    fetch(r0, min(kRefitRowChunk, r1 - r0));  // in flight while workgroup 0 solves
+    __shared__ uint32_t s_status;
+    if (tid == 0) {
+        // wait for workgroup 0's coefficients (bounded: ~0.5 s, then give up as failed)
+        uint32_t st = 1u;
+        for (uint32_t it = 0; it < (1u << 22); ++it) {
+            if (__hip_atomic_load(a.flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == a.seq) {
+                st = __hip_atomic_load(a.flag + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        s_status = st;
     }
     __syncthreads();
-    const int st = solve_track<kRefitBlock>(P, M, 0.0, 0.0, P + 3 * W, P + 3 * W + 3, P + 3 * W + 6, scr, dv, rhs, Tm,
-                                            s_err, nullptr, C);
-    EPP_TL(7);
-    if (st == 0) {
-        __syncthreads();  // coefficients complete
-        auto row = [&](int j, double tin, double tac, int seg) {
-            const double* cs = C + (size_t)seg * 30;
-            double r[10];
+    EPP_TL(12);
+    if (s_status == 0) {
+        for (int e = tid; e < M * 30; e += kRefitBlock) C[e] = a.coef[e];
+        for (int c0 = r0; c0 < r1; c0 += kRefitRowChunk) {
+            const int cnt = min(kRefitRowChunk, r1 - c0);
+            if (c0 != r0) {
+                __syncthreads();  // the previous chunk copied out
+                fetch(c0, cnt);
+            }
+            __syncthreads();
+            if (tid < cnt) {
+                const double* cs = C + (size_t)s_seg[tid] * 30;
+                const double tin = s_tin[tid];
+                double* r = rbuf + (size_t)tid * 10;
 #pragma unroll
-            for (int d = 0; d < 3; ++d)
+                for (int d = 0; d < 3; ++d)
 #pragma unroll
-                for (int q = 0; q < 3; ++q) r[3 * d + q] = poly_eval(cs + d * N, tin, q);
-            r[9] = tac + a.t0;  // sampling_times[i] + startTimeOffset
-            double2* o = reinterpret_cast<double2*>(a.out + (size_t)j * 10);
-#pragma unroll
-            for (int q = 0; q < 5; ++q) o[q] = make_double2(r[2 * q], r[2 * q + 1]);
-        };
-        if (a.rows_lds)
-            for (int j = tid; j < R; j += kRefitBlock) row(j, s_tin[j], s_tac[j], s_seg[j]);
-        else
-            for (int j = tid; j < R; j += kRefitBlock) row(j, h_tin[j], h_tac[j], h_seg[j]);
+                    for (int q = 0; q < 3; ++q) r[3 * d + q] = poly_eval(cs + d * N, tin, q);
+                r[9] = s_tac[tid] + a.t0;  // sampling_times[i] + startTimeOffset
+            }
+            __syncthreads();
+            // contiguous 16-byte stores: a wave writes 1 KB runs
+            const double2* src2 = reinterpret_cast<const double2*>(rbuf);
+            double2* dst2 = reinterpret_cast<double2*>(a.out + (size_t)c0 * 10);
+            for (int q = tid; q < cnt * 5; q += kRefitBlock) dst2[q] = src2[q];
+        }
     }
-    EPP_TL(11);
-    if (tid == 0) a.info[0] = st;
+    EPP_TL(13);
+    // completion: this slice's rows are visible system-wide before the slot is
+    __threadfence_system();
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(a.done + g, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 bool g_consts_ready[64];
@@ -768,7 +761,39 @@ epp_status ensure_consts() {
         for (int i = N - 1 - order; i < N; ++i) B[n][i] = (order - (N - 1) + i) * B[n - 1][i];
         order--;
     }
+    // B5 = B[k][j+5] (5x5), inverted by Gauss-Jordan in long double; K from it (closed-form
+    // mapping inverse, ainv_entry)
+    long double G[HALF][2 * HALF];
+    for (int k = 0; k < HALF; ++k)
+        for (int j = 0; j < 2 * HALF; ++j) G[k][j] = j < HALF ? (long double)B[k][j + HALF] : (j - HALF == k ? 1.0L : 0.0L);
+    for (int col = 0; col < HALF; ++col) {
+        int p = col;
+        for (int r = col + 1; r < HALF; ++r)
+            if (std::fabs((double)G[r][col]) > std::fabs((double)G[p][col])) p = r;
+        for (int j = 0; j < 2 * HALF; ++j) std::swap(G[col][j], G[p][j]);
+        const long double piv = G[col][col];
+        for (int j = 0; j < 2 * HALF; ++j) G[col][j] /= piv;
+        for (int r = 0; r < HALF; ++r)
+            if (r != col) {
+                const long double f = G[r][col];
+                for (int j = 0; j < 2 * HALF; ++j) G[r][j] -= f * G[col][j];
+            }
+    }
+    double B5inv[HALF][HALF], K[HALF][HALF];
+    long double fact = 1.0L;
+    for (int c = 0; c < HALF; ++c) {
+        if (c > 0) fact *= c;
+        for (int r = 0; r < HALF; ++r) {
+            long double s = 0.0L;
+            for (int k = 0; k <= c; ++k) s += G[r][HALF + k] * (long double)B[k][c];
+            K[r][c] = (double)(-s / fact);
+        }
+    }
+    for (int r = 0; r < HALF; ++r)
+        for (int c = 0; c < HALF; ++c) B5inv[r][c] = (double)G[r][HALF + c];
     hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(cB), B, sizeof(B));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(cB5inv), B5inv, sizeof(B5inv));
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(cK), K, sizeof(K));
     if (e != hipSuccess) {
         set_error(std::string("epp minsnap: constants: ") + hipGetErrorString(e));
         return EPP_ERR_HIP;
@@ -850,28 +875,35 @@ epp_status minsnap_batch(const double* wp, const int32_t* wp_offsets, int32_t n_
 }
 
 // Per-host-thread state of the single-track latency path: a stream, pinned host buffers
-// the kernel reads / writes directly, and the device segment scratch of long tracks.
+// the kernel reads / writes directly, the device segment scratch of long tracks and the
+// coefficient hand-off (workgroup 0 -> row writers) with its flag.
 struct RefitCache {
     hipStream_t s = nullptr;
     int dev = -1;
     double* h_in = nullptr;
     size_t in_cap = 0;
-    char* h_out = nullptr;
+    char* h_out = nullptr;  // [status (8 B) | pad | writer slots (64 B) | rows (at +128)]
     size_t out_cap = 0;
-    double* d_scr = nullptr;
+    double* d_scr = nullptr;  // coefficients (kMaxCoef doubles... grown) then segment scratch
     size_t scr_cap = 0;
+    uint32_t* d_flag = nullptr;  // [seq, status], zeroed once
+    uint32_t seq = 0;
     std::vector<double> T, tin, tac;  // host side of the refit: times and samples
     std::vector<int32_t> seg;
     void release() {
+        if (s) (void)hipStreamSynchronize(s);
         if (h_in) (void)hipHostFree(h_in);
         if (h_out) (void)hipHostFree(h_out);
         if (d_scr) (void)hipFree(d_scr);
+        if (d_flag) (void)hipFree(d_flag);
         if (s) (void)hipStreamDestroy(s);
         h_in = nullptr;
         h_out = nullptr;
         d_scr = nullptr;
+        d_flag = nullptr;
         s = nullptr;
         in_cap = out_cap = scr_cap = 0;
+        seq = 0;
     }
     ~RefitCache() { release(); }
     epp_status ensure(size_t in_b, size_t out_b, size_t scr_b) {
@@ -881,8 +913,14 @@ struct RefitCache {
         dev = d;
         hipError_t e = hipSuccess;
         if (!s) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+        if (e == hipSuccess && !d_flag) {
+            e = hipMalloc(reinterpret_cast<void**>(&d_flag), 16);
+            if (e == hipSuccess) e = hipMemset(d_flag, 0, 16);
+            if (e == hipSuccess) e = hipDeviceSynchronize();
+        }
         auto grow_host = [&](auto*& p, size_t& cap, size_t need) {
             if (e != hipSuccess || need <= cap) return;
+            if (s) (void)hipStreamSynchronize(s);  // (the previous call's kernel has ended)
             if (p) (void)hipHostFree(p);
             p = nullptr;
             cap = 0;
@@ -892,6 +930,7 @@ struct RefitCache {
         grow_host(h_in, in_cap, in_b);
         grow_host(h_out, out_cap, out_b);
         if (e == hipSuccess && scr_b > scr_cap) {
+            (void)hipStreamSynchronize(s);
             if (d_scr) (void)hipFree(d_scr);
             d_scr = nullptr;
             scr_cap = 0;
@@ -1011,7 +1050,10 @@ epp_status generate_trajectory(const double* wp, int32_t n_wp, const double* tim
     }
     const int R = (int)c.tin.size();
     const bool lds = M <= kMaxLdsSeg;
-    if ((rc = c.ensure(refit_in_doubles(n_wp, R) * 8, (size_t)R * 80 + 16, lds ? 0 : (size_t)M * Seg::kSize * 8))) return rc;
+    const size_t coef_b = ((size_t)M * 30 * 8 + 255) & ~size_t(255);
+    if ((rc = c.ensure(refit_in_doubles(n_wp, R) * 8, (size_t)R * 80 + 128,
+                       coef_b + (lds ? 0 : (size_t)M * Seg::kSize * 8))))
+        return rc;
     double* in = c.h_in;
     std::memcpy(in, wp, (size_t)n_wp * 24);
     for (int k = 0; k < 3; ++k) {
@@ -1029,25 +1071,47 @@ epp_status generate_trajectory(const double* wp, int32_t n_wp, const double* tim
     a.in = in;
     a.W = n_wp;
     a.R = R;
+    a.writers = R ? std::min(kRefitMaxWriters, (R + kRefitRowChunk - 1) / kRefitRowChunk) : 0;
+    if (++c.seq == 0) c.seq = 1;
+    a.seq = c.seq;
     a.t0 = t0;
     if (n_wp <= kRefitArgW) std::memcpy(a.small, in, (size_t)(3 * n_wp + 6 + M) * 8);
-    // stage the sample data in LDS when it fits next to the solve's scratch
-    a.rows_lds = refit_lds_doubles(M, lds, R) * 8 <= 160u * 1024u ? 1 : 0;
-    a.out = reinterpret_cast<double*>(c.h_out + 16);
     a.info = reinterpret_cast<int64_t*>(c.h_out);
-    a.scratch = c.d_scr;
+    a.done = reinterpret_cast<uint32_t*>(c.h_out + 64);
+    a.out = reinterpret_cast<double*>(c.h_out + 128);
+    a.coef = c.d_scr;
+    a.flag = c.d_flag;
+    a.scratch = c.d_scr + coef_b / 8;
     a.info[0] = -100;
-    const size_t shm = refit_lds_doubles(M, lds, a.rows_lds ? R : 0) * sizeof(double);
-    if (lds) hipLaunchKernelGGL(k_refit<true>, dim3(1), dim3(kRefitBlock), shm, c.s, a);
-    else hipLaunchKernelGGL(k_refit<false>, dim3(1), dim3(kRefitBlock), shm, c.s, a);
+    const size_t shm = refit_lds_doubles(M, lds) * sizeof(double);
+    if (lds) hipLaunchKernelGGL(k_refit<true>, dim3(1 + a.writers), dim3(kRefitBlock), shm, c.s, a);
+    else hipLaunchKernelGGL(k_refit<false>, dim3(1 + a.writers), dim3(kRefitBlock), shm, c.s, a);
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = hipStreamSynchronize(c.s);
+    // wait for the status word and every writer's slot (polled; the stream is queried
+    // every ~1k polls so a failed launch ends the wait)
+    auto complete = [&]() {
+        if (__atomic_load_n(a.info, __ATOMIC_ACQUIRE) == -100) return false;
+        for (int g = 0; g < a.writers; ++g)
+            if (__atomic_load_n(a.done + g, __ATOMIC_ACQUIRE) != a.seq) return false;
+        return true;
+    };
+    for (uint64_t spin = 0; e == hipSuccess && !complete(); ++spin) {
+        if ((spin & 1023) == 1023) {
+            const hipError_t q = hipStreamQuery(c.s);
+            if (q == hipErrorNotReady) continue;
+            if (q != hipSuccess) e = q;
+            else if (!complete()) e = hipErrorUnknown;  // finished without its completion words
+            break;
+        }
+        _mm_pause();
+    }
+    const int64_t info = __atomic_load_n(a.info, __ATOMIC_ACQUIRE);
     if (e != hipSuccess) {
         set_error(std::string("generateTrajectory: ") + hipGetErrorString(e));
         return EPP_ERR_HIP;
     }
-    if (a.info[0] != 0) {
-        set_error(a.info[0] == -2 ? "Segment times need to be greater than zero" : "min-snap solve failed");
+    if (info != 0) {
+        set_error(info == -2 ? "Segment times need to be greater than zero" : "min-snap solve failed");
         return EPP_ERR_RUNTIME;
     }
     double* host_rows = (double*)std::malloc((size_t)std::max(R, 1) * 80);

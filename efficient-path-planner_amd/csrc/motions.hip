@@ -436,16 +436,11 @@ __global__ __launch_bounds__(BLOCK) void k_motions_d32b(const WorldView* __restr
 // those tiles is kept only in the first one along each axis (FX / FY rows), with
 // can_pass_gate the filling OBBs are masked out (:150-153).  The (edge, OBB) pairs go to
 // the wave's queue at offsets from a wave scan of the lanes' popcounts and are tested 64
-// at a time:
-//   MODE 0  exact closed AABB overlap in doubles + OBB::checkCollisionWithRay (src/OBB.cpp:10-61);
-//   MODE 1  the points s + (e - s) k/32, k = 1..32, through the rtree's strict containment
-//           and OBB::checkCollisionWithPoint (src/World.cpp:80-128, src/OBB.cpp:63-91).  The
-//           range of k that can hit is bounded first: every test is |a + b t| <= h (or
-//           lo < a + b t < hi) along the edge, so t lies in an interval, computed here
-//           with a slack eta (1e-6 m + 1e-12 of the coordinates' magnitude) far above the
-//           rounding of the points and of the interval; only the k inside it are tested
-//           exactly, in order, until one hits.  The slab range is widened by one slab per
-//           side, so points rounded past the edge's box stay covered.
+// at a time, after an exact AABB prefilter in doubles (the rtree's closed overlap):
+//   MODE 0  OBB::checkCollisionWithRay (src/OBB.cpp:10-61);
+//   MODE 1  the points s + (e - s) k/32, k = 1..32 (d32_pair_hit: only the k an interval
+//           bound admits are evaluated exactly).  The slab range and the prefilter box are
+//           widened by a hair, so points rounded past the edge's box stay covered.
 // An edge is invalid iff some pair hits — the reference's answer.
 constexpr int kQueueV5 = 256;
 
@@ -533,55 +528,7 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
                         const uint32_t m = (uint32_t)__double_as_longlong(rec[R_META]);
                         hit = rec_ray_hit(rec, ps, pe, (m & META_GATE) ? rg : ro);
                     } else {
-                        double rr[kRecDoubles];  // the record in registers
-#pragma unroll
-                        for (int k = 0; k <= F_HZ; ++k) rr[k] = rec[k];
-                        rr[R_META] = rec[R_META];
-                        const uint32_t m = (uint32_t)__double_as_longlong(rr[R_META]);
-                        const bool fillb = (m & META_FILLING) != 0u;
-                        const double r = (m & META_GATE) ? rg : ro;
-                        const double d[3] = {pe[0] - ps[0], pe[1] - ps[1], pe[2] - ps[2]};
-                        const double mag = fmax(fmax(fmax(fabs(ps[0]), fabs(ps[1])), fmax(fabs(ps[2]), fabs(pe[0]))),
-                                                fmax(fmax(fabs(pe[1]), fabs(pe[2])),
-                                                     fmax(fmax(fabs(rr[F_CX]), fabs(rr[F_CY])), fabs(rr[F_CZ]))));
-                        const double eta = 1e-6 + 1e-12 * mag;
-                        double t0 = 0.0, t1 = 1.0;
-                        // lo - eta <= a + b t <= hi + eta
-                        auto clip = [&](double a, double b, double lo, double hi) {
-                            const double u0 = lo - eta - a, u1 = hi + eta - a;
-                            if (b == 0.0) {
-                                if (!(u0 <= 0.0 && 0.0 <= u1)) t1 = -1.0;
-                            } else {
-                                const double v0 = u0 / b, v1 = u1 / b;
-                                t0 = fmax(t0, fmin(v0, v1));
-                                t1 = fmin(t1, fmax(v0, v1));
-                            }
-                        };
-                        // rtree contains (strict)  src/World.cpp:83
-                        clip(ps[0], d[0], rr[F_LOX], rr[F_HIX]);
-                        clip(ps[1], d[1], rr[F_LOY], rr[F_HIY]);
-                        clip(ps[2], d[2], rr[F_LOZ], rr[F_HIZ]);
-                        // OBB::checkCollisionWithPoint in the OBB frame  src/OBB.cpp:63-91
-                        const double c = rr[F_COS], sn = rr[F_SIN];
-                        const double ax = ps[0] - rr[F_CX], ay = ps[1] - rr[F_CY];
-                        const double tx = fillb ? rr[F_HX] : rr[F_HX] + r, ty = fillb ? rr[F_HY] : rr[F_HY] + r,
-                                     tz = fillb ? rr[F_HZ] : rr[F_HZ] + r;
-                        clip(c * ax + sn * ay, c * d[0] + sn * d[1], -tx, tx);
-                        clip(c * ay - sn * ax, c * d[1] - sn * d[0], -ty, ty);
-                        clip(ps[2] - rr[F_CZ], d[2], -tz, tz);
-                        int k0 = 33, k1 = 0;
-                        if (t0 <= t1) {  // (NaN bounds: fmax/fmin drop them -> the whole edge)
-                            k0 = max(1, (int)ceil(32.0 * t0));
-                            k1 = min(32, (int)floor(32.0 * t1));
-                        }
-                        hit = false;
-                        for (int k = k0; k <= k1 && !hit; ++k) {
-                            const double t = (double)k / 32.0;
-                            const double qx = ps[0] + (pe[0] - ps[0]) * t;
-                            const double qy = ps[1] + (pe[1] - ps[1]) * t;
-                            const double qz = ps[2] + (pe[2] - ps[2]) * t;
-                            hit = rec_hit<false>(rr, rg, ro, qx, qy, qz, cp, 0.0);
-                        }
+                        hit = d32_pair_hit(rec, ps, pe, rg, ro, cp);
                     }
                     if (hit) flags[owner] = 0;
                 }
@@ -696,7 +643,8 @@ using namespace epp;
 
 extern "C" {
 
-// Kernel choice: k_motions_v5 (slab filter) for worlds of <= 1024 OBBs whose records and
+// Kernel choice: small batches (<= kSmallMotions edges, <= kSmallMaxObbs OBBs) take the
+// brute-force k_motions_small (small.hip; no index needed); else k_motions_v5 (slab filter) for worlds of <= 1024 OBBs whose records and
 // slab rows fit a CU's LDS; else the cell-list LDS kernels (k_motions_v4 analytic,
 // k_motions_d32b discrete32) when the coarse grid, the records and the wave queues fit;
 // else k_motions.  Test hooks (not for production use): EPP_MOTIONS_KERNEL=generic forces
@@ -709,6 +657,9 @@ epp_status epp_check_motions(const epp_world* world, const double* s1, const dou
         return EPP_ERR_INVALID_ARGUMENT;
     }
     if (n == 0) return EPP_OK;
+    const SmallWorld sw = small_world(world);
+    if (small_motions(sw, n)) return launch_motions_small(sw, mode, s1, s2, n, can_pass_gate, valid, (hipStream_t)stream);
+    if (const epp_status st = ensure_index(world)) return st;
     const WorldView& w = world_view(world);
     hipStream_t st = (hipStream_t)stream;
     const char* forced = std::getenv("EPP_MOTIONS_KERNEL");

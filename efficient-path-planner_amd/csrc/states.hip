@@ -606,7 +606,8 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
 }
 
 // ---- launch ---------------------------------------------------------------------------
-// Kernel choice: k_states_v5 when its staged part fits and the buffers are aligned, else
+// Kernel choice: small batches (<= kSmallStates states, <= kSmallMaxObbs OBBs) take the
+// brute-force k_states_small (small.hip; no index needed); else k_states_v5 when its staged part fits and the buffers are aligned, else
 // k_states_v4 (aligned buffers), else k_states.  Test hooks (not for production use):
 // EPP_STATES_KERNEL = v4 | generic skips the faster kernels, EPP_V5_BLOCK = 512 | 1024
 // forces the k_states_v5 workgroup size, so every path and shape can be checked against
@@ -778,6 +779,11 @@ epp_status epp_check_states(const epp_world* world, const double* xyz, int64_t n
         return EPP_ERR_INVALID_ARGUMENT;
     }
     if (n == 0) return EPP_OK;
+    const SmallWorld sw = small_world(world);
+    if (small_states(sw, n))
+        return launch_states_small(sw, false, xyz, n, can_pass_gate, 0.0, valid, compact_idx, n_valid,
+                                   (hipStream_t)stream);
+    if (const epp_status st = ensure_index(world)) return st;
     return launch_states<false>(world_view(world), world_dview(world), xyz, n, can_pass_gate, 0.0, valid,
                                 compact_idx, n_valid, stream);
 }
@@ -798,6 +804,10 @@ epp_status epp_check_states_mindist(const epp_world* world, const double* xyz, i
         return EPP_ERR_INVALID_ARGUMENT;
     }
     if (n == 0) return EPP_OK;
+    const SmallWorld sw = small_world(world);
+    if (small_states(sw, n))
+        return launch_states_small(sw, true, xyz, n, 0, min_distance, valid, nullptr, nullptr, (hipStream_t)stream);
+    if (const epp_status st = ensure_index(world)) return st;
     return launch_states<true>(world_view(world), world_dview(world), xyz, n, 0, min_distance, valid, nullptr,
                                nullptr, stream);
 }

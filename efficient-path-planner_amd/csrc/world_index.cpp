@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -53,6 +54,49 @@ bool is_rz(const epp_obb& o) {
 }
 
 inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+
+// The OBB records of a new version (AABBs, kRecDoubles-double records with the filling /
+// gate bits) into hw.aabbs and the pinned hw.h_recs; the cheap part of an update.
+bool build_records(HostWorld& hw, const epp_obb* obbs, int n) {
+    for (int i = 0; i < n; ++i)
+        if (!is_rz(obbs[i])) {  // (checked first: a failed update leaves the world as it was)
+            set_error("epp_world: OBB rotation must be a rotation about z (src/Object.cpp:38-47)");
+            return false;
+        }
+    const size_t need = std::max<size_t>(1, (size_t)n * kRecDoubles) * sizeof(double);
+    if (need > hw.h_recs_cap) {
+        if (hw.h_recs) (void)hipHostFree(hw.h_recs);
+        hw.h_recs = nullptr;
+        hw.h_recs_cap = 0;
+        const hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&hw.h_recs), need * 2, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            set_error(std::string("epp_world: allocation: ") + hipGetErrorString(e));
+            return false;
+        }
+        hw.h_recs_cap = need * 2;
+    }
+    hw.aabbs.assign((size_t)n * 6, 0.0);
+    for (int i = 0; i < n; ++i) {
+        const epp_obb& o = obbs[i];
+        double lo[3], hi[3];
+        compute_aabb(o, o.is_gate ? hw.r_gate : hw.r_obst, lo, hi);  // src/World.cpp:89-90
+        double* r = hw.h_recs + (size_t)i * kRecDoubles;
+        for (int k = 0; k < 3; ++k) {
+            hw.aabbs[(size_t)i * 6 + k] = r[F_LOX + k] = lo[k];
+            hw.aabbs[(size_t)i * 6 + 3 + k] = r[F_HIX + k] = hi[k];
+            r[F_CX + k] = o.center[k];
+            r[F_HX + k] = o.half[k];
+        }
+        r[F_COS] = o.rot[0];
+        r[F_SIN] = o.rot[3];
+        r[14] = r[15] = 0.0;
+        const uint64_t m = (o.filling ? META_FILLING : 0u) | (o.is_gate ? META_GATE : 0u);
+        std::memcpy(&r[R_META], &m, 8);
+    }
+    hw.obbs.assign(obbs, obbs + n);
+    hw.view.n_obb = n;
+    return true;
+}
 
 // Builds the blob (layout in epp_internal.h).  Returns false with an error set.
 bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
@@ -490,11 +534,11 @@ bool upload(HostWorld& hw) {
         set_error(std::string("epp_world: upload: ") + hipGetErrorString(e));
         return false;
     }
-    ++hw.generation;
     return true;
 }
 
 }  // namespace
+
 }  // namespace epp
 
 struct epp_world : epp::HostWorld {};
@@ -516,7 +560,7 @@ epp_status epp_world_create(const epp_obb* obbs, int32_t n, double r_gate, doubl
     w->r_gate = r_gate;
     w->r_obst = r_obst;
     (void)hipGetDevice(&w->device);
-    if (!epp::build_blob(*w, obbs, n)) {
+    if (!epp::build_records(*w, obbs, n) || !epp::build_blob(*w, obbs, n)) {
         delete w;
         return EPP_ERR_UNSUPPORTED;
     }
@@ -524,6 +568,7 @@ epp_status epp_world_create(const epp_obb* obbs, int32_t n, double r_gate, doubl
         delete w;
         return EPP_ERR_HIP;
     }
+    w->generation = 1;
     *out = w;
     return EPP_OK;
 }
@@ -533,17 +578,21 @@ epp_status epp_world_update(epp_world* w, const epp_obb* obbs, int32_t n) {
         epp::set_error("epp_world_update: invalid argument");
         return EPP_ERR_INVALID_ARGUMENT;
     }
-    // the previous blob may still be read by in-flight kernels on any stream
+    // the previous records / blob may still be read by in-flight kernels on any stream
     (void)hipDeviceSynchronize();
-    if (!epp::build_blob(*w, obbs, n)) return EPP_ERR_UNSUPPORTED;
-    if (!epp::upload(*w)) return EPP_ERR_HIP;
+    std::lock_guard<std::mutex> lk(w->mu);
+    if (!epp::build_records(*w, obbs, n)) return EPP_ERR_UNSUPPORTED;
+    w->index_stale = true;
+    ++w->generation;
     return EPP_OK;
 }
 
 epp_status epp_world_destroy(epp_world* w) {
     if (!w) return EPP_OK;
+    (void)hipDeviceSynchronize();
     if (w->d_blob) (void)hipFree(w->d_blob);
     if (w->h_stage) (void)hipHostFree(w->h_stage);
+    if (w->h_recs) (void)hipHostFree(w->h_recs);
     if (w->stream) (void)hipStreamDestroy(w->stream);
     delete w;
     return EPP_OK;
@@ -576,6 +625,31 @@ epp_status epp_world_get_aabbs(const epp_world* w, double* lo_hi) {
 namespace epp {
 const WorldView& world_view(const epp_world* w) { return w->view; }
 const WorldView* world_dview(const epp_world* w) { return w->d_view; }
+
+// The device index of the current version: rebuilt and uploaded here when an update made
+// it stale (after every kernel that may still read the old blob has finished).
+epp_status ensure_index(const epp_world* cw) {
+    HostWorld& hw = const_cast<epp_world&>(*cw);
+    std::lock_guard<std::mutex> lk(hw.mu);
+    if (!hw.index_stale) return EPP_OK;
+    (void)hipDeviceSynchronize();
+    if (!build_blob(hw, hw.obbs.data(), (int)hw.obbs.size())) return EPP_ERR_UNSUPPORTED;
+    if (!upload(hw)) return EPP_ERR_HIP;
+    hw.index_stale = false;
+    return EPP_OK;
+}
+
+SmallWorld small_world(const epp_world* cw) {
+    HostWorld& hw = const_cast<epp_world&>(*cw);
+    std::lock_guard<std::mutex> lk(hw.mu);
+    SmallWorld s;
+    s.recs = hw.index_stale ? hw.h_recs : reinterpret_cast<const double*>(hw.view.blob + hw.view.off_aos);
+    s.n_obb = (int32_t)hw.obbs.size();
+    s.r_gate = hw.r_gate;
+    s.r_obst = hw.r_obst;
+    return s;
+}
+
 }  // namespace epp
 
 // Debug entry (not part of include/epp.h): sizes of the device index, for tests and
@@ -590,5 +664,27 @@ extern "C" epp_status epp_dbg_world_info(const epp_world* w, int64_t out[6]) {
     out[3] = (int64_t)v.bnx * v.bny * v.bnz;
     out[4] = (int64_t)v.nx * v.ny * v.nz;
     out[5] = v.n_obb;
+    return EPP_OK;
+}
+
+// Debug entry (not part of include/epp.h): host-side index build only (no device), for
+// timing the world rebuild on the CPU.  out: [microseconds per build, blob bytes, tile
+// count per axis, tile words, slab words W, slabs S].
+extern "C" epp_status epp_dbg_build_blob(const epp_obb* obbs, int32_t n, double r_gate, double r_obst, int32_t reps,
+                                         double out[6]) {
+    if (!out || n < 0 || (n > 0 && !obbs) || reps < 1) return EPP_ERR_INVALID_ARGUMENT;
+    epp::HostWorld hw;
+    hw.r_gate = r_gate;
+    hw.r_obst = r_obst;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int r = 0; r < reps; ++r)
+        if (!epp::build_blob(hw, obbs, n)) return EPP_ERR_UNSUPPORTED;
+    const auto t1 = std::chrono::steady_clock::now();
+    out[0] = std::chrono::duration<double, std::micro>(t1 - t0).count() / reps;
+    out[1] = hw.view.blob_bytes;
+    out[2] = hw.view.tile_n;
+    out[3] = hw.view.tile_words;
+    out[4] = hw.view.slab_w;
+    out[5] = hw.view.slab_n;
     return EPP_OK;
 }

@@ -63,8 +63,8 @@ private:
     };
     void addObject(int id, bool gate, const std::vector<double>& coordinates, bool update);
     void sync() const;
-    template <typename Launch>
-    void query(int64_t n, int n_in, Launch&& launch, const double* const* in, uint8_t* out) const;
+    template <typename Launch, typename Small>
+    void query(int64_t n, int n_in, Launch&& launch, Small&& small, const double* const* in, uint8_t* out) const;
 
     std::shared_ptr<ConfigParser> config_;
     double rGate_, rObst_;

@@ -1,8 +1,9 @@
 """Phase timeline of the fused single-track refit (k_refit): builds a diagnostics copy of
 libepp.so with -DEPP_REFIT_TL into scripts/dbg/ (not the product library), runs 50
 refits and prints the median time of every phase boundary (s_memrealtime, 100 MHz)
-relative to the kernel's first stamp.  Stamps: 0 entry, 1 inputs + A^-1, 2 Q, 3 G, 4 H,
-5 assembly, 6 block Cholesky, 7 coefficients, 11 rows written."""
+relative to the kernel's first stamp.  Solver (wg0): 0 entry, 9 A^-1, 1 vertex values,
+2 Q, 3 G, 4 H, 5 assembly, 6 block Cholesky, 7 coefficients, 11 published; row writer
+(wg1): 12 coefficients received, 13 rows written."""
 import ctypes as C
 import os
 import subprocess
@@ -37,7 +38,7 @@ for r in range(60):
 st = np.array(stamps[10:]).reshape(-1, 2, 16)
 t0 = st[:, :, 0].min(axis=1)
 for wg in range(2):
-    for k in range(12):
+    for k in range(16):
         d = (st[:, wg, k] - t0) * 10  # ns
         if (st[:, wg, k] > 0).all():
             print(f"wg{wg} stamp {k:2d}: median {np.median(d) / 1000:7.2f} us")

@@ -439,3 +439,53 @@ def test_world_update_small_queries_zero_copy(cfg, geom, worlds):
             assert pp.check_trajectory_validity(rows, 0.1) == bool(exp.all())
             for p, e in zip(pts[:50], O.check_states(ref, rg, ro, pts[:50], False)):
                 assert pp.check_point_validity(p, False) == bool(e)
+
+
+@pytest.mark.parametrize("name", ["c1", "c2"])
+def test_small_query_path(fworlds, name, monkeypatch):
+    """Small batches (<= 4096 states / 1024 edges on worlds of <= 256 OBBs) take the
+    brute-force kernels of small.hip: with a current index (records from the device blob),
+    after epp_world_update (stale index: records read from the pinned host copy), and a
+    large query afterwards rebuilds the index.  Every answer vs the oracle, both can_pass
+    values, both motion modes, minDistance; and equal to the index kernels' answers."""
+    fgeom, rg, ro, ws = fworlds
+    gates, obstacles, (lo, hi) = ws[name]
+    w = capi.World(capi.build_obbs(fgeom, gates, obstacles), rg, ro)
+    rs = np.random.RandomState(11)
+    g = np.array(gates, float)
+    for version in range(3):
+        if version:
+            g[:, 0] += rs.uniform(-0.2, 0.2, len(g))
+            g[:, 5] += rs.uniform(-0.2, 0.2, len(g))
+            w.update(capi.build_obbs(fgeom, g, obstacles))  # index stale until a large query
+        ref = O.world_build(fgeom, g, obstacles, rg, ro)
+        a = _gate_openings(g, fgeom, 200, seed=version)
+        pts = np.vstack([synth.sample_states(40 + version, lo, hi, 4096 - len(a)), a])  # 4096: still "small"
+        yaw = np.repeat(g[:, 5], 200)[:1024 - 500]
+        nrm = np.stack([-np.sin(yaw), np.cos(yaw), np.zeros_like(yaw)], 1)
+        e1, e2 = synth.edges(50 + version, 51, lo, hi, 500, max_len=1.0)
+        s1 = np.vstack([e1, a[:len(yaw)] - 0.4 * nrm])
+        s2 = np.vstack([e2, a[:len(yaw)] + 0.4 * nrm])
+        for cp in (0, 1):
+            exp = O.check_states(ref, rg, ro, pts, cp)
+            for n in (1, 37, len(pts)):
+                assert np.array_equal(w.check_states(pts[:n], cp), exp[:n]), (version, cp, n)
+            for mode in (0, 1):
+                exp_m = O.check_motions(ref, rg, ro, s1, s2, cp, mode, threads=8)
+                assert exp_m.min() == 0 and exp_m.max() == 1
+                assert np.array_equal(w.check_motions(s1, s2, cp, mode), exp_m), (version, cp, mode)
+        for md in (0.0, 0.2):
+            assert np.array_equal(w.check_states_mindist(pts, md), O.check_states_mindist(ref, pts, md))
+        # the index kernels agree (forced; the first call after an update rebuilds the index)
+        monkeypatch.setenv("EPP_STATES_KERNEL", "v5")
+        monkeypatch.setenv("EPP_MOTIONS_KERNEL", "v5")
+        assert np.array_equal(w.check_states(pts, 1), O.check_states(ref, rg, ro, pts, 1))
+        assert np.array_equal(w.check_motions(s1, s2, 1, 1), O.check_motions(ref, rg, ro, s1, s2, 1, 1))
+        monkeypatch.delenv("EPP_STATES_KERNEL")
+        monkeypatch.delenv("EPP_MOTIONS_KERNEL")
+    # a large query after an update rebuilds the index on its own
+    g[0, 1] += 0.3
+    w.update(capi.build_obbs(fgeom, g, obstacles))
+    ref = O.world_build(fgeom, g, obstacles, rg, ro)
+    big = synth.sample_states(99, lo, hi, 50_000)
+    assert np.array_equal(w.check_states(big), O.check_states(ref, rg, ro, big, threads=8))
