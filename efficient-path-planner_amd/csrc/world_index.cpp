@@ -543,6 +543,10 @@ bool upload(HostWorld& hw) {
 
 struct epp_world : epp::HostWorld {};
 
+namespace epp {
+epp_status ensure_index(const epp_world* w);
+}
+
 extern "C" {
 
 epp_status epp_world_create(const epp_obb* obbs, int32_t n, double r_gate, double r_obst,
@@ -596,6 +600,14 @@ epp_status epp_world_destroy(epp_world* w) {
     if (w->stream) (void)hipStreamDestroy(w->stream);
     delete w;
     return EPP_OK;
+}
+
+epp_status epp_world_build_index(const epp_world* w) {
+    if (!w) {
+        epp::set_error("epp_world_build_index: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    return epp::ensure_index(w);
 }
 
 epp_status epp_world_generation(const epp_world* w, uint64_t* generation) {

@@ -68,6 +68,7 @@ def lib() -> C.CDLL:
             "epp_world_num_obbs": (i32, [vp, C.POINTER(i32)]),
             "epp_world_get_aabbs": (i32, [vp, vp]),
             "epp_world_generation": (i32, [vp, C.POINTER(C.c_uint64)]),
+            "epp_world_build_index": (i32, [vp]),
             "epp_comm_unique_id": (i32, [vp]),
             "epp_comm_init": (i32, [vp, i32, i32, C.POINTER(vp)]),
             "epp_comm_init_all": (i32, [i32, vp, vp]),
@@ -124,7 +125,7 @@ EXPORTED = [
     "epp_knn_edges", "epp_compact_states", "epp_mask_edges", "epp_optimal_trajectory_host",
     "epp_spline_trajectory_host", "epp_compact_workspace_size", "epp_compact_states_ws",
     "epp_graph_begin", "epp_graph_end", "epp_graph_launch", "epp_graph_destroy", "epp_minsnap_batch_times",
-    "epp_generate_trajectory_times_host", "epp_world_generation", "epp_comm_unique_id", "epp_comm_init",
+    "epp_generate_trajectory_times_host", "epp_world_generation", "epp_world_build_index", "epp_comm_unique_id", "epp_comm_init",
     "epp_comm_init_all", "epp_comm_destroy", "epp_comm_rank", "epp_comm_allgather_waypoints",
 ]
 
@@ -217,6 +218,10 @@ class World:
         obbs = np.ascontiguousarray(obbs, dtype=OBB_DTYPE)
         check(lib().epp_world_update(self.handle, _ptr(obbs) if len(obbs) else None, len(obbs)))
         self.n = len(obbs)
+
+    def build_index(self) -> None:
+        """Rebuild + upload a stale device index now (epp_world_build_index)."""
+        check(lib().epp_world_build_index(self.handle))
 
     def generation(self) -> int:
         g = C.c_uint64(0)

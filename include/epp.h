@@ -116,11 +116,19 @@ epp_status epp_build_obbs(const epp_obb_desc* gate_desc, const int32_t* gate_des
 epp_status epp_world_create(const epp_obb* obbs, int32_t n_obbs, double r_gate, double r_obst,
                             epp_world** out);
 /* Replaces the OBB set (gate-pose update = full rebuild, src/OnlineTrajGenerator.cpp:146).
- * Waits for every kernel on the device first (they may read the old index), then
- * uploads.  HIP graphs that captured launches on this world must be re-captured
- * afterwards: launch shapes depend on the index size (epp_world_generation changes). */
+ * Waits for every kernel on the device first (they may read the old records / index),
+ * then rebuilds the OBB records only (pinned host memory): small queries (<= 4096 states
+ * or 1024 edges on worlds of <= 256 OBBs) read those directly; the device index is
+ * rebuilt and uploaded by the first call that needs it (or epp_world_build_index), so
+ * an index error (e.g. too many distinct candidate lists) is reported there.  HIP graphs
+ * that captured launches on this world must be re-captured afterwards, and only after
+ * epp_world_build_index (launch shapes depend on the index; epp_world_generation
+ * changes). */
 epp_status epp_world_update(epp_world* w, const epp_obb* obbs, int32_t n_obbs);
-/* Number of uploads of this world so far (create = 1, every update + 1). */
+/* Rebuilds and uploads the device index now if an update left it stale (synchronous;
+ * not inside a stream capture). */
+epp_status epp_world_build_index(const epp_world* w);
+/* Number of versions of this world so far (create = 1, every update + 1). */
 epp_status epp_world_generation(const epp_world* w, uint64_t* generation);
 epp_status epp_world_destroy(epp_world* w);
 epp_status epp_world_num_obbs(const epp_world* w, int32_t* n);

@@ -409,10 +409,24 @@ def test_graph_replay_matches_direct_launch(geom, worlds):
         assert np.array_equal(got, w.check_states(pts[b]))
         assert np.array_equal(got, O.check_states(ref, rg, ro, pts[b], False, threads=8))
     capi.check(L.epp_graph_destroy(g.value))
-    L.epp_stream_destroy(s.value)
-    # an update is a new upload: captured graphs must be re-captured (epp.h)
-    w.update(capi.build_obbs(geom, gates, obstacles))
+    # an update is a new version: captured graphs must be re-captured, after the index
+    # is rebuilt (epp.h); a capture over a rebuilt index replays the new world
+    g2 = np.array(gates, float)
+    g2[:, 0] += 0.15
+    w.update(capi.build_obbs(geom, g2, obstacles))
     assert w.generation() == gen0 + 1
+    w.build_index()
+    ref2 = O.world_build(geom, g2, obstacles, rg, ro)
+    capi.check(L.epp_graph_begin(s.value))
+    w.check_states_dev(d_in[0].ptr, n, 0, d_out[0].ptr, stream=s.value)
+    capi.check(L.epp_graph_end(s.value, C.byref(g)))
+    d_out[0].zero()
+    capi.sync()
+    capi.check(L.epp_graph_launch(g.value, s.value))
+    capi.check(L.epp_stream_sync(s.value))
+    assert np.array_equal(d_out[0].download(np.uint8, n), O.check_states(ref2, rg, ro, pts[0], False, threads=8))
+    capi.check(L.epp_graph_destroy(g.value))
+    L.epp_stream_destroy(s.value)
 
 
 def test_world_update_small_queries_zero_copy(cfg, geom, worlds):
