@@ -149,8 +149,22 @@ inline int bm_axis(double p, float off, float inv) {
 struct HostWorld {
     WorldView view{};
     std::vector<epp_obb> obbs;          // the OBBs of the current version
-    double* h_recs = nullptr;           // pinned: n x kRecDoubles records of the current version
-    size_t h_recs_cap = 0;
+    // Pinned records of the versions (n x kRecDoubles): two slots, the current version's
+    // and the previous one's, so an update never rewrites records a kernel of the current
+    // version may still read.  Kernels launched asynchronously on the host copy (the small
+    // path while the index is stale) record an event per (slot, stream) after them; an
+    // update waits for the slot's events before it reuses the slot.  (Polled host calls
+    // have finished reading when they return.)
+    struct RecReader {
+        hipStream_t stream;
+        hipEvent_t ev;
+        bool pending;
+    };
+    double* h_recs = nullptr;           // = rec_buf[rec_slot]
+    double* rec_buf[2] = {nullptr, nullptr};
+    size_t rec_cap[2] = {0, 0};
+    int rec_slot = 0;
+    std::vector<RecReader> rec_readers[2];
     bool index_stale = false;           // the device blob is an older version
     std::mutex mu;                      // guards the lazy index rebuild
     double r_gate = 0, r_obst = 0;
@@ -196,6 +210,7 @@ struct SmallWorld {
     const double* recs;
     int32_t n_obb;
     double r_gate, r_obst;
+    int host_slot;  // recs is the pinned host copy of this slot (index stale), else -1
 };
 
 }  // namespace epp

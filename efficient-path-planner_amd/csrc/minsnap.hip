@@ -39,8 +39,18 @@ constexpr int N = 10;
 constexpr int HALF = 5;
 constexpr int kWave = 64;
 
-// falling factorials: B[k][j] = j! / (j-k)!  (src/polynomial.cpp:145-160)
-__constant__ double cB[N][N];
+// The kernels' constants, one block (kNC doubles, set once per device by ensure_consts and
+// staged into LDS at kernel entry, overlapping the inputs' loads — lane-indexed reads of
+// __constant__ memory are vector loads that miss the caches on the latency path):
+//   kCB   falling factorials B[k][j] = j! / (j-k)!  (src/polynomial.cpp:145-160), 10 x 10
+//   kCB5  B5^-1, kCK  K (the closed-form mapping inverse, ainv_entry), 5 x 5 each
+//   kCF   1 / r!, r = 0..4
+constexpr int kCB = 0, kCB5 = 100, kCK = 125, kCF = 150, kNC = 156;  // (kNC even: 16-byte aligned LDS after it)
+__constant__ double cC[kNC];
+template <int BLOCK>
+__device__ __forceinline__ void stage_consts(double* dst) {
+    for (int e = threadIdx.x; e < kNC; e += BLOCK) dst[e] = cC[e];
+}
 
 // Phase timeline of the fused refit (diagnostics builds only: -DEPP_REFIT_TL, see
 // scripts/refit_timeline.py): thread 0 of each workgroup stamps s_memrealtime (100 MHz).
@@ -50,7 +60,24 @@ __device__ unsigned long long g_refit_tl[2][16];
     do {                                                                                  \
         if (threadIdx.x == 0) g_refit_tl[blockIdx.x & 1][k] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+// (per-iteration shader clocks of the block solve's forward / backward loops)
+__device__ unsigned long long g_refit_it[2][64];
+#define EPP_TLI(k)                                                                           \
+    do {                                                                                     \
+        if (threadIdx.x == 0 && (k) < 64) g_refit_it[blockIdx.x & 1][k] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+// (slots 14, 15: the shader clock, s_memtime, around the block solve)
+#define EPP_TLC(k)                                                                        \
+    do {                                                                                  \
+        if (threadIdx.x == 0) g_refit_tl[blockIdx.x & 1][k] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
 #else
+#define EPP_TLC(k) \
+    do {           \
+    } while (0)
+#define EPP_TLI(k) \
+    do {           \
+    } while (0)
 #define EPP_TL(k) \
     do {          \
     } while (0)
@@ -73,8 +100,20 @@ __device__ __forceinline__ double rsq_nr(double x) {
     return fma(0.5 * y, fma(-(x * y), y, 1.0), y);
 }
 
-// 1 / r! for r = 0..4 (the same roundings as dividing at run time)
-__device__ constexpr double kInvFact[HALF] = {1.0, 1.0, 1.0 / 2.0, 1.0 / 6.0, 1.0 / 24.0};
+// Workgroup barrier.  SCR_LDS (all the solve's shared data in LDS): waits for this
+// wave's LDS operations only, so global loads issued earlier (e.g. the refit's host
+// reads of its sample data) stay in flight across it; else a full __syncthreads.
+template <bool SCR_LDS>
+__device__ __forceinline__ void block_sync() {
+    if (SCR_LDS) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    else __syncthreads();
+}
+
+// Orders one wavefront's LDS accesses across its lanes (LDS operations of a wavefront
+// complete in order; this waits for them and stops the compiler moving memory accesses
+// across the point).
+__device__ __forceinline__ void wave_sync_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 
 // setupMappingMatrix + invertMappingMatrix (impl :111-121, :142-179) in closed form.  The
 // mapping matrix is A = [[diag(k!), 0], [C, D]] with C[k][j] = B[k][j] T^(j-k) and
@@ -86,42 +125,44 @@ __device__ constexpr double kInvFact[HALF] = {1.0, 1.0, 1.0 / 2.0, 1.0 / 6.0, 1.
 // a constant times a power of 1/T, so the 100 entries are independent (one thread each)
 // instead of a 5x5 LU per segment on one lane.  The reference's LU with partial pivoting
 // gives the same matrix to rounding (the parity target of the solve is 1e-6).
-__constant__ double cB5inv[HALF][HALF];
-__constant__ double cK[HALF][HALF];
-
-__device__ __forceinline__ double ainv_entry(double invT, int r, int c) {
-    if (r < HALF) return r == c ? kInvFact[r] : 0.0;
+// ipow: (1/T)^0..(1/T)^9
+__device__ __forceinline__ double ainv_entry(const double* kc, const double* ipow, int r, int c) {
+    if (r < HALF) return r == c ? kc[kCF + r] : 0.0;
     const int rr = r - HALF;
     const int ex = (c < HALF ? c : c - HALF) - rr - HALF;  // in [-9, -1]
-    double p = invT;
-    for (int k = 1; k < -ex; ++k) p = p * invT;
-    return (c < HALF ? cK[rr][c] : cB5inv[rr][c - HALF]) * p;
+    return (c < HALF ? kc[kCK + rr * HALF + c] : kc[kCB5 + rr * HALF + c - HALF]) * ipow[-ex];
 }
 
 // Per-segment scratch (doubles): A^-1 (10x10), H (10x10), the 6x6 snap block Q of Q_i,
-// G = Q * (rows 4..9 of A^-1) (6x10), and the R_pp blocks: W (coupling to the next inner
-// vertex) and L (diagonal block, then its Cholesky factor), I (1 / diagonal of the factor).
+// G = Q * (rows 4..9 of A^-1) (6x10), the R_pp blocks: W (coupling to the next inner
+// vertex) and L (diagonal block, then its Cholesky factor), I (1 / diagonal of the
+// factor), and the powers of T.
 struct Seg {
-    static constexpr int kAinv = 0, kH = 100, kQ = 200, kG = 236, kW = 296, kL = 312, kI = 328, kSize = 332;
+    static constexpr int kAinv = 0, kH = 100, kQ = 200, kG = 236, kW = 296, kL = 312, kI = 328, kPow = 332,
+                         kSize = 354;
 };
+// kPow: T^0..T^11 (Q's powers) then (1/T)^0..(1/T)^9 (A^-1's), each the same chain of
+// products as evaluated per entry before (12 + 10 doubles)
+constexpr int kNPow = 22;
 // Per track, besides the segment scratch: (M+1) x 5 x 3 vertex values, (M+1) x 4 x 3
-// right-hand sides, M segment times.
-__host__ __device__ constexpr size_t vertex_doubles(int M) { return (size_t)(M + 1) * 27 + (size_t)M; }
+// right-hand sides, M segment times and the block solve's lane exchange (kXch, in LDS).
+constexpr int kXch = 32;
+__host__ __device__ constexpr size_t vertex_doubles(int M) { return (size_t)(M + 1) * 27 + (size_t)M + kXch; }
 // Tracks with up to this many segments keep the segment scratch in LDS (~114 KB at 40).
 constexpr int kMaxLdsSeg = 40;
 
 // The min-snap solve of one track by one workgroup of BLOCK threads (every thread calls
-// it; it contains barriers).  P: W x 3 waypoints; v0/a0: the start vertex's velocity and
+// it; it contains barriers).  kc: the constants (LDS).  P: W x 3 waypoints; v0/a0: the start vertex's velocity and
 // acceleration (NULL = 0); times_in: caller segment times (NULL = Nfabian).  scr: M x
-// Seg::kSize, dv/rhs/Tm: vertex_doubles(M) (LDS or global).  *s_err must be 0 and
+// Seg::kSize, dv/rhs/Tm/xch: vertex_doubles(M) (LDS).  *s_err must be 0 and
 // visible to every thread on entry.  Writes T_out (M, may be NULL) and C_out (M x 3 x 10,
 // increasing powers).  Returns 0, -2 (a segment time <= 0: the reference's
 // CHECK_GT(segment_time, 0), impl :297) or -3 (R_pp not SPD).
-template <int BLOCK>
-__device__ __forceinline__ int solve_track(const double* __restrict__ P, int M, double vmax, double amax,
+template <int BLOCK, bool SCR_LDS>
+__device__ __forceinline__ int solve_track(const double* __restrict__ kc, const double* __restrict__ P, int M, double vmax, double amax,
                                            const double* v0, const double* a0, const double* times_in,
-                                           double* scr, double* dv, double* rhs, double* Tm, int* s_err,
-                                           double* T_out, double* C_out) {
+                                           double* scr, double* dv, double* rhs, double* Tm, double* xch,
+                                           int* s_err, double* T_out, double* C_out) {
     const int tid = threadIdx.x;
     // ---- phase 1: segment times, mapping inverses, fixed vertex values ----------
     for (int i = tid; i < M; i += BLOCK) {
@@ -130,19 +171,33 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ P, int M, 
         if (T_out) T_out[i] = T;
         if (!(T > 0)) atomicOr(s_err, 1);  // CHECK_GT(segment_time, 0)  impl :297
     }
-    __syncthreads();
+    block_sync<SCR_LDS>();
+    for (int e = tid; e < M * kNPow; e += BLOCK) {  // the powers of T and 1/T
+        const int i = e / kNPow, k = e % kNPow;
+        const double T = Tm[i];
+        double p = 1.0;
+        if (k < 12) {
+            if (k > 0) p = T;
+            for (int q = 1; q < k; ++q) p = p * T;
+        } else if (k > 12) {
+            // 1/T: the hardware reciprocal refined by two Newton steps (~1e-16; a division
+            // would cost ~10 dependent instructions)
+            double it = __builtin_amdgcn_rcp(T);
+            it = fma(it, fma(-T, it, 1.0), it);
+            it = fma(it, fma(-T, it, 1.0), it);
+            p = it;
+            for (int q = 13; q < k; ++q) p = p * it;
+        }
+        scr[(size_t)i * Seg::kSize + Seg::kPow + k] = p;
+    }
+    block_sync<SCR_LDS>();
     for (int e = tid; e < M * N * N; e += BLOCK) {
         const int i = e / (N * N), r = (e % (N * N)) / N, c = e % N;
-        // 1/T: the hardware reciprocal refined by two Newton steps (~1e-16; a division
-        // per entry would cost ~10 dependent instructions)
-        const double T = Tm[i];
-        double it = __builtin_amdgcn_rcp(T);
-        it = fma(it, fma(-T, it, 1.0), it);
-        it = fma(it, fma(-T, it, 1.0), it);
-        scr[(size_t)i * Seg::kSize + Seg::kAinv + r * N + c] = ainv_entry(it, r, c);
+        double* S = scr + (size_t)i * Seg::kSize;
+        S[Seg::kAinv + r * N + c] = ainv_entry(kc, S + Seg::kPow + 12, r, c);
     }
 #ifdef EPP_REFIT_TL
-    __syncthreads();
+    block_sync<SCR_LDS>();
     EPP_TL(9);
 #endif
     // start vertex {p0, v0, a0, 0, 0}, inner {p}, end {p, 0, 0, 0, 0}: makeStartOrEnd
@@ -155,17 +210,19 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ P, int M, 
         else if (v == 0 && k == 2) val = a0 ? a0[d] : 0.0;
         dv[e] = val;
     }
-    __syncthreads();
+    block_sync<SCR_LDS>();
     EPP_TL(1);
     if (*s_err) return -2;
     // ---- phase 2: Q (6x6 snap block), G = Q A^-1, H = A^-T G ------------------------
     // computeQuadraticCostJacobian (impl :567-583): Q[9-r][9-c] = B[4][9-r] B[4][9-c] t^e 2/e
+    // (t^e by repeated products, e = 1..11: within a few ulp of pow, ~10x cheaper)
     for (int e = tid; e < M * 36; e += BLOCK) {
         const int i = e / 36, a = 4 + (e % 36) / 6, b = 4 + e % 6;
-        const double ex = (double)(a + b - 7);
-        scr[(size_t)i * Seg::kSize + Seg::kQ + (a - 4) * 6 + (b - 4)] = cB[4][a] * cB[4][b] * pow(Tm[i], ex) * 2.0 / ex;
+        const int ex = a + b - 7;
+        double* S = scr + (size_t)i * Seg::kSize;
+        S[Seg::kQ + (a - 4) * 6 + (b - 4)] = kc[kCB + 4 * N + a] * kc[kCB + 4 * N + b] * S[Seg::kPow + ex] * 2.0 / (double)ex;
     }
-    __syncthreads();
+    block_sync<SCR_LDS>();
     EPP_TL(2);
     for (int e = tid; e < M * 60; e += BLOCK) {
         const int i = e / 60, a = (e % 60) / 10, c = e % 10;
@@ -175,7 +232,7 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ P, int M, 
         for (int b = 0; b < 6; ++b) g = g + S[Seg::kQ + a * 6 + b] * S[Seg::kAinv + (b + 4) * N + c];
         S[Seg::kG + a * 10 + c] = g;
     }
-    __syncthreads();
+    block_sync<SCR_LDS>();
     EPP_TL(3);
     // All 100 entries (no mirrored triangle): every row keeps the exact translation
     // invariance H[r][0] == -H[r][5] that the reference's full product has.
@@ -187,7 +244,7 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ P, int M, 
         for (int a = 0; a < 6; ++a) h = h + S[Seg::kAinv + (a + 4) * N + r] * S[Seg::kG + a * 10 + c];
         S[Seg::kH + r * N + c] = h;
     }
-    __syncthreads();
+    block_sync<SCR_LDS>();
     EPP_TL(4);
     // ---- phase 3: block-tridiagonal system over the inner vertices ----------------
     // free variable (v, p): vertex v in 1..M-1, derivative p+1.  Diagonal block D_v is
@@ -223,55 +280,68 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ P, int M, 
         }
         rhs[(v * 4 + p) * 3 + d] = -s;
     }
-    __syncthreads();
+    block_sync<SCR_LDS>();
     EPP_TL(5);
+    EPP_TLC(14);
     // ---- phase 4: block Cholesky solve (4x4 blocks, 3 right-hand sides) ---------------
-    // The inner vertices are eliminated in order (block Thomas) by one lane with every
-    // carried block in registers: per step v the Schur complement S_v = D_v - W_{v-1}^T
-    // W_{v-1}, z_v = b_v - W_{v-1}^T z_{v-1}, the Cholesky factor L_v of S_v and the
-    // forward solves z_v <- L_v^-1 z_v, W_v = L_v^-1 E_v; then x_v = L_v^-T (z_v - W_v
-    // x_{v+1}) backwards.  The step's inputs are loaded before the previous step's
-    // results are stored, FMAs throughout and Newton-refined reciprocals instead of
-    // divisions / square roots (within ~1e-15 of them): the chain is issue-bound, and a
-    // wave64 fp64 instruction costs the same whatever the active lanes.
-    if (tid == 0 && nin > 0) {
+    // The inner vertices are eliminated in order (block Thomas): per step v the Schur
+    // complement S_v = D_v - W_{v-1}^T W_{v-1}, z_v = b_v - W_{v-1}^T z_{v-1}, the Cholesky
+    // factor L_v of S_v and the forward solves z_v <- L_v^-1 z_v, W_v = L_v^-1 E_v; then
+    // x_v = L_v^-T (z_v - W_v x_{v+1}) backwards.  Seven lanes of the first wavefront own
+    // one column each of the seven column operations a step consists of: lanes 0..3 the
+    // columns of S (Schur update) and then of W (forward solve of E's column), lanes 4..6
+    // the columns of z; S is exchanged through LDS (`xch`) and every lane factors it
+    // redundantly in registers; W_v goes to LDS for the next step's Schur update.  Per
+    // entry the arithmetic is the single-lane elimination's (same FMAs in the same order),
+    // but a step is ~4x fewer dependent instructions.  Newton-refined reciprocal square
+    // roots instead of divisions / square roots (within ~1e-15 of them).
+    if (tid < 7 && nin > 0) {
+        const int c = tid;
+        const bool wcol = c < 4;  // else z column d = c - 4
+        const int d = c - 4;
+        double* xS = xch;       // S_v, row-major (p * 4 + q)
+        double* xW = xch + 16;  // W_{v-1}, row-major
         bool ok = true;
-        double Wp[16], zp[12];
-        double D[16], E[16], b[12];
-        auto load = [&](int v) {
+        double prev[4];  // this lane's column of step v-1: W_{v-1}[:, c] or z_{v-1}[:, d]
+        double base[4], ecol[4];  // step v's D_v[:, c] or b_v[:, d]; E_v[:, c]
+        auto load = [&](int v, double (&bs)[4], double (&ec)[4]) {
             const double* Sg = scr + (size_t)(v - 1) * Seg::kSize;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) D[i] = Sg[Seg::kL + i];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) E[i] = Sg[Seg::kW + i];
-#pragma unroll
-            for (int i = 0; i < 12; ++i) b[i] = rhs[(size_t)v * 12 + i];
-        };
-        load(1);
-        for (int v = 1; v <= nin; ++v) {
-            double L[16], inv[4], z[12], Wn[16];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) L[i] = D[i];
-#pragma unroll
-            for (int i = 0; i < 12; ++i) z[i] = b[i];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) Wn[i] = E[i];
-            if (v < nin) load(v + 1);  // independent of this step: in flight meanwhile
-            if (v > 1) {
-#pragma unroll
-                for (int p = 0; p < 4; ++p)
-#pragma unroll
-                    for (int q = 0; q <= p; ++q)
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) L[p * 4 + q] = fma(-Wp[k * 4 + p], Wp[k * 4 + q], L[p * 4 + q]);
-#pragma unroll
-                for (int p = 0; p < 4; ++p)
-#pragma unroll
-                    for (int d = 0; d < 3; ++d)
-#pragma unroll
-                        for (int k = 0; k < 4; ++k) z[p * 3 + d] = fma(-Wp[k * 4 + p], zp[k * 3 + d], z[p * 3 + d]);
+            for (int p = 0; p < 4; ++p) {
+                bs[p] = wcol ? Sg[Seg::kL + p * 4 + c] : rhs[((size_t)v * 4 + p) * 3 + d];
+                ec[p] = wcol ? Sg[Seg::kW + p * 4 + c] : 0.0;
             }
-            // Cholesky (lower triangle of L)
+        };
+        load(1, base, ecol);
+        for (int v = 1; v <= nin; ++v) {
+            EPP_TLI(v);
+            double col[4], e[4];
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                col[p] = base[p];
+                e[p] = ecol[p];
+            }
+            if (v < nin) load(v + 1, base, ecol);  // independent of this step: in flight meanwhile
+            if (v > 1) {
+                double Wp[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) Wp[i] = xW[i];
+#pragma unroll
+                for (int p = 0; p < 4; ++p)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) col[p] = fma(-Wp[k * 4 + p], prev[k], col[p]);
+            }
+            if (wcol) {
+#pragma unroll
+                for (int p = 0; p < 4; ++p) xS[p * 4 + c] = col[p];
+            }
+            if (v == 5) EPP_TLI(40);
+            wave_sync_lds();
+            if (v == 5) EPP_TLI(41);
+            // Cholesky of S (lower triangle), on every lane
+            double L[16], inv[4];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) L[i] = xS[i];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 double dd = L[j * 5];
@@ -289,78 +359,78 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ P, int M, 
                     L[i * 4 + j] = t * r;
                 }
             }
-            if (!ok) break;
-            // forward solves: z (3 columns) and, but for the last vertex, W (4 columns)
+            if (!ok) break;  // (the same on every lane)
+            if (v == 5) EPP_TLI(42);
+            // forward solve of this lane's column: E_v[:, c] -> W_v[:, c], or z
+            double x[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
+                double t = wcol ? e[i] : col[i];
 #pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    double t = z[i * 3 + c];
-#pragma unroll
-                    for (int k = 0; k < i; ++k) t = fma(-L[i * 4 + k], z[k * 3 + c], t);
-                    z[i * 3 + c] = t * inv[i];
-                }
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    double t = Wn[i * 4 + c];
-#pragma unroll
-                    for (int k = 0; k < i; ++k) t = fma(-L[i * 4 + k], Wn[k * 4 + c], t);
-                    Wn[i * 4 + c] = t * inv[i];
-                }
+                for (int k = 0; k < i; ++k) t = fma(-L[i * 4 + k], x[k], t);
+                x[i] = t * inv[i];
             }
             double* Sg = scr + (size_t)(v - 1) * Seg::kSize;
+            if (wcol) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) Sg[Seg::kL + i] = L[i];
+                for (int i = 0; i < 4; ++i) {
+                    Sg[Seg::kW + i * 4 + c] = x[i];
+                    xW[i * 4 + c] = x[i];
+                }
+            } else {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) Sg[Seg::kI + i] = inv[i];
+                for (int i = 0; i < 4; ++i) rhs[((size_t)v * 4 + i) * 3 + d] = x[i];
+            }
+            if (c == 0) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                Sg[Seg::kW + i] = Wn[i];
-                Wp[i] = Wn[i];
+                for (int i = 0; i < 16; ++i) Sg[Seg::kL + i] = L[i];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) Sg[Seg::kI + i] = inv[i];
             }
 #pragma unroll
-            for (int i = 0; i < 12; ++i) {
-                rhs[(size_t)v * 12 + i] = z[i];
-                zp[i] = z[i];
-            }
+            for (int i = 0; i < 4; ++i) prev[i] = x[i];
+            wave_sync_lds();
         }
-        if (ok) {
-            double xn[12];
+        // (W, L, z of every vertex written by other lanes of this wave: LDS or, for long
+        // tracks, global scratch — a workgroup-scope fence makes the latter visible)
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        wave_sync_lds();
+        if (ok && !wcol) {
+            // back substitution of column d: x_v = L_v^-T (z_v - W_v x_{v+1})
+            double xn[4];
+            EPP_TLI(32);
             for (int v = nin; v >= 1; --v) {
+                EPP_TLI(32 + nin + 1 - v);
                 const double* Sg = scr + (size_t)(v - 1) * Seg::kSize;
-                double x[12];
+                double x[4];
 #pragma unroll
-                for (int i = 0; i < 12; ++i) x[i] = rhs[(size_t)v * 12 + i];
-                if (v < nin) {  // z_v - W_v x_{v+1}
+                for (int i = 0; i < 4; ++i) x[i] = rhs[((size_t)v * 4 + i) * 3 + d];
+                if (v < nin) {
 #pragma unroll
                     for (int p = 0; p < 4; ++p)
 #pragma unroll
-                        for (int d = 0; d < 3; ++d)
-#pragma unroll
-                            for (int k = 0; k < 4; ++k) x[p * 3 + d] = fma(-Sg[Seg::kW + p * 4 + k], xn[k * 3 + d], x[p * 3 + d]);
+                        for (int k = 0; k < 4; ++k) x[p] = fma(-Sg[Seg::kW + p * 4 + k], xn[k], x[p]);
                 }
 #pragma unroll
-                for (int i = 3; i >= 0; --i)
+                for (int i = 3; i >= 0; --i) {
+                    double t = x[i];
 #pragma unroll
-                    for (int d = 0; d < 3; ++d) {
-                        double t = x[i * 3 + d];
+                    for (int k = i + 1; k < 4; ++k) t = fma(-Sg[Seg::kL + k * 4 + i], x[k], t);
+                    x[i] = t * Sg[Seg::kI + i];
+                }
 #pragma unroll
-                        for (int k = i + 1; k < 4; ++k) t = fma(-Sg[Seg::kL + k * 4 + i], x[k * 3 + d], t);
-                        x[i * 3 + d] = t * Sg[Seg::kI + i];
-                    }
-#pragma unroll
-                for (int i = 0; i < 12; ++i) xn[i] = x[i];
-#pragma unroll
-                for (int p = 0; p < 4; ++p)
-#pragma unroll
-                    for (int d = 0; d < 3; ++d) dv[(v * HALF + 1 + p) * 3 + d] = x[p * 3 + d];
+                for (int i = 0; i < 4; ++i) {
+                    xn[i] = x[i];
+                    dv[((size_t)v * HALF + 1 + i) * 3 + d] = x[i];
+                }
             }
-        } else {
-            *s_err = 1;
         }
+        if (!ok && c == 0) *s_err = 1;
+        EPP_TLI(63);
     }
-    __syncthreads();
+    block_sync<SCR_LDS>();
     EPP_TL(6);
+    EPP_TLC(15);
     if (*s_err) return -3;
     // ---- phase 5: p_i = A_i^-1 [d_i ; d_{i+1}] -------------------------------------
     for (int e = tid; e < M * 30; e += BLOCK) {
@@ -386,11 +456,13 @@ __global__ __launch_bounds__(BLOCK) void k_minsnap(const double* __restrict__ wp
                                                    const double* __restrict__ a0, const double* __restrict__ times_in,
                                                    double* __restrict__ seg_times, double* __restrict__ coeffs,
                                                    int32_t* __restrict__ status, double* __restrict__ gscratch) {
-    // one dynamic LDS array (cdna_hip_programming.md Guideline 17); the first 16 bytes
-    // hold the error flag
+    // one dynamic LDS array (cdna_hip_programming.md Guideline 17): the error flag (16
+    // bytes), the constants, then the solve's scratch
     extern __shared__ __attribute__((aligned(16))) double smem[];
     int* s_err = reinterpret_cast<int*>(smem);
-    double* sm = smem + 2;
+    double* kc = smem + 2;
+    double* sm = kc + kNC;
+    stage_consts<BLOCK>(kc);
     const int track = blockIdx.x;
     if (track >= n_tracks) return;
     const int w0 = wp_off[track];
@@ -407,9 +479,9 @@ __global__ __launch_bounds__(BLOCK) void k_minsnap(const double* __restrict__ wp
     double* rhs = dv + (size_t)(M + 1) * 15;
     double* Tm = rhs + (size_t)(M + 1) * 12;
     __syncthreads();
-    const int st = solve_track<BLOCK>(wp + (size_t)w0 * 3, M, vmax, amax, v0 ? v0 + 3 * track : nullptr,
+    const int st = solve_track<BLOCK, LDS>(kc, wp + (size_t)w0 * 3, M, vmax, amax, v0 ? v0 + 3 * track : nullptr,
                                       a0 ? a0 + 3 * track : nullptr, times_in ? times_in + seg0 : nullptr, scr, dv, rhs,
-                                      Tm, s_err, seg_times + seg0, coeffs + (size_t)seg0 * 30);
+                                      Tm, Tm + M, s_err, seg_times + seg0, coeffs + (size_t)seg0 * 30);
     if (threadIdx.x == 0 && status) status[track] = st;
 }
 
@@ -515,9 +587,9 @@ __global__ __launch_bounds__(kWave) void k_sample_count(const double* __restrict
 // Polynomial::evaluate(t, k) — polynomial.h:136-149
 // (Horner with fused multiply-adds: the sampled values are compared at 1e-6, the time
 // column, which does not go through here, exactly)
-__device__ __forceinline__ double poly_eval(const double* c, double t, int k) {
-    double r = cB[k][N - 1] * c[N - 1];
-    for (int j = N - 2; j >= k; --j) r = fma(r, t, cB[k][j] * c[j]);
+__device__ __forceinline__ double poly_eval(const double* B, const double* c, double t, int k) {
+    double r = B[k * N + N - 1] * c[N - 1];
+    for (int j = N - 2; j >= k; --j) r = fma(r, t, B[k * N + j] * c[j]);
     return r;
 }
 
@@ -531,12 +603,14 @@ __global__ __launch_bounds__(kWave) void k_sample_rows(const double* __restrict_
     // one dynamic LDS array (Guideline 17): [T (M) | tin | tac | seg (kRowChunk each) | cnt, done]
     // lane 0 runs the sequential time recurrence for kRowChunk samples at a time, then the
     // wave evaluates them (fewer barriers / coefficient-load round trips than 64 a round)
-    extern __shared__ __attribute__((aligned(16))) double sm[];
+    extern __shared__ __attribute__((aligned(16))) double smB[];  // [B (kNC block) | ...]
     const int t = blockIdx.x;
     if (t >= n_tracks) return;
     const int lane = threadIdx.x;
     const int M = wp_off[t + 1] - wp_off[t] - 1;
     if (M < 1 || !(dt > 0)) return;
+    stage_consts<kWave>(smB);
+    double* sm = smB + kNC;
     const int seg0 = wp_off[t] - t;
     double* sT = sm;
     double* s_tin = sT + ((M + 1) & ~1);
@@ -589,7 +663,7 @@ __global__ __launch_bounds__(kWave) void k_sample_rows(const double* __restrict_
             const double tin = s_tin[j];
             double* row = out + (base + j) * 10;
             for (int d = 0; d < 3; ++d)
-                for (int k = 0; k < 3; ++k) row[3 * d + k] = poly_eval(cs + d * N, tin, k);
+                for (int k = 0; k < 3; ++k) row[3 * d + k] = poly_eval(smB + kCB, cs + d * N, tin, k);
             row[9] = s_tac[j] + toff;  // sampling_times[i] + startTimeOffset
         }
         base += cnt;
@@ -603,93 +677,77 @@ __global__ __launch_bounds__(kWave) void k_sample_rows(const double* __restrict_
 // writing the rows to pinned host memory (no copies).  The host has already run the two
 // sequential parts, which a GPU lane runs slowly (~65 ns per dependent step): the segment
 // times (Nfabian with the host's libm, as the reference) and Trajectory::evaluateRange's
-// `acc += dt` recurrence (sample times and segments, exact).
-//   workgroup 0        solves the min-snap problem with those times (solve_track) and
-//                      publishes the coefficients (device memory) and its status;
-//   workgroups 1..G    each own a slice of the rows: they fetch its sample data from the
-//                      host while workgroup 0 solves, wait for the coefficients, evaluate
-//                      the rows (Polynomial::evaluate) and write them to the host — G CUs
-//                      writing in parallel instead of one (one CU's PCIe writes are slow).
-// Completion is published in host memory (workgroup 0: the status; writers: their slot)
-// and polled by the host instead of synchronising the stream.
+// `acc += dt` recurrence (sample times and segments, exact).  G workgroups each own a
+// slice of the rows; every one of them solves the (small) min-snap problem itself with
+// those times (solve_track — the same arithmetic, so the same coefficients) while its
+// slice's sample data arrives from the host, then evaluates its rows
+// (Polynomial::evaluate) and writes them to the host: G CUs writing in parallel (one CU's
+// PCIe writes are slow) and no hand-off of the coefficients between workgroups.
+// Completion is published in host memory (workgroup 0: the status; every workgroup: its
+// slot) and polled by the host instead of synchronising the stream.
 constexpr int kRefitArgW = 41;  // tracks up to this many waypoints pass wp, v0, a0, T as kernel arguments
 constexpr int kRefitMaxWriters = 16;
 struct RefitArgs {
     const double* in;  // host-mapped: [wp (W x 3) | v0 (3) | a0 (3) | T (M)] | t_in (R) | t (R) | segment (R, int32)
     int32_t W;
     int32_t R;         // rows
-    int32_t writers;   // G
+    int32_t writers;   // G (>= 1)
     uint32_t seq;      // this call's number (completion words hold it)
     double t0;         // startTimeOffset
     double* out;       // host-mapped: R x 10 rows
     int64_t* info;     // host-mapped: [status]
-    uint32_t* done;    // host-mapped: the writers' completion slots
-    double* coef;      // device: M x 30 coefficients (workgroup 0 -> writers)
-    uint32_t* flag;    // device: [seq of the published coefficients, status]
-    double* scratch;   // device: segment scratch (tracks longer than kMaxLdsSeg)
+    uint32_t* done;    // host-mapped: the workgroups' completion slots
+    double* scratch;   // device: G x segment scratch (tracks longer than kMaxLdsSeg)
     double small[3 * kRefitArgW + 6 + kRefitArgW - 1];  // wp | v0 | a0 | T when W <= kRefitArgW
 };
 constexpr int kRefitBlock = 256;
-constexpr int kRefitRowChunk = 128;  // rows per writer round (LDS staged)
-__host__ __device__ inline size_t refit_in_doubles(int W, int R) {
-    return (size_t)3 * W + 6 + (W - 1) + 2 * (size_t)R + ((size_t)R + 1) / 2;
+constexpr int kRefitRowChunk = 128;  // rows per round (LDS staged)
+__host__ __device__ inline size_t refit_in_doubles(int W, int R) {  // (+ 3: row 0 readable when R = 0)
+    return (size_t)3 * W + 6 + (W - 1) + 2 * (size_t)R + ((size_t)R + 1) / 2 + 3;
 }
-// LDS doubles of the solver: flag (2) | wp, v0, a0, T | solve scratch | coefficients; of a
-// writer: coefficients | sample chunk (t_in, t, segment) | row chunk
+__host__ __device__ inline size_t refit_nin_even(int W) { return ((size_t)3 * W + 6 + (W - 1) + 1) & ~size_t(1); }
+// LDS doubles: flag (2) | constants | wp, v0, a0, T | solve scratch | coefficients |
+// sample chunk (t_in, t, segment) | row chunk
 __host__ __device__ inline size_t refit_lds_doubles(int M, bool lds) {
-    const size_t solver = 2 + (((size_t)3 * (M + 1) + 6 + M + 1) & ~size_t(1)) + (lds ? (size_t)M * Seg::kSize : 0) +
-                          vertex_doubles(M) + (size_t)M * 30;
-    const size_t writer = (size_t)M * 30 + 2 + (size_t)kRefitRowChunk * 3 + (size_t)kRefitRowChunk * 10;
-    return solver > writer ? solver : writer;
+    return 2 + kNC + refit_nin_even(M + 1) + (lds ? (size_t)M * Seg::kSize : 0) + vertex_doubles(M) + (size_t)M * 30 +
+           (size_t)kRefitRowChunk * 3 + 2 + (size_t)kRefitRowChunk * 10;
 }
 
 template <bool LDS>
 __global__ __launch_bounds__(kRefitBlock) void k_refit(RefitArgs a) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int tid = threadIdx.x, W = a.W, M = W - 1, R = a.R;
+    const int tid = threadIdx.x, W = a.W, M = W - 1, R = a.R, g = blockIdx.x;
     const double* h_tin = a.in + 3 * W + 6 + M;
     const double* h_tac = h_tin + R;
     const int32_t* h_seg = reinterpret_cast<const int32_t*>(h_tac + R);
-    if (blockIdx.x == 0) {  // ---- the solver ----
-        int* s_err = reinterpret_cast<int*>(smem);
-        EPP_TL(0);
-        double* P = smem + 2;  // wp | v0 | a0 | T
-        const int nin = 3 * W + 6 + M;
-        const double* src = W <= kRefitArgW ? a.small : a.in;  // kernel arguments or host memory
-        for (int e = tid; e < nin; e += kRefitBlock) P[e] = src[e];
-        if (tid == 0) *s_err = 0;
-        double* rest = smem + 2 + (((size_t)nin + 1) & ~size_t(1));
-        double* scr = LDS ? rest : a.scratch;
-        double* dv = LDS ? rest + (size_t)M * Seg::kSize : rest;
-        double* rhs = dv + (size_t)(M + 1) * 15;
-        double* Tm = rhs + (size_t)(M + 1) * 12;
-        double* C = Tm + M;  // coefficients (M x 3 x 10)
-        __syncthreads();
-        const int st = solve_track<kRefitBlock>(P, M, 0.0, 0.0, P + 3 * W, P + 3 * W + 3, P + 3 * W + 6, scr, dv,
-                                                rhs, Tm, s_err, nullptr, C);
-        EPP_TL(7);
-        __syncthreads();  // coefficients complete
-        for (int e = tid; e < M * 30; e += kRefitBlock) a.coef[e] = C[e];
-        __threadfence();  // (every storing wave) -> the barrier -> the release below
-        __syncthreads();
-        if (tid == 0) {
-            a.flag[1] = (uint32_t)st;
-            __hip_atomic_store(a.flag, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a.info, (int64_t)st, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        EPP_TL(11);
-        return;
-    }
-    // ---- a row writer: rows [r0, r1) ----
-    const int g = blockIdx.x - 1;
-    const int per = (R + a.writers - 1) / a.writers;
-    const int r0 = min(R, g * per), r1 = min(R, r0 + per);
-    double* C = smem;
-    double* s_tin = C + (size_t)M * 30 + 2;
+    int* s_err = reinterpret_cast<int*>(smem);
+    double* kc = smem + 2;
+    double* P = kc + kNC;  // wp | v0 | a0 | T
+    double* scr = P + refit_nin_even(W);
+    double* dv = LDS ? scr + (size_t)M * Seg::kSize : scr;
+    if (!LDS) scr = a.scratch + (size_t)g * M * Seg::kSize;
+    double* rhs = dv + (size_t)(M + 1) * 15;
+    double* Tm = rhs + (size_t)(M + 1) * 12;
+    double* C = Tm + M + kXch;  // coefficients (M x 3 x 10)
+    double* s_tin = C + (size_t)M * 30;
     double* s_tac = s_tin + kRefitRowChunk;
     int32_t* s_seg = reinterpret_cast<int32_t*>(s_tac + kRefitRowChunk);
     double* rbuf = reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(s_tac + 2 * kRefitRowChunk) + 15) &
                                              ~uintptr_t(15));
+    const int per = (R + a.writers - 1) / a.writers;
+    const int r0 = min(R, g * per), r1 = min(R, r0 + per);
+    EPP_TL(0);
+    // every input load in flight at once: the constants, the problem (kernel arguments or
+    // host memory) and this slice's first sample chunk (host memory)
+    // (unconditional loads at clamped addresses: no branches, so the stores below wait
+    // with counted vmcnt for their own loads only and the host reads stay in flight)
+    const int nin = 3 * W + 6 + M;
+    const double* src = W <= kRefitArgW ? a.small : a.in;
+    const double cv = cC[min(tid, kNC - 1)];
+    double pv[(3 * kRefitArgW + 6 + kRefitArgW - 1 + kRefitBlock - 1) / kRefitBlock];
+    constexpr int kPv = sizeof(pv) / sizeof(double);
+#pragma unroll
+    for (int q = 0; q < kPv; ++q) pv[q] = src[min(tid + q * kRefitBlock, nin - 1)];
     auto fetch = [&](int c0, int cnt) {  // sample data of rows [c0, c0 + cnt) (host reads)
         if (tid < cnt) {
             s_tin[tid] = h_tin[c0 + tid];
@@ -697,31 +755,37 @@ __global__ __launch_bounds__(kRefitBlock) void k_refit(RefitArgs a) {
             s_seg[tid] = h_seg[c0 + tid];
         }
     };
-    fetch(r0, min(kRefitRowChunk, r1 - r0));  // in flight while workgroup 0 solves
-    __shared__ uint32_t s_status;
-    if (tid == 0) {
-        // wait for workgroup 0's coefficients (bounded: ~0.5 s, then give up as failed)
-        uint32_t st = 1u;
-        for (uint32_t it = 0; it < (1u << 22); ++it) {
-            if (__hip_atomic_load(a.flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == a.seq) {
-                st = __hip_atomic_load(a.flag + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        s_status = st;
+    // the first chunk's sample data is loaded now and kept in registers until the solve
+    // is done (the host pads the input so row 0 is readable even when R = 0)
+    const int cnt0 = min(kRefitRowChunk, r1 - r0);
+    const int fr = r0 + min(tid, max(cnt0 - 1, 0));
+    const double f_tin = h_tin[fr], f_tac = h_tac[fr];
+    const int32_t f_seg = h_seg[fr];
+    if (tid < kNC) kc[tid] = cv;
+#pragma unroll
+    for (int q = 0; q < kPv; ++q)
+        if (tid + q * kRefitBlock < nin) P[tid + q * kRefitBlock] = pv[q];
+    for (int e = kPv * kRefitBlock + tid; e < nin; e += kRefitBlock) P[e] = src[e];  // (long tracks)
+    if (tid == 0) *s_err = 0;
+    block_sync<LDS>();
+    EPP_TL(8);
+    const int st = solve_track<kRefitBlock, LDS>(kc, P, M, 0.0, 0.0, P + 3 * W, P + 3 * W + 3, P + 3 * W + 6, scr, dv,
+                                            rhs, Tm, Tm + M, s_err, nullptr, C);
+    EPP_TL(7);
+    if (tid < cnt0) {
+        s_tin[tid] = f_tin;
+        s_tac[tid] = f_tac;
+        s_seg[tid] = f_seg;
     }
-    __syncthreads();
-    EPP_TL(12);
-    if (s_status == 0) {
-        for (int e = tid; e < M * 30; e += kRefitBlock) C[e] = a.coef[e];
+    __syncthreads();  // coefficients complete
+    if (st == 0) {
         for (int c0 = r0; c0 < r1; c0 += kRefitRowChunk) {
             const int cnt = min(kRefitRowChunk, r1 - c0);
             if (c0 != r0) {
                 __syncthreads();  // the previous chunk copied out
                 fetch(c0, cnt);
+                __syncthreads();
             }
-            __syncthreads();
             if (tid < cnt) {
                 const double* cs = C + (size_t)s_seg[tid] * 30;
                 const double tin = s_tin[tid];
@@ -729,7 +793,7 @@ __global__ __launch_bounds__(kRefitBlock) void k_refit(RefitArgs a) {
 #pragma unroll
                 for (int d = 0; d < 3; ++d)
 #pragma unroll
-                    for (int q = 0; q < 3; ++q) r[3 * d + q] = poly_eval(cs + d * N, tin, q);
+                    for (int q = 0; q < 3; ++q) r[3 * d + q] = poly_eval(kc + kCB, cs + d * N, tin, q);
                 r[9] = s_tac[tid] + a.t0;  // sampling_times[i] + startTimeOffset
             }
             __syncthreads();
@@ -740,10 +804,14 @@ __global__ __launch_bounds__(kRefitBlock) void k_refit(RefitArgs a) {
         }
     }
     EPP_TL(13);
-    // completion: this slice's rows are visible system-wide before the slot is
+    // completion: this slice's rows (and workgroup 0's status) are visible system-wide
+    // before the slot is
     __threadfence_system();
     __syncthreads();
-    if (tid == 0) __hip_atomic_store(a.done + g, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid == 0) {
+        if (g == 0) __hip_atomic_store(a.info, (int64_t)st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.done + g, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 bool g_consts_ready[64];
@@ -791,9 +859,17 @@ epp_status ensure_consts() {
     }
     for (int r = 0; r < HALF; ++r)
         for (int c = 0; c < HALF; ++c) B5inv[r][c] = (double)G[r][HALF + c];
-    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(cB), B, sizeof(B));
-    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(cB5inv), B5inv, sizeof(B5inv));
-    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(cK), K, sizeof(K));
+    double cc[kNC] = {};
+    for (int k = 0; k < N; ++k)
+        for (int j = 0; j < N; ++j) cc[kCB + k * N + j] = B[k][j];
+    for (int r = 0; r < HALF; ++r)
+        for (int c = 0; c < HALF; ++c) {
+            cc[kCB5 + r * HALF + c] = B5inv[r][c];
+            cc[kCK + r * HALF + c] = K[r][c];
+        }
+    const double inv_fact[HALF] = {1.0, 1.0, 1.0 / 2.0, 1.0 / 6.0, 1.0 / 24.0};
+    for (int r = 0; r < HALF; ++r) cc[kCF + r] = inv_fact[r];
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(cC), cc, sizeof(cc));
     if (e != hipSuccess) {
         set_error(std::string("epp minsnap: constants: ") + hipGetErrorString(e));
         return EPP_ERR_HIP;
@@ -850,7 +926,7 @@ epp_status minsnap_batch(const double* wp, const int32_t* wp_offsets, int32_t n_
     if ((st = read_offsets(wp_offsets, n_tracks, s, what, &max_m, &total_m))) return st;
     constexpr int kB = 64;  // one wavefront per track: the batch is throughput-bound
     if (max_m <= kMaxLdsSeg) {
-        const size_t shm = ((size_t)max_m * Seg::kSize + vertex_doubles(max_m) + 2) * sizeof(double);
+        const size_t shm = ((size_t)max_m * Seg::kSize + vertex_doubles(max_m) + 2 + kNC) * sizeof(double);
         hipLaunchKernelGGL((k_minsnap<kB, true>), dim3(n_tracks), dim3(kB), shm, s, wp, wp_offsets, n_tracks, v_max,
                            a_max, v0, a0, times_in, seg_times, coeffs, status, nullptr);
         return launch_error(what);
@@ -866,7 +942,7 @@ epp_status minsnap_batch(const double* wp, const int32_t* wp_offsets, int32_t n_
         set_error(std::string(what) + ": workspace: " + hipGetErrorString(e));
         return EPP_ERR_HIP;
     }
-    const size_t shm = (vertex_doubles(max_m) + 2) * sizeof(double);
+    const size_t shm = (vertex_doubles(max_m) + 2 + kNC) * sizeof(double);
     hipLaunchKernelGGL((k_minsnap<kB, false>), dim3(n_tracks), dim3(kB), shm, s, wp, wp_offsets, n_tracks, v_max, a_max,
                        v0, a0, times_in, seg_times, coeffs, status, static_cast<double*>(ws.buf));
     st = launch_error(what);
@@ -875,8 +951,7 @@ epp_status minsnap_batch(const double* wp, const int32_t* wp_offsets, int32_t n_
 }
 
 // Per-host-thread state of the single-track latency path: a stream, pinned host buffers
-// the kernel reads / writes directly, the device segment scratch of long tracks and the
-// coefficient hand-off (workgroup 0 -> row writers) with its flag.
+// the kernel reads / writes directly and the device segment scratch of long tracks.
 struct RefitCache {
     hipStream_t s = nullptr;
     int dev = -1;
@@ -884,9 +959,8 @@ struct RefitCache {
     size_t in_cap = 0;
     char* h_out = nullptr;  // [status (8 B) | pad | writer slots (64 B) | rows (at +128)]
     size_t out_cap = 0;
-    double* d_scr = nullptr;  // coefficients (kMaxCoef doubles... grown) then segment scratch
+    double* d_scr = nullptr;  // segment scratch (one per workgroup) of long tracks
     size_t scr_cap = 0;
-    uint32_t* d_flag = nullptr;  // [seq, status], zeroed once
     uint32_t seq = 0;
     std::vector<double> T, tin, tac;  // host side of the refit: times and samples
     std::vector<int32_t> seg;
@@ -895,12 +969,10 @@ struct RefitCache {
         if (h_in) (void)hipHostFree(h_in);
         if (h_out) (void)hipHostFree(h_out);
         if (d_scr) (void)hipFree(d_scr);
-        if (d_flag) (void)hipFree(d_flag);
         if (s) (void)hipStreamDestroy(s);
         h_in = nullptr;
         h_out = nullptr;
         d_scr = nullptr;
-        d_flag = nullptr;
         s = nullptr;
         in_cap = out_cap = scr_cap = 0;
         seq = 0;
@@ -913,11 +985,6 @@ struct RefitCache {
         dev = d;
         hipError_t e = hipSuccess;
         if (!s) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-        if (e == hipSuccess && !d_flag) {
-            e = hipMalloc(reinterpret_cast<void**>(&d_flag), 16);
-            if (e == hipSuccess) e = hipMemset(d_flag, 0, 16);
-            if (e == hipSuccess) e = hipDeviceSynchronize();
-        }
         auto grow_host = [&](auto*& p, size_t& cap, size_t need) {
             if (e != hipSuccess || need <= cap) return;
             if (s) (void)hipStreamSynchronize(s);  // (the previous call's kernel has ended)
@@ -997,7 +1064,7 @@ epp_status epp_sample_batch(const double* seg_times, const double* coeffs, const
     if (st) return st;
     int max_m = 0;
     if ((st = read_offsets(wp_offsets, n_tracks, (hipStream_t)stream, "epp_sample_batch", &max_m, nullptr))) return st;
-    const size_t shm = ((size_t)((max_m + 1) & ~1) + 3 * kRowChunk + 2) * 8;
+    const size_t shm = ((size_t)kNC + ((max_m + 1) & ~1) + 3 * kRowChunk + 2) * 8;
     hipLaunchKernelGGL(k_sample_rows, dim3(n_tracks), dim3(kWave), shm, (hipStream_t)stream, seg_times, coeffs,
                        wp_offsets, n_tracks, dt, t0, row_offsets, rows, (int64_t)INT64_MAX);
     return launch_error("epp_sample_batch");
@@ -1050,9 +1117,9 @@ epp_status generate_trajectory(const double* wp, int32_t n_wp, const double* tim
     }
     const int R = (int)c.tin.size();
     const bool lds = M <= kMaxLdsSeg;
-    const size_t coef_b = ((size_t)M * 30 * 8 + 255) & ~size_t(255);
+    const int G = R ? std::min(kRefitMaxWriters, (R + kRefitRowChunk - 1) / kRefitRowChunk) : 1;
     if ((rc = c.ensure(refit_in_doubles(n_wp, R) * 8, (size_t)R * 80 + 128,
-                       coef_b + (lds ? 0 : (size_t)M * Seg::kSize * 8))))
+                       lds ? 0 : (size_t)G * M * Seg::kSize * 8)))
         return rc;
     double* in = c.h_in;
     std::memcpy(in, wp, (size_t)n_wp * 24);
@@ -1071,7 +1138,7 @@ epp_status generate_trajectory(const double* wp, int32_t n_wp, const double* tim
     a.in = in;
     a.W = n_wp;
     a.R = R;
-    a.writers = R ? std::min(kRefitMaxWriters, (R + kRefitRowChunk - 1) / kRefitRowChunk) : 0;
+    a.writers = G;
     if (++c.seq == 0) c.seq = 1;
     a.seq = c.seq;
     a.t0 = t0;
@@ -1079,15 +1146,13 @@ epp_status generate_trajectory(const double* wp, int32_t n_wp, const double* tim
     a.info = reinterpret_cast<int64_t*>(c.h_out);
     a.done = reinterpret_cast<uint32_t*>(c.h_out + 64);
     a.out = reinterpret_cast<double*>(c.h_out + 128);
-    a.coef = c.d_scr;
-    a.flag = c.d_flag;
-    a.scratch = c.d_scr + coef_b / 8;
+    a.scratch = c.d_scr;
     a.info[0] = -100;
     const size_t shm = refit_lds_doubles(M, lds) * sizeof(double);
-    if (lds) hipLaunchKernelGGL(k_refit<true>, dim3(1 + a.writers), dim3(kRefitBlock), shm, c.s, a);
-    else hipLaunchKernelGGL(k_refit<false>, dim3(1 + a.writers), dim3(kRefitBlock), shm, c.s, a);
+    if (lds) hipLaunchKernelGGL(k_refit<true>, dim3(G), dim3(kRefitBlock), shm, c.s, a);
+    else hipLaunchKernelGGL(k_refit<false>, dim3(G), dim3(kRefitBlock), shm, c.s, a);
     hipError_t e = hipGetLastError();
-    // wait for the status word and every writer's slot (polled; the stream is queried
+    // wait for the status word and every workgroup's slot (polled; the stream is queried
     // every ~1k polls so a failed launch ends the wait)
     auto complete = [&]() {
         if (__atomic_load_n(a.info, __ATOMIC_ACQUIRE) == -100) return false;
@@ -1144,7 +1209,9 @@ epp_status epp_generate_trajectory_times_host(const double* wp, int32_t n_wp, co
 #ifdef EPP_REFIT_TL
 // diagnostics builds only: the last refit's phase timeline (2 workgroups x 16 stamps)
 epp_status epp_dbg_refit_tl(unsigned long long* out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_refit_tl), sizeof(g_refit_tl)) == hipSuccess ? EPP_OK : EPP_ERR_HIP;
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_refit_tl), sizeof(g_refit_tl));
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(out + 32, HIP_SYMBOL(g_refit_it), sizeof(g_refit_it));
+    return e == hipSuccess ? EPP_OK : EPP_ERR_HIP;
 }
 #endif
 

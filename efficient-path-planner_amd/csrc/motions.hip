@@ -658,7 +658,11 @@ epp_status epp_check_motions(const epp_world* world, const double* s1, const dou
     }
     if (n == 0) return EPP_OK;
     const SmallWorld sw = small_world(world);
-    if (small_motions(sw, n)) return launch_motions_small(sw, mode, s1, s2, n, can_pass_gate, valid, (hipStream_t)stream);
+    if (small_motions(sw, n)) {
+        if (const epp_status st = launch_motions_small(sw, mode, s1, s2, n, can_pass_gate, valid, (hipStream_t)stream))
+            return st;
+        return note_record_reader(world, sw, (hipStream_t)stream);
+    }
     if (const epp_status st = ensure_index(world)) return st;
     const WorldView& w = world_view(world);
     hipStream_t st = (hipStream_t)stream;

@@ -33,42 +33,93 @@ __device__ __forceinline__ void publish_done(uint32_t* done, uint32_t seq) {
     if (threadIdx.x == 0) __hip_atomic_store(done + blockIdx.x, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__device__ __forceinline__ void stage_records(double* srec, const double* recs, int nd) {
-    // four loads in flight per lane (the records may be in host memory: PCIe latency)
-    for (int e = threadIdx.x; e < nd; e += 4 * kSmallBlock) {
-        double v[4];
+// The records (n_obb x kRecDoubles doubles, 16-byte aligned start) into LDS: every 16-byte load
+// of up to 128 OBBs in flight at once (the records may be in host memory: one PCIe round
+// trip instead of one per few loads); `before` runs between the loads and the stores
+// (the caller issues its own loads there, so they overlap too).
+template <typename F>
+__device__ __forceinline__ void stage_records(double* srec, const double* recs, int nd, F&& before) {
+    constexpr int kQ = (128 * kRecDoubles / 2 + kSmallBlock - 1) / kSmallBlock;  // 16-byte loads per lane
+    const int n2 = nd / 2;
+    const double2* s2 = reinterpret_cast<const double2*>(recs);
+    double2* d2 = reinterpret_cast<double2*>(srec);
+    double2 v[kQ];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = e + q * kSmallBlock < nd ? recs[e + q * kSmallBlock] : 0.0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            if (e + q * kSmallBlock < nd) srec[e + q * kSmallBlock] = v[q];
+    for (int q = 0; q < kQ; ++q) {
+        const int e = threadIdx.x + q * kSmallBlock;
+        v[q] = e < n2 ? s2[e] : make_double2(0.0, 0.0);
     }
+    before();
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+        const int e = threadIdx.x + q * kSmallBlock;
+        if (e < n2) d2[e] = v[q];
+    }
+    for (int e = threadIdx.x + kQ * kSmallBlock; e < n2; e += kSmallBlock) d2[e] = s2[e];  // (> 128 OBBs)
+    if ((nd & 1) && threadIdx.x == 0) srec[nd - 1] = recs[nd - 1];  // (odd OBB count: 136-byte records)
 }
+
+// A workgroup takes `per` queries (64, 128 or 256) and splits the OBB list into
+// kSmallBlock / per slices, one per group of `per` threads: the few hundred queries of a
+// latency-path call keep every wave of the workgroup busy, and each wave walks a shorter
+// list.  A slice's hit marks the query's LDS flag; slice 0 writes the answers.
+__host__ __device__ inline int small_per(int64_t n) { return n <= 64 ? 64 : (n <= 128 ? 128 : kSmallBlock); }
+__host__ __device__ inline size_t small_shm(int n_obb) { return (((size_t)n_obb * kRecDoubles + 1) & ~size_t(1)) * 8 + kSmallBlock * 4; }
 
 template <bool MINDIST, bool COMPACT>
 __global__ __launch_bounds__(kSmallBlock) void k_states_small(const double* __restrict__ recs, int n_obb, double rg,
                                                               double ro, const double* __restrict__ xyz, int64_t n,
-                                                              int can_pass, double md, uint8_t* __restrict__ valid,
+                                                              int per, int can_pass, double md,
+                                                              uint8_t* __restrict__ valid,
                                                               int32_t* __restrict__ compact_idx,
                                                               unsigned long long* __restrict__ n_valid,
                                                               uint32_t* done, uint32_t seq) {
     extern __shared__ double srec[];
-    stage_records(srec, recs, n_obb * kRecDoubles);
-    const int64_t i = (int64_t)blockIdx.x * kSmallBlock + threadIdx.x;
+    uint32_t* s_hit = reinterpret_cast<uint32_t*>(srec + (((size_t)n_obb * kRecDoubles + 1) & ~size_t(1)));
+    const int t = threadIdx.x, slices = kSmallBlock / per, slice = t / per, j = t - slice * per;
+    const int64_t i = (int64_t)blockIdx.x * per + j;
     const bool act = i < n;
-    const double px = act ? xyz[3 * i] : 0.0, py = act ? xyz[3 * i + 1] : 0.0, pz = act ? xyz[3 * i + 2] : 0.0;
+    double px = 0.0, py = 0.0, pz = 0.0;
+    stage_records(srec, recs, n_obb * kRecDoubles, [&] {
+        if (act) {
+            px = xyz[3 * i];
+            py = xyz[3 * i + 1];
+            pz = xyz[3 * i + 2];
+        }
+    });
+    if (t < per) s_hit[t] = 0u;
     __syncthreads();
+    const int o0 = (int)((int64_t)slice * n_obb / slices), o1 = (int)((int64_t)(slice + 1) * n_obb / slices);
+    const bool cp = can_pass != 0;
+    // rtree contains(point): strict  src/World.cpp:83
+    auto inside = [&](const double* r) {
+        return act & (r[F_LOX] < px) & (px < r[F_HIX]) & (r[F_LOY] < py) & (py < r[F_HIY]) & (r[F_LOZ] < pz) &
+               (pz < r[F_HIZ]);
+    };
     bool hit = false;
-    for (int o = 0; o < n_obb; ++o) {
+    int o = o0;
+    for (; o + 4 <= o1; o += 4) {  // four records' AABB tests before any branch (their LDS reads overlap)
         const double* r = srec + (size_t)o * kRecDoubles;
-        // rtree contains(point): strict  src/World.cpp:83
-        const bool in = act & (r[F_LOX] < px) & (px < r[F_HIX]) & (r[F_LOY] < py) & (py < r[F_HIY]) &
-                        (r[F_LOZ] < pz) & (pz < r[F_HIZ]);
-        if (__builtin_amdgcn_ballot_w64(in)) hit |= in && rec_hit<MINDIST>(r, rg, ro, px, py, pz, can_pass != 0, md);
+        const bool in0 = inside(r), in1 = inside(r + kRecDoubles), in2 = inside(r + 2 * kRecDoubles),
+                   in3 = inside(r + 3 * kRecDoubles);
+        if (__builtin_amdgcn_ballot_w64(in0 | in1 | in2 | in3)) {
+            hit |= in0 && rec_hit<MINDIST>(r, rg, ro, px, py, pz, cp, md);
+            hit |= in1 && rec_hit<MINDIST>(r + kRecDoubles, rg, ro, px, py, pz, cp, md);
+            hit |= in2 && rec_hit<MINDIST>(r + 2 * kRecDoubles, rg, ro, px, py, pz, cp, md);
+            hit |= in3 && rec_hit<MINDIST>(r + 3 * kRecDoubles, rg, ro, px, py, pz, cp, md);
+        }
     }
-    if (act) {
-        valid[i] = hit ? 0 : 1;
-        if (COMPACT && !hit) compact_idx[atomicAdd(n_valid, 1ull)] = (int32_t)i;
+    for (; o < o1; ++o) {
+        const double* r = srec + (size_t)o * kRecDoubles;
+        const bool in = inside(r);
+        if (__builtin_amdgcn_ballot_w64(in)) hit |= in && rec_hit<MINDIST>(r, rg, ro, px, py, pz, cp, md);
+    }
+    if (hit) s_hit[j] = 1u;
+    __syncthreads();
+    if (slice == 0 && act) {
+        const bool ok = s_hit[j] == 0u;
+        valid[i] = ok ? 1 : 0;
+        if (COMPACT && ok) compact_idx[atomicAdd(n_valid, 1ull)] = (int32_t)i;
     }
     publish_done(done, seq);
 }
@@ -76,37 +127,62 @@ __global__ __launch_bounds__(kSmallBlock) void k_states_small(const double* __re
 template <int MODE>
 __global__ __launch_bounds__(kSmallBlock) void k_motions_small(const double* __restrict__ recs, int n_obb, double rg,
                                                                double ro, const double* __restrict__ s1,
-                                                               const double* __restrict__ s2, int64_t n, int can_pass,
-                                                               uint8_t* __restrict__ valid, uint32_t* done,
-                                                               uint32_t seq) {
+                                                               const double* __restrict__ s2, int64_t n, int per,
+                                                               int can_pass, uint8_t* __restrict__ valid,
+                                                               uint32_t* done, uint32_t seq) {
     extern __shared__ double srec[];
-    stage_records(srec, recs, n_obb * kRecDoubles);
-    const int64_t i = (int64_t)blockIdx.x * kSmallBlock + threadIdx.x;
+    uint32_t* s_hit = reinterpret_cast<uint32_t*>(srec + (((size_t)n_obb * kRecDoubles + 1) & ~size_t(1)));
+    const int t = threadIdx.x, slices = kSmallBlock / per, slice = t / per, j = t - slice * per;
+    const int64_t i = (int64_t)blockIdx.x * per + j;
     const bool act = i < n;
-    double s[3], e[3], lo[3], hi[3];
+    double s[3] = {0.0, 0.0, 0.0}, e[3] = {0.0, 0.0, 0.0}, lo[3], hi[3];
+    stage_records(srec, recs, n_obb * kRecDoubles, [&] {
+        if (act) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                s[k] = s1[3 * i + k];
+                e[k] = s2[3 * i + k];
+            }
+        }
+    });
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        s[k] = act ? s1[3 * i + k] : 0.0;
-        e[k] = act ? s2[3 * i + k] : 0.0;
         // the rtree query box (src/World.cpp:137-141); mode 1: widened by a hair, since a
         // rounded point may sit an ulp past it
         const double l = (e[k] < s[k]) ? e[k] : s[k], h = (s[k] < e[k]) ? e[k] : s[k];
         lo[k] = MODE == 1 ? l - (1e-9 + 1e-12 * fabs(l)) : l;
         hi[k] = MODE == 1 ? h + (1e-9 + 1e-12 * fabs(h)) : h;
     }
+    if (t < per) s_hit[t] = 0u;
     __syncthreads();
+    const int o0 = (int)((int64_t)slice * n_obb / slices), o1 = (int)((int64_t)(slice + 1) * n_obb / slices);
     const bool cp = can_pass != 0;
-    bool hit = false;
-    for (int o = 0; o < n_obb; ++o) {
-        const double* r = srec + (size_t)o * kRecDoubles;
+    auto cand_of = [&](const double* r, bool hit) {
         const uint32_t m = (uint32_t)__double_as_longlong(r[R_META]);
         const bool overlap = !((r[F_HIX] < lo[0]) | (hi[0] < r[F_LOX]) | (r[F_HIY] < lo[1]) | (hi[1] < r[F_LOY]) |
                                (r[F_HIZ] < lo[2]) | (hi[2] < r[F_LOZ]));
-        const bool cand = act & !hit & overlap & !(cp & ((m & META_FILLING) != 0u));  // :150-153
-        if (__builtin_amdgcn_ballot_w64(cand) && cand)
-            hit = MODE == 0 ? rec_ray_hit(r, s, e, (m & META_GATE) ? rg : ro) : d32_pair_hit(r, s, e, rg, ro, cp);
+        return act & !hit & overlap & !(cp & ((m & META_FILLING) != 0u));  // :150-153
+    };
+    auto test = [&](const double* r) {
+        const uint32_t m = (uint32_t)__double_as_longlong(r[R_META]);
+        return MODE == 0 ? rec_ray_hit(r, s, e, (m & META_GATE) ? rg : ro) : d32_pair_hit(r, s, e, rg, ro, cp);
+    };
+    bool hit = false;
+    int o = o0;
+    for (; o + 2 <= o1; o += 2) {  // two records' AABB tests before any branch
+        const double* r = srec + (size_t)o * kRecDoubles;
+        const bool c0 = cand_of(r, hit), c1 = cand_of(r + kRecDoubles, hit);
+        if (__builtin_amdgcn_ballot_w64(c0) && c0) hit = test(r);
+        if (__builtin_amdgcn_ballot_w64(c1 & !hit) && c1 && !hit) hit = test(r + kRecDoubles);
     }
-    if (act) valid[i] = hit ? 0 : 1;
+    for (; o < o1; ++o) {
+        const double* r = srec + (size_t)o * kRecDoubles;
+        const bool c = cand_of(r, hit);
+        if (__builtin_amdgcn_ballot_w64(c) && c) hit = test(r);
+    }
+    if (hit) s_hit[j] = 1u;
+    __syncthreads();
+    if (slice == 0 && act) valid[i] = s_hit[j] ? 0 : 1;
     publish_done(done, seq);
 }
 
@@ -129,12 +205,12 @@ bool small_motions(const SmallWorld& sw, int64_t n) {
 epp_status launch_states_small(const SmallWorld& sw, bool mindist, const double* xyz, int64_t n, int32_t can_pass,
                                double md, uint8_t* valid, int32_t* compact_idx, int64_t* n_valid, hipStream_t st,
                                uint32_t* done, uint32_t seq) {
-    const int grid = (int)((n + kSmallBlock - 1) / kSmallBlock);
-    const size_t shm = (size_t)sw.n_obb * kRecDoubles * sizeof(double);
+    const int per = small_per(n), grid = (int)((n + per - 1) / per);
+    const size_t shm = small_shm(sw.n_obb);
     auto nv = reinterpret_cast<unsigned long long*>(n_valid);
 #define EPP_LAUNCH_SS(M, C)                                                                                          \
     hipLaunchKernelGGL((k_states_small<M, C>), dim3(grid), dim3(kSmallBlock), shm, st, sw.recs, sw.n_obb, sw.r_gate, \
-                       sw.r_obst, xyz, n, can_pass, md, valid, compact_idx, nv, done, seq)
+                       sw.r_obst, xyz, n, per, can_pass, md, valid, compact_idx, nv, done, seq)
     if (mindist) EPP_LAUNCH_SS(true, false);
     else if (compact_idx) EPP_LAUNCH_SS(false, true);
     else EPP_LAUNCH_SS(false, false);
@@ -144,14 +220,14 @@ epp_status launch_states_small(const SmallWorld& sw, bool mindist, const double*
 
 epp_status launch_motions_small(const SmallWorld& sw, int32_t mode, const double* s1, const double* s2, int64_t n,
                                 int32_t can_pass, uint8_t* valid, hipStream_t st, uint32_t* done, uint32_t seq) {
-    const int grid = (int)((n + kSmallBlock - 1) / kSmallBlock);
-    const size_t shm = (size_t)sw.n_obb * kRecDoubles * sizeof(double);
+    const int per = small_per(n), grid = (int)((n + per - 1) / per);
+    const size_t shm = small_shm(sw.n_obb);
     if (mode == 0)
         hipLaunchKernelGGL((k_motions_small<0>), dim3(grid), dim3(kSmallBlock), shm, st, sw.recs, sw.n_obb, sw.r_gate,
-                           sw.r_obst, s1, s2, n, can_pass, valid, done, seq);
+                           sw.r_obst, s1, s2, n, per, can_pass, valid, done, seq);
     else
         hipLaunchKernelGGL((k_motions_small<1>), dim3(grid), dim3(kSmallBlock), shm, st, sw.recs, sw.n_obb, sw.r_gate,
-                           sw.r_obst, s1, s2, n, can_pass, valid, done, seq);
+                           sw.r_obst, s1, s2, n, per, can_pass, valid, done, seq);
     return launch_error("epp_check_motions");
 }
 
@@ -201,7 +277,7 @@ epp_status run_sync(int64_t n, hipStream_t st, const char* what, Launch&& launch
         return EPP_ERR_HIP;
     }
     const uint32_t seq = ++ds.seq;
-    const int groups = (int)((n + kSmallBlock - 1) / kSmallBlock);
+    const int groups = (int)((n + small_per(n) - 1) / small_per(n));
     if (const epp_status rc = launch(ds.p, seq)) return rc;
     return wait_done(ds.p, groups, seq, st, what);
 }

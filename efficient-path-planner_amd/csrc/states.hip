@@ -780,9 +780,12 @@ epp_status epp_check_states(const epp_world* world, const double* xyz, int64_t n
     }
     if (n == 0) return EPP_OK;
     const SmallWorld sw = small_world(world);
-    if (small_states(sw, n))
-        return launch_states_small(sw, false, xyz, n, can_pass_gate, 0.0, valid, compact_idx, n_valid,
-                                   (hipStream_t)stream);
+    if (small_states(sw, n)) {
+        if (const epp_status st = launch_states_small(sw, false, xyz, n, can_pass_gate, 0.0, valid, compact_idx,
+                                                      n_valid, (hipStream_t)stream))
+            return st;
+        return note_record_reader(world, sw, (hipStream_t)stream);
+    }
     if (const epp_status st = ensure_index(world)) return st;
     return launch_states<false>(world_view(world), world_dview(world), xyz, n, can_pass_gate, 0.0, valid,
                                 compact_idx, n_valid, stream);
@@ -805,8 +808,12 @@ epp_status epp_check_states_mindist(const epp_world* world, const double* xyz, i
     }
     if (n == 0) return EPP_OK;
     const SmallWorld sw = small_world(world);
-    if (small_states(sw, n))
-        return launch_states_small(sw, true, xyz, n, 0, min_distance, valid, nullptr, nullptr, (hipStream_t)stream);
+    if (small_states(sw, n)) {
+        if (const epp_status st =
+                launch_states_small(sw, true, xyz, n, 0, min_distance, valid, nullptr, nullptr, (hipStream_t)stream))
+            return st;
+        return note_record_reader(world, sw, (hipStream_t)stream);
+    }
     if (const epp_status st = ensure_index(world)) return st;
     return launch_states<true>(world_view(world), world_dview(world), xyz, n, 0, min_distance, valid, nullptr,
                                nullptr, stream);

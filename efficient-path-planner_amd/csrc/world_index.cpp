@@ -56,31 +56,43 @@ bool is_rz(const epp_obb& o) {
 inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
 // The OBB records of a new version (AABBs, kRecDoubles-double records with the filling /
-// gate bits) into hw.aabbs and the pinned hw.h_recs; the cheap part of an update.
+// gate bits) into hw.aabbs and the pinned record slot other than the current one (the
+// cheap part of an update); that slot becomes current.
 bool build_records(HostWorld& hw, const epp_obb* obbs, int n) {
     for (int i = 0; i < n; ++i)
         if (!is_rz(obbs[i])) {  // (checked first: a failed update leaves the world as it was)
             set_error("epp_world: OBB rotation must be a rotation about z (src/Object.cpp:38-47)");
             return false;
         }
+    const int slot = hw.h_recs ? 1 - hw.rec_slot : 0;
+    for (auto& r : hw.rec_readers[slot])  // asynchronous kernels may still read this slot's version
+        if (r.pending) {
+            const hipError_t e = hipEventSynchronize(r.ev);
+            if (e != hipSuccess) {
+                set_error(std::string("epp_world: waiting for the readers of the records: ") + hipGetErrorString(e));
+                return false;
+            }
+            r.pending = false;
+        }
     const size_t need = std::max<size_t>(1, (size_t)n * kRecDoubles) * sizeof(double);
-    if (need > hw.h_recs_cap) {
-        if (hw.h_recs) (void)hipHostFree(hw.h_recs);
-        hw.h_recs = nullptr;
-        hw.h_recs_cap = 0;
-        const hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&hw.h_recs), need * 2, hipHostMallocDefault);
+    if (need > hw.rec_cap[slot]) {
+        if (hw.rec_buf[slot]) (void)hipHostFree(hw.rec_buf[slot]);
+        hw.rec_buf[slot] = nullptr;
+        hw.rec_cap[slot] = 0;
+        const hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&hw.rec_buf[slot]), need * 2, hipHostMallocDefault);
         if (e != hipSuccess) {
             set_error(std::string("epp_world: allocation: ") + hipGetErrorString(e));
             return false;
         }
-        hw.h_recs_cap = need * 2;
+        hw.rec_cap[slot] = need * 2;
     }
+    double* recs = hw.rec_buf[slot];
     hw.aabbs.assign((size_t)n * 6, 0.0);
     for (int i = 0; i < n; ++i) {
         const epp_obb& o = obbs[i];
         double lo[3], hi[3];
         compute_aabb(o, o.is_gate ? hw.r_gate : hw.r_obst, lo, hi);  // src/World.cpp:89-90
-        double* r = hw.h_recs + (size_t)i * kRecDoubles;
+        double* r = recs + (size_t)i * kRecDoubles;
         for (int k = 0; k < 3; ++k) {
             hw.aabbs[(size_t)i * 6 + k] = r[F_LOX + k] = lo[k];
             hw.aabbs[(size_t)i * 6 + 3 + k] = r[F_HIX + k] = hi[k];
@@ -95,6 +107,8 @@ bool build_records(HostWorld& hw, const epp_obb* obbs, int n) {
     }
     hw.obbs.assign(obbs, obbs + n);
     hw.view.n_obb = n;
+    hw.rec_slot = slot;
+    hw.h_recs = recs;
     return true;
 }
 
@@ -582,8 +596,8 @@ epp_status epp_world_update(epp_world* w, const epp_obb* obbs, int32_t n) {
         epp::set_error("epp_world_update: invalid argument");
         return EPP_ERR_INVALID_ARGUMENT;
     }
-    // the previous records / blob may still be read by in-flight kernels on any stream
-    (void)hipDeviceSynchronize();
+    // (the device blob is not touched: ensure_index rebuilds it after in-flight kernels;
+    // the records go to the other pinned slot, see HostWorld)
     std::lock_guard<std::mutex> lk(w->mu);
     if (!epp::build_records(*w, obbs, n)) return EPP_ERR_UNSUPPORTED;
     w->index_stale = true;
@@ -596,7 +610,10 @@ epp_status epp_world_destroy(epp_world* w) {
     (void)hipDeviceSynchronize();
     if (w->d_blob) (void)hipFree(w->d_blob);
     if (w->h_stage) (void)hipHostFree(w->h_stage);
-    if (w->h_recs) (void)hipHostFree(w->h_recs);
+    for (int k = 0; k < 2; ++k) {
+        if (w->rec_buf[k]) (void)hipHostFree(w->rec_buf[k]);
+        for (auto& r : w->rec_readers[k]) (void)hipEventDestroy(r.ev);
+    }
     if (w->stream) (void)hipStreamDestroy(w->stream);
     delete w;
     return EPP_OK;
@@ -656,10 +673,39 @@ SmallWorld small_world(const epp_world* cw) {
     std::lock_guard<std::mutex> lk(hw.mu);
     SmallWorld s;
     s.recs = hw.index_stale ? hw.h_recs : reinterpret_cast<const double*>(hw.view.blob + hw.view.off_aos);
+    s.host_slot = hw.index_stale ? hw.rec_slot : -1;
     s.n_obb = (int32_t)hw.obbs.size();
     s.r_gate = hw.r_gate;
     s.r_obst = hw.r_obst;
     return s;
+}
+
+// An asynchronous launch reading the pinned records of `sw`'s slot was queued on `st`:
+// the next update that would rewrite that slot waits for it.
+epp_status note_record_reader(const epp_world* cw, const SmallWorld& sw, hipStream_t st) {
+    if (sw.host_slot < 0) return EPP_OK;
+    HostWorld& hw = const_cast<epp_world&>(*cw);
+    std::lock_guard<std::mutex> lk(hw.mu);
+    auto& rd = hw.rec_readers[sw.host_slot];
+    HostWorld::RecReader* r = nullptr;  // one event per stream: a later launch on it ends later
+    for (auto& x : rd)
+        if (x.stream == st) r = &x;
+    hipError_t e = hipSuccess;
+    if (!r) {
+        hipEvent_t ev = nullptr;
+        e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e == hipSuccess) {
+            rd.push_back({st, ev, false});
+            r = &rd.back();
+        }
+    }
+    if (e == hipSuccess) e = hipEventRecord(r->ev, st);
+    if (e != hipSuccess) {
+        set_error(std::string("epp_world: recording a reader of the records: ") + hipGetErrorString(e));
+        return EPP_ERR_HIP;
+    }
+    r->pending = true;
+    return EPP_OK;
 }
 
 }  // namespace epp

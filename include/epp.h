@@ -116,11 +116,14 @@ epp_status epp_build_obbs(const epp_obb_desc* gate_desc, const int32_t* gate_des
 epp_status epp_world_create(const epp_obb* obbs, int32_t n_obbs, double r_gate, double r_obst,
                             epp_world** out);
 /* Replaces the OBB set (gate-pose update = full rebuild, src/OnlineTrajGenerator.cpp:146).
- * Waits for every kernel on the device first (they may read the old records / index),
- * then rebuilds the OBB records only (pinned host memory): small queries (<= 4096 states
- * or 1024 edges on worlds of <= 256 OBBs) read those directly; the device index is
- * rebuilt and uploaded by the first call that needs it (or epp_world_build_index), so
- * an index error (e.g. too many distinct candidate lists) is reported there.  HIP graphs
+ * Rebuilds the OBB records only, into the one of two pinned host slots that is not the
+ * current version's (after the asynchronous small-query launches that read that slot
+ * have finished; nothing else is waited for): small queries (<= 4096 states or 1024
+ * edges on worlds of <= 256 OBBs) read those directly; the device index is rebuilt and
+ * uploaded by the first call that needs it (or epp_world_build_index), after every kernel
+ * that may read the old index, so an index error (e.g. too many distinct candidate
+ * lists) is reported there.  No call reading this world may run on another host thread
+ * meanwhile (kernels already queued on streams may).  HIP graphs
  * that captured launches on this world must be re-captured afterwards, and only after
  * epp_world_build_index (launch shapes depend on the index; epp_world_generation
  * changes). */

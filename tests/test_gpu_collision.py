@@ -503,3 +503,39 @@ def test_small_query_path(fworlds, name, monkeypatch):
     ref = O.world_build(fgeom, g, obstacles, rg, ro)
     big = synth.sample_states(99, lo, hi, 50_000)
     assert np.array_equal(w.check_states(big), O.check_states(ref, rg, ro, big, threads=8))
+
+
+def test_async_small_queries_across_updates(fworlds):
+    """Asynchronous small queries on a stale index read the pinned records of their
+    version; the updates in between go to the other record slot, and an update that
+    reuses a slot waits for the queued kernels reading it (no device-wide wait).  Four
+    versions queued back to back on one stream without host synchronisation, each
+    answer vs the oracle of its version."""
+    import ctypes as C
+    fgeom, rg, ro, ws = fworlds
+    gates, obstacles, (lo, hi) = ws["c2"]
+    w = capi.World(capi.build_obbs(fgeom, gates, obstacles), rg, ro)
+    L = capi.lib()
+    st = C.c_void_p()
+    capi.check(L.epp_stream_create(C.byref(st)))
+    rs = np.random.RandomState(21)
+    g = np.array(gates, float)
+    pts = np.vstack([synth.sample_states(70, lo, hi, 4000), _gate_openings(g, fgeom, 12, seed=3)])
+    s1, s2 = synth.edges(71, 72, lo, hi, 1000, max_len=1.0)
+    d_pts, d1, d2 = (capi.DeviceBuffer.from_array(a) for a in (pts, s1, s2))
+    outs, refs = [], []
+    for version in range(4):
+        if version:
+            g[:, 0] += rs.uniform(-0.2, 0.2, len(g))
+            g[:, 5] += rs.uniform(-0.2, 0.2, len(g))
+            w.update(capi.build_obbs(fgeom, g, obstacles))
+        refs.append(O.world_build(fgeom, g, obstacles, rg, ro))
+        o_s, o_m = capi.DeviceBuffer(len(pts)), capi.DeviceBuffer(len(s1))
+        w.check_states_dev(d_pts.ptr, len(pts), 1, o_s.ptr, stream=st.value)
+        w.check_motions_dev(d1.ptr, d2.ptr, len(s1), 0, 1, o_m.ptr, stream=st.value)
+        outs.append((o_s, o_m))
+    capi.check(L.epp_stream_sync(st.value))
+    for (o_s, o_m), ref in zip(outs, refs):
+        assert np.array_equal(o_s.download(np.uint8, len(pts)), O.check_states(ref, rg, ro, pts, 1))
+        assert np.array_equal(o_m.download(np.uint8, len(s1)), O.check_motions(ref, rg, ro, s1, s2, 0, 1, threads=8))
+    L.epp_stream_destroy(st.value)
