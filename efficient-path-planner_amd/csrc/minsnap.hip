@@ -304,12 +304,17 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ kc, const 
         bool ok = true;
         double prev[4];  // this lane's column of step v-1: W_{v-1}[:, c] or z_{v-1}[:, d]
         double base[4], ecol[4];  // step v's D_v[:, c] or b_v[:, d]; E_v[:, c]
+        // (branch-free: one address per lane, so the loads of a step are not split over
+        // exec-masked branches that each wait for their own LDS round trip)
         auto load = [&](int v, double (&bs)[4], double (&ec)[4]) {
             const double* Sg = scr + (size_t)(v - 1) * Seg::kSize;
+            const double* bp = wcol ? Sg + Seg::kL + c : rhs + (size_t)v * 12 + d;
+            const int bstride = wcol ? 4 : 3;
+            const double* ep = Sg + Seg::kW + (wcol ? c : 0);  // (z lanes: read, unused)
 #pragma unroll
             for (int p = 0; p < 4; ++p) {
-                bs[p] = wcol ? Sg[Seg::kL + p * 4 + c] : rhs[((size_t)v * 4 + p) * 3 + d];
-                ec[p] = wcol ? Sg[Seg::kW + p * 4 + c] : 0.0;
+                bs[p] = bp[p * bstride];
+                ec[p] = ep[p * 4];
             }
         };
         load(1, base, ecol);
@@ -335,9 +340,7 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ kc, const 
 #pragma unroll
                 for (int p = 0; p < 4; ++p) xS[p * 4 + c] = col[p];
             }
-            if (v == 5) EPP_TLI(40);
             wave_sync_lds();
-            if (v == 5) EPP_TLI(41);
             // Cholesky of S (lower triangle), on every lane
             double L[16], inv[4];
 #pragma unroll
@@ -360,7 +363,6 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ kc, const 
                 }
             }
             if (!ok) break;  // (the same on every lane)
-            if (v == 5) EPP_TLI(42);
             // forward solve of this lane's column: E_v[:, c] -> W_v[:, c], or z
             double x[4];
 #pragma unroll

@@ -44,8 +44,6 @@ fw = np.diff(it[:, 1:nin + 1], axis=1)
 print("block solve forward, cycles per vertex step (median):", np.median(fw, axis=0).astype(int).tolist())
 bw = np.diff(it[:, 32:32 + nin + 1], axis=1)
 print("back substitution, cycles per vertex step (median):", np.median(bw, axis=0).astype(int).tolist())
-print("vertex 5: start -> Schur done", int(np.median(it[:, 40] - it[:, 5])), "-> S exchanged", int(np.median(it[:, 41] - it[:, 40])),
-      "-> factored", int(np.median(it[:, 42] - it[:, 41])), "-> step end", int(np.median(it[:, 6] - it[:, 42])), "cycles")
 print("forward end -> back start:", int(np.median(it[:, 32] - it[:, nin])), "cycles; back end -> phase end:",
       int(np.median(it[:, 63] - it[:, 32 + nin])), "cycles")
 st = allst[:, :32].reshape(-1, 2, 16)
