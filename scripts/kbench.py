@@ -110,7 +110,7 @@ def main():
             ms = timed_kernel_ms(capi, st, f, 5)
             for k in env:
                 del os.environ[k]
-            key = f"c3_motion_mode{mode}{'_nolds' if env else ''}"
+            key = f"c3_motion_mode{mode}" + "".join(f"_{k}={v}" for k, v in env.items())
             res[key] = {"us": ms * 1e3, "edges_per_s": N / (ms * 1e-3)}
             print(key, res[key], flush=True)
     json.dump(res, open(os.path.join(ROOT, "gpurun_out", "kbench.json"), "w"), indent=1)
