@@ -10,6 +10,7 @@
 #include <stdexcept>
 #include <string>
 
+#include "epp/ConfigParser.h"
 #include "epp/MultiTrackPlanner.h"
 #include "epp/OnlineTrajGenerator.h"
 
@@ -193,6 +194,68 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["ms_search"] = s.ms_search;
             return d;
         });
+
+    // ConfigParser (src/ConfigParserYAML.cpp:10-118): the parsed configuration as a dict
+    // (JSON or block-YAML file, as YAML::LoadFile reads either); no GPU involved
+    m.def(
+        "load_config",
+        [](const std::string& configPath) {
+            epp::ConfigParser c(configPath);
+            auto v3 = [](const Vec3& v) { return py::make_tuple(v[0], v[1], v[2]); };
+            auto obbs = [&](const std::vector<epp::OBBDescription>& ds) {
+                py::list l;
+                for (const auto& d : ds) {
+                    py::dict o;
+                    o["center"] = v3(d.center);
+                    o["half_size"] = v3(d.halfSize);
+                    o["type"] = d.type;
+                    o["name"] = d.name;
+                    l.append(o);
+                }
+                return l;
+            };
+            py::dict out, gates, heights;
+            for (int t = 0; t < c.numGateTypes(); ++t) {
+                gates[py::int_(t)] = obbs(c.getGateGeometryByTypeId(t));
+                heights[py::int_(t)] = c.getObjectPropertiesByTypeId(t).height;
+            }
+            out["gate_geometry"] = gates;
+            out["gate_height"] = heights;
+            out["obstacle_geometry"] = obbs(c.getObstacleGeometry());
+            const auto& w = c.getWorldProperties();
+            py::dict wd;
+            wd["lower_bound"] = v3(w.lowerBound);
+            wd["upper_bound"] = v3(w.upperBound);
+            wd["inflate_radius"] = w.inflateRadius;
+            out["world"] = wd;
+            const auto& p = c.getPathPlannerProperties();
+            py::dict pd;
+            pd["optimality_threshold_percentage"] = p.optimalityThresholdPercentage;
+            pd["time_limit_online"] = p.timeLimitOnline;
+            pd["time_limit_offline"] = p.timeLimitOffline;
+            pd["checkpoint_gate_offset"] = p.checkpointGateOffset;
+            pd["range"] = p.range;
+            pd["min_dist_check_traj_collision"] = p.minDistCheckTrajCollision;
+            pd["path_simplification"] = p.pathSimplification;
+            pd["recalculate_online"] = p.recalculateOnline;
+            pd["can_pass_gate"] = p.canPassGate;
+            pd["advance_for_calculation"] = p.advanceForCalculation;
+            pd["planner"] = p.planner;
+            pd["samples_fmt"] = p.samplesFMT;
+            out["path_planner"] = pd;
+            const auto& g = c.getTrajectoryGeneratorProperties();
+            py::dict gd;
+            gd["max_velocity"] = g.maxVelocity;
+            gd["max_acceleration"] = g.maxAcceleration;
+            gd["sampling_interval"] = g.samplingInterval;
+            gd["type"] = g.type;
+            gd["max_time"] = g.maxTime;
+            gd["prepend_traj_time"] = g.prependTrajTime;
+            gd["max_traj_divergence"] = g.maxTrajDivergence;
+            out["trajectory_generator"] = gd;
+            return out;
+        },
+        py::arg("configPath"));
 
     // planTracks (include/epp/MultiTrackPlanner.h): independent tracks across GPUs of this
     // node, one host thread per device, waypoint sets all-gathered over RCCL

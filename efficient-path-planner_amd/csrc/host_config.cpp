@@ -1,6 +1,6 @@
-// host_config.cpp — ConfigParser (src/ConfigParserYAML.cpp:10-118) over a small
-// order-preserving JSON reader.  Object members keep document order, which is the
-// iteration order yaml-cpp gives the reference for component_geometry.
+// host_config.cpp — ConfigParser (src/ConfigParserYAML.cpp:10-118) over small
+// order-preserving JSON and block-YAML readers.  Object members keep document order,
+// which is the iteration order yaml-cpp gives the reference for component_geometry.
 #include <cstdlib>
 #include <fstream>
 #include <sstream>
@@ -158,6 +158,336 @@ private:
     }
 };
 
+// ---- YAML (block style) ------------------------------------------------------------
+// The reference reads its config with YAML::LoadFile (src/ConfigParserYAML.cpp:12), so a
+// config may be a JSON document (YAML's flow style; the shipped config.json) or block
+// YAML.  This reader covers the block subset a config uses: nested mappings and "- "
+// sequences by indentation, inline flow collections ([..], {..}, possibly spanning
+// lines), quoted and plain scalars, '#' comments.  Plain scalars are typed the way the
+// parser's .as<T>() calls read them: numbers, YAML 1.1 booleans, null / ~, else strings
+// (a number keeps its text, for .as<std::string>()).  Anchors, tags, multi-document
+// streams and block scalars (| >) are not supported and raise.
+class YamlReader {
+public:
+    explicit YamlReader(const std::string& text) {
+        std::istringstream in(text);
+        std::string raw;
+        int no = 0;
+        while (std::getline(in, raw)) {
+            ++no;
+            if (!raw.empty() && raw.back() == '\r') raw.pop_back();
+            const std::string s = strip_comment(raw);
+            size_t ind = 0;
+            while (ind < s.size() && s[ind] == ' ') ++ind;
+            if (ind < s.size() && s[ind] == '\t') fail(no, "tab indentation");
+            std::string body = trim(s.substr(ind));
+            if (body.empty()) continue;
+            if (body == "---" && lines_.empty()) continue;
+            if (body == "---" || body == "...") fail(no, "multi-document streams are not supported");
+            lines_.push_back({(int)ind, body, no});
+        }
+    }
+    JsonValue parse() {
+        if (lines_.empty()) return JsonValue();
+        JsonValue v = block(lines_[0].indent);
+        if (i_ != lines_.size()) fail(lines_[i_].no, "bad indentation");
+        return v;
+    }
+
+private:
+    struct Line {
+        int indent;
+        std::string body;
+        int no;
+    };
+    std::vector<Line> lines_;
+    size_t i_ = 0;
+
+    [[noreturn]] static void fail(int no, const std::string& m) {
+        throw std::runtime_error("config YAML parse error at line " + std::to_string(no) + ": " + m);
+    }
+    static std::string trim(const std::string& s) {
+        size_t a = 0, b = s.size();
+        while (a < b && (s[a] == ' ' || s[a] == '\t')) ++a;
+        while (b > a && (s[b - 1] == ' ' || s[b - 1] == '\t')) --b;
+        return s.substr(a, b - a);
+    }
+    // drops a comment: '#' at the start or after a blank, outside quotes
+    static std::string strip_comment(const std::string& s) {
+        char q = 0;
+        for (size_t k = 0; k < s.size(); ++k) {
+            const char c = s[k];
+            if (q) {
+                if (c == q) q = 0;
+                else if (c == '\\' && q == '"') ++k;
+            } else if (c == '"' || c == '\'') {
+                q = c;
+            } else if (c == '#' && (k == 0 || s[k - 1] == ' ' || s[k - 1] == '\t')) {
+                return s.substr(0, k);
+            }
+        }
+        return s;
+    }
+    static bool is_seq_item(const std::string& b) { return b == "-" || b.rfind("- ", 0) == 0; }
+    // position of the ':' that ends a mapping key (followed by a blank or the line end), or npos
+    static size_t key_colon(const std::string& b) {
+        if (b.empty() || b[0] == '[' || b[0] == '{') return std::string::npos;
+        char q = 0;
+        size_t k = 0;
+        if (b[0] == '"' || b[0] == '\'') {
+            q = b[0];
+            for (k = 1; k < b.size() && b[k] != q; ++k)
+                if (b[k] == '\\' && q == '"') ++k;
+            ++k;
+        }
+        for (; k < b.size(); ++k)
+            if (b[k] == ':' && (k + 1 == b.size() || b[k + 1] == ' ')) return k;
+        return std::string::npos;
+    }
+    static std::string unquote_key(const std::string& k, int no) {
+        if (k.size() >= 2 && (k[0] == '"' || k[0] == '\'')) {
+            JsonValue v = scalar(k, no);
+            return v.str;
+        }
+        return k;
+    }
+    // a plain or quoted scalar, typed
+    static JsonValue scalar(const std::string& t, int no) {
+        JsonValue v;
+        if (t.empty()) return v;  // null
+        if (t[0] == '"' || t[0] == '\'') {
+            const char q = t[0];
+            std::string out;
+            size_t k = 1;
+            for (; k < t.size(); ++k) {
+                char c = t[k];
+                if (c == q) {
+                    if (q == '\'' && k + 1 < t.size() && t[k + 1] == '\'') {
+                        out += '\'';
+                        ++k;
+                        continue;
+                    }
+                    break;
+                }
+                if (q == '"' && c == '\\' && k + 1 < t.size()) {
+                    c = t[++k];
+                    out += c == 'n' ? '\n' : c == 't' ? '\t' : c;
+                    continue;
+                }
+                out += c;
+            }
+            if (k >= t.size() || trim(t.substr(k + 1)) != "") fail(no, "bad quoted scalar " + t);
+            v.kind = JsonValue::String;
+            v.str = out;
+            return v;
+        }
+        if (t[0] == '&' || t[0] == '*' || t[0] == '!' || t[0] == '|' || t[0] == '>')
+            fail(no, "anchors, aliases, tags and block scalars are not supported");
+        if (t == "~" || t == "null" || t == "Null" || t == "NULL") return v;
+        static const char* yes[] = {"true", "True", "TRUE", "yes", "Yes", "YES", "on", "On", "ON", "y", "Y"};
+        static const char* no_[] = {"false", "False", "FALSE", "no", "No", "NO", "off", "Off", "OFF", "n", "N"};
+        for (const char* s : yes)
+            if (t == s) {
+                v.kind = JsonValue::Bool;
+                v.b = true;
+                return v;
+            }
+        for (const char* s : no_)
+            if (t == s) {
+                v.kind = JsonValue::Bool;
+                v.b = false;
+                return v;
+            }
+        char* end = nullptr;
+        const double d = std::strtod(t.c_str(), &end);
+        if (end && *end == '\0' && end != t.c_str()) {
+            v.kind = JsonValue::Number;
+            v.num = d;
+            v.str = t;
+            return v;
+        }
+        v.kind = JsonValue::String;
+        v.str = t;
+        return v;
+    }
+    // flow collection text -> value; plain scalars inside are typed as above
+    static JsonValue flow(const std::string& t, int no) {
+        size_t k = 0;
+        JsonValue v = flow_value(t, k, no);
+        while (k < t.size() && t[k] == ' ') ++k;
+        if (k != t.size()) fail(no, "trailing characters after a flow collection");
+        return v;
+    }
+    static JsonValue flow_value(const std::string& t, size_t& k, int no) {
+        while (k < t.size() && t[k] == ' ') ++k;
+        if (k >= t.size()) fail(no, "unexpected end of a flow collection");
+        JsonValue v;
+        const char c = t[k];
+        if (c == '[' || c == '{') {
+            const bool map = c == '{';
+            v.kind = map ? JsonValue::Object : JsonValue::Array;
+            ++k;
+            while (true) {
+                while (k < t.size() && t[k] == ' ') ++k;
+                if (k < t.size() && t[k] == (map ? '}' : ']')) {
+                    ++k;
+                    return v;
+                }
+                if (map) {
+                    const size_t a = k;
+                    JsonValue key = flow_value(t, k, no);
+                    while (k < t.size() && t[k] == ' ') ++k;
+                    if (k >= t.size() || t[k] != ':') fail(no, "expected ':' in a flow mapping");
+                    ++k;
+                    std::string ks = key.kind == JsonValue::String || key.kind == JsonValue::Number
+                                         ? key.str
+                                         : trim(t.substr(a, k - 1 - a));
+                    v.obj.emplace_back(ks, flow_value(t, k, no));
+                } else {
+                    v.arr.push_back(flow_value(t, k, no));
+                }
+                while (k < t.size() && t[k] == ' ') ++k;
+                if (k < t.size() && t[k] == ',') {
+                    ++k;
+                    continue;
+                }
+                if (k < t.size() && t[k] == (map ? '}' : ']')) {
+                    ++k;
+                    return v;
+                }
+                fail(no, "expected ',' or a closing bracket");
+            }
+        }
+        // a scalar: quoted, or plain up to the next , ] } (or ':' + blank in a mapping)
+        const size_t a = k;
+        if (c == '"' || c == '\'') {
+            ++k;
+            while (k < t.size() && t[k] != c) k += (t[k] == '\\' && c == '"') ? 2 : 1;
+            ++k;
+        } else {
+            while (k < t.size() && t[k] != ',' && t[k] != ']' && t[k] != '}' &&
+                   !(t[k] == ':' && (k + 1 == t.size() || t[k + 1] == ' ')))
+                ++k;
+        }
+        return scalar(trim(t.substr(a, k - a)), no);
+    }
+    // a value written after "key:" or "- " on line `no`: flow collections may continue on
+    // the following lines until their brackets balance
+    JsonValue inline_value(std::string t, int no) {
+        if (!t.empty() && (t[0] == '[' || t[0] == '{')) {
+            auto depth = [](const std::string& s) {
+                int d = 0;
+                char q = 0;
+                for (size_t k = 0; k < s.size(); ++k) {
+                    const char c = s[k];
+                    if (q) {
+                        if (c == q) q = 0;
+                    } else if (c == '"' || c == '\'') {
+                        q = c;
+                    } else if (c == '[' || c == '{') {
+                        ++d;
+                    } else if (c == ']' || c == '}') {
+                        --d;
+                    }
+                }
+                return d;
+            };
+            while (depth(t) > 0) {
+                if (i_ >= lines_.size()) fail(no, "unterminated flow collection");
+                t += " " + lines_[i_++].body;
+            }
+            return flow(t, no);
+        }
+        return scalar(t, no);
+    }
+    JsonValue block(int indent) {
+        if (i_ >= lines_.size()) return JsonValue();
+        return is_seq_item(lines_[i_].body) ? sequence(indent) : mapping(indent);
+    }
+    // the value of a "key:" / "- " with nothing after it: the more-indented block below
+    // (a sequence may sit at the key's own indentation), else null
+    JsonValue nested(int indent, bool seq_same_level) {
+        if (i_ < lines_.size()) {
+            const Line& n = lines_[i_];
+            if (n.indent > indent) return block(n.indent);
+            if (seq_same_level && n.indent == indent && is_seq_item(n.body)) return sequence(indent);
+        }
+        return JsonValue();
+    }
+    JsonValue mapping(int indent) {
+        JsonValue v;
+        v.kind = JsonValue::Object;
+        while (i_ < lines_.size() && lines_[i_].indent == indent && !is_seq_item(lines_[i_].body)) {
+            const Line ln = lines_[i_++];
+            const size_t c = key_colon(ln.body);
+            if (c == std::string::npos) {
+                if (v.obj.empty() && ln.body[0] != '[' && ln.body[0] != '{') fail(ln.no, "expected 'key: value'");
+                if (!v.obj.empty()) fail(ln.no, "expected 'key: value'");
+                --i_;  // a document that is a single flow collection / scalar
+                const Line one = lines_[i_++];
+                return inline_value(one.body, one.no);
+            }
+            const std::string key = unquote_key(trim(ln.body.substr(0, c)), ln.no);
+            const std::string rest = trim(ln.body.substr(c + 1));
+            for (const auto& kv : v.obj)
+                if (kv.first == key) fail(ln.no, "duplicate key " + key);
+            v.obj.emplace_back(key, rest.empty() ? nested(indent, true) : inline_value(rest, ln.no));
+        }
+        if (i_ < lines_.size() && lines_[i_].indent > indent) fail(lines_[i_].no, "bad indentation");
+        return v;
+    }
+    JsonValue sequence(int indent) {
+        JsonValue v;
+        v.kind = JsonValue::Array;
+        while (i_ < lines_.size() && lines_[i_].indent == indent && is_seq_item(lines_[i_].body)) {
+            Line& ln = lines_[i_];
+            const std::string rest = ln.body == "-" ? std::string() : trim(ln.body.substr(2));
+            if (rest.empty()) {
+                ++i_;
+                v.arr.push_back(nested(indent, false));
+            } else if (key_colon(rest) != std::string::npos || is_seq_item(rest)) {
+                // "- key: value" / "- - x": a nested block starting on this line
+                const int inner = indent + (int)(ln.body.size() - rest.size());
+                ln.indent = inner;
+                ln.body = rest;
+                v.arr.push_back(block(inner));
+            } else {
+                ++i_;
+                v.arr.push_back(inline_value(rest, ln.no));
+            }
+        }
+        return v;
+    }
+};
+
+// A document whose first significant character opens a JSON object or array is read as
+// JSON (the shipped config.json), anything else as block YAML.
+JsonValue parse_config_text(const std::string& text) {
+    size_t k = 0;
+    while (k < text.size()) {
+        const char c = text[k];
+        if (c == ' ' || c == '\t' || c == '\r' || c == '\n') {
+            ++k;
+        } else if (c == '#') {
+            while (k < text.size() && text[k] != '\n') ++k;
+        } else {
+            break;
+        }
+    }
+    if (k < text.size() && (text[k] == '{' || text[k] == '[')) {
+        try {
+            return Reader(text).parse();
+        } catch (const std::runtime_error&) {
+            try {
+                return YamlReader(text).parse();  // flow YAML that is not strict JSON
+            } catch (const std::runtime_error&) {
+            }
+            throw;  // report the JSON error
+        }
+    }
+    return YamlReader(text).parse();
+}
+
 const JsonValue& at(const JsonValue& v, const std::string& k, const std::string& path) {
     const JsonValue* r = v.kind == JsonValue::Object ? v.find(k) : nullptr;
     if (!r) throw std::runtime_error("config: missing key " + path + k);
@@ -176,6 +506,7 @@ bool boolean(const JsonValue& v, const std::string& what) {
 }
 std::string str(const JsonValue& v, const std::string& what) {
     if (v.kind == JsonValue::String) return v.str;
+    if (v.kind == JsonValue::Number && !v.str.empty()) return v.str;  // YAML plain scalar
     throw std::runtime_error("config: " + what + " is not a string");
 }
 Vec3 vec3(const JsonValue& v, const std::string& what) {
@@ -190,13 +521,12 @@ ConfigParser::ConfigParser(const std::string& configPath) {
     if (!f) throw std::runtime_error("bad file: " + configPath);  // YAML::BadFile
     std::stringstream ss;
     ss << f.rdbuf();
-    const std::string text = ss.str();
-    parse(Reader(text).parse());
+    parse(parse_config_text(ss.str()));
 }
 
 std::shared_ptr<ConfigParser> ConfigParser::fromString(const std::string& json) {
     std::shared_ptr<ConfigParser> p(new ConfigParser());
-    p->parse(Reader(json).parse());
+    p->parse(parse_config_text(json));
     return p;
 }
 
