@@ -454,12 +454,25 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     EPP_MTL_DECL;
     {
-        const uint4* src0 = reinterpret_cast<const uint4*>(wv->blob + wv->off_aos);
-        const uint4* src1 = reinterpret_cast<const uint4*>(wv->blob + wv->off_slab);
-        uint4* dst0 = reinterpret_cast<uint4*>(lds);
-        uint4* dst1 = reinterpret_cast<uint4*>(lds + rec_bytes);
-        for (uint32_t o = threadIdx.x; o < rec_bytes / 16; o += BLOCK) dst0[o] = src0[o];
-        for (uint32_t o = threadIdx.x; o < tile_bytes / 16; o += BLOCK) dst1[o] = src1[o];
+        // records and tile rows: up to 8 16-byte loads per thread in flight before the
+        // first store (a load -> store loop would wait out one L2 round trip per chunk)
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4* src0 = reinterpret_cast<const u32x4*>(wv->blob + wv->off_aos);
+        const u32x4* src1 = reinterpret_cast<const u32x4*>(wv->blob + wv->off_slab);
+        u32x4* dst = reinterpret_cast<u32x4*>(lds);
+        const uint32_t n0 = rec_bytes / 16, n1 = tile_bytes / 16, nt = n0 + n1;
+        constexpr int U = 8;
+        for (uint32_t b = threadIdx.x; b < nt; b += U * BLOCK) {
+            u32x4 r[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {  // (unconditional loads: clamped in range)
+                const uint32_t o = min(b + u * BLOCK, nt - 1);
+                r[u] = *(o < n0 ? src0 + o : src1 + (o - n0));
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)  // (past the end: the last chunk again, same bytes)
+                dst[min(b + u * BLOCK, nt - 1)] = r[u];
+        }
     }
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const double* recs = reinterpret_cast<const double*>(lds);
@@ -475,6 +488,9 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
     const double rg = wv->r_gate, ro = wv->r_obst;
     const bool cp = can_pass != 0;
     __syncthreads();
+#ifdef EPP_MOTIONS_TL
+    tl_c = __builtin_readcyclecounter() - tl_t0;  // staging
+#endif
     const int64_t stride = (int64_t)gridDim.x * BLOCK;
     for (int64_t i0 = (int64_t)blockIdx.x * BLOCK + wave * 64; i0 < n; i0 += stride) {
         const int64_t i = i0 + lane;
@@ -510,6 +526,7 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
         uint32_t qn = 0;  // queued pairs (wave-uniform)
         auto flush = [&]() {
             EPP_MTL_NOW(tl_f);
+            wave_lds_sync();  // the appends are visible
             for (uint32_t base = 0; base < qn; base += 64) {
                 const uint32_t jq = base + lane;
                 const bool has = jq < qn;
@@ -537,96 +554,83 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
             qn = 0;
             EPP_MTL_ADD(tl_flush, tl_f);
         };
-        // the tiles the edges' boxes reach (wave-uniform loop; mostly one)
-        for (int j = 0;; ++j) {
-            const bool has_t = j < ntiles;
-            if (!__builtin_amdgcn_ballot_w64(has_t)) break;
-            uint32_t cand[W];
-#pragma unroll
-            for (int w = 0; w < W; ++w) cand[w] = 0u;
-            const uint16_t* ids = nullptr;
-            if (has_t) {
-                const int tx = tx0 + j % ntx, ty = ty0 + j / ntx;
-                const uint32_t* tile = tiles + (size_t)(ty * T + tx) * TW;
-                const int la[3] = {min(max(ga[0] - (tx << SL), 0), S - 1), min(max(ga[1] - (ty << SL), 0), S - 1), ga[2]};
-                const int lb[3] = {min(max(gb[0] - (tx << SL), 0), S - 1), min(max(gb[1] - (ty << SL), 0), S - 1), gb[2]};
-#pragma unroll
-                for (int w = 0; w < W; ++w) cand[w] = ~0u;
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    const uint32_t* le = tile + ((2 * k) * S + lb[k]) * STRIDE;
-                    const uint32_t* ge = tile + ((2 * k + 1) * S + la[k]) * STRIDE;
-#pragma unroll
-                    for (int w = 0; w < W; ++w) cand[w] &= le[w] & ge[w];
-                }
-                const uint32_t* tail = tile + 6 * S * STRIDE;
-                if (tx > tx0) {
-#pragma unroll
-                    for (int w = 0; w < W; ++w) cand[w] &= tail[w];
-                }
-                if (ty > ty0) {
-#pragma unroll
-                    for (int w = 0; w < W; ++w) cand[w] &= tail[W + w];
-                }
-                if (cp) {
-#pragma unroll
-                    for (int w = 0; w < W; ++w) cand[w] &= ~tail[2 * W + w];
-                }
-                ids = reinterpret_cast<const uint16_t*>(tail + 3 * W);
+        // Candidate words of tile j (0 <= j < ntiles) of this lane's edge; returns the
+        // tile's OBB ids.  An OBB in several of the box's tiles is kept in its first tile
+        // along x and y only (FX / FY rows), filling OBBs are dropped with can_pass_gate.
+        auto tile_cand = [&](int j, uint32_t (&cand)[W]) __attribute__((always_inline)) -> const uint16_t* {
+            int tx = tx0, ty = ty0;
+            if (j == 1) {
+                tx = ntx > 1 ? tx0 + 1 : tx0;
+                ty = ntx > 1 ? ty0 : ty0 + 1;
+            } else if (j > 1) {
+                tx = tx0 + j % ntx;
+                ty = ty0 + j / ntx;
             }
+            const uint32_t* tile = tiles + (size_t)(ty * T + tx) * TW;
+            const int la[3] = {min(max(ga[0] - (tx << SL), 0), S - 1), min(max(ga[1] - (ty << SL), 0), S - 1), ga[2]};
+            const int lb[3] = {min(max(gb[0] - (tx << SL), 0), S - 1), min(max(gb[1] - (ty << SL), 0), S - 1), gb[2]};
+#pragma unroll
+            for (int w = 0; w < W; ++w) cand[w] = ~0u;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const uint32_t* le = tile + ((2 * k) * S + lb[k]) * STRIDE;
+                const uint32_t* ge = tile + ((2 * k + 1) * S + la[k]) * STRIDE;
+#pragma unroll
+                for (int w = 0; w < W; ++w) cand[w] &= le[w] & ge[w];
+            }
+            const uint32_t* tail = tile + 6 * S * STRIDE;
+            const uint32_t fx = tx > tx0 ? ~0u : 0u, fy = ty > ty0 ? ~0u : 0u, fl = cp ? ~0u : 0u;
+#pragma unroll
+            for (int w = 0; w < W; ++w) cand[w] &= (tail[w] | ~fx) & (tail[W + w] | ~fy) & ~(tail[2 * W + w] & fl);
+            return reinterpret_cast<const uint16_t*>(tail + 3 * W);
+        };
+        // Tiles are taken two at a time (the second is where an edge crossing one tile
+        // boundary continues; more is rare).  One wave-uniform loop then walks every
+        // lane's candidates, one per lane and round: the exact prefilter in doubles drops
+        // the OBBs whose AABB misses the edge's box (closed, as the rtree query; MODE 1:
+        // the box widened by a hair, since a rounded point may sit an ulp past it), and the
+        // survivors are appended to the wave's queue at ballot ranks.
+        for (int jp = 0;; jp += 2) {
+            if (!__builtin_amdgcn_ballot_w64(jp < ntiles)) break;
+            uint32_t ca[W], cb[W];
+            const uint16_t* ida = nullptr;
+            const uint16_t* idb = nullptr;
+#pragma unroll
+            for (int w = 0; w < W; ++w) ca[w] = cb[w] = 0u;
+            if (jp < ntiles) ida = tile_cand(jp, ca);
+            if (jp + 1 < ntiles) idb = tile_cand(jp + 1, cb);
             EPP_MTL_NOW(tl_p);
-            if (has_t) {
-                // exact prefilter: drop the candidates whose AABB misses the edge's box in
-                // doubles (closed, as the rtree query; MODE 1: the box widened by a hair,
-                // since a rounded point may sit an ulp past it), so only true rtree hits
-                // (MODE 0) reach the queue
+            for (;;) {
+                bool has = false;
+                uint32_t wsel = 0, bit = 0;
 #pragma unroll
-                for (int w = 0; w < W; ++w) {
-                    uint32_t m = cand[w];
-                    while (m) {
-                        const uint32_t bit = (uint32_t)__builtin_ctz(m);
-                        m &= m - 1u;
-                        const double* rec = recs + (size_t)ids[32 * w + bit] * kRecDoubles;
-                        const bool overlap = !((rec[F_HIX] < blo[0]) | (bhi[0] < rec[F_LOX]) | (rec[F_HIY] < blo[1]) |
-                                               (bhi[1] < rec[F_LOY]) | (rec[F_HIZ] < blo[2]) | (bhi[2] < rec[F_LOZ]));
-                        if (!overlap) cand[w] &= ~(1u << bit);
+                for (int w = 0; w < 2 * W; ++w) {
+                    uint32_t& cw = w < W ? ca[w] : cb[w - W];
+                    const bool take = !has && cw != 0u;
+                    if (take) {
+                        wsel = (uint32_t)w;
+                        bit = (uint32_t)__builtin_ctz(cw);
+                        cw &= cw - 1u;
                     }
+                    has = has || take;
                 }
+                if (!__builtin_amdgcn_ballot_w64(has)) break;
+                uint32_t id = 0;
+                bool keep = false;
+                if (has) {
+                    const uint16_t* tid = wsel < (uint32_t)W ? ida : idb;
+                    id = tid[32 * (wsel % (uint32_t)W) + bit];
+                    const double* rec = recs + (size_t)id * kRecDoubles;
+                    keep = !((rec[F_HIX] < blo[0]) | (bhi[0] < rec[F_LOX]) | (rec[F_HIY] < blo[1]) |
+                             (bhi[1] < rec[F_LOY]) | (rec[F_HIZ] < blo[2]) | (bhi[2] < rec[F_LOZ]));
+                }
+                const unsigned long long kb = __builtin_amdgcn_ballot_w64(keep);
+                if (keep) queue[qn + lanes_below(kb)] = id << 6 | (uint32_t)lane;
+                qn += (uint32_t)__popcll(kb);
+                EPP_MTL_CNT(tl_q, (uint32_t)__popcll(kb));
+                if (qn > (uint32_t)(kQueueV5 - 64)) flush();
             }
-#ifdef EPP_MOTIONS_TL
-            __builtin_amdgcn_wave_barrier();
-#endif
             EPP_MTL_ADD(tl_e, tl_p);
-            EPP_MTL_NOW(tl_u);
-            uint32_t cnt = 0;
-#pragma unroll
-            for (int w = 0; w < W; ++w) cnt += __popc(cand[w]);
-            uint32_t total;
-            const uint32_t off = wave_excl_scan(cnt, lane, total);
-            EPP_MTL_CNT(tl_q, total);
-            // append in windows that fit the queue (one unless the edges are very long)
-            for (uint32_t done = 0; done < total;) {
-                if (qn == (uint32_t)kQueueV5) flush();
-                const uint32_t take = min((uint32_t)kQueueV5 - qn, total - done);
-                if (cnt && off < done + take && off + cnt > done) {
-                    uint32_t jj = off;
-#pragma unroll
-                    for (int w = 0; w < W; ++w) {
-                        uint32_t m = cand[w];
-                        while (m) {
-                            const uint32_t bit = (uint32_t)__builtin_ctz(m);
-                            m &= m - 1u;
-                            if (jj >= done && jj < done + take)
-                                queue[qn + jj - done] = (uint32_t)ids[32 * w + bit] << 6 | (uint32_t)lane;
-                            ++jj;
-                        }
-                    }
-                }
-                wave_lds_sync();
-                qn += take;
-                done += take;
-            }
-            EPP_MTL_ADD(tl_c, tl_u);
         }
         EPP_MTL_ADD(tl_walk, tl_b);
         flush();

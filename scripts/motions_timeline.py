@@ -34,7 +34,7 @@ kernel = sys.argv[1] if len(sys.argv) > 1 else "v5"
 if kernel == "v4":
     os.environ["EPP_MOTIONS_KERNEL"] = "v4"
 names = (("walk cycles", "flush cycles", "total cycles", "entries", "queued", "cell pairs") if kernel == "v4" else
-         ("filter+queue", "flush cycles", "total cycles", "prefilter", "pairs", "push"))
+         ("filter+queue", "flush cycles", "total cycles", "cand loop", "pairs", "staging"))
 for mode in (0, 1):
     for r in range(20):
         w.check_motions_dev(d1.ptr, d2.ptr, N, 0, mode, dv.ptr)
