@@ -114,6 +114,13 @@ struct WorldView {
 
 constexpr int kSlabMaxWords = 32;              // tiles of up to 1024 OBBs
 constexpr size_t kSlabBudget = 40 * 1024;      // bytes of tile tables
+// Words from one slab row of a tile to the next: the row width W rounded up to an odd
+// number, so a wave's row gathers spread over all the LDS banks (an even stride would use
+// half of them).
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+constexpr int slab_row_stride(int w) { return (w & 1) ? w : w + 1; }
 
 // Global slab index along one axis: the same float operations on host and device, monotone in p
 // (fmaf is correctly rounded), so an AABB overlap in doubles implies an overlap of the

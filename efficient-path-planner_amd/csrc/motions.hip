@@ -450,7 +450,7 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
                                                      uint8_t* __restrict__ valid, uint32_t rec_bytes,
                                                      uint32_t tile_bytes) {
     constexpr int BLOCK = 1024;
-    constexpr int STRIDE = W + 1;
+    constexpr int STRIDE = slab_row_stride(W);
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     EPP_MTL_DECL;
     {
@@ -488,6 +488,9 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
     const double rg = wv->r_gate, ro = wv->r_obst;
     const bool cp = can_pass != 0;
     __syncthreads();
+#ifdef EPP_MOTIONS_TL
+    tl_c = __builtin_readcyclecounter() - tl_t0;  // staging
+#endif
 #ifdef EPP_MOTIONS_TL
     tl_c = __builtin_readcyclecounter() - tl_t0;  // staging
 #endif

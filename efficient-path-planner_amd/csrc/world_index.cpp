@@ -387,7 +387,7 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
     float so[3] = {0, 0, 0}, si[3] = {0, 0, 0};
     std::vector<int> gsl((size_t)n * 6);  // per OBB: global slab lo / hi per axis
     auto tile_words = [](int s_, int w_) {
-        return (uint32_t)((6 * s_ * (w_ + 1) + 3 * w_ + 16 * w_ + 3) & ~3);
+        return (uint32_t)((6 * s_ * slab_row_stride(w_) + 3 * w_ + 16 * w_ + 3) & ~3);
     };
     auto place = [&](int t_, int sl_) {  // slab ranges for (T, S); returns the largest tile population
         const int s_ = 1 << sl_;
@@ -428,7 +428,7 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
         S = 1 << SL;
         place(T, SL);
         tw = tile_words(S, W);
-        const int stride = W + 1;
+        const int stride = slab_row_stride(W);
         slab.assign((size_t)T * T * tw, 0u);
         std::vector<int> fill_n((size_t)T * T, 0);
         for (int i = 0; i < n; ++i) {

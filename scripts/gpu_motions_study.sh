@@ -6,5 +6,6 @@ timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 for cfg in "scripts/dbg/libepp_head.so" "" "scripts/dbg/libepp_head.so" ""; do
   timeout -k 10 120 python scripts/motions_ab.py $cfg || exit $?
 done
+[ "${STUDY_QUICK:-0}" = 1 ] && exit 0
 timeout -k 10 120 python scripts/motions_timeline.py v5 || exit $?
 bash scripts/gpu_pmc_motions.sh || exit $?
