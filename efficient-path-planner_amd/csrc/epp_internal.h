@@ -114,6 +114,8 @@ struct WorldView {
 
 constexpr int kSlabMaxWords = 32;              // tiles of up to 1024 OBBs
 constexpr size_t kSlabBudget = 40 * 1024;      // bytes of tile tables
+constexpr size_t kSlabBudgetMax = 64 * 1024;   // ... when the records leave LDS room
+constexpr size_t kMotionsLdsFree = 150 * 1024 - 16 * (256 * 4 + 64);  // k_motions_v5 LDS less its wave queues
 // Words from one slab row of a tile to the next: the row width W rounded up to an odd
 // number, so a wave's row gathers spread over all the LDS banks (an even stride would use
 // half of them).

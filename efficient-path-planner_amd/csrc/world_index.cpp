@@ -386,6 +386,12 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
     uint32_t tw = 0;
     float so[3] = {0, 0, 0}, si[3] = {0, 0, 0};
     std::vector<int> gsl((size_t)n * 6);  // per OBB: global slab lo / hi per axis
+    // tile bytes: kSlabBudget, or up to kSlabBudgetMax while the records, the tiles and the
+    // wave queues of k_motions_v5 still fit its LDS budget (finer slabs, fewer candidates)
+    const size_t slab_budget = std::max<size_t>(
+        kSlabBudget, std::min<size_t>(kSlabBudgetMax, kMotionsLdsFree > (size_t)n * kRecDoubles * 8
+                                                          ? kMotionsLdsFree - (size_t)n * kRecDoubles * 8
+                                                          : 0));
     auto tile_words = [](int s_, int w_) {
         return (uint32_t)((6 * s_ * slab_row_stride(w_) + 3 * w_ + 16 * w_ + 3) & ~3);
     };
@@ -416,7 +422,7 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
         for (int w_ = 1; w_ <= kSlabMaxWords && !W; w_ *= 2)
             for (int t_ = 1; t_ <= 16 && !W; ++t_) {
                 int sl_ = 6;
-                while (sl_ >= min_sl && (size_t)t_ * t_ * tile_words(1 << sl_, w_) * 4 > kSlabBudget) --sl_;
+                while (sl_ >= min_sl && (size_t)t_ * t_ * tile_words(1 << sl_, w_) * 4 > slab_budget) --sl_;
                 if (sl_ < min_sl) break;
                 if (place(t_, sl_) <= 32 * w_) {
                     W = w_;
