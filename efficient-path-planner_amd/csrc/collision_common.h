@@ -414,7 +414,11 @@ __device__ __forceinline__ bool d32_pair_hit(const double* rec, const double ps[
         if (b == 0.0) {
             if (!(u0 <= 0.0 && 0.0 <= u1)) t1 = -1.0;
         } else {
-            const double v0 = u0 / b, v1 = u1 / b;
+            // (a bound, not a decision: the reciprocal by v_rcp_f64 and one Newton step,
+            // ~1e-15 relative, far inside the slack eta)
+            double ib = __builtin_amdgcn_rcp(b);
+            ib = fma(ib, fma(-b, ib, 1.0), ib);
+            const double v0 = u0 * ib, v1 = u1 * ib;
             t0 = fmax(t0, fmin(v0, v1));
             t1 = fmin(t1, fmax(v0, v1));
         }

@@ -491,9 +491,6 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
 #ifdef EPP_MOTIONS_TL
     tl_c = __builtin_readcyclecounter() - tl_t0;  // staging
 #endif
-#ifdef EPP_MOTIONS_TL
-    tl_c = __builtin_readcyclecounter() - tl_t0;  // staging
-#endif
     const int64_t stride = (int64_t)gridDim.x * BLOCK;
     for (int64_t i0 = (int64_t)blockIdx.x * BLOCK + wave * 64; i0 < n; i0 += stride) {
         const int64_t i = i0 + lane;
