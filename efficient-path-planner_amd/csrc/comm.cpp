@@ -1,8 +1,8 @@
 // comm.cpp — the multi-track path's one exchange step over RCCL (xGMI): every rank plans
 // its own track, then the final waypoint sets are all-gathered (the
-// reference has no multi-GPU code).  RCCL is opened at first use (dlopen of
-// librccl.so.1: the one already in the process, e.g. PyTorch's, or ROCm's), so the
-// library does not depend on it unless the exchange is used.
+// reference has no multi-GPU code).  RCCL is opened at first use (dlopen of the
+// librccl next to the HIP runtime this library runs on), so the library does not depend
+// on it unless the exchange is used.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -32,8 +32,26 @@ const Rccl* rccl() {
     static Rccl r;
     static std::once_flag once;
     std::call_once(once, [] {
-        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
-            r.h = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+        // The RCCL that belongs to the HIP runtime this library is bound to: the one in the
+        // directory of the loaded libamdhip64 (ROCm's librccl.so.1, or PyTorch's bundled
+        // librccl.so when PyTorch's runtime came first).  A process may hold both runtimes
+        // (this library loaded before PyTorch): a bare dlopen("librccl.so.1") would then
+        // return PyTorch's RCCL, whose runtime does not know this library's buffers
+        // ("no ROCm-capable device").  RTLD_LOCAL: no symbol interposition either way.
+        std::vector<std::string> names;
+        Dl_info info;
+        if (dladdr(reinterpret_cast<void*>(&hipGetDevice), &info) && info.dli_fname) {
+            std::string dir(info.dli_fname);
+            const size_t slash = dir.rfind('/');
+            if (slash != std::string::npos) {
+                dir.resize(slash + 1);
+                names.push_back(dir + "librccl.so.1");
+                names.push_back(dir + "librccl.so");
+            }
+        }
+        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) names.push_back(name);
+        for (const std::string& name : names) {
+            r.h = dlopen(name.c_str(), RTLD_NOW | RTLD_LOCAL);
             if (r.h) break;
         }
         if (!r.h) return;

@@ -20,7 +20,7 @@ import pytest
 import oracle as O
 from eppamd import capi, config, synth
 
-from conftest import CONFIG
+from conftest import CONFIG, ROOT
 
 pytestmark = pytest.mark.gpu
 
@@ -643,6 +643,19 @@ def test_comm_single_rank_allgather():
     (ca,) = capi.Comm.init_all([0])
     assert np.array_equal(ca.allgather_waypoints(wp[:5])[0], wp[:5])
     ca.close()
+
+
+@pytest.mark.parametrize("order", ["no-torch", "epp-first", "torch-first"])
+def test_comm_any_import_order(order):
+    """The exchange step works whichever HIP runtime the process loaded first: libepp.so
+    before PyTorch leaves two runtimes (and two RCCLs) in the process, and epp_comm must
+    use the RCCL of its own runtime (scripts/rccl_probe.py, one process per order)."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "rccl_probe.py"), order],
+                       capture_output=True, text=True, timeout=120)
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith(order)]
+    assert r.returncode == 0 and line and line[-1].split()[1] == "ok", (r.stdout[-2000:], r.stderr[-2000:])
 
 
 def test_plan_tracks_across_devices(track, geom):
