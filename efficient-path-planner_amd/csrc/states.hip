@@ -441,6 +441,9 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
         const uint32_t idx = __umul24(__umul24(cz, ny) + cy, nx) + cx;
         return C8 ? (uint32_t)cls_base[idx] : (uint32_t)reinterpret_cast<const uint16_t*>(cls_base)[idx];
     };
+#ifdef EPP_STATES_TL
+    uint32_t tl_needy = 0, tl_pairs = 0;  // (diagnostics) queued states and pairs
+#endif
     auto process = [&](int64_t gg, const double (&v)[NV]) {
         const bool live = gg < groups;
         uint32_t c[SPL];
@@ -493,6 +496,10 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
                 const uint32_t cnt = hq & 4095u, first = hq >> 12;
                 uint32_t ptot;
                 const uint32_t poff = wave_excl_scan(cnt, lane, ptot);
+#ifdef EPP_STATES_TL
+                tl_needy += tq;
+                tl_pairs += ptot;
+#endif
                 bool hit_e = false;
                 if (ptot <= 128u) {
                     // one (state, candidate) pair per lane and round (two rounds at most):
@@ -591,7 +598,9 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
         unsigned hw;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
         const int w_ = (int)((blockIdx.x * BLOCK + threadIdx.x) >> 6);
-        if (w_ < kTlWaves) g_states_tl[w_][5] = hw;
+        if (w_ < kTlWaves)
+            g_states_tl[w_][5] = hw | ((unsigned long long)min(tl_needy, 65535u) << 32) |
+                                 ((unsigned long long)min(tl_pairs, 65535u) << 48);
     }
 #endif
     if (blockIdx.x == 0 && threadIdx.x < (int)(n - SPL * groups)) {  // tail: the last n % SPL states

@@ -51,3 +51,8 @@ v = np.concatenate([(t[:, 0] - t[:, 0].min()) * 10 for t in rows]) / 1000.0
 print(f"{'entry':16s} p50 {np.percentile(v, 50):6.2f} max {v.max():6.2f} us")
 ex = np.concatenate([(t[:, 3] - t[:, 2]) * 10 for t in rows]) / 1000.0
 print(f"exact path per wave: p50 {np.percentile(ex, 50):.2f} p90 {np.percentile(ex, 90):.2f} max {ex.max():.2f} us")
+nd = np.concatenate([(t[:, 5] >> 32) & 0xFFFF for t in rows])
+pr = np.concatenate([(t[:, 5] >> 48) & 0xFFFF for t in rows])
+print(f"queued states per wave: p50 {np.percentile(nd, 50):.0f} p90 {np.percentile(nd, 90):.0f} max {nd.max()}"
+      f"; pairs per wave: p50 {np.percentile(pr, 50):.0f} p90 {np.percentile(pr, 90):.0f} max {pr.max()}"
+      f"; > 64 pairs: {np.mean(pr > 64):.2f}, > 128: {np.mean(pr > 128):.3f}")
