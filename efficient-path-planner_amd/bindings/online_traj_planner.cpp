@@ -341,6 +341,7 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["ms"] = s.ms;
             d["ms_device"] = s.ms_device;
             d["ms_search"] = s.ms_search;
+            d["attempts"] = s.attempts;
             return d;
         })
         .def("get_checkpoints", [](const epp::OnlineTrajGenerator& self) {

@@ -1,0 +1,50 @@
+"""Full-plan (C4) breakdown (diagnostics): one track through OnlineTrajGenerator.
+pre_compute_traj as bench.py runs it, timed per call, with the planner's own split (device
+pipeline vs host search, summed over the segments) and the planner call alone; under the
+planner thread counts given as arguments (EPP_PLAN_THREADS, each in its own process)."""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "efficient-path-planner_amd")]
+
+if len(sys.argv) > 1 and sys.argv[1] == "--child":
+    import numpy as np
+    import online_traj_planner as otp
+    from eppamd import config, synth
+    cfg = config.load(os.path.join(ROOT, "configs", "config.json"))
+    cfg["world_properties"]["lower_bound"] = [-6, -6, 0]
+    cfg["world_properties"]["upper_bound"] = [6, 6, 2]
+    cfg["path_planner_properties"]["samples_fmt"] = 65536
+    geom = config.geometry(cfg)
+    fd, path = tempfile.mkstemp(suffix=".json")
+    with os.fdopen(fd, "w") as f:
+        json.dump(cfg, f)
+    gates, obstacles = synth.track_world(100)
+    cps = synth.gate_checkpoints(gates, geom.gate_height, 0.55)
+    otg = otp.OnlineTrajGenerator(cps[0], cps[-1], gates, obstacles, path)
+    otg.pre_compute_traj(0.0)
+    ts, st = [], []
+    for _ in range(30):
+        t = time.perf_counter()
+        otg.pre_compute_traj(0.0)
+        ts.append((time.perf_counter() - t) * 1e3)
+        st.append(otg.planner_stats())
+    os.unlink(path)
+    print(f"threads {os.environ.get('EPP_PLAN_THREADS', '4')}: pre_compute_traj p50 {np.median(ts):.2f} ms "
+          f"(mean {np.mean(ts):.2f}, min {min(ts):.2f}); planner: ms {np.median([s['ms'] for s in st]):.2f}, device sum "
+          f"{np.median([s['ms_device'] for s in st]):.2f}, search sum {np.median([s['ms_search'] for s in st]):.2f}",
+          flush=True)
+    order = np.argsort(ts)[::-1][:6]
+    print("   slowest:", ", ".join(f"{ts[i]:.1f} ms (attempts {st[i]['attempts']}, states {st[i]['states_sampled']})"
+                                   for i in order), flush=True)
+else:
+    for t in (sys.argv[1:] or ["4"]):
+        env = dict(os.environ, EPP_PLAN_THREADS=t)
+        r = subprocess.run([sys.executable, __file__, "--child"], env=env, timeout=120)
+        if r.returncode:
+            sys.exit(r.returncode)
