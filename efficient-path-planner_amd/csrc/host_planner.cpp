@@ -123,12 +123,13 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     const size_t ws_bytes = (size_t)epp_knn_workspace_size((int32_t)max_nodes);
     const size_t cws_bytes = (size_t)epp_compact_workspace_size((int64_t)n_s);
     ts.reset(ThreadScratch::rounded(n_s * 24) + ThreadScratch::rounded(n_s) + ThreadScratch::rounded(max_nodes * 24) +
-             ThreadScratch::rounded(8) + ThreadScratch::rounded(m_max * 4) + 2 * ThreadScratch::rounded(m_max * 24) +
+             ThreadScratch::rounded(8) + ThreadScratch::rounded(16) + ThreadScratch::rounded(m_max * 4) + 2 * ThreadScratch::rounded(m_max * 24) +
              ThreadScratch::rounded(m_max) + ThreadScratch::rounded(ws_bytes) + ThreadScratch::rounded(cws_bytes));
     double* d_s = static_cast<double*>(ts.carve(n_s * 24));
     uint8_t* d_v = static_cast<uint8_t*>(ts.carve(n_s));
     double* d_nodes = static_cast<double*>(ts.carve(max_nodes * 24));
     int64_t* d_cnt = static_cast<int64_t*>(ts.carve(8));
+    int64_t* d_ecnt = static_cast<int64_t*>(ts.carve(16));
     int32_t* d_nbr = static_cast<int32_t*>(ts.carve(m_max * 4));
     double* d_e1 = static_cast<double*>(ts.carve(m_max * 24));
     double* d_e2 = static_cast<double*>(ts.carve(m_max * 24));
@@ -150,11 +151,16 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     check(epp_knn_ws(d_nodes, n, k, 0.0, d_nbr, d_ws, ws_bytes, st), "knn");
     check(epp_knn_edges(d_nodes, d_nbr, n, k, d_e1, d_e2, st), "edges");
     check(epp_check_motions(w, d_e1, d_e2, (int64_t)m, canPass ? 1 : 0, 0, d_ev, st), "motion check");
-    check(epp_mask_edges(d_nbr, d_ev, (int64_t)m, st), "mask edges");  // failed motions -> -1
+    // failed motions -> -1; the valid edges, and those into the goal (node 1)
+    check(epp_mask_edges_count(d_nbr, d_ev, (int64_t)m, 1, d_ecnt, st), "mask edges");
     // node coordinates and the masked k-NN table into pinned host staging
     const double* nodes = static_cast<const double*>(ts.pinned(0, (size_t)n * 24));
     const int32_t* nbr = static_cast<const int32_t*>(ts.pinned(1, m * 4));
     check(epp_memcpy_d2h(const_cast<double*>(nodes), d_nodes, (uint64_t)n * 24, st), "download");
+    int64_t ecnt[2] = {0, 0};
+    check(epp_memcpy_d2h(ecnt, d_ecnt, 16, st), "download");
+    const int64_t n_valid_edges = ecnt[0];
+    const bool goal_has_forward_edge = ecnt[1] > 0;
     check(epp_memcpy_d2h(const_cast<int32_t*>(nbr), d_nbr, m * 4, st), "download");
     const auto t_dev1 = std::chrono::steady_clock::now();
     // ---- 3. shortest path over the valid edges, start = 0, goal = 1 ----------------------
@@ -163,8 +169,6 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     // edges alone, read straight from the k-NN table (no graph build: A* touches only
     // the nodes it expands); only if the goal is not reached that way, again over the
     // symmetrised graph (reverse edges added as a CSR).
-    int64_t n_valid_edges = 0;
-    for (size_t e = 0; e < m; ++e) n_valid_edges += nbr[e] >= 0 ? 1 : 0;
     {
         std::lock_guard<std::mutex> lk(g_stats_mu);
         stats_.states_sampled += samples;
@@ -212,7 +216,9 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
         }
         return false;
     };
-    if (!astar(false)) {
+    // (no forward edge into the goal: the forward pass cannot reach it — it would only
+    // explore start's whole component first; same result, so go straight to the second)
+    if (!goal_has_forward_edge || !astar(false)) {
         roff.assign(n + 1, 0);
         for (size_t e = 0; e < m; ++e)
             if (nbr[e] >= 0) ++roff[nbr[e] + 1];

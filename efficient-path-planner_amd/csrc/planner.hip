@@ -1026,6 +1026,34 @@ __global__ void k_mask_edges(int32_t* __restrict__ nbr, const uint8_t* __restric
     if (e < m && !valid[e]) nbr[e] = -1;
 }
 
+// The same, plus count[0] += the surviving edges (entries >= 0 after masking) and
+// count[1] += the surviving edges into node `target`: wave popcounts, one atomic per
+// 256-thread block and counter.
+__global__ __launch_bounds__(256) void k_mask_edges_count(int32_t* __restrict__ nbr, const uint8_t* __restrict__ valid,
+                                                          int64_t m, int32_t target,
+                                                          unsigned long long* __restrict__ count) {
+    __shared__ uint32_t part[8];
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    bool keep = false, into = false;
+    if (e < m) {
+        const int32_t v = nbr[e];
+        if (!valid[e]) nbr[e] = -1;
+        keep = valid[e] && v >= 0;
+        into = keep && v == target;
+    }
+    const uint32_t c = (uint32_t)__popcll(__ballot(keep)), ci = (uint32_t)__popcll(__ballot(into));
+    if ((threadIdx.x & 63) == 0) {
+        part[threadIdx.x >> 6] = c;
+        part[4 + (threadIdx.x >> 6)] = ci;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        const uint32_t* p = part + 4 * threadIdx.x;
+        const uint32_t t = p[0] + p[1] + p[2] + p[3];
+        if (t) atomicAdd(count + threadIdx.x, (unsigned long long)t);
+    }
+}
+
 epp_status last(const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -1186,6 +1214,20 @@ epp_status epp_mask_edges(int32_t* nbr, const uint8_t* valid, int64_t m, void* s
     hipLaunchKernelGGL(k_mask_edges, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, (hipStream_t)stream, nbr,
                        valid, m);
     return last("epp_mask_edges");
+}
+
+epp_status epp_mask_edges_count(int32_t* nbr, const uint8_t* valid, int64_t m, int32_t target, int64_t* count,
+                                void* stream) {
+    if (m < 0 || !count || (m > 0 && (!nbr || !valid))) {
+        set_error("epp_mask_edges_count: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(count, 0, 2 * sizeof(int64_t), s) != hipSuccess) return last("epp_mask_edges_count");
+    if (m == 0) return EPP_OK;
+    hipLaunchKernelGGL(k_mask_edges_count, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, nbr, valid, m, target,
+                       reinterpret_cast<unsigned long long*>(count));
+    return last("epp_mask_edges_count");
 }
 
 epp_status epp_knn_edges(const double* nodes, const int32_t* nbr, int32_t n, int32_t k, double* s1,

@@ -103,6 +103,7 @@ def lib() -> C.CDLL:
             "epp_compact_workspace_size": (C.c_uint64, [i64]),
             "epp_compact_states_ws": (i32, [vp, vp, i64, vp, vp, vp, C.c_uint64, vp]),
             "epp_mask_edges": (i32, [vp, vp, i64, vp]),
+            "epp_mask_edges_count": (i32, [vp, vp, i64, i32, vp, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(l, name)
@@ -122,7 +123,7 @@ EXPORTED = [
     "epp_check_states_mindist", "epp_check_motions", "epp_minsnap_batch", "epp_sample_count",
     "epp_sample_batch", "epp_generate_trajectory_host", "epp_host_free", "epp_sample_uniform", "epp_knn",
     "epp_knn_bruteforce", "epp_knn_grid", "epp_knn_workspace_size", "epp_knn_ws", "epp_knn_grid_ws",
-    "epp_knn_edges", "epp_compact_states", "epp_mask_edges", "epp_optimal_trajectory_host",
+    "epp_knn_edges", "epp_compact_states", "epp_mask_edges", "epp_mask_edges_count", "epp_optimal_trajectory_host",
     "epp_spline_trajectory_host", "epp_compact_workspace_size", "epp_compact_states_ws",
     "epp_graph_begin", "epp_graph_end", "epp_graph_launch", "epp_graph_destroy", "epp_minsnap_batch_times",
     "epp_generate_trajectory_times_host", "epp_world_generation", "epp_world_build_index", "epp_comm_unique_id", "epp_comm_init",
@@ -464,6 +465,18 @@ def mask_edges(nbr: np.ndarray, valid: np.ndarray) -> np.ndarray:
     check(lib().epp_mask_edges(d_n.ptr, d_v.ptr, nbr.size, None))
     sync()
     return d_n.download(np.int32, nbr.size).reshape(nbr.shape)
+
+
+def mask_edges_count(nbr: np.ndarray, valid: np.ndarray, target: int = 1):
+    """epp_mask_edges_count: (nbr with -1 where valid == 0, entries >= 0 afterwards,
+    entries == target afterwards)."""
+    nbr = np.ascontiguousarray(np.asarray(nbr, np.int32))
+    valid = np.ascontiguousarray(np.asarray(valid, np.uint8).reshape(nbr.shape))
+    d_n, d_v, d_c = DeviceBuffer.from_array(nbr), DeviceBuffer.from_array(valid), DeviceBuffer(16)
+    check(lib().epp_mask_edges_count(d_n.ptr, d_v.ptr, nbr.size, target, d_c.ptr, None))
+    sync()
+    c = d_c.download(np.int64, 2)
+    return d_n.download(np.int32, nbr.size).reshape(nbr.shape), int(c[0]), int(c[1])
 
 
 def knn_edges(nodes: np.ndarray, nbr: np.ndarray):

@@ -218,6 +218,11 @@ epp_status epp_compact_states_ws(const double* xyz, const uint8_t* valid, int64_
                                  void* ws, uint64_t ws_bytes, void* stream);
 /* nbr[e] = -1 where valid[e] == 0 (edges that failed the motion check), in place. */
 epp_status epp_mask_edges(int32_t* nbr, const uint8_t* valid, int64_t m, void* stream);
+/* The same, and count[0..1] (device memory, set by the call) = the entries of nbr that are
+ * >= 0 afterwards and those equal to `target` (the planner's valid-edge statistic and the
+ * goal's incoming edges, without a host pass over nbr). */
+epp_status epp_mask_edges_count(int32_t* nbr, const uint8_t* valid, int64_t m, int32_t target, int64_t* count,
+                                void* stream);
 
 /* ---- multi-GPU: the multi-track plan's exchange step (RCCL over xGMI) --------------- */
 /* BASELINE config 4 / SURVEY §8e: every rank (one GPU) plans its own track; the final

@@ -35,16 +35,19 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
         ts.append((time.perf_counter() - t) * 1e3)
         st.append(otg.planner_stats())
     os.unlink(path)
-    print(f"threads {os.environ.get('EPP_PLAN_THREADS', '4')}: pre_compute_traj p50 {np.median(ts):.2f} ms "
+    print(f"threads {os.environ.get('EPP_PLAN_THREADS', '4')} writer {os.environ.get('EPP_PATH_WRITER', '1')}: pre_compute_traj p50 {np.median(ts):.2f} ms "
           f"(mean {np.mean(ts):.2f}, min {min(ts):.2f}); planner: ms {np.median([s['ms'] for s in st]):.2f}, device sum "
           f"{np.median([s['ms_device'] for s in st]):.2f}, search sum {np.median([s['ms_search'] for s in st]):.2f}",
           flush=True)
     order = np.argsort(ts)[::-1][:6]
-    print("   slowest:", ", ".join(f"{ts[i]:.1f} ms (attempts {st[i]['attempts']}, states {st[i]['states_sampled']})"
+    print("   slowest:", ", ".join(f"#{i} {ts[i]:.1f} ms (attempts {st[i]['attempts']}, states {st[i]['states_sampled']})"
                                    for i in order), flush=True)
 else:
     for t in (sys.argv[1:] or ["4"]):
+        t, _, pw = t.partition(":")  # "4" or "4:0" (EPP_PATH_WRITER=0)
         env = dict(os.environ, EPP_PLAN_THREADS=t)
+        if pw:
+            env["EPP_PATH_WRITER"] = pw
         r = subprocess.run([sys.executable, __file__, "--child"], env=env, timeout=120)
         if r.returncode:
             sys.exit(r.returncode)

@@ -523,6 +523,12 @@ def test_mask_edges():
     nbr = rs.randint(-1, 1000, (777, 16)).astype(np.int32)
     valid = (rs.rand(777, 16) < 0.7).astype(np.uint8)
     assert np.array_equal(capi.mask_edges(nbr, valid), np.where(valid.astype(bool), nbr, -1))
+    for n in (777, 1, 64, 65537):  # ragged, single, one wave, several blocks
+        nb = rs.randint(-1, 1000, (n, 16)).astype(np.int32)
+        va = (rs.rand(n, 16) < 0.7).astype(np.uint8)
+        want = np.where(va.astype(bool), nb, -1)
+        got, cnt, into = capi.mask_edges_count(nb, va, 7)
+        assert np.array_equal(got, want) and cnt == int((want >= 0).sum()) and into == int((want == 7).sum())
 
 
 def test_online_update_while_replanning_throws(track):
