@@ -1027,29 +1027,37 @@ __global__ void k_mask_edges(int32_t* __restrict__ nbr, const uint8_t* __restric
 }
 
 // The same, plus count[0] += the surviving edges (entries >= 0 after masking) and
-// count[1] += the surviving edges into node `target`: wave popcounts, one atomic per
-// 256-thread block and counter.
-__global__ __launch_bounds__(256) void k_mask_edges_count(int32_t* __restrict__ nbr, const uint8_t* __restrict__ valid,
-                                                          int64_t m, int32_t target,
-                                                          unsigned long long* __restrict__ count) {
-    __shared__ uint32_t part[8];
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    bool keep = false, into = false;
-    if (e < m) {
+// count[1] += the surviving edges into node `target`.  Grid-stride over at most one
+// 1024-thread block per CU, wave popcounts, one atomic per block and counter (an atomic
+// per 256 edges put thousands on one address: ~45 us for 1M edges).
+constexpr int kMaskThreads = 1024;
+__global__ __launch_bounds__(kMaskThreads) void k_mask_edges_count(int32_t* __restrict__ nbr,
+                                                                   const uint8_t* __restrict__ valid, int64_t m,
+                                                                   int32_t target,
+                                                                   unsigned long long* __restrict__ count) {
+    __shared__ uint32_t part[2][kMaskThreads / 64];
+    uint32_t c = 0, ci = 0;
+    for (int64_t e = (int64_t)blockIdx.x * kMaskThreads + threadIdx.x; e < m;
+         e += (int64_t)gridDim.x * kMaskThreads) {  // (uniform trip count per wave but the last)
         const int32_t v = nbr[e];
-        if (!valid[e]) nbr[e] = -1;
-        keep = valid[e] && v >= 0;
-        into = keep && v == target;
+        const bool ok = valid[e] != 0;
+        if (!ok) nbr[e] = -1;
+        const bool keep = ok && v >= 0;
+        c += keep ? 1u : 0u;
+        ci += (keep && v == target) ? 1u : 0u;
     }
-    const uint32_t c = (uint32_t)__popcll(__ballot(keep)), ci = (uint32_t)__popcll(__ballot(into));
+    for (int o = 32; o > 0; o >>= 1) {
+        c += (uint32_t)__shfl_xor((int)c, o, 64);
+        ci += (uint32_t)__shfl_xor((int)ci, o, 64);
+    }
     if ((threadIdx.x & 63) == 0) {
-        part[threadIdx.x >> 6] = c;
-        part[4 + (threadIdx.x >> 6)] = ci;
+        part[0][threadIdx.x >> 6] = c;
+        part[1][threadIdx.x >> 6] = ci;
     }
     __syncthreads();
     if (threadIdx.x < 2) {
-        const uint32_t* p = part + 4 * threadIdx.x;
-        const uint32_t t = p[0] + p[1] + p[2] + p[3];
+        uint32_t t = 0;
+        for (int w = 0; w < kMaskThreads / 64; ++w) t += part[threadIdx.x][w];
         if (t) atomicAdd(count + threadIdx.x, (unsigned long long)t);
     }
 }
@@ -1225,7 +1233,8 @@ epp_status epp_mask_edges_count(int32_t* nbr, const uint8_t* valid, int64_t m, i
     hipStream_t s = (hipStream_t)stream;
     if (hipMemsetAsync(count, 0, 2 * sizeof(int64_t), s) != hipSuccess) return last("epp_mask_edges_count");
     if (m == 0) return EPP_OK;
-    hipLaunchKernelGGL(k_mask_edges_count, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, nbr, valid, m, target,
+    const int64_t blocks = std::min<int64_t>((m + kMaskThreads - 1) / kMaskThreads, 256);
+    hipLaunchKernelGGL(k_mask_edges_count, dim3((unsigned)blocks), dim3(kMaskThreads), 0, s, nbr, valid, m, target,
                        reinterpret_cast<unsigned long long*>(count));
     return last("epp_mask_edges_count");
 }
