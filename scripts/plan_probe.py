@@ -40,7 +40,8 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
           f"{np.median([s['ms_device'] for s in st]):.2f}, search sum {np.median([s['ms_search'] for s in st]):.2f}",
           flush=True)
     order = np.argsort(ts)[::-1][:6]
-    print("   slowest:", ", ".join(f"#{i} {ts[i]:.1f} ms (attempts {st[i]['attempts']}, states {st[i]['states_sampled']})"
+    print("   slowest:", ", ".join(f"#{i} {ts[i]:.1f} ms (planner {st[i]['ms']:.1f}, device {st[i]['ms_device']:.1f}, "
+                                   f"search {st[i]['ms_search']:.1f}, attempts {st[i]['attempts']})"
                                    for i in order), flush=True)
 else:
     for t in (sys.argv[1:] or ["4"]):
