@@ -235,14 +235,25 @@ __global__ __launch_bounds__(kBoundsThreads) void k_knn_scan(const KnnGrid* __re
     const int nc = gp->ncell;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     // tiles staged through LDS: coalesced loads and stores, kScanPer consecutive cells
-    // per thread for the scan; the carry runs across tiles
+    // per thread for the scan; the carry runs across tiles; the next tile's loads are in
+    // flight while this one is scanned (one workgroup: its load latency is the cost)
     int carry = 0;
+    int nxt[kScanPer];
+    auto fetch = [&](int t0) {
+#pragma unroll
+        for (int u = 0; u < kScanPer; ++u) {
+            const int i = t0 + u * kBoundsThreads + threadIdx.x;
+            nxt[u] = i < nc ? cnt[i] : 0;
+        }
+    };
+    fetch(0);
     for (int t0 = 0; t0 < nc; t0 += kScanTile) {  // block-uniform
 #pragma unroll
         for (int u = 0; u < kScanPer; ++u) {
             const int i = u * kBoundsThreads + threadIdx.x;
-            tile_v[i + (i >> 5)] = t0 + i < nc ? cnt[t0 + i] : 0;
+            tile_v[i + (i >> 5)] = nxt[u];
         }
+        if (t0 + kScanTile < nc) fetch(t0 + kScanTile);
         __syncthreads();
         int v[kScanPer], s = 0;
 #pragma unroll
