@@ -6,9 +6,12 @@
 //   s + (e - s) k/32, k = 1..32, each World::checkPointValidity(p, canPassGate))
 //
 // Kernels, chosen by what fits (epp_check_motions):
-//   k_motions_v4   analytic, coarse grid + records in LDS, lane-balanced list walk;
-//   k_motions_d32b discrete32, same staging, lane-balanced list walk per step;
-//   k_motions      generic (worlds too large for LDS): one lane per edge, L2-resident world.
+//   k_motions_small  batches of <= 1024 edges on worlds of <= 256 OBBs (small.hip);
+//   k_motions_v5     both modes, tile/slab bit-set candidate filter (records and tile rows
+//                    in LDS; worlds of <= 1024 OBBs per tile) — the default;
+//   k_motions_v4     analytic, coarse grid + records in LDS, lane-balanced list walk;
+//   k_motions_d32b   discrete32, same staging, lane-balanced list walk per step;
+//   k_motions        generic (worlds too large for LDS): one lane per edge, L2-resident world.
 #include "collision_common.h"
 
 namespace epp {
