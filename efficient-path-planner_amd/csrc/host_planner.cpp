@@ -149,8 +149,15 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     // ---- 2. k-NN graph + batched motion checks (MotionValidator::checkMotion) --------
     const size_t m = (size_t)n * k;
     check(epp_knn_ws(d_nodes, n, k, 0.0, d_nbr, d_ws, ws_bytes, st), "knn");
-    check(epp_knn_edges(d_nodes, d_nbr, n, k, d_e1, d_e2, st), "edges");
-    check(epp_check_motions(w, d_e1, d_e2, (int64_t)m, canPass ? 1 : 0, 0, d_ev, st), "motion check");
+    // motion checks straight off the k-NN table; small batches / worlds without tile tables
+    // through materialised endpoints
+    const epp_status ks = epp_check_knn_motions(w, d_nodes, d_nbr, n, k, canPass ? 1 : 0, 0, d_ev, st);
+    if (ks == EPP_ERR_UNSUPPORTED) {
+        check(epp_knn_edges(d_nodes, d_nbr, n, k, d_e1, d_e2, st), "edges");
+        check(epp_check_motions(w, d_e1, d_e2, (int64_t)m, canPass ? 1 : 0, 0, d_ev, st), "motion check");
+    } else {
+        check(ks, "motion check");
+    }
     // failed motions -> -1; the valid edges, and those into the goal (node 1)
     check(epp_mask_edges_count(d_nbr, d_ev, (int64_t)m, 1, d_ecnt, st), "mask edges");
     // node coordinates and the masked k-NN table into pinned host staging

@@ -447,11 +447,14 @@ __global__ __launch_bounds__(BLOCK) void k_motions_d32b(const WorldView* __restr
 // An edge is invalid iff some pair hits — the reference's answer.
 constexpr int kQueueV5 = 256;
 
-template <int W, int MODE>
+// IDX: the edges are given as a k-NN table instead of endpoint arrays — edge e runs from
+// node e / kk to node nbr[e] (s1 = the nodes; a missing neighbour, -1, is the degenerate
+// edge from the node to itself), as epp_knn_edges would lay them out.
+template <int W, int MODE, bool IDX>
 __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict__ wv, const double* __restrict__ s1,
-                                                     const double* __restrict__ s2, int64_t n, int can_pass,
-                                                     uint8_t* __restrict__ valid, uint32_t rec_bytes,
-                                                     uint32_t tile_bytes) {
+                                                     const double* __restrict__ s2, const int32_t* __restrict__ nbr,
+                                                     int kk, int64_t n, int can_pass, uint8_t* __restrict__ valid,
+                                                     uint32_t rec_bytes, uint32_t tile_bytes) {
     constexpr int BLOCK = 1024;
     constexpr int STRIDE = slab_row_stride(W);
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -500,10 +503,21 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
         const bool act = i < n;
         double s[3] = {0.0, 0.0, 0.0}, e[3] = {0.0, 0.0, 0.0};
         if (act) {
+            if (IDX) {
+                const int64_t u = i / kk;
+                const int32_t j = nbr[i];
+                const int64_t v = j < 0 ? u : (int64_t)j;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                s[k] = s1[3 * i + k];
-                e[k] = s2[3 * i + k];
+                for (int k = 0; k < 3; ++k) {
+                    s[k] = s1[3 * u + k];
+                    e[k] = s1[3 * v + k];
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    s[k] = s1[3 * i + k];
+                    e[k] = s2[3 * i + k];
+                }
             }
         }
         flags[lane] = 1;
@@ -648,6 +662,54 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
 
 using namespace epp;
 
+namespace {
+// k_motions_v5 when the world has tile tables and they, the records and the wave queues
+// fit the LDS budget; returns false (nothing launched) otherwise.
+bool launch_motions_v5(const epp_world* world, const WorldView& w, const double* s1, const double* s2,
+                       const int32_t* nbr, int kk, int64_t n, int32_t can_pass_gate, int32_t mode, uint8_t* valid,
+                       hipStream_t st) {
+    if (w.slab_n <= 0) return false;
+    const uint32_t recb5 = (uint32_t)(((size_t)w.n_obb * kRecDoubles * 8 + 15) & ~size_t(15));
+    const uint32_t tileb = (uint32_t)((size_t)w.tile_n * w.tile_n * w.tile_words * 4);
+    const uint32_t shm5 = recb5 + tileb + 16u * (kQueueV5 * 4 + 64);
+    if (shm5 > kLdsBudget) return false;
+    const int per_cu = std::max(1, std::min(2, (int)((160u * 1024u) / shm5)));
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + 1023) / 1024, (int64_t)cu_count() * per_cu));
+    const WorldView* dw = world_dview(world);
+#define EPP_LAUNCH_M5(WW, MM, II)                                                                                 \
+    do {                                                                                                          \
+        allow_lds(k_motions_v5<WW, MM, II>);                                                                      \
+        hipLaunchKernelGGL((k_motions_v5<WW, MM, II>), dim3(grid), dim3(1024), shm5, st, dw, s1, s2, nbr, kk, n, \
+                           can_pass_gate, valid, recb5, tileb);                                                   \
+    } while (0)
+#define EPP_LAUNCH_M5W(MM, II)                       \
+    switch (w.slab_w) {                              \
+        case 1: EPP_LAUNCH_M5(1, MM, II); break;     \
+        case 2: EPP_LAUNCH_M5(2, MM, II); break;     \
+        case 4: EPP_LAUNCH_M5(4, MM, II); break;     \
+        case 8: EPP_LAUNCH_M5(8, MM, II); break;     \
+        case 16: EPP_LAUNCH_M5(16, MM, II); break;   \
+        default: EPP_LAUNCH_M5(32, MM, II); break;   \
+    }
+    if (nbr) {
+        if (mode == 0) {
+            EPP_LAUNCH_M5W(0, true)
+        } else {
+            EPP_LAUNCH_M5W(1, true)
+        }
+    } else {
+        if (mode == 0) {
+            EPP_LAUNCH_M5W(0, false)
+        } else {
+            EPP_LAUNCH_M5W(1, false)
+        }
+    }
+#undef EPP_LAUNCH_M5W
+#undef EPP_LAUNCH_M5
+    return true;
+}
+}  // namespace
+
 extern "C" {
 
 // Kernel choice: small batches (<= kSmallMotions edges, <= kSmallMaxObbs OBBs) take the
@@ -688,39 +750,9 @@ epp_status epp_check_motions(const epp_world* world, const double* s1, const dou
     // per CU, and 1024 threads double the waves behind the LDS walk: v4 52 vs 69 us)
     // k_motions_v5 when the world has tile tables and they, the records and the queues fit
     const bool force_v4 = forced && std::string(forced) == "v4";
-    if (!generic && !force_v4 && w.slab_n > 0) {
-        const uint32_t recb5 = (uint32_t)(((size_t)w.n_obb * kRecDoubles * 8 + 15) & ~size_t(15));
-        const uint32_t tileb = (uint32_t)((size_t)w.tile_n * w.tile_n * w.tile_words * 4);
-        const uint32_t shm5 = recb5 + tileb + 16u * (kQueueV5 * 4 + 64);
-        if (shm5 <= kLdsBudget) {
-            const int per_cu = std::max(1, std::min(2, (int)((160u * 1024u) / shm5)));
-            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + 1023) / 1024, (int64_t)cu_count() * per_cu));
-            const WorldView* dw = world_dview(world);
-#define EPP_LAUNCH_M5(WW, MM)                                                                                   \
-    do {                                                                                                        \
-        allow_lds(k_motions_v5<WW, MM>);                                                                        \
-        hipLaunchKernelGGL((k_motions_v5<WW, MM>), dim3(grid), dim3(1024), shm5, st, dw, s1, s2, n, can_pass_gate, \
-                           valid, recb5, tileb);                                                                \
-    } while (0)
-#define EPP_LAUNCH_M5W(MM)                                    \
-    switch (w.slab_w) {                                       \
-        case 1: EPP_LAUNCH_M5(1, MM); break;                  \
-        case 2: EPP_LAUNCH_M5(2, MM); break;                  \
-        case 4: EPP_LAUNCH_M5(4, MM); break;                  \
-        case 8: EPP_LAUNCH_M5(8, MM); break;                  \
-        case 16: EPP_LAUNCH_M5(16, MM); break;                \
-        default: EPP_LAUNCH_M5(32, MM); break;                \
-    }
-            if (mode == 0) {
-                EPP_LAUNCH_M5W(0)
-            } else {
-                EPP_LAUNCH_M5W(1)
-            }
-#undef EPP_LAUNCH_M5W
-#undef EPP_LAUNCH_M5
-            return launch_error("epp_check_motions");
-        }
-    }
+    if (!generic && !force_v4 &&
+        launch_motions_v5(world, w, s1, s2, nullptr, 1, n, can_pass_gate, mode, valid, st))
+        return launch_error("epp_check_motions");
     const int eb = env_int("EPP_MOTIONS_BLOCK", 0);
     const int block = eb == 512 ? 512 : eb == 1024 ? 1024 : (2u * (front + recb + extra_for(512)) <= 160u * 1024u ? 512 : 1024);
     const uint32_t shm = front + recb + extra_for(block);
@@ -750,6 +782,28 @@ epp_status epp_check_motions(const epp_world* world, const double* s1, const dou
     else
         hipLaunchKernelGGL((k_motions<1>), dim3(grid), dim3(kBlock), 0, st, w, s1, s2, n, can_pass_gate, valid, aligned);
     return launch_error("epp_check_motions");
+}
+
+epp_status epp_check_knn_motions(const epp_world* world, const double* nodes, const int32_t* nbr, int32_t n,
+                                 int32_t k, int32_t can_pass_gate, int32_t mode, uint8_t* valid, void* stream) {
+    if (!world || n < 0 || k <= 0 || (n > 0 && (!nodes || !nbr || !valid)) || (mode != 0 && mode != 1)) {
+        set_error("epp_check_knn_motions: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    const int64_t m = (int64_t)n * k;
+    if (m == 0) return EPP_OK;
+    const SmallWorld sw = small_world(world);
+    if (small_motions(sw, m) || std::getenv("EPP_MOTIONS_KERNEL")) {
+        set_error("epp_check_knn_motions: not for this batch / world (use epp_knn_edges + epp_check_motions)");
+        return EPP_ERR_UNSUPPORTED;
+    }
+    if (const epp_status st = ensure_index(world)) return st;
+    if (!launch_motions_v5(world, world_view(world), nodes, nullptr, nbr, k, m, can_pass_gate, mode, valid,
+                           (hipStream_t)stream)) {
+        set_error("epp_check_knn_motions: not for this batch / world (use epp_knn_edges + epp_check_motions)");
+        return EPP_ERR_UNSUPPORTED;
+    }
+    return launch_error("epp_check_knn_motions");
 }
 
 #ifdef EPP_MOTIONS_TL

@@ -104,6 +104,7 @@ def lib() -> C.CDLL:
             "epp_compact_states_ws": (i32, [vp, vp, i64, vp, vp, vp, C.c_uint64, vp]),
             "epp_mask_edges": (i32, [vp, vp, i64, vp]),
             "epp_mask_edges_count": (i32, [vp, vp, i64, i32, vp, vp]),
+            "epp_check_knn_motions": (i32, [vp, vp, vp, i32, i32, i32, i32, vp, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(l, name)
@@ -123,7 +124,7 @@ EXPORTED = [
     "epp_check_states_mindist", "epp_check_motions", "epp_minsnap_batch", "epp_sample_count",
     "epp_sample_batch", "epp_generate_trajectory_host", "epp_host_free", "epp_sample_uniform", "epp_knn",
     "epp_knn_bruteforce", "epp_knn_grid", "epp_knn_workspace_size", "epp_knn_ws", "epp_knn_grid_ws",
-    "epp_knn_edges", "epp_compact_states", "epp_mask_edges", "epp_mask_edges_count", "epp_optimal_trajectory_host",
+    "epp_knn_edges", "epp_compact_states", "epp_mask_edges", "epp_mask_edges_count", "epp_check_knn_motions", "epp_optimal_trajectory_host",
     "epp_spline_trajectory_host", "epp_compact_workspace_size", "epp_compact_states_ws",
     "epp_graph_begin", "epp_graph_end", "epp_graph_launch", "epp_graph_destroy", "epp_minsnap_batch_times",
     "epp_generate_trajectory_times_host", "epp_world_generation", "epp_world_build_index", "epp_comm_unique_id", "epp_comm_init",

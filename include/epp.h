@@ -206,6 +206,13 @@ epp_status epp_knn_grid_ws(const double* nodes, int32_t n, int32_t k, double max
  * (s2 = s1 for a missing neighbour).  s1, s2: n k x 3. */
 epp_status epp_knn_edges(const double* nodes, const int32_t* nbr, int32_t n, int32_t k, double* s1,
                          double* s2, void* stream);
+/* The motion checks of a k-NN table without materialising its edges: valid[e] for edge e
+ * from node e / k to node nbr[e] (a missing neighbour, -1: the degenerate edge to itself),
+ * as epp_check_motions on epp_knn_edges' output would give.  EPP_ERR_UNSUPPORTED when the
+ * batch or world is not for the tile-filtered kernel (small batches, worlds without tile
+ * tables): then use epp_knn_edges + epp_check_motions. */
+epp_status epp_check_knn_motions(const epp_world* w, const double* nodes, const int32_t* nbr, int32_t n, int32_t k,
+                                 int32_t can_pass_gate, int32_t mode, uint8_t* valid, void* stream);
 /* Ordered stream compaction of the valid states (planner node list): out = xyz[i] for
  * valid[i] != 0, in index order; *n_out (device int64) = their count.  out holds n x 3. */
 epp_status epp_compact_states(const double* xyz, const uint8_t* valid, int64_t n, double* out, int64_t* n_out,

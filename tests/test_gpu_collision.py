@@ -539,3 +539,45 @@ def test_async_small_queries_across_updates(fworlds):
         assert np.array_equal(o_s.download(np.uint8, len(pts)), O.check_states(ref, rg, ro, pts, 1))
         assert np.array_equal(o_m.download(np.uint8, len(s1)), O.check_motions(ref, rg, ro, s1, s2, 0, 1, threads=8))
     L.epp_stream_destroy(st.value)
+
+
+@pytest.mark.parametrize("name", ["c2", "c3"])
+@pytest.mark.parametrize("filling", [False, True])
+def test_knn_motions_equal_materialised(cfg, geom, fworlds, name, filling):
+    """epp_check_knn_motions (edges read off a k-NN table, no endpoint arrays) gives the
+    flags of epp_knn_edges + epp_check_motions, both modes and can_pass_gate values,
+    missing neighbours (-1) and edges far longer than a tile included."""
+    if filling:
+        g_, rg, ro, ws = fworlds
+    else:
+        g_ = geom
+        rg, ro, ws = _worlds(cfg, geom)
+    gates, obstacles, (lo, hi) = ws[name]
+    w = capi.World(capi.build_obbs(g_, gates, obstacles), rg, ro)
+    rs = np.random.RandomState(11)
+    n, k = 6000, 16
+    nodes = rs.uniform(lo, hi, size=(n, 3))
+    near = np.clip(np.arange(n)[:, None] + rs.randint(-40, 41, size=(n, k)), 0, n - 1)
+    far = rs.randint(0, n, size=(n, k))  # long edges across many tiles
+    nbr = np.where(rs.rand(n, k) < 0.9, near, far).astype(np.int32)
+    nbr[rs.rand(n, k) < 0.03] = -1
+    s1, s2 = capi.knn_edges(nodes, nbr)
+    d_n, d_k, d_v = capi.DeviceBuffer.from_array(nodes), capi.DeviceBuffer.from_array(nbr), capi.DeviceBuffer(n * k)
+    for mode in (0, 1):
+        for cp in (0, 1):
+            want = w.check_motions(s1, s2, bool(cp), mode)
+            capi.check(capi.lib().epp_check_knn_motions(w.handle, d_n.ptr, d_k.ptr, n, k, cp, mode, d_v.ptr, None))
+            capi.sync()
+            got = d_v.download(np.uint8, n * k)
+            assert np.array_equal(got, want), (mode, cp, int((got != want).sum()))
+
+
+def test_knn_motions_unsupported_small_batch(cfg, geom):
+    rg, ro, ws = _worlds(cfg, geom)
+    gates, obstacles, (lo, hi) = ws["c2"]
+    w = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
+    nodes = np.random.RandomState(1).uniform(lo, hi, size=(8, 3))
+    nbr = np.zeros((8, 4), np.int32)
+    d_n, d_k, d_v = capi.DeviceBuffer.from_array(nodes), capi.DeviceBuffer.from_array(nbr), capi.DeviceBuffer(32)
+    rc = capi.lib().epp_check_knn_motions(w.handle, d_n.ptr, d_k.ptr, 8, 4, 0, 0, d_v.ptr, None)
+    assert rc == capi.EPP_ERR_UNSUPPORTED
