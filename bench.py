@@ -7,9 +7,14 @@ checks a FRESH batch of 1M states (a sampler streaming new samples): 16 resident
 (400 MB, larger than the 256 MB Infinity Cache) are rotated, so the timed kernels stream
 from HBM.  Inputs are resident in HBM before the timed region.
 
-Multi-GPU: one process per GPU (torchrun); every rank checks its own stream of states
-against its own copy of the world (independent samplers, no data-path collective:
-"scaling": "weak"); ranks synchronise with a barrier and the slowest rank's time is used.
+Multi-GPU: one process per GPU (torchrun, or `--gpus N` spawning its own ranks); every
+rank checks its own stream of states against its own copy of the world (independent
+samplers, no data-path collective: "scaling": "weak"); ranks synchronise with a barrier
+and the slowest rank's time is used.  The ranks' collectives (barrier, max over ranks, the
+waypoint all-gather) go through the product's own RCCL communicator (epp_comm_* in
+libepp.so, bootstrapped by a file rendezvous: eppamd/dist.py) — no torch in a GPU rank, so
+libepp runs on ROCm's HIP runtime at every N.  A leg that fails on one rank fails on every
+rank (Group.check / the all-gather's count -1) and the job exits non-zero.
 
 Full plan ms/track (the metric's second half, BASELINE configs[3] = C4): every rank plans
 its own randomised track (world seed 100 + rank, 8 gates, 24 obstacles, bounds
@@ -84,9 +89,13 @@ def main():
                     help="launch the timed steps from a host loop instead of replaying a captured HIP graph")
     ap.add_argument("--launcher-check", action="store_true",
                     help="CPU-only: run the rank launch + gloo exchange plumbing and print one JSON line")
+    ap.add_argument("--fail-rank", type=int, default=-1,
+                    help="with --launcher-check: this rank's (simulated) plan fails (error-protocol test)")
+    ap.add_argument("--fail-at", choices=("plan", "exchange"), default="plan",
+                    help="with --fail-rank: fail inside the plan leg (collective check) or at the all-gather (count -1)")
     args = ap.parse_args()
 
-    from eppamd.dist import Dist, env, spawn_ranks
+    from eppamd.dist import LegFailed, env, make_group, spawn_ranks
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # `bench.py --gpus N` without a launcher: one child process per GPU (rank = local
         # rank = GPU index), started before this process touches the GPU
@@ -95,15 +104,23 @@ def main():
     ws, rank, local = env()
     if ws != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws} (launch one process per GPU)")
-    if args.launcher_check:
-        return launcher_check(ws, rank, local, out_stream)
-    dist = Dist(ws, rank, local, "nccl")
+    try:
+        if args.launcher_check:
+            return launcher_check(ws, rank, local, out_stream, args.fail_rank, args.fail_at)
+        run(args, ws, rank, local, out_stream)
+    except LegFailed as e:
+        sys.exit(f"bench.py rank {rank}: {e}")
+
+
+def run(args, ws, rank, local, out_stream):
     import ctypes as C
 
     from eppamd import capi, config, synth
+    from eppamd.dist import make_group
 
     L = capi.lib()
     capi.check(L.epp_set_device(local))
+    dist = make_group(ws, rank, "rccl")  # the product's communicator (Solo at N = 1)
     stream = C.c_void_p()
     capi.check(L.epp_stream_create(C.byref(stream)))
     stream = stream.value
@@ -119,8 +136,9 @@ def main():
     # ---- the metric's second half and the side legs (before the headline's timed region)
     plan = full_plan(dist, rank, args.plan_reps) if not args.no_plan else None
     side, c5_inputs = {}, None
-    if not args.no_side and rank == 0:
-        side, c5_inputs = side_measurements(capi, L, stream, geom, cfg, rg, ro)
+    if not args.no_side:  # rank 0 only; collective so that a failure there ends every rank
+        side, c5_inputs = dist.run(lambda: side_measurements(capi, L, stream, geom, cfg, rg, ro)
+                                   if rank == 0 else ({}, None), "side legs")
 
     # ---- resident inputs: 16 fresh 1M-state batches per rank ------------------------
     d_states = capi.DeviceBuffer(N_BATCHES * N_STATES * 24)
@@ -193,7 +211,7 @@ def main():
     traffic, traffic_src = committed_traffic()
 
     cpu = None
-    if not args.no_cpu and rank == 0 and ws == 1:
+    if not args.no_cpu and ws == 1:
         cpu = cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs)
     if c5_inputs:
         os.unlink(c5_inputs["cfg_path"])
@@ -215,7 +233,7 @@ def main():
             "config": {"workload": "C2: 1 track, 8 gates, 64 OBBs, 1,048,576 sampled states per step",
                        "states_per_step_per_gpu": N_STATES, "obbs": int(len(obbs)),
                        "can_pass_gate": False, "valid_fraction": n_valid / N_STATES,
-                       "parallelism": f"replicas x{ws} (independent samplers)",
+                       "parallelism": f"replicas x{ws} (independent samplers)", "process_group": dist.kind,
                        "launch": "hip graph of the K steps" if graph is not None else "host loop"},
             "roofline": {"bound": "hbm", "kernel": "k_states_v5", "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
@@ -233,19 +251,28 @@ def main():
     dist.close()
 
 
-def launcher_check(ws, rank, local, out_stream):
+def launcher_check(ws, rank, local, out_stream, fail_rank=-1, fail_at="plan"):
     """The multi-rank plumbing of this bench without a GPU (gloo): the same launch, env,
-    barrier, max-over-ranks reduction and ragged waypoint all-gather as the GPU run."""
-    from eppamd.dist import Dist
-    dist = Dist(ws, rank, local, "gloo")
+    barrier, max-over-ranks reduction, error protocol and ragged waypoint all-gather as the
+    GPU run (eppamd.dist.Group; the GPU run's group is the product's RCCL communicator).
+    fail_rank >= 0 makes that rank's simulated plan fail, inside the leg (fail_at="plan":
+    Group.run's collective check) or at the exchange (fail_at="exchange": count -1)."""
+    from eppamd.dist import make_group
+    dist = make_group(ws, rank, "gloo")
     dist.barrier()
-    wp = np.arange(3 * (5 + rank), dtype=np.float64).reshape(-1, 3) + 1000 * rank
-    sets = dist.all_gather_waypoints(wp)
+
+    def plan():
+        if rank == fail_rank and fail_at == "plan":
+            raise RuntimeError("Path not found")
+        return np.arange(3 * (5 + rank), dtype=np.float64).reshape(-1, 3) + 1000 * rank
+
+    wp = dist.run(plan, "full plan")
+    sets = dist.all_gather_waypoints(None if (rank == fail_rank and fail_at == "exchange") else wp)
     t = dist.max(float(rank + 1))
     if rank == 0:
         print(json.dumps({"n_gpus": ws, "ranks_seen": [int(s[0, 0] // 1000) for s in sets],
                           "waypoints_per_track": [len(s) for s in sets], "max_over_ranks": t,
-                          "local_rank": local}), file=out_stream, flush=True)
+                          "local_rank": local, "process_group": dist.kind}), file=out_stream, flush=True)
     dist.close()
 
 
@@ -275,64 +302,69 @@ def committed_traffic():
 
 def full_plan(dist, rank, reps):
     """C4: plan this rank's track end to end (OnlineTrajGenerator.preComputeTraj), time it,
-    all-gather the waypoint sets.  Returns the slowest rank's mean ms per track."""
-    import tempfile
-
+    all-gather the waypoint sets through the product's RCCL communicator.  Returns the
+    slowest rank's mean ms per track.  Collective: a rank whose plan fails makes every rank
+    raise (dist.run / the all-gather's count -1)."""
     import online_traj_planner as otp
     from eppamd import config, synth
+    from eppamd.dist import RcclGroup
 
-    cfg = config.load(os.path.join(ROOT, "configs", "config.json"))
-    cfg["world_properties"]["lower_bound"] = [-6, -6, 0]
-    cfg["world_properties"]["upper_bound"] = [6, 6, 2]
-    cfg["path_planner_properties"]["samples_fmt"] = PLAN_SAMPLES
+    cfg, path = _track_config()
     geom = config.geometry(cfg)
-    fd, path = tempfile.mkstemp(suffix=".json")
-    with os.fdopen(fd, "w") as f:
-        json.dump(cfg, f)
     gates, obstacles = synth.track_world(100 + rank)
-    cps = synth.gate_checkpoints(gates, geom.gate_height, 0.55)
-    start, goal = cps[0], cps[-1]
-    otg = otp.OnlineTrajGenerator(start, goal, gates, obstacles, path)
-    otg.pre_compute_traj(0.0)  # warm-up: allocations, first launches
-    dist.barrier()
-    per = []
-    for _ in range(reps):
-        t = time.perf_counter()
-        otg.pre_compute_traj(0.0)
-        per.append((time.perf_counter() - t) * 1e3)
+    state = {}
+
+    def setup():
+        cps = synth.gate_checkpoints(gates, geom.gate_height, 0.55)
+        otg = otp.OnlineTrajGenerator(cps[0], cps[-1], gates, obstacles, path)
+        otg.pre_compute_traj(0.0)  # warm-up: allocations, first launches
+        state["otg"] = otg
+
+    def timed():
+        per = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            state["otg"].pre_compute_traj(0.0)
+            per.append((time.perf_counter() - t) * 1e3)
+        # one gate-to-gate segment alone, with the planner's device / host split
+        pp = otp.PathPlanner(gates, obstacles, path)
+        all_cps = state["otg"].get_checkpoints()
+        pp.plan_path(all_cps[2], all_cps[3], 2.0)
+        return per, pp.last_stats()
+
+    try:
+        dist.run(setup, "full plan (warm-up)")
+        dist.barrier()
+        per, seg = dist.run(timed, "full plan")
+    finally:
+        os.unlink(path)
     ms = float(np.mean(per))
-    # one gate-to-gate segment alone, with the planner's device / host split
-    pp = otp.PathPlanner(gates, obstacles, path)
-    all_cps = otg.get_checkpoints()
-    pp.plan_path(all_cps[2], all_cps[3], 2.0)
-    seg = pp.last_stats()
-    os.unlink(path)
     ms_max = dist.max(ms)
+    otg = state["otg"]
     wp = np.ascontiguousarray(otg.get_waypoints())
     traj = otg.get_planned_traj()
-    # the exchange step through the product's RCCL communicator (epp_comm_*; torch only
-    # carries the 128-byte id from rank 0 to the others)
-    from eppamd import capi
+    # the exchange step through the product's RCCL communicator (epp_comm_allgather_waypoints):
+    # the job's group at N > 1; a one-rank communicator at N = 1
     via = "RCCL (epp_comm_allgather_waypoints)"
-    try:
-        uid = dist.broadcast_bytes(capi.Comm.unique_id() if rank == 0 else None, 128)
-        comm = capi.Comm(uid, dist.ws, rank)
-        comm.allgather_waypoints(wp)  # (first call: connection setup)
+    gather_ms, sets = None, [wp]
+    if isinstance(dist, RcclGroup):
+        comm = dist
+    else:
+        try:
+            comm = RcclGroup(1, 0)
+        except Exception as e:  # noqa: BLE001 — N = 1 only: reported in the leg, not hidden
+            print(f"bench: product communicator unavailable at N=1 ({e})", file=sys.stderr)
+            comm, via = None, f"FAILED: {e}"
+    if comm is not None:
+        comm.all_gather_waypoints(wp)  # (first call: connection setup)
         dist.barrier()
         t = time.perf_counter()
-        sets = comm.allgather_waypoints(wp)
+        sets = comm.all_gather_waypoints(wp)
         gather_ms = dist.max((time.perf_counter() - t) * 1e3)
-        comm.close()
-    except capi.EppError as e:
-        # the exchange is this leg's last step, not the headline: report the failure and
-        # gather through torch.distributed instead of losing the whole run
-        print(f"bench: product all-gather failed ({e}); torch.distributed instead", file=sys.stderr)
-        via = f"torch.distributed all_gather (epp_comm failed: {e})"
-        dist.barrier()
-        t = time.perf_counter()
-        sets = dist.all_gather_waypoints(wp)
-        gather_ms = dist.max((time.perf_counter() - t) * 1e3)
-    return {"ms_per_track": ms_max, "ms_per_track_p50": dist.max(float(np.median(per))), "tracks": dist.ws, "samples_per_segment": PLAN_SAMPLES, "k": 16,
+        if comm is not dist:
+            comm.close()
+    return {"ms_per_track": ms_max, "ms_per_track_p50": dist.max(float(np.median(per))), "tracks": dist.ws,
+            "samples_per_segment": PLAN_SAMPLES, "k": 16,
             "segments_per_track": 9, "reps": reps, "waypoints_per_track": [len(x) for x in sets],
             "traj_rows": int(len(traj)), "traj_duration_s": float(traj[-1, 9] - traj[0, 9]),
             "all_gather_ms": gather_ms, "all_gather": via, "one_segment": seg,

@@ -179,6 +179,19 @@ PYBIND11_MODULE(online_traj_planner, m) {
                 return out;
             },
             py::arg("start"), py::arg("goal"), py::arg("samples"), py::arg("seed"))
+        .def(
+            "world_obbs",  // the world's OBBs as built (center xyz, half sizes): (n, 6)
+            [](const epp::PathPlanner& self) {
+                (void)self.worldPtr->device();  // the flattened table is rebuilt lazily
+                const auto& o = self.worldPtr->obbs();
+                py::array_t<double> out({(py::ssize_t)o.size(), (py::ssize_t)6});
+                for (size_t i = 0; i < o.size(); ++i)
+                    for (int k = 0; k < 3; ++k) {
+                        out.mutable_data()[i * 6 + k] = o[i].center[k];
+                        out.mutable_data()[i * 6 + 3 + k] = o[i].half[k];
+                    }
+                return out;
+            })
         .def("set_seed", &epp::PathPlanner::setSeed)
         .def("set_neighbours", &epp::PathPlanner::setNeighbours)
         .def("last_stats", [](const epp::PathPlanner& self) {

@@ -25,6 +25,7 @@ struct Rccl {
     decltype(&ncclCommInitAll) commInitAll = nullptr;
     decltype(&ncclCommDestroy) commDestroy = nullptr;
     decltype(&ncclAllGather) allGather = nullptr;
+    decltype(&ncclAllReduce) allReduce = nullptr;
     decltype(&ncclGetErrorString) errorString = nullptr;
 };
 
@@ -60,10 +61,11 @@ const Rccl* rccl() {
         r.commInitAll = reinterpret_cast<decltype(r.commInitAll)>(dlsym(r.h, "ncclCommInitAll"));
         r.commDestroy = reinterpret_cast<decltype(r.commDestroy)>(dlsym(r.h, "ncclCommDestroy"));
         r.allGather = reinterpret_cast<decltype(r.allGather)>(dlsym(r.h, "ncclAllGather"));
+        r.allReduce = reinterpret_cast<decltype(r.allReduce)>(dlsym(r.h, "ncclAllReduce"));
         r.errorString = reinterpret_cast<decltype(r.errorString)>(dlsym(r.h, "ncclGetErrorString"));
     });
     if (!r.h || !r.getUniqueId || !r.commInitRank || !r.commInitAll || !r.commDestroy || !r.allGather ||
-        !r.errorString) {
+        !r.allReduce || !r.errorString) {
         set_error("epp_comm: RCCL (librccl.so.1) is not available");
         return nullptr;
     }
@@ -88,7 +90,40 @@ struct epp_comm {
 
 using namespace epp;
 
+namespace {
+
+// Binds the communicator's device and stream for one call (restores the caller's device).
+struct CommScope {
+    int prev = 0;
+    hipError_t he = hipSuccess;
+    explicit CommScope(epp_comm* c) {
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(c->device);
+        if (!c->stream) he = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    }
+    ~CommScope() { (void)hipSetDevice(prev); }
+};
+
+hipError_t comm_grow(epp_comm* c, size_t need) {
+    if (need <= c->cap) return hipSuccess;
+    if (c->d_buf) (void)hipFree(c->d_buf);
+    c->d_buf = nullptr;
+    c->cap = 0;
+    const hipError_t he = hipMalloc(&c->d_buf, need);
+    if (he == hipSuccess) c->cap = need;
+    return he;
+}
+
+epp_status hip_fail(const char* what, hipError_t he) {
+    set_error(std::string(what) + ": " + hipGetErrorString(he));
+    return EPP_ERR_HIP;
+}
+
+}  // namespace
+
 extern "C" {
+
+epp_status epp_comm_available(void) { return rccl() ? EPP_OK : EPP_ERR_UNSUPPORTED; }
 
 epp_status epp_comm_unique_id(uint8_t id[128]) {
     if (!id) {
@@ -171,48 +206,36 @@ epp_status epp_comm_rank(const epp_comm* c, int32_t* rank, int32_t* n_ranks) {
 
 epp_status epp_comm_allgather_waypoints(epp_comm* c, const double* wp, int32_t n, int32_t cap, double* out,
                                         int32_t* counts) {
-    if (!c || n < 0 || cap < 0 || (n > 0 && !wp) || !counts || (cap > 0 && !out)) {
+    if (!c || n < -1 || cap < 0 || (n > 0 && !wp) || !counts || (cap > 0 && !out)) {
         set_error("epp_comm_allgather_waypoints: invalid argument");
         return EPP_ERR_INVALID_ARGUMENT;
     }
     const Rccl* r = rccl();
     if (!r) return EPP_ERR_UNSUPPORTED;
-    int prev = 0;
-    (void)hipGetDevice(&prev);
-    (void)hipSetDevice(c->device);
-    struct Restore {
-        int d;
-        ~Restore() { (void)hipSetDevice(d); }
-    } restore{prev};
+    CommScope scope(c);
+    hipError_t he = scope.he;
     const int R = c->n_ranks;
     const size_t cnt_b = ((size_t)(R + 1) * 4 + 255) & ~size_t(255);
-    hipError_t he = hipSuccess;
-    if (!c->stream) he = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-    auto grow = [&](size_t need) {
-        if (he != hipSuccess || need <= c->cap) return;
-        if (c->d_buf) (void)hipFree(c->d_buf);
-        c->d_buf = nullptr;
-        c->cap = 0;
-        he = hipMalloc(&c->d_buf, need);
-        if (he == hipSuccess) c->cap = need;
-    };
-    grow(cnt_b);
-    // 1. the counts
+    if (he == hipSuccess) he = comm_grow(c, cnt_b);
+    // 1. the counts (-1: that rank failed before it had a set; every rank then stops here)
     if (he == hipSuccess) he = hipMemcpyAsync(c->d_buf, &n, 4, hipMemcpyHostToDevice, c->stream);
-    if (he != hipSuccess) {
-        set_error(std::string("epp_comm_allgather_waypoints: ") + hipGetErrorString(he));
-        return EPP_ERR_HIP;
-    }
+    if (he != hipSuccess) return hip_fail("epp_comm_allgather_waypoints", he);
     ncclResult_t e = r->allGather(c->d_buf, c->d_buf + 4, 1, ncclInt32, c->comm, c->stream);
     if (e != ncclSuccess) return nccl_error(r, e, "ncclAllGather (counts)");
     he = hipMemcpyAsync(counts, c->d_buf + 4, (size_t)R * 4, hipMemcpyDeviceToHost, c->stream);
     if (he == hipSuccess) he = hipStreamSynchronize(c->stream);
-    if (he != hipSuccess) {
-        set_error(std::string("epp_comm_allgather_waypoints: ") + hipGetErrorString(he));
-        return EPP_ERR_HIP;
+    if (he != hipSuccess) return hip_fail("epp_comm_allgather_waypoints", he);
+    // every rank holds the same counts, so every rank takes the same branch below
+    int32_t maxw = 0, failed = -1, n_failed = 0;
+    for (int i = 0; i < R; ++i) {
+        maxw = std::max(maxw, counts[i]);
+        if (counts[i] < 0 && n_failed++ == 0) failed = i;
     }
-    int32_t maxw = 0;
-    for (int i = 0; i < R; ++i) maxw = std::max(maxw, counts[i]);
+    if (n_failed) {
+        set_error("epp_comm_allgather_waypoints: " + std::to_string(n_failed) + " rank(s) reported a failure (first: rank " +
+                  std::to_string(failed) + "; counts filled, -1 marks them)");
+        return EPP_ERR_PEER;
+    }
     if (maxw > cap) {
         set_error("epp_comm_allgather_waypoints: a rank has more waypoints than cap (counts filled)");
         return EPP_ERR_CAPACITY;
@@ -220,15 +243,12 @@ epp_status epp_comm_allgather_waypoints(epp_comm* c, const double* wp, int32_t n
     if (maxw == 0) return EPP_OK;
     // 2. the sets, padded to the longest (zeros after a rank's own points)
     const size_t set_b = (size_t)maxw * 24;
-    grow(cnt_b + set_b * (R + 1));
+    he = comm_grow(c, cnt_b + set_b * (R + 1));
     char* d_send = c->d_buf + cnt_b;
     char* d_recv = d_send + set_b;
     if (he == hipSuccess) he = hipMemsetAsync(d_send, 0, set_b, c->stream);
     if (he == hipSuccess && n > 0) he = hipMemcpyAsync(d_send, wp, (size_t)n * 24, hipMemcpyHostToDevice, c->stream);
-    if (he != hipSuccess) {
-        set_error(std::string("epp_comm_allgather_waypoints: ") + hipGetErrorString(he));
-        return EPP_ERR_HIP;
-    }
+    if (he != hipSuccess) return hip_fail("epp_comm_allgather_waypoints", he);
     e = r->allGather(d_send, d_recv, (size_t)maxw * 3, ncclFloat64, c->comm, c->stream);
     if (e != ncclSuccess) return nccl_error(r, e, "ncclAllGather (waypoints)");
     for (int i = 0; i < R && he == hipSuccess; ++i)
@@ -236,11 +256,36 @@ epp_status epp_comm_allgather_waypoints(epp_comm* c, const double* wp, int32_t n
             he = hipMemcpyAsync(out + (size_t)i * cap * 3, d_recv + (size_t)i * set_b, (size_t)counts[i] * 24,
                                 hipMemcpyDeviceToHost, c->stream);
     if (he == hipSuccess) he = hipStreamSynchronize(c->stream);
-    if (he != hipSuccess) {
-        set_error(std::string("epp_comm_allgather_waypoints: ") + hipGetErrorString(he));
-        return EPP_ERR_HIP;
-    }
+    if (he != hipSuccess) return hip_fail("epp_comm_allgather_waypoints", he);
     return EPP_OK;
+}
+
+epp_status epp_comm_allreduce_f64(epp_comm* c, double* x, int32_t n, int32_t op) {
+    if (!c || n < 0 || (n > 0 && !x) || op < EPP_REDUCE_SUM || op > EPP_REDUCE_MIN) {
+        set_error("epp_comm_allreduce_f64: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    const Rccl* r = rccl();
+    if (!r) return EPP_ERR_UNSUPPORTED;
+    if (n == 0) return EPP_OK;
+    CommScope scope(c);
+    hipError_t he = scope.he;
+    const size_t bytes = ((size_t)n * 8 + 255) & ~size_t(255);
+    if (he == hipSuccess) he = comm_grow(c, bytes);
+    if (he == hipSuccess) he = hipMemcpyAsync(c->d_buf, x, (size_t)n * 8, hipMemcpyHostToDevice, c->stream);
+    if (he != hipSuccess) return hip_fail("epp_comm_allreduce_f64", he);
+    const ncclRedOp_t rop = op == EPP_REDUCE_SUM ? ncclSum : op == EPP_REDUCE_MAX ? ncclMax : ncclMin;
+    const ncclResult_t e = r->allReduce(c->d_buf, c->d_buf, (size_t)n, ncclFloat64, rop, c->comm, c->stream);
+    if (e != ncclSuccess) return nccl_error(r, e, "ncclAllReduce");
+    he = hipMemcpyAsync(x, c->d_buf, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(c->stream);
+    if (he != hipSuccess) return hip_fail("epp_comm_allreduce_f64", he);
+    return EPP_OK;
+}
+
+epp_status epp_comm_barrier(epp_comm* c) {
+    double x = 0.0;
+    return epp_comm_allreduce_f64(c, &x, 1, EPP_REDUCE_SUM);
 }
 
 }  // extern "C"

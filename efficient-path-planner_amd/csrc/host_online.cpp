@@ -41,14 +41,26 @@ void OnlineTrajGenerator::waitForUpdate() {
 }
 
 // Takes the finished online recomputation's result; its failure (e.g. "Pre path not
-// found. Exiting") is reported here, named as the previous update's.
+// found. Exiting") is reported here, named as the previous update's.  Gate updates that
+// arrived meanwhile are applied to the world now.
 void OnlineTrajGenerator::collectUpdate() {
     if (!pending.valid()) return;
+    std::exception_ptr failure;
     try {
         pending.get();
     } catch (const std::exception& e) {
-        throw std::runtime_error(std::string("previous trajectory update failed: ") + e.what());
+        failure = std::make_exception_ptr(std::runtime_error(std::string("previous trajectory update failed: ") + e.what()));
     }
+    applyDeferredGates();
+    if (failure) std::rethrow_exception(failure);
+}
+
+// src/OnlineTrajGenerator.cpp:146-147 for the updates received while the worker planned
+void OnlineTrajGenerator::applyDeferredGates() {
+    if (deferredGates.empty()) return;
+    pathPlanner.parseGatesAndObstacles(nominalGatePositionAndType, nominalObstaclePosition);
+    for (int g : deferredGates) pathWriter.updateGatePos(g, gateRow(g));
+    deferredGates.clear();
 }
 
 std::vector<double> OnlineTrajGenerator::gateRow(int gateId) const {
@@ -156,21 +168,20 @@ bool OnlineTrajGenerator::updateGatePos(int gateId, const std::vector<double>& n
     if (gatesObservedWithinRange.count(gateId)) return false;
     if (!pathPlanner.worldPtr->checkPointValidity(dronePos, false)) return false;
     if (newPose.size() < 6) throw std::invalid_argument("newPose needs 6 values");
-    // An online recomputation (recalculate_online) still running: the reference throws
-    // when it gets here (src/OnlineTrajGenerator.cpp:208-212).  Here the check comes
-    // before the world is rebuilt, since the running recomputation plans on that world
-    // (the reference rebuilds it under the planning threads' feet).
-    if (pending.valid()) {
-        if (pending.wait_for(std::chrono::seconds(0)) != std::future_status::ready) {
-            std::cerr << "Call to update trajectory, while previous update is still going on";
-            throw std::runtime_error("Call to update trajectory, while previous update is still going on");
-        }
-        collectUpdate();
-    }
+    (void)gateRow(gateId);  // range check before anything is recorded
+    // a finished online recomputation is collected first (its failure surfaces here)
+    if (pending.valid() && pending.wait_for(std::chrono::seconds(0)) == std::future_status::ready) collectUpdate();
+    // still running (recalculate_online): it plans on the current world, which is left
+    // alone; the new pose is checked on a snapshot and the rebuild deferred (see header)
+    const bool busy = pending.valid();
     gatesObservedWithinRange.insert(gateId);
     for (int k = 0; k < 6; ++k) nominalGatePositionAndType(gateId, k) = newPose[k];
-    pathPlanner.parseGatesAndObstacles(nominalGatePositionAndType, nominalObstaclePosition);
-    pathWriter.updateGatePos(gateId, gateRow(gateId));
+    if (busy) {
+        deferredGates.push_back(gateId);
+    } else {
+        pathPlanner.parseGatesAndObstacles(nominalGatePositionAndType, nominalObstaclePosition);
+        pathWriter.updateGatePos(gateId, gateRow(gateId));
+    }
 
     Matrix traj;
     {
@@ -188,8 +199,12 @@ bool OnlineTrajGenerator::updateGatePos(int gateId, const std::vector<double>& n
             startIdx = i;
         }
     }
-    const size_t next = 2 * (size_t)gateId + 3 < checkpoints.size() ? 2 * (size_t)gateId + 3 : checkpoints.size() - 1;
-    const Vec3 nc = checkpoints[next];
+    Vec3 nc;
+    {
+        std::lock_guard<std::mutex> lk(cpMu);
+        const size_t next = 2 * (size_t)gateId + 3 < checkpoints.size() ? 2 * (size_t)gateId + 3 : checkpoints.size() - 1;
+        nc = checkpoints[next];
+    }
     size_t endIdx = 0;
     best = std::numeric_limits<double>::infinity();
     for (size_t i = 0; i < traj.rows; ++i) {
@@ -210,10 +225,18 @@ bool OnlineTrajGenerator::updateGatePos(int gateId, const std::vector<double>& n
             break;
         }
     }
-    if (passing)
-        valid = pathPlanner.checkTrajectoryValidity(look, configParser->getPathPlannerProperties().minDistCheckTrajCollision);
+    if (passing) {
+        const double md = configParser->getPathPlannerProperties().minDistCheckTrajCollision;
+        if (busy) {
+            World snapshot(configParser);
+            PathPlanner::fillWorld(snapshot, nominalGatePositionAndType, nominalObstaclePosition);
+            valid = PathPlanner::checkTrajectoryValidityOn(snapshot, look, md);
+        } else {
+            valid = pathPlanner.checkTrajectoryValidity(look, md);
+        }
+    }
     if (valid && passing) return false;
-    if (trajectoryCurrentlyUpdating.load()) {
+    if (busy || trajectoryCurrentlyUpdating.load()) {
         std::cerr << "Call to update trajectory, while previous update is still going on";
         throw std::runtime_error("Call to update trajectory, while previous update is still going on");
     }
@@ -239,8 +262,11 @@ void OnlineTrajGenerator::recomputeTraj(int gateId, const Vec3& /*dronePos*/, do
     const size_t cpPre = 2 * (size_t)gateId + 1, cpPost = 2 * (size_t)gateId + 2, cpNext = 2 * (size_t)gateId + 3;
     Vec3 center, normal;
     getGateCenterAndNormal(gateRow(segPre), center, normal);
-    checkpoints[cpPre] = center - normal * pp.checkpointGateOffset;
-    checkpoints[cpPost] = center + normal * pp.checkpointGateOffset;
+    {
+        std::lock_guard<std::mutex> lk(cpMu);
+        checkpoints[cpPre] = center - normal * pp.checkpointGateOffset;
+        checkpoints[cpPost] = center + normal * pp.checkpointGateOffset;
+    }
     pathWriter.writeCheckpoints(checkpoints);
 
     double advancedTime = flightTime;

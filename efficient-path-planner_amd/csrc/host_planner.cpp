@@ -87,17 +87,21 @@ PathPlanner::PathPlanner(const Matrix& gates, const Matrix& obstacles, std::shar
 
 // src/PathPlanner.cpp:60-78
 void PathPlanner::parseGatesAndObstacles(const Matrix& gates, const Matrix& obstacles) {
-    worldPtr->resetWorld();
+    fillWorld(*worldPtr, gates, obstacles);
+}
+
+void PathPlanner::fillWorld(World& world, const Matrix& gates, const Matrix& obstacles) {
+    world.resetWorld();
     for (size_t i = 0; i < gates.rows; ++i) {
         std::vector<double> g(gates.row(i), gates.row(i) + gates.cols);
         if (g.size() < 7) throw std::invalid_argument("gate rows need 7 columns");
         g[2] = 0.0;  // put all gates to ground  :68
-        worldPtr->addGate((int)i, g);
+        world.addGate((int)i, g);
     }
     for (size_t i = 0; i < obstacles.rows; ++i) {
         std::vector<double> o(obstacles.row(i), obstacles.row(i) + obstacles.cols);
         if (o.size() < 6) throw std::invalid_argument("obstacle rows need 6 columns");
-        worldPtr->addObstacle((int)i, o);
+        world.addObstacle((int)i, o);
     }
 }
 
@@ -491,6 +495,10 @@ std::vector<Vec3> PathPlanner::pruneWaypoints(const std::vector<Vec3>& w) const 
 
 // PathPlanner::checkTrajectoryValidity — src/PathPlanner.cpp:267-280 (one batched launch)
 bool PathPlanner::checkTrajectoryValidity(const Matrix& traj, double minDistance) const {
+    return checkTrajectoryValidityOn(*worldPtr, traj, minDistance);
+}
+
+bool PathPlanner::checkTrajectoryValidityOn(const World& world, const Matrix& traj, double minDistance) {
     if (traj.rows == 0) return true;
     std::vector<double> xyz(traj.rows * 3);
     for (size_t i = 0; i < traj.rows; ++i) {
@@ -499,7 +507,7 @@ bool PathPlanner::checkTrajectoryValidity(const Matrix& traj, double minDistance
         xyz[3 * i + 2] = traj(i, 6);
     }
     std::vector<uint8_t> ok(traj.rows);
-    worldPtr->checkPointsMinDistance(xyz.data(), (int64_t)traj.rows, minDistance, ok.data());
+    world.checkPointsMinDistance(xyz.data(), (int64_t)traj.rows, minDistance, ok.data());
     for (uint8_t v : ok)
         if (!v) return false;
     return true;

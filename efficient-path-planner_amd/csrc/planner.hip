@@ -654,7 +654,9 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
         const int ox = bx * kTileB - kTileH, oy = by * kTileB - kTileH, oz = bz * kTileB - kTileH;
         const double cen[3] = {g.lo[0] + (ox + 0.5 * kTileE) * g.h, g.lo[1] + (oy + 0.5 * kTileE) * g.h,
                                g.lo[2] + (oz + 0.5 * kTileE) * g.h};
+#ifdef EPP_KNN_DIAG
         const unsigned long long t_begin = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
+#endif
         // 1. halo cell sizes -> exclusive scan (thread t owns halo cells kPer*t ..)
         int cnt[kPer], cell0[kPer], tot = 0;
 #pragma unroll
@@ -715,7 +717,11 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
             }
             __syncthreads();
             // 3. queries, lpq adjacent lanes per query
-            const int nq = mode == 4 ? 0 : s_nq;  // mode 4: timing ablation (inexact)
+#ifdef EPP_KNN_DIAG
+            const int nq = mode == 4 ? 0 : s_nq;  // mode 4: timing ablation (inexact; diagnostics builds only)
+#else
+            const int nq = s_nq;
+#endif
             const int lpq = nq <= kTileThreads / 4 ? 4 : nq <= kTileThreads / 2 ? 2 : 1;  // block-uniform
             const int slot = threadIdx.x / lpq, sub = threadIdx.x % lpq;
             for (int qb = 0; qb < nq; qb += kTileThreads / lpq) {  // block-uniform
@@ -823,6 +829,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
             }
         }
         __syncthreads();  // the LDS tile is rewritten by the next block
+#ifdef EPP_KNN_DIAG
         if (dbg && threadIdx.x == 0) {  // diagnostics: per-block timing (EPP_KNN_TILE_DBG)
             const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
             dbg[4 * b] = t_begin;
@@ -830,6 +837,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
             dbg[4 * b + 2] = (unsigned long long)s_nq;
             dbg[4 * b + 3] = blockIdx.x;
         }
+#endif
     }
 }
 
@@ -911,17 +919,26 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
     hipLaunchKernelGGL(k_knn_count, g256, b256, 0, s, nodes, n, g, cell_of, cnt);
     hipLaunchKernelGGL(k_knn_scan, dim3(1), dim3(kBoundsThreads), 0, s, g, cnt, start);
     hipLaunchKernelGGL(k_knn_scatter, g256, b256, 0, s, nodes, n, cell_of, start, fill, sxyz, sidx);
+    // EPP_KNN_TILE=0 selects the untiled grid walk (same answer; a test hook); the product
+    // accepts only {0, 1}.  The timing ablations and the per-block dump exist only in a
+    // -DEPP_KNN_DIAG diagnostics build.
     const char* tile_env = std::getenv("EPP_KNN_TILE");
-    if ((!tile_env || std::atoi(tile_env) != 0) && (k == 4 || k == 8 || k == 16)) {
+    const bool tiled = !(tile_env && *tile_env && std::atoi(tile_env) == 0);
+    if (tiled && (k == 4 || k == 8 || k == 16)) {
         // persistent: the block count is only known on the device (grid shape)
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         const dim3 gt((unsigned)std::max(1, cus * 3)), bt(kTileThreads);
-        const int mode = tile_env ? std::atoi(tile_env) : 1;  // 2, 4..6: ablations (inexact)
-        static unsigned long long* dbg = nullptr;           // diagnostics only
+#ifdef EPP_KNN_DIAG
+        const int mode = tile_env ? std::atoi(tile_env) : 1;  // 4: timing ablation (inexact)
+        static unsigned long long* dbg = nullptr;
         if (std::getenv("EPP_KNN_TILE_DBG") && !dbg && hipMalloc(&dbg, 4 * 8 * 65536) != hipSuccess) dbg = nullptr;
         unsigned long long* d = std::getenv("EPP_KNN_TILE_DBG") ? dbg : nullptr;
         if (d) (void)hipMemsetAsync(d, 0, 4 * 8 * 65536, s);
+#else
+        const int mode = 1;
+        unsigned long long* d = nullptr;
+#endif
         int* retry = cell_of;  // free once the scatter has run
         if (k == 4) hipLaunchKernelGGL(k_knn_tile<4>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr, mode, d);
         else if (k == 8) hipLaunchKernelGGL(k_knn_tile<8>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr, mode, d);
@@ -930,6 +947,7 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
         if (k == 4) hipLaunchKernelGGL(k_knn_retry<4>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr);
         else if (k == 8) hipLaunchKernelGGL(k_knn_retry<8>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr);
         else hipLaunchKernelGGL(k_knn_retry<16>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr);
+#ifdef EPP_KNN_DIAG
         if (d) {
             std::vector<unsigned long long> h(4 * 65536);
             (void)hipStreamSynchronize(s);
@@ -949,6 +967,7 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
                     std::fprintf(stderr, "%d %.2f %.2f %llu %llu\n", i, (h[4 * i] - t0) / 100.0, (h[4 * i + 1] - t0) / 100.0,
                                  h[4 * i + 2], h[4 * i + 3]);
         }
+#endif
     } else {
         switch (k) {
             case 4: hipLaunchKernelGGL(k_knn_grid<4>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;

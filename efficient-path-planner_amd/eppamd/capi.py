@@ -22,6 +22,8 @@ EPP_ERR_RUNTIME = -2
 EPP_ERR_HIP = -3
 EPP_ERR_UNSUPPORTED = -4
 EPP_ERR_CAPACITY = -5
+EPP_ERR_PEER = -6
+EPP_REDUCE_SUM, EPP_REDUCE_MAX, EPP_REDUCE_MIN = 0, 1, 2
 
 _lib = None
 
@@ -75,6 +77,9 @@ def lib() -> C.CDLL:
             "epp_comm_destroy": (i32, [vp]),
             "epp_comm_rank": (i32, [vp, C.POINTER(i32), C.POINTER(i32)]),
             "epp_comm_allgather_waypoints": (i32, [vp, vp, i32, i32, vp, vp]),
+            "epp_comm_allreduce_f64": (i32, [vp, vp, i32, i32]),
+            "epp_comm_barrier": (i32, [vp]),
+            "epp_comm_available": (i32, []),
             "epp_check_states": (i32, [vp, vp, i64, i32, vp, vp, vp, vp]),
             "epp_check_states_mindist": (i32, [vp, vp, i64, dp, vp, vp]),
             "epp_check_motions": (i32, [vp, vp, vp, i64, i32, i32, vp, vp]),
@@ -129,6 +134,7 @@ EXPORTED = [
     "epp_graph_begin", "epp_graph_end", "epp_graph_launch", "epp_graph_destroy", "epp_minsnap_batch_times",
     "epp_generate_trajectory_times_host", "epp_world_generation", "epp_world_build_index", "epp_comm_unique_id", "epp_comm_init",
     "epp_comm_init_all", "epp_comm_destroy", "epp_comm_rank", "epp_comm_allgather_waypoints",
+    "epp_comm_allreduce_f64", "epp_comm_barrier", "epp_comm_available",
 ]
 
 
@@ -524,13 +530,31 @@ class Comm:
         check(lib().epp_comm_init_all(len(devs), _ptr(devs), C.cast(hs, C.c_void_p)))
         return [cls(b"", 0, 0, handle=h) for h in hs]
 
-    def allgather_waypoints(self, wp: np.ndarray, cap: int = 4096) -> list[np.ndarray]:
-        wp = np.ascontiguousarray(np.asarray(wp, np.float64).reshape(-1, 3))
+    def allgather_waypoints(self, wp: np.ndarray | None, cap: int = 4096) -> list[np.ndarray]:
+        """Every rank's (W_r, 3) set.  wp=None: this rank failed (count -1); every rank then
+        raises EppError(EPP_ERR_PEER) with `.counts` naming the failed ranks (-1)."""
         out = np.zeros((self.n_ranks, cap, 3))
         counts = np.zeros(self.n_ranks, np.int32)
-        check(lib().epp_comm_allgather_waypoints(self.handle, _ptr(wp) if len(wp) else None, len(wp), cap,
-                                                 _ptr(out), _ptr(counts)))
+        if wp is None:
+            rc = lib().epp_comm_allgather_waypoints(self.handle, None, -1, cap, _ptr(out), _ptr(counts))
+        else:
+            wp = np.ascontiguousarray(np.asarray(wp, np.float64).reshape(-1, 3))
+            rc = lib().epp_comm_allgather_waypoints(self.handle, _ptr(wp) if len(wp) else None, len(wp), cap,
+                                                    _ptr(out), _ptr(counts))
+        if rc != EPP_OK:
+            err = EppError(rc, lib().epp_last_error().decode())
+            err.counts = counts.copy()
+            raise err
         return [out[r, :counts[r]].copy() for r in range(self.n_ranks)]
+
+    def allreduce(self, x, op: int = EPP_REDUCE_SUM) -> np.ndarray:
+        """x (doubles) reduced over the ranks (epp_comm_allreduce_f64)."""
+        a = np.ascontiguousarray(np.array(x, np.float64).reshape(-1))
+        check(lib().epp_comm_allreduce_f64(self.handle, _ptr(a), len(a), op))
+        return a
+
+    def barrier(self) -> None:
+        check(lib().epp_comm_barrier(self.handle))
 
     def close(self) -> None:
         if self.handle:

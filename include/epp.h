@@ -46,6 +46,7 @@ typedef int32_t epp_status;
 #define EPP_ERR_HIP (-3)              /* HIP runtime error */
 #define EPP_ERR_UNSUPPORTED (-4)      /* rotation other than about z (src/Object.cpp:38-47) */
 #define EPP_ERR_CAPACITY (-5)         /* an output buffer was too small */
+#define EPP_ERR_PEER (-6)             /* another rank of a collective reported a failure */
 
 /* An oriented bounding box after the world build (reference class OBB,
  * include/OBB.h:19-57).  rot is the row-major rotation matrix; the reference only
@@ -237,10 +238,13 @@ epp_status epp_mask_edges_count(int32_t* nbr, const uint8_t* valid, int64_t m, i
  * single-threaded CPU code).  RCCL is loaded at first use (librccl.so.1); without it these
  * return EPP_ERR_UNSUPPORTED.
  * One process per GPU: rank 0 calls epp_comm_unique_id and shares the 128 bytes out of
- * band (e.g. torch.distributed, MPI); every rank calls epp_comm_init on its device.
+ * band (bench.py: a file rendezvous, eppamd/dist.py; or MPI, torch.distributed); every
+ * rank calls epp_comm_init on its device.
  * One process, several GPUs: epp_comm_init_all (one communicator per device; use each
  * from its own host thread). */
 typedef struct epp_comm epp_comm;
+/* EPP_OK if RCCL can be loaded in this process (no communicator is created). */
+epp_status epp_comm_available(void);
 epp_status epp_comm_unique_id(uint8_t id[128]);
 epp_status epp_comm_init(const uint8_t id[128], int32_t n_ranks, int32_t rank, epp_comm** out);
 epp_status epp_comm_init_all(int32_t n_devices, const int32_t* devices, epp_comm** out /* n_devices */);
@@ -248,9 +252,21 @@ epp_status epp_comm_destroy(epp_comm* comm);
 epp_status epp_comm_rank(const epp_comm* comm, int32_t* rank, int32_t* n_ranks);
 /* All-gather of every rank's waypoint set (wp: n x 3 HOST doubles): counts[r] = rank r's
  * count (n_ranks entries), out + r * cap * 3 = its points (HOST, n_ranks x cap x 3).  Every
- * rank must call it.  EPP_ERR_CAPACITY (counts filled) if a rank has more than cap. */
+ * rank must call it, also a rank that has no set because its own work failed: it passes
+ * n = -1 (wp may be NULL).  Every rank then returns EPP_ERR_PEER with counts filled (-1
+ * marks the failed ranks) and the sets are not exchanged, so one rank's failure ends the
+ * exchange on all ranks instead of leaving them in the collective.  EPP_ERR_CAPACITY
+ * (counts filled, on every rank) if a rank has more than cap. */
 epp_status epp_comm_allgather_waypoints(epp_comm* comm, const double* wp, int32_t n, int32_t cap, double* out,
                                         int32_t* counts);
+/* x[0..n) (HOST doubles, in place) reduced over the ranks: op EPP_REDUCE_SUM / MAX / MIN.
+ * The max-over-ranks timing and the collective error flags of a multi-rank caller. */
+#define EPP_REDUCE_SUM 0
+#define EPP_REDUCE_MAX 1
+#define EPP_REDUCE_MIN 2
+epp_status epp_comm_allreduce_f64(epp_comm* comm, double* x, int32_t n, int32_t op);
+/* Returns once every rank has called it (an all-reduce of one double). */
+epp_status epp_comm_barrier(epp_comm* comm);
 
 /* ---- host-buffer convenience (synchronous; used by the C++ API shims) ------------- */
 /* generateTrajectory for one track with host buffers (poly_traj::generateTrajectory,

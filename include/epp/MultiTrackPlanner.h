@@ -24,7 +24,12 @@ struct TrackResult {
     int device = -1;
 };
 
-// Throws std::runtime_error on a planning failure ("Path not found") or an RCCL error.
+// Throws the exception of the lowest failed rank on a planning failure (e.g.
+// std::runtime_error "Path not found"): the failed rank still joins that round's
+// all-gather with a count of -1, so every rank leaves at the same round (no rank waits in
+// RCCL for one that stopped).  Also throws on an RCCL error or a track with more than 4096
+// waypoints (reported on every rank).  A fault of the communicator itself is not
+// recoverable.
 std::vector<TrackResult> planTracks(const std::vector<TrackProblem>& tracks, const std::string& configPath,
                                     const std::vector<int>& devices, double takeoffTime = 0.0);
 

@@ -2,11 +2,16 @@
 // (include/OnlineTrajGenerator.h:26-77, src/OnlineTrajGenerator.cpp).
 //
 // Concurrency: the reference recomputes on a detached std::thread and writes the
-// trajectory while Python may read it.  Here every access to the planned
-// trajectory goes through one mutex; with recalculate_online the recomputation runs on
-// a worker thread.  An update arriving while it runs throws the reference's
-// "Call to update trajectory, while previous update is still going on" before touching
-// the world; the destructor and wait_for_update() wait for it.
+// trajectory while Python may read it, and rebuilds the World under the planning threads
+// (SURVEY.md §5).  Here every access to the planned trajectory goes through one mutex;
+// with recalculate_online the recomputation runs on a worker thread.  An update arriving
+// while it runs keeps the reference's return values: the gate is recorded, the current
+// trajectory is checked against a snapshot world holding the new pose (the worker's
+// world is not touched; the rebuild is applied once the worker finished), false is
+// returned when it is still valid and the reference's "Call to update trajectory, while
+// previous update is still going on" is thrown only when a new recomputation is needed
+// (src/OnlineTrajGenerator.cpp:203-212).  The destructor and wait_for_update() wait for
+// the worker.
 #pragma once
 #include <atomic>
 #include <future>
@@ -52,6 +57,7 @@ private:
     bool checkGatePassed(const Vec3& p1, const Vec3& p2, int gateId) const;
     void recomputeTraj(int gateId, const Vec3& dronePos, double flightTime);
     void collectUpdate();
+    void applyDeferredGates();
     Matrix generate(const std::vector<Vec3>& path, double t0, const Vec3& v0, const Vec3& a0,
                     const std::vector<Vec3>& pre = {}) const;
     static size_t nearestRow(const Matrix& traj, double t);
@@ -64,6 +70,8 @@ private:
     std::vector<Vec3> checkpoints;
     std::set<int> gatesObservedWithinRange;
     std::vector<std::vector<Vec3>> pathSegments;
+    std::vector<int> deferredGates;  // gate updates received while the worker ran (world rebuild pending)
+    mutable std::mutex cpMu;         // checkpoints: written by the worker, read by updateGatePos
     Matrix plannedTraj;
     std::vector<Vec3> waypoints;  // guarded by trajMu
     mutable std::mutex trajMu;

@@ -41,6 +41,11 @@ public:
                 std::shared_ptr<ConfigParser> configParser);
 
     void parseGatesAndObstacles(const Matrix& nominalGatePositionAndType, const Matrix& nominalObstaclePosition);
+    // The world build of parseGatesAndObstacles into any World (src/PathPlanner.cpp:60-78):
+    // reset, gates with z := 0, obstacles.
+    static void fillWorld(World& world, const Matrix& nominalGatePositionAndType, const Matrix& nominalObstaclePosition);
+    // checkTrajectoryValidity against any World (one batched launch)
+    static bool checkTrajectoryValidityOn(const World& world, const Matrix& trajectory, double minDistance);
     bool planPath(const Vec3& start, const Vec3& goal, double timeLimit, std::vector<Vec3>& resultPath) const;
     // Independent (start, goal) problems planned concurrently, one host thread and one
     // HIP stream each (their small kernels overlap on the GPU).  Problem i gets the seed

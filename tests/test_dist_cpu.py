@@ -1,6 +1,7 @@
-"""world_size-2 gloo test of the multi-GPU path's exchange step (eppamd.dist): the
-all-gather of ragged waypoint sets and the max-over-ranks timing reduction that bench.py
-uses over RCCL."""
+"""world_size-2 gloo tests of the multi-GPU path's plumbing (eppamd.dist): the all-gather
+of ragged waypoint sets, the max-over-ranks timing reduction and the error protocol that
+bench.py runs over the product's RCCL communicator, plus the file
+rendezvous that bootstraps that communicator without torch."""
 import os
 import socket
 
@@ -23,8 +24,9 @@ def _worker(rank, ws, port, q):
     sys.path.insert(0, PKG)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(ws), RANK=str(rank),
                       LOCAL_RANK=str(rank))
-    from eppamd.dist import Dist, env
-    d = Dist(*env(), backend="gloo")
+    from eppamd.dist import env, make_group
+    ws_, rank_, _ = env()
+    d = make_group(ws_, rank_, "gloo")
     wp = np.arange(3 * (4 + 3 * rank), dtype=np.float64).reshape(-1, 3) + 100 * rank
     sets = d.all_gather_waypoints(wp)
     mx = d.max(float(rank + 1))
@@ -83,3 +85,85 @@ def test_bench_rejects_mismatched_world_size():
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--launcher-check"],
                          env=env, capture_output=True, text=True, timeout=120)
     assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr
+
+
+def _run_bench_ws2(extra, timeout=240):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--launcher-check"] + extra,
+                          env=env, capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_rank_failure_in_plan_fails_every_rank():
+    """Rank 1's plan fails: both ranks leave through the collective check (no rank waits in
+    the next collective) and the job exits non-zero well inside the timeout."""
+    import time
+    t = time.monotonic()
+    out = _run_bench_ws2(["--fail-rank", "1", "--fail-at", "plan"], timeout=180)
+    assert out.returncode != 0
+    assert time.monotonic() - t < 150
+    assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    # both ranks report the same failed rank
+    assert "rank 0: full plan failed on rank(s) [1]" in out.stderr, out.stderr[-2000:]
+    assert "rank 1: full plan failed on rank(s) [1]" in out.stderr
+    assert "Path not found" in out.stderr
+
+
+def test_bench_rank_failure_at_exchange_fails_every_rank():
+    """A rank that joins the waypoint all-gather with no set (count -1, the protocol of
+    epp_comm_allgather_waypoints) makes the all-gather raise on every rank."""
+    out = _run_bench_ws2(["--fail-rank", "0", "--fail-at", "exchange"], timeout=180)
+    assert out.returncode != 0
+    assert out.stderr.count("reported a failure") >= 2, out.stderr[-2000:]
+
+
+def _exchange_worker(rank, ws, d, q):
+    import sys
+    sys.path.insert(0, PKG)
+    os.environ["EPP_RDV_DIR"] = d
+    from eppamd.dist import file_exchange
+    q.put((rank, file_exchange("init", rank, ws, {"rank": rank, "uid": "ab" * 64 if rank == 0 else ""})))
+
+
+def test_file_rendezvous_ws2(tmp_path):
+    """The torch-free bootstrap of the RCCL communicator: every rank sees every rank's
+    payload (rank 0's id included)."""
+    ws = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, ws, str(tmp_path), q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(ws))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(ws):
+        assert [x["rank"] for x in res[r]] == [0, 1] and res[r][0]["uid"] == "ab" * 64
+
+
+def test_file_rendezvous_missing_rank_times_out(tmp_path, monkeypatch):
+    """A rank that never arrives (died before the rendezvous) ends the wait with an error
+    instead of a hang."""
+    import pytest
+    monkeypatch.setenv("EPP_RDV_DIR", str(tmp_path))
+    import sys
+    sys.path.insert(0, PKG)
+    from eppamd.dist import file_exchange
+    with pytest.raises(TimeoutError, match=r"ranks \[1\]"):
+        file_exchange("init", 0, 2, {"ok": True}, timeout=0.5)
+
+
+def test_spawn_ranks_terminates_hung_peers():
+    """spawn_ranks: when one rank exits non-zero the others get a grace period and are
+    then terminated (a rank stuck in a collective cannot hang the job)."""
+    import sys
+    import time
+    sys.path.insert(0, PKG)
+    from eppamd.dist import spawn_ranks
+    code = "import os, sys, time\nif os.environ['RANK'] == '1': sys.exit(3)\ntime.sleep(600)"
+    t = time.monotonic()
+    rc = spawn_ranks(2, [sys.executable, "-c", code], grace_s=1.0)
+    assert rc != 0 and time.monotonic() - t < 60

@@ -533,8 +533,9 @@ def test_mask_edges():
 
 def test_online_update_while_replanning_throws(track):
     """An update arriving while the online recomputation (recalculate_online) still runs
-    gets the reference's runtime_error (src/OnlineTrajGenerator.cpp:208-212), raised
-    before the world is touched; wait_for_update() then completes the first one."""
+    and needing a recomputation itself gets the reference's runtime_error
+    (src/OnlineTrajGenerator.cpp:208-212); the running worker's world is not touched;
+    wait_for_update() then completes the first one."""
     path, c, gates, obstacles, start, goal = track
     c2 = json.loads(json.dumps(c))
     c2["path_planner_properties"]["recalculate_online"] = True
@@ -679,3 +680,163 @@ def test_plan_tracks_across_devices(track, geom):
         assert dev == 0
         assert np.array_equal(wp, otg.get_waypoints())
         assert np.array_equal(traj, otg.get_planned_traj())
+
+
+# ---- the online replan against its CPU restatement (oracle/track_planner.py) ----------
+def _online_pair(track, geom, tmp_path, recalc):
+    import track_planner as TP
+    path, c, gates, obstacles, start, goal = track
+    c2 = json.loads(json.dumps(c))
+    c2["path_planner_properties"]["recalculate_online"] = recalc
+    p2 = tmp_path / f"c_online_{int(recalc)}.json"
+    p2.write_text(json.dumps(c2))
+    otg = _ot().OnlineTrajGenerator(start, goal, gates, obstacles, str(p2))
+    otg.pre_compute_traj(0.0)
+    cpu = TP.OnlineTrajGeneratorCPU(geom, c2, start, goal, gates, obstacles, threads=8)
+    cpu.pre_compute_traj(0.0)
+    assert np.array_equal(otg.get_waypoints(), cpu.waypoints)
+    return otg, cpu, c2, gates
+
+
+def _assert_same_state(otg, cpu, tol=1e-6):
+    assert np.array_equal(otg.get_checkpoints(), np.array(cpu.checkpoints))
+    assert np.array_equal(otg.get_waypoints(), cpu.waypoints)
+    traj = otg.get_planned_traj()
+    assert traj.shape == cpu.traj.shape and np.array_equal(traj[:, 9], cpu.traj[:, 9])
+    assert np.abs(traj[:, :9] - cpu.traj[:, :9]).max() < tol
+
+
+@pytest.mark.parametrize("recalc", [False, True])
+def test_online_replan_equals_cpu_restatement(tmp_path, track, geom, recalc):
+    """OnlineTrajGenerator::updateGatePos -> recomputeTraj (src/OnlineTrajGenerator.cpp:
+    123-226, :258-421) pinned to the CPU restatement: the same decision, the two segment
+    plans (seeded by the planner's call index), includeGates2 on the slice, the refit from
+    the advanced state and the merge give identical checkpoints and waypoints and a
+    trajectory within 1e-6 with the time column exact -- for a sequence of updates (two
+    replans and a gate already observed), inline and on the online worker.
+
+    The replan starts from a row of the current trajectory, whose bits seed the planner:
+    the CPU copy continues from the product's rows (equal to its own within 1e-6, checked),
+    so both replan from the same state."""
+    otg, cpu, c2, gates = _online_pair(track, geom, tmp_path, recalc)
+    before = otg.get_planned_traj()
+    assert np.array_equal(before[:, 9], cpu.traj[:, 9]) and np.abs(before[:, :9] - cpu.traj[:, :9]).max() < 1e-6
+    replans = 0
+    for gid, shift, t_fly in ((2, 0.3, 2.0), (5, 0.3, 6.5), (2, 0.3, 6.6)):
+        cur = otg.get_planned_traj()
+        cpu.traj = cur.copy()
+        i = int(np.argmin(np.abs(cur[:, 9] - t_fly)))
+        drone = cur[i, [0, 3, 6]]
+        pose = _lateral(gates[gid], shift)
+        r = otg.update_gate_pos(gid, pose, drone, True, t_fly)
+        if recalc:
+            otg.wait_for_update()
+        rc = cpu.update_gate_pos(gid, np.array(pose), drone, True, t_fly)
+        assert r == rc, (gid, r, rc)
+        replans += int(r)
+        _assert_same_state(otg, cpu)
+    assert replans >= 1 and cpu.calls == 9 + 2 * replans  # each replan took two planner calls
+
+
+def test_online_update_during_replan_keeps_reference_returns(tmp_path, track, geom):
+    """While an online recomputation runs (recalculate_online), another gate's update gets
+    the reference's answer: the gate is recorded and checked against the world with the
+    new pose, False when the current trajectory stays valid and passing, the reference's
+    "still going on" error only when a new recomputation would be needed
+    (src/OnlineTrajGenerator.cpp:141-212).  The decision equals the CPU restatement's on
+    the same trajectory and world; the world rebuild reaches the product once the worker
+    finished."""
+    import track_planner as TP
+    path, c, gates, obstacles, start, goal = track
+    c2 = json.loads(json.dumps(c))
+    c2["path_planner_properties"]["recalculate_online"] = True
+    c2["path_planner_properties"]["samples_fmt"] = 1 << 20  # a replan of ~10 ms: still running below
+    p2 = tmp_path / "c_busy.json"
+    p2.write_text(json.dumps(c2))
+    otg = _ot().OnlineTrajGenerator(start, goal, gates, obstacles, str(p2))
+    otg.pre_compute_traj(0.0)
+    before = otg.get_planned_traj()
+    t_fly = 2.0
+    i = int(np.argmin(np.abs(before[:, 9] - t_fly)))
+    drone = before[i, [0, 3, 6]]
+    first = 2
+    pose_first = _lateral(gates[first], 0.3)
+    assert otg.update_gate_pos(first, pose_first, drone, True, t_fly) is True
+    # gate 4 (yaw near pi: the reference's gate-frame test, src/OnlineTrajGenerator.cpp:
+    # 234-245, sees the trajectory pass it) unchanged: valid and passing -> False
+    updates = ((4, 0.0), (6, 0.02), (5, 0.3))
+    # the CPU restatement sees the same trajectory and the same sequence of recorded poses
+    cpu = TP.OnlineTrajGeneratorCPU(geom, c2, start, goal, gates, obstacles)
+    cpu.traj = before.copy()
+    cpu.observe(first, np.array(pose_first), drone, True, t_fly)
+    outcomes = []
+    for gid, shift in updates:
+        pose = _lateral(gates[gid], shift)
+        need = cpu.observe(gid, np.array(pose), drone, True, t_fly)
+        try:
+            got = "true" if otg.update_gate_pos(gid, pose, drone, True, t_fly) else "false"
+        except RuntimeError as e:
+            assert "while previous update is still going on" in str(e)
+            got = "busy"
+        assert got == ("busy" if need else "false"), (gid, got, need)
+        outcomes.append(got)
+    assert "false" in outcomes  # an update that needs no replan returns False, not an error
+    otg.wait_for_update()
+    # the deferred rebuild: the product's world now holds every recorded pose
+    g_now = gates.copy()
+    g_now[first, :6] = pose_first
+    for gid, shift in updates:
+        g_now[gid, :6] = _lateral(gates[gid], shift)
+    exp = _ot().PathPlanner(g_now, obstacles, str(p2)).world_obbs()
+    assert np.array_equal(otg.planner().world_obbs(), exp)
+    # recorded gates are not observed again
+    assert otg.update_gate_pos(4, _lateral(gates[4], 0.3), drone, True, t_fly) is False
+
+
+# ---- multi-GPU error protocol ------------------------------------------------------------
+def test_comm_failure_protocol_single_rank():
+    """A rank with no set (its own work failed) joins the all-gather with count -1: every
+    rank gets EPP_ERR_PEER with the counts naming it; the all-reduce and barrier the bench
+    uses for its max-over-ranks timing and collective error flags."""
+    c = capi.Comm(capi.Comm.unique_id(), 1, 0)
+    with pytest.raises(capi.EppError) as e:
+        c.allgather_waypoints(None, cap=16)
+    assert e.value.code == capi.EPP_ERR_PEER and list(e.value.counts) == [-1]
+    wp = synth.sample_states(4, [-6, -6, 0], [6, 6, 2], 9)
+    assert np.array_equal(c.allgather_waypoints(wp, cap=16)[0], wp)  # usable afterwards
+    x = np.array([1.5, -2.0, 7.25])
+    for op in (capi.EPP_REDUCE_SUM, capi.EPP_REDUCE_MAX, capi.EPP_REDUCE_MIN):
+        assert np.array_equal(c.allreduce(x, op), x)
+    c.barrier()
+    c.close()
+
+
+def test_rccl_group_single_rank():
+    """eppamd.dist.RcclGroup (the bench's torch-free process group) on one rank."""
+    from eppamd.dist import LegFailed, RcclGroup
+    g = RcclGroup(1, 0)
+    g.barrier()
+    assert g.max(3.0) == 3.0 and g.sum(2.0) == 2.0
+    wp = synth.sample_states(5, [-6, -6, 0], [6, 6, 2], 4)
+    assert np.array_equal(g.all_gather_waypoints(wp)[0], wp)
+    with pytest.raises(LegFailed) as e:
+        g.all_gather_waypoints(None)
+    assert e.value.failed == [0]
+    with pytest.raises(LegFailed):
+        g.check(RuntimeError("Path not found"))
+    g.check(None)
+    g.close()
+
+
+def test_plan_tracks_failure_raises_not_hangs(track, geom):
+    """planTracks with an unplannable track (its goal inside an obstacle) raises that
+    track's "Path not found" instead of stranding the other rounds in the all-gather;
+    a later call on the same device still works."""
+    path, c, gates, obstacles, start, goal = track
+    blocked_goal = obstacles[0, :3] + [0.0, 0.0, 0.5]
+    problems = [(start, goal, gates, obstacles), (start, blocked_goal, gates, obstacles),
+                (start, goal, gates, obstacles)]
+    with pytest.raises(RuntimeError, match="Path not found"):
+        _ot().plan_tracks(problems, path, [0])
+    res = _ot().plan_tracks(problems[:1], path, [0])
+    assert len(res) == 1 and len(res[0][0]) > 2
