@@ -13,8 +13,8 @@
 //   p_i      = A_i^-1 [d(vertex i); d(vertex i+1)]           impl :262-283
 // The free constraints are derivatives 1..4 of the inner vertices, so R_pp is
 // block-tridiagonal with 4x4 blocks (vertex v couples only with v-1 and v+1).  It is
-// SPD and solved by a block Cholesky (block Thomas) instead of the reference's
-// Eigen SparseQR/COLAMD; the two agree to rounding (parity target 1e-6).
+// SPD and solved by block elimination (block Thomas with explicit 4x4 inverses) instead
+// of the reference's Eigen SparseQR/COLAMD; the two agree to rounding (parity target 1e-6).
 //
 // Sampling reproduces Trajectory::evaluateRange (src/trajectory.cpp:81-141) exactly:
 // one lane runs the sequential `acc += dt` / segment roll-over recurrence (so sample
@@ -135,11 +135,10 @@ __device__ __forceinline__ double ainv_entry(const double* kc, const double* ipo
 
 // Per-segment scratch (doubles): A^-1 (10x10), H (10x10), the 6x6 snap block Q of Q_i,
 // G = Q * (rows 4..9 of A^-1) (6x10), the R_pp blocks: W (coupling to the next inner
-// vertex) and L (diagonal block, then its Cholesky factor), I (1 / diagonal of the
-// factor), and the powers of T.
+// vertex, then the block solve's S^-1 E) and L (diagonal block), 4 spare, and the powers
+// of T.
 struct Seg {
-    static constexpr int kAinv = 0, kH = 100, kQ = 200, kG = 236, kW = 296, kL = 312, kI = 328, kPow = 332,
-                         kSize = 354;
+    static constexpr int kAinv = 0, kH = 100, kQ = 200, kG = 236, kW = 296, kL = 312, kPow = 332, kSize = 354;
 };
 // kPow: T^0..T^11 (Q's powers) then (1/T)^0..(1/T)^9 (A^-1's), each the same chain of
 // products as evaluated per entry before (12 + 10 doubles)
@@ -283,151 +282,135 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ kc, const 
     block_sync<SCR_LDS>();
     EPP_TL(5);
     EPP_TLC(14);
-    // ---- phase 4: block Cholesky solve (4x4 blocks, 3 right-hand sides) ---------------
-    // The inner vertices are eliminated in order (block Thomas): per step v the Schur
-    // complement S_v = D_v - W_{v-1}^T W_{v-1}, z_v = b_v - W_{v-1}^T z_{v-1}, the Cholesky
-    // factor L_v of S_v and the forward solves z_v <- L_v^-1 z_v, W_v = L_v^-1 E_v; then
-    // x_v = L_v^-T (z_v - W_v x_{v+1}) backwards.  Seven lanes of the first wavefront own
-    // one column each of the seven column operations a step consists of: lanes 0..3 the
-    // columns of S (Schur update) and then of W (forward solve of E's column), lanes 4..6
-    // the columns of z; S is exchanged through LDS (`xch`) and every lane factors it
-    // redundantly in registers; W_v goes to LDS for the next step's Schur update.  Per
-    // entry the arithmetic is the single-lane elimination's (same FMAs in the same order),
-    // but a step is ~4x fewer dependent instructions.  Newton-refined reciprocal square
-    // roots instead of divisions / square roots (within ~1e-15 of them).
-    if (tid < 7 && nin > 0) {
-        const int c = tid;
-        const bool wcol = c < 4;  // else z column d = c - 4
-        const int d = c - 4;
-        double* xS = xch;       // S_v, row-major (p * 4 + q)
-        double* xW = xch + 16;  // W_{v-1}, row-major
+    // ---- phase 4: block-tridiagonal solve (block Thomas, explicit 4x4 inverses) ---------
+    // Inner vertices v = 1..nin, diagonal blocks D_v, couplings E_v (v -> v+1), right-hand
+    // sides b_v (3 columns):
+    //   S_1 = D_1, y_1 = b_1;  G_v = S_v^-1 E_v, g_v = S_v^-1 y_v;
+    //   S_{v+1} = D_{v+1} - E_v^T G_v, y_{v+1} = b_{v+1} - E_v^T g_v;
+    //   back: x_nin = g_nin, x_v = g_v - G_v x_{v+1}.
+    // S_v^-1 = adj(S_v) / det(S_v) from the 2x2 minors of its row pairs: independent
+    // products, no square roots or pivots, so a step is ~20 dependent instructions where
+    // the Cholesky's chain (4 dependent square roots, 4 dependent forward substitutions)
+    // was ~80.  The whole first wavefront runs every step with the same (uniform) values --
+    // no lane exchange, no barrier inside the chain; lane 0 stores G_v, g_v for the back
+    // substitution, which the same wave then runs.  The Schur complements of an SPD
+    // R_pp are SPD (det > 0); the explicit inverse is within ~cond(S_v) ulp of the
+    // factorisation's answer (parity target 1e-6).
+    if (tid < kWave && nin > 0) {
         bool ok = true;
-        double prev[4];  // this lane's column of step v-1: W_{v-1}[:, c] or z_{v-1}[:, d]
-        double base[4], ecol[4];  // step v's D_v[:, c] or b_v[:, d]; E_v[:, c]
-        // (branch-free: one address per lane, so the loads of a step are not split over
-        // exec-masked branches that each wait for their own LDS round trip)
-        auto load = [&](int v, double (&bs)[4], double (&ec)[4]) {
-            const double* Sg = scr + (size_t)(v - 1) * Seg::kSize;
-            const double* bp = wcol ? Sg + Seg::kL + c : rhs + (size_t)v * 12 + d;
-            const int bstride = wcol ? 4 : 3;
-            const double* ep = Sg + Seg::kW + (wcol ? c : 0);  // (z lanes: read, unused)
+        double S[16], y[12];
+        {
+            const double* Sg = scr;  // segment 0: D_1
 #pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                bs[p] = bp[p * bstride];
-                ec[p] = ep[p * 4];
-            }
-        };
-        load(1, base, ecol);
+            for (int i = 0; i < 16; ++i) S[i] = Sg[Seg::kL + i];
+#pragma unroll
+            for (int i = 0; i < 12; ++i) y[i] = rhs[4 * 3 + i];
+        }
         for (int v = 1; v <= nin; ++v) {
             EPP_TLI(v);
-            double col[4], e[4];
+            double* Sg = scr + (size_t)(v - 1) * Seg::kSize;
+            double E[16], Dn[16], bn[12];
 #pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                col[p] = base[p];
-                e[p] = ecol[p];
+            for (int i = 0; i < 16; ++i) E[i] = Sg[Seg::kW + i];  // (zero for v = nin)
+            if (v < nin) {  // next step's D and b: independent of this step, in flight meanwhile
+                const double* Sn = Sg + Seg::kSize;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) Dn[i] = Sn[Seg::kL + i];
+#pragma unroll
+                for (int i = 0; i < 12; ++i) bn[i] = rhs[(size_t)(v + 1) * 12 + i];
             }
-            if (v < nin) load(v + 1, base, ecol);  // independent of this step: in flight meanwhile
-            if (v > 1) {
-                double Wp[16];
-#pragma unroll
-                for (int i = 0; i < 16; ++i) Wp[i] = xW[i];
-#pragma unroll
-                for (int p = 0; p < 4; ++p)
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) col[p] = fma(-Wp[k * 4 + p], prev[k], col[p]);
-            }
-            if (wcol) {
-#pragma unroll
-                for (int p = 0; p < 4; ++p) xS[p * 4 + c] = col[p];
-            }
-            wave_sync_lds();
-            // Cholesky of S (lower triangle), on every lane
-            double L[16], inv[4];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) L[i] = xS[i];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                double dd = L[j * 5];
-#pragma unroll
-                for (int k = 0; k < j; ++k) dd = fma(-L[j * 4 + k], L[j * 4 + k], dd);
-                ok = ok && (dd > 0.0);
-                const double r = rsq_nr(dd);
-                inv[j] = r;
-                L[j * 5] = dd * r;
-#pragma unroll
-                for (int i = j + 1; i < 4; ++i) {
-                    double t = L[i * 4 + j];
-#pragma unroll
-                    for (int k = 0; k < j; ++k) t = fma(-L[i * 4 + k], L[j * 4 + k], t);
-                    L[i * 4 + j] = t * r;
-                }
-            }
-            if (!ok) break;  // (the same on every lane)
-            // forward solve of this lane's column: E_v[:, c] -> W_v[:, c], or z
-            double x[4];
+            // adj(S) from the 2x2 minors of rows (0,1) and (2,3)
+            const double s0 = S[0] * S[5] - S[4] * S[1], s1 = S[0] * S[6] - S[4] * S[2];
+            const double s2 = S[0] * S[7] - S[4] * S[3], s3 = S[1] * S[6] - S[5] * S[2];
+            const double s4 = S[1] * S[7] - S[5] * S[3], s5 = S[2] * S[7] - S[6] * S[3];
+            const double c5 = S[10] * S[15] - S[14] * S[11], c4 = S[9] * S[15] - S[13] * S[11];
+            const double c3 = S[9] * S[14] - S[13] * S[10], c2 = S[8] * S[15] - S[12] * S[11];
+            const double c1 = S[8] * S[14] - S[12] * S[10], c0 = S[8] * S[13] - S[12] * S[9];
+            const double det = ((s0 * c5 - s1 * c4) + (s2 * c3 + s3 * c2)) + (s5 * c0 - s4 * c1);
+            double A[16];
+            A[0] = (S[5] * c5 - S[6] * c4) + S[7] * c3;
+            A[1] = (S[2] * c4 - S[1] * c5) - S[3] * c3;
+            A[2] = (S[13] * s5 - S[14] * s4) + S[15] * s3;
+            A[3] = (S[10] * s4 - S[9] * s5) - S[11] * s3;
+            A[4] = (S[6] * c2 - S[4] * c5) - S[7] * c1;
+            A[5] = (S[0] * c5 - S[2] * c2) + S[3] * c1;
+            A[6] = (S[14] * s2 - S[12] * s5) - S[15] * s1;
+            A[7] = (S[8] * s5 - S[10] * s2) + S[11] * s1;
+            A[8] = (S[4] * c4 - S[5] * c2) + S[7] * c0;
+            A[9] = (S[1] * c2 - S[0] * c4) - S[3] * c0;
+            A[10] = (S[12] * s4 - S[13] * s2) + S[15] * s0;
+            A[11] = (S[9] * s2 - S[8] * s4) - S[11] * s0;
+            A[12] = (S[5] * c1 - S[4] * c3) - S[6] * c0;
+            A[13] = (S[0] * c3 - S[1] * c1) + S[2] * c0;
+            A[14] = (S[13] * s1 - S[12] * s3) - S[14] * s0;
+            A[15] = (S[8] * s3 - S[9] * s1) + S[10] * s0;
+            ok = ok && det > 0.0 && S[0] > 0.0 && S[5] > 0.0 && S[10] > 0.0 && S[15] > 0.0;
+            // 1/det: the hardware reciprocal refined by two Newton steps
+            double id = __builtin_amdgcn_rcp(det);
+            id = fma(id, fma(-det, id, 1.0), id);
+            id = fma(id, fma(-det, id, 1.0), id);
+            // G = S^-1 E, g = S^-1 y (adj products first: they do not wait for 1/det)
+            double G[16], gy[12];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                double t = wcol ? e[i] : col[i];
 #pragma unroll
-                for (int k = 0; k < i; ++k) t = fma(-L[i * 4 + k], x[k], t);
-                x[i] = t * inv[i];
+                for (int j = 0; j < 4; ++j)
+                    G[i * 4 + j] = ((A[i * 4] * E[j] + A[i * 4 + 1] * E[4 + j]) + (A[i * 4 + 2] * E[8 + j] + A[i * 4 + 3] * E[12 + j])) * id;
+#pragma unroll
+                for (int d = 0; d < 3; ++d)
+                    gy[i * 3 + d] = ((A[i * 4] * y[d] + A[i * 4 + 1] * y[3 + d]) + (A[i * 4 + 2] * y[6 + d] + A[i * 4 + 3] * y[9 + d])) * id;
             }
-            double* Sg = scr + (size_t)(v - 1) * Seg::kSize;
-            if (wcol) {
+            if (tid == 0) {  // for the back substitution (W slot: E_v is not needed again)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    Sg[Seg::kW + i * 4 + c] = x[i];
-                    xW[i * 4 + c] = x[i];
+                for (int i = 0; i < 16; ++i) Sg[Seg::kW + i] = G[i];
+#pragma unroll
+                for (int i = 0; i < 12; ++i) rhs[(size_t)v * 12 + i] = gy[i];
+            }
+            if (v < nin) {
+#pragma unroll
+                for (int p = 0; p < 4; ++p) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        S[p * 4 + q] = Dn[p * 4 + q] - ((E[p] * G[q] + E[4 + p] * G[4 + q]) + (E[8 + p] * G[8 + q] + E[12 + p] * G[12 + q]));
+#pragma unroll
+                    for (int d = 0; d < 3; ++d)
+                        y[p * 3 + d] = bn[p * 3 + d] - ((E[p] * gy[d] + E[4 + p] * gy[3 + d]) + (E[8 + p] * gy[6 + d] + E[12 + p] * gy[9 + d]));
                 }
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) rhs[((size_t)v * 4 + i) * 3 + d] = x[i];
             }
-            if (c == 0) {
-#pragma unroll
-                for (int i = 0; i < 16; ++i) Sg[Seg::kL + i] = L[i];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) Sg[Seg::kI + i] = inv[i];
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) prev[i] = x[i];
-            wave_sync_lds();
         }
-        // (W, L, z of every vertex written by other lanes of this wave: LDS or, for long
-        // tracks, global scratch — a workgroup-scope fence makes the latter visible)
+        // (lane 0's stores, LDS or, for long tracks, global scratch: a workgroup-scope fence
+        // makes the latter visible to the wave's own later loads)
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         wave_sync_lds();
-        if (ok && !wcol) {
-            // back substitution of column d: x_v = L_v^-T (z_v - W_v x_{v+1})
-            double xn[4];
+        if (ok) {
             EPP_TLI(32);
+            double xn[12];
             for (int v = nin; v >= 1; --v) {
                 EPP_TLI(32 + nin + 1 - v);
                 const double* Sg = scr + (size_t)(v - 1) * Seg::kSize;
-                double x[4];
+                double x[12];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) x[i] = rhs[((size_t)v * 4 + i) * 3 + d];
+                for (int i = 0; i < 12; ++i) x[i] = rhs[(size_t)v * 12 + i];
                 if (v < nin) {
+                    double G[16];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) G[i] = Sg[Seg::kW + i];
 #pragma unroll
                     for (int p = 0; p < 4; ++p)
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) x[p] = fma(-Sg[Seg::kW + p * 4 + k], xn[k], x[p]);
+                        for (int d = 0; d < 3; ++d)
+                            x[p * 3 + d] = x[p * 3 + d] - ((G[p * 4] * xn[d] + G[p * 4 + 1] * xn[3 + d]) +
+                                                           (G[p * 4 + 2] * xn[6 + d] + G[p * 4 + 3] * xn[9 + d]));
                 }
 #pragma unroll
-                for (int i = 3; i >= 0; --i) {
-                    double t = x[i];
+                for (int i = 0; i < 12; ++i) xn[i] = x[i];
+                if (tid == 0) {  // derivatives 1..4 of vertex v: 12 consecutive values of dv
 #pragma unroll
-                    for (int k = i + 1; k < 4; ++k) t = fma(-Sg[Seg::kL + k * 4 + i], x[k], t);
-                    x[i] = t * Sg[Seg::kI + i];
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    xn[i] = x[i];
-                    dv[((size_t)v * HALF + 1 + i) * 3 + d] = x[i];
+                    for (int i = 0; i < 12; ++i) dv[((size_t)v * HALF + 1) * 3 + i] = x[i];
                 }
             }
         }
-        if (!ok && c == 0) *s_err = 1;
+        if (!ok && tid == 0) *s_err = 1;
         EPP_TLI(63);
     }
     block_sync<SCR_LDS>();

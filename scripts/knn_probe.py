@@ -1,0 +1,55 @@
+"""k-NN microbenchmark (diagnostics; not the driver's bench): the planner's node set of one
+C4 segment (65,536 samples in [-6,6]^2 x [0,2], the valid ones compacted: ~63k nodes),
+k = 16, through epp_knn_grid_ws on one stream; HIP-event time per call for each
+implementation selected by EPP_KNN_TILE (argv: the values to try, default "1 0").  Every
+implementation's table is compared with the first one's.  Run under
+`rocprofv3 --kernel-trace --stats` for the per-kernel split."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "efficient-path-planner_amd"), ROOT]
+from eppamd import capi, config, synth  # noqa: E402
+from bench import timed_kernel_ms  # noqa: E402
+
+
+def main():
+    modes = sys.argv[1:] or ["1", "0"]
+    L = capi.lib()
+    st = C.c_void_p()
+    capi.check(L.epp_stream_create(C.byref(st)))
+    st = st.value
+    cfg = config.load(os.path.join(ROOT, "configs", "config.json"))
+    geom = config.geometry(cfg)
+    rg, ro = config.inflate_radii(cfg)
+    gates, obstacles = synth.track_world(100)
+    w = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
+    lo, hi = synth.C2_BOUNDS
+    s = synth.sample_states(1234, lo, hi, 65536)
+    nodes = s[w.check_states(s, False).astype(bool)]
+    n, k = len(nodes), 16
+    d_n = capi.DeviceBuffer.from_array(np.ascontiguousarray(nodes), st)
+    d_k = capi.DeviceBuffer(4 * n * k)
+    ws = int(L.epp_knn_workspace_size(n))
+    d_ws = capi.DeviceBuffer(ws)
+    ref = None
+    for m in modes:
+        os.environ["EPP_KNN_TILE"] = m
+
+        def f(r):
+            capi.check(L.epp_knn_grid_ws(d_n.ptr, n, k, 0.0, d_k.ptr, d_ws.ptr, ws, st))
+        for r in range(3):
+            f(r)
+        ms = timed_kernel_ms(capi, st, f, 20)
+        capi.check(L.epp_stream_sync(st))
+        tab = d_k.download(np.int32, n * k).reshape(n, k)
+        same = True if ref is None else bool(np.array_equal(tab, ref))
+        ref = tab if ref is None else ref
+        print(f"EPP_KNN_TILE={m} nodes {n} k {k}: {ms * 1e3:.1f} us per call, equal to first: {same}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
