@@ -2,7 +2,7 @@
 C4 segment (65,536 samples in [-6,6]^2 x [0,2], the valid ones compacted: ~63k nodes),
 k = 16, through epp_knn_grid_ws on one stream; HIP-event time per call for each
 implementation selected by EPP_KNN_TILE (argv: the values to try, default "1 0").  Every
-implementation's table is compared with the first one's.  Run under
+implementation's table is compared with the all-pairs kernel's.  Run under
 `rocprofv3 --kernel-trace --stats` for the per-kernel split."""
 import ctypes as C
 import os
@@ -35,7 +35,10 @@ def main():
     d_k = capi.DeviceBuffer(4 * n * k)
     ws = int(L.epp_knn_workspace_size(n))
     d_ws = capi.DeviceBuffer(ws)
-    ref = None
+    # the all-pairs kernel's table (exact, the oracle-checked reference of the grid ones)
+    capi.check(L.epp_knn_bruteforce(d_n.ptr, n, k, 0.0, d_k.ptr, st))
+    capi.check(L.epp_stream_sync(st))
+    ref = d_k.download(np.int32, n * k).reshape(n, k)
     for m in modes:
         os.environ["EPP_KNN_TILE"] = m
 
@@ -46,9 +49,16 @@ def main():
         ms = timed_kernel_ms(capi, st, f, 20)
         capi.check(L.epp_stream_sync(st))
         tab = d_k.download(np.int32, n * k).reshape(n, k)
-        same = True if ref is None else bool(np.array_equal(tab, ref))
-        ref = tab if ref is None else ref
-        print(f"EPP_KNN_TILE={m} nodes {n} k {k}: {ms * 1e3:.1f} us per call, equal to first: {same}", flush=True)
+        same = bool(np.array_equal(tab, ref))
+        # the workspace starts with the grid parameters (struct KnnGrid, planner.hip):
+        # lo[3], h, inv_h (f64), dims[3], ncell, next, nretry, why[4] (i32)
+        hdr = d_ws.download(np.uint8, 80)
+        dims = hdr[40:52].view(np.int32)
+        nretry = int(hdr[60:64].view(np.int32)[0])
+        why = hdr[64:80].view(np.int32).tolist()
+        print(f"EPP_KNN_TILE={m} nodes {n} k {k}: {ms * 1e3:.1f} us per call, equal to all-pairs: {same}; "
+              f"grid {dims.tolist()} h {float(hdr[24:32].view(np.float64)[0]):.4f}, retries {nretry} "
+              f"(list/range/shell/crowded {why})", flush=True)
 
 
 if __name__ == "__main__":

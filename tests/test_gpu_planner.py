@@ -75,12 +75,12 @@ def test_knn_vs_bruteforce(k, method):
     assert np.array_equal(got, _knn_ref(nodes, k))
 
 
-@pytest.mark.parametrize("tile", ["1", "0"])
+@pytest.mark.parametrize("tile", ["2", "1", "0"])
 @pytest.mark.parametrize("k", [4, 8, 16, 32])
 def test_knn_grid_large(k, tile, monkeypatch):
     """Grid k-NN (used above 2048 nodes) vs the all-pairs kernel and numpy: clustered,
-    duplicated and lattice (many exact ties) nodes; with the tiled LDS kernel (k 8/16)
-    and with the per-query walk."""
+    duplicated and lattice (many exact ties) nodes; with the LDS cube kernel (the
+    default, k 4/8/16), the histogram-tile kernel and the per-query walk."""
     monkeypatch.setenv("EPP_KNN_TILE", tile)
     rs = np.random.RandomState(k)
     nodes = synth.sample_states(100 + k, [-6, -6, 0], [6, 6, 2], 4000)
@@ -96,10 +96,12 @@ def test_knn_grid_large(k, tile, monkeypatch):
     assert np.array_equal(capi.knn(nodes, k, method="grid_ws"), got)
 
 
+@pytest.mark.parametrize("tile", ["2", "1"])
 @pytest.mark.parametrize("k", [8, 16])
-def test_knn_tile_crowded_halo(k):
+def test_knn_tile_crowded_halo(k, tile, monkeypatch):
     """A cluster far denser than the grid's cell size: the tiles around it overflow their
     LDS capacity and walk from global memory; the answer stays exact."""
+    monkeypatch.setenv("EPP_KNN_TILE", tile)
     rs = np.random.RandomState(3)
     nodes = synth.sample_states(200 + k, [-6, -6, 0], [6, 6, 2], 6000)
     nodes[:3000] = rs.normal(0, 0.02, (3000, 3)) + [0.5, -0.5, 1]
