@@ -841,216 +841,6 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
     }
 }
 
-// ---- k_knn_cube: exact top-K straight out of LDS, one query per lane -----------------
-// A workgroup takes a block of kTileB^3 cells; the block plus a kTileH-cell halo (8^3
-// cells) is copied into LDS as the nodes' exact doubles (SoA) and ids.  Every query of
-// the block gets its own lane, which walks the 5^3 cube of cells around its own cell
-// (25 x-rows, each one contiguous LDS range), inner rows first, with the row / cell
-// pruning of tile_rows_near against its current K-th distance, and keeps its top-K
-// sorted by (distance, index) in registers (knn_insert: the exact distances and tie
-// rule of k_knn).  Exact when the K-th distance is below the distance to the cube's
-// nearest face with cells beyond it (knn_done after shell kTileH); else, and for halos
-// over capacity, the query goes to the retry list (k_knn_retry).  Against k_knn_tile
-// (float histogram, candidate list, then exact distances from global memory with only
-// one lane per query busy): no LDS atomics, no barriers between a block's queries, no
-// global loads after the copy.
-//
-// The halo copy: the halo's 64 x-rows are contiguous ranges of the cell-sorted nodes, so
-// the copy is a flattened gather (each element found by a binary search over the rows'
-// LDS offsets), eight elements per thread in flight.
-constexpr int kCubeThreads = 128;
-constexpr int kCubeCap = 1344;  // candidates a halo may hold (else its queries retry)
-constexpr int kCubeRows = kTileE * kTileE;  // halo x-rows (64)
-
-template <int K>
-__global__ __launch_bounds__(kCubeThreads) void k_knn_cube(KnnGrid* __restrict__ gp, double r2max,
-                                                           const double* __restrict__ sxyz,
-                                                           const int* __restrict__ sidx,
-                                                           const int* __restrict__ start,
-                                                           int* __restrict__ retry, int32_t* __restrict__ nbr) {
-    __shared__ double cx[kCubeCap], cy[kCubeCap], cz[kCubeCap];
-    __shared__ int cid[kCubeCap];
-    __shared__ int cst[kTileCells + 1];   // halo cell -> LDS offset
-    __shared__ int rbase[kCubeRows + 1];  // halo row -> LDS offset of its first element
-    __shared__ int rgs[kCubeRows];        // halo row -> its first element in the sorted nodes
-    __shared__ int qbase[kTileB * kTileB + 1];  // inner row -> first query index
-    __shared__ int s_b;
-    const KnnGrid g = *gp;
-    const int nbx = (g.dims[0] + kTileB - 1) / kTileB, nby = (g.dims[1] + kTileB - 1) / kTileB,
-              nbz = (g.dims[2] + kTileB - 1) / kTileB;
-    const int nblocks = nbx * nby * nbz;
-    const int tid = threadIdx.x, lane = tid & 63;
-    for (;;) {
-        if (tid == 0) s_b = atomicAdd(&gp->next, 1);
-        __syncthreads();
-        const int b = s_b;  // block-uniform
-        if (b >= nblocks) break;
-        const int bx = b % nbx, by = (b / nbx) % nby, bz = b / (nbx * nby);
-        const int ox = bx * kTileB - kTileH, oy = by * kTileB - kTileH, oz = bz * kTileB - kTileH;
-        // 1. rows: the global range of each halo x-row, and every halo cell's LDS offset
-        //    (threads 0..63: one row each; a wave scan of the row lengths)
-        if (tid < kCubeRows) {
-            const int hy = tid % kTileE, hz = tid / kTileE;
-            const int y = oy + hy, z = oz + hz;
-            const int x0 = max(ox, 0), x1 = min(ox + kTileE - 1, g.dims[0] - 1);
-            const bool in = y >= 0 && y < g.dims[1] && z >= 0 && z < g.dims[2] && x0 <= x1;
-            const int c0 = in ? (z * g.dims[1] + y) * g.dims[0] + x0 : 0;
-            int sx[kTileE + 1];
-#pragma unroll
-            for (int k = 0; k <= kTileE; ++k) {  // start[] of the row's cells (clamped: empty outside the grid)
-                const int x = min(max(ox + k, x0), x1 + 1);
-                sx[k] = in ? start[c0 + (x - x0)] : 0;
-            }
-            const int len = sx[kTileE] - sx[0];
-            int incl = len;
-            for (int o = 1; o < 64; o <<= 1) {
-                const int v = __shfl_up(incl, o, 64);
-                if (lane >= o) incl += v;
-            }
-            const int rb = incl - len;
-            rbase[tid] = rb;
-            rgs[tid] = sx[0];
-            if (tid == kCubeRows - 1) rbase[kCubeRows] = incl;
-#pragma unroll
-            for (int k = 0; k < kTileE; ++k) cst[tid * kTileE + k] = rb + (sx[k] - sx[0]);
-            if (tid == kCubeRows - 1) cst[kTileCells] = incl;
-        }
-        __syncthreads();
-        const int total = rbase[kCubeRows];
-        if (total <= kCubeCap) {  // block-uniform
-            // 2. copy the halo: element f of the concatenated rows, 8 per thread in flight
-            for (int f0 = 0; f0 < total; f0 += 8 * kCubeThreads) {
-                int q[8];
-                double vx[8], vy[8], vz[8];
-                int vi[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int f = min(f0 + u * kCubeThreads + tid, total - 1);
-                    int lo = 0, hi = kCubeRows - 1;  // last row with rbase <= f
-#pragma unroll
-                    for (int st = 0; st < 6; ++st) {
-                        const int mid = (lo + hi + 1) >> 1;
-                        if (rbase[mid] <= f) lo = mid;
-                        else hi = mid - 1;
-                    }
-                    q[u] = rgs[lo] + (f - rbase[lo]);
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    vx[u] = sxyz[3 * (int64_t)q[u]];
-                    vy[u] = sxyz[3 * (int64_t)q[u] + 1];
-                    vz[u] = sxyz[3 * (int64_t)q[u] + 2];
-                    vi[u] = sidx[q[u]];
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int f = f0 + u * kCubeThreads + tid;
-                    if (f < total) {
-                        cx[f] = vx[u];
-                        cy[f] = vy[u];
-                        cz[f] = vz[u];
-                        cid[f] = vi[u];
-                    }
-                }
-            }
-            // the block's queries: the inner cells' nodes, inner row by inner row
-            if (tid < 64) {
-                const int r = tid < kTileB * kTileB ? tid : 0;
-                const int hrow = (kTileH + r / kTileB) * kTileE + kTileH + r % kTileB;
-                const int a = hrow * kTileE;
-                const int len = tid < kTileB * kTileB ? cst[a + kTileH + kTileB] - cst[a + kTileH] : 0;
-                int incl = len;
-                for (int o = 1; o < 64; o <<= 1) {
-                    const int v = __shfl_up(incl, o, 64);
-                    if (lane >= o) incl += v;
-                }
-                if (tid < kTileB * kTileB) qbase[tid] = incl - len;
-                if (tid == 63) qbase[kTileB * kTileB] = incl;
-            }
-            __syncthreads();
-            const int nq = qbase[kTileB * kTileB];
-            for (int qi = tid; qi < nq; qi += kCubeThreads) {
-                int ir = 0;  // inner row holding query qi
-#pragma unroll
-                for (int st = 8; st > 0; st >>= 1)
-                    if (ir + st < kTileB * kTileB && qbase[ir + st] <= qi) ir += st;
-                const int hrow = (kTileH + ir / kTileB) * kTileE + kTileH + ir % kTileB;
-                const int me = cst[hrow * kTileE + kTileH] + (qi - qbase[ir]);
-                const double p[3] = {cx[me], cy[me], cz[me]};
-                const int self = cid[me];
-                const int c[3] = {knn_cell_axis(p[0], g, 0), knn_cell_axis(p[1], g, 1), knn_cell_axis(p[2], g, 2)};
-                const int hx = c[0] - ox, hy = c[1] - oy, hz = c[2] - oz;  // in [kTileH, kTileH + kTileB)
-                const double fr[3] = {p[0] - (g.lo[0] + (double)c[0] * g.h), p[1] - (g.lo[1] + (double)c[1] * g.h),
-                                      p[2] - (g.lo[2] + (double)c[2] * g.h)};
-                double gx[5];
-#pragma unroll
-                for (int k = 0; k < 5; ++k) gx[k] = tile_gap(k - 2, fr[0], g.h);
-                double bd[K];
-                int bi[K];
-#pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    bd[k] = r2max;
-                    bi[k] = 0x7fffffff;
-                }
-                // rows by distance class: the 9 rows of the 3x3 core first
-                for (int rr = 0; rr < 25; ++rr) {
-                    int dy, dz;
-                    if (rr < 9) {
-                        dy = rr % 3 - 1;
-                        dz = rr / 3 - 1;
-                    } else {  // the 16 outer rows of the 5x5 (|dy| == 2 or |dz| == 2)
-                        const int o = rr - 9;
-                        if (o < 5) { dy = o - 2; dz = -2; }
-                        else if (o < 10) { dy = o - 7; dz = 2; }
-                        else if (o < 13) { dy = -2; dz = o - 11; }
-                        else { dy = 2; dz = o - 14; }
-                    }
-                    const double gy = tile_gap(dy, fr[1], g.h), gz = tile_gap(dz, fr[2], g.h);
-                    const double gyz = gy * gy + gz * gz;
-                    const double thr = bd[K - 1];
-                    if (gyz > thr) continue;
-                    const double rem = thr - gyz;
-                    const int xa = gx[0] * gx[0] <= rem ? -2 : (gx[1] * gx[1] <= rem ? -1 : 0);
-                    const int xb = gx[4] * gx[4] <= rem ? 2 : (gx[3] * gx[3] <= rem ? 1 : 0);
-                    const int a = ((hz + dz) * kTileE + (hy + dy)) * kTileE + hx;
-                    const int q1 = cst[a + xb + 1];
-                    for (int q0 = cst[a + xa]; q0 < q1; q0 += 4) {
-                        double dd[4];
-                        int jj[4];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const int q = min(q0 + u, q1 - 1);
-                            const double ddx = cx[q] - p[0], ddy = cy[q] - p[1], ddz = cz[q] - p[2];
-                            dd[u] = (ddx * ddx + ddy * ddy) + ddz * ddz;
-                            jj[u] = q0 + u < q1 ? cid[q] : self;  // past the row: skipped below
-                        }
-#pragma unroll
-                        for (int u = 0; u < 4; ++u)
-                            if (jj[u] != self) knn_insert<K>(bd, bi, dd[u], jj[u]);
-                    }
-                }
-                if (knn_done<K>(g, c, p, kTileH, bd)) knn_store<K>(nbr, self, bi);
-                else {
-                    atomicAdd(&gp->why[2], 1);
-                    retry[atomicAdd(&gp->nretry, 1)] = self;
-                }
-            }
-        } else {
-            // crowded halo: the block's queries retry from global memory
-            for (int t2 = tid; t2 < kTileB * kTileB * kTileB; t2 += kCubeThreads) {
-                const int x = bx * kTileB + t2 % kTileB, y = by * kTileB + (t2 / kTileB) % kTileB,
-                          z = bz * kTileB + t2 / (kTileB * kTileB);
-                if (x >= g.dims[0] || y >= g.dims[1] || z >= g.dims[2]) continue;
-                const int cell = (z * g.dims[1] + y) * g.dims[0] + x;
-                const int e = start[cell + 1];
-                for (int t = start[cell]; t < e; ++t) retry[atomicAdd(&gp->nretry, 1)] = sidx[t];
-                if (e > start[cell]) atomicAdd(&gp->why[3], e - start[cell]);
-            }
-        }
-        __syncthreads();  // the LDS tile is rewritten by the next block
-    }
-}
-
 // Retry list of k_knn_tile: one wave per query (knn_retry_wave).
 template <int K>
 __global__ __launch_bounds__(256) void k_knn_retry(const KnnGrid* __restrict__ gp, double r2max,
@@ -1129,12 +919,14 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
     hipLaunchKernelGGL(k_knn_count, g256, b256, 0, s, nodes, n, g, cell_of, cnt);
     hipLaunchKernelGGL(k_knn_scan, dim3(1), dim3(kBoundsThreads), 0, s, g, cnt, start);
     hipLaunchKernelGGL(k_knn_scatter, g256, b256, 0, s, nodes, n, cell_of, start, fill, sxyz, sidx);
-    // EPP_KNN_TILE (a test hook choosing among exact implementations: same answers):
-    // unset / 2 = k_knn_cube, 1 = k_knn_tile, 0 = the untiled grid walk.  The timing
-    // ablations and the per-block dump exist only in a -DEPP_KNN_DIAG diagnostics build.
+    // EPP_KNN_TILE=0 selects the untiled grid walk (same answer; a test hook); the product
+    // accepts only {0, 1}.  The timing ablations and the per-block dump exist only in a
+    // -DEPP_KNN_DIAG diagnostics build.  (A one-query-per-lane variant that keeps the exact
+    // top-K in registers straight out of an LDS copy of the halo was tried: 425 us per
+    // 63k-node table against k_knn_tile's 134 us -- the sorted insert then runs for nearly
+    // every candidate of every lane.)
     const char* tile_env = std::getenv("EPP_KNN_TILE");
-    const int impl = tile_env && *tile_env ? std::atoi(tile_env) : 2;
-    const bool tiled = impl != 0;
+    const bool tiled = !(tile_env && *tile_env && std::atoi(tile_env) == 0);
     if (tiled && (k == 4 || k == 8 || k == 16)) {
         // persistent: the block count is only known on the device (grid shape)
         int dev = 0, cus = 256;
@@ -1151,17 +943,9 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
         unsigned long long* d = nullptr;
 #endif
         int* retry = cell_of;  // free once the scatter has run
-        if (impl == 1) {
-            if (k == 4) hipLaunchKernelGGL(k_knn_tile<4>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr, mode, d);
-            else if (k == 8) hipLaunchKernelGGL(k_knn_tile<8>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr, mode, d);
-            else hipLaunchKernelGGL(k_knn_tile<16>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr, mode, d);
-        } else {
-            // persistent, four 128-thread workgroups per CU (40 KB of LDS each)
-            const dim3 gc((unsigned)std::max(1, cus * 4)), bc(kCubeThreads);
-            if (k == 4) hipLaunchKernelGGL(k_knn_cube<4>, gc, bc, 0, s, g, r2, sxyz, sidx, start, retry, nbr);
-            else if (k == 8) hipLaunchKernelGGL(k_knn_cube<8>, gc, bc, 0, s, g, r2, sxyz, sidx, start, retry, nbr);
-            else hipLaunchKernelGGL(k_knn_cube<16>, gc, bc, 0, s, g, r2, sxyz, sidx, start, retry, nbr);
-        }
+        if (k == 4) hipLaunchKernelGGL(k_knn_tile<4>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr, mode, d);
+        else if (k == 8) hipLaunchKernelGGL(k_knn_tile<8>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr, mode, d);
+        else hipLaunchKernelGGL(k_knn_tile<16>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr, mode, d);
         // one wave per retried query: up to two resident waves per SIMD (k_knn_retry<16>
         // holds ~250 VGPRs), so 2048 waves fill the chip; the rest exit at once
         const dim3 gr((unsigned)std::max(1, cus * 2)), br(256);
