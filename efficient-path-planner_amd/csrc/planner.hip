@@ -530,7 +530,7 @@ __device__ __forceinline__ void knn_store(int32_t* __restrict__ nbr, int self, c
 // bound" over all lanes -- then K rounds of a wave-wide (distance, index) arg-min merge
 // the lane lists; lane 0 writes the result.  Called by whole waves.
 template <int K>
-__device__ void knn_retry_wave(const KnnGrid& g, double r2max, const double* __restrict__ nodes,
+__device__ __forceinline__ void knn_retry_wave(const KnnGrid& g, double r2max, const double* __restrict__ nodes,
                                const double* __restrict__ sxyz, const int* __restrict__ sidx,
                                const int* __restrict__ start, int self, int32_t* __restrict__ nbr) {
     const int lane = threadIdx.x & 63;
@@ -843,7 +843,10 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
 
 // Retry list of k_knn_tile: one wave per query (knn_retry_wave).
 template <int K>
-__global__ __launch_bounds__(256) void k_knn_retry(const KnnGrid* __restrict__ gp, double r2max,
+// One wavefront per workgroup.  (knn_retry_wave is inlined: as a call it took the grid
+// parameters by reference to the caller's local copy, which then lived in scratch --
+// global-memory round trips on every cell index.)
+__global__ __launch_bounds__(64) void k_knn_retry(const KnnGrid* __restrict__ gp, double r2max,
                                                    const double* __restrict__ nodes,
                                                    const double* __restrict__ sxyz,
                                                    const int* __restrict__ sidx,
@@ -946,9 +949,8 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
         if (k == 4) hipLaunchKernelGGL(k_knn_tile<4>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr, mode, d);
         else if (k == 8) hipLaunchKernelGGL(k_knn_tile<8>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr, mode, d);
         else hipLaunchKernelGGL(k_knn_tile<16>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr, mode, d);
-        // one wave per retried query: up to two resident waves per SIMD (k_knn_retry<16>
-        // holds ~250 VGPRs), so 2048 waves fill the chip; the rest exit at once
-        const dim3 gr((unsigned)std::max(1, cus * 2)), br(256);
+        // one wave per retried query: 8 per CU; waves without a query exit at once
+        const dim3 gr((unsigned)std::max(1, cus * 8)), br(64);
         if (k == 4) hipLaunchKernelGGL(k_knn_retry<4>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr);
         else if (k == 8) hipLaunchKernelGGL(k_knn_retry<8>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr);
         else hipLaunchKernelGGL(k_knn_retry<16>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr);

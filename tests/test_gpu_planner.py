@@ -768,9 +768,12 @@ def test_online_update_during_replan_keeps_reference_returns(tmp_path, track, ge
         i = int(np.argmin(np.abs(before[:, 9] - t)))
         return t, before[i, [0, 3, 6]].copy()
 
+    # the running replan: gate 2 moved 0.3 m sideways, seen at t = 2 s (as
+    # test_online_update_gate_pos: its advanced start state is valid, so it plans)
     first = 2
     pose_first = _lateral(gates[first], 0.3)
-    t_first, d_first = seen(first)
+    t_first = 2.0
+    d_first = before[int(np.argmin(np.abs(before[:, 9] - t_first))), [0, 3, 6]].copy()
     assert otg.update_gate_pos(first, pose_first, d_first, True, t_first) is True
     updates = ((0, 0.0), (4, 0.0), (6, 0.02), (5, 0.3))
     # the CPU restatement sees the same trajectory and the same sequence of recorded poses
