@@ -447,6 +447,9 @@ __global__ __launch_bounds__(256) void k_knn_grid(const KnnGrid* __restrict__ gp
 // queries than threads, 2 or 4 adjacent lanes share one query (cube rows split between
 // them; the histogram and the list are shared through LDS atomics), so blocks take about
 // the same time whatever their query count.  Blocks come from a queue (costs differ).
+#ifdef EPP_KNN_DIAG
+constexpr int kKnnTlBlocks = 65536;  // timeline records
+#endif
 constexpr int kTileB = 4, kTileH = 2, kTileE = kTileB + 2 * kTileH, kTileCells = kTileE * kTileE * kTileE;
 constexpr int kTileW = 2 * kTileH + 1;  // cube edge around the query's cell
 constexpr int kTileRows = kTileW * kTileW;
@@ -655,7 +658,17 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
         const double cen[3] = {g.lo[0] + (ox + 0.5 * kTileE) * g.h, g.lo[1] + (oy + 0.5 * kTileE) * g.h,
                                g.lo[2] + (oz + 0.5 * kTileE) * g.h};
 #ifdef EPP_KNN_DIAG
-        const unsigned long long t_begin = dbg ? __builtin_amdgcn_s_memrealtime() : 0ull;
+        // phase timeline (diagnostics builds): begin, halo sizes scanned, halo copied, first
+        // query round's pass 1 / pass 2 / exact phase done, all queries done, end; counts
+        unsigned long long tl[8] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0, 0, 0, 0};
+#define EPP_KTL(k) \
+    do {           \
+        if (tl[k] == 0ull) tl[k] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define EPP_KTL(k) \
+    do {           \
+    } while (0)
 #endif
         // 1. halo cell sizes -> exclusive scan (thread t owns halo cells kPer*t ..)
         int cnt[kPer], cell0[kPer], tot = 0;
@@ -697,6 +710,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
             s_nq = 0;
         }
         __syncthreads();
+        EPP_KTL(1);
         if (total <= kTileCap) {  // block-uniform
             // 2. copy the halo's candidates; list the block's own nodes as queries
             int acc = base;
@@ -716,6 +730,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                 acc += cnt[u];
             }
             __syncthreads();
+            EPP_KTL(2);
             // 3. queries, lpq adjacent lanes per query
 #ifdef EPP_KNN_DIAG
             const int nq = mode == 4 ? 0 : s_nq;  // mode 4: timing ablation (inexact; diagnostics builds only)
@@ -747,6 +762,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                         if (valid && j != self && kb < kTileNB) atomicAdd(&hist[kb >> 1][slot], 1u << ((kb & 1) << 4));
                     });
                 __syncthreads();
+                EPP_KTL(3);
                 int cut = -1, run = 0;
 #pragma unroll
                 for (int w = 0; w < kTileNB / 2; ++w) {
@@ -774,6 +790,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                     });
                 }
                 __syncthreads();
+                EPP_KTL(4);
                 if (!live || sub != 0) continue;
                 const int nl = nls[slot];
                 bool ok = nl <= kTileL;
@@ -815,7 +832,11 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                     atomicAdd(&gp->why[0], 1);
                 }
                 if (!ok) retry[atomicAdd(&gp->nretry, 1)] = self;
+#ifdef EPP_KNN_DIAG
+                if (tl[5] == 0ull) tl[5] = __builtin_amdgcn_s_memrealtime();
+#endif
             }
+            EPP_KTL(6);
         } else {
             // crowded halo: the block's queries retry from global memory
             for (int t2 = threadIdx.x; t2 < kTileB * kTileB * kTileB; t2 += kTileThreads) {
@@ -830,12 +851,12 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
         }
         __syncthreads();  // the LDS tile is rewritten by the next block
 #ifdef EPP_KNN_DIAG
-        if (dbg && threadIdx.x == 0) {  // diagnostics: per-block timing (EPP_KNN_TILE_DBG)
-            const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
-            dbg[4 * b] = t_begin;
-            dbg[4 * b + 1] = t_end;
-            dbg[4 * b + 2] = (unsigned long long)s_nq;
-            dbg[4 * b + 3] = blockIdx.x;
+        if (dbg && threadIdx.x == 0 && b < kKnnTlBlocks) {  // (thread 0 is a query lane of slot 0)
+            tl[7] = __builtin_amdgcn_s_memrealtime();
+            for (int k = 0; k < 8; ++k) dbg[16 * b + k] = tl[k];
+            dbg[16 * b + 8] = (unsigned long long)s_nq;
+            dbg[16 * b + 9] = (unsigned long long)total;
+            dbg[16 * b + 10] = blockIdx.x;
         }
 #endif
     }
@@ -896,6 +917,18 @@ KnnLayout knn_layout(int n) {
 
 epp_status last(const char* what);
 
+#ifdef EPP_KNN_DIAG
+// the k_knn_tile phase timeline (diagnostics builds): 16 u64 per block, see the kernel
+unsigned long long* knn_tl_buffer() {
+    static unsigned long long* buf = nullptr;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        if (hipMalloc(&buf, (size_t)16 * 8 * kKnnTlBlocks) != hipSuccess) buf = nullptr;
+    });
+    return buf;
+}
+#endif
+
 epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, int32_t* nbr, char* buf,
                            const KnnLayout& L, hipStream_t s) {
     KnnGrid* g = reinterpret_cast<KnnGrid*>(buf);
@@ -937,10 +970,8 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
         const dim3 gt((unsigned)std::max(1, cus * 3)), bt(kTileThreads);
 #ifdef EPP_KNN_DIAG
         const int mode = tile_env ? std::atoi(tile_env) : 1;  // 4: timing ablation (inexact)
-        static unsigned long long* dbg = nullptr;
-        if (std::getenv("EPP_KNN_TILE_DBG") && !dbg && hipMalloc(&dbg, 4 * 8 * 65536) != hipSuccess) dbg = nullptr;
-        unsigned long long* d = std::getenv("EPP_KNN_TILE_DBG") ? dbg : nullptr;
-        if (d) (void)hipMemsetAsync(d, 0, 4 * 8 * 65536, s);
+        unsigned long long* d = knn_tl_buffer();
+        if (d) (void)hipMemsetAsync(d, 0, (size_t)16 * 8 * kKnnTlBlocks, s);
 #else
         const int mode = 1;
         unsigned long long* d = nullptr;
@@ -954,27 +985,6 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
         if (k == 4) hipLaunchKernelGGL(k_knn_retry<4>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr);
         else if (k == 8) hipLaunchKernelGGL(k_knn_retry<8>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr);
         else hipLaunchKernelGGL(k_knn_retry<16>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr);
-#ifdef EPP_KNN_DIAG
-        if (d) {
-            std::vector<unsigned long long> h(4 * 65536);
-            (void)hipStreamSynchronize(s);
-            (void)hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost);
-            unsigned long long t0 = ~0ull, t1 = 0;
-            for (int i = 0; i < 65536; ++i)
-                if (h[4 * i + 1]) t0 = std::min(t0, h[4 * i]), t1 = std::max(t1, h[4 * i + 1]);
-            KnnGrid hg;
-            (void)hipMemcpy(&hg, g, sizeof(hg), hipMemcpyDeviceToHost);
-            std::fprintf(stderr, "knn_tile n %d dims %d %d %d h %g retries %d (list %d range %d shell %d crowded %d) span_us %.1f\n",
-                         n, hg.dims[0], hg.dims[1], hg.dims[2], hg.h, hg.nretry, hg.why[0], hg.why[1], hg.why[2], hg.why[3],
-                         (t1 - t0) / 100.0);
-            const bool list = std::atoi(std::getenv("EPP_KNN_TILE_DBG")) == 1;
-            if (list) std::fprintf(stderr, "knn_tile blocks (start_us end_us nq wg):\n");
-            for (int i = 0; list && i < 65536; ++i)
-                if (h[4 * i + 1])
-                    std::fprintf(stderr, "%d %.2f %.2f %llu %llu\n", i, (h[4 * i] - t0) / 100.0, (h[4 * i + 1] - t0) / 100.0,
-                                 h[4 * i + 2], h[4 * i + 3]);
-        }
-#endif
     } else {
         switch (k) {
             case 4: hipLaunchKernelGGL(k_knn_grid<4>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
@@ -1157,6 +1167,15 @@ epp_status epp_knn(const double* nodes, int32_t n, int32_t k, double max_dist, i
 }
 
 uint64_t epp_knn_workspace_size(int32_t n) { return n <= 0 ? 0 : (uint64_t)knn_layout(n).bytes; }
+
+#ifdef EPP_KNN_DIAG
+// (diagnostics builds only) the last k_knn_tile launch's phase timeline: 16 u64 per block
+epp_status epp_dbg_knn_tl(unsigned long long* out, int64_t blocks) {
+    unsigned long long* d = knn_tl_buffer();
+    if (!d || blocks > kKnnTlBlocks) return EPP_ERR_RUNTIME;
+    return hipMemcpy(out, d, (size_t)blocks * 16 * 8, hipMemcpyDeviceToHost) == hipSuccess ? EPP_OK : EPP_ERR_HIP;
+}
+#endif
 
 epp_status epp_knn_ws(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr, void* ws,
                       uint64_t ws_bytes, void* stream) {

@@ -1,0 +1,62 @@
+"""Phase timeline of k_knn_tile (diagnostics; not the product): builds a diagnostics copy of
+libepp.so with -DEPP_KNN_DIAG into scripts/dbg/, runs the planner's k-NN (one C4 segment's
+~63k nodes, k = 16) and prints, over the blocks, percentiles of each phase's duration
+(thread 0's s_memrealtime stamps, 10 ns): halo sizes + scan, halo copy, first query
+round's pass 1 (histogram), pass 2 (list), exact phase, the other rounds, the tail."""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "efficient-path-planner_amd")]
+from eppamd import capi, config, synth  # noqa: E402
+
+out = os.path.join(ROOT, "scripts", "dbg")
+lib_path = os.path.join(out, "libepp_knndiag.so")
+if not os.path.exists(lib_path):
+    subprocess.run(["make", "-s", "-j16", "-C", os.path.join(ROOT, "efficient-path-planner_amd"),
+                    f"BUILD={out}/build_knn", f"LIB={lib_path}", "EXTRA=-DEPP_KNN_DIAG", lib_path], check=True)
+capi.LIB_PATH = lib_path
+L = capi.lib()
+L.epp_dbg_knn_tl.argtypes = [C.c_void_p, C.c_int64]
+cfg = config.load(os.path.join(ROOT, "configs", "config.json"))
+geom = config.geometry(cfg)
+rg, ro = config.inflate_radii(cfg)
+gates, obstacles = synth.track_world(100)
+w = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
+s = synth.sample_states(1234, *synth.C2_BOUNDS, 65536)
+nodes = np.ascontiguousarray(s[w.check_states(s, False).astype(bool)])
+n, k = len(nodes), 16
+d_n = capi.DeviceBuffer.from_array(nodes)
+d_k = capi.DeviceBuffer(4 * n * k)
+ws = int(L.epp_knn_workspace_size(n))
+d_ws = capi.DeviceBuffer(ws)
+recs = []
+for r in range(12):
+    capi.check(L.epp_knn_grid_ws(d_n.ptr, n, k, 0.0, d_k.ptr, d_ws.ptr, ws, None))
+    capi.sync()
+    if r >= 2:
+        tl = np.zeros((1024, 16), np.uint64)
+        capi.check(L.epp_dbg_knn_tl(tl.ctypes.data, 1024))
+        tl = tl[tl[:, 7] != 0].astype(np.int64)
+        recs.append(tl)
+t = np.concatenate(recs)
+names = ["scan", "copy", "pass1", "pass2", "exact", "rounds", "tail"]
+print(f"blocks per launch {len(recs[0])}, queries per block p50 {np.median(t[:, 8]):.0f} max {t[:, 8].max()}, "
+      f"halo candidates p50 {np.median(t[:, 9]):.0f} max {t[:, 9].max()}")
+for i, nm in enumerate(names):
+    a, b = t[:, i], t[:, i + 1]
+    ok = (a > 0) & (b > 0)
+    v = (b[ok] - a[ok]) * 10 / 1000.0
+    print(f"{nm:7s} p10 {np.percentile(v, 10):7.2f} p50 {np.percentile(v, 50):7.2f} p90 {np.percentile(v, 90):7.2f} "
+          f"max {v.max():7.2f} us")
+tot = (t[:, 7] - t[:, 0]) * 10 / 1000.0
+print(f"block   p10 {np.percentile(tot, 10):7.2f} p50 {np.percentile(tot, 50):7.2f} p90 {np.percentile(tot, 90):7.2f} "
+      f"max {tot.max():7.2f} us")
+for r in recs[:3]:
+    st = (r[:, 0] - r[:, 0].min()) * 10 / 1000.0
+    en = (r[:, 7] - r[:, 0].min()) * 10 / 1000.0
+    print(f"launch: block starts p50 {np.median(st):.2f} max {st.max():.2f} us, ends max {en.max():.2f} us")
