@@ -1,6 +1,8 @@
 // host_config.cpp — ConfigParser (src/ConfigParserYAML.cpp:10-118) over small
 // order-preserving JSON and block-YAML readers.  Object members keep document order,
 // which is the iteration order yaml-cpp gives the reference for component_geometry.
+#include <cctype>
+#include <cmath>
 #include <cstdlib>
 #include <fstream>
 #include <sstream>
@@ -142,15 +144,19 @@ private:
         } else if (lit("true")) {
             v.kind = JsonValue::Bool;
             v.b = true;
+            v.str = "true";  // (yaml-cpp reads a JSON scalar's text as the string)
         } else if (lit("false")) {
             v.kind = JsonValue::Bool;
             v.b = false;
+            v.str = "false";
         } else if (lit("null")) {
             v.kind = JsonValue::Null;
         } else {
             char* end = nullptr;
-            v.num = std::strtod(s_.c_str() + i_, &end);
-            if (end == s_.c_str() + i_) fail("bad value");
+            const char* at = s_.c_str() + i_;
+            v.num = std::strtod(at, &end);
+            if (end == at) fail("bad value");
+            v.str.assign(at, (size_t)(end - at));
             i_ = end - s_.c_str();
             v.kind = JsonValue::Number;
         }
@@ -286,6 +292,8 @@ private:
         if (t == "~" || t == "null" || t == "Null" || t == "NULL") return v;
         static const char* yes[] = {"true", "True", "TRUE", "yes", "Yes", "YES", "on", "On", "ON", "y", "Y"};
         static const char* no_[] = {"false", "False", "FALSE", "no", "No", "NO", "off", "Off", "OFF", "n", "N"};
+        // Bool and Number scalars keep their text: yaml-cpp's .as<std::string>() returns it
+        v.str = t;
         for (const char* s : yes)
             if (t == s) {
                 v.kind = JsonValue::Bool;
@@ -298,17 +306,48 @@ private:
                 v.b = false;
                 return v;
             }
-        char* end = nullptr;
-        const double d = std::strtod(t.c_str(), &end);
-        if (end && *end == '\0' && end != t.c_str()) {
+        double d = 0.0;
+        if (yaml_number(t, d)) {
             v.kind = JsonValue::Number;
             v.num = d;
-            v.str = t;
             return v;
         }
         v.kind = JsonValue::String;
-        v.str = t;
         return v;
+    }
+    // A plain scalar yaml-cpp's .as<double>() reads: decimal [-+]?(digits[.digits]|.digits)
+    // with an optional exponent, or [-+]?.inf / .nan (any of the three spellings).  Text
+    // strtod alone would also take (nan, inf, hex, ...) stays a string.
+    static bool yaml_number(const std::string& t, double& out) {
+        size_t k = 0;
+        const bool neg = k < t.size() && t[k] == '-';
+        if (k < t.size() && (t[k] == '-' || t[k] == '+')) ++k;
+        const std::string rest = t.substr(k);
+        if (rest == ".inf" || rest == ".Inf" || rest == ".INF") {
+            out = neg ? -HUGE_VAL : HUGE_VAL;
+            return true;
+        }
+        if (k == 0 && (rest == ".nan" || rest == ".NaN" || rest == ".NAN")) {
+            out = std::nan("");
+            return true;
+        }
+        size_t digits = 0;
+        while (k < t.size() && std::isdigit((unsigned char)t[k])) ++k, ++digits;
+        if (k < t.size() && t[k] == '.') {
+            ++k;
+            while (k < t.size() && std::isdigit((unsigned char)t[k])) ++k, ++digits;
+        }
+        if (digits == 0) return false;
+        if (k < t.size() && (t[k] == 'e' || t[k] == 'E')) {
+            ++k;
+            if (k < t.size() && (t[k] == '-' || t[k] == '+')) ++k;
+            size_t ed = 0;
+            while (k < t.size() && std::isdigit((unsigned char)t[k])) ++k, ++ed;
+            if (ed == 0) return false;
+        }
+        if (k != t.size()) return false;
+        out = std::strtod(t.c_str(), nullptr);
+        return true;
     }
     // flow collection text -> value; plain scalars inside are typed as above
     static JsonValue flow(const std::string& t, int no) {
@@ -506,7 +545,7 @@ bool boolean(const JsonValue& v, const std::string& what) {
 }
 std::string str(const JsonValue& v, const std::string& what) {
     if (v.kind == JsonValue::String) return v.str;
-    if (v.kind == JsonValue::Number && !v.str.empty()) return v.str;  // YAML plain scalar
+    if ((v.kind == JsonValue::Number || v.kind == JsonValue::Bool) && !v.str.empty()) return v.str;  // YAML plain scalar
     throw std::runtime_error("config: " + what + " is not a string");
 }
 Vec3 vec3(const JsonValue& v, const std::string& what) {

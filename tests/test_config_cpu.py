@@ -99,3 +99,27 @@ def test_missing_key_and_file(tmp_path):
         otp.load_config(str(p))
     with pytest.raises(RuntimeError, match="bad file"):
         otp.load_config(os.path.join(str(tmp_path), "nope.yaml"))
+
+
+def test_yaml_plain_scalars_keep_their_text(tmp_path, ref_dict):
+    """Plain scalars that YAML would type as bool (on, y, no ...) or that strtod alone
+    would read as a number (nan, inf, 0x10) stay readable as strings, as yaml-cpp's
+    .as<std::string>() returns their text: here a component called "on" (a gate type's
+    name, src/ConfigParserYAML.cpp:21-52) and OBB names "nan" / "0x10"."""
+    d = json.load(open(CONFIG))
+    mapping = d["gate_id_to_name_mapping"]
+    old = mapping["1"]
+    mapping["1"] = "on"
+    d["component_geometry"]["on"] = d["component_geometry"].pop(old)
+    d["component_properties"]["on"] = d["component_properties"].pop(old)
+    obbs = list(d["component_geometry"]["on"].values())
+    obbs[0]["name"], obbs[1]["name"] = "nan", "0x10"
+    text = "\n".join(_to_yaml(d, "plain")) + "\n"
+    assert "\n  1: on" in text or "1: on" in text
+    p = tmp_path / "config.yaml"
+    p.write_text(text)
+    got = otp.load_config(str(p))
+    assert [o["name"] for o in got["gate_geometry"][1][:2]] == ["nan", "0x10"]
+    strip = lambda g: {t: [{k: v for k, v in o.items() if k != "name"} for o in obbs] for t, obbs in g.items()}  # noqa: E731
+    assert strip(got["gate_geometry"]) == strip(ref_dict["gate_geometry"])
+    assert got["path_planner"] == ref_dict["path_planner"]
