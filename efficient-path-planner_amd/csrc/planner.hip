@@ -455,6 +455,7 @@ constexpr int kTileW = 2 * kTileH + 1;  // cube edge around the query's cell
 constexpr int kTileRows = kTileW * kTileW;
 constexpr int kTileCap = 1344;          // candidates a halo may hold (else its queries retry)
 constexpr int kTileThreads = 256;
+constexpr int kTileSlots = kTileThreads / 2;  // query slots (>= 2 lanes per query)
 constexpr int kTileL = 32;              // per-query list length
 constexpr int kTileNB = 16;             // histogram bins (16-bit counters, two per word)
 constexpr double kTileDelta = 1e-3;     // float error allowance, in h^2
@@ -619,7 +620,7 @@ __device__ __forceinline__ void knn_retry_wave(const KnnGrid& g, double r2max, c
 }
 
 template <int K>
-__global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restrict__ gp, double r2max,
+__global__ __launch_bounds__(kTileThreads, 2) void k_knn_tile(KnnGrid* __restrict__ gp, double r2max,
                                                            const double* __restrict__ nodes,
                                                            const double* __restrict__ sxyz,
                                                            const int* __restrict__ sidx,
@@ -628,11 +629,12 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                                                            int32_t* __restrict__ nbr, int mode,
                                                            unsigned long long* __restrict__ dbg) {
     __shared__ float4 cand[kTileCap];                      // x, y, z (block-centre relative), id
+    __shared__ double ex[3][kTileCap];                     // the exact coordinates (the exact phase)
     __shared__ uint16_t qh[kTileCap];                      // the block's queries (LDS positions)
     __shared__ int cst[kTileCells + 1];                    // halo cell -> LDS offset
-    __shared__ uint32_t hist[kTileNB / 2][kTileThreads];   // [bin pair][query slot]
-    __shared__ uint16_t lst[kTileL][kTileThreads];         // [entry][query slot]
-    __shared__ int nls[kTileThreads];                      // list lengths
+    __shared__ uint32_t hist[kTileNB / 2][kTileSlots];     // [bin pair][query slot]
+    __shared__ uint16_t lst[kTileL][kTileSlots];           // [entry][query slot]
+    __shared__ int nls[kTileSlots];                        // list lengths
     __shared__ int wsum[kTileThreads / 64];
     __shared__ int s_nq, s_b;
     const KnnGrid g = *gp;
@@ -723,8 +725,12 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                 const int q0 = (inner && cnt[u]) ? atomicAdd(&s_nq, cnt[u]) : 0;
                 for (int q = 0; q < cnt[u]; ++q) {
                     const int sg = cell0[u] + q;
-                    cand[acc + q] = make_float4((float)(sxyz[3 * sg] - cen[0]), (float)(sxyz[3 * sg + 1] - cen[1]),
-                                                (float)(sxyz[3 * sg + 2] - cen[2]), __int_as_float(sidx[sg]));
+                    const double x = sxyz[3 * sg], y = sxyz[3 * sg + 1], z = sxyz[3 * sg + 2];
+                    cand[acc + q] = make_float4((float)(x - cen[0]), (float)(y - cen[1]), (float)(z - cen[2]),
+                                                __int_as_float(sidx[sg]));
+                    ex[0][acc + q] = x;
+                    ex[1][acc + q] = y;
+                    ex[2][acc + q] = z;
                     if (inner) qh[q0 + q] = (uint16_t)(acc + q);
                 }
                 acc += cnt[u];
@@ -737,7 +743,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
 #else
             const int nq = s_nq;
 #endif
-            const int lpq = nq <= kTileThreads / 4 ? 4 : nq <= kTileThreads / 2 ? 2 : 1;  // block-uniform
+            const int lpq = nq <= kTileThreads / 4 ? 4 : 2;  // block-uniform (kTileSlots query slots)
             const int slot = threadIdx.x / lpq, sub = threadIdx.x % lpq;
             for (int qb = 0; qb < nq; qb += kTileThreads / lpq) {  // block-uniform
                 const int qi = qb + slot;
@@ -751,7 +757,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                 const float4 pf = cand[me];
                 const int self = __float_as_int(pf.w);
                 // exact coordinates and cell (the row offsets; the final distances)
-                const double p[3] = {nodes[3 * (int64_t)self], nodes[3 * (int64_t)self + 1], nodes[3 * (int64_t)self + 2]};
+                const double p[3] = {ex[0][me], ex[1][me], ex[2][me]};
                 const int c[3] = {knn_cell_axis(p[0], g, 0), knn_cell_axis(p[1], g, 1), knn_cell_axis(p[2], g, 2)};
                 const int h0 = ((c[2] - oz - kTileH) * kTileE + (c[1] - oy - kTileH)) * kTileE + (c[0] - ox - kTileH);
                 __syncthreads();  // cleared counters visible to the query's lanes
@@ -802,20 +808,17 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                         bd[k] = r2max;
                         bi[k] = 0x7fffffff;
                     }
-                    // exact distances of the listed candidates, kLoads at a time in flight
+                    // exact distances of the listed candidates (exact coordinates from LDS),
+                    // kLoads at a time in flight
                     constexpr int kLoads = 4;
                     for (int i0 = 0; i0 < nl; i0 += kLoads) {
                         double dd[kLoads];
                         int jj[kLoads];
 #pragma unroll
                         for (int u = 0; u < kLoads; ++u) {
-                            const int i = min(i0 + u, nl - 1);
-                            jj[u] = __float_as_int(cand[lst[i][slot]].w);
-                        }
-#pragma unroll
-                        for (int u = 0; u < kLoads; ++u) {
-                            const double ddx = nodes[3 * (int64_t)jj[u]] - p[0], ddy = nodes[3 * (int64_t)jj[u] + 1] - p[1],
-                                         ddz = nodes[3 * (int64_t)jj[u] + 2] - p[2];
+                            const int q = lst[min(i0 + u, nl - 1)][slot];
+                            jj[u] = __float_as_int(cand[q].w);
+                            const double ddx = ex[0][q] - p[0], ddy = ex[1][q] - p[1], ddz = ex[2][q] - p[2];
                             dd[u] = (ddx * ddx + ddy * ddy) + ddz * ddz;
                         }
 #pragma unroll
@@ -967,7 +970,7 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
         // persistent: the block count is only known on the device (grid shape)
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const dim3 gt((unsigned)std::max(1, cus * 3)), bt(kTileThreads);
+        const dim3 gt((unsigned)std::max(1, cus * 2)), bt(kTileThreads);  // (LDS: two workgroups per CU)
 #ifdef EPP_KNN_DIAG
         const int mode = tile_env ? std::atoi(tile_env) : 1;  // 4: timing ablation (inexact)
         unsigned long long* d = knn_tl_buffer();
