@@ -619,8 +619,11 @@ __device__ __forceinline__ void knn_retry_wave(const KnnGrid& g, double r2max, c
     }
 }
 
-template <int K>
-__global__ __launch_bounds__(kTileThreads, 2) void k_knn_tile(KnnGrid* __restrict__ gp, double r2max,
+// EXL: the halo's exact coordinates are copied to LDS too and the exact phase reads them
+// there (71 KB of LDS: two workgroups per CU), else it reads them from global memory (48 KB:
+// three per CU).
+template <int K, bool EXL>
+__global__ __launch_bounds__(kTileThreads, EXL ? 2 : 3) void k_knn_tile(KnnGrid* __restrict__ gp, double r2max,
                                                            const double* __restrict__ nodes,
                                                            const double* __restrict__ sxyz,
                                                            const int* __restrict__ sidx,
@@ -629,7 +632,7 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_knn_tile(KnnGrid* __restric
                                                            int32_t* __restrict__ nbr, int mode,
                                                            unsigned long long* __restrict__ dbg) {
     __shared__ float4 cand[kTileCap];                      // x, y, z (block-centre relative), id
-    __shared__ double ex[3][kTileCap];                     // the exact coordinates (the exact phase)
+    __shared__ double ex[EXL ? 3 : 1][EXL ? kTileCap : 1];  // the exact coordinates (EXL)
     __shared__ uint16_t qh[kTileCap];                      // the block's queries (LDS positions)
     __shared__ int cst[kTileCells + 1];                    // halo cell -> LDS offset
     __shared__ uint32_t hist[kTileNB / 2][kTileSlots];     // [bin pair][query slot]
@@ -728,9 +731,11 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_knn_tile(KnnGrid* __restric
                     const double x = sxyz[3 * sg], y = sxyz[3 * sg + 1], z = sxyz[3 * sg + 2];
                     cand[acc + q] = make_float4((float)(x - cen[0]), (float)(y - cen[1]), (float)(z - cen[2]),
                                                 __int_as_float(sidx[sg]));
-                    ex[0][acc + q] = x;
-                    ex[1][acc + q] = y;
-                    ex[2][acc + q] = z;
+                    if (EXL) {
+                        ex[0][acc + q] = x;
+                        ex[EXL ? 1 : 0][acc + q] = y;
+                        ex[EXL ? 2 : 0][acc + q] = z;
+                    }
                     if (inner) qh[q0 + q] = (uint16_t)(acc + q);
                 }
                 acc += cnt[u];
@@ -757,7 +762,8 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_knn_tile(KnnGrid* __restric
                 const float4 pf = cand[me];
                 const int self = __float_as_int(pf.w);
                 // exact coordinates and cell (the row offsets; the final distances)
-                const double p[3] = {ex[0][me], ex[1][me], ex[2][me]};
+                const double p[3] = {EXL ? ex[0][me] : nodes[3 * (int64_t)self], EXL ? ex[EXL ? 1 : 0][me] : nodes[3 * (int64_t)self + 1],
+                                     EXL ? ex[EXL ? 2 : 0][me] : nodes[3 * (int64_t)self + 2]};
                 const int c[3] = {knn_cell_axis(p[0], g, 0), knn_cell_axis(p[1], g, 1), knn_cell_axis(p[2], g, 2)};
                 const int h0 = ((c[2] - oz - kTileH) * kTileE + (c[1] - oy - kTileH)) * kTileE + (c[0] - ox - kTileH);
                 __syncthreads();  // cleared counters visible to the query's lanes
@@ -818,9 +824,18 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_knn_tile(KnnGrid* __restric
                         for (int u = 0; u < kLoads; ++u) {
                             const int q = lst[min(i0 + u, nl - 1)][slot];
                             jj[u] = __float_as_int(cand[q].w);
-                            const double ddx = ex[0][q] - p[0], ddy = ex[1][q] - p[1], ddz = ex[2][q] - p[2];
+                            const double qx = EXL ? ex[0][q] : nodes[3 * (int64_t)jj[u]];
+                            const double qy = EXL ? ex[EXL ? 1 : 0][q] : nodes[3 * (int64_t)jj[u] + 1];
+                            const double qz = EXL ? ex[EXL ? 2 : 0][q] : nodes[3 * (int64_t)jj[u] + 2];
+                            const double ddx = qx - p[0], ddy = qy - p[1], ddz = qz - p[2];
                             dd[u] = (ddx * ddx + ddy * ddy) + ddz * ddz;
                         }
+#ifdef EPP_KNN_DIAG
+                        if (mode == 5 || mode == 6) {  // timing ablation (inexact): no inserts
+                            bd[0] = fmin(bd[0], fmin(fmin(dd[0], dd[1]), fmin(dd[2], dd[3])));
+                            continue;
+                        }
+#endif
 #pragma unroll
                         for (int u = 0; u < kLoads; ++u)
                             if (i0 + u < nl) knn_insert<K>(bd, bi, dd[u], jj[u]);
@@ -970,7 +985,15 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
         // persistent: the block count is only known on the device (grid shape)
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const dim3 gt((unsigned)std::max(1, cus * 2)), bt(kTileThreads);  // (LDS: two workgroups per CU)
+        // EPP_KNN_TILE=3: the exact phase from an LDS copy of the coordinates (two
+        // workgroups per CU; else three, and the coordinates from global memory)
+        const int tmode = tile_env && *tile_env ? std::atoi(tile_env) : 1;
+#ifdef EPP_KNN_DIAG
+        const bool exl = tmode == 3 || tmode == 6;  // (6: + the no-insert ablation)
+#else
+        const bool exl = tmode == 3;
+#endif
+        const dim3 gt((unsigned)std::max(1, cus * (exl ? 2 : 3))), bt(kTileThreads);
 #ifdef EPP_KNN_DIAG
         const int mode = tile_env ? std::atoi(tile_env) : 1;  // 4: timing ablation (inexact)
         unsigned long long* d = knn_tl_buffer();
@@ -980,9 +1003,17 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
         unsigned long long* d = nullptr;
 #endif
         int* retry = cell_of;  // free once the scatter has run
-        if (k == 4) hipLaunchKernelGGL(k_knn_tile<4>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr, mode, d);
-        else if (k == 8) hipLaunchKernelGGL(k_knn_tile<8>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr, mode, d);
-        else hipLaunchKernelGGL(k_knn_tile<16>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr, mode, d);
+#define EPP_KNN_TILE_LAUNCH(KK, X) hipLaunchKernelGGL((k_knn_tile<KK, X>), gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr, mode, d)
+        if (exl) {
+            if (k == 4) EPP_KNN_TILE_LAUNCH(4, true);
+            else if (k == 8) EPP_KNN_TILE_LAUNCH(8, true);
+            else EPP_KNN_TILE_LAUNCH(16, true);
+        } else {
+            if (k == 4) EPP_KNN_TILE_LAUNCH(4, false);
+            else if (k == 8) EPP_KNN_TILE_LAUNCH(8, false);
+            else EPP_KNN_TILE_LAUNCH(16, false);
+        }
+#undef EPP_KNN_TILE_LAUNCH
         // one wave per retried query: 8 per CU; waves without a query exit at once
         const dim3 gr((unsigned)std::max(1, cus * 8)), br(64);
         if (k == 4) hipLaunchKernelGGL(k_knn_retry<4>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr);

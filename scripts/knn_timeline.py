@@ -34,29 +34,38 @@ d_n = capi.DeviceBuffer.from_array(nodes)
 d_k = capi.DeviceBuffer(4 * n * k)
 ws = int(L.epp_knn_workspace_size(n))
 d_ws = capi.DeviceBuffer(ws)
-recs = []
-for r in range(12):
-    capi.check(L.epp_knn_grid_ws(d_n.ptr, n, k, 0.0, d_k.ptr, d_ws.ptr, ws, None))
-    capi.sync()
-    if r >= 2:
-        tl = np.zeros((1024, 16), np.uint64)
-        capi.check(L.epp_dbg_knn_tl(tl.ctypes.data, 1024))
-        tl = tl[tl[:, 7] != 0].astype(np.int64)
-        recs.append(tl)
-t = np.concatenate(recs)
-names = ["scan", "copy", "pass1", "pass2", "exact", "rounds", "tail"]
-print(f"blocks per launch {len(recs[0])}, queries per block p50 {np.median(t[:, 8]):.0f} max {t[:, 8].max()}, "
-      f"halo candidates p50 {np.median(t[:, 9]):.0f} max {t[:, 9].max()}")
-for i, nm in enumerate(names):
-    a, b = t[:, i], t[:, i + 1]
-    ok = (a > 0) & (b > 0)
-    v = (b[ok] - a[ok]) * 10 / 1000.0
-    print(f"{nm:7s} p10 {np.percentile(v, 10):7.2f} p50 {np.percentile(v, 50):7.2f} p90 {np.percentile(v, 90):7.2f} "
-          f"max {v.max():7.2f} us")
-tot = (t[:, 7] - t[:, 0]) * 10 / 1000.0
-print(f"block   p10 {np.percentile(tot, 10):7.2f} p50 {np.percentile(tot, 50):7.2f} p90 {np.percentile(tot, 90):7.2f} "
-      f"max {tot.max():7.2f} us")
-for r in recs[:3]:
-    st = (r[:, 0] - r[:, 0].min()) * 10 / 1000.0
-    en = (r[:, 7] - r[:, 0].min()) * 10 / 1000.0
-    print(f"launch: block starts p50 {np.median(st):.2f} max {st.max():.2f} us, ends max {en.max():.2f} us")
+
+
+def report(recs):
+    t = np.concatenate(recs)
+    names = ["scan", "copy", "pass1", "pass2", "exact", "rounds", "tail"]
+    print(f"blocks per launch {len(recs[0])}, queries per block p50 {np.median(t[:, 8]):.0f} max {t[:, 8].max()}, "
+          f"halo candidates p50 {np.median(t[:, 9]):.0f} max {t[:, 9].max()}")
+    for i, nm in enumerate(names):
+        a, b = t[:, i], t[:, i + 1]
+        ok = (a > 0) & (b > 0)
+        v = (b[ok] - a[ok]) * 10 / 1000.0
+        print(f"{nm:7s} p10 {np.percentile(v, 10):7.2f} p50 {np.percentile(v, 50):7.2f} p90 {np.percentile(v, 90):7.2f} "
+              f"max {v.max():7.2f} us")
+    tot = (t[:, 7] - t[:, 0]) * 10 / 1000.0
+    print(f"block   p10 {np.percentile(tot, 10):7.2f} p50 {np.percentile(tot, 50):7.2f} p90 {np.percentile(tot, 90):7.2f} "
+          f"max {tot.max():7.2f} us")
+    for r in recs[:3]:
+        st = (r[:, 0] - r[:, 0].min()) * 10 / 1000.0
+        en = (r[:, 7] - r[:, 0].min()) * 10 / 1000.0
+        print(f"launch: block starts p50 {np.median(st):.2f} max {st.max():.2f} us, ends max {en.max():.2f} us")
+
+
+modes = sys.argv[1:] or ["1"]  # EPP_KNN_TILE values (5, 6: no-insert ablations, diagnostics only)
+for m in modes:
+    os.environ["EPP_KNN_TILE"] = m
+    recs = []
+    for r in range(12):
+        capi.check(L.epp_knn_grid_ws(d_n.ptr, n, k, 0.0, d_k.ptr, d_ws.ptr, ws, None))
+        capi.sync()
+        if r >= 2:
+            tl = np.zeros((1024, 16), np.uint64)
+            capi.check(L.epp_dbg_knn_tl(tl.ctypes.data, 1024))
+            recs.append(tl[tl[:, 7] != 0].astype(np.int64))
+    print(f"== EPP_KNN_TILE={m}")
+    report(recs)
