@@ -308,25 +308,24 @@ __global__ void k_knn_scatter(const double* __restrict__ nodes, int n, const int
 }
 
 // Insert candidate (d, j) into the sorted top-K (distance, then index): ties keep the
-// lower index first, so the visiting order never changes the result.
+// lower index first, so the visiting order never changes the result.  Branch-free: the
+// entries ahead of (d, j) form a prefix of the list; each slot keeps its entry, takes
+// (d, j), or takes its predecessor -- independent selects instead of a shifting chain of
+// per-slot branches (which compiled to ~12 instructions, an exec-mask branch and four
+// 64-bit moves per slot).
 template <int K>
 __device__ __forceinline__ void knn_insert(double (&bd)[K], int (&bi)[K], double d, int j) {
-    if (!(d < bd[K - 1] || (d == bd[K - 1] && j < bi[K - 1]))) return;
-    double vd = d;
-    int vi = j;
-    bool shift = false;
+    if (!((d < bd[K - 1]) | ((d == bd[K - 1]) & (j < bi[K - 1])))) return;
+    bool ahead[K];  // (bitwise, not short-circuit: no branches)
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        shift = shift || vd < bd[k] || (vd == bd[k] && vi < bi[k]);
-        if (shift) {
-            const double td = bd[k];
-            const int ti = bi[k];
-            bd[k] = vd;
-            bi[k] = vi;
-            vd = td;
-            vi = ti;
-        }
+    for (int k = 0; k < K; ++k) ahead[k] = (bd[k] < d) | ((bd[k] == d) & (bi[k] < j));
+#pragma unroll
+    for (int k = K - 1; k >= 1; --k) {  // (reads slot k-1 before it is rewritten)
+        bd[k] = ahead[k] ? bd[k] : (ahead[k - 1] ? d : bd[k - 1]);
+        bi[k] = ahead[k] ? bi[k] : (ahead[k - 1] ? j : bi[k - 1]);
     }
+    bd[0] = ahead[0] ? bd[0] : d;
+    bi[0] = ahead[0] ? bi[0] : j;
 }
 
 // Exact stopping rule after shell r: the K-th best squared distance is below the squared
