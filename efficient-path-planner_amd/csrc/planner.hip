@@ -454,7 +454,6 @@ constexpr int kTileW = 2 * kTileH + 1;  // cube edge around the query's cell
 constexpr int kTileRows = kTileW * kTileW;
 constexpr int kTileCap = 1344;          // candidates a halo may hold (else its queries retry)
 constexpr int kTileThreads = 256;
-constexpr int kTileSlots = kTileThreads / 2;  // query slots (>= 2 lanes per query)
 constexpr int kTileL = 32;              // per-query list length
 constexpr int kTileNB = 16;             // histogram bins (16-bit counters, two per word)
 constexpr double kTileDelta = 1e-3;     // float error allowance, in h^2
@@ -634,9 +633,7 @@ __global__ __launch_bounds__(kTileThreads, EXL ? 2 : 3) void k_knn_tile(KnnGrid*
     __shared__ double ex[EXL ? 3 : 1][EXL ? kTileCap : 1];  // the exact coordinates (EXL)
     __shared__ uint16_t qh[kTileCap];                      // the block's queries (LDS positions)
     __shared__ int cst[kTileCells + 1];                    // halo cell -> LDS offset
-    __shared__ uint32_t hist[kTileNB / 2][kTileSlots];     // [bin pair][query slot]
-    __shared__ uint16_t lst[kTileL][kTileSlots];           // [entry][query slot]
-    __shared__ int nls[kTileSlots];                        // list lengths
+    __shared__ uint16_t lst[kTileL][kTileThreads];         // [entry][lane]: each lane's own list
     __shared__ int wsum[kTileThreads / 64];
     __shared__ int s_nq, s_b;
     const KnnGrid g = *gp;
@@ -749,14 +746,12 @@ __global__ __launch_bounds__(kTileThreads, EXL ? 2 : 3) void k_knn_tile(KnnGrid*
 #endif
             const int lpq = nq <= kTileThreads / 4 ? 4 : 2;  // block-uniform (kTileSlots query slots)
             const int slot = threadIdx.x / lpq, sub = threadIdx.x % lpq;
+            // (a query's lpq lanes are adjacent lanes of one wave: its histogram is combined
+            // by lane shuffles and its list entries are read back by the same wave, so the
+            // query rounds need no workgroup barrier)
             for (int qb = 0; qb < nq; qb += kTileThreads / lpq) {  // block-uniform
                 const int qi = qb + slot;
                 const bool live = qi < nq;
-                if (sub == 0) {
-#pragma unroll
-                    for (int w = 0; w < kTileNB / 2; ++w) hist[w][slot] = 0u;
-                    nls[slot] = 0;
-                }
                 const int me = live ? qh[qi] : 0;
                 const float4 pf = cand[me];
                 const int self = __float_as_int(pf.w);
@@ -765,46 +760,65 @@ __global__ __launch_bounds__(kTileThreads, EXL ? 2 : 3) void k_knn_tile(KnnGrid*
                                      EXL ? ex[EXL ? 2 : 0][me] : nodes[3 * (int64_t)self + 2]};
                 const int c[3] = {knn_cell_axis(p[0], g, 0), knn_cell_axis(p[1], g, 1), knn_cell_axis(p[2], g, 2)};
                 const int h0 = ((c[2] - oz - kTileH) * kTileE + (c[1] - oy - kTileH)) * kTileE + (c[0] - ox - kTileH);
-                __syncthreads();  // cleared counters visible to the query's lanes
-                // pass 1: histogram of bin keys (exponent + two mantissa bits of d / t0)
+                // pass 1: histogram of bin keys (exponent + two mantissa bits of d / t0), in
+                // registers: 16-bit counters, four bins per 64-bit word
+                uint64_t hw[kTileNB / 4] = {0ull, 0ull, 0ull, 0ull};
+                static_assert(kTileNB == 16, "four 64-bit histogram words");
                 if (live)
                     tile_rows(cst, cand, h0, sub, lpq, pf, [&](int, float d, int j, bool valid) {
                         const int kb = max((int)(__float_as_uint(d * inv_t0) >> 21) - (127 << 2), 0);
-                        if (valid && j != self && kb < kTileNB) atomicAdd(&hist[kb >> 1][slot], 1u << ((kb & 1) << 4));
+                        const uint64_t inc = ((valid & (j != self)) & (kb < kTileNB)) ? 1ull << (16 * (kb & 3)) : 0ull;
+#pragma unroll
+                        for (int w = 0; w < kTileNB / 4; ++w) hw[w] += (kb >> 2) == w ? inc : 0ull;
                     });
-                __syncthreads();
+#pragma unroll
+                for (int o = 1; o < 4; o <<= 1)  // the query's lanes (lpq is 2 or 4)
+                    if (o < lpq) {
+#pragma unroll
+                        for (int w = 0; w < kTileNB / 4; ++w) hw[w] += (uint64_t)__shfl_xor((long long)hw[w], o, 64);
+                    }
                 EPP_KTL(3);
                 int cut = -1, run = 0;
 #pragma unroll
-                for (int w = 0; w < kTileNB / 2; ++w) {
-                    const uint32_t hv = hist[w][slot];
-                    run += hv & 0xffff;
-                    if (run >= K && cut < 0) cut = 2 * w;
-                    run += hv >> 16;
-                    if (run >= K && cut < 0) cut = 2 * w + 1;
+                for (int b2 = 0; b2 < kTileNB; ++b2) {
+                    run += (int)((hw[b2 >> 2] >> (16 * (b2 & 3))) & 0xffffull);
+                    cut = (run >= K && cut < 0) ? b2 : cut;
                 }
                 // Dcut: upper edge of bin `cut` (none reached K: no bound)
                 const double dcut = cut < 0 ? INFINITY : (double)__uint_as_float((uint32_t)(cut + 1 + (127 << 2)) << 21) * t0;
                 const float dlist = (float)(dcut + 2.0 * delta);
                 // pass 2: list the candidates below Dcut + 2 delta, visiting only the cells
                 // within Dcut + 3 delta (a candidate's float distance is within delta of
-                // its exact one, which is at least its cell's distance)
+                // its exact one, which is at least its cell's distance); every lane keeps
+                // its own list (its column of lst: no atomics)
+                int nown = 0;
                 if (live) {
                     const double fr[3] = {p[0] - (g.lo[0] + (double)c[0] * g.h), p[1] - (g.lo[1] + (double)c[1] * g.h),
                                           p[2] - (g.lo[2] + (double)c[2] * g.h)};
                     const double thr2 = cut < 0 ? INFINITY : dcut + 3.0 * delta;
                     tile_rows_near(cst, cand, h0, sub, lpq, pf, fr, g.h, thr2, [&](int q, float d, int j, bool valid) {
                         if (valid && j != self && d < dlist) {
-                            const int at = atomicAdd(&nls[slot], 1);
-                            if (at < kTileL) lst[at][slot] = (uint16_t)q;
+                            if (nown < kTileL) lst[nown][threadIdx.x] = (uint16_t)q;
+                            ++nown;
                         }
                     });
                 }
-                __syncthreads();
+                // the other lanes' entry counts (the same wave: its LDS writes are ordered
+                // before the reads below)
+                int ncol[4] = {nown, 0, 0, 0};
+#pragma unroll
+                for (int o = 1; o < 4; ++o) ncol[o] = __shfl((int)nown, (int)(threadIdx.x & 63) + (o < lpq ? o : 0), 64);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 EPP_KTL(4);
                 if (!live || sub != 0) continue;
-                const int nl = nls[slot];
-                bool ok = nl <= kTileL;
+                int nl = 0;
+                bool ok = true;
+#pragma unroll
+                for (int o = 0; o < 4; ++o)
+                    if (o < lpq) {
+                        nl += ncol[o];
+                        ok = ok && ncol[o] <= kTileL;
+                    }
                 if (ok) {
                     double bd[K];
                     int bi[K];
@@ -813,15 +827,24 @@ __global__ __launch_bounds__(kTileThreads, EXL ? 2 : 3) void k_knn_tile(KnnGrid*
                         bd[k] = r2max;
                         bi[k] = 0x7fffffff;
                     }
-                    // exact distances of the listed candidates (exact coordinates from LDS),
-                    // kLoads at a time in flight
+                    // exact distances of the listed candidates (the query's lanes' columns in
+                    // turn), kLoads at a time in flight
                     constexpr int kLoads = 4;
                     for (int i0 = 0; i0 < nl; i0 += kLoads) {
                         double dd[kLoads];
                         int jj[kLoads];
 #pragma unroll
                         for (int u = 0; u < kLoads; ++u) {
-                            const int q = lst[min(i0 + u, nl - 1)][slot];
+                            int e = min(i0 + u, nl - 1), col = 0;  // entry e -> (lane column, row)
+                            bool go = true;
+#pragma unroll
+                            for (int o = 0; o < 3; ++o) {
+                                const bool past = (go & (o + 1 < lpq)) & (e >= ncol[o]);
+                                e -= past ? ncol[o] : 0;
+                                col += past ? 1 : 0;
+                                go = past;
+                            }
+                            const int q = lst[e][threadIdx.x + col];
                             jj[u] = __float_as_int(cand[q].w);
                             const double qx = EXL ? ex[0][q] : nodes[3 * (int64_t)jj[u]];
                             const double qy = EXL ? ex[EXL ? 1 : 0][q] : nodes[3 * (int64_t)jj[u] + 1];
