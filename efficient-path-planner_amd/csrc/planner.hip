@@ -457,6 +457,7 @@ constexpr int kTileThreads = 256;
 constexpr int kTileL = 32;              // per-query list length
 constexpr int kTileNB = 16;             // histogram bins (16-bit counters, two per word)
 constexpr double kTileDelta = 1e-3;     // float error allowance, in h^2
+constexpr double kPass1R2 = 4.5;        // pass 1 first visits the cells within sqrt(4.5) h
 
 // Visits the candidates of cube rows row0, row0 + rstep, ... around a query (a row =
 // kTileW consecutive halo cells along x, one contiguous LDS range), four candidates at a
@@ -633,6 +634,7 @@ __global__ __launch_bounds__(kTileThreads, EXL ? 2 : 3) void k_knn_tile(KnnGrid*
     __shared__ double ex[EXL ? 3 : 1][EXL ? kTileCap : 1];  // the exact coordinates (EXL)
     __shared__ uint16_t qh[kTileCap];                      // the block's queries (LDS positions)
     __shared__ int cst[kTileCells + 1];                    // halo cell -> LDS offset
+    __shared__ uint32_t hist[kTileNB / 2][kTileThreads / 2];  // [bin pair][query slot]
     __shared__ uint16_t lst[kTileL][kTileThreads];         // [entry][lane]: each lane's own list
     __shared__ int wsum[kTileThreads / 64];
     __shared__ int s_nq, s_b;
@@ -760,30 +762,45 @@ __global__ __launch_bounds__(kTileThreads, EXL ? 2 : 3) void k_knn_tile(KnnGrid*
                                      EXL ? ex[EXL ? 2 : 0][me] : nodes[3 * (int64_t)self + 2]};
                 const int c[3] = {knn_cell_axis(p[0], g, 0), knn_cell_axis(p[1], g, 1), knn_cell_axis(p[2], g, 2)};
                 const int h0 = ((c[2] - oz - kTileH) * kTileE + (c[1] - oy - kTileH)) * kTileE + (c[0] - ox - kTileH);
-                // pass 1: histogram of bin keys (exponent + two mantissa bits of d / t0), in
-                // registers: 16-bit counters, four bins per 64-bit word
-                uint64_t hw[kTileNB / 4] = {0ull, 0ull, 0ull, 0ull};
-                static_assert(kTileNB == 16, "four 64-bit histogram words");
-                if (live)
-                    tile_rows(cst, cand, h0, sub, lpq, pf, [&](int, float d, int j, bool valid) {
-                        const int kb = max((int)(__float_as_uint(d * inv_t0) >> 21) - (127 << 2), 0);
-                        const uint64_t inc = ((valid & (j != self)) & (kb < kTileNB)) ? 1ull << (16 * (kb & 3)) : 0ull;
+                const double fr[3] = {p[0] - (g.lo[0] + (double)c[0] * g.h), p[1] - (g.lo[1] + (double)c[1] * g.h),
+                                      p[2] - (g.lo[2] + (double)c[2] * g.h)};
+                // pass 1: histogram of bin keys (exponent + two mantissa bits of d / t0): the
+                // query's slot of `hist`, LDS atomics from its lanes (one wave: in-order LDS
+                // operations order the clear before them and the read after).  First over
+                // the cells within sqrt(kPass1R2) h only (about half the cube); its counts
+                // are complete for every bin ending below kPass1R2 h^2 - delta (a candidate
+                // of a skipped cell has exact d > kPass1R2 h^2, float d > that - delta), so
+                // its cut stands when it ends there -- nearly always; else the whole cube.
+                int cut = -1;
+                for (int full = 0; full < 2; ++full) {  // query-uniform (the slot's lanes read one histogram)
+                    if (sub == 0) {
 #pragma unroll
-                        for (int w = 0; w < kTileNB / 4; ++w) hw[w] += (kb >> 2) == w ? inc : 0ull;
-                    });
-#pragma unroll
-                for (int o = 1; o < 4; o <<= 1)  // the query's lanes (lpq is 2 or 4)
-                    if (o < lpq) {
-#pragma unroll
-                        for (int w = 0; w < kTileNB / 4; ++w) hw[w] += (uint64_t)__shfl_xor((long long)hw[w], o, 64);
+                        for (int w = 0; w < kTileNB / 2; ++w) hist[w][slot] = 0u;
                     }
-                EPP_KTL(3);
-                int cut = -1, run = 0;
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    auto bin = [&](int, float d, int j, bool valid) {
+                        const int kb = max((int)(__float_as_uint(d * inv_t0) >> 21) - (127 << 2), 0);
+                        if (valid && j != self && kb < kTileNB) atomicAdd(&hist[kb >> 1][slot], 1u << ((kb & 1) << 4));
+                    };
+                    if (live) {
+                        if (full) tile_rows(cst, cand, h0, sub, lpq, pf, bin);
+                        else tile_rows_near(cst, cand, h0, sub, lpq, pf, fr, g.h, kPass1R2 * g.h * g.h, bin);
+                    }
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    int run = 0;
+                    cut = -1;
 #pragma unroll
-                for (int b2 = 0; b2 < kTileNB; ++b2) {
-                    run += (int)((hw[b2 >> 2] >> (16 * (b2 & 3))) & 0xffffull);
-                    cut = (run >= K && cut < 0) ? b2 : cut;
+                    for (int w = 0; w < kTileNB / 2; ++w) {
+                        const uint32_t hv = hist[w][slot];
+                        run += hv & 0xffff;
+                        if (run >= K && cut < 0) cut = 2 * w;
+                        run += hv >> 16;
+                        if (run >= K && cut < 0) cut = 2 * w + 1;
+                    }
+                    const double edge = cut < 0 ? INFINITY : (double)__uint_as_float((uint32_t)(cut + 1 + (127 << 2)) << 21) * t0;
+                    if (full || edge <= kPass1R2 * g.h * g.h - delta) break;
                 }
+                EPP_KTL(3);
                 // Dcut: upper edge of bin `cut` (none reached K: no bound)
                 const double dcut = cut < 0 ? INFINITY : (double)__uint_as_float((uint32_t)(cut + 1 + (127 << 2)) << 21) * t0;
                 const float dlist = (float)(dcut + 2.0 * delta);
@@ -793,8 +810,6 @@ __global__ __launch_bounds__(kTileThreads, EXL ? 2 : 3) void k_knn_tile(KnnGrid*
                 // its own list (its column of lst: no atomics)
                 int nown = 0;
                 if (live) {
-                    const double fr[3] = {p[0] - (g.lo[0] + (double)c[0] * g.h), p[1] - (g.lo[1] + (double)c[1] * g.h),
-                                          p[2] - (g.lo[2] + (double)c[2] * g.h)};
                     const double thr2 = cut < 0 ? INFINITY : dcut + 3.0 * delta;
                     tile_rows_near(cst, cand, h0, sub, lpq, pf, fr, g.h, thr2, [&](int q, float d, int j, bool valid) {
                         if (valid && j != self && d < dlist) {

@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "libepp.so")
+# EPP_LIB: another build of the same ABI (diagnostics A/B builds under scripts/dbg/)
+LIB_PATH = os.environ.get("EPP_LIB") or os.path.join(os.path.dirname(_HERE), "libepp.so")
 
 OBB_DTYPE = np.dtype([("center", "<f8", 3), ("half", "<f8", 3), ("rot", "<f8", 9),
                       ("filling", "<i4"), ("is_gate", "<i4")])
