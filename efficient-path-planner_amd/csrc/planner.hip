@@ -634,7 +634,7 @@ __global__ __launch_bounds__(kTileThreads, EXL ? 2 : 3) void k_knn_tile(KnnGrid*
     __shared__ double ex[EXL ? 3 : 1][EXL ? kTileCap : 1];  // the exact coordinates (EXL)
     __shared__ uint16_t qh[kTileCap];                      // the block's queries (LDS positions)
     __shared__ int cst[kTileCells + 1];                    // halo cell -> LDS offset
-    __shared__ uint32_t hist[kTileNB / 2][kTileThreads / 2];  // [bin pair][query slot]
+    __shared__ uint32_t hist[kTileNB / 2][kTileThreads];  // [bin pair][query slot]
     __shared__ uint16_t lst[kTileL][kTileThreads];         // [entry][lane]: each lane's own list
     __shared__ int wsum[kTileThreads / 64];
     __shared__ int s_nq, s_b;
@@ -746,7 +746,9 @@ __global__ __launch_bounds__(kTileThreads, EXL ? 2 : 3) void k_knn_tile(KnnGrid*
 #else
             const int nq = s_nq;
 #endif
-            const int lpq = nq <= kTileThreads / 4 ? 4 : 2;  // block-uniform (kTileSlots query slots)
+            // block-uniform; one lane per query only above 128 queries (a second round of
+            // queries would cost the block ~45 us: the kernel's slowest blocks)
+            const int lpq = nq <= kTileThreads / 4 ? 4 : nq <= kTileThreads / 2 ? 2 : 1;
             const int slot = threadIdx.x / lpq, sub = threadIdx.x % lpq;
             // (a query's lpq lanes are adjacent lanes of one wave: its histogram is combined
             // by lane shuffles and its list entries are read back by the same wave, so the
