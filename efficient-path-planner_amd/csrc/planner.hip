@@ -535,7 +535,7 @@ __device__ __forceinline__ void knn_store(int32_t* __restrict__ nbr, int self, c
 template <int K>
 __device__ __forceinline__ void knn_retry_wave(const KnnGrid& g, double r2max, const double* __restrict__ nodes,
                                const double* __restrict__ sxyz, const int* __restrict__ sidx,
-                               const int* __restrict__ start, int self, int32_t* __restrict__ nbr) {
+                               const int* __restrict__ start, int self, double bound2, int32_t* __restrict__ nbr) {
     const int lane = threadIdx.x & 63;
     const int rmax = max(g.dims[0], max(g.dims[1], g.dims[2]));
     const double p[3] = {nodes[3 * (int64_t)self], nodes[3 * (int64_t)self + 1], nodes[3 * (int64_t)self + 2]};
@@ -566,6 +566,21 @@ __device__ __forceinline__ void knn_retry_wave(const KnnGrid& g, double r2max, c
                 if (jj[u] != self) knn_insert<K>(bd, bi, dd[u], jj[u]);
         }
     };
+    if (bound2 < 1e299) {  // wave-uniform
+        // K actual candidates lie within sqrt(bound2) (the tile pass found them), so every
+        // candidate of the true top K does too: one pass over the cells of the box
+        // p +- sqrt(bound2) (the cell mapping is monotone; the radius is padded against
+        // the rounding of p +- r), rows spread over the lanes, no stopping rule
+        const double r = sqrt(bound2) * (1.0 + 1e-9) + 1e-12 * (1.0 + fabs(p[0]) + fabs(p[1]) + fabs(p[2]));
+        int lo[3], hi[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            lo[d] = knn_cell_axis(p[d] - r, g, d);
+            hi[d] = knn_cell_axis(p[d] + r, g, d);
+        }
+        const int ny = hi[1] - lo[1] + 1, nz = hi[2] - lo[2] + 1;
+        for (int row = lane; row < ny * nz; row += 64) scan(lo[1] + row % ny, lo[2] + row / ny, lo[0], hi[0]);
+    } else {
     for (int R = kTileH + 1;; ++R) {  // wave-uniform
         // rows of shell R (the whole cube the first time)
         const bool cube = R == kTileH + 1;
@@ -591,6 +606,7 @@ __device__ __forceinline__ void knn_retry_wave(const KnnGrid& g, double r2max, c
             if (below < K) continue;
         }
         break;
+    }
     }
     // merge: K rounds of arg-min over the lane list heads
 #pragma unroll
@@ -618,20 +634,18 @@ __device__ __forceinline__ void knn_retry_wave(const KnnGrid& g, double r2max, c
     }
 }
 
-// EXL: the halo's exact coordinates are copied to LDS too and the exact phase reads them
-// there (71 KB of LDS: two workgroups per CU), else it reads them from global memory (48 KB:
-// three per CU).
-template <int K, bool EXL>
-__global__ __launch_bounds__(kTileThreads, EXL ? 2 : 3) void k_knn_tile(KnnGrid* __restrict__ gp, double r2max,
+// (An LDS copy of the halo's exact coordinates for the exact phase was tried: with it two
+// workgroups fit per CU instead of three, and the kernel was slower.)
+template <int K>
+__global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restrict__ gp, double r2max,
                                                            const double* __restrict__ nodes,
                                                            const double* __restrict__ sxyz,
                                                            const int* __restrict__ sidx,
                                                            const int* __restrict__ start,
-                                                           int* __restrict__ retry,
+                                                           int* __restrict__ retry, double* __restrict__ retry_b,
                                                            int32_t* __restrict__ nbr, int mode,
                                                            unsigned long long* __restrict__ dbg) {
     __shared__ float4 cand[kTileCap];                      // x, y, z (block-centre relative), id
-    __shared__ double ex[EXL ? 3 : 1][EXL ? kTileCap : 1];  // the exact coordinates (EXL)
     __shared__ uint16_t qh[kTileCap];                      // the block's queries (LDS positions)
     __shared__ int cst[kTileCells + 1];                    // halo cell -> LDS offset
     __shared__ uint32_t hist[kTileNB / 2][kTileThreads];  // [bin pair][query slot]
@@ -729,11 +743,6 @@ __global__ __launch_bounds__(kTileThreads, EXL ? 2 : 3) void k_knn_tile(KnnGrid*
                     const double x = sxyz[3 * sg], y = sxyz[3 * sg + 1], z = sxyz[3 * sg + 2];
                     cand[acc + q] = make_float4((float)(x - cen[0]), (float)(y - cen[1]), (float)(z - cen[2]),
                                                 __int_as_float(sidx[sg]));
-                    if (EXL) {
-                        ex[0][acc + q] = x;
-                        ex[EXL ? 1 : 0][acc + q] = y;
-                        ex[EXL ? 2 : 0][acc + q] = z;
-                    }
                     if (inner) qh[q0 + q] = (uint16_t)(acc + q);
                 }
                 acc += cnt[u];
@@ -760,8 +769,7 @@ __global__ __launch_bounds__(kTileThreads, EXL ? 2 : 3) void k_knn_tile(KnnGrid*
                 const float4 pf = cand[me];
                 const int self = __float_as_int(pf.w);
                 // exact coordinates and cell (the row offsets; the final distances)
-                const double p[3] = {EXL ? ex[0][me] : nodes[3 * (int64_t)self], EXL ? ex[EXL ? 1 : 0][me] : nodes[3 * (int64_t)self + 1],
-                                     EXL ? ex[EXL ? 2 : 0][me] : nodes[3 * (int64_t)self + 2]};
+                const double p[3] = {nodes[3 * (int64_t)self], nodes[3 * (int64_t)self + 1], nodes[3 * (int64_t)self + 2]};
                 const int c[3] = {knn_cell_axis(p[0], g, 0), knn_cell_axis(p[1], g, 1), knn_cell_axis(p[2], g, 2)};
                 const int h0 = ((c[2] - oz - kTileH) * kTileE + (c[1] - oy - kTileH)) * kTileE + (c[0] - ox - kTileH);
                 const double fr[3] = {p[0] - (g.lo[0] + (double)c[0] * g.h), p[1] - (g.lo[1] + (double)c[1] * g.h),
@@ -830,6 +838,7 @@ __global__ __launch_bounds__(kTileThreads, EXL ? 2 : 3) void k_knn_tile(KnnGrid*
                 if (!live || sub != 0) continue;
                 int nl = 0;
                 bool ok = true;
+                double rbound = INFINITY;  // (none: the retry walks shells)
 #pragma unroll
                 for (int o = 0; o < 4; ++o)
                     if (o < lpq) {
@@ -863,10 +872,8 @@ __global__ __launch_bounds__(kTileThreads, EXL ? 2 : 3) void k_knn_tile(KnnGrid*
                             }
                             const int q = lst[e][threadIdx.x + col];
                             jj[u] = __float_as_int(cand[q].w);
-                            const double qx = EXL ? ex[0][q] : nodes[3 * (int64_t)jj[u]];
-                            const double qy = EXL ? ex[EXL ? 1 : 0][q] : nodes[3 * (int64_t)jj[u] + 1];
-                            const double qz = EXL ? ex[EXL ? 2 : 0][q] : nodes[3 * (int64_t)jj[u] + 2];
-                            const double ddx = qx - p[0], ddy = qy - p[1], ddz = qz - p[2];
+                            const double ddx = nodes[3 * (int64_t)jj[u]] - p[0], ddy = nodes[3 * (int64_t)jj[u] + 1] - p[1],
+                                         ddz = nodes[3 * (int64_t)jj[u] + 2] - p[2];
                             dd[u] = (ddx * ddx + ddy * ddy) + ddz * ddz;
                         }
 #ifdef EPP_KNN_DIAG
@@ -885,10 +892,16 @@ __global__ __launch_bounds__(kTileThreads, EXL ? 2 : 3) void k_knn_tile(KnnGrid*
                     ok = in_range && knn_done<K>(g, c, p, kTileH, bd);
                     if (ok) knn_store<K>(nbr, self, bi);
                     else atomicAdd(&gp->why[in_range ? 2 : 1], 1);
+                    // a retry's search bound: K actual candidates within bd[K-1] (<= r2max)
+                    rbound = bd[K - 1];
                 } else {
                     atomicAdd(&gp->why[0], 1);
                 }
-                if (!ok) retry[atomicAdd(&gp->nretry, 1)] = self;
+                if (!ok) {
+                    const int at = atomicAdd(&gp->nretry, 1);
+                    retry[at] = self;
+                    retry_b[at] = rbound;
+                }
 #ifdef EPP_KNN_DIAG
                 if (tl[5] == 0ull) tl[5] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -902,7 +915,11 @@ __global__ __launch_bounds__(kTileThreads, EXL ? 2 : 3) void k_knn_tile(KnnGrid*
                 if (x >= g.dims[0] || y >= g.dims[1] || z >= g.dims[2]) continue;
                 const int cell = (z * g.dims[1] + y) * g.dims[0] + x;
                 const int e = start[cell + 1];
-                for (int t = start[cell]; t < e; ++t) retry[atomicAdd(&gp->nretry, 1)] = sidx[t];
+                for (int t = start[cell]; t < e; ++t) {
+                    const int at = atomicAdd(&gp->nretry, 1);
+                    retry[at] = sidx[t];
+                    retry_b[at] = INFINITY;
+                }
                 if (e > start[cell]) atomicAdd(&gp->why[3], e - start[cell]);
             }
         }
@@ -930,11 +947,12 @@ __global__ __launch_bounds__(64) void k_knn_retry(const KnnGrid* __restrict__ gp
                                                    const int* __restrict__ sidx,
                                                    const int* __restrict__ start,
                                                    const int* __restrict__ retry,
+                                                   const double* __restrict__ retry_b,
                                                    int32_t* __restrict__ nbr) {
     const KnnGrid g = *gp;
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwaves = (gridDim.x * blockDim.x) >> 6;
     for (int i = wave; i < g.nretry; i += nwaves)  // wave-uniform
-        knn_retry_wave<K>(g, r2max, nodes, sxyz, sidx, start, retry[i], nbr);
+        knn_retry_wave<K>(g, r2max, nodes, sxyz, sidx, start, retry[i], retry_b[i], nbr);
 }
 
 __global__ void k_knn_edges(const double* __restrict__ nodes, const int32_t* __restrict__ nbr, int64_t m,
@@ -952,9 +970,9 @@ __global__ void k_knn_edges(const double* __restrict__ nodes, const int32_t* __r
 }
 
 // Scratch of the grid k-NN, every part 256-byte aligned: grid params | bounds partials | cell_of[n] |
-// sidx[n] | sxyz[3n] | cnt[cap+1] | fill[cap+1] | start[cap+1]   (cap = max(64, n))
+// sidx[n] | sxyz[3n] | cnt[cap+1] | fill[cap+1] | start[cap+1] | retry bounds[n]  (cap = max(64, n))
 struct KnnLayout {
-    size_t part, cell, sidx, sxyz, cnt, start, fill, bytes;
+    size_t part, cell, sidx, sxyz, cnt, start, fill, rbnd, bytes;
     int cap;
 };
 KnnLayout knn_layout(int n) {
@@ -968,7 +986,8 @@ KnnLayout knn_layout(int n) {
     L.cnt = L.sxyz + al((size_t)n * 24);
     L.fill = L.cnt + al((size_t)(L.cap + 1) * 4);
     L.start = L.fill + al((size_t)(L.cap + 1) * 4);
-    L.bytes = L.start + al((size_t)(L.cap + 1) * 4);
+    L.rbnd = L.start + al((size_t)(L.cap + 1) * 4);
+    L.bytes = L.rbnd + al((size_t)std::max(n, 1) * 8);
     return L;
 }
 
@@ -1024,15 +1043,7 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
         // persistent: the block count is only known on the device (grid shape)
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        // EPP_KNN_TILE=3: the exact phase from an LDS copy of the coordinates (two
-        // workgroups per CU; else three, and the coordinates from global memory)
-        const int tmode = tile_env && *tile_env ? std::atoi(tile_env) : 1;
-#ifdef EPP_KNN_DIAG
-        const bool exl = tmode == 3 || tmode == 6;  // (6: + the no-insert ablation)
-#else
-        const bool exl = tmode == 3;
-#endif
-        const dim3 gt((unsigned)std::max(1, cus * (exl ? 2 : 3))), bt(kTileThreads);
+        const dim3 gt((unsigned)std::max(1, cus * 3)), bt(kTileThreads);  // (LDS: three workgroups per CU)
 #ifdef EPP_KNN_DIAG
         const int mode = tile_env ? std::atoi(tile_env) : 1;  // 4: timing ablation (inexact)
         unsigned long long* d = knn_tl_buffer();
@@ -1042,22 +1053,15 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
         unsigned long long* d = nullptr;
 #endif
         int* retry = cell_of;  // free once the scatter has run
-#define EPP_KNN_TILE_LAUNCH(KK, X) hipLaunchKernelGGL((k_knn_tile<KK, X>), gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr, mode, d)
-        if (exl) {
-            if (k == 4) EPP_KNN_TILE_LAUNCH(4, true);
-            else if (k == 8) EPP_KNN_TILE_LAUNCH(8, true);
-            else EPP_KNN_TILE_LAUNCH(16, true);
-        } else {
-            if (k == 4) EPP_KNN_TILE_LAUNCH(4, false);
-            else if (k == 8) EPP_KNN_TILE_LAUNCH(8, false);
-            else EPP_KNN_TILE_LAUNCH(16, false);
-        }
-#undef EPP_KNN_TILE_LAUNCH
+        double* retry_b = reinterpret_cast<double*>(buf + L.rbnd);
+        if (k == 4) hipLaunchKernelGGL(k_knn_tile<4>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr, mode, d);
+        else if (k == 8) hipLaunchKernelGGL(k_knn_tile<8>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr, mode, d);
+        else hipLaunchKernelGGL(k_knn_tile<16>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr, mode, d);
         // one wave per retried query: 8 per CU; waves without a query exit at once
         const dim3 gr((unsigned)std::max(1, cus * 8)), br(64);
-        if (k == 4) hipLaunchKernelGGL(k_knn_retry<4>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr);
-        else if (k == 8) hipLaunchKernelGGL(k_knn_retry<8>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr);
-        else hipLaunchKernelGGL(k_knn_retry<16>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, nbr);
+        if (k == 4) hipLaunchKernelGGL(k_knn_retry<4>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr);
+        else if (k == 8) hipLaunchKernelGGL(k_knn_retry<8>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr);
+        else hipLaunchKernelGGL(k_knn_retry<16>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr);
     } else {
         switch (k) {
             case 4: hipLaunchKernelGGL(k_knn_grid<4>, g256, b256, 0, s, g, n, r2, sxyz, sidx, start, nbr); break;
