@@ -152,7 +152,12 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     const int32_t n = (int32_t)(n_valid_states + 2);
     // ---- 2. k-NN graph + batched motion checks (MotionValidator::checkMotion) --------
     const size_t m = (size_t)n * k;
-    check(epp_knn_ws(d_nodes, n, k, 0.0, d_nbr, d_ws, ws_bytes, st), "knn");
+    // the grid over the sampling box widened by start and goal (every node lies inside)
+    const double blo[3] = {std::min({lo[0], start.x, goal.x}), std::min({lo[1], start.y, goal.y}),
+                           std::min({lo[2], start.z, goal.z})};
+    const double bhi[3] = {std::max({hi[0], start.x, goal.x}), std::max({hi[1], start.y, goal.y}),
+                           std::max({hi[2], start.z, goal.z})};
+    check(epp_knn_ws_box(d_nodes, n, k, 0.0, blo, bhi, d_nbr, d_ws, ws_bytes, st), "knn");
     // motion checks straight off the k-NN table; small batches / worlds without tile tables
     // through materialised endpoints
     const epp_status ks = epp_check_knn_motions(w, d_nodes, d_nbr, n, k, canPass ? 1 : 0, 0, d_ev, st);

@@ -121,9 +121,49 @@ constexpr int kBoundsThreads = 1024;
 constexpr int kBoundsBlocks = 64;
 constexpr double kNodesPerCell = 1.5;  // mean nodes per grid cell (EPP_KNN_NPC overrides; tuned for k_knn_tile: ~90 queries per 4^3 block -> 2 lanes each)
 
-// Per-block min/max of the node coordinates: part[6 * block] = (min xyz, max xyz).
+// The grid over the box [mn, mx] for n nodes: cells of edge h with ~npc nodes each (flat
+// point sets: thin slabs), at most cap cells.  Host (caller-given box) and device (the
+// nodes' bounding box) compute it the same way.
+__host__ __device__ inline void knn_grid_shape(const double (&mn)[3], const double (&mx)[3], int n, int cap,
+                                               double npc, KnnGrid* g) {
+    double ext[3], vol = 1.0, emax = 0.0;
+    for (int d = 0; d < 3; ++d) {
+        ext[d] = mx[d] - mn[d];
+        emax = fmax(emax, ext[d]);
+    }
+    const double floor_ext = fmax(emax, 1e-9) * 1e-3;
+    for (int d = 0; d < 3; ++d) vol *= fmax(ext[d], floor_ext);
+    double h = cbrt(npc * vol / (double)(n > 1 ? n : 1));
+    h = fmax(h, 1e-12);
+    int dims[3];
+    long long cells;
+    for (;;) {
+        cells = 1;
+        for (int d = 0; d < 3; ++d) {
+            dims[d] = (int)fmin(ext[d] / h, 1023.0) + 1;
+            cells *= dims[d];
+        }
+        if (cells <= cap) break;
+        h *= 1.25;
+    }
+    for (int d = 0; d < 3; ++d) {
+        g->lo[d] = mn[d];
+        g->dims[d] = dims[d];
+    }
+    g->h = h;
+    g->inv_h = 1.0 / h;
+    g->ncell = (int)cells;
+    g->next = 0;
+    g->nretry = 0;
+    for (int i = 0; i < 4; ++i) g->why[i] = 0;
+}
+
+// Per-block min/max of the node coordinates: part[6 * block] = (min xyz, max xyz).  Also
+// clears the cell counters (cnt and fill, nclr ints) for k_knn_count / k_knn_scatter.
 __global__ __launch_bounds__(kBoundsThreads) void k_knn_bounds_part(const double* __restrict__ nodes, int n,
-                                                                    double* __restrict__ part) {
+                                                                    double* __restrict__ part, int* __restrict__ clr,
+                                                                    int nclr) {
+    for (int i = blockIdx.x * kBoundsThreads + threadIdx.x; i < nclr; i += gridDim.x * kBoundsThreads) clr[i] = 0;
     __shared__ double smin[3][kBoundsThreads / 64], smax[3][kBoundsThreads / 64];
     double mn[3] = {1e308, 1e308, 1e308}, mx[3] = {-1e308, -1e308, -1e308};
     for (int i = blockIdx.x * kBoundsThreads + threadIdx.x; i < n; i += gridDim.x * kBoundsThreads)
@@ -174,36 +214,14 @@ __global__ void k_knn_setup(const double* __restrict__ part, int nparts, int n, 
             mx[d] = fmax(mx[d], __shfl_xor(mx[d], o, 64));
         }
     if (threadIdx.x != 0) return;
-    double ext[3], vol = 1.0, emax = 0.0;
-    for (int d = 0; d < 3; ++d) {
-        ext[d] = mx[d] - mn[d];
-        emax = fmax(emax, ext[d]);
-    }
-    const double floor_ext = fmax(emax, 1e-9) * 1e-3;  // flat point sets: thin slabs
-    for (int d = 0; d < 3; ++d) vol *= fmax(ext[d], floor_ext);
-    double h = cbrt(npc * vol / (double)max(n, 1));
-    h = fmax(h, 1e-12);
-    int dims[3];
-    long long cells;
-    for (;;) {
-        cells = 1;
-        for (int d = 0; d < 3; ++d) {
-            dims[d] = (int)fmin(ext[d] / h, 1023.0) + 1;
-            cells *= dims[d];
-        }
-        if (cells <= cell_cap) break;
-        h *= 1.25;
-    }
-    for (int d = 0; d < 3; ++d) {
-        g->lo[d] = mn[d];
-        g->dims[d] = dims[d];
-    }
-    g->h = h;
-    g->inv_h = 1.0 / h;
-    g->ncell = (int)cells;
-    g->next = 0;
-    g->nretry = 0;
-    for (int i = 0; i < 4; ++i) g->why[i] = 0;
+    knn_grid_shape(mn, mx, n, cell_cap, npc, g);
+}
+
+// The caller-box path: the grid computed on the host, written here; clears the counters.
+__global__ __launch_bounds__(kBoundsThreads) void k_knn_prep(KnnGrid gv, KnnGrid* __restrict__ g,
+                                                             int* __restrict__ clr, int nclr) {
+    for (int i = blockIdx.x * kBoundsThreads + threadIdx.x; i < nclr; i += gridDim.x * kBoundsThreads) clr[i] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *g = gv;
 }
 
 __device__ __forceinline__ int knn_cell_axis(double v, const KnnGrid& g, int d) {
@@ -1006,7 +1024,8 @@ unsigned long long* knn_tl_buffer() {
 #endif
 
 epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, int32_t* nbr, char* buf,
-                           const KnnLayout& L, hipStream_t s) {
+                           const KnnLayout& L, hipStream_t s, const double* box_lo = nullptr,
+                           const double* box_hi = nullptr) {
     KnnGrid* g = reinterpret_cast<KnnGrid*>(buf);
     int* cell_of = reinterpret_cast<int*>(buf + L.cell);
     int* sidx = reinterpret_cast<int*>(buf + L.sidx);
@@ -1014,20 +1033,24 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
     int* cnt = reinterpret_cast<int*>(buf + L.cnt);
     int* start = reinterpret_cast<int*>(buf + L.start);
     int* fill = reinterpret_cast<int*>(buf + L.fill);
-    // cnt and fill are adjacent: one clear (never launch the scatter on stale counters)
-    const hipError_t e = hipMemsetAsync(cnt, 0, L.start - L.cnt, s);
-    if (e != hipSuccess) {
-        set_error(std::string("epp_knn_grid: hipMemsetAsync: ") + hipGetErrorString(e));
-        return EPP_ERR_HIP;
-    }
     const double r2 = max_dist > 0 ? max_dist * max_dist : 1e300;
     const dim3 g256((n + 255) / 256), b256(256);
     const int nb = std::max(1, std::min(kBoundsBlocks, (n + kBoundsThreads - 1) / kBoundsThreads));
-    double* part = reinterpret_cast<double*>(buf + L.part);
-    hipLaunchKernelGGL(k_knn_bounds_part, dim3(nb), dim3(kBoundsThreads), 0, s, nodes, n, part);
     const char* npc_env = std::getenv("EPP_KNN_NPC");
     const double npc = npc_env && *npc_env ? std::max(0.5, std::atof(npc_env)) : kNodesPerCell;
-    hipLaunchKernelGGL(k_knn_setup, dim3(1), dim3(64), 0, s, part, nb, n, L.cap, npc, g);
+    // cnt and fill are adjacent: cleared together by the first kernel (never run the
+    // scatter on stale counters)
+    const int nclr = (int)((L.start - L.cnt) / sizeof(int));
+    if (box_lo && box_hi) {  // the caller's box: the grid shape on the host, one kernel
+        KnnGrid gv{};
+        const double mn[3] = {box_lo[0], box_lo[1], box_lo[2]}, mx[3] = {box_hi[0], box_hi[1], box_hi[2]};
+        knn_grid_shape(mn, mx, n, L.cap, npc, &gv);
+        hipLaunchKernelGGL(k_knn_prep, dim3(nb), dim3(kBoundsThreads), 0, s, gv, g, cnt, nclr);
+    } else {
+        double* part = reinterpret_cast<double*>(buf + L.part);
+        hipLaunchKernelGGL(k_knn_bounds_part, dim3(nb), dim3(kBoundsThreads), 0, s, nodes, n, part, cnt, nclr);
+        hipLaunchKernelGGL(k_knn_setup, dim3(1), dim3(64), 0, s, part, nb, n, L.cap, npc, g);
+    }
     hipLaunchKernelGGL(k_knn_count, g256, b256, 0, s, nodes, n, g, cell_of, cnt);
     hipLaunchKernelGGL(k_knn_scan, dim3(1), dim3(kBoundsThreads), 0, s, g, cnt, start);
     hipLaunchKernelGGL(k_knn_scatter, g256, b256, 0, s, nodes, n, cell_of, start, fill, sxyz, sidx);
@@ -1257,6 +1280,28 @@ epp_status epp_dbg_knn_tl(unsigned long long* out, int64_t blocks) {
 epp_status epp_knn_ws(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr, void* ws,
                       uint64_t ws_bytes, void* stream) {
     if (n > 2048) return epp_knn_grid_ws(nodes, n, k, max_dist, nbr, ws, ws_bytes, stream);
+    return epp_knn_bruteforce(nodes, n, k, max_dist, nbr, stream);
+}
+
+epp_status epp_knn_grid_ws_box(const double* nodes, int32_t n, int32_t k, double max_dist, const double lo[3],
+                               const double hi[3], int32_t* nbr, void* ws, uint64_t ws_bytes, void* stream) {
+    if (n < 0 || (n > 0 && (!nodes || !nbr)) || (k != 4 && k != 8 && k != 16 && k != 32) || !lo || !hi ||
+        !(lo[0] <= hi[0] && lo[1] <= hi[1] && lo[2] <= hi[2])) {
+        set_error("epp_knn_grid_ws_box: invalid argument (k must be 4, 8, 16 or 32; lo <= hi)");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    if (n == 0) return EPP_OK;
+    const KnnLayout L = knn_layout(n);
+    if (!ws || ws_bytes < L.bytes || (reinterpret_cast<uintptr_t>(ws) & 255)) {
+        set_error("epp_knn_grid_ws_box: workspace missing, unaligned or smaller than epp_knn_workspace_size(n)");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    return knn_grid_launch(nodes, n, k, max_dist, nbr, static_cast<char*>(ws), L, (hipStream_t)stream, lo, hi);
+}
+
+epp_status epp_knn_ws_box(const double* nodes, int32_t n, int32_t k, double max_dist, const double lo[3],
+                          const double hi[3], int32_t* nbr, void* ws, uint64_t ws_bytes, void* stream) {
+    if (n > 2048) return epp_knn_grid_ws_box(nodes, n, k, max_dist, lo, hi, nbr, ws, ws_bytes, stream);
     return epp_knn_bruteforce(nodes, n, k, max_dist, nbr, stream);
 }
 

@@ -104,6 +104,8 @@ def lib() -> C.CDLL:
             "epp_knn_workspace_size": (C.c_uint64, [i32]),
             "epp_knn_ws": (i32, [vp, i32, i32, dp, vp, vp, C.c_uint64, vp]),
             "epp_knn_grid_ws": (i32, [vp, i32, i32, dp, vp, vp, C.c_uint64, vp]),
+            "epp_knn_ws_box": (i32, [vp, i32, i32, dp, vp, vp, vp, vp, C.c_uint64, vp]),
+            "epp_knn_grid_ws_box": (i32, [vp, i32, i32, dp, vp, vp, vp, vp, C.c_uint64, vp]),
             "epp_knn_edges": (i32, [vp, vp, i32, i32, vp, vp, vp]),
             "epp_compact_states": (i32, [vp, vp, i64, vp, vp, vp]),
             "epp_compact_workspace_size": (C.c_uint64, [i64]),
@@ -135,7 +137,7 @@ EXPORTED = [
     "epp_graph_begin", "epp_graph_end", "epp_graph_launch", "epp_graph_destroy", "epp_minsnap_batch_times",
     "epp_generate_trajectory_times_host", "epp_world_generation", "epp_world_build_index", "epp_comm_unique_id", "epp_comm_init",
     "epp_comm_init_all", "epp_comm_destroy", "epp_comm_rank", "epp_comm_allgather_waypoints",
-    "epp_comm_allreduce_f64", "epp_comm_barrier", "epp_comm_available",
+    "epp_comm_allreduce_f64", "epp_comm_barrier", "epp_comm_available", "epp_knn_ws_box", "epp_knn_grid_ws_box",
 ]
 
 
@@ -428,18 +430,24 @@ def sample_uniform(seed: int, lo, hi, n: int, start: int = 0) -> np.ndarray:
     return d.download(np.float64, 3 * n).reshape(n, 3)
 
 
-def knn(nodes: np.ndarray, k: int, max_dist: float = 0.0, method: str = "auto") -> np.ndarray:
+def knn(nodes: np.ndarray, k: int, max_dist: float = 0.0, method: str = "auto", box=None) -> np.ndarray:
     """epp_knn (method "auto"), epp_knn_bruteforce ("brute") or epp_knn_grid ("grid"):
     (n, k) neighbour indices, nearest first, ties to the lower index, -1 where fewer
-    than k exist."""
+    than k exist.  box=(lo, hi) with method "ws" / "grid_ws": the caller-box variants
+    (epp_knn_ws_box / epp_knn_grid_ws_box; every node inside the box)."""
     nodes = np.ascontiguousarray(np.asarray(nodes, np.float64).reshape(-1, 3))
     n = len(nodes)
     d_n = DeviceBuffer.from_array(nodes)
     d_k = DeviceBuffer(4 * max(n * k, 1))
     if method in ("ws", "grid_ws"):  # caller workspace variants
         d_w = DeviceBuffer(max(int(lib().epp_knn_workspace_size(n)), 256))
-        fn = lib().epp_knn_ws if method == "ws" else lib().epp_knn_grid_ws
-        check(fn(d_n.ptr, n, int(k), float(max_dist), d_k.ptr, d_w.ptr, d_w.nbytes, None))
+        if box is not None:
+            lo, hi = (np.ascontiguousarray(np.asarray(b, np.float64).reshape(3)) for b in box)
+            fn = lib().epp_knn_ws_box if method == "ws" else lib().epp_knn_grid_ws_box
+            check(fn(d_n.ptr, n, int(k), float(max_dist), _ptr(lo), _ptr(hi), d_k.ptr, d_w.ptr, d_w.nbytes, None))
+        else:
+            fn = lib().epp_knn_ws if method == "ws" else lib().epp_knn_grid_ws
+            check(fn(d_n.ptr, n, int(k), float(max_dist), d_k.ptr, d_w.ptr, d_w.nbytes, None))
     else:
         fn = {"auto": lib().epp_knn, "brute": lib().epp_knn_bruteforce, "grid": lib().epp_knn_grid}[method]
         check(fn(d_n.ptr, n, int(k), float(max_dist), d_k.ptr, None))

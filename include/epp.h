@@ -203,6 +203,14 @@ epp_status epp_knn_ws(const double* nodes, int32_t n, int32_t k, double max_dist
                       uint64_t ws_bytes, void* stream);
 epp_status epp_knn_grid_ws(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr, void* ws,
                            uint64_t ws_bytes, void* stream);
+/* The same with the grid laid over the caller's box [lo, hi] (host arrays) instead of the
+ * nodes' bounding box, which saves its device reduction (two kernels fewer): every node
+ * must lie inside the closed box (the planner's samples lie in the world bounds; start and
+ * goal widen them).  Same answers. */
+epp_status epp_knn_ws_box(const double* nodes, int32_t n, int32_t k, double max_dist, const double lo[3],
+                          const double hi[3], int32_t* nbr, void* ws, uint64_t ws_bytes, void* stream);
+epp_status epp_knn_grid_ws_box(const double* nodes, int32_t n, int32_t k, double max_dist, const double lo[3],
+                               const double hi[3], int32_t* nbr, void* ws, uint64_t ws_bytes, void* stream);
 /* Edge endpoints for every (node i, neighbour c): s1 = nodes[i], s2 = nodes[nbr[i k + c]]
  * (s2 = s1 for a missing neighbour).  s1, s2: n k x 3. */
 epp_status epp_knn_edges(const double* nodes, const int32_t* nbr, int32_t n, int32_t k, double* s1,

@@ -94,6 +94,12 @@ def test_knn_grid_large(k, tile, monkeypatch):
     assert np.array_equal(capi.knn(nodes, k), got)                   # auto -> grid
     assert np.array_equal(capi.knn(nodes, k, method="ws"), got)      # caller workspace
     assert np.array_equal(capi.knn(nodes, k, method="grid_ws"), got)
+    # the caller-box variants: the grid over a given box that holds every node (tight,
+    # wider, and lopsided)
+    lo, hi = nodes.min(0), nodes.max(0)
+    for box in ((lo, hi), (lo - 1.0, hi + 2.0), (lo - [0.0, 3.0, 0.0], hi + [0.5, 0.0, 4.0])):
+        assert np.array_equal(capi.knn(nodes, k, method="grid_ws", box=box), got)
+        assert np.array_equal(capi.knn(nodes, k, method="ws", box=box), got)
 
 
 @pytest.mark.parametrize("tile", ["1", "0"])
