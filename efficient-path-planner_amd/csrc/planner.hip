@@ -241,46 +241,41 @@ __global__ void k_knn_count(const double* __restrict__ nodes, int n, const KnnGr
     atomicAdd(&cnt[c], 1);
 }
 
-// exclusive scan of cnt[0..ncell) into start[0..ncell], one block: per-thread chunk sums,
-// wave scans (shuffles), wave totals in LDS
+// exclusive scan of cnt[0..ncell) into start[0..ncell], one block: every thread loads a
+// run of kScanPer consecutive counts at once (16-byte loads, all in flight together: one
+// global round trip per tile instead of staging tiles through LDS), wave scans of the run
+// sums (shuffles), wave totals in LDS; the carry runs across tiles (one tile at ~64k
+// nodes: 1024 x 48 cells)
+constexpr int kScanPer = 48;
 __global__ __launch_bounds__(kBoundsThreads) void k_knn_scan(const KnnGrid* __restrict__ gp,
                                                              const int* __restrict__ cnt,
                                                              int* __restrict__ start) {
-    constexpr int kScanPer = 16;  // cells per thread per tile
     constexpr int kScanTile = kScanPer * kBoundsThreads;
-    __shared__ int tile_v[kScanTile + kScanTile / 32];  // padded: i -> i + i / 32
+    static_assert(kScanPer % 4 == 0, "16-byte runs");
     __shared__ int wsum[kBoundsThreads / 64];
     const int nc = gp->ncell;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    // tiles staged through LDS: coalesced loads and stores, kScanPer consecutive cells
-    // per thread for the scan; the carry runs across tiles; the next tile's loads are in
-    // flight while this one is scanned (one workgroup: its load latency is the cost)
     int carry = 0;
-    int nxt[kScanPer];
-    auto fetch = [&](int t0) {
-#pragma unroll
-        for (int u = 0; u < kScanPer; ++u) {
-            const int i = t0 + u * kBoundsThreads + threadIdx.x;
-            nxt[u] = i < nc ? cnt[i] : 0;
-        }
-    };
-    fetch(0);
     for (int t0 = 0; t0 < nc; t0 += kScanTile) {  // block-uniform
+        const int b0 = t0 + kScanPer * threadIdx.x;
+        int v[kScanPer];
+        if (b0 + kScanPer <= nc) {  // (cnt and start are 256-byte aligned, b0 a multiple of 4)
 #pragma unroll
-        for (int u = 0; u < kScanPer; ++u) {
-            const int i = u * kBoundsThreads + threadIdx.x;
-            tile_v[i + (i >> 5)] = nxt[u];
-        }
-        if (t0 + kScanTile < nc) fetch(t0 + kScanTile);
-        __syncthreads();
-        int v[kScanPer], s = 0;
+            for (int u = 0; u < kScanPer / 4; ++u) {
+                const int4 q = reinterpret_cast<const int4*>(cnt + b0)[u];
+                v[4 * u] = q.x;
+                v[4 * u + 1] = q.y;
+                v[4 * u + 2] = q.z;
+                v[4 * u + 3] = q.w;
+            }
+        } else {
 #pragma unroll
-        for (int u = 0; u < kScanPer; ++u) {
-            const int i = kScanPer * threadIdx.x + u;
-            v[u] = tile_v[i + (i >> 5)];
-            s += v[u];
+            for (int u = 0; u < kScanPer; ++u) v[u] = b0 + u < nc ? cnt[b0 + u] : 0;
         }
-        int incl = s;
+        int sum = 0;
+#pragma unroll
+        for (int u = 0; u < kScanPer; ++u) sum += v[u];
+        int incl = sum;
         for (int o = 1; o < 64; o <<= 1) {
             const int t = __shfl_up(incl, o, 64);
             if (lane >= o) incl += t;
@@ -292,21 +287,27 @@ __global__ __launch_bounds__(kBoundsThreads) void k_knn_scan(const KnnGrid* __re
             wbase += w < wv ? wsum[w] : 0;
             tile += wsum[w];
         }
-        int acc = carry + wbase + incl - s;
+        int acc = carry + wbase + incl - sum;
+        if (b0 + kScanPer <= nc) {
 #pragma unroll
-        for (int u = 0; u < kScanPer; ++u) {
-            const int i = kScanPer * threadIdx.x + u;
-            tile_v[i + (i >> 5)] = acc;
-            acc += v[u];
+            for (int u = 0; u < kScanPer / 4; ++u) {
+                int4 q;
+                q.x = acc;
+                q.y = q.x + v[4 * u];
+                q.z = q.y + v[4 * u + 1];
+                q.w = q.z + v[4 * u + 2];
+                acc = q.w + v[4 * u + 3];
+                reinterpret_cast<int4*>(start + b0)[u] = q;
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < kScanPer; ++u) {
+                if (b0 + u < nc) start[b0 + u] = acc;
+                acc += v[u];
+            }
         }
         carry += tile;
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < kScanPer; ++u) {
-            const int i = u * kBoundsThreads + threadIdx.x;
-            if (t0 + i < nc) start[t0 + i] = tile_v[i + (i >> 5)];
-        }
-        __syncthreads();  // tile_v and wsum are rewritten by the next tile
+        __syncthreads();  // wsum is rewritten by the next tile
     }
     if (threadIdx.x == 0) start[nc] = carry;
 }
