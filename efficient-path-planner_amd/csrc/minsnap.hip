@@ -145,7 +145,7 @@ struct Seg {
 constexpr int kNPow = 22;
 // Per track, besides the segment scratch: (M+1) x 5 x 3 vertex values, (M+1) x 4 x 3
 // right-hand sides, M segment times and the block solve's lane exchange (kXch, in LDS).
-constexpr int kXch = 32;
+constexpr int kXch = 96;
 __host__ __device__ constexpr size_t vertex_doubles(int M) { return (size_t)(M + 1) * 27 + (size_t)M + kXch; }
 // Tracks with up to this many segments keep the segment scratch in LDS (~114 KB at 40).
 constexpr int kMaxLdsSeg = 40;
@@ -282,132 +282,104 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ kc, const 
     block_sync<SCR_LDS>();
     EPP_TL(5);
     EPP_TLC(14);
-    // ---- phase 4: block-tridiagonal solve (block Thomas, explicit 4x4 inverses) ---------
+    // ---- phase 4: block-tridiagonal solve (block Thomas, lanes over the block entries) ---
     // Inner vertices v = 1..nin, diagonal blocks D_v, couplings E_v (v -> v+1), right-hand
     // sides b_v (3 columns):
     //   S_1 = D_1, y_1 = b_1;  G_v = S_v^-1 E_v, g_v = S_v^-1 y_v;
     //   S_{v+1} = D_{v+1} - E_v^T G_v, y_{v+1} = b_{v+1} - E_v^T g_v;
     //   back: x_nin = g_nin, x_v = g_v - G_v x_{v+1}.
-    // S_v^-1 = adj(S_v) / det(S_v) from the 2x2 minors of its row pairs: independent
-    // products, no square roots or pivots, so a step is ~20 dependent instructions where
-    // the Cholesky's chain (4 dependent square roots, 4 dependent forward substitutions)
-    // was ~80.  The whole first wavefront runs every step with the same (uniform) values --
-    // no lane exchange, no barrier inside the chain; lane 0 stores G_v, g_v for the back
-    // substitution, which the same wave then runs.  The Schur complements of an SPD
-    // R_pp are SPD (det > 0); the explicit inverse is within ~cond(S_v) ulp of the
-    // factorisation's answer (parity target 1e-6).
+    // The first wavefront's lanes 0..27 each own one entry: lanes 0..15 the 4x4 block
+    // entry (L>>2, L&3), lanes 16..27 the 4x3 right-hand-side entry ((L-16)/3, (L-16)%3).
+    // A step is three LDS-exchanged stages -- adj(S) (one cofactor per lane), [G g] = adj
+    // [E y] / det, [S' y'] = [D b] - E^T [G g] -- each ~10 FP64 instructions wide, where
+    // a one-lane factorisation runs ~150 dependent ones.  S_v^-1 = adj(S_v) / det(S_v):
+    // no pivots or square roots; the Schur complements of an SPD R_pp are SPD (det > 0),
+    // and the explicit inverse is within ~cond(S_v) ulp of a factorisation's answer
+    // (parity target 1e-6).  G_v is kept in segment v-1's L slot (D_v is consumed by
+    // then), g_v in rhs[v]; the back substitution runs on lanes 0..11.
+    // xch: S|y [0,28), adj(S) [28,44), G|g [44,72), x (two buffers) [72,96).
     if (tid < kWave && nin > 0) {
+        const int L = tid;
+        const bool mat = L < 16, act = L < 28;
+        const int row = mat ? (L >> 2) : (L - 16) / 3;  // block row (S, G) or rhs row (y, g)
+        const int col = mat ? (L & 3) : (L - 16) % 3;
+        if (act) xch[L] = mat ? scr[Seg::kL + L] : rhs[12 + (L - 16)];
+        // the cofactor this lane computes: adj(S)[ar][ac] = (-1)^(ar+ac) det(S minus row ac, col ar)
+        const int ar = (L >> 2) & 3, ac = L & 3;
+        const int r0 = ac == 0 ? 1 : 0, r1 = ac <= 1 ? 2 : 1, r2 = ac <= 2 ? 3 : 2;
+        const int c0 = ar == 0 ? 1 : 0, c1 = ar <= 1 ? 2 : 1, c2 = ar <= 2 ? 3 : 2;
+        const double sgn = ((ar + ac) & 1) ? -1.0 : 1.0;
         bool ok = true;
-        double S[16], y[12];
-        {
-            const double* Sg = scr;  // segment 0: D_1
-#pragma unroll
-            for (int i = 0; i < 16; ++i) S[i] = Sg[Seg::kL + i];
-#pragma unroll
-            for (int i = 0; i < 12; ++i) y[i] = rhs[4 * 3 + i];
-        }
+        wave_sync_lds();
         for (int v = 1; v <= nin; ++v) {
             EPP_TLI(v);
             double* Sg = scr + (size_t)(v - 1) * Seg::kSize;
-            double E[16], Dn[16], bn[12];
+            // E_v column `row` (for [S' y']) and, matrix lanes, column `col` (for G);
+            // next step's D/b entry: independent of this step, in flight meanwhile
+            double Ep[4], Ec[4], nxt = 0.0;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) E[i] = Sg[Seg::kW + i];  // (zero for v = nin)
-            if (v < nin) {  // next step's D and b: independent of this step, in flight meanwhile
-                const double* Sn = Sg + Seg::kSize;
-#pragma unroll
-                for (int i = 0; i < 16; ++i) Dn[i] = Sn[Seg::kL + i];
-#pragma unroll
-                for (int i = 0; i < 12; ++i) bn[i] = rhs[(size_t)(v + 1) * 12 + i];
+            for (int k = 0; k < 4; ++k) {
+                Ep[k] = act ? Sg[Seg::kW + k * 4 + row] : 0.0;
+                Ec[k] = mat ? Sg[Seg::kW + k * 4 + col] : 0.0;
             }
-            // adj(S) from the 2x2 minors of rows (0,1) and (2,3)
-            const double s0 = S[0] * S[5] - S[4] * S[1], s1 = S[0] * S[6] - S[4] * S[2];
-            const double s2 = S[0] * S[7] - S[4] * S[3], s3 = S[1] * S[6] - S[5] * S[2];
-            const double s4 = S[1] * S[7] - S[5] * S[3], s5 = S[2] * S[7] - S[6] * S[3];
-            const double c5 = S[10] * S[15] - S[14] * S[11], c4 = S[9] * S[15] - S[13] * S[11];
-            const double c3 = S[9] * S[14] - S[13] * S[10], c2 = S[8] * S[15] - S[12] * S[11];
-            const double c1 = S[8] * S[14] - S[12] * S[10], c0 = S[8] * S[13] - S[12] * S[9];
-            const double det = ((s0 * c5 - s1 * c4) + (s2 * c3 + s3 * c2)) + (s5 * c0 - s4 * c1);
-            double A[16];
-            A[0] = (S[5] * c5 - S[6] * c4) + S[7] * c3;
-            A[1] = (S[2] * c4 - S[1] * c5) - S[3] * c3;
-            A[2] = (S[13] * s5 - S[14] * s4) + S[15] * s3;
-            A[3] = (S[10] * s4 - S[9] * s5) - S[11] * s3;
-            A[4] = (S[6] * c2 - S[4] * c5) - S[7] * c1;
-            A[5] = (S[0] * c5 - S[2] * c2) + S[3] * c1;
-            A[6] = (S[14] * s2 - S[12] * s5) - S[15] * s1;
-            A[7] = (S[8] * s5 - S[10] * s2) + S[11] * s1;
-            A[8] = (S[4] * c4 - S[5] * c2) + S[7] * c0;
-            A[9] = (S[1] * c2 - S[0] * c4) - S[3] * c0;
-            A[10] = (S[12] * s4 - S[13] * s2) + S[15] * s0;
-            A[11] = (S[9] * s2 - S[8] * s4) - S[11] * s0;
-            A[12] = (S[5] * c1 - S[4] * c3) - S[6] * c0;
-            A[13] = (S[0] * c3 - S[1] * c1) + S[2] * c0;
-            A[14] = (S[13] * s1 - S[12] * s3) - S[14] * s0;
-            A[15] = (S[8] * s3 - S[9] * s1) + S[10] * s0;
-            ok = ok && det > 0.0 && S[0] > 0.0 && S[5] > 0.0 && S[10] > 0.0 && S[15] > 0.0;
-            // 1/det: the hardware reciprocal refined by two Newton steps
-            double id = __builtin_amdgcn_rcp(det);
+            if (v < nin && act) nxt = mat ? Sg[Seg::kSize + Seg::kL + L] : rhs[(size_t)(v + 1) * 12 + (L - 16)];
+            // stage 1: one cofactor per lane (lanes 0..15)
+            if (mat) {
+                const double a = xch[r0 * 4 + c0], b = xch[r0 * 4 + c1], c = xch[r0 * 4 + c2];
+                const double d = xch[r1 * 4 + c0], e = xch[r1 * 4 + c1], f = xch[r1 * 4 + c2];
+                const double g = xch[r2 * 4 + c0], h = xch[r2 * 4 + c1], i = xch[r2 * 4 + c2];
+                xch[28 + L] = sgn * ((a * (e * i - f * h) - b * (d * i - f * g)) + c * (d * h - e * g));
+            }
+            wave_sync_lds();
+            // stage 2: det (every lane, uniform), [G g] = adj(S) [E y] / det
+            const double det = (xch[0] * xch[28] + xch[1] * xch[32]) + (xch[2] * xch[36] + xch[3] * xch[40]);
+            ok = ok && det > 0.0 && xch[0] > 0.0 && xch[5] > 0.0 && xch[10] > 0.0 && xch[15] > 0.0;
+            double id = __builtin_amdgcn_rcp(det);  // refined by two Newton steps
             id = fma(id, fma(-det, id, 1.0), id);
             id = fma(id, fma(-det, id, 1.0), id);
-            // G = S^-1 E, g = S^-1 y (adj products first: they do not wait for 1/det)
-            double G[16], gy[12];
+            if (act) {
+                double o[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    G[i * 4 + j] = ((A[i * 4] * E[j] + A[i * 4 + 1] * E[4 + j]) + (A[i * 4 + 2] * E[8 + j] + A[i * 4 + 3] * E[12 + j])) * id;
-#pragma unroll
-                for (int d = 0; d < 3; ++d)
-                    gy[i * 3 + d] = ((A[i * 4] * y[d] + A[i * 4 + 1] * y[3 + d]) + (A[i * 4 + 2] * y[6 + d] + A[i * 4 + 3] * y[9 + d])) * id;
+                for (int k = 0; k < 4; ++k) o[k] = mat ? Ec[k] : xch[16 + k * 3 + col];
+                const double* Ar = xch + 28 + row * 4;
+                const double gv = ((Ar[0] * o[0] + Ar[1] * o[1]) + (Ar[2] * o[2] + Ar[3] * o[3])) * id;
+                xch[44 + L] = gv;
+                if (mat) Sg[Seg::kL + L] = gv;  // G_v for the back substitution
+                else rhs[(size_t)v * 12 + (L - 16)] = gv;
             }
-            if (tid == 0) {  // for the back substitution (W slot: E_v is not needed again)
+            wave_sync_lds();
+            // stage 3: [S' y'] = [D b] - E^T [G g]
+            if (v < nin && act) {
+                double o[4];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) Sg[Seg::kW + i] = G[i];
-#pragma unroll
-                for (int i = 0; i < 12; ++i) rhs[(size_t)v * 12 + i] = gy[i];
+                for (int k = 0; k < 4; ++k) o[k] = mat ? xch[44 + k * 4 + col] : xch[60 + k * 3 + col];
+                xch[L] = nxt - ((Ep[0] * o[0] + Ep[1] * o[1]) + (Ep[2] * o[2] + Ep[3] * o[3]));
             }
-            if (v < nin) {
-#pragma unroll
-                for (int p = 0; p < 4; ++p) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        S[p * 4 + q] = Dn[p * 4 + q] - ((E[p] * G[q] + E[4 + p] * G[4 + q]) + (E[8 + p] * G[8 + q] + E[12 + p] * G[12 + q]));
-#pragma unroll
-                    for (int d = 0; d < 3; ++d)
-                        y[p * 3 + d] = bn[p * 3 + d] - ((E[p] * gy[d] + E[4 + p] * gy[3 + d]) + (E[8 + p] * gy[6 + d] + E[12 + p] * gy[9 + d]));
-                }
-            }
+            wave_sync_lds();
         }
-        // (lane 0's stores, LDS or, for long tracks, global scratch: a workgroup-scope fence
+        // (the G/g stores, LDS or, for long tracks, global scratch: a workgroup-scope fence
         // makes the latter visible to the wave's own later loads)
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         wave_sync_lds();
         if (ok) {
             EPP_TLI(32);
-            double xn[12];
+            // lanes 0..11: x_v entry (p, d) = (L/3, L%3)
+            const int p = L / 3, d = L % 3;
+            int buf = 0;
             for (int v = nin; v >= 1; --v) {
                 EPP_TLI(32 + nin + 1 - v);
-                const double* Sg = scr + (size_t)(v - 1) * Seg::kSize;
-                double x[12];
-#pragma unroll
-                for (int i = 0; i < 12; ++i) x[i] = rhs[(size_t)v * 12 + i];
-                if (v < nin) {
-                    double G[16];
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) G[i] = Sg[Seg::kW + i];
-#pragma unroll
-                    for (int p = 0; p < 4; ++p)
-#pragma unroll
-                        for (int d = 0; d < 3; ++d)
-                            x[p * 3 + d] = x[p * 3 + d] - ((G[p * 4] * xn[d] + G[p * 4 + 1] * xn[3 + d]) +
-                                                           (G[p * 4 + 2] * xn[6 + d] + G[p * 4 + 3] * xn[9 + d]));
+                if (L < 12) {
+                    const double* Gr = scr + (size_t)(v - 1) * Seg::kSize + Seg::kL + p * 4;
+                    double x = rhs[(size_t)v * 12 + L];
+                    if (v < nin) {
+                        const double* xn = xch + 72 + buf * 12;
+                        x = x - ((Gr[0] * xn[d] + Gr[1] * xn[3 + d]) + (Gr[2] * xn[6 + d] + Gr[3] * xn[9 + d]));
+                    }
+                    xch[72 + (buf ^ 1) * 12 + L] = x;
+                    dv[((size_t)v * HALF + 1) * 3 + L] = x;  // derivatives 1..4 of vertex v
                 }
-#pragma unroll
-                for (int i = 0; i < 12; ++i) xn[i] = x[i];
-                if (tid == 0) {  // derivatives 1..4 of vertex v: 12 consecutive values of dv
-#pragma unroll
-                    for (int i = 0; i < 12; ++i) dv[((size_t)v * HALF + 1) * 3 + i] = x[i];
-                }
+                buf ^= 1;
+                wave_sync_lds();
             }
         }
         if (!ok && tid == 0) *s_err = 1;
