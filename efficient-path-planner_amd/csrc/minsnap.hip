@@ -290,99 +290,132 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ kc, const 
     //   back: x_nin = g_nin, x_v = g_v - G_v x_{v+1}.
     // The first wavefront's lanes 0..27 each own one entry: lanes 0..15 the 4x4 block
     // entry (L>>2, L&3), lanes 16..27 the 4x3 right-hand-side entry ((L-16)/3, (L-16)%3).
-    // A step is three LDS-exchanged stages -- adj(S) (one cofactor per lane), [G g] = adj
-    // [E y] / det, [S' y'] = [D b] - E^T [G g] -- each ~10 FP64 instructions wide, where
-    // a one-lane factorisation runs ~150 dependent ones.  S_v^-1 = adj(S_v) / det(S_v):
-    // no pivots or square roots; the Schur complements of an SPD R_pp are SPD (det > 0),
-    // and the explicit inverse is within ~cond(S_v) ulp of a factorisation's answer
-    // (parity target 1e-6).  G_v is kept in segment v-1's L slot (D_v is consumed by
-    // then), g_v in rhs[v]; the back substitution runs on lanes 0..11.
-    // xch: S|y [0,28), adj(S) [28,44), G|g [44,72), x (two buffers) [72,96).
+    // A step is two LDS-exchanged stages: (1) adj(S) (one cofactor per lane); (2) every
+    // lane reads all of adj(S) and forms the column t = adj(S) X of its own right-hand
+    // side X (E column for block lanes, y column for rhs lanes) while det(S) and its
+    // reciprocal are computed beside it; its entry of [G g] = t / det (kept for the back
+    // substitution) and of [S' y'] = [D b] - E^T t / det (the next step's S, exchanged)
+    // follow without another exchange.  S_v^-1 = adj(S_v) / det(S_v): no pivots or square
+    // roots; the Schur complements of an SPD R_pp are SPD (det > 0), and the explicit
+    // inverse is within ~cond(S_v) ulp of a factorisation's answer (parity target 1e-6).
+    // Every value a step needs that does not depend on the chain (E_v, the next D / b
+    // entry) is loaded at its start, and every LDS read of a stage is issued together (no
+    // short-circuit reads).  G_v is kept in segment v-1's L slot (D_v is consumed by then),
+    // g_v in rhs[v]; the back substitution runs on lanes 0..11.
+    // xch: S|y [0,28), adj(S) [28,44), x (two buffers) [72,96).
     if (tid < kWave && nin > 0) {
         const int L = tid;
         const bool mat = L < 16, act = L < 28;
         const int row = mat ? (L >> 2) : (L - 16) / 3;  // block row (S, G) or rhs row (y, g)
         const int col = mat ? (L & 3) : (L - 16) % 3;
-        if (act) xch[L] = mat ? scr[Seg::kL + L] : rhs[12 + (L - 16)];
+        const int ycol = mat ? 0 : col;                   // (block lanes read a dummy y column)
+        const bool diag = mat && (L % 5) == 0;            // S[i][i]: must stay > 0 (SPD)
+        double cur = act ? (mat ? scr[Seg::kL + L] : rhs[12 + (L - 16)]) : 1.0;  // this lane's S / y entry
+        if (act) xch[L] = cur;
+        bool ok = !diag || cur > 0.0;
         // the cofactor this lane computes: adj(S)[ar][ac] = (-1)^(ar+ac) det(S minus row ac, col ar)
         const int ar = (L >> 2) & 3, ac = L & 3;
         const int r0 = ac == 0 ? 1 : 0, r1 = ac <= 1 ? 2 : 1, r2 = ac <= 2 ? 3 : 2;
         const int c0 = ar == 0 ? 1 : 0, c1 = ar <= 1 ? 2 : 1, c2 = ar <= 2 ? 3 : 2;
         const double sgn = ((ar + ac) & 1) ? -1.0 : 1.0;
-        bool ok = true;
         wave_sync_lds();
         for (int v = 1; v <= nin; ++v) {
             EPP_TLI(v);
             double* Sg = scr + (size_t)(v - 1) * Seg::kSize;
-            // E_v column `row` (for [S' y']) and, matrix lanes, column `col` (for G);
-            // next step's D/b entry: independent of this step, in flight meanwhile
+            // E_v column `row` (for E^T t) and column `col` (block lanes' X); the next
+            // step's D / b entry: independent of the chain, in flight meanwhile
             double Ep[4], Ec[4], nxt = 0.0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                Ep[k] = act ? Sg[Seg::kW + k * 4 + row] : 0.0;
-                Ec[k] = mat ? Sg[Seg::kW + k * 4 + col] : 0.0;
+                Ep[k] = Sg[Seg::kW + k * 4 + (row & 3)];
+                Ec[k] = Sg[Seg::kW + k * 4 + (col & 3)];
             }
             if (v < nin && act) nxt = mat ? Sg[Seg::kSize + Seg::kL + L] : rhs[(size_t)(v + 1) * 12 + (L - 16)];
-            // stage 1: one cofactor per lane (lanes 0..15)
-            if (mat) {
-                const double a = xch[r0 * 4 + c0], b = xch[r0 * 4 + c1], c = xch[r0 * 4 + c2];
-                const double d = xch[r1 * 4 + c0], e = xch[r1 * 4 + c1], f = xch[r1 * 4 + c2];
-                const double g = xch[r2 * 4 + c0], h = xch[r2 * 4 + c1], i = xch[r2 * 4 + c2];
-                xch[28 + L] = sgn * ((a * (e * i - f * h) - b * (d * i - f * g)) + c * (d * h - e * g));
+            // stage 1: one cofactor per block lane; S row 0 (det) and the y column (rhs
+            // lanes' X) read with it
+            const double a = xch[r0 * 4 + c0], b = xch[r0 * 4 + c1], c = xch[r0 * 4 + c2];
+            const double d = xch[r1 * 4 + c0], e = xch[r1 * 4 + c1], f = xch[r1 * 4 + c2];
+            const double g = xch[r2 * 4 + c0], h = xch[r2 * 4 + c1], i = xch[r2 * 4 + c2];
+            double s0[4], yc[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                s0[k] = xch[k];
+                yc[k] = xch[16 + k * 3 + ycol];
             }
+            const double m0 = fma(e, i, -(f * h)), m1 = fma(d, i, -(f * g)), m2 = fma(d, h, -(e * g));
+            const double cof = sgn * fma(c, m2, fma(a, m0, -(b * m1)));
+            if (mat) xch[28 + L] = cof;
             wave_sync_lds();
-            // stage 2: det (every lane, uniform), [G g] = adj(S) [E y] / det
-            const double det = (xch[0] * xch[28] + xch[1] * xch[32]) + (xch[2] * xch[36] + xch[3] * xch[40]);
-            ok = ok && det > 0.0 && xch[0] > 0.0 && xch[5] > 0.0 && xch[10] > 0.0 && xch[15] > 0.0;
+            // stage 2: adj(S) to every lane; det = S row 0 . adj column 0
+            double adj[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) adj[k] = xch[28 + k];
+            const double det = fma(s0[0], adj[0], s0[1] * adj[4]) + fma(s0[2], adj[8], s0[3] * adj[12]);
             double id = __builtin_amdgcn_rcp(det);  // refined by two Newton steps
             id = fma(id, fma(-det, id, 1.0), id);
             id = fma(id, fma(-det, id, 1.0), id);
-            if (act) {
-                double o[4];
+            ok = ok && det > 0.0;
+            double X[4], t[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) o[k] = mat ? Ec[k] : xch[16 + k * 3 + col];
-                const double* Ar = xch + 28 + row * 4;
-                const double gv = ((Ar[0] * o[0] + Ar[1] * o[1]) + (Ar[2] * o[2] + Ar[3] * o[3])) * id;
-                xch[44 + L] = gv;
+            for (int k = 0; k < 4; ++k) X[k] = mat ? Ec[k] : yc[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                t[k] = fma(adj[4 * k], X[0], adj[4 * k + 1] * X[1]) + fma(adj[4 * k + 2], X[2], adj[4 * k + 3] * X[3]);
+            const double tr = row == 0 ? t[0] : row == 1 ? t[1] : row == 2 ? t[2] : t[3];
+            const double gv = tr * id;
+            const double et = fma(Ep[0], t[0], Ep[1] * t[1]) + fma(Ep[2], t[2], Ep[3] * t[3]);
+            if (act) {
                 if (mat) Sg[Seg::kL + L] = gv;  // G_v for the back substitution
                 else rhs[(size_t)v * 12 + (L - 16)] = gv;
             }
-            wave_sync_lds();
-            // stage 3: [S' y'] = [D b] - E^T [G g]
-            if (v < nin && act) {
-                double o[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) o[k] = mat ? xch[44 + k * 4 + col] : xch[60 + k * 3 + col];
-                xch[L] = nxt - ((Ep[0] * o[0] + Ep[1] * o[1]) + (Ep[2] * o[2] + Ep[3] * o[3]));
+            if (v < nin) {
+                cur = fma(-et, id, nxt);  // [S' y'] = [D b] - E^T t / det
+                if (act) xch[L] = cur;
+                ok = ok && (!diag || cur > 0.0);
             }
             wave_sync_lds();
         }
         // (the G/g stores, LDS or, for long tracks, global scratch: a workgroup-scope fence
         // makes the latter visible to the wave's own later loads)
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        if (!SCR_LDS) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         wave_sync_lds();
-        if (ok) {
+        if (__ballot(!ok) == 0ull) {  // wave-uniform
             EPP_TLI(32);
-            // lanes 0..11: x_v entry (p, d) = (L/3, L%3)
-            const int p = L / 3, d = L % 3;
+            // lanes 0..11: x_v entry (p, d) = (L/3, L%3); G_v row p and g_v entry of the
+            // next step are loaded before this step's exchange completes
+            const int p = (L / 3) & 3, d = L % 3;
+            const int Lr = L < 12 ? L : 0;
             int buf = 0;
+            double Gr[4], gx;
+            auto load_step = [&](int v, double (&G)[4], double& gg) {
+                const double* Gp = scr + (size_t)(v - 1) * Seg::kSize + Seg::kL + p * 4;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) G[k] = Gp[k];
+                gg = rhs[(size_t)v * 12 + Lr];
+            };
+            load_step(nin, Gr, gx);
             for (int v = nin; v >= 1; --v) {
                 EPP_TLI(32 + nin + 1 - v);
+                double Gn[4] = {0.0, 0.0, 0.0, 0.0}, gn = 0.0;
+                if (v > 1) load_step(v - 1, Gn, gn);
+                double x = gx;
+                if (v < nin) {
+                    const double* xn = xch + 72 + buf * 12;
+                    x = x - (fma(Gr[0], xn[d], Gr[1] * xn[3 + d]) + fma(Gr[2], xn[6 + d], Gr[3] * xn[9 + d]));
+                }
                 if (L < 12) {
-                    const double* Gr = scr + (size_t)(v - 1) * Seg::kSize + Seg::kL + p * 4;
-                    double x = rhs[(size_t)v * 12 + L];
-                    if (v < nin) {
-                        const double* xn = xch + 72 + buf * 12;
-                        x = x - ((Gr[0] * xn[d] + Gr[1] * xn[3 + d]) + (Gr[2] * xn[6 + d] + Gr[3] * xn[9 + d]));
-                    }
                     xch[72 + (buf ^ 1) * 12 + L] = x;
                     dv[((size_t)v * HALF + 1) * 3 + L] = x;  // derivatives 1..4 of vertex v
                 }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) Gr[k] = Gn[k];
+                gx = gn;
                 buf ^= 1;
                 wave_sync_lds();
             }
+        } else if (tid == 0) {
+            *s_err = 1;
         }
-        if (!ok && tid == 0) *s_err = 1;
         EPP_TLI(63);
     }
     block_sync<SCR_LDS>();
