@@ -1,3 +1,6 @@
+#include <algorithm>
+#include <cstdlib>
+#include <thread>
 // host_online.cpp — epp::OnlineTrajGenerator, the drop-in for the reference's
 // OnlineTrajGenerator (src/OnlineTrajGenerator.cpp).  Each function cites the lines it
 // follows; planning and the min-snap refit run on the GPU (PathPlanner,
@@ -242,7 +245,12 @@ bool OnlineTrajGenerator::updateGatePos(int gateId, const std::vector<double>& n
     }
     trajectoryCurrentlyUpdating = true;
     if (configParser->getPathPlannerProperties().recalculateOnline) {
-        pending = std::async(std::launch::async, [this, gateId, dronePos, flightTime] {
+        // EPP_TEST_REPLAN_HOLD_MS (test hook): the worker starts that much later, so a test
+        // can rely on the recomputation still running while it makes further calls
+        const char* hold = std::getenv("EPP_TEST_REPLAN_HOLD_MS");
+        const int hold_ms = hold && *hold ? std::max(0, std::atoi(hold)) : 0;
+        pending = std::async(std::launch::async, [this, gateId, dronePos, flightTime, hold_ms] {
+            if (hold_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(hold_ms));
             recomputeTraj(gateId, dronePos, flightTime);
         });
     } else {

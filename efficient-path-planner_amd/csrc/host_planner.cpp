@@ -146,9 +146,15 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     check(epp_sample_uniform(seed, lo, hi, samples, 0, d_s, st), "sample");
     check(epp_check_states(w, d_s, samples, canPass ? 1 : 0, d_v, nullptr, nullptr, st), "state check");
     check(epp_compact_states_ws(d_s, d_v, samples, d_nodes + 6, d_cnt, d_cws, cws_bytes, st), "compact");
-    check(epp_memcpy_h2d(d_nodes, ends, sizeof(ends), st), "upload");  // (synchronises the stream)
-    int64_t n_valid_states = 0;
-    check(epp_memcpy_d2h(&n_valid_states, d_cnt, 8, st), "download");
+    // start / goal up, the valid-state count down: both queued, one synchronisation
+    // (pinned staging: [ends (6 doubles) | count | edge counts (2)])
+    double* h_small = static_cast<double*>(ts.pinned(2, 16 * sizeof(double)));
+    std::copy(ends, ends + 6, h_small);
+    int64_t* h_cnt = reinterpret_cast<int64_t*>(h_small + 6);
+    check(epp_memcpy_h2d_async(d_nodes, h_small, sizeof(ends), st), "upload");
+    check(epp_memcpy_d2h_async(h_cnt, d_cnt, 8, st), "download");
+    check(epp_stream_sync(st), "sync");
+    const int64_t n_valid_states = h_cnt[0];
     const int32_t n = (int32_t)(n_valid_states + 2);
     // ---- 2. k-NN graph + batched motion checks (MotionValidator::checkMotion) --------
     const size_t m = (size_t)n * k;
@@ -170,14 +176,18 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     // failed motions -> -1; the valid edges, and those into the goal (node 1)
     check(epp_mask_edges_count(d_nbr, d_ev, (int64_t)m, 1, d_ecnt, st), "mask edges");
     // node coordinates and the masked k-NN table into pinned host staging
-    const double* nodes = static_cast<const double*>(ts.pinned(0, (size_t)n * 24));
-    const int32_t* nbr = static_cast<const int32_t*>(ts.pinned(1, m * 4));
-    check(epp_memcpy_d2h(const_cast<double*>(nodes), d_nodes, (uint64_t)n * 24, st), "download");
-    int64_t ecnt[2] = {0, 0};
-    check(epp_memcpy_d2h(ecnt, d_ecnt, 16, st), "download");
+    // (sized for the attempt's largest node count, not this one's: a pinned buffer that
+    // grows is freed and reallocated, and hipHostFree waits for the whole device)
+    const double* nodes = static_cast<const double*>(ts.pinned(0, max_nodes * 24));
+    const int32_t* nbr = static_cast<const int32_t*>(ts.pinned(1, m_max * 4));
+    // the three downloads queued back to back, one synchronisation
+    int64_t* ecnt = h_cnt + 1;
+    check(epp_memcpy_d2h_async(ecnt, d_ecnt, 16, st), "download");
+    check(epp_memcpy_d2h_async(const_cast<int32_t*>(nbr), d_nbr, m * 4, st), "download");
+    check(epp_memcpy_d2h_async(const_cast<double*>(nodes), d_nodes, (uint64_t)n * 24, st), "download");
+    check(epp_stream_sync(st), "sync");
     const int64_t n_valid_edges = ecnt[0];
     const bool goal_has_forward_edge = ecnt[1] > 0;
-    check(epp_memcpy_d2h(const_cast<int32_t*>(nbr), d_nbr, m * 4, st), "download");
     const auto t_dev1 = std::chrono::steady_clock::now();
     // ---- 3. shortest path over the valid edges, start = 0, goal = 1 ----------------------
     // A* with the Euclidean distance to the goal (admissible and consistent for Euclidean

@@ -3,6 +3,7 @@
 // from several threads (the reference plans two segments concurrently,
 // src/OnlineTrajGenerator.cpp:324-340) never share a stream or a buffer.
 #pragma once
+#include <algorithm>
 #include <cstddef>
 #include <cstdint>
 #include <stdexcept>
@@ -53,10 +54,12 @@ public:
         return p;
     }
     static size_t rounded(size_t bytes) { return (bytes + 255) & ~size_t(255); }
-    // Pinned (page-locked) host staging of at least `bytes`, slot 0 or 1: device-to-host
+    // Pinned (page-locked) host staging of at least `bytes`, slot 0, 1 or 2: device-to-host
     // copies into it run at DMA speed instead of through a pageable bounce buffer.
+    // Grows geometrically (x1.5): reallocating pinned memory synchronises the device.
     void* pinned(int slot, size_t bytes) {
         if (bytes > pcap_[slot]) {
+            bytes = std::max(bytes, pcap_[slot] + pcap_[slot] / 2);
             if (pin_[slot]) (void)hipHostFree(pin_[slot]);
             pin_[slot] = nullptr;
             pcap_[slot] = 0;
@@ -79,8 +82,8 @@ private:
     void* stream_ = nullptr;
     void* buf_ = nullptr;
     size_t cap_ = 0, used_ = 0;
-    void* pin_[2] = {nullptr, nullptr};
-    size_t pcap_[2] = {0, 0};
+    void* pin_[3] = {nullptr, nullptr, nullptr};
+    size_t pcap_[3] = {0, 0, 0};
 };
 
 }  // namespace epp

@@ -45,7 +45,8 @@ constexpr int kWave = 64;
 //   kCB   falling factorials B[k][j] = j! / (j-k)!  (src/polynomial.cpp:145-160), 10 x 10
 //   kCB5  B5^-1, kCK  K (the closed-form mapping inverse, ainv_entry), 5 x 5 each
 //   kCF   1 / r!, r = 0..4
-constexpr int kCB = 0, kCB5 = 100, kCK = 125, kCF = 150, kNC = 156;  // (kNC even: 16-byte aligned LDS after it)
+//   kCH   Hc, the constant part of H = A^-T Q A^-1 (hessian_const below), 10 x 10
+constexpr int kCB = 0, kCB5 = 100, kCK = 125, kCF = 150, kCH = 156, kNC = 256;  // (kNC even: 16-byte aligned LDS after it)
 __constant__ double cC[kNC];
 template <int BLOCK>
 __device__ __forceinline__ void stage_consts(double* dst) {
@@ -133,16 +134,25 @@ __device__ __forceinline__ double ainv_entry(const double* kc, const double* ipo
     return (c < HALF ? kc[kCK + rr * HALF + c] : kc[kCB5 + rr * HALF + c - HALF]) * ipow[-ex];
 }
 
-// Per-segment scratch (doubles): A^-1 (10x10), H (10x10), the 6x6 snap block Q of Q_i,
-// G = Q * (rows 4..9 of A^-1) (6x10), the R_pp blocks: W (coupling to the next inner
-// vertex, then the block solve's S^-1 E) and L (diagonal block), 4 spare, and the powers
-// of T.
+// H_i = A_i^-T Q_i A_i^-1 in closed form.  Row a >= 4 of A^-1 is a constant times
+// T^(c%5 - a) in column c (ainv_entry), and Q[a][b] (a, b >= 4) a constant times
+// T^(a+b-7) (computeQuadraticCostJacobian, impl :567-583), so every term of
+//   H[r][c] = sum_{a,b >= 4} A^-1[a][r] Q[a][b] A^-1[b][c]
+// carries the same power T^((r%5) + (c%5) - 7): H[r][c] = Hc[r][c] T^((r%5) + (c%5) - 7)
+// with the constant Hc (computed once on the host in long double, kCH).  The solve
+// reads the H entries it needs straight from Hc and the powers of T: no per-segment
+// A^-1 / Q / G / H products and none of their barriers.
+// Per-segment scratch (doubles): the R_pp blocks -- W (coupling to the next inner vertex,
+// then G = S^-1 E of the block solve) and L (diagonal block) -- and the powers of T.
 struct Seg {
-    static constexpr int kAinv = 0, kH = 100, kQ = 200, kG = 236, kW = 296, kL = 312, kPow = 332, kSize = 354;
+    static constexpr int kW = 0, kL = 16, kPow = 32, kSize = 44;
 };
-// kPow: T^0..T^11 (Q's powers) then (1/T)^0..(1/T)^9 (A^-1's), each the same chain of
-// products as evaluated per entry before (12 + 10 doubles)
-constexpr int kNPow = 22;
+// kPow: (1/T)^0..(1/T)^9 (A^-1's and H's negative powers) then T (H's one positive power)
+constexpr int kNPow = 11;
+__device__ __forceinline__ double seg_pow(const double* pw, int e) { return e > 0 ? pw[10] : pw[-e]; }  // T^e, e in [-9, 1]
+__device__ __forceinline__ double hess(const double* kc, const double* pw, int r, int c) {
+    return kc[kCH + r * 10 + c] * seg_pow(pw, (r % 5) + (c % 5) - 7);
+}
 // Per track, besides the segment scratch: (M+1) x 5 x 3 vertex values, (M+1) x 4 x 3
 // right-hand sides, M segment times and the block solve's lane exchange (kXch, in LDS).
 constexpr int kXch = 96;
@@ -163,42 +173,13 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ kc, const 
                                            double* scr, double* dv, double* rhs, double* Tm, double* xch,
                                            int* s_err, double* T_out, double* C_out) {
     const int tid = threadIdx.x;
-    // ---- phase 1: segment times, mapping inverses, fixed vertex values ----------
+    // ---- phase 1: segment times, powers of T, fixed vertex values ---------------
     for (int i = tid; i < M; i += BLOCK) {
         const double T = times_in ? times_in[i] : nfabian(P + 3 * i, P + 3 * (i + 1), vmax, amax);
         Tm[i] = T;
         if (T_out) T_out[i] = T;
         if (!(T > 0)) atomicOr(s_err, 1);  // CHECK_GT(segment_time, 0)  impl :297
     }
-    block_sync<SCR_LDS>();
-    for (int e = tid; e < M * kNPow; e += BLOCK) {  // the powers of T and 1/T
-        const int i = e / kNPow, k = e % kNPow;
-        const double T = Tm[i];
-        double p = 1.0;
-        if (k < 12) {
-            if (k > 0) p = T;
-            for (int q = 1; q < k; ++q) p = p * T;
-        } else if (k > 12) {
-            // 1/T: the hardware reciprocal refined by two Newton steps (~1e-16; a division
-            // would cost ~10 dependent instructions)
-            double it = __builtin_amdgcn_rcp(T);
-            it = fma(it, fma(-T, it, 1.0), it);
-            it = fma(it, fma(-T, it, 1.0), it);
-            p = it;
-            for (int q = 13; q < k; ++q) p = p * it;
-        }
-        scr[(size_t)i * Seg::kSize + Seg::kPow + k] = p;
-    }
-    block_sync<SCR_LDS>();
-    for (int e = tid; e < M * N * N; e += BLOCK) {
-        const int i = e / (N * N), r = (e % (N * N)) / N, c = e % N;
-        double* S = scr + (size_t)i * Seg::kSize;
-        S[Seg::kAinv + r * N + c] = ainv_entry(kc, S + Seg::kPow + 12, r, c);
-    }
-#ifdef EPP_REFIT_TL
-    block_sync<SCR_LDS>();
-    EPP_TL(9);
-#endif
     // start vertex {p0, v0, a0, 0, 0}, inner {p}, end {p, 0, 0, 0, 0}: makeStartOrEnd
     // (src/vertex.cpp:146-170) and trajectory_generator.cpp:28-50
     for (int e = tid; e < (M + 1) * 15; e += BLOCK) {
@@ -210,71 +191,52 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ kc, const 
         dv[e] = val;
     }
     block_sync<SCR_LDS>();
+    for (int e = tid; e < M * kNPow; e += BLOCK) {  // (1/T)^k, k = 0..9, and T
+        const int i = e / kNPow, k = e % kNPow;
+        const double T = Tm[i];
+        // 1/T: the hardware reciprocal refined by two Newton steps (~1e-16; a division
+        // would cost ~10 dependent instructions)
+        double it = __builtin_amdgcn_rcp(T);
+        it = fma(it, fma(-T, it, 1.0), it);
+        it = fma(it, fma(-T, it, 1.0), it);
+        double p = k == 10 ? T : 1.0;
+        for (int q = 0; q < k && k < 10; ++q) p = p * it;
+        scr[(size_t)i * Seg::kSize + Seg::kPow + k] = p;
+    }
+    block_sync<SCR_LDS>();
     EPP_TL(1);
     if (*s_err) return -2;
-    // ---- phase 2: Q (6x6 snap block), G = Q A^-1, H = A^-T G ------------------------
-    // computeQuadraticCostJacobian (impl :567-583): Q[9-r][9-c] = B[4][9-r] B[4][9-c] t^e 2/e
-    // (t^e by repeated products, e = 1..11: within a few ulp of pow, ~10x cheaper)
-    for (int e = tid; e < M * 36; e += BLOCK) {
-        const int i = e / 36, a = 4 + (e % 36) / 6, b = 4 + e % 6;
-        const int ex = a + b - 7;
-        double* S = scr + (size_t)i * Seg::kSize;
-        S[Seg::kQ + (a - 4) * 6 + (b - 4)] = kc[kCB + 4 * N + a] * kc[kCB + 4 * N + b] * S[Seg::kPow + ex] * 2.0 / (double)ex;
-    }
-    block_sync<SCR_LDS>();
-    EPP_TL(2);
-    for (int e = tid; e < M * 60; e += BLOCK) {
-        const int i = e / 60, a = (e % 60) / 10, c = e % 10;
-        double* S = scr + (size_t)i * Seg::kSize;
-        double g = 0.0;
-#pragma unroll
-        for (int b = 0; b < 6; ++b) g = g + S[Seg::kQ + a * 6 + b] * S[Seg::kAinv + (b + 4) * N + c];
-        S[Seg::kG + a * 10 + c] = g;
-    }
-    block_sync<SCR_LDS>();
-    EPP_TL(3);
-    // All 100 entries (no mirrored triangle): every row keeps the exact translation
-    // invariance H[r][0] == -H[r][5] that the reference's full product has.
-    for (int e = tid; e < M * 100; e += BLOCK) {
-        const int i = e / 100, r = (e % 100) / 10, c = e % 10;
-        double* S = scr + (size_t)i * Seg::kSize;
-        double h = 0.0;
-#pragma unroll
-        for (int a = 0; a < 6; ++a) h = h + S[Seg::kAinv + (a + 4) * N + r] * S[Seg::kG + a * 10 + c];
-        S[Seg::kH + r * N + c] = h;
-    }
-    block_sync<SCR_LDS>();
-    EPP_TL(4);
-    // ---- phase 3: block-tridiagonal system over the inner vertices ----------------
+    // ---- phase 2: block-tridiagonal system over the inner vertices ----------------
     // free variable (v, p): vertex v in 1..M-1, derivative p+1.  Diagonal block D_v is
     // kept in the L slot of segment v-1, the coupling E_v (v -> v+1) in the W slot.
+    // Segment i's H (closed form, hess) couples vertex i (rows 0..4) and i+1 (rows 5..9).
     const int nin = M - 1;
     for (int e = tid; e < nin * 16; e += BLOCK) {
         const int v = 1 + e / 16, p = (e % 16) / 4, q = e % 4;
-        const double* Hm = scr + (size_t)(v - 1) * Seg::kSize + Seg::kH;
-        const double* Hp = scr + (size_t)v * Seg::kSize + Seg::kH;
-        scr[(size_t)(v - 1) * Seg::kSize + Seg::kL + p * 4 + q] = Hm[(6 + p) * N + 6 + q] + Hp[(1 + p) * N + 1 + q];
-        scr[(size_t)(v - 1) * Seg::kSize + Seg::kW + p * 4 + q] = (v < nin) ? Hp[(1 + p) * N + 6 + q] : 0.0;
+        const double* pm = scr + (size_t)(v - 1) * Seg::kSize + Seg::kPow;
+        const double* pp = scr + (size_t)v * Seg::kSize + Seg::kPow;
+        scr[(size_t)(v - 1) * Seg::kSize + Seg::kL + p * 4 + q] = hess(kc, pm, 6 + p, 6 + q) + hess(kc, pp, 1 + p, 1 + q);
+        scr[(size_t)(v - 1) * Seg::kSize + Seg::kW + p * 4 + q] = (v < nin) ? hess(kc, pp, 1 + p, 6 + q) : 0.0;
     }
     for (int e = tid; e < nin * 12; e += BLOCK) {
         const int v = 1 + e / 12, p = (e % 12) / 3, d = e % 3;
         double s = 0.0;
         // segment v-1: rows 0..4 = vertex v-1, rows 5..9 = vertex v; row of (v,p+1) = 6+p
         {
-            const double* H = scr + (size_t)(v - 1) * Seg::kSize + Seg::kH;
+            const double* pw = scr + (size_t)(v - 1) * Seg::kSize + Seg::kPow;
             for (int r = 0; r < N; ++r) {
                 const int vv = (r < HALF) ? v - 1 : v, k = r % HALF;
                 const bool fixed = (k == 0) || vv == 0 || vv == M;
-                if (fixed) s = s + H[(6 + p) * N + r] * dv[(vv * HALF + k) * 3 + d];
+                if (fixed) s = s + hess(kc, pw, 6 + p, r) * dv[(vv * HALF + k) * 3 + d];
             }
         }
         // segment v: rows 0..4 = vertex v (row of (v,p+1) = 1+p), rows 5..9 = vertex v+1
         {
-            const double* H = scr + (size_t)v * Seg::kSize + Seg::kH;
+            const double* pw = scr + (size_t)v * Seg::kSize + Seg::kPow;
             for (int r = 0; r < N; ++r) {
                 const int vv = (r < HALF) ? v : v + 1, k = r % HALF;
                 const bool fixed = (k == 0) || vv == 0 || vv == M;
-                if (fixed) s = s + H[(1 + p) * N + r] * dv[(vv * HALF + k) * 3 + d];
+                if (fixed) s = s + hess(kc, pw, 1 + p, r) * dv[(vv * HALF + k) * 3 + d];
             }
         }
         rhs[(v * 4 + p) * 3 + d] = -s;
@@ -282,7 +244,7 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ kc, const 
     block_sync<SCR_LDS>();
     EPP_TL(5);
     EPP_TLC(14);
-    // ---- phase 4: block-tridiagonal solve (block Thomas, lanes over the block entries) ---
+    // ---- phase 3: block-tridiagonal solve (block Thomas, lanes over the block entries) ---
     // Inner vertices v = 1..nin, diagonal blocks D_v, couplings E_v (v -> v+1), right-hand
     // sides b_v (3 columns):
     //   S_1 = D_1, y_1 = b_1;  G_v = S_v^-1 E_v, g_v = S_v^-1 y_v;
@@ -422,14 +384,23 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ kc, const 
     EPP_TL(6);
     EPP_TLC(15);
     if (*s_err) return -3;
-    // ---- phase 5: p_i = A_i^-1 [d_i ; d_{i+1}] -------------------------------------
+    // ---- phase 4: p_i = A_i^-1 [d_i ; d_{i+1}] -------------------------------------
     for (int e = tid; e < M * 30; e += BLOCK) {
         const int i = e / 30, d = (e % 30) / 10, r = e % 10;
-        const double* Ai = scr + (size_t)i * Seg::kSize + Seg::kAinv;
-        double s = 0.0;
-        for (int k = 0; k < N; ++k) {
-            const int v = i + (k >= HALF ? 1 : 0);
-            s = s + Ai[r * N + k] * dv[(v * HALF + (k % HALF)) * 3 + d];
+        const double* ipow = scr + (size_t)i * Seg::kSize + Seg::kPow;
+        const double* d0 = dv + (size_t)i * HALF * 3 + d;  // vertex i's values, then vertex i+1's
+        double s;
+        if (r < HALF) {  // rows 0..4 of A^-1: diag(1 / r!)
+            s = kc[kCF + r] * d0[3 * r];
+        } else {  // rows 5..9: [K | B5^-1] row rr, column c scaled by (1/T)^(rr + 5 - c % 5)
+            const int rr = r - HALF;
+            s = 0.0;
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                const double a = (k < HALF ? kc[kCK + rr * HALF + k] : kc[kCB5 + rr * HALF + k - HALF]) *
+                                 ipow[rr + HALF - k % HALF];
+                s = s + a * d0[3 * k];
+            }
         }
         C_out[((size_t)i * 3 + d) * N + r] = s;
     }
@@ -859,6 +830,34 @@ epp_status ensure_consts() {
         }
     const double inv_fact[HALF] = {1.0, 1.0, 1.0 / 2.0, 1.0 / 6.0, 1.0 / 24.0};
     for (int r = 0; r < HALF; ++r) cc[kCF + r] = inv_fact[r];
+    // Hc (see hess): the constant parts of rows 4..9 of A^-1 (ainv_entry) and of Q's snap
+    // block (B[4][a] B[4][b] 2 / (a+b-7), impl :567-583), multiplied out in long double
+    long double Ac[N][N] = {}, Qc[N][N] = {};
+    Ac[4][4] = 1.0L / 24.0L;
+    for (int a = HALF; a < N; ++a)
+        for (int c = 0; c < N; ++c) {
+            const int rr = a - HALF;
+            long double kv = 0.0L;
+            if (c < HALF) {
+                long double f = 1.0L;
+                for (int q = 2; q <= c; ++q) f *= q;
+                for (int k = 0; k <= c; ++k) kv += G[rr][HALF + k] * (long double)B[k][c];
+                kv = -kv / f;
+            } else {
+                kv = G[rr][HALF + c - HALF];
+            }
+            Ac[a][c] = kv;
+        }
+    for (int a = 4; a < N; ++a)
+        for (int b = 4; b < N; ++b)
+            Qc[a][b] = (long double)B[4][a] * (long double)B[4][b] * 2.0L / (long double)(a + b - 7);
+    for (int r = 0; r < N; ++r)
+        for (int c = 0; c < N; ++c) {
+            long double h = 0.0L;
+            for (int a = 4; a < N; ++a)
+                for (int b = 4; b < N; ++b) h += Ac[a][r] * Qc[a][b] * Ac[b][c];
+            cc[kCH + r * N + c] = (double)h;
+        }
     hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(cC), cc, sizeof(cc));
     if (e != hipSuccess) {
         set_error(std::string("epp minsnap: constants: ") + hipGetErrorString(e));

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <vector>
 #include <cstdio>
@@ -241,75 +242,127 @@ __global__ void k_knn_count(const double* __restrict__ nodes, int n, const KnnGr
     atomicAdd(&cnt[c], 1);
 }
 
-// exclusive scan of cnt[0..ncell) into start[0..ncell], one block: every thread loads a
-// run of kScanPer consecutive counts at once (16-byte loads, all in flight together: one
-// global round trip per tile instead of staging tiles through LDS), wave scans of the run
-// sums (shuffles), wave totals in LDS; the carry runs across tiles (one tile at ~64k
-// nodes: 1024 x 48 cells)
-constexpr int kScanPer = 48;
-__global__ __launch_bounds__(kBoundsThreads) void k_knn_scan(const KnnGrid* __restrict__ gp,
-                                                             const int* __restrict__ cnt,
-                                                             int* __restrict__ start) {
-    constexpr int kScanTile = kScanPer * kBoundsThreads;
-    static_assert(kScanPer % 4 == 0, "16-byte runs");
-    __shared__ int wsum[kBoundsThreads / 64];
-    const int nc = gp->ncell;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int carry = 0;
-    for (int t0 = 0; t0 < nc; t0 += kScanTile) {  // block-uniform
-        const int b0 = t0 + kScanPer * threadIdx.x;
-        int v[kScanPer];
-        if (b0 + kScanPer <= nc) {  // (cnt and start are 256-byte aligned, b0 a multiple of 4)
-#pragma unroll
-            for (int u = 0; u < kScanPer / 4; ++u) {
-                const int4 q = reinterpret_cast<const int4*>(cnt + b0)[u];
-                v[4 * u] = q.x;
-                v[4 * u + 1] = q.y;
-                v[4 * u + 2] = q.z;
-                v[4 * u + 3] = q.w;
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < kScanPer; ++u) v[u] = b0 + u < nc ? cnt[b0 + u] : 0;
+// ---- decoupled look-back (single-pass ordered scans) ---------------------------------
+// A block publishes its chunk's total as soon as it has counted it ("aggregate"), then
+// its inclusive prefix once it knows its exclusive one.  Its look-back reads the status
+// words of the 64 blocks before it at once (one lane each), waits for every one of them to
+// be published in this launch, and sums back to the nearest inclusive prefix -- no
+// block waits on a chain of predecessors (they publish their aggregates without waiting).
+// Status word: [63..40] launch tag (24 bits, never 0), [39] inclusive flag, [38..0] value.
+// Tags make stale words of earlier launches invisible: the workspace needs no clearing.
+// Blocks only wait on lower-numbered blocks, which are dispatched first, so the wait
+// always ends.
+constexpr int kTagShift = 40;
+constexpr unsigned long long kIncl = 1ull << 39, kValMask = kIncl - 1ull;
+std::atomic<uint32_t> g_scan_tag{0};
+uint32_t next_scan_tag() {
+    uint32_t t;
+    do t = (g_scan_tag.fetch_add(1, std::memory_order_relaxed) + 1u) & 0xffffffu;
+    while (t == 0u);
+    return t;
+}
+__device__ __forceinline__ void lb_publish(unsigned long long* st, int b, uint32_t tag, bool incl, long long v) {
+    const unsigned long long w = ((unsigned long long)tag << kTagShift) | (incl ? kIncl : 0ull) | ((unsigned long long)v & kValMask);
+    __hip_atomic_store(st + b, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Exclusive prefix of block b (called by one whole wavefront; every lane gets it).
+__device__ __forceinline__ long long lb_exclusive(unsigned long long* st, int b, uint32_t tag) {
+    const int lane = threadIdx.x & 63;
+    long long acc = 0;
+    for (int hi = b - 1; hi >= 0; hi -= 64) {  // window [hi - 63, hi], lane l reads block hi - l
+        const int j = hi - lane;
+        unsigned long long w = 0ull;
+        if (j >= 0) {
+            do w = __hip_atomic_load(st + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            while ((uint32_t)(w >> kTagShift) != tag);
         }
-        int sum = 0;
-#pragma unroll
-        for (int u = 0; u < kScanPer; ++u) sum += v[u];
-        int incl = sum;
-        for (int o = 1; o < 64; o <<= 1) {
-            const int t = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += t;
-        }
-        if (lane == 63) wsum[wv] = incl;
-        __syncthreads();
-        int wbase = 0, tile = 0;
-        for (int w = 0; w < kBoundsThreads / 64; ++w) {
-            wbase += w < wv ? wsum[w] : 0;
-            tile += wsum[w];
-        }
-        int acc = carry + wbase + incl - sum;
-        if (b0 + kScanPer <= nc) {
-#pragma unroll
-            for (int u = 0; u < kScanPer / 4; ++u) {
-                int4 q;
-                q.x = acc;
-                q.y = q.x + v[4 * u];
-                q.z = q.y + v[4 * u + 1];
-                q.w = q.z + v[4 * u + 2];
-                acc = q.w + v[4 * u + 3];
-                reinterpret_cast<int4*>(start + b0)[u] = q;
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < kScanPer; ++u) {
-                if (b0 + u < nc) start[b0 + u] = acc;
-                acc += v[u];
-            }
-        }
-        carry += tile;
-        __syncthreads();  // wsum is rewritten by the next tile
+        const unsigned long long pm = __ballot(j >= 0 && (w & kIncl));
+        // the nearest inclusive prefix (lowest lane with one) ends the walk
+        const int stop = pm ? __builtin_ctzll(pm) : 64;
+        long long v = (lane <= stop && j >= 0) ? (long long)(w & kValMask) : 0ll;
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        acc += v;
+        if (pm) break;
     }
-    if (threadIdx.x == 0) start[nc] = carry;
+    return acc;
+}
+
+// exclusive scan of cnt[0..ncell) into start[0..ncell]: block b scans cells
+// [b kScanTile, (b+1) kScanTile), 16 consecutive counts per thread (16-byte loads and
+// stores), its offset by look-back (lb_exclusive).  The grid is
+// sized for the largest possible cell count (the count itself is on the device); blocks
+// past it exit (no block waits on a later one).
+constexpr int kScanThreads = 256, kScanPer = 16, kScanTile = kScanThreads * kScanPer;
+__global__ __launch_bounds__(kScanThreads) void k_knn_scan(const KnnGrid* __restrict__ gp,
+                                                           const int* __restrict__ cnt,
+                                                           int* __restrict__ start,
+                                                           unsigned long long* __restrict__ st, uint32_t tag) {
+    static_assert(kScanPer % 4 == 0, "16-byte runs");
+    __shared__ int wsum[kScanThreads / 64];
+    __shared__ int s_excl;
+    const int nc = gp->ncell;
+    const int b = blockIdx.x;
+    if (b * kScanTile > nc) return;  // (block-uniform; the block holding nc itself writes start[nc])
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int b0 = b * kScanTile + kScanPer * threadIdx.x;
+    int v[kScanPer];
+    if (b0 + kScanPer <= nc) {  // (cnt and start are 256-byte aligned, b0 a multiple of 16)
+#pragma unroll
+        for (int u = 0; u < kScanPer / 4; ++u) {
+            const int4 q = reinterpret_cast<const int4*>(cnt + b0)[u];
+            v[4 * u] = q.x;
+            v[4 * u + 1] = q.y;
+            v[4 * u + 2] = q.z;
+            v[4 * u + 3] = q.w;
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < kScanPer; ++u) v[u] = b0 + u < nc ? cnt[b0 + u] : 0;
+    }
+    int sum = 0;
+#pragma unroll
+    for (int u = 0; u < kScanPer; ++u) sum += v[u];
+    int incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int wbase = 0, tile = 0;
+#pragma unroll
+    for (int w = 0; w < kScanThreads / 64; ++w) {
+        wbase += w < wv ? wsum[w] : 0;
+        tile += wsum[w];
+    }
+    if (wv == 0) {
+        if (lane == 0) lb_publish(st, b, tag, b == 0, tile);
+        const long long ex = b == 0 ? 0ll : lb_exclusive(st, b, tag);
+        if (lane == 0) {
+            if (b > 0) lb_publish(st, b, tag, true, ex + tile);
+            s_excl = (int)ex;
+        }
+    }
+    __syncthreads();
+    int acc = s_excl + wbase + incl - sum;
+    if (b0 + kScanPer <= nc) {
+#pragma unroll
+        for (int u = 0; u < kScanPer / 4; ++u) {
+            int4 q;
+            q.x = acc;
+            q.y = q.x + v[4 * u];
+            q.z = q.y + v[4 * u + 1];
+            q.w = q.z + v[4 * u + 2];
+            acc = q.w + v[4 * u + 3];
+            reinterpret_cast<int4*>(start + b0)[u] = q;
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < kScanPer; ++u) {
+            if (b0 + u <= nc) start[b0 + u] = acc;  // (b0 + u == nc: the total)
+            acc += v[u];
+        }
+    }
 }
 
 __global__ void k_knn_scatter(const double* __restrict__ nodes, int n, const int* __restrict__ cell_of,
@@ -989,10 +1042,11 @@ __global__ void k_knn_edges(const double* __restrict__ nodes, const int32_t* __r
 }
 
 // Scratch of the grid k-NN, every part 256-byte aligned: grid params | bounds partials | cell_of[n] |
-// sidx[n] | sxyz[3n] | cnt[cap+1] | fill[cap+1] | start[cap+1] | retry bounds[n]  (cap = max(64, n))
+// sidx[n] | sxyz[3n] | cnt[cap+1] | fill[cap+1] | start[cap+1] | retry bounds[n] | scan
+// status words  (cap = max(64, n))
 struct KnnLayout {
-    size_t part, cell, sidx, sxyz, cnt, start, fill, rbnd, bytes;
-    int cap;
+    size_t part, cell, sidx, sxyz, cnt, start, fill, rbnd, stat, bytes;
+    int cap, scan_blocks;
 };
 KnnLayout knn_layout(int n) {
     auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
@@ -1006,7 +1060,9 @@ KnnLayout knn_layout(int n) {
     L.fill = L.cnt + al((size_t)(L.cap + 1) * 4);
     L.start = L.fill + al((size_t)(L.cap + 1) * 4);
     L.rbnd = L.start + al((size_t)(L.cap + 1) * 4);
-    L.bytes = L.rbnd + al((size_t)std::max(n, 1) * 8);
+    L.stat = L.rbnd + al((size_t)std::max(n, 1) * 8);
+    L.scan_blocks = (L.cap + 1 + kScanTile) / kScanTile;  // cells <= cap; start[ncell] too
+    L.bytes = L.stat + al((size_t)L.scan_blocks * 8);
     return L;
 }
 
@@ -1053,7 +1109,8 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
         hipLaunchKernelGGL(k_knn_setup, dim3(1), dim3(64), 0, s, part, nb, n, L.cap, npc, g);
     }
     hipLaunchKernelGGL(k_knn_count, g256, b256, 0, s, nodes, n, g, cell_of, cnt);
-    hipLaunchKernelGGL(k_knn_scan, dim3(1), dim3(kBoundsThreads), 0, s, g, cnt, start);
+    hipLaunchKernelGGL(k_knn_scan, dim3(L.scan_blocks), dim3(kScanThreads), 0, s, g, cnt, start,
+                       reinterpret_cast<unsigned long long*>(buf + L.stat), next_scan_tag());
     hipLaunchKernelGGL(k_knn_scatter, g256, b256, 0, s, nodes, n, cell_of, start, fill, sxyz, sidx);
     // EPP_KNN_TILE=0 selects the untiled grid walk (same answer; a test hook); the product
     // accepts only {0, 1}.  The timing ablations and the per-block dump exist only in a
@@ -1101,71 +1158,69 @@ CachedWs g_knn_ws[64];
 CachedWs g_compact_ws[64];
 
 // ---- ordered compaction of the valid states ----------------------------------------
-// Chunks of kCompactChunk states per block: (1) per-block counts, (2) one block scans the
-// counts, (3) every block writes its valid states at its offset in index order (wave
-// ballots + per-wave counts in LDS).  Deterministic: the planner's node order (and with
+// One pass: block b owns states [b C, (b+1) C) (C = kCompactChunk) in kCompactRounds rounds
+// of one state per thread (coalesced flag loads and row copies); ranks from wave ballots
+// and the per-(round, wave) counts in LDS, the block's offset by look-back.  The valid
+// states are written in index order.  Deterministic: the planner's node order (and with
 // it k-NN tie breaks and the search) does not depend on scheduling.
 constexpr int kCompactThreads = 256;
-constexpr int kCompactChunk = 4096;
+constexpr int kCompactRounds = 4;
+constexpr int kCompactChunk = kCompactThreads * kCompactRounds;
 
-__global__ __launch_bounds__(kCompactThreads) void k_compact_count(const uint8_t* __restrict__ valid, int64_t n,
-                                                                   int* __restrict__ counts) {
-    __shared__ int ws[kCompactThreads / 64];
-    const int64_t b0 = (int64_t)blockIdx.x * kCompactChunk;
-    int c = 0;
-    for (int j = threadIdx.x; j < kCompactChunk; j += kCompactThreads) {
-        const int64_t i = b0 + j;
-        c += (i < n && valid[i]) ? 1 : 0;
-    }
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int t = 0;
-        for (int w = 0; w < kCompactThreads / 64; ++w) t += ws[w];
-        counts[blockIdx.x] = t;
-    }
-}
-
-__global__ void k_compact_scan(int* __restrict__ counts, int nb, int64_t* __restrict__ n_out) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    int64_t acc = 0;
-    for (int b = 0; b < nb; ++b) {
-        const int c = counts[b];
-        counts[b] = (int)acc;
-        acc += c;
-    }
-    *n_out = acc;
-}
-
-__global__ __launch_bounds__(kCompactThreads) void k_compact_scatter(const double* __restrict__ xyz,
-                                                                     const uint8_t* __restrict__ valid, int64_t n,
-                                                                     const int* __restrict__ offsets,
-                                                                     double* __restrict__ out) {
-    __shared__ int wcnt[kCompactThreads / 64];
+__global__ __launch_bounds__(kCompactThreads) void k_compact(const double* __restrict__ xyz,
+                                                             const uint8_t* __restrict__ valid, int64_t n,
+                                                             unsigned long long* __restrict__ st, uint32_t tag,
+                                                             double* __restrict__ out, int64_t* __restrict__ n_out) {
+    constexpr int NW = kCompactThreads / 64;
+    __shared__ int wcnt[kCompactRounds * NW];
+    __shared__ long long s_excl;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t b0 = (int64_t)blockIdx.x * kCompactChunk;
-    int64_t base = offsets[blockIdx.x];
-    for (int j0 = 0; j0 < kCompactChunk; j0 += kCompactThreads) {  // block-uniform rounds, index order
-        const int64_t i = b0 + j0 + threadIdx.x;
-        const bool v = i < n && valid[i];
-        const unsigned long long bal = __ballot(v);
-        if (lane == 0) wcnt[wv] = __popcll(bal);
-        __syncthreads();
-        int before = 0, total = 0;
-        for (int w = 0; w < kCompactThreads / 64; ++w) {
-            before += w < wv ? wcnt[w] : 0;
-            total += wcnt[w];
+    const int b = blockIdx.x;
+    const int64_t i0 = (int64_t)b * kCompactChunk + threadIdx.x;
+    bool v[kCompactRounds];
+    unsigned long long bal[kCompactRounds];
+#pragma unroll
+    for (int r = 0; r < kCompactRounds; ++r) {
+        const int64_t i = i0 + r * kCompactThreads;
+        v[r] = i < n && valid[i] != 0;
+    }
+#pragma unroll
+    for (int r = 0; r < kCompactRounds; ++r) {
+        bal[r] = __ballot(v[r]);
+        if (lane == 0) wcnt[r * NW + wv] = __popcll(bal[r]);
+    }
+    __syncthreads();
+    // (round, wave) slots in index order: round-major
+    int before[kCompactRounds], total = 0;
+#pragma unroll
+    for (int q = 0; q < kCompactRounds * NW; ++q) {
+#pragma unroll
+        for (int r = 0; r < kCompactRounds; ++r)
+            if (q == r * NW + wv) before[r] = total;
+        total += wcnt[q];
+    }
+    if (wv == 0) {
+        if (lane == 0) lb_publish(st, b, tag, b == 0, total);
+        const long long ex = b == 0 ? 0ll : lb_exclusive(st, b, tag);
+        if (lane == 0) {
+            if (b > 0) lb_publish(st, b, tag, true, ex + total);
+            s_excl = ex;
+            if (b == (int)gridDim.x - 1) *n_out = ex + total;
         }
-        if (v) {
-            const int64_t p = base + before + (int64_t)__builtin_amdgcn_mbcnt_hi(
-                                                     (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+    }
+    __syncthreads();
+    const long long ex = s_excl;
+#pragma unroll
+    for (int r = 0; r < kCompactRounds; ++r) {
+        if (v[r]) {
+            const int64_t i = i0 + r * kCompactThreads;
+            const int64_t p = ex + before[r] +
+                              (int64_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal[r] >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)bal[r], 0u));
             out[3 * p] = xyz[3 * i];
             out[3 * p + 1] = xyz[3 * i + 1];
             out[3 * p + 2] = xyz[3 * i + 2];
         }
-        base += total;
-        __syncthreads();  // wcnt is rewritten next round
     }
 }
 
@@ -1354,41 +1409,35 @@ epp_status epp_compact_states(const double* xyz, const uint8_t* valid, int64_t n
         return EPP_ERR_INVALID_ARGUMENT;
     }
     hipStream_t s = (hipStream_t)stream;
-    const int nb = (int)std::max<int64_t>(1, (n + kCompactChunk - 1) / kCompactChunk);
-    int* counts = nullptr;
-    // the per-block counts live in the cached k-NN workspace's device (small, stream-ordered use)
+    // the look-back status words live in a cached per-device workspace (stream-ordered reuse)
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
     CachedWs& c = g_compact_ws[dev & 63];
     std::lock_guard<std::mutex> lk(c.mu);
-    hipError_t e = hipSuccess;
-    e = c.acquire(s, (size_t)nb * 4);
+    hipError_t e = c.acquire(s, (size_t)epp_compact_workspace_size(n));
     if (e != hipSuccess) {
         set_error(std::string("epp_compact_states: workspace: ") + hipGetErrorString(e));
         return EPP_ERR_HIP;
     }
-    counts = static_cast<int*>(c.buf);
-    const epp_status rc = epp_compact_states_ws(xyz, valid, n, out, n_out, counts, c.cap, stream);
+    const epp_status rc = epp_compact_states_ws(xyz, valid, n, out, n_out, c.buf, c.cap, stream);
     c.release(s);
     return rc;
 }
 
 uint64_t epp_compact_workspace_size(int64_t n) {
-    return n <= 0 ? 4 : (uint64_t)((n + kCompactChunk - 1) / kCompactChunk) * 4;
+    return n <= 0 ? 8 : (uint64_t)((n + kCompactChunk - 1) / kCompactChunk) * 8;
 }
 
 epp_status epp_compact_states_ws(const double* xyz, const uint8_t* valid, int64_t n, double* out, int64_t* n_out,
                                  void* ws, uint64_t ws_bytes, void* stream) {
-    if (n < 0 || !n_out || (n > 0 && (!xyz || !valid || !out)) || !ws || ws_bytes < epp_compact_workspace_size(n)) {
+    if (n < 0 || !n_out || (n > 0 && (!xyz || !valid || !out)) || !ws || ws_bytes < epp_compact_workspace_size(n) ||
+        (reinterpret_cast<uintptr_t>(ws) & 7)) {
         set_error("epp_compact_states: invalid argument");
         return EPP_ERR_INVALID_ARGUMENT;
     }
-    hipStream_t s = (hipStream_t)stream;
     const int nb = (int)std::max<int64_t>(1, (n + kCompactChunk - 1) / kCompactChunk);
-    int* counts = static_cast<int*>(ws);
-    hipLaunchKernelGGL(k_compact_count, dim3(nb), dim3(kCompactThreads), 0, s, valid, n, counts);
-    hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(64), 0, s, counts, nb, n_out);
-    hipLaunchKernelGGL(k_compact_scatter, dim3(nb), dim3(kCompactThreads), 0, s, xyz, valid, n, counts, out);
+    hipLaunchKernelGGL(k_compact, dim3(nb), dim3(kCompactThreads), 0, (hipStream_t)stream, xyz, valid, n,
+                       static_cast<unsigned long long*>(ws), next_scan_tag(), out, n_out);
     return last("epp_compact_states");
 }
 

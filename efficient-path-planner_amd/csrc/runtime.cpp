@@ -56,6 +56,16 @@ epp_status epp_memcpy_d2h(void* dst, const void* src, uint64_t bytes, void* stre
     EPP_HIP_RET(hipStreamSynchronize((hipStream_t)stream));
     return EPP_OK;
 }
+epp_status epp_memcpy_h2d_async(void* dst, const void* src, uint64_t bytes, void* stream) {
+    if (!bytes) return EPP_OK;
+    EPP_HIP_RET(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+    return EPP_OK;
+}
+epp_status epp_memcpy_d2h_async(void* dst, const void* src, uint64_t bytes, void* stream) {
+    if (!bytes) return EPP_OK;
+    EPP_HIP_RET(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+    return EPP_OK;
+}
 epp_status epp_memset(void* dst, int value, uint64_t bytes, void* stream) {
     if (!bytes) return EPP_OK;
     EPP_HIP_RET(hipMemsetAsync(dst, value, bytes, (hipStream_t)stream));

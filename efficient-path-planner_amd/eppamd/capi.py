@@ -51,6 +51,8 @@ def lib() -> C.CDLL:
             "epp_free": (i32, [vp]),
             "epp_memcpy_h2d": (i32, [vp, vp, u64, vp]),
             "epp_memcpy_d2h": (i32, [vp, vp, u64, vp]),
+            "epp_memcpy_h2d_async": (i32, [vp, vp, u64, vp]),
+            "epp_memcpy_d2h_async": (i32, [vp, vp, u64, vp]),
             "epp_memset": (i32, [vp, C.c_int, u64, vp]),
             "epp_stream_create": (i32, [C.POINTER(vp)]),
             "epp_stream_destroy": (i32, [vp]),
@@ -127,7 +129,7 @@ def lib() -> C.CDLL:
 # every symbol include/epp.h declares (the CPU test checks the library exports them)
 EXPORTED = [
     "epp_last_error", "epp_version", "epp_device_count", "epp_set_device", "epp_malloc", "epp_free",
-    "epp_memcpy_h2d", "epp_memcpy_d2h", "epp_memset", "epp_stream_create", "epp_stream_destroy",
+    "epp_memcpy_h2d", "epp_memcpy_d2h", "epp_memcpy_h2d_async", "epp_memcpy_d2h_async", "epp_memset", "epp_stream_create", "epp_stream_destroy",
     "epp_stream_sync", "epp_device_sync", "epp_event_create", "epp_event_destroy", "epp_event_record",
     "epp_event_elapsed_ms", "epp_build_obbs", "epp_world_create", "epp_world_update",
     "epp_world_destroy", "epp_world_num_obbs", "epp_world_get_aabbs", "epp_check_states",

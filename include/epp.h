@@ -80,6 +80,11 @@ epp_status epp_malloc(void** ptr, uint64_t bytes);
 epp_status epp_free(void* ptr);
 epp_status epp_memcpy_h2d(void* dst, const void* src, uint64_t bytes, void* stream);
 epp_status epp_memcpy_d2h(void* dst, const void* src, uint64_t bytes, void* stream);
+/* Stream-ordered copies that return without waiting (epp_memcpy_* above synchronise the
+ * stream); the host side should be pinned (page-locked) memory and must stay
+ * untouched until the stream is synchronised. */
+epp_status epp_memcpy_h2d_async(void* dst, const void* src, uint64_t bytes, void* stream);
+epp_status epp_memcpy_d2h_async(void* dst, const void* src, uint64_t bytes, void* stream);
 epp_status epp_memset(void* dst, int value, uint64_t bytes, void* stream);
 epp_status epp_stream_create(void** stream);
 epp_status epp_stream_destroy(void* stream);

@@ -10,7 +10,8 @@ import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "efficient-path-planner_amd")]
+# EPP_PKG: another build of the package (scripts/ab_pkg.sh) for a same-box A/B
+sys.path[:0] = [ROOT, os.environ.get("EPP_PKG") or os.path.join(ROOT, "efficient-path-planner_amd")]
 
 if len(sys.argv) > 1 and sys.argv[1] == "--child":
     import numpy as np
@@ -35,7 +36,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
         ts.append((time.perf_counter() - t) * 1e3)
         st.append(otg.planner_stats())
     os.unlink(path)
-    print(f"threads {os.environ.get('EPP_PLAN_THREADS', '4')} writer {os.environ.get('EPP_PATH_WRITER', '1')}: pre_compute_traj p50 {np.median(ts):.2f} ms "
+    print(f"{os.path.basename(os.environ.get('EPP_PKG', '') or 'cur')} threads {os.environ.get('EPP_PLAN_THREADS', '4')} writer {os.environ.get('EPP_PATH_WRITER', '1')}: pre_compute_traj p50 {np.median(ts):.2f} ms "
           f"(mean {np.mean(ts):.2f}, min {min(ts):.2f}); planner: ms {np.median([s['ms'] for s in st]):.2f}, device sum "
           f"{np.median([s['ms_device'] for s in st]):.2f}, search sum {np.median([s['ms_search'] for s in st]):.2f}",
           flush=True)

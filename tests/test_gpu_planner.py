@@ -115,6 +115,14 @@ def test_knn_tile_crowded_halo(k, tile, monkeypatch):
     assert np.array_equal(got, capi.knn(nodes, k, method="brute"))
 
 
+def test_knn_grid_many_scan_blocks():
+    """300k nodes: the cell-count scan spans ~70 look-back blocks (more than one 64-block
+    window); the grid table equals the all-pairs one."""
+    nodes = synth.sample_states(321, [-6, -6, 0], [6, 6, 2], 300_000)
+    got = capi.knn(nodes, 8, method="grid_ws")
+    assert np.array_equal(got, capi.knn(nodes, 8, method="brute"))
+
+
 def test_knn_grid_back_to_back_streams():
     """Cached-workspace reuse is ordered on the GPU: grid k-NN launched on two streams and
     repeatedly without host syncs in between gives the synchronous answer every time."""
@@ -516,9 +524,10 @@ def test_vector_and_matrix_helpers():
     assert m.shape == (2, 3) and np.array_equal(np.asarray(m), np.arange(6.0).reshape(2, 3))
 
 
-@pytest.mark.parametrize("n", [1, 4095, 4096, 65536, 100_003])
+@pytest.mark.parametrize("n", [1, 15, 4095, 4096, 65536, 100_003, 1_000_003])
 def test_compact_states_ordered(n):
-    """Ordered compaction (the planner's node list): same rows, same order as numpy."""
+    """Ordered compaction (the planner's node list): same rows, same order as numpy.  The
+    single-pass kernel's look-back crosses several 64-block windows at 1M states."""
     xyz = synth.sample_states(12, [-6, -6, 0], [6, 6, 2], n)
     valid = (np.random.RandomState(n).rand(n) < 0.9).astype(np.uint8)
     assert np.array_equal(capi.compact_states(xyz, valid), xyz[valid.astype(bool)])
@@ -746,7 +755,7 @@ def test_online_replan_equals_cpu_restatement(tmp_path, track, geom, recalc):
     assert replans >= 1 and cpu.calls == 9 + 2 * replans  # each replan took two planner calls
 
 
-def test_online_update_during_replan_keeps_reference_returns(tmp_path, track, geom):
+def test_online_update_during_replan_keeps_reference_returns(tmp_path, track, geom, monkeypatch):
     """While an online recomputation runs (recalculate_online), another gate's update gets
     the reference's answer: the gate is recorded and checked against the world with the
     new pose, False when the current trajectory stays valid and passing, the reference's
@@ -759,7 +768,9 @@ def test_online_update_during_replan_keeps_reference_returns(tmp_path, track, ge
     path, c, gates, obstacles, start, goal = track
     c2 = json.loads(json.dumps(c))
     c2["path_planner_properties"]["recalculate_online"] = True
-    c2["path_planner_properties"]["samples_fmt"] = 1 << 20  # a replan of ~10 ms: still running below
+    # the worker is held 3 s before it plans (test hook): the calls below all arrive while
+    # the recomputation is still going on, however fast it is
+    monkeypatch.setenv("EPP_TEST_REPLAN_HOLD_MS", "3000")
     p2 = tmp_path / "c_busy.json"
     p2.write_text(json.dumps(c2))
     otg = _ot().OnlineTrajGenerator(start, goal, gates, obstacles, str(p2))
