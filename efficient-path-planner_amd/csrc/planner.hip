@@ -612,6 +612,70 @@ __device__ __forceinline__ void knn_retry_wave(const KnnGrid& g, double r2max, c
     const int rmax = max(g.dims[0], max(g.dims[1], g.dims[2]));
     const double p[3] = {nodes[3 * (int64_t)self], nodes[3 * (int64_t)self + 1], nodes[3 * (int64_t)self + 2]};
     const int c[3] = {knn_cell_axis(p[0], g, 0), knn_cell_axis(p[1], g, 1), knn_cell_axis(p[2], g, 2)};
+    if (bound2 < 1e299) {  // wave-uniform
+        // K actual candidates lie within sqrt(bound2) (the tile pass found them, with the
+        // same exact distances), so the true top K is among the candidates with
+        // d <= bound2 in the box p +- sqrt(bound2) (cell mapping monotone; the radius is
+        // padded against the rounding of p +- r).  Rows of the box are spread over the
+        // lanes; every candidate within the bound goes to an LDS list (a few dozen), and
+        // each listed entry's rank in (distance, index) order is counted against the whole
+        // list: the K lowest ranks are the answer.  No per-lane sorted lists, no merge
+        // rounds.  (A list over capacity falls through to the per-lane walk below.)
+        constexpr int kCap = 512;
+        __shared__ double s_d[kCap];
+        __shared__ int s_j[kCap];
+        __shared__ int s_n;
+        if (lane == 0) s_n = 0;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the clear before any append
+        const double r = sqrt(bound2) * (1.0 + 1e-9) + 1e-12 * (1.0 + fabs(p[0]) + fabs(p[1]) + fabs(p[2]));
+        int lo[3], hi[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            lo[d] = knn_cell_axis(p[d] - r, g, d);
+            hi[d] = knn_cell_axis(p[d] + r, g, d);
+        }
+        const int ny = hi[1] - lo[1] + 1, nz = hi[2] - lo[2] + 1;
+        for (int row = lane; row < ny * nz; row += 64) {
+            const int a = ((lo[2] + row / ny) * g.dims[1] + lo[1] + row % ny) * g.dims[0];
+            const int e = start[a + hi[0] + 1];
+            for (int q0 = start[a + lo[0]]; q0 < e; q0 += 4) {
+                double dd[4];
+                int jj[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int q = min(q0 + u, e - 1);
+                    jj[u] = q0 + u < e ? sidx[q] : self;  // past the row: skipped below
+                    const double ddx = sxyz[3 * q] - p[0], ddy = sxyz[3 * q + 1] - p[1], ddz = sxyz[3 * q + 2] - p[2];
+                    dd[u] = (ddx * ddx + ddy * ddy) + ddz * ddz;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (jj[u] != self && dd[u] <= bound2 && dd[u] < r2max) {
+                        const int at = atomicAdd(&s_n, 1);
+                        if (at < kCap) {
+                            s_d[at] = dd[u];
+                            s_j[at] = jj[u];
+                        }
+                    }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's appends are complete
+        const int cnt = s_n;
+        if (cnt <= kCap) {  // wave-uniform
+            for (int i = lane; i < cnt; i += 64) {
+                const double di = s_d[i];
+                const int ji = s_j[i];
+                int rank = 0;
+                for (int f = 0; f < cnt; ++f) {  // (every lane reads entry f: LDS broadcast)
+                    const double df = s_d[f];
+                    rank += ((df < di) | ((df == di) & (s_j[f] < ji))) ? 1 : 0;
+                }
+                if (rank < K) nbr[(int64_t)self * K + rank] = ji;
+            }
+            for (int k = cnt + lane; k < K; k += 64) nbr[(int64_t)self * K + k] = -1;  // (fewer than K)
+            return;
+        }
+    }
     double bd[K];
     int bi[K];
 #pragma unroll
