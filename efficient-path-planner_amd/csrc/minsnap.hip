@@ -155,7 +155,7 @@ __device__ __forceinline__ double hess(const double* kc, const double* pw, int r
 }
 // Per track, besides the segment scratch: (M+1) x 5 x 3 vertex values, (M+1) x 4 x 3
 // right-hand sides, M segment times and the block solve's lane exchange (kXch, in LDS).
-constexpr int kXch = 96;
+constexpr int kXch = 144;
 __host__ __device__ constexpr size_t vertex_doubles(int M) { return (size_t)(M + 1) * 27 + (size_t)M + kXch; }
 // Tracks with up to this many segments keep the segment scratch in LDS (~114 KB at 40).
 constexpr int kMaxLdsSeg = 40;
@@ -174,11 +174,24 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ kc, const 
                                            int* s_err, double* T_out, double* C_out) {
     const int tid = threadIdx.x;
     // ---- phase 1: segment times, powers of T, fixed vertex values ---------------
-    for (int i = tid; i < M; i += BLOCK) {
+    // (one barrier: every thread of a segment's powers takes its time itself -- the
+    // caller's, or Nfabian of the same two waypoints, the same arithmetic each time)
+    for (int e = tid; e < M * kNPow; e += BLOCK) {  // (1/T)^k, k = 0..9, and T
+        const int i = e / kNPow, k = e % kNPow;
         const double T = times_in ? times_in[i] : nfabian(P + 3 * i, P + 3 * (i + 1), vmax, amax);
-        Tm[i] = T;
-        if (T_out) T_out[i] = T;
-        if (!(T > 0)) atomicOr(s_err, 1);  // CHECK_GT(segment_time, 0)  impl :297
+        if (k == 0) {
+            Tm[i] = T;
+            if (T_out) T_out[i] = T;
+            if (!(T > 0)) atomicOr(s_err, 1);  // CHECK_GT(segment_time, 0)  impl :297
+        }
+        // 1/T: the hardware reciprocal refined by two Newton steps (~1e-16; a division
+        // would cost ~10 dependent instructions)
+        double it = __builtin_amdgcn_rcp(T);
+        it = fma(it, fma(-T, it, 1.0), it);
+        it = fma(it, fma(-T, it, 1.0), it);
+        double p = k == 10 ? T : 1.0;
+        for (int q = 0; q < k && k < 10; ++q) p = p * it;
+        scr[(size_t)i * Seg::kSize + Seg::kPow + k] = p;
     }
     // start vertex {p0, v0, a0, 0, 0}, inner {p}, end {p, 0, 0, 0, 0}: makeStartOrEnd
     // (src/vertex.cpp:146-170) and trajectory_generator.cpp:28-50
@@ -189,19 +202,6 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ kc, const 
         else if (v == 0 && k == 1) val = v0 ? v0[d] : 0.0;
         else if (v == 0 && k == 2) val = a0 ? a0[d] : 0.0;
         dv[e] = val;
-    }
-    block_sync<SCR_LDS>();
-    for (int e = tid; e < M * kNPow; e += BLOCK) {  // (1/T)^k, k = 0..9, and T
-        const int i = e / kNPow, k = e % kNPow;
-        const double T = Tm[i];
-        // 1/T: the hardware reciprocal refined by two Newton steps (~1e-16; a division
-        // would cost ~10 dependent instructions)
-        double it = __builtin_amdgcn_rcp(T);
-        it = fma(it, fma(-T, it, 1.0), it);
-        it = fma(it, fma(-T, it, 1.0), it);
-        double p = k == 10 ? T : 1.0;
-        for (int q = 0; q < k && k < 10; ++q) p = p * it;
-        scr[(size_t)i * Seg::kSize + Seg::kPow + k] = p;
     }
     block_sync<SCR_LDS>();
     EPP_TL(1);
@@ -244,98 +244,137 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ kc, const 
     block_sync<SCR_LDS>();
     EPP_TL(5);
     EPP_TLC(14);
-    // ---- phase 3: block-tridiagonal solve (block Thomas, lanes over the block entries) ---
+    // ---- phase 3: block-tridiagonal solve (twisted block Thomas, lanes over the block entries)
     // Inner vertices v = 1..nin, diagonal blocks D_v, couplings E_v (v -> v+1), right-hand
-    // sides b_v (3 columns):
-    //   S_1 = D_1, y_1 = b_1;  G_v = S_v^-1 E_v, g_v = S_v^-1 y_v;
-    //   S_{v+1} = D_{v+1} - E_v^T G_v, y_{v+1} = b_{v+1} - E_v^T g_v;
-    //   back: x_nin = g_nin, x_v = g_v - G_v x_{v+1}.
-    // The first wavefront's lanes 0..27 each own one entry: lanes 0..15 the 4x4 block
-    // entry (L>>2, L&3), lanes 16..27 the 4x3 right-hand-side entry ((L-16)/3, (L-16)%3).
-    // A step is two LDS-exchanged stages: (1) adj(S) (one cofactor per lane); (2) every
-    // lane reads all of adj(S) and forms the column t = adj(S) X of its own right-hand
-    // side X (E column for block lanes, y column for rhs lanes) while det(S) and its
-    // reciprocal are computed beside it; its entry of [G g] = t / det (kept for the back
-    // substitution) and of [S' y'] = [D b] - E^T t / det (the next step's S, exchanged)
-    // follow without another exchange.  S_v^-1 = adj(S_v) / det(S_v): no pivots or square
-    // roots; the Schur complements of an SPD R_pp are SPD (det > 0), and the explicit
-    // inverse is within ~cond(S_v) ulp of a factorisation's answer (parity target 1e-6).
-    // Every value a step needs that does not depend on the chain (E_v, the next D / b
-    // entry) is loaded at its start, and every LDS read of a stage is issued together (no
-    // short-circuit reads).  G_v is kept in segment v-1's L slot (D_v is consumed by then),
-    // g_v in rhs[v]; the back substitution runs on lanes 0..11.
-    // xch: S|y [0,28), adj(S) [28,44), x (two buffers) [72,96).
+    // sides b_v (3 columns).  Two eliminations run at once and meet at m = (nin+1)/2:
+    //   top    (v = 1..m-1): S_1 = D_1, y_1 = b_1;  G_v = S_v^-1 E_v, g_v = S_v^-1 y_v;
+    //                        S_{v+1} = D_{v+1} - E_v^T G_v,  y_{v+1} = b_{v+1} - E_v^T g_v
+    //   bottom (v = nin..m+1): T_nin = D_nin, z_nin = b_nin;  H_v = T_v^-1 E_{v-1}^T,
+    //                        h_v = T_v^-1 z_v;  T_{v-1} = D_{v-1} - E_{v-1} H_v, z likewise
+    //   middle: x_m = (D_m - E_{m-1}^T G_{m-1} - E_m H_{m+1})^-1 (b_m - ...) -- the full Schur
+    //           complement of vertex m: the top's S_m minus the bottom's correction
+    //   back:   x_v = g_v - G_v x_{v+1} (v = m-1..1) and x_v = h_v - H_v x_{v-1} (v = m+1..nin),
+    //           both directions at once.
+    // The same elimination as one sweep from the top, in about half the dependent steps
+    // (11 inner vertices: 5 + 1 + 5 instead of 11 + 11).  Lanes 0..27 run the top, lanes
+    // 32..59 the bottom (the same instructions: the bottom reads its coupling transposed).
+    // In a group, lane L owns one entry: L < 16 the 4x4 block entry (L>>2, L&3), 16..27
+    // the 4x3 right-hand-side entry ((L-16)/3, (L-16)%3).  A step is two LDS-exchanged
+    // stages: (1) adj(S) (one cofactor per lane); (2) every lane reads all of adj(S) and
+    // forms the column t = adj(S) X of its own right-hand side X (coupling column for block
+    // lanes, y column for rhs lanes) while det(S) and its reciprocal are computed beside
+    // it; its entry of [G g] = t / det (kept for the back substitution) and of
+    // [S' y'] = [D b] - E^T t / det (the next step's S, exchanged) follow without another
+    // exchange.  S^-1 = adj(S) / det(S): no pivots or square roots; the Schur complements
+    // of an SPD R_pp are SPD (det > 0), and the explicit inverse is within ~cond(S) ulp of
+    // a factorisation's answer (parity target 1e-6).  Every value a step needs that does
+    // not depend on the chain (the coupling, the next D / b entry) is loaded at its start.
+    // G_v / H_v are kept in segment v-1's L slot (D_v is consumed by then), g_v / h_v in
+    // rhs[v].  xch: per group (base 48 g) S|y [0,28), adj(S) [28,44); x buffers
+    // [96 + 24 g, +24).
     if (tid < kWave && nin > 0) {
-        const int L = tid;
+        const int L = tid & 31, grp = tid >> 5;
         const bool mat = L < 16, act = L < 28;
         const int row = mat ? (L >> 2) : (L - 16) / 3;  // block row (S, G) or rhs row (y, g)
         const int col = mat ? (L & 3) : (L - 16) % 3;
         const int ycol = mat ? 0 : col;                   // (block lanes read a dummy y column)
         const bool diag = mat && (L % 5) == 0;            // S[i][i]: must stay > 0 (SPD)
-        double cur = act ? (mat ? scr[Seg::kL + L] : rhs[12 + (L - 16)]) : 1.0;  // this lane's S / y entry
-        if (act) xch[L] = cur;
-        bool ok = !diag || cur > 0.0;
+        const int m = (nin + 1) / 2;
+        const int nstep = nin - m;                        // the bottom's steps (the top's: m - 1 <= nstep)
+        const int gsteps = grp == 0 ? m - 1 : nin - m;
+        double* xg = xch + 48 * grp;
+        const int vs = grp == 0 ? 1 : nin;
+        double cur = act ? (mat ? scr[(size_t)(vs - 1) * Seg::kSize + Seg::kL + L] : rhs[(size_t)vs * 12 + (L - 16)])
+                         : 1.0;  // this lane's S / y entry
+        if (act) xg[L] = cur;
+        bool ok = !act || !diag || cur > 0.0;
         // the cofactor this lane computes: adj(S)[ar][ac] = (-1)^(ar+ac) det(S minus row ac, col ar)
         const int ar = (L >> 2) & 3, ac = L & 3;
         const int r0 = ac == 0 ? 1 : 0, r1 = ac <= 1 ? 2 : 1, r2 = ac <= 2 ? 3 : 2;
         const int c0 = ar == 0 ? 1 : 0, c1 = ar <= 1 ? 2 : 1, c2 = ar <= 2 ? 3 : 2;
         const double sgn = ((ar + ac) & 1) ? -1.0 : 1.0;
-        wave_sync_lds();
-        for (int v = 1; v <= nin; ++v) {
-            EPP_TLI(v);
-            double* Sg = scr + (size_t)(v - 1) * Seg::kSize;
-            // E_v column `row` (for E^T t) and column `col` (block lanes' X); the next
-            // step's D / b entry: independent of the chain, in flight meanwhile
-            double Ep[4], Ec[4], nxt = 0.0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                Ep[k] = Sg[Seg::kW + k * 4 + (row & 3)];
-                Ec[k] = Sg[Seg::kW + k * 4 + (col & 3)];
-            }
-            if (v < nin && act) nxt = mat ? Sg[Seg::kSize + Seg::kL + L] : rhs[(size_t)(v + 1) * 12 + (L - 16)];
-            // stage 1: one cofactor per block lane; S row 0 (det) and the y column (rhs
-            // lanes' X) read with it
-            const double a = xch[r0 * 4 + c0], b = xch[r0 * 4 + c1], c = xch[r0 * 4 + c2];
-            const double d = xch[r1 * 4 + c0], e = xch[r1 * 4 + c1], f = xch[r1 * 4 + c2];
-            const double g = xch[r2 * 4 + c0], h = xch[r2 * 4 + c1], i = xch[r2 * 4 + c2];
+        // one elimination step on S|y in xg with coupling rows Ep (E^T row `row`) and
+        // columns Ec (block lanes' X); returns t (4) and 1/det; ok updated
+        auto step_core = [&](const double (&Ec)[4], double (&t)[4], double& id, bool live) {
+            const double a = xg[r0 * 4 + c0], b = xg[r0 * 4 + c1], c = xg[r0 * 4 + c2];
+            const double d = xg[r1 * 4 + c0], e = xg[r1 * 4 + c1], f = xg[r1 * 4 + c2];
+            const double g = xg[r2 * 4 + c0], h = xg[r2 * 4 + c1], i = xg[r2 * 4 + c2];
             double s0[4], yc[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                s0[k] = xch[k];
-                yc[k] = xch[16 + k * 3 + ycol];
+                s0[k] = xg[k];
+                yc[k] = xg[16 + k * 3 + ycol];
             }
             const double m0 = fma(e, i, -(f * h)), m1 = fma(d, i, -(f * g)), m2 = fma(d, h, -(e * g));
             const double cof = sgn * fma(c, m2, fma(a, m0, -(b * m1)));
-            if (mat) xch[28 + L] = cof;
+            if (mat && live) xg[28 + L] = cof;
             wave_sync_lds();
-            // stage 2: adj(S) to every lane; det = S row 0 . adj column 0
             double adj[16];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) adj[k] = xch[28 + k];
+            for (int k = 0; k < 16; ++k) adj[k] = xg[28 + k];
             const double det = fma(s0[0], adj[0], s0[1] * adj[4]) + fma(s0[2], adj[8], s0[3] * adj[12]);
-            double id = __builtin_amdgcn_rcp(det);  // refined by two Newton steps
+            id = __builtin_amdgcn_rcp(det);  // refined by two Newton steps
             id = fma(id, fma(-det, id, 1.0), id);
             id = fma(id, fma(-det, id, 1.0), id);
-            ok = ok && det > 0.0;
-            double X[4], t[4];
+            ok = ok && (!live || det > 0.0);
+            double X[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) X[k] = mat ? Ec[k] : yc[k];
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 t[k] = fma(adj[4 * k], X[0], adj[4 * k + 1] * X[1]) + fma(adj[4 * k + 2], X[2], adj[4 * k + 3] * X[3]);
-            const double tr = row == 0 ? t[0] : row == 1 ? t[1] : row == 2 ? t[2] : t[3];
-            const double gv = tr * id;
-            const double et = fma(Ep[0], t[0], Ep[1] * t[1]) + fma(Ep[2], t[2], Ep[3] * t[3]);
-            if (act) {
-                if (mat) Sg[Seg::kL + L] = gv;  // G_v for the back substitution
-                else rhs[(size_t)v * 12 + (L - 16)] = gv;
+        };
+        wave_sync_lds();
+        for (int s = 0; s < nstep; ++s) {
+            EPP_TLI(1 + s);
+            const bool live = s < gsteps;
+            const int v = grp == 0 ? 1 + s : nin - s;
+            const int vn = grp == 0 ? v + 1 : v - 1;  // the next vertex of this sweep
+            // coupling: top E_v (segment v-1's W slot, E[k][q] at 4k + q), bottom E_{v-1}
+            // transposed (segment v-2's W slot); E^T row `row`, and column `col`
+            const double* Eb = scr + (size_t)(grp == 0 ? v - 1 : max(v - 2, 0)) * Seg::kSize + Seg::kW;
+            double Ep[4], Ec[4], nxt = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                Ep[k] = grp == 0 ? Eb[k * 4 + (row & 3)] : Eb[(row & 3) * 4 + k];
+                Ec[k] = grp == 0 ? Eb[k * 4 + (col & 3)] : Eb[(col & 3) * 4 + k];
             }
-            if (v < nin) {
-                cur = fma(-et, id, nxt);  // [S' y'] = [D b] - E^T t / det
-                if (act) xch[L] = cur;
+            if (live && act) nxt = mat ? scr[(size_t)(vn - 1) * Seg::kSize + Seg::kL + L] : rhs[(size_t)vn * 12 + (L - 16)];
+            double t[4], id;
+            step_core(Ec, t, id, live);
+            const double tr = row == 0 ? t[0] : row == 1 ? t[1] : row == 2 ? t[2] : t[3];
+            const double et = fma(Ep[0], t[0], Ep[1] * t[1]) + fma(Ep[2], t[2], Ep[3] * t[3]);
+            if (live && act) {
+                if (mat) scr[(size_t)(v - 1) * Seg::kSize + Seg::kL + L] = tr * id;  // G_v / H_v
+                else rhs[(size_t)v * 12 + (L - 16)] = tr * id;                       // g_v / h_v
+                const double corr = et * id;
+                cur = nxt - corr;  // [S' y'] = [D b] - E^T t / det
+                // (the bottom's last step publishes its correction instead: the middle block
+                // is the top's S_m minus it)
+                xg[L] = (grp == 1 && s == nstep - 1) ? corr : cur;
                 ok = ok && (!diag || cur > 0.0);
             }
             wave_sync_lds();
+        }
+        // middle: the top's S_m | y_m minus the bottom's last correction
+        if (grp == 0 && act) {
+            cur = cur - (nstep > 0 ? xch[48 + L] : 0.0);
+            xg[L] = cur;
+            ok = ok && (!diag || cur > 0.0);
+        }
+        wave_sync_lds();
+        {
+            const double Ec0[4] = {0.0, 0.0, 0.0, 0.0};
+            double t[4], id;
+            step_core(Ec0, t, id, grp == 0);
+            const double tr = row == 0 ? t[0] : row == 1 ? t[1] : row == 2 ? t[2] : t[3];
+            if (grp == 0 && act && !mat) {  // x_m = (middle block)^-1 (middle rhs)
+                const double x = tr * id;
+                rhs[(size_t)m * 12 + (L - 16)] = x;
+                dv[((size_t)m * HALF + 1) * 3 + (L - 16)] = x;  // derivatives 1..4 of vertex m
+                xch[96 + (L - 16)] = x;
+                xch[96 + 24 + (L - 16)] = x;
+            }
         }
         // (the G/g stores, LDS or, for long tracks, global scratch: a workgroup-scope fence
         // makes the latter visible to the wave's own later loads)
@@ -343,30 +382,31 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ kc, const 
         wave_sync_lds();
         if (__ballot(!ok) == 0ull) {  // wave-uniform
             EPP_TLI(32);
-            // lanes 0..11: x_v entry (p, d) = (L/3, L%3); G_v row p and g_v entry of the
-            // next step are loaded before this step's exchange completes
+            // lanes 0..11 of each group: x_v entry (p, d) = (L/3, L%3); the next step's G / H
+            // row and g / h entry are loaded before this step's exchange completes
             const int p = (L / 3) & 3, d = L % 3;
             const int Lr = L < 12 ? L : 0;
+            const int bsteps = grp == 0 ? m - 1 : nin - m;
+            double* xb = xch + 96 + 24 * grp;
             int buf = 0;
-            double Gr[4], gx;
+            double Gr[4] = {0.0, 0.0, 0.0, 0.0}, gx = 0.0;
             auto load_step = [&](int v, double (&G)[4], double& gg) {
                 const double* Gp = scr + (size_t)(v - 1) * Seg::kSize + Seg::kL + p * 4;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) G[k] = Gp[k];
                 gg = rhs[(size_t)v * 12 + Lr];
             };
-            load_step(nin, Gr, gx);
-            for (int v = nin; v >= 1; --v) {
-                EPP_TLI(32 + nin + 1 - v);
+            if (bsteps > 0) load_step(grp == 0 ? m - 1 : m + 1, Gr, gx);
+            for (int s = 0; s < nstep; ++s) {
+                EPP_TLI(33 + s);
+                const bool live = s < bsteps;
+                const int v = grp == 0 ? m - 1 - s : m + 1 + s;
                 double Gn[4] = {0.0, 0.0, 0.0, 0.0}, gn = 0.0;
-                if (v > 1) load_step(v - 1, Gn, gn);
-                double x = gx;
-                if (v < nin) {
-                    const double* xn = xch + 72 + buf * 12;
-                    x = x - (fma(Gr[0], xn[d], Gr[1] * xn[3 + d]) + fma(Gr[2], xn[6 + d], Gr[3] * xn[9 + d]));
-                }
-                if (L < 12) {
-                    xch[72 + (buf ^ 1) * 12 + L] = x;
+                if (s + 1 < bsteps) load_step(grp == 0 ? v - 1 : v + 1, Gn, gn);
+                const double* xn = xb + buf * 12;
+                const double x = gx - (fma(Gr[0], xn[d], Gr[1] * xn[3 + d]) + fma(Gr[2], xn[6 + d], Gr[3] * xn[9 + d]));
+                if (live && L < 12) {
+                    xb[(buf ^ 1) * 12 + L] = x;
                     dv[((size_t)v * HALF + 1) * 3 + L] = x;  // derivatives 1..4 of vertex v
                 }
 #pragma unroll

@@ -1,8 +1,8 @@
 """Phase timeline of the fused single-track refit (k_refit): builds a diagnostics copy of
 libepp.so with -DEPP_REFIT_TL into scripts/dbg/ (not the product library), runs 50
 refits and prints the median time of every phase boundary (s_memrealtime, 100 MHz)
-relative to the kernel's first stamp.  Solver (wg0): 0 entry, 9 A^-1, 1 vertex values,
-2 Q, 3 G, 4 H, 5 assembly, 6 block Cholesky, 7 coefficients, 8 inputs staged, 13 rows
+relative to the kernel's first stamp.  Solver (wg0): 0 entry,
+1 times / powers / vertex values, 5 assembly, 6 block solve, 7 coefficients, 8 inputs staged, 13 rows
 written; slots 14/15 hold the shader clock (s_memtime) around the block solve."""
 import ctypes as C
 import os
@@ -40,12 +40,13 @@ allst = np.array(stamps[10:])
 it = allst[:, 32:32 + 64]  # wg0's per-iteration shader clocks of the block solve
 W = len(wp)
 nin = W - 2
-fw = np.diff(it[:, 1:nin + 1], axis=1)
-print("block solve forward, cycles per vertex step (median):", np.median(fw, axis=0).astype(int).tolist())
-bw = np.diff(it[:, 32:32 + nin + 1], axis=1)
-print("back substitution, cycles per vertex step (median):", np.median(bw, axis=0).astype(int).tolist())
-print("forward end -> back start:", int(np.median(it[:, 32] - it[:, nin])), "cycles; back end -> phase end:",
-      int(np.median(it[:, 63] - it[:, 32 + nin])), "cycles")
+nstep = nin - (nin + 1) // 2  # the twisted solve's steps per sweep (slots 1.. forward, 33.. back)
+fw = np.diff(it[:, 1:nstep + 1], axis=1)
+print("block solve forward, cycles per step (median):", np.median(fw, axis=0).astype(int).tolist())
+bw = np.diff(it[:, 32:32 + nstep + 1], axis=1)
+print("back substitution, cycles per step (median):", np.median(bw, axis=0).astype(int).tolist())
+print("last forward step -> back start (middle solve):", int(np.median(it[:, 32] - it[:, nstep])),
+      "cycles; back end -> phase end:", int(np.median(it[:, 63] - it[:, 32 + nstep])), "cycles")
 st = allst[:, :32].reshape(-1, 2, 16)
 t0 = st[:, :, 0].min(axis=1)
 for wg in range(2):
