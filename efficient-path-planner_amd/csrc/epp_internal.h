@@ -44,6 +44,15 @@
 #include "epp.h"
 
 namespace epp {
+// poly_traj::generateTrajectory of one track on the device (k_refit, minsnap.hip); the R
+// sampled rows (R x 10 doubles) are copied into the buffer alloc(ctx, R) returns (NULL:
+// out of memory).  times: the caller's segment times, or NULL for Nfabian's.
+epp_status generate_trajectory_into(const double* wp, int32_t n_wp, const double* times, double v_max,
+                                    double a_max, double dt, double t0, const double v0[3], const double a0[3],
+                                    double* (*alloc)(void*, int64_t), void* ctx, int64_t* n_rows);
+}  // namespace epp
+
+namespace epp {
 
 // field index into the SoA table
 enum Field : int {

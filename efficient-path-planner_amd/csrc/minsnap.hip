@@ -1104,14 +1104,17 @@ epp_status epp_sample_batch(const double* seg_times, const double* coeffs, const
 // reference, or the caller's) and runs Trajectory::evaluateRange's sample recurrence
 // (src/trajectory.cpp:81-141: exact count, times and segments); one launch of k_refit then
 // solves and writes the rows straight into pinned memory; one stream synchronisation.
-epp_status generate_trajectory(const double* wp, int32_t n_wp, const double* times, double v_max, double a_max,
-                               double dt, double t0, const double v0[3], const double a0[3], double** rows_out,
-                               int64_t* n_rows) {
-    if (!rows_out || !n_rows || (n_wp > 0 && !wp)) {
+// The rows are copied once, from the pinned buffer the kernel wrote into the buffer
+// alloc(ctx, R) returns (the C ABI: malloc; the C++ API: the result matrix itself).
+}  // extern "C"
+
+epp_status epp::generate_trajectory_into(const double* wp, int32_t n_wp, const double* times, double v_max,
+                                         double a_max, double dt, double t0, const double v0[3], const double a0[3],
+                                         double* (*alloc)(void*, int64_t), void* ctx, int64_t* n_rows) {
+    if (!alloc || !n_rows || (n_wp > 0 && !wp)) {
         set_error("generateTrajectory: invalid argument");
         return EPP_ERR_INVALID_ARGUMENT;
     }
-    *rows_out = nullptr;
     *n_rows = 0;
     if (n_wp < 2) {
         set_error("At least two waypoints are required");  // trajectory_generator.cpp:24
@@ -1208,16 +1211,43 @@ epp_status generate_trajectory(const double* wp, int32_t n_wp, const double* tim
         set_error(info == -2 ? "Segment times need to be greater than zero" : "min-snap solve failed");
         return EPP_ERR_RUNTIME;
     }
-    double* host_rows = (double*)std::malloc((size_t)std::max(R, 1) * 80);
+    double* host_rows = alloc(ctx, R);
     if (!host_rows) {
         set_error("generateTrajectory: out of host memory");
         return EPP_ERR_RUNTIME;
     }
     if (R) std::memcpy(host_rows, a.out, (size_t)R * 80);
-    *rows_out = host_rows;
     *n_rows = R;
     return EPP_OK;
 }
+
+namespace epp {
+namespace {
+double* malloc_rows(void* ctx, int64_t R) {
+    double* p = (double*)std::malloc((size_t)std::max<int64_t>(R, 1) * 80);
+    *static_cast<double**>(ctx) = p;
+    return p;
+}
+epp_status generate_trajectory(const double* wp, int32_t n_wp, const double* times, double v_max, double a_max,
+                               double dt, double t0, const double v0[3], const double a0[3], double** rows_out,
+                               int64_t* n_rows) {
+    if (!rows_out || !n_rows) {
+        set_error("generateTrajectory: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    *rows_out = nullptr;
+    const epp_status rc = generate_trajectory_into(wp, n_wp, times, v_max, a_max, dt, t0, v0, a0, malloc_rows,
+                                                   rows_out, n_rows);
+    if (rc != EPP_OK && *rows_out) {
+        std::free(*rows_out);
+        *rows_out = nullptr;
+    }
+    return rc;
+}
+}  // namespace
+}  // namespace epp
+
+extern "C" {
 
 epp_status epp_generate_trajectory_host(const double* wp, int32_t n_wp, double v_max, double a_max, double dt,
                                         double t0, const double v0[3], const double a0[3], double** rows_out,

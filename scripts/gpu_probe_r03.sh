@@ -1,12 +1,16 @@
 #!/bin/bash
-# Round-3 probe session (diagnostics): min-snap / planner GPU tests, refit A/B against
-# scripts/dbg/libepp_prev.so, refit timeline.
+# Round-3 probe session (diagnostics): k-NN grid density (EPP_KNN_NPC) vs k_knn_tile time.
 set -u
 cd "${GRAFT_REPO_ROOT}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-PYTEST_FILES="tests/test_gpu_minsnap.py tests/test_gpu_planner.py" AB_LIBS="prev" bash scripts/gpu_refit_ab.sh || exit $?
-echo "== refit timeline"; timeout -k 10 120 python3 scripts/refit_timeline.py > gpurun_out/refit_tl.log 2>&1 || exit $?
-tail -16 gpurun_out/refit_tl.log
-echo "== C5 latency split"
-PYTEST_K=minsnap_batch_golden bash scripts/gpu_c5probe.sh 2>&1 | grep -v "^\.\|passed" | head -60
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+for npc in 1.5 1.25 1.1 1.0 1.35 1.5; do
+  EPP_KNN_NPC=$npc timeout -k 10 120 python3 scripts/knn_probe.py 1 > gpurun_out/knn_v.log 2>&1 || { tail -5 gpurun_out/knn_v.log; exit 1; }
+  grep "per call" gpurun_out/knn_v.log | sed "s|^|npc $npc |"
+done
+for npc in 1.25 1.1; do
+  echo "== timeline npc $npc"
+  EPP_KNN_NPC=$npc timeout -k 10 120 python3 scripts/knn_timeline.py > gpurun_out/knn_tl.log 2>&1 || exit 1
+  grep -v "^launch" gpurun_out/knn_tl.log | tail -10
+done
