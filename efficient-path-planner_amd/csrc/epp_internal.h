@@ -50,6 +50,10 @@ namespace epp {
 epp_status generate_trajectory_into(const double* wp, int32_t n_wp, const double* times, double v_max,
                                     double a_max, double dt, double t0, const double v0[3], const double a0[3],
                                     double* (*alloc)(void*, int64_t), void* ctx, int64_t* n_rows);
+// epp_mask_edges_count without clearing `count` first: the counts are added to what it
+// holds (the planner clears them with its first upload).
+epp_status mask_edges_count_acc(int32_t* nbr, const uint8_t* valid, int64_t m, int32_t target, int64_t* count,
+                                void* stream);
 }  // namespace epp
 
 namespace epp {

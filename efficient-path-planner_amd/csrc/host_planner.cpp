@@ -19,6 +19,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "epp/PathPlanner.h"
+#include "epp_internal.h"
 #include "host_scratch.h"
 
 namespace epp {
@@ -126,14 +127,17 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     const size_t m_max = max_nodes * (size_t)k;
     const size_t ws_bytes = (size_t)epp_knn_workspace_size((int32_t)max_nodes);
     const size_t cws_bytes = (size_t)epp_compact_workspace_size((int64_t)n_s);
-    ts.reset(ThreadScratch::rounded(n_s * 24) + ThreadScratch::rounded(n_s) + ThreadScratch::rounded(max_nodes * 24) +
+    ts.reset(ThreadScratch::rounded(n_s * 24) + ThreadScratch::rounded(n_s) + ThreadScratch::rounded(256 + max_nodes * 24) +
              ThreadScratch::rounded(8) + ThreadScratch::rounded(16) + ThreadScratch::rounded(m_max * 4) + 2 * ThreadScratch::rounded(m_max * 24) +
              ThreadScratch::rounded(m_max) + ThreadScratch::rounded(ws_bytes) + ThreadScratch::rounded(cws_bytes));
     double* d_s = static_cast<double*>(ts.carve(n_s * 24));
     uint8_t* d_v = static_cast<uint8_t*>(ts.carve(n_s));
-    double* d_nodes = static_cast<double*>(ts.carve(max_nodes * 24));
+    // [.. | edge counts (16 B) | 32 B | start, goal, the valid samples]: the counters and
+    // the two end nodes are set by one upload (no separate clearing of the counters)
+    char* d_head = static_cast<char*>(ts.carve(256 + max_nodes * 24));
+    double* d_nodes = reinterpret_cast<double*>(d_head + 256);
+    int64_t* d_ecnt = reinterpret_cast<int64_t*>(d_head + 256 - 48);
     int64_t* d_cnt = static_cast<int64_t*>(ts.carve(8));
-    int64_t* d_ecnt = static_cast<int64_t*>(ts.carve(16));
     int32_t* d_nbr = static_cast<int32_t*>(ts.carve(m_max * 4));
     double* d_e1 = static_cast<double*>(ts.carve(m_max * 24));
     double* d_e2 = static_cast<double*>(ts.carve(m_max * 24));
@@ -148,10 +152,12 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     check(epp_compact_states_ws(d_s, d_v, samples, d_nodes + 6, d_cnt, d_cws, cws_bytes, st), "compact");
     // start / goal up, the valid-state count down: both queued, one synchronisation
     // (pinned staging: [ends (6 doubles) | count | edge counts (2)])
+    // pinned staging: [edge counts = 0 (2) | pad (4) | ends (6) | count | edge counts (2)]
     double* h_small = static_cast<double*>(ts.pinned(2, 16 * sizeof(double)));
-    std::copy(ends, ends + 6, h_small);
-    int64_t* h_cnt = reinterpret_cast<int64_t*>(h_small + 6);
-    check(epp_memcpy_h2d_async(d_nodes, h_small, sizeof(ends), st), "upload");
+    std::fill(h_small, h_small + 6, 0.0);
+    std::copy(ends, ends + 6, h_small + 6);
+    int64_t* h_cnt = reinterpret_cast<int64_t*>(h_small + 12);
+    check(epp_memcpy_h2d_async(d_ecnt, h_small, 12 * sizeof(double), st), "upload");
     check(epp_memcpy_d2h_async(h_cnt, d_cnt, 8, st), "download");
     check(epp_stream_sync(st), "sync");
     const int64_t n_valid_states = h_cnt[0];
@@ -174,7 +180,7 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
         check(ks, "motion check");
     }
     // failed motions -> -1; the valid edges, and those into the goal (node 1)
-    check(epp_mask_edges_count(d_nbr, d_ev, (int64_t)m, 1, d_ecnt, st), "mask edges");
+    check(mask_edges_count_acc(d_nbr, d_ev, (int64_t)m, 1, d_ecnt, st), "mask edges");  // (counters zeroed above)
     // node coordinates and the masked k-NN table into pinned host staging
     // (sized for the attempt's largest node count, not this one's: a pinned buffer that
     // grows is freed and reallocated, and hipHostFree waits for the whole device)

@@ -1522,14 +1522,27 @@ epp_status epp_mask_edges_count(int32_t* nbr, const uint8_t* valid, int64_t m, i
         set_error("epp_mask_edges_count: invalid argument");
         return EPP_ERR_INVALID_ARGUMENT;
     }
+    if (hipMemsetAsync(count, 0, 2 * sizeof(int64_t), (hipStream_t)stream) != hipSuccess) return last("epp_mask_edges_count");
+    return epp::mask_edges_count_acc(nbr, valid, m, target, count, stream);
+}
+
+}  // extern "C"
+
+epp_status epp::mask_edges_count_acc(int32_t* nbr, const uint8_t* valid, int64_t m, int32_t target, int64_t* count,
+                                     void* stream) {
+    if (m < 0 || !count || (m > 0 && (!nbr || !valid))) {
+        set_error("epp_mask_edges_count: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
     hipStream_t s = (hipStream_t)stream;
-    if (hipMemsetAsync(count, 0, 2 * sizeof(int64_t), s) != hipSuccess) return last("epp_mask_edges_count");
     if (m == 0) return EPP_OK;
     const int64_t blocks = std::min<int64_t>((m + kMaskThreads - 1) / kMaskThreads, 256);
     hipLaunchKernelGGL(k_mask_edges_count, dim3((unsigned)blocks), dim3(kMaskThreads), 0, s, nbr, valid, m, target,
                        reinterpret_cast<unsigned long long*>(count));
     return last("epp_mask_edges_count");
 }
+
+extern "C" {
 
 epp_status epp_knn_edges(const double* nodes, const int32_t* nbr, int32_t n, int32_t k, double* s1,
                          double* s2, void* stream) {
