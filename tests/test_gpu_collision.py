@@ -545,8 +545,10 @@ def test_async_small_queries_across_updates(fworlds):
 @pytest.mark.parametrize("filling", [False, True])
 def test_knn_motions_equal_materialised(cfg, geom, fworlds, name, filling):
     """epp_check_knn_motions (edges read off a k-NN table, no endpoint arrays) gives the
-    flags of epp_knn_edges + epp_check_motions, both modes and can_pass_gate values,
-    missing neighbours (-1) and edges far longer than a tile included."""
+    CPU oracle's flags for the same edges (World::checkRayValid / the 32-step check, src/
+    World.cpp:130-162) and those of epp_knn_edges + epp_check_motions, both modes and
+    can_pass_gate values, missing neighbours (-1) and edges far longer than a tile
+    included."""
     if filling:
         g_, rg, ro, ws = fworlds
     else:
@@ -562,14 +564,21 @@ def test_knn_motions_equal_materialised(cfg, geom, fworlds, name, filling):
     nbr = np.where(rs.rand(n, k) < 0.9, near, far).astype(np.int32)
     nbr[rs.rand(n, k) < 0.03] = -1
     s1, s2 = capi.knn_edges(nodes, nbr)
+    # the edges the table denotes, built on the host (a missing neighbour: the node to itself)
+    src = np.repeat(np.arange(n), k)
+    dst = np.where(nbr.reshape(-1) < 0, src, nbr.reshape(-1))
+    assert np.array_equal(s1, nodes[src]) and np.array_equal(s2, nodes[dst])
+    ref = O.world_build(g_, gates, obstacles, rg, ro)
     d_n, d_k, d_v = capi.DeviceBuffer.from_array(nodes), capi.DeviceBuffer.from_array(nbr), capi.DeviceBuffer(n * k)
     for mode in (0, 1):
         for cp in (0, 1):
+            exp = O.check_motions(ref, rg, ro, nodes[src], nodes[dst], bool(cp), mode, threads=8)
             want = w.check_motions(s1, s2, bool(cp), mode)
+            assert np.array_equal(want, exp), (mode, cp)
             capi.check(capi.lib().epp_check_knn_motions(w.handle, d_n.ptr, d_k.ptr, n, k, cp, mode, d_v.ptr, None))
             capi.sync()
             got = d_v.download(np.uint8, n * k)
-            assert np.array_equal(got, want), (mode, cp, int((got != want).sum()))
+            assert np.array_equal(got, exp), (mode, cp, int((got != exp).sum()))
 
 
 def test_knn_motions_unsupported_small_batch(cfg, geom):
