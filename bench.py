@@ -675,7 +675,8 @@ def host_info():
 
 # host threads for the all-cores legs: the box's CPU share of one GPU (16; the machine
 # reports more logical CPUs than a one-GPU job may use, and the pool's rules size worker
-# pools to that share, so the all-cores figures are not run wider)
+# pools to that share).  States and C3 are also sampled briefly at 32 threads and at every
+# logical CPU (states_wide, c3_*.edges_per_s_<T>_threads).
 CPU_SHARE_THREADS = 16
 
 
@@ -709,6 +710,17 @@ def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None):
         O.check_states(w, rg, ro, pts, False, threads=nt)
     dt2 = (time.perf_counter() - t2) / 3
     host = host_info()
+    # wider sweeps, short samples: 32 threads (256 logical CPUs / 8 GPUs: one GPU's share
+    # on an 8-GPU node) and every logical CPU the box reports (measured, not the bound;
+    # on a shared box other jobs' threads compete for those cores)
+    wide = {}
+    for tw in sorted({32, host["affinity_cpus"] or 1}):
+        reps_w = 8 if tw <= 64 else 32
+        t3 = time.perf_counter()
+        for _ in range(reps_w):
+            O.check_states(w, rg, ro, pts, False, threads=tw)
+        wide[str(tw)] = {"value": reps_w * N_STATES / (time.perf_counter() - t3), "threads": tw,
+                         "checks": reps_w * N_STATES}
     out = {"value": reps * N_STATES / dt, "unit": "state validity checks/s", "cores": 1, "kind": "port",
            "sample": f"{reps} passes over the same {N_STATES:,}-state C2 batch ({reps * N_STATES} checks, {dt:.1f} s)",
            "all_cores_value": N_STATES / dt2, "all_cores_threads": nt, "host": host,
@@ -716,7 +728,8 @@ def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None):
            # (perfect scaling, no memory-bandwidth or SMT limits) -- the most CPU-favourable
            # bound for "all host cores"; running that wide exceeds one GPU job's CPU share
            "all_cores_ideal_bound": {"value": reps * N_STATES / dt * (host["nproc"] or 1),
-                                     "threads": host["nproc"], "kind": "bound: 1-thread rate x nproc"}}
+                                     "threads": host["nproc"], "kind": "bound: 1-thread rate x nproc"},
+           "states_wide": wide}
     # C3 motions: 512 OBBs, the same edge generator as the GPU leg (bounded edge counts)
     g3, o3 = synth.track_world(42, n_obstacles=472)
     w3 = O.world_build(geom, g3, o3, rg, ro)
@@ -726,6 +739,10 @@ def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None):
         O.check_motions(w3, rg, ro, s1, s2, False, mode, threads=nt)
         el = time.perf_counter() - t
         out[key] = {"edges_per_s": n / el, "threads": nt, "edges": n}
+        for tw in sorted({32, host["affinity_cpus"] or 1}):
+            t = time.perf_counter()
+            O.check_motions(w3, rg, ro, s1, s2, False, mode, threads=tw)
+            out[key][f"edges_per_s_{tw}_threads"] = n / (time.perf_counter() - t)
     # C4 full plan on the CPU: the same batch planner restated (oracle/track_planner.py):
     # 9 gate-to-gate plans (65,536 samples, k = 16; each plan's checks and k-NN on nt
     # threads) + includeGates2 + min-snap + sampling, the rank-0 track (seed 100)

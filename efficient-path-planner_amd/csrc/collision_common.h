@@ -19,9 +19,6 @@
 #include "epp_internal.h"
 
 namespace epp {
-const WorldView& world_view(const epp_world* w);
-const WorldView* world_dview(const epp_world* w);
-epp_status ensure_index(const epp_world* w);  // rebuild + upload a stale index (world_index.cpp)
 SmallWorld small_world(const epp_world* w);
 epp_status note_record_reader(const epp_world* w, const SmallWorld& sw, hipStream_t st);  // async reader of sw.recs
 

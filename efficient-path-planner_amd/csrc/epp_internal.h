@@ -36,6 +36,7 @@
 #include <stdint.h>
 
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <vector>
 
@@ -189,6 +190,12 @@ struct HostWorld {
     std::vector<RecReader> rec_readers[2];
     bool index_stale = false;           // the device blob is an older version
     std::mutex mu;                      // guards the lazy index rebuild
+    // Held shared by a launcher from its snapshot of the device index until its kernel is
+    // queued (IndexLease, SmallWorld::lease), exclusively by a rebuild: a rebuild on one
+    // thread cannot free or rewrite the blob between another thread's snapshot and launch.
+    // Lock order: index_mu, then mu.
+    std::shared_mutex index_mu;
+    WorldView dev_view{};               // `view` as uploaded (an update changes view.n_obb first)
     double r_gate = 0, r_obst = 0;
     int device = 0;
     void* d_blob = nullptr;
@@ -233,6 +240,18 @@ struct SmallWorld {
     int32_t n_obb;
     double r_gate, r_obst;
     int host_slot;  // recs is the pinned host copy of this slot (index stale), else -1
+    std::shared_lock<std::shared_mutex> lease;  // held while recs is the device blob's
 };
+
+// A launcher's snapshot of the device index (host view as uploaded + its device copy),
+// valid while the lease is held: a rebuild on another thread waits for it.
+struct IndexLease {
+    std::shared_lock<std::shared_mutex> lk;
+    WorldView view{};
+    const WorldView* dview = nullptr;
+};
+// rebuild + upload a stale index (world_index.cpp); with a lease, the current index's
+// snapshot, held until the lease is released (after the launch)
+epp_status ensure_index(const epp_world* w, IndexLease* lease = nullptr);
 
 }  // namespace epp

@@ -665,7 +665,7 @@ using namespace epp;
 namespace {
 // k_motions_v5 when the world has tile tables and they, the records and the wave queues
 // fit the LDS budget; returns false (nothing launched) otherwise.
-bool launch_motions_v5(const epp_world* world, const WorldView& w, const double* s1, const double* s2,
+bool launch_motions_v5(const WorldView* dw, const WorldView& w, const double* s1, const double* s2,
                        const int32_t* nbr, int kk, int64_t n, int32_t can_pass_gate, int32_t mode, uint8_t* valid,
                        hipStream_t st) {
     if (w.slab_n <= 0) return false;
@@ -675,7 +675,6 @@ bool launch_motions_v5(const epp_world* world, const WorldView& w, const double*
     if (shm5 > kLdsBudget) return false;
     const int per_cu = std::max(1, std::min(2, (int)((160u * 1024u) / shm5)));
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + 1023) / 1024, (int64_t)cu_count() * per_cu));
-    const WorldView* dw = world_dview(world);
 #define EPP_LAUNCH_M5(WW, MM, II)                                                                                 \
     do {                                                                                                          \
         allow_lds(k_motions_v5<WW, MM, II>);                                                                      \
@@ -726,14 +725,16 @@ epp_status epp_check_motions(const epp_world* world, const double* s1, const dou
         return EPP_ERR_INVALID_ARGUMENT;
     }
     if (n == 0) return EPP_OK;
-    const SmallWorld sw = small_world(world);
+    SmallWorld sw = small_world(world);
     if (small_motions(sw, n)) {
         if (const epp_status st = launch_motions_small(sw, mode, s1, s2, n, can_pass_gate, valid, (hipStream_t)stream))
             return st;
         return note_record_reader(world, sw, (hipStream_t)stream);
     }
-    if (const epp_status st = ensure_index(world)) return st;
-    const WorldView& w = world_view(world);
+    sw.lease = {};  // (a stale index is rebuilt below)
+    IndexLease ix;
+    if (const epp_status st = ensure_index(world, &ix)) return st;
+    const WorldView& w = ix.view;
     hipStream_t st = (hipStream_t)stream;
     const char* forced = std::getenv("EPP_MOTIONS_KERNEL");
     const bool generic = forced && std::string(forced) == "generic";
@@ -751,7 +752,7 @@ epp_status epp_check_motions(const epp_world* world, const double* s1, const dou
     // k_motions_v5 when the world has tile tables and they, the records and the queues fit
     const bool force_v4 = forced && std::string(forced) == "v4";
     if (!generic && !force_v4 &&
-        launch_motions_v5(world, w, s1, s2, nullptr, 1, n, can_pass_gate, mode, valid, st))
+        launch_motions_v5(ix.dview, w, s1, s2, nullptr, 1, n, can_pass_gate, mode, valid, st))
         return launch_error("epp_check_motions");
     const int eb = env_int("EPP_MOTIONS_BLOCK", 0);
     const int block = eb == 512 ? 512 : eb == 1024 ? 1024 : (2u * (front + recb + extra_for(512)) <= 160u * 1024u ? 512 : 1024);
@@ -759,7 +760,7 @@ epp_status epp_check_motions(const epp_world* world, const double* s1, const dou
     if (!generic && front % 16 == 0 && shm <= 160u * 1024u) {
         const int grid = (int)std::max<int64_t>(
             1, std::min<int64_t>((n + block - 1) / block, (int64_t)cu_count() * std::max(1, (int)((160u * 1024u) / shm))));
-        const WorldView* dw = world_dview(world);
+        const WorldView* dw = ix.dview;
 #define EPP_LAUNCH_M(KERNEL)                                                                                           \
     do {                                                                                                               \
         allow_lds(KERNEL);                                                                                             \
@@ -792,13 +793,15 @@ epp_status epp_check_knn_motions(const epp_world* world, const double* nodes, co
     }
     const int64_t m = (int64_t)n * k;
     if (m == 0) return EPP_OK;
-    const SmallWorld sw = small_world(world);
+    SmallWorld sw = small_world(world);
     if (small_motions(sw, m) || std::getenv("EPP_MOTIONS_KERNEL")) {
         set_error("epp_check_knn_motions: not for this batch / world (use epp_knn_edges + epp_check_motions)");
         return EPP_ERR_UNSUPPORTED;
     }
-    if (const epp_status st = ensure_index(world)) return st;
-    if (!launch_motions_v5(world, world_view(world), nodes, nullptr, nbr, k, m, can_pass_gate, mode, valid,
+    sw.lease = {};
+    IndexLease ix;
+    if (const epp_status st = ensure_index(world, &ix)) return st;
+    if (!launch_motions_v5(ix.dview, ix.view, nodes, nullptr, nbr, k, m, can_pass_gate, mode, valid,
                            (hipStream_t)stream)) {
         set_error("epp_check_knn_motions: not for this batch / world (use epp_knn_edges + epp_check_motions)");
         return EPP_ERR_UNSUPPORTED;

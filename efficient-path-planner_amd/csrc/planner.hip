@@ -781,7 +781,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                                                            int* __restrict__ retry, double* __restrict__ retry_b,
                                                            int32_t* __restrict__ nbr, int mode,
                                                            unsigned long long* __restrict__ dbg) {
-    __shared__ float4 cand[kTileCap];                      // x, y, z (block-centre relative), id
+    __shared__ float4 cand[kTileCap];                      // x, y, z (block-centre relative), sorted position
     __shared__ uint16_t qh[kTileCap];                      // the block's queries (LDS positions)
     __shared__ int cst[kTileCells + 1];                    // halo cell -> LDS offset
     __shared__ uint32_t hist[kTileNB / 2][kTileThreads];  // [bin pair][query slot]
@@ -878,7 +878,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                     const int sg = cell0[u] + q;
                     const double x = sxyz[3 * sg], y = sxyz[3 * sg + 1], z = sxyz[3 * sg + 2];
                     cand[acc + q] = make_float4((float)(x - cen[0]), (float)(y - cen[1]), (float)(z - cen[2]),
-                                                __int_as_float(sidx[sg]));
+                                                __int_as_float(sg));  // (sorted position: see the exact phase)
                     if (inner) qh[q0 + q] = (uint16_t)(acc + q);
                 }
                 acc += cnt[u];
@@ -903,9 +903,10 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                 const bool live = qi < nq;
                 const int me = live ? qh[qi] : 0;
                 const float4 pf = cand[me];
-                const int self = __float_as_int(pf.w);
+                const int sself = __float_as_int(pf.w);  // the query's sorted position
+                const int self = sidx[sself];
                 // exact coordinates and cell (the row offsets; the final distances)
-                const double p[3] = {nodes[3 * (int64_t)self], nodes[3 * (int64_t)self + 1], nodes[3 * (int64_t)self + 2]};
+                const double p[3] = {sxyz[3 * (int64_t)sself], sxyz[3 * (int64_t)sself + 1], sxyz[3 * (int64_t)sself + 2]};
                 const int c[3] = {knn_cell_axis(p[0], g, 0), knn_cell_axis(p[1], g, 1), knn_cell_axis(p[2], g, 2)};
                 const int h0 = ((c[2] - oz - kTileH) * kTileE + (c[1] - oy - kTileH)) * kTileE + (c[0] - ox - kTileH);
                 const double fr[3] = {p[0] - (g.lo[0] + (double)c[0] * g.h), p[1] - (g.lo[1] + (double)c[1] * g.h),
@@ -926,7 +927,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                     auto bin = [&](int, float d, int j, bool valid) {
                         const int kb = max((int)(__float_as_uint(d * inv_t0) >> 21) - (127 << 2), 0);
-                        if (valid && j != self && kb < kTileNB) atomicAdd(&hist[kb >> 1][slot], 1u << ((kb & 1) << 4));
+                        if (valid && j != sself && kb < kTileNB) atomicAdd(&hist[kb >> 1][slot], 1u << ((kb & 1) << 4));
                     };
                     if (live) {
                         if (full) tile_rows(cst, cand, h0, sub, lpq, pf, bin);
@@ -958,7 +959,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                 if (live) {
                     const double thr2 = cut < 0 ? INFINITY : dcut + 3.0 * delta;
                     tile_rows_near(cst, cand, h0, sub, lpq, pf, fr, g.h, thr2, [&](int q, float d, int j, bool valid) {
-                        if (valid && j != self && d < dlist) {
+                        if (valid && j != sself && d < dlist) {
                             if (nown < kTileL) lst[nown][threadIdx.x] = (uint16_t)q;
                             ++nown;
                         }
@@ -1006,10 +1007,14 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                                 col += past ? 1 : 0;
                                 go = past;
                             }
+                            // (the halo's entries are its cells' contiguous runs of the cell-sorted
+                            // copy: these gathers hit the few KB the block's queries share in L1,
+                            // where the nodes' original order scattered them over the table)
                             const int q = lst[e][threadIdx.x + col];
-                            jj[u] = __float_as_int(cand[q].w);
-                            const double ddx = nodes[3 * (int64_t)jj[u]] - p[0], ddy = nodes[3 * (int64_t)jj[u] + 1] - p[1],
-                                         ddz = nodes[3 * (int64_t)jj[u] + 2] - p[2];
+                            const int sg = __float_as_int(cand[q].w);
+                            jj[u] = sidx[sg];
+                            const double ddx = sxyz[3 * (int64_t)sg] - p[0], ddy = sxyz[3 * (int64_t)sg + 1] - p[1],
+                                         ddz = sxyz[3 * (int64_t)sg + 2] - p[2];
                             dd[u] = (ddx * ddx + ddy * ddy) + ddz * ddz;
                         }
 #ifdef EPP_KNN_DIAG

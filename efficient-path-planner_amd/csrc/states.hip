@@ -788,15 +788,17 @@ epp_status epp_check_states(const epp_world* world, const double* xyz, int64_t n
         return EPP_ERR_INVALID_ARGUMENT;
     }
     if (n == 0) return EPP_OK;
-    const SmallWorld sw = small_world(world);
+    SmallWorld sw = small_world(world);
     if (small_states(sw, n)) {
         if (const epp_status st = launch_states_small(sw, false, xyz, n, can_pass_gate, 0.0, valid, compact_idx,
                                                       n_valid, (hipStream_t)stream))
             return st;
         return note_record_reader(world, sw, (hipStream_t)stream);
     }
-    if (const epp_status st = ensure_index(world)) return st;
-    return launch_states<false>(world_view(world), world_dview(world), xyz, n, can_pass_gate, 0.0, valid,
+    sw.lease = {};  // (a stale index is rebuilt below)
+    IndexLease ix;
+    if (const epp_status st = ensure_index(world, &ix)) return st;
+    return launch_states<false>(ix.view, ix.dview, xyz, n, can_pass_gate, 0.0, valid,
                                 compact_idx, n_valid, stream);
 }
 
@@ -816,15 +818,17 @@ epp_status epp_check_states_mindist(const epp_world* world, const double* xyz, i
         return EPP_ERR_INVALID_ARGUMENT;
     }
     if (n == 0) return EPP_OK;
-    const SmallWorld sw = small_world(world);
+    SmallWorld sw = small_world(world);
     if (small_states(sw, n)) {
         if (const epp_status st =
                 launch_states_small(sw, true, xyz, n, 0, min_distance, valid, nullptr, nullptr, (hipStream_t)stream))
             return st;
         return note_record_reader(world, sw, (hipStream_t)stream);
     }
-    if (const epp_status st = ensure_index(world)) return st;
-    return launch_states<true>(world_view(world), world_dview(world), xyz, n, 0, min_distance, valid, nullptr,
+    sw.lease = {};  // (a stale index is rebuilt below)
+    IndexLease ix;
+    if (const epp_status st = ensure_index(world, &ix)) return st;
+    return launch_states<true>(ix.view, ix.dview, xyz, n, 0, min_distance, valid, nullptr,
                                nullptr, stream);
 }
 

@@ -546,6 +546,7 @@ bool upload(HostWorld& hw) {
     }
     hw.view.blob = (const unsigned char*)hw.d_blob;
     hw.d_view = reinterpret_cast<const WorldView*>(static_cast<char*>(hw.d_blob) + view_off);
+    hw.dev_view = hw.view;
     std::memcpy(hw.h_stage, hw.blob.data(), bytes);
     std::memcpy(static_cast<char*>(hw.h_stage) + view_off, &hw.view, sizeof(WorldView));
     e = hipMemcpyAsync(hw.d_blob, hw.h_stage, need, hipMemcpyHostToDevice, hw.stream);
@@ -563,9 +564,6 @@ bool upload(HostWorld& hw) {
 
 struct epp_world : epp::HostWorld {};
 
-namespace epp {
-epp_status ensure_index(const epp_world* w);
-}
 
 extern "C" {
 
@@ -630,7 +628,7 @@ epp_status epp_world_build_index(const epp_world* w) {
         epp::set_error("epp_world_build_index: invalid argument");
         return EPP_ERR_INVALID_ARGUMENT;
     }
-    return epp::ensure_index(w);
+    return epp::ensure_index(w, nullptr);
 }
 
 epp_status epp_world_generation(const epp_world* w, uint64_t* generation) {
@@ -656,33 +654,51 @@ epp_status epp_world_get_aabbs(const epp_world* w, double* lo_hi) {
 
 }  // extern "C"
 
-// Accessor for the kernels' launchers (states.hip, motions.hip, planner.hip).
 namespace epp {
-const WorldView& world_view(const epp_world* w) { return w->view; }
-const WorldView* world_dview(const epp_world* w) { return w->d_view; }
 
 // The device index of the current version: rebuilt and uploaded here when an update made
-// it stale (after every kernel that may still read the old blob has finished).
-epp_status ensure_index(const epp_world* cw) {
+// it stale (exclusively: after every launcher holding a lease has queued its kernel, and
+// after every kernel that may still read the old blob has finished).  With a lease, a
+// snapshot of the uploaded index that stays valid until the lease is released.
+epp_status ensure_index(const epp_world* cw, IndexLease* lease) {
     HostWorld& hw = const_cast<epp_world&>(*cw);
-    std::lock_guard<std::mutex> lk(hw.mu);
-    if (!hw.index_stale) return EPP_OK;
-    (void)hipDeviceSynchronize();
-    if (!build_blob(hw, hw.obbs.data(), (int)hw.obbs.size())) return EPP_ERR_UNSUPPORTED;
-    if (!upload(hw)) return EPP_ERR_HIP;
-    hw.index_stale = false;
+    bool stale;
+    {
+        std::lock_guard<std::mutex> lk(hw.mu);
+        stale = hw.index_stale;
+    }
+    if (stale) {
+        std::unique_lock<std::shared_mutex> ix(hw.index_mu);
+        std::lock_guard<std::mutex> lk(hw.mu);
+        if (hw.index_stale) {
+            (void)hipDeviceSynchronize();
+            if (!build_blob(hw, hw.obbs.data(), (int)hw.obbs.size())) return EPP_ERR_UNSUPPORTED;
+            if (!upload(hw)) return EPP_ERR_HIP;
+            hw.index_stale = false;
+        }
+    }
+    if (lease) {
+        // (an update after the rebuild above leaves the uploaded index consistent: the
+        // launch checks the version it snapshots, as if it had run before the update)
+        lease->lk = std::shared_lock<std::shared_mutex>(hw.index_mu);
+        std::lock_guard<std::mutex> lk(hw.mu);
+        lease->view = hw.dev_view;
+        lease->dview = hw.d_view;
+    }
     return EPP_OK;
 }
 
 SmallWorld small_world(const epp_world* cw) {
     HostWorld& hw = const_cast<epp_world&>(*cw);
+    std::shared_lock<std::shared_mutex> ix(hw.index_mu);
     std::lock_guard<std::mutex> lk(hw.mu);
     SmallWorld s;
-    s.recs = hw.index_stale ? hw.h_recs : reinterpret_cast<const double*>(hw.view.blob + hw.view.off_aos);
+    s.recs = hw.index_stale ? hw.h_recs : reinterpret_cast<const double*>(hw.dev_view.blob + hw.dev_view.off_aos);
     s.host_slot = hw.index_stale ? hw.rec_slot : -1;
     s.n_obb = (int32_t)hw.obbs.size();
     s.r_gate = hw.r_gate;
     s.r_obst = hw.r_obst;
+    if (!hw.index_stale) s.lease = std::move(ix);  // the device records: no rebuild until launched
     return s;
 }
 

@@ -590,3 +590,45 @@ def test_knn_motions_unsupported_small_batch(cfg, geom):
     d_n, d_k, d_v = capi.DeviceBuffer.from_array(nodes), capi.DeviceBuffer.from_array(nbr), capi.DeviceBuffer(32)
     rc = capi.lib().epp_check_knn_motions(w.handle, d_n.ptr, d_k.ptr, 8, 4, 0, 0, d_v.ptr, None)
     assert rc == capi.EPP_ERR_UNSUPPORTED
+
+
+def test_updates_racing_large_checks(geom, worlds):
+    """One thread updates the world back and forth between C2 (64 OBBs) and C3 (512 OBBs:
+    the index grows, the device blob is reallocated) while another launches large state and
+    motion checks.  A launch holds its snapshot of the device index until it is queued
+    (IndexLease), so every answer is the oracle's for one of the two versions, never a mix
+    or a read of a freed blob."""
+    import threading
+    rg, ro, ws = worlds
+    (g2, o2, (lo, hi)), (g3, o3, _) = ws["c2"], ws["c3"]
+    obbs = [capi.build_obbs(geom, g2, o2), capi.build_obbs(geom, g3, o3)]
+    refs = [O.world_build(geom, g2, o2, rg, ro), O.world_build(geom, g3, o3, rg, ro)]
+    pts = synth.sample_states(11, lo, hi, 1 << 17)
+    s1, s2 = synth.edges(12, 8, lo, hi, 1 << 14)
+    exp_s = [O.check_states(r, rg, ro, pts) for r in refs]
+    exp_m = [O.check_motions(r, rg, ro, s1, s2) for r in refs]
+    world = capi.World(obbs[0], rg, ro)
+    stop, err = threading.Event(), []
+
+    def updater():
+        k = 1
+        try:
+            while not stop.is_set():
+                world.update(obbs[k % 2])
+                k += 1
+        except Exception as e:  # pragma: no cover - reported below
+            err.append(e)
+
+    t = threading.Thread(target=updater)
+    t.start()
+    try:
+        for i in range(24):
+            got = world.check_states(pts)
+            assert any(np.array_equal(got, e) for e in exp_s), f"states call {i}: no version matches"
+            got = world.check_motions(s1, s2)
+            assert any(np.array_equal(got, e) for e in exp_m), f"motions call {i}: no version matches"
+    finally:
+        stop.set()
+        t.join()
+    assert not err, err
+    world.close()
