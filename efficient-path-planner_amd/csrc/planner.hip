@@ -787,6 +787,8 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
     __shared__ uint32_t hist[kTileNB / 2][kTileThreads];  // [bin pair][query slot]
     __shared__ uint16_t lst[kTileL][kTileThreads];         // [entry][lane]: each lane's own list
     __shared__ int wsum[kTileThreads / 64];
+    __shared__ uint8_t s_nown[kTileThreads];  // list entries per lane (saturated)
+    __shared__ int8_t s_cut[kTileThreads];    // histogram cut per query slot
     __shared__ int s_nq, s_b;
     const KnnGrid g = *gp;
     const int nbx = (g.dims[0] + kTileB - 1) / kTileB, nby = (g.dims[1] + kTileB - 1) / kTileB,
@@ -895,16 +897,14 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
             // queries would cost the block ~45 us: the kernel's slowest blocks)
             const int lpq = nq <= kTileThreads / 4 ? 4 : nq <= kTileThreads / 2 ? 2 : 1;
             const int slot = threadIdx.x / lpq, sub = threadIdx.x % lpq;
-            // (a query's lpq lanes are adjacent lanes of one wave: its histogram is combined
-            // by lane shuffles and its list entries are read back by the same wave, so the
-            // query rounds need no workgroup barrier)
+            // (a query's lpq lanes are adjacent lanes of one wave: its histogram needs no
+            // workgroup barrier; the exact phase reads the lists on other threads, after one)
             for (int qb = 0; qb < nq; qb += kTileThreads / lpq) {  // block-uniform
                 const int qi = qb + slot;
                 const bool live = qi < nq;
                 const int me = live ? qh[qi] : 0;
                 const float4 pf = cand[me];
                 const int sself = __float_as_int(pf.w);  // the query's sorted position
-                const int self = sidx[sself];
                 // exact coordinates and cell (the row offsets; the final distances)
                 const double p[3] = {sxyz[3 * (int64_t)sself], sxyz[3 * (int64_t)sself + 1], sxyz[3 * (int64_t)sself + 2]};
                 const int c[3] = {knn_cell_axis(p[0], g, 0), knn_cell_axis(p[1], g, 1), knn_cell_axis(p[2], g, 2)};
@@ -965,14 +965,26 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                         }
                     });
                 }
-                // the other lanes' entry counts (the same wave: its LDS writes are ordered
-                // before the reads below)
-                int ncol[4] = {nown, 0, 0, 0};
-#pragma unroll
-                for (int o = 1; o < 4; ++o) ncol[o] = __shfl((int)nown, (int)(threadIdx.x & 63) + (o < lpq ? o : 0), 64);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                // The exact phase runs compacted: query slot t on thread t, i.e. the first
+                // 256 / lpq threads as full waves (with lpq lanes per query only one lane of
+                // each would work, and the idle lanes would still take the SIMD's issue
+                // cycles).  The list counts and cuts go through LDS, ordered by a barrier.
+                s_nown[threadIdx.x] = (uint8_t)min(nown, 255);
+                if (sub == 0) s_cut[slot] = (int8_t)cut;
+                __syncthreads();
                 EPP_KTL(4);
-                if (!live || sub != 0) continue;
+                const int qx = qb + (int)threadIdx.x;
+                if ((int)threadIdx.x < kTileThreads / lpq && qx < nq) {
+                const int tcol = (int)threadIdx.x * lpq;  // the query's first list column
+                const int sx = __float_as_int(cand[qh[qx]].w);
+                const int self = sidx[sx];
+                const double p[3] = {sxyz[3 * (int64_t)sx], sxyz[3 * (int64_t)sx + 1], sxyz[3 * (int64_t)sx + 2]};
+                const int c[3] = {knn_cell_axis(p[0], g, 0), knn_cell_axis(p[1], g, 1), knn_cell_axis(p[2], g, 2)};
+                const int cutx = s_cut[threadIdx.x];
+                const double dcut = cutx < 0 ? INFINITY : (double)__uint_as_float((uint32_t)(cutx + 1 + (127 << 2)) << 21) * t0;
+                int ncol[4];
+#pragma unroll
+                for (int o = 0; o < 4; ++o) ncol[o] = o < lpq ? (int)s_nown[tcol + o] : 0;
                 int nl = 0;
                 bool ok = true;
                 double rbound = INFINITY;  // (none: the retry walks shells)
@@ -1010,7 +1022,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                             // (the halo's entries are its cells' contiguous runs of the cell-sorted
                             // copy: these gathers hit the few KB the block's queries share in L1,
                             // where the nodes' original order scattered them over the table)
-                            const int q = lst[e][threadIdx.x + col];
+                            const int q = lst[e][tcol + col];
                             const int sg = __float_as_int(cand[q].w);
                             jj[u] = sidx[sg];
                             const double ddx = sxyz[3 * (int64_t)sg] - p[0], ddy = sxyz[3 * (int64_t)sg + 1] - p[1],
@@ -1046,6 +1058,8 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
 #ifdef EPP_KNN_DIAG
                 if (tl[5] == 0ull) tl[5] = __builtin_amdgcn_s_memrealtime();
 #endif
+                }
+                __syncthreads();  // the next round rewrites the lists, histograms and counts
             }
             EPP_KTL(6);
         } else {

@@ -128,8 +128,9 @@ epp_status epp_world_create(const epp_obb* obbs, int32_t n_obbs, double r_gate, 
  * edges on worlds of <= 256 OBBs) read those directly; the device index is rebuilt and
  * uploaded by the first call that needs it (or epp_world_build_index), after every kernel
  * that may read the old index, so an index error (e.g. too many distinct candidate
- * lists) is reported there.  No call reading this world may run on another host thread
- * meanwhile (kernels already queued on streams may).  HIP graphs
+ * lists) is reported there.  Checks may run on other host threads meanwhile: each launch
+ * uses the version of the index it finds (the one before or after the update, never a mix;
+ * a rebuild waits until launches holding the old one are queued).  HIP graphs
  * that captured launches on this world must be re-captured afterwards, and only after
  * epp_world_build_index (launch shapes depend on the index; epp_world_generation
  * changes). */
