@@ -43,7 +43,7 @@ for r in range(50):
     f(r)
 us = float(np.median([timed_kernel_ms(capi, st, f, 200) for _ in range(3)])) * 1e3
 print(os.path.basename(lib or "libepp.so"), " ".join(a for a in args if "=" in a),
-      f"c2 {us:.3f} us  {25 * N / us / 1e6:.0f} GB/s", flush=True)
+      f"c2 {us:.3f} us  {25 * N / us / 1e6:.2f} TB/s", flush=True)
 if stream_floor:
     so = os.path.join(ROOT, "scripts", "dbg", "libdiag.so")
     diag = C.CDLL(so)
@@ -54,4 +54,4 @@ if stream_floor:
             for r in range(20):
                 fs(r)
             us = float(np.median([timed_kernel_ms(capi, st, fs, 200) for _ in range(3)])) * 1e3
-            print(f"stream mode{mode} blocks {blocks}: {us:.3f} us  {25 * N / us / 1e6:.0f} GB/s", flush=True)
+            print(f"stream mode{mode} blocks {blocks}: {us:.3f} us  {25 * N / us / 1e6:.2f} TB/s", flush=True)
