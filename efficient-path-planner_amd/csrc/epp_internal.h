@@ -52,9 +52,10 @@ epp_status generate_trajectory_into(const double* wp, int32_t n_wp, const double
                                     double a_max, double dt, double t0, const double v0[3], const double a0[3],
                                     double* (*alloc)(void*, int64_t), void* ctx, int64_t* n_rows);
 // epp_mask_edges_count without clearing `count` first: the counts are added to what it
-// holds (the planner clears them with its first upload).
+// holds (the planner clears them with its first upload).  out16 != NULL: also a copy of
+// the masked table as u16, 0xFFFF for no edge (node counts <= 65535).
 epp_status mask_edges_count_acc(int32_t* nbr, const uint8_t* valid, int64_t m, int32_t target, int64_t* count,
-                                void* stream);
+                                void* stream, uint16_t* out16 = nullptr);
 }  // namespace epp
 
 namespace epp {

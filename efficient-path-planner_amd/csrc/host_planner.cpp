@@ -180,16 +180,28 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
         check(ks, "motion check");
     }
     // failed motions -> -1; the valid edges, and those into the goal (node 1)
-    check(mask_edges_count_acc(d_nbr, d_ev, (int64_t)m, 1, d_ecnt, st), "mask edges");  // (counters zeroed above)
+    // Up to 65535 nodes the table goes down as u16 (0xFFFF: no edge), half the bytes of the
+    // largest download; its copy is written by the mask kernel into d_e1, free by then.
+    const bool narrow = n <= 65535;
+    uint16_t* d_nbr16 = narrow ? reinterpret_cast<uint16_t*>(d_e1) : nullptr;
+    check(mask_edges_count_acc(d_nbr, d_ev, (int64_t)m, 1, d_ecnt, st, d_nbr16), "mask edges");  // (counters zeroed above)
     // node coordinates and the masked k-NN table into pinned host staging
     // (sized for the attempt's largest node count, not this one's: a pinned buffer that
     // grows is freed and reallocated, and hipHostFree waits for the whole device)
     const double* nodes = static_cast<const double*>(ts.pinned(0, max_nodes * 24));
-    const int32_t* nbr = static_cast<const int32_t*>(ts.pinned(1, m_max * 4));
+    void* h_tab = ts.pinned(1, m_max * 4);
+    const int32_t* nbr32 = static_cast<const int32_t*>(h_tab);
+    const uint16_t* nbr16 = static_cast<const uint16_t*>(h_tab);
+    auto nbr = [&](size_t e) -> int {
+        if (!narrow) return nbr32[e];
+        const uint16_t x = nbr16[e];
+        return x == 0xFFFF ? -1 : (int)x;
+    };
     // the three downloads queued back to back, one synchronisation
     int64_t* ecnt = h_cnt + 1;
     check(epp_memcpy_d2h_async(ecnt, d_ecnt, 16, st), "download");
-    check(epp_memcpy_d2h_async(const_cast<int32_t*>(nbr), d_nbr, m * 4, st), "download");
+    if (narrow) check(epp_memcpy_d2h_async(h_tab, d_nbr16, m * 2, st), "download");
+    else check(epp_memcpy_d2h_async(h_tab, d_nbr, m * 4, st), "download");
     check(epp_memcpy_d2h_async(const_cast<double*>(nodes), d_nodes, (uint64_t)n * 24, st), "download");
     check(epp_stream_sync(st), "sync");
     const int64_t n_valid_edges = ecnt[0];
@@ -240,7 +252,7 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
             const Vec3 pu = node(u);
             const size_t e0 = (size_t)u * k;
             for (int c = 0; c < k; ++c) {
-                const int v = nbr[e0 + c];
+                const int v = nbr(e0 + c);
                 if (v >= 0) relax(u, pu, v);
             }
             if (with_reverse)
@@ -253,14 +265,14 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     if (!goal_has_forward_edge || !astar(false)) {
         roff.assign(n + 1, 0);
         for (size_t e = 0; e < m; ++e)
-            if (nbr[e] >= 0) ++roff[nbr[e] + 1];
+            if (nbr(e) >= 0) ++roff[nbr(e) + 1];
         for (int i = 0; i < n; ++i) roff[i + 1] += roff[i];
         radj.resize(roff[n]);
         std::vector<int32_t> fill(roff.begin(), roff.end() - 1);
         for (int i = 0; i < n; ++i)
             for (int c = 0; c < k; ++c) {
                 const size_t e = (size_t)i * k + c;
-                if (nbr[e] >= 0) radj[fill[nbr[e]]++] = i;
+                if (nbr(e) >= 0) radj[fill[nbr(e)]++] = i;
             }
         astar(true);
     }

@@ -1320,7 +1320,8 @@ constexpr int kMaskThreads = 1024;
 __global__ __launch_bounds__(kMaskThreads) void k_mask_edges_count(int32_t* __restrict__ nbr,
                                                                    const uint8_t* __restrict__ valid, int64_t m,
                                                                    int32_t target,
-                                                                   unsigned long long* __restrict__ count) {
+                                                                   unsigned long long* __restrict__ count,
+                                                                   uint16_t* __restrict__ out16) {
     __shared__ uint32_t part[2][kMaskThreads / 64];
     uint32_t c = 0, ci = 0;
     for (int64_t e = (int64_t)blockIdx.x * kMaskThreads + threadIdx.x; e < m;
@@ -1329,6 +1330,7 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_edges_count(int32_t* __re
         const bool ok = valid[e] != 0;
         if (!ok) nbr[e] = -1;
         const bool keep = ok && v >= 0;
+        if (out16) out16[e] = keep ? (uint16_t)v : (uint16_t)0xFFFF;  // (a narrow copy for the download)
         c += keep ? 1u : 0u;
         ci += (keep && v == target) ? 1u : 0u;
     }
@@ -1548,7 +1550,7 @@ epp_status epp_mask_edges_count(int32_t* nbr, const uint8_t* valid, int64_t m, i
 }  // extern "C"
 
 epp_status epp::mask_edges_count_acc(int32_t* nbr, const uint8_t* valid, int64_t m, int32_t target, int64_t* count,
-                                     void* stream) {
+                                     void* stream, uint16_t* out16) {
     if (m < 0 || !count || (m > 0 && (!nbr || !valid))) {
         set_error("epp_mask_edges_count: invalid argument");
         return EPP_ERR_INVALID_ARGUMENT;
@@ -1557,7 +1559,7 @@ epp_status epp::mask_edges_count_acc(int32_t* nbr, const uint8_t* valid, int64_t
     if (m == 0) return EPP_OK;
     const int64_t blocks = std::min<int64_t>((m + kMaskThreads - 1) / kMaskThreads, 256);
     hipLaunchKernelGGL(k_mask_edges_count, dim3((unsigned)blocks), dim3(kMaskThreads), 0, s, nbr, valid, m, target,
-                       reinterpret_cast<unsigned long long*>(count));
+                       reinterpret_cast<unsigned long long*>(count), out16);
     return last("epp_mask_edges_count");
 }
 

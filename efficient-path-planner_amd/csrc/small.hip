@@ -37,40 +37,37 @@ __device__ __forceinline__ void publish_done(uint32_t* done, uint32_t seq) {
 // of up to 128 OBBs in flight at once (the records may be in host memory: one PCIe round
 // trip instead of one per few loads); `before` runs between the loads and the stores
 // (the caller issues its own loads there, so they overlap too).
-template <int BLK, typename F>
+template <typename F>
 __device__ __forceinline__ void stage_records(double* srec, const double* recs, int nd, F&& before) {
-    constexpr int kQ = (128 * kRecDoubles / 2 + BLK - 1) / BLK;  // 16-byte loads per lane
+    constexpr int kQ = (128 * kRecDoubles / 2 + kSmallBlock - 1) / kSmallBlock;  // 16-byte loads per lane
     const int n2 = nd / 2;
     const double2* s2 = reinterpret_cast<const double2*>(recs);
     double2* d2 = reinterpret_cast<double2*>(srec);
     double2 v[kQ];
 #pragma unroll
     for (int q = 0; q < kQ; ++q) {
-        const int e = threadIdx.x + q * BLK;
+        const int e = threadIdx.x + q * kSmallBlock;
         v[q] = e < n2 ? s2[e] : make_double2(0.0, 0.0);
     }
     before();
 #pragma unroll
     for (int q = 0; q < kQ; ++q) {
-        const int e = threadIdx.x + q * BLK;
+        const int e = threadIdx.x + q * kSmallBlock;
         if (e < n2) d2[e] = v[q];
     }
-    for (int e = threadIdx.x + kQ * BLK; e < n2; e += BLK) d2[e] = s2[e];  // (> 128 OBBs)
+    for (int e = threadIdx.x + kQ * kSmallBlock; e < n2; e += kSmallBlock) d2[e] = s2[e];  // (> 128 OBBs)
     if ((nd & 1) && threadIdx.x == 0) srec[nd - 1] = recs[nd - 1];  // (odd OBB count: 136-byte records)
 }
 
 // A workgroup takes `per` queries (64, 128 or 256) and splits the OBB list into
-// BLK / per slices, one per group of `per` threads: the few hundred queries of a
+// kSmallBlock / per slices, one per group of `per` threads: the few hundred queries of a
 // latency-path call keep every wave of the workgroup busy, and each wave walks a shorter
-// list.  A slice's hit marks the query's LDS flag; slice 0 writes the answers.  A call
-// that fits one workgroup (<= 256 queries: the lookahead check) runs 1024 threads, i.e.
-// 4x the slices: a quarter of the OBB walk per wave on the call's critical path.
+// list.  A slice's hit marks the query's LDS flag; slice 0 writes the answers.
 __host__ __device__ inline int small_per(int64_t n) { return n <= 64 ? 64 : (n <= 128 ? 128 : kSmallBlock); }
 __host__ __device__ inline size_t small_shm(int n_obb) { return (((size_t)n_obb * kRecDoubles + 1) & ~size_t(1)) * 8 + kSmallBlock * 4; }
 
-constexpr int kSmallWide = 1024;
-template <bool MINDIST, bool COMPACT, int BLK>
-__global__ __launch_bounds__(BLK) void k_states_small(const double* __restrict__ recs, int n_obb, double rg,
+template <bool MINDIST, bool COMPACT>
+__global__ __launch_bounds__(kSmallBlock) void k_states_small(const double* __restrict__ recs, int n_obb, double rg,
                                                               double ro, const double* __restrict__ xyz, int64_t n,
                                                               int per, int can_pass, double md,
                                                               uint8_t* __restrict__ valid,
@@ -79,11 +76,11 @@ __global__ __launch_bounds__(BLK) void k_states_small(const double* __restrict__
                                                               uint32_t* done, uint32_t seq) {
     extern __shared__ double srec[];
     uint32_t* s_hit = reinterpret_cast<uint32_t*>(srec + (((size_t)n_obb * kRecDoubles + 1) & ~size_t(1)));
-    const int t = threadIdx.x, slices = BLK / per, slice = t / per, j = t - slice * per;
+    const int t = threadIdx.x, slices = kSmallBlock / per, slice = t / per, j = t - slice * per;
     const int64_t i = (int64_t)blockIdx.x * per + j;
     const bool act = i < n;
     double px = 0.0, py = 0.0, pz = 0.0;
-    stage_records<BLK>(srec, recs, n_obb * kRecDoubles, [&] {
+    stage_records(srec, recs, n_obb * kRecDoubles, [&] {
         if (act) {
             px = xyz[3 * i];
             py = xyz[3 * i + 1];
@@ -127,19 +124,19 @@ __global__ __launch_bounds__(BLK) void k_states_small(const double* __restrict__
     publish_done(done, seq);
 }
 
-template <int MODE, int BLK>
-__global__ __launch_bounds__(BLK) void k_motions_small(const double* __restrict__ recs, int n_obb, double rg,
+template <int MODE>
+__global__ __launch_bounds__(kSmallBlock) void k_motions_small(const double* __restrict__ recs, int n_obb, double rg,
                                                                double ro, const double* __restrict__ s1,
                                                                const double* __restrict__ s2, int64_t n, int per,
                                                                int can_pass, uint8_t* __restrict__ valid,
                                                                uint32_t* done, uint32_t seq) {
     extern __shared__ double srec[];
     uint32_t* s_hit = reinterpret_cast<uint32_t*>(srec + (((size_t)n_obb * kRecDoubles + 1) & ~size_t(1)));
-    const int t = threadIdx.x, slices = BLK / per, slice = t / per, j = t - slice * per;
+    const int t = threadIdx.x, slices = kSmallBlock / per, slice = t / per, j = t - slice * per;
     const int64_t i = (int64_t)blockIdx.x * per + j;
     const bool act = i < n;
     double s[3] = {0.0, 0.0, 0.0}, e[3] = {0.0, 0.0, 0.0}, lo[3], hi[3];
-    stage_records<BLK>(srec, recs, n_obb * kRecDoubles, [&] {
+    stage_records(srec, recs, n_obb * kRecDoubles, [&] {
         if (act) {
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
@@ -211,18 +208,12 @@ epp_status launch_states_small(const SmallWorld& sw, bool mindist, const double*
     const int per = small_per(n), grid = (int)((n + per - 1) / per);
     const size_t shm = small_shm(sw.n_obb);
     auto nv = reinterpret_cast<unsigned long long*>(n_valid);
-#define EPP_LAUNCH_SS(M, C, B)                                                                                    \
-    hipLaunchKernelGGL((k_states_small<M, C, B>), dim3(grid), dim3(B), shm, st, sw.recs, sw.n_obb, sw.r_gate,     \
+#define EPP_LAUNCH_SS(M, C)                                                                                          \
+    hipLaunchKernelGGL((k_states_small<M, C>), dim3(grid), dim3(kSmallBlock), shm, st, sw.recs, sw.n_obb, sw.r_gate, \
                        sw.r_obst, xyz, n, per, can_pass, md, valid, compact_idx, nv, done, seq)
-#define EPP_LAUNCH_SSB(B)                               \
-    do {                                                \
-        if (mindist) EPP_LAUNCH_SS(true, false, B);     \
-        else if (compact_idx) EPP_LAUNCH_SS(false, true, B); \
-        else EPP_LAUNCH_SS(false, false, B);            \
-    } while (0)
-    if (grid == 1) EPP_LAUNCH_SSB(kSmallWide);
-    else EPP_LAUNCH_SSB(kSmallBlock);
-#undef EPP_LAUNCH_SSB
+    if (mindist) EPP_LAUNCH_SS(true, false);
+    else if (compact_idx) EPP_LAUNCH_SS(false, true);
+    else EPP_LAUNCH_SS(false, false);
 #undef EPP_LAUNCH_SS
     return launch_error(mindist ? "epp_check_states_mindist" : "epp_check_states");
 }
@@ -231,17 +222,12 @@ epp_status launch_motions_small(const SmallWorld& sw, int32_t mode, const double
                                 int32_t can_pass, uint8_t* valid, hipStream_t st, uint32_t* done, uint32_t seq) {
     const int per = small_per(n), grid = (int)((n + per - 1) / per);
     const size_t shm = small_shm(sw.n_obb);
-#define EPP_LAUNCH_MS(M, B)                                                                                       \
-    hipLaunchKernelGGL((k_motions_small<M, B>), dim3(grid), dim3(B), shm, st, sw.recs, sw.n_obb, sw.r_gate,       \
-                       sw.r_obst, s1, s2, n, per, can_pass, valid, done, seq)
-    if (grid == 1) {
-        if (mode == 0) EPP_LAUNCH_MS(0, kSmallWide);
-        else EPP_LAUNCH_MS(1, kSmallWide);
-    } else {
-        if (mode == 0) EPP_LAUNCH_MS(0, kSmallBlock);
-        else EPP_LAUNCH_MS(1, kSmallBlock);
-    }
-#undef EPP_LAUNCH_MS
+    if (mode == 0)
+        hipLaunchKernelGGL((k_motions_small<0>), dim3(grid), dim3(kSmallBlock), shm, st, sw.recs, sw.n_obb, sw.r_gate,
+                           sw.r_obst, s1, s2, n, per, can_pass, valid, done, seq);
+    else
+        hipLaunchKernelGGL((k_motions_small<1>), dim3(grid), dim3(kSmallBlock), shm, st, sw.recs, sw.n_obb, sw.r_gate,
+                           sw.r_obst, s1, s2, n, per, can_pass, valid, done, seq);
     return launch_error("epp_check_motions");
 }
 
