@@ -162,6 +162,12 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     check(epp_stream_sync(st), "sync");
     const int64_t n_valid_states = h_cnt[0];
     const int32_t n = (int32_t)(n_valid_states + 2);
+    // the node coordinates (final now) go down on the copy stream while the k-NN and the
+    // motion checks run on this one (pinned staging sized for the attempt's largest node
+    // count: a pinned buffer that grows is freed, and hipHostFree waits for the device)
+    void* cst = ts.copy_stream();
+    const double* nodes = static_cast<const double*>(ts.pinned(0, max_nodes * 24));
+    check(epp_memcpy_d2h_async(const_cast<double*>(nodes), d_nodes, (uint64_t)n * 24, cst), "download");
     // ---- 2. k-NN graph + batched motion checks (MotionValidator::checkMotion) --------
     const size_t m = (size_t)n * k;
     // the grid over the sampling box widened by start and goal (every node lies inside)
@@ -185,10 +191,7 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     const bool narrow = n <= 65535;
     uint16_t* d_nbr16 = narrow ? reinterpret_cast<uint16_t*>(d_e1) : nullptr;
     check(mask_edges_count_acc(d_nbr, d_ev, (int64_t)m, 1, d_ecnt, st, d_nbr16), "mask edges");  // (counters zeroed above)
-    // node coordinates and the masked k-NN table into pinned host staging
-    // (sized for the attempt's largest node count, not this one's: a pinned buffer that
-    // grows is freed and reallocated, and hipHostFree waits for the whole device)
-    const double* nodes = static_cast<const double*>(ts.pinned(0, max_nodes * 24));
+    // the masked k-NN table into pinned host staging (sized as the nodes' staging)
     void* h_tab = ts.pinned(1, m_max * 4);
     const int32_t* nbr32 = static_cast<const int32_t*>(h_tab);
     const uint16_t* nbr16 = static_cast<const uint16_t*>(h_tab);
@@ -197,13 +200,13 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
         const uint16_t x = nbr16[e];
         return x == 0xFFFF ? -1 : (int)x;
     };
-    // the three downloads queued back to back, one synchronisation
+    // the two downloads queued back to back, one synchronisation (and the nodes' stream)
     int64_t* ecnt = h_cnt + 1;
     check(epp_memcpy_d2h_async(ecnt, d_ecnt, 16, st), "download");
     if (narrow) check(epp_memcpy_d2h_async(h_tab, d_nbr16, m * 2, st), "download");
     else check(epp_memcpy_d2h_async(h_tab, d_nbr, m * 4, st), "download");
-    check(epp_memcpy_d2h_async(const_cast<double*>(nodes), d_nodes, (uint64_t)n * 24, st), "download");
     check(epp_stream_sync(st), "sync");
+    check(epp_stream_sync(cst), "sync");
     const int64_t n_valid_edges = ecnt[0];
     const bool goal_has_forward_edge = ecnt[1] > 0;
     const auto t_dev1 = std::chrono::steady_clock::now();

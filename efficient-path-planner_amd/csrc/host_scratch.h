@@ -33,6 +33,11 @@ public:
         if (!stream_) check(epp_stream_create(&stream_), "stream");
         return stream_;
     }
+    // A second stream for copies that overlap the first stream's kernels.
+    void* copy_stream() {
+        if (!cstream_) check(epp_stream_create(&cstream_), "stream");
+        return cstream_;
+    }
     // Device buffer of at least `bytes`, 256-byte aligned sub-allocations handed out
     // by `carve` until the next reset().
     void reset(size_t bytes) {
@@ -76,10 +81,12 @@ public:
         for (void* p : pin_)
             if (p) (void)hipHostFree(p);
         if (stream_) epp_stream_destroy(stream_);
+        if (cstream_) epp_stream_destroy(cstream_);
     }
 
 private:
     void* stream_ = nullptr;
+    void* cstream_ = nullptr;
     void* buf_ = nullptr;
     size_t cap_ = 0, used_ = 0;
     void* pin_[3] = {nullptr, nullptr, nullptr};
