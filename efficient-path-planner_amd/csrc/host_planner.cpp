@@ -225,32 +225,62 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     }
     auto node = [&](int v) { return Vec3(nodes[3 * v], nodes[3 * v + 1], nodes[3 * v + 2]); };
     const Vec3 gp = node(1);
-    std::vector<double> dist(n);
-    std::vector<int> prev(n);
-    std::vector<uint8_t> closed(n);
-    std::vector<int32_t> roff, radj;  // reverse edges (second pass only)
+    // Search state per host thread, reused across calls: a node's dist / prev hold this
+    // search's values only when its stamp is the search's (no O(n) clearing per search:
+    // A* touches a small part of the ~63k nodes); the heap keeps its storage.
     using QE = std::pair<double, int>;  // (g + h, node)
+    struct SearchState {
+        std::vector<double> dist;
+        std::vector<int> prev;
+        std::vector<uint32_t> seen, done;  // stamps: dist/prev valid, closed
+        std::vector<QE> heap;
+        uint32_t cur = 0;
+    };
+    thread_local SearchState ss;
+    if (ss.dist.size() < (size_t)n) {
+        ss.dist.resize(n);
+        ss.prev.resize(n);
+        ss.seen.resize(n, 0u);
+        ss.done.resize(n, 0u);
+    }
+    std::vector<int32_t> roff, radj;  // reverse edges (second pass only)
+    auto dist_of = [&](int v) { return ss.seen[v] == ss.cur ? ss.dist[v] : std::numeric_limits<double>::infinity(); };
+    auto prev_of = [&](int v) { return ss.seen[v] == ss.cur ? ss.prev[v] : -1; };
     auto astar = [&](bool with_reverse) {
-        std::fill(dist.begin(), dist.end(), std::numeric_limits<double>::infinity());
-        std::fill(prev.begin(), prev.end(), -1);
-        std::fill(closed.begin(), closed.end(), 0);
-        std::priority_queue<QE, std::vector<QE>, std::greater<QE>> q;
-        dist[0] = 0.0;
-        q.push({(node(0) - gp).norm(), 0});
+        if (++ss.cur == 0u) {  // (stamp wrap-around: clear once)
+            std::fill(ss.seen.begin(), ss.seen.end(), 0u);
+            std::fill(ss.done.begin(), ss.done.end(), 0u);
+            ss.cur = 1u;
+        }
+        // (the heap as std::priority_queue keeps it: push_heap / pop_heap with std::greater,
+        // over storage reused across searches)
+        std::vector<QE>& q = ss.heap;
+        q.clear();
+        const std::greater<QE> cmp;
+        auto push = [&](QE e) {
+            q.push_back(e);
+            std::push_heap(q.begin(), q.end(), cmp);
+        };
+        ss.seen[0] = ss.cur;
+        ss.dist[0] = 0.0;
+        ss.prev[0] = -1;
+        push({(node(0) - gp).norm(), 0});
         auto relax = [&](int u, const Vec3& pu, int v) {
-            if (closed[v]) return;
-            const double nd = dist[u] + (node(v) - pu).norm();
-            if (nd < dist[v]) {
-                dist[v] = nd;
-                prev[v] = u;
-                q.push({nd + (node(v) - gp).norm(), v});
+            if (ss.done[v] == ss.cur) return;
+            const double nd = ss.dist[u] + (node(v) - pu).norm();
+            if (nd < dist_of(v)) {
+                ss.seen[v] = ss.cur;
+                ss.dist[v] = nd;
+                ss.prev[v] = u;
+                push({nd + (node(v) - gp).norm(), v});
             }
         };
         while (!q.empty()) {
-            const int u = q.top().second;
-            q.pop();
-            if (closed[u]) continue;
-            closed[u] = 1;
+            const int u = q.front().second;
+            std::pop_heap(q.begin(), q.end(), cmp);
+            q.pop_back();
+            if (ss.done[u] == ss.cur) continue;
+            ss.done[u] = ss.cur;
             if (u == 1) return true;
             const Vec3 pu = node(u);
             const size_t e0 = (size_t)u * k;
@@ -285,12 +315,12 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
         stats_.ms_device += std::chrono::duration<double, std::milli>(t_dev1 - t_dev0).count();
         stats_.ms_search += std::chrono::duration<double, std::milli>(t_end - t_dev1).count();
     };
-    if (prev[1] < 0) {
+    if (prev_of(1) < 0) {
         account();
         return false;
     }
     std::vector<Vec3> path;
-    for (int v = 1; v >= 0; v = prev[v]) path.push_back({nodes[3 * v], nodes[3 * v + 1], nodes[3 * v + 2]});
+    for (int v = 1; v >= 0; v = prev_of(v)) path.push_back({nodes[3 * v], nodes[3 * v + 1], nodes[3 * v + 2]});
     std::reverse(path.begin(), path.end());
     out = shortcut(path);
     account();
