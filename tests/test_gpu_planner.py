@@ -626,6 +626,11 @@ def test_plan_once_equals_cpu_restatement_track(track, geom):
         got = pp.plan_once(cps[s], cps[s + 1], 65536, 1000 + s)
         exp, _ = O.plan_once(w, rg, ro, lo, hi, cps[s], cps[s + 1], 65536, 1000 + s, 16, False, 16)
         assert got is not None and np.array_equal(got, exp), s
+    # one segment past 65,535 nodes: the k-NN table goes down as int32 instead of u16
+    got = pp.plan_once(cps[1], cps[2], 80_000, 77)
+    exp, st = O.plan_once(w, rg, ro, lo, hi, cps[1], cps[2], 80_000, 77, 16, False, 16)
+    assert st[1] + 2 > 65535
+    assert got is not None and np.array_equal(got, exp)
 
 
 def test_precompute_traj_equals_cpu_track(track, geom):
