@@ -529,7 +529,10 @@ constexpr int kTileThreads = 256;
 constexpr int kTileL = 32;              // per-query list length
 constexpr int kTileNB = 16;             // histogram bins (16-bit counters, two per word)
 constexpr double kTileDelta = 1e-3;     // float error allowance, in h^2
-constexpr double kPass1R2 = 4.5;        // pass 1 first visits the cells within sqrt(4.5) h
+#ifndef EPP_KNN_PASS1R2  // (diagnostics A/B builds may override; exact either way)
+#define EPP_KNN_PASS1R2 4.5
+#endif
+constexpr double kPass1R2 = EPP_KNN_PASS1R2;  // pass 1 first visits the cells within sqrt(4.5) h
 
 // Visits the candidates of cube rows row0, row0 + rstep, ... around a query (a row =
 // kTileW consecutive halo cells along x, one contiguous LDS range), four candidates at a
