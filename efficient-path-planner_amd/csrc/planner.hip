@@ -1224,8 +1224,12 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
         if (k == 4) hipLaunchKernelGGL(k_knn_tile<4>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr, mode, d);
         else if (k == 8) hipLaunchKernelGGL(k_knn_tile<8>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr, mode, d);
         else hipLaunchKernelGGL(k_knn_tile<16>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr, mode, d);
-        // one wave per retried query: 8 per CU; waves without a query exit at once
-        const dim3 gr((unsigned)std::max(1, cus * 8)), br(64);
+        // one wave per retried query: EPP_KNN_RETRY_PER_CU per CU (waves without a query
+        // exit at once; more retries than waves loop)
+#ifndef EPP_KNN_RETRY_PER_CU
+#define EPP_KNN_RETRY_PER_CU 8
+#endif
+        const dim3 gr((unsigned)std::max(1, cus * EPP_KNN_RETRY_PER_CU)), br(64);
         if (k == 4) hipLaunchKernelGGL(k_knn_retry<4>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr);
         else if (k == 8) hipLaunchKernelGGL(k_knn_retry<8>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr);
         else hipLaunchKernelGGL(k_knn_retry<16>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr);
