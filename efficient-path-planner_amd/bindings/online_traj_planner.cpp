@@ -336,6 +336,15 @@ PYBIND11_MODULE(online_traj_planner, m) {
         .def("get_planned_traj", [](const epp::OnlineTrajGenerator& self) { return from_matrix(self.getPlannedTraj()); })
         // additions of this build
         .def("wait_for_update", &epp::OnlineTrajGenerator::waitForUpdate, py::call_guard<py::gil_scoped_release>())
+        .def("recompute_counts",
+             [](const epp::OnlineTrajGenerator& self) {
+                 const auto c = self.recomputeCounts();
+                 py::dict d;
+                 d["planned"] = c.planned;
+                 d["skipped_invalid_start"] = c.skippedInvalidStart;
+                 d["failed"] = c.failed;
+                 return d;
+             })
         .def(
             "planner", [](epp::OnlineTrajGenerator& self) -> epp::PathPlanner& { return self.planner(); },
             py::return_value_policy::reference_internal)

@@ -191,9 +191,10 @@ struct HostWorld {
     std::vector<RecReader> rec_readers[2];
     bool index_stale = false;           // the device blob is an older version
     std::mutex mu;                      // guards the lazy index rebuild
-    // Held shared by a launcher from its snapshot of the device index until its kernel is
-    // queued (IndexLease, SmallWorld::lease), exclusively by a rebuild: a rebuild on one
-    // thread cannot free or rewrite the blob between another thread's snapshot and launch.
+    // Held shared by a launcher from its snapshot of the device index or of the pinned
+    // records until its kernel is queued (IndexLease, SmallWorld::lease), exclusively by a
+    // rebuild and by epp_world_update: neither can free or rewrite the blob or a record slot
+    // between another thread's snapshot and launch.
     // Lock order: index_mu, then mu.
     std::shared_mutex index_mu;
     WorldView dev_view{};               // `view` as uploaded (an update changes view.n_obb first)
@@ -241,7 +242,7 @@ struct SmallWorld {
     int32_t n_obb;
     double r_gate, r_obst;
     int host_slot;  // recs is the pinned host copy of this slot (index stale), else -1
-    std::shared_lock<std::shared_mutex> lease;  // held while recs is the device blob's
+    std::shared_lock<std::shared_mutex> lease;  // held until the launch reading recs is queued
 };
 
 // A launcher's snapshot of the device index (host view as uploaded + its device copy),

@@ -245,10 +245,15 @@ bool OnlineTrajGenerator::updateGatePos(int gateId, const std::vector<double>& n
     }
     trajectoryCurrentlyUpdating = true;
     if (configParser->getPathPlannerProperties().recalculateOnline) {
-        // EPP_TEST_REPLAN_HOLD_MS (test hook): the worker starts that much later, so a test
-        // can rely on the recomputation still running while it makes further calls
+#ifdef EPP_TEST_HOOKS
+        // EPP_TEST_REPLAN_HOLD_MS (test builds only, -DEPP_TEST_HOOKS: testhooks/): the
+        // worker starts that much later, so a test can rely on the recomputation still
+        // running while it makes further calls
         const char* hold = std::getenv("EPP_TEST_REPLAN_HOLD_MS");
         const int hold_ms = hold && *hold ? std::max(0, std::atoi(hold)) : 0;
+#else
+        const int hold_ms = 0;
+#endif
         pending = std::async(std::launch::async, [this, gateId, dronePos, flightTime, hold_ms] {
             if (hold_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(hold_ms));
             recomputeTraj(gateId, dronePos, flightTime);
@@ -263,8 +268,13 @@ bool OnlineTrajGenerator::updateGatePos(int gateId, const std::vector<double>& n
 void OnlineTrajGenerator::recomputeTraj(int gateId, const Vec3& /*dronePos*/, double flightTime) {
     struct Reset {
         std::atomic<bool>& f;
-        ~Reset() { f = false; }
-    } reset{trajectoryCurrentlyUpdating};
+        std::atomic<uint64_t>& failed;
+        bool done = false;
+        ~Reset() {
+            if (!done) ++failed;  // (an exception left the recomputation)
+            f = false;
+        }
+    } reset{trajectoryCurrentlyUpdating, nFailed};
     const auto& pp = configParser->getPathPlannerProperties();
     const int segPre = gateId, segPost = gateId + 1;
     const size_t cpPre = 2 * (size_t)gateId + 1, cpPost = 2 * (size_t)gateId + 2, cpNext = 2 * (size_t)gateId + 3;
@@ -295,6 +305,8 @@ void OnlineTrajGenerator::recomputeTraj(int gateId, const Vec3& /*dronePos*/, do
     if (!pathPlanner.worldPtr->checkPointValidity(posA, pp.canPassGate)) {
         std::cerr << "Advanced trajectory does not end at valid position. No recomputation and hope for best"
                   << std::endl;
+        ++nSkipped;
+        reset.done = true;
         return;
     }
     if (cpNext >= checkpoints.size()) throw std::runtime_error("Post segment path not found. Exiting");
@@ -337,6 +349,8 @@ void OnlineTrajGenerator::recomputeTraj(int gateId, const Vec3& /*dronePos*/, do
     std::lock_guard<std::mutex> lk(trajMu);
     plannedTraj = std::move(merged);
     waypoints = filled;
+    ++nPlanned;
+    reset.done = true;
 }
 
 // the row whose time (last column) is nearest to t, first on ties (src/OnlineTrajGenerator.cpp:423-439)

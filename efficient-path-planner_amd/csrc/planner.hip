@@ -120,7 +120,7 @@ struct KnnGrid {
 
 constexpr int kBoundsThreads = 1024;
 constexpr int kBoundsBlocks = 64;
-constexpr double kNodesPerCell = 1.5;  // mean nodes per grid cell (EPP_KNN_NPC overrides; tuned for k_knn_tile: ~90 queries per 4^3 block -> 2 lanes each)
+constexpr double kNodesPerCell = 1.5;  // mean nodes per grid cell (EPP_KNN_NPC overrides in -DEPP_KNN_DIAG builds; tuned for k_knn_tile: ~90 queries per 4^3 block -> 2 lanes each)
 
 // The grid over the box [mn, mx] for n nodes: cells of edge h with ~npc nodes each (flat
 // point sets: thin slabs), at most cap cells.  Host (caller-given box) and device (the
@@ -249,9 +249,10 @@ __global__ void k_knn_count(const double* __restrict__ nodes, int n, const KnnGr
 // be published in this launch, and sums back to the nearest inclusive prefix -- no
 // block waits on a chain of predecessors (they publish their aggregates without waiting).
 // Status word: [63..40] launch tag (24 bits, never 0), [39] inclusive flag, [38..0] value.
-// Tags make stale words of earlier launches invisible: the workspace needs no clearing.
-// Blocks only wait on lower-numbered blocks, which are dispatched first, so the wait
-// always ends.
+// The status words are zeroed on the stream before every launch (a zero word carries no
+// tag, so it reads as unpublished); the tag is a second guard, against a word published by
+// an earlier launch on another stream.  Blocks only wait on lower-numbered blocks, which are
+// dispatched first, so the wait always ends.
 constexpr int kTagShift = 40;
 constexpr unsigned long long kIncl = 1ull << 39, kValMask = kIncl - 1ull;
 std::atomic<uint32_t> g_scan_tag{0};
@@ -1128,8 +1129,10 @@ __global__ void k_knn_edges(const double* __restrict__ nodes, const int32_t* __r
 }
 
 // Scratch of the grid k-NN, every part 256-byte aligned: grid params | bounds partials | cell_of[n] |
-// sidx[n] | sxyz[3n] | cnt[cap+1] | fill[cap+1] | start[cap+1] | retry bounds[n] | scan
-// status words  (cap = max(64, n))
+// sidx[n] | sxyz[3n] | cnt[cap+1] | fill[cap+1] | scan status words | start[cap+1] | retry
+// bounds[n]  (cap = max(64, n)).  cnt, fill and the status words are one range, cleared by
+// the launch's first kernel: the workspace may hold anything when a launch starts (a caller
+// workspace carved from a buffer that held other data, a tag of an earlier launch).
 struct KnnLayout {
     size_t part, cell, sidx, sxyz, cnt, start, fill, rbnd, stat, bytes;
     int cap, scan_blocks;
@@ -1144,11 +1147,11 @@ KnnLayout knn_layout(int n) {
     L.sxyz = L.sidx + al((size_t)n * 4);
     L.cnt = L.sxyz + al((size_t)n * 24);
     L.fill = L.cnt + al((size_t)(L.cap + 1) * 4);
-    L.start = L.fill + al((size_t)(L.cap + 1) * 4);
-    L.rbnd = L.start + al((size_t)(L.cap + 1) * 4);
-    L.stat = L.rbnd + al((size_t)std::max(n, 1) * 8);
+    L.stat = L.fill + al((size_t)(L.cap + 1) * 4);
     L.scan_blocks = (L.cap + 1 + kScanTile) / kScanTile;  // cells <= cap; start[ncell] too
-    L.bytes = L.stat + al((size_t)L.scan_blocks * 8);
+    L.start = L.stat + al((size_t)L.scan_blocks * 8);
+    L.rbnd = L.start + al((size_t)(L.cap + 1) * 4);
+    L.bytes = L.rbnd + al((size_t)std::max(n, 1) * 8);
     return L;
 }
 
@@ -1179,10 +1182,16 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
     const double r2 = max_dist > 0 ? max_dist * max_dist : 1e300;
     const dim3 g256((n + 255) / 256), b256(256);
     const int nb = std::max(1, std::min(kBoundsBlocks, (n + kBoundsThreads - 1) / kBoundsThreads));
+#ifdef EPP_KNN_DIAG
+    // (diagnostics builds only) EPP_KNN_NPC: the grid density, an exact-either-way A/B knob
     const char* npc_env = std::getenv("EPP_KNN_NPC");
     const double npc = npc_env && *npc_env ? std::max(0.5, std::atof(npc_env)) : kNodesPerCell;
-    // cnt and fill are adjacent: cleared together by the first kernel (never run the
-    // scatter on stale counters)
+#else
+    const double npc = kNodesPerCell;
+#endif
+    // cnt, fill and the scan's status words are adjacent: cleared together by the first
+    // kernel (never run the scatter on stale counters, never let the look-back take a stale
+    // word for a published one)
     const int nclr = (int)((L.start - L.cnt) / sizeof(int));
     if (box_lo && box_hi) {  // the caller's box: the grid shape on the host, one kernel
         KnnGrid gv{};
@@ -1528,6 +1537,9 @@ epp_status epp_compact_states_ws(const double* xyz, const uint8_t* valid, int64_
         return EPP_ERR_INVALID_ARGUMENT;
     }
     const int nb = (int)std::max<int64_t>(1, (n + kCompactChunk - 1) / kCompactChunk);
+    // the workspace may hold anything (e.g. carved from a buffer that held other data):
+    // zero its status words first, so none reads as published in this launch
+    if (hipMemsetAsync(ws, 0, (size_t)nb * 8, (hipStream_t)stream) != hipSuccess) return last("epp_compact_states");
     hipLaunchKernelGGL(k_compact, dim3(nb), dim3(kCompactThreads), 0, (hipStream_t)stream, xyz, valid, n,
                        static_cast<unsigned long long*>(ws), next_scan_tag(), out, n_out);
     return last("epp_compact_states");

@@ -601,7 +601,10 @@ epp_status epp_world_update(epp_world* w, const epp_obb* obbs, int32_t n) {
         return EPP_ERR_INVALID_ARGUMENT;
     }
     // (the device blob is not touched: ensure_index rebuilds it after in-flight kernels;
-    // the records go to the other pinned slot, see HostWorld)
+    // the records go to the other pinned slot, see HostWorld).  Exclusive on index_mu: a
+    // launcher holding a SmallWorld snapshot of the pinned records has queued its kernel and
+    // recorded its reader event (or, polled, finished) before the slot can be rewritten.
+    std::unique_lock<std::shared_mutex> ix(w->index_mu);
     std::lock_guard<std::mutex> lk(w->mu);
     if (!epp::build_records(*w, obbs, n)) return EPP_ERR_UNSUPPORTED;
     w->index_stale = true;
@@ -698,7 +701,10 @@ SmallWorld small_world(const epp_world* cw) {
     s.n_obb = (int32_t)hw.obbs.size();
     s.r_gate = hw.r_gate;
     s.r_obst = hw.r_obst;
-    if (!hw.index_stale) s.lease = std::move(ix);  // the device records: no rebuild until launched
+    // held until the caller's kernel is queued (and its reader event recorded) or, polled,
+    // has finished: no rebuild frees the device records and no update rewrites or
+    // reallocates the pinned slot under a launch
+    s.lease = std::move(ix);
     return s;
 }
 

@@ -434,17 +434,30 @@ def sample_uniform(seed: int, lo, hi, n: int, start: int = 0) -> np.ndarray:
     return d.download(np.float64, 3 * n).reshape(n, 3)
 
 
-def knn(nodes: np.ndarray, k: int, max_dist: float = 0.0, method: str = "auto", box=None) -> np.ndarray:
+def _filled(nbytes: int, word) -> DeviceBuffer:
+    """A device buffer of nbytes (multiple of 8) holding `word` (u64) in every slot, or
+    zeros when word is None -- a caller workspace that held other data."""
+    b = DeviceBuffer(nbytes)
+    if word is None:
+        b.zero()
+    else:
+        b.upload(np.full(nbytes // 8, int(word) & 0xFFFFFFFFFFFFFFFF, np.uint64))
+    return b
+
+
+def knn(nodes: np.ndarray, k: int, max_dist: float = 0.0, method: str = "auto", box=None,
+        ws_fill=None) -> np.ndarray:
     """epp_knn (method "auto"), epp_knn_bruteforce ("brute") or epp_knn_grid ("grid"):
     (n, k) neighbour indices, nearest first, ties to the lower index, -1 where fewer
     than k exist.  box=(lo, hi) with method "ws" / "grid_ws": the caller-box variants
-    (epp_knn_ws_box / epp_knn_grid_ws_box; every node inside the box)."""
+    (epp_knn_ws_box / epp_knn_grid_ws_box; every node inside the box).  ws_fill: the u64
+    word the caller workspace holds before the call (tests: stale data)."""
     nodes = np.ascontiguousarray(np.asarray(nodes, np.float64).reshape(-1, 3))
     n = len(nodes)
     d_n = DeviceBuffer.from_array(nodes)
     d_k = DeviceBuffer(4 * max(n * k, 1))
     if method in ("ws", "grid_ws"):  # caller workspace variants
-        d_w = DeviceBuffer(max(int(lib().epp_knn_workspace_size(n)), 256))
+        d_w = _filled(max(int(lib().epp_knn_workspace_size(n)), 256), ws_fill)
         if box is not None:
             lo, hi = (np.ascontiguousarray(np.asarray(b, np.float64).reshape(3)) for b in box)
             fn = lib().epp_knn_ws_box if method == "ws" else lib().epp_knn_grid_ws_box
@@ -459,16 +472,16 @@ def knn(nodes: np.ndarray, k: int, max_dist: float = 0.0, method: str = "auto", 
     return d_k.download(np.int32, n * k).reshape(n, k)
 
 
-def compact_states(xyz: np.ndarray, valid: np.ndarray, ws: bool = False) -> np.ndarray:
+def compact_states(xyz: np.ndarray, valid: np.ndarray, ws: bool = False, ws_fill=None) -> np.ndarray:
     """epp_compact_states (ws: epp_compact_states_ws, caller workspace): the valid rows of
-    xyz, in index order."""
+    xyz, in index order.  ws_fill: the u64 word the caller workspace holds before the call."""
     xyz = np.ascontiguousarray(np.asarray(xyz, np.float64).reshape(-1, 3))
     valid = np.ascontiguousarray(np.asarray(valid, np.uint8))
     n = len(xyz)
     d_x, d_v = DeviceBuffer.from_array(xyz), DeviceBuffer.from_array(valid)
     d_o, d_c = DeviceBuffer(24 * max(n, 1)), DeviceBuffer(8)
     if ws:
-        d_w = DeviceBuffer(int(lib().epp_compact_workspace_size(n)))
+        d_w = _filled(int(lib().epp_compact_workspace_size(n)), ws_fill)
         check(lib().epp_compact_states_ws(d_x.ptr, d_v.ptr, n, d_o.ptr, d_c.ptr, d_w.ptr, d_w.nbytes, None))
     else:
         check(lib().epp_compact_states(d_x.ptr, d_v.ptr, n, d_o.ptr, d_c.ptr, None))

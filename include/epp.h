@@ -202,7 +202,8 @@ epp_status epp_knn_bruteforce(const double* nodes, int32_t n, int32_t k, double 
 epp_status epp_knn_grid(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr, void* stream);
 /* Caller-workspace variants (no allocation, no cross-stream ordering inside): `ws` is a
  * 256-byte aligned device buffer of at least epp_knn_workspace_size(n) bytes that no
- * other stream touches until this call's kernels completed.  epp_knn / epp_knn_grid
+ * other stream touches until this call's kernels completed.  Its prior contents do not
+ * matter (the call clears what it reads before writing it).  epp_knn / epp_knn_grid
  * use a cached per-device workspace whose reuse is ordered by a completion event. */
 uint64_t epp_knn_workspace_size(int32_t n);
 epp_status epp_knn_ws(const double* nodes, int32_t n, int32_t k, double max_dist, int32_t* nbr, void* ws,
@@ -212,7 +213,9 @@ epp_status epp_knn_grid_ws(const double* nodes, int32_t n, int32_t k, double max
 /* The same with the grid laid over the caller's box [lo, hi] (host arrays) instead of the
  * nodes' bounding box, which saves its device reduction (two kernels fewer): every node
  * must lie inside the closed box (the planner's samples lie in the world bounds; start and
- * goal widen them).  Same answers. */
+ * goal widen them).  Same answers.  Precondition, not checked: a node outside the box is
+ * clamped into a boundary cell, which breaks the search's distance bounds, and the table is
+ * then unspecified (not necessarily exact). */
 epp_status epp_knn_ws_box(const double* nodes, int32_t n, int32_t k, double max_dist, const double lo[3],
                           const double hi[3], int32_t* nbr, void* ws, uint64_t ws_bytes, void* stream);
 epp_status epp_knn_grid_ws_box(const double* nodes, int32_t n, int32_t k, double max_dist, const double lo[3],
@@ -233,7 +236,8 @@ epp_status epp_check_knn_motions(const epp_world* w, const double* nodes, const 
 epp_status epp_compact_states(const double* xyz, const uint8_t* valid, int64_t n, double* out, int64_t* n_out,
                               void* stream);
 /* Caller-workspace variant (ws: >= epp_compact_workspace_size(n) device bytes that no
- * other stream uses until this call's kernels completed); epp_compact_states uses a
+ * other stream uses until this call's kernels completed; any prior contents: the call
+ * zeroes its look-back status words first); epp_compact_states uses a
  * cached per-device workspace ordered by an event (serialising concurrent streams). */
 uint64_t epp_compact_workspace_size(int64_t n);
 epp_status epp_compact_states_ws(const double* xyz, const uint8_t* valid, int64_t n, double* out, int64_t* n_out,

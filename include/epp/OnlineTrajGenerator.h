@@ -14,6 +14,7 @@
 // the worker.
 #pragma once
 #include <atomic>
+#include <cstdint>
 #include <future>
 #include <memory>
 #include <mutex>
@@ -50,6 +51,18 @@ public:
     // waits for an in-flight online recomputation (recalculate_online); rethrows its
     // failure as std::runtime_error("previous trajectory update failed: ...")
     void waitForUpdate();
+    // Which exit the recomputations took so far (an addition of this build, for callers
+    // that time or log them): `planned` ran the two segment plans, includeGates2 and the
+    // refit; `skippedInvalidStart` took the reference's "Advanced trajectory does not end
+    // at valid position" exit (updateGatePos still returned true,
+    // src/OnlineTrajGenerator.cpp:304-310); `failed` threw.  updateGatePos calls that
+    // returned false never recompute.
+    struct RecomputeCounts {
+        uint64_t planned = 0, skippedInvalidStart = 0, failed = 0;
+    };
+    RecomputeCounts recomputeCounts() const {
+        return {nPlanned.load(), nSkipped.load(), nFailed.load()};
+    }
 
 private:
     void init(const Vec3& start, const Vec3& goal);
@@ -76,6 +89,7 @@ private:
     std::vector<Vec3> waypoints;  // guarded by trajMu
     mutable std::mutex trajMu;
     std::atomic<bool> trajectoryCurrentlyUpdating{false};
+    std::atomic<uint64_t> nPlanned{0}, nSkipped{0}, nFailed{0};
     std::future<void> pending;
     PathWriter pathWriter{"path_segments"};  // include/OnlineTrajGenerator.h:132
 };

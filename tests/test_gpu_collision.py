@@ -632,3 +632,74 @@ def test_updates_racing_large_checks(geom, worlds):
         t.join()
     assert not err, err
     world.close()
+
+
+def test_updates_racing_small_checks(geom, worlds):
+    """small-path checks (<= 4096 states / 1024 edges, <= 256 OBBs) read the
+    pinned host records of the newest version while the index is stale.  One thread runs
+    back-to-back updates over three versions (64 OBBs, 190 OBBs: the pinned slot is
+    reallocated, 64 OBBs with every gate moved) while another launches small checks: a
+    launcher holds its snapshot of the records until its kernel is queued and its reader
+    recorded, so every answer is the oracle's for one version."""
+    import threading
+    rg, ro, ws = worlds
+    g2, o2, (lo, hi) = ws["c2"]
+    gb, ob = synth.track_world(42, n_obstacles=150)
+    gm = g2.copy()
+    gm[:, :2] += 0.3
+    gm[:, 5] += 0.2
+    versions = [(g2, o2), (gb, ob), (gm, o2)]
+    obbs = [capi.build_obbs(geom, g, o) for g, o in versions]
+    assert all(len(b) <= 256 for b in obbs) and len(obbs[1]) > 2 * len(obbs[0])
+    refs = [O.world_build(geom, g, o, rg, ro) for g, o in versions]
+    pts = synth.sample_states(13, lo, hi, 4096)
+    s1, s2 = synth.edges(14, 9, lo, hi, 1024)
+    exp_s = [O.check_states(r, rg, ro, pts) for r in refs]
+    exp_m = [O.check_motions(r, rg, ro, s1, s2) for r in refs]
+    assert not np.array_equal(exp_s[0], exp_s[2]) and not np.array_equal(exp_s[0], exp_s[1])
+    world = capi.World(obbs[0], rg, ro)
+    world.update(obbs[1])  # index stale from here on: every check below reads pinned records
+    stop, err = threading.Event(), []
+
+    def updater():
+        k = 2
+        try:
+            while not stop.is_set():
+                world.update(obbs[k % 3])
+                world.update(obbs[(k + 1) % 3])  # two updates back to back
+                k += 1
+        except Exception as e:  # pragma: no cover - reported below
+            err.append(e)
+
+    t = threading.Thread(target=updater)
+    t.start()
+    try:
+        for i in range(200):
+            got = world.check_states(pts)
+            assert any(np.array_equal(got, e) for e in exp_s), f"states call {i}: no version matches"
+            got = world.check_motions(s1, s2)
+            assert any(np.array_equal(got, e) for e in exp_m), f"motions call {i}: no version matches"
+    finally:
+        stop.set()
+        t.join()
+    assert not err, err
+    world.close()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("can_pass", [0, 1])
+def test_c3_motions_full_bench_size(geom, worlds, mode, can_pass):
+    """BASELINE C3 at the bench's own size and inputs (bench.py side_measurements: 512 OBBs,
+    1,048,576 edges from seeds 43 / 8): analytic and 32-step discretised flags bit-exact
+    against the oracle (World::checkRayValid, src/World.cpp:130-162), both can_pass_gate
+    values -- the grid and window-count shape of the bench launch itself."""
+    rg, ro, ws = worlds
+    g3, o3, (lo, hi) = ws["c3"]
+    ref = O.world_build(geom, g3, o3, rg, ro)
+    w = capi.World(capi.build_obbs(geom, g3, o3), rg, ro)
+    s1, s2 = synth.edges(43, 8, lo, hi, 1 << 20)
+    got = w.check_motions(s1, s2, bool(can_pass), mode)
+    exp = O.check_motions(ref, rg, ro, s1, s2, bool(can_pass), mode, threads=16)
+    assert 0 < int(exp.sum()) < len(exp)
+    assert np.array_equal(got, exp), int((got != exp).sum())
+    w.close()

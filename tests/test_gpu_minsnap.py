@@ -119,11 +119,20 @@ def test_generate_trajectory_two_waypoints_and_errors():
 
 
 def test_large_batch_property():
-    """4096 twelve-segment problems (BASELINE config 5 batched variant): continuity of
-    derivatives 0..4 at every inner vertex and the end constraints, size-independent."""
+    """4096 twelve-segment problems -- the bench's C5 batched launch itself (same seeds,
+    bench.py side_measurements): EVERY problem's segment times within 1e-12 relative and
+    coefficients within 1e-6 of the oracle (north_star), plus continuity of derivatives
+    0..4 at every inner vertex and the end constraints (size-independent)."""
     tracks = [synth.random_track_waypoints(10_000 + k, 12) for k in range(4096)]
     Ts, Cs, st = capi.minsnap_batch(tracks, 1.0, 2.0)
     assert (st == 0).all()
+    worst_c = worst_t = 0.0
+    for k, wp in enumerate(tracks):
+        T_ref, C_ref = O.minsnap_track(wp, 1.0, 2.0)
+        worst_t = max(worst_t, float(np.max(np.abs(Ts[k] - T_ref) / T_ref)))
+        worst_c = max(worst_c, float(np.max(np.abs(Cs[k] - C_ref))))
+    assert worst_t <= 1e-12, worst_t
+    assert worst_c < 1e-6, worst_c
     for k in range(0, 4096, 97):
         T, Cf = Ts[k], Cs[k]
         for i in range(1, 12):
