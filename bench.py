@@ -91,8 +91,9 @@ def main():
                     help="CPU-only: run the rank launch + gloo exchange plumbing and print one JSON line")
     ap.add_argument("--fail-rank", type=int, default=-1,
                     help="with --launcher-check: this rank's (simulated) plan fails (error-protocol test)")
-    ap.add_argument("--fail-at", choices=("plan", "exchange"), default="plan",
-                    help="with --fail-rank: fail inside the plan leg (collective check) or at the all-gather (count -1)")
+    ap.add_argument("--fail-at", choices=("plan", "exchange", "after-count"), default="plan",
+                    help="with --fail-rank: fail inside the plan leg (collective check), at the all-gather (count -1) "
+                         "or die right after sending its count (the peers are then inside the data all-gather)")
     args = ap.parse_args()
 
     from eppamd.dist import LegFailed, env, make_group, spawn_ranks
@@ -167,6 +168,9 @@ def run(args, ws, rank, local, out_stream):
                 step(i)
             capi.check(L.epp_graph_end(stream, C.byref(g)))
             graph = g.value
+            # one untimed replay: the graph's first launch pays its upload to the device;
+            # the timed replay below is the steady state (the same K launches, same work)
+            capi.check(L.epp_graph_launch(graph, stream))
         except capi.EppError as e:
             print(f"bench: graph capture failed ({e}); timing the host loop", file=sys.stderr)
             if L.epp_graph_end(stream, C.byref(g)) == 0:  # leave capture mode if still in it
@@ -267,6 +271,14 @@ def launcher_check(ws, rank, local, out_stream, fail_rank=-1, fail_at="plan"):
         return np.arange(3 * (5 + rank), dtype=np.float64).reshape(-1, 3) + 1000 * rank
 
     wp = dist.run(plan, "full plan")
+    if rank == fail_rank and fail_at == "after-count":
+        # this rank's process dies between the two steps of the exchange: its count is sent,
+        # its set never is (the peers must leave the data all-gather with an error)
+        import torch
+        n = torch.tensor([len(wp)], dtype=torch.int64)
+        dist.dist.all_gather([torch.zeros_like(n) for _ in range(ws)], n)
+        print(f"bench.py rank {rank}: dying after the counts (test)", file=sys.stderr, flush=True)
+        os._exit(7)
     sets = dist.all_gather_waypoints(None if (rank == fail_rank and fail_at == "exchange") else wp)
     t = dist.max(float(rank + 1))
     if rank == 0:
@@ -326,11 +338,15 @@ def full_plan(dist, rank, reps):
             t = time.perf_counter()
             state["otg"].pre_compute_traj(0.0)
             per.append((time.perf_counter() - t) * 1e3)
-        # one gate-to-gate segment alone, with the planner's device / host split
-        pp = otp.PathPlanner(gates, obstacles, path)
+        # one gate-to-gate segment alone, with the planner's device / host split: a fresh
+        # PathPlanner's first plan (cold: its construction included) and its second (warm)
         all_cps = state["otg"].get_checkpoints()
+        t = time.perf_counter()
+        pp = otp.PathPlanner(gates, obstacles, path)
         pp.plan_path(all_cps[2], all_cps[3], 2.0)
-        return per, pp.last_stats()
+        cold = dict(pp.last_stats(), wall_ms_with_construction=(time.perf_counter() - t) * 1e3)
+        pp.plan_path(all_cps[4], all_cps[5], 2.0)
+        return per, {"cold": cold, "warm": pp.last_stats()}
 
     try:
         dist.run(setup, "full plan (warm-up)")
@@ -373,9 +389,55 @@ def full_plan(dist, rank, reps):
                         "batch plans (65,536 samples, k=16) + includeGates2 + min-snap + sampling"}
 
 
+C1_REPS = 20
+
+
+def c1_plan(reps=C1_REPS, cpu_threads=None):
+    """BASELINE C1 (single gate + 4 OBB obstacles, bounds [-2,2]^2 x [0,2], the shipped
+    config: samples_fmt 4096): ms per plan through the pybind module, as a Python caller of
+    the reference's online_traj_planner sees it (src/pybind.cpp:10-27): OnlineTrajGenerator
+    -> pre_compute_traj (2 gate-to-gate plans + includeGates2 + min-snap + sampling).  The
+    first plan of a fresh generator (cold: construction, workspaces, first launches) is
+    reported apart from the steady state.  cpu_threads: the same plans on the CPU
+    restatement (oracle/track_planner.OnlineTrajGeneratorCPU; equal waypoints,
+    tests/test_gpu_planner.py)."""
+    from eppamd import config, synth
+    path = os.path.join(ROOT, "configs", "config.json")
+    cfg = config.load(path)
+    geom = config.geometry(cfg)
+    g, o, start, goal = synth.c1_world()
+    if cpu_threads:
+        import track_planner as TP
+
+        def make():
+            return TP.OnlineTrajGeneratorCPU(geom, cfg, start, goal, g, o, threads=cpu_threads)
+    else:
+        import online_traj_planner as otp
+
+        def make():
+            return otp.OnlineTrajGenerator(start, goal, g, o, path)
+    t = time.perf_counter()
+    otg = make()
+    otg.pre_compute_traj(0.0)
+    cold = (time.perf_counter() - t) * 1e3
+    per = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        otg.pre_compute_traj(0.0)
+        per.append((time.perf_counter() - t) * 1e3)
+    out = {"ms_per_plan": float(np.mean(per)), "ms_per_plan_p50": float(np.median(per)), "reps": reps,
+           "cold_first_plan_ms": cold, "segments": 2, "samples_per_segment": int(cfg["path_planner_properties"]
+                                                                                ["samples_fmt"]),
+           "workload": "C1: single gate + 4 obstacles, OnlineTrajGenerator.pre_compute_traj (2 batch plans + "
+                       "includeGates2 + min-snap + sampling)"}
+    if cpu_threads:
+        out["threads"] = cpu_threads
+    return out
+
+
 def side_measurements(capi, L, stream, geom, cfg, rg, ro):
     from eppamd import synth
-    res = {}
+    res = {"c1_plan": c1_plan()}
     # C3: 512 OBBs, 1M edges (analytic) and 32-step discretised
     g3, o3 = synth.track_world(42, n_obstacles=472)
     w3 = capi.World(capi.build_obbs(geom, g3, o3), rg, ro)
@@ -537,23 +599,34 @@ def run_native(argv, via, timeout=120):
         return {"error": f"{type(e).__name__}: {e}", "via": via}
 
 
-def c5_events(cfg_path, geom, gates, obstacles, n_tracks=24, cpu_threads=None):
+C5_EVENT_TRACKS = 8
+
+
+def c5_events(cfg_path, geom, gates, obstacles, n_tracks=C5_EVENT_TRACKS, cpu_threads=None):
     """C5 through the reference's entry point, OnlineTrajGenerator.update_gate_pos
     (src/OnlineTrajGenerator.cpp:123-226): every gate of a planned track is observed once
     (as the reference allows), 1 s of flight before the trajectory reaches its centre, at
     a pose perturbed by +-0.1 m / +-0.1 rad; the call checks the lookahead (checkGatePassed
-    + A11) and, when the trajectory no longer passes or collides, replans the two segments
-    around the gate and refits (recomputeTraj, inline: recalculate_online false).  Each
-    event is timed; n_tracks fresh generators (planned untimed).  cpu_threads: the same
-    events on the CPU restatement (oracle/track_planner.OnlineTrajGeneratorCPU: planner in
-    C++, driven from Python), fewer tracks."""
+    + A11) and, when the trajectory no longer passes or collides, calls recomputeTraj
+    (inline: recalculate_online false).  Each event is timed and filed by what it ran:
+      check_only             -- returned False (no recomputation);
+      skipped_invalid_start  -- returned True, but recomputeTraj took the reference's
+                                "Advanced trajectory does not end at valid position" exit
+                                (:304-310): no plan, no refit;
+      replan                 -- returned True after two segment plans + includeGates2 +
+                                refit + merge.
+    (The product reports the exit through OnlineTrajGenerator.recompute_counts(); the CPU
+    restatement through its planner call counter: +2 per replan.)  n_tracks fresh
+    generators (planned untimed), the same tracks and perturbations for cpu_threads: the
+    CPU restatement (oracle/track_planner.OnlineTrajGeneratorCPU: planner in C++, driven
+    from Python) -- the same events, so the two distributions compare."""
     rs = np.random.RandomState(11)
     from eppamd import synth
     cps = synth.gate_checkpoints(gates, geom.gate_height, 0.55)
     centres = gates[:, :3] + np.stack([np.zeros(len(gates)), np.zeros(len(gates)),
                                        geom.gate_height[gates[:, 6].astype(int)]], 1)
     perturb = [[rs.uniform(-0.1, 0.1, 3) for _ in range(len(gates))] for _ in range(n_tracks)]
-    check_us, replan_us = [], []
+    us = {"check_only": [], "skipped_invalid_start": [], "replan": []}
     if cpu_threads:
         import track_planner as TP
         cfg = cfg_json(cfg_path)
@@ -576,15 +649,19 @@ def c5_events(cfg_path, geom, gates, obstacles, n_tracks=24, cpu_threads=None):
             drone = cur[i, [0, 3, 6]].copy()
             pose = gates[g, :6].copy()
             pose[[0, 1, 5]] += perturb[k][g]
+            before = otg.calls if cpu_threads else otg.recompute_counts()["planned"]
             t = time.perf_counter()
             r = otg.update_gate_pos(g, pose, drone, True, t_obs)
             el = (time.perf_counter() - t) * 1e6
-            (replan_us if r else check_us).append(el)
-    out = {"events": len(check_us) + len(replan_us), "tracks": n_tracks, "replans": len(replan_us),
-           "check_only": _pct(np.array(check_us)) if check_us else None,
-           "replan": _pct(np.array(replan_us)) if replan_us else None,
+            after = otg.calls if cpu_threads else otg.recompute_counts()["planned"]
+            planned = (after - before) == (2 if cpu_threads else 1)
+            us["replan" if planned else ("skipped_invalid_start" if r else "check_only")].append(el)
+    out = {"events": sum(len(v) for v in us.values()), "tracks": n_tracks,
+           "counts": {k: len(v) for k, v in us.items()},
+           **{k: (_pct(np.array(v)) if v else None) for k, v in us.items()},
            "workload": "C5 via OnlineTrajGenerator.update_gate_pos: each gate observed once, 1 s ahead, pose +-0.1 m / "
-                       "+-0.1 rad; check-only events (checkGatePassed + A11) and replan events (2 segment plans of "
+                       "+-0.1 rad; check_only (checkGatePassed + A11, returned False), skipped_invalid_start "
+                       "(returned True, the reference's no-recomputation exit) and replan (2 segment plans of "
                        f"{PLAN_SAMPLES:,} samples + includeGates2 + refit) timed separately"}
     if cpu_threads:
         out["threads"] = cpu_threads
@@ -767,6 +844,7 @@ def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None):
     out["full_plan"] = {"threads": nt, "tracks": 1, "waypoints": int(len(wp4)), "traj_rows": int(len(rows4)),
                         "workload": "C4 rank-0 track: 9 batch plans (65,536 samples, k=16) + includeGates2 + "
                                     "min-snap + sampling, the planner restated on the CPU (oracle/track_planner.py)"}
+    out["c1_plan"] = c1_plan(reps=5, cpu_threads=1)
     if c5_inputs:
         c = c5_inputs
         lat = c5_online(c["cfg_path"], c["geom"], c["gates"], c["obstacles"], c["wp"], c["window"], c["vmax"],
@@ -779,6 +857,23 @@ def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None):
             O.generate_trajectory(wp1, 1.0, 2.0, 0.1)
             lat[r] = time.perf_counter() - t
         out["c5_refit"] = dict(_pct(lat[20:] * 1e6), threads=1, via="Python (ctypes oracle)")
+        # C5 batched: the GPU leg's 4096 x 12-segment problems, one generateTrajectory solve
+        # each (the reference's per-problem shape), on the CPU share and on 32 threads
+        tracks = [synth.random_track_waypoints(10_000 + k, 12) for k in range(4096)]
+        out["c5_minsnap_batch"] = {"problems": len(tracks), "segments": 12,
+                                   "workload": "4096 x 12-segment min-snap solves (or_minsnap_track: Nfabian times + "
+                                               "QP), the GPU leg's problems, contiguous ranges per thread"}
+        for tw in sorted({nt, 32}):
+            O.minsnap_batch(tracks[:256], 1.0, 2.0, threads=tw)  # (thread start-up, page faults)
+            t = time.perf_counter()
+            reps = 0
+            while reps < 3 or time.perf_counter() - t < 0.5:
+                O.minsnap_batch(tracks, 1.0, 2.0, threads=tw)
+                reps += 1
+            el = (time.perf_counter() - t) / reps
+            out["c5_minsnap_batch"][f"problems_per_s_{tw}_threads"] = len(tracks) / el
+        out["c5_minsnap_batch"]["problems_per_s"] = out["c5_minsnap_batch"][f"problems_per_s_{nt}_threads"]
+        out["c5_minsnap_batch"]["threads"] = nt
         out["c5_online"]["via"] = "Python (ctypes oracle)"
         # native: the same loops from the same input file, C++ calls into the oracle
         nat = run_native([os.path.join(ROOT, "oracle", "cpu_bench"), c["native_input"]],
@@ -789,8 +884,9 @@ def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None):
         if "error" in nat:
             out["c5_native_error"] = nat["error"]
         os.unlink(c["native_input"])
-        # the update_gate_pos events on the CPU restatement (2 tracks, planner on nt threads)
-        out["c5_update_gate_pos"] = c5_events(c["cfg_path"], c["geom"], c["gates"], c["obstacles"], n_tracks=2,
+        # the update_gate_pos events on the CPU restatement: the GPU leg's tracks and
+        # perturbations (planner on nt threads)
+        out["c5_update_gate_pos"] = c5_events(c["cfg_path"], c["geom"], c["gates"], c["obstacles"],
                                               cpu_threads=nt)
     return out
 

@@ -8,9 +8,12 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "epp_internal.h"
@@ -27,6 +30,8 @@ struct Rccl {
     decltype(&ncclAllGather) allGather = nullptr;
     decltype(&ncclAllReduce) allReduce = nullptr;
     decltype(&ncclGetErrorString) errorString = nullptr;
+    decltype(&ncclCommGetAsyncError) getAsyncError = nullptr;
+    decltype(&ncclCommAbort) commAbort = nullptr;
 };
 
 const Rccl* rccl() {
@@ -63,9 +68,11 @@ const Rccl* rccl() {
         r.allGather = reinterpret_cast<decltype(r.allGather)>(dlsym(r.h, "ncclAllGather"));
         r.allReduce = reinterpret_cast<decltype(r.allReduce)>(dlsym(r.h, "ncclAllReduce"));
         r.errorString = reinterpret_cast<decltype(r.errorString)>(dlsym(r.h, "ncclGetErrorString"));
+        r.getAsyncError = reinterpret_cast<decltype(r.getAsyncError)>(dlsym(r.h, "ncclCommGetAsyncError"));
+        r.commAbort = reinterpret_cast<decltype(r.commAbort)>(dlsym(r.h, "ncclCommAbort"));
     });
     if (!r.h || !r.getUniqueId || !r.commInitRank || !r.commInitAll || !r.commDestroy || !r.allGather ||
-        !r.allReduce || !r.errorString) {
+        !r.allReduce || !r.errorString || !r.getAsyncError || !r.commAbort) {
         set_error("epp_comm: RCCL (librccl.so.1) is not available");
         return nullptr;
     }
@@ -86,6 +93,9 @@ struct epp_comm {
     char* d_buf = nullptr;  // counts (n_ranks + 1 int32, padded) | send set | gathered sets
     size_t cap = 0;
     hipStream_t stream = nullptr;
+    double timeout_s = 120.0;              // epp_comm_set_timeout
+    std::atomic<bool> abort_req{false};    // epp_comm_abort (any thread)
+    bool aborted = false;                  // ncclCommAbort ran: every later call fails
 };
 
 using namespace epp;
@@ -117,6 +127,67 @@ hipError_t comm_grow(epp_comm* c, size_t need) {
 epp_status hip_fail(const char* what, hipError_t he) {
     set_error(std::string(what) + ": " + hipGetErrorString(he));
     return EPP_ERR_HIP;
+}
+
+// Tears the communicator down without waiting for its peers: RCCL's kernels and proxy
+// leave their collectives, the comm is unusable afterwards (epp_comm_destroy still frees
+// the rest).
+void do_abort(const Rccl* r, epp_comm* c) {
+    if (c->aborted) return;
+    if (c->comm) r->commAbort(c->comm);
+    c->comm = nullptr;
+    c->aborted = true;
+}
+
+epp_status aborted_error(const char* what) {
+    set_error(std::string(what) + ": the communicator was aborted (a peer failed or timed out)");
+    return EPP_ERR_PEER;
+}
+
+// Waits for the communicator's stream WITHOUT blocking in the runtime: the collective
+// queued on it completes only if every peer takes part.  While it runs, RCCL's
+// asynchronous error state (a peer process died, a broken connection) and an abort
+// requested from another thread (epp_comm_abort) are polled; either, or the deadline
+// (epp_comm_set_timeout), aborts the communicator, and the call returns an error instead
+// of leaving this rank inside the collective.
+epp_status comm_wait(const Rccl* r, epp_comm* c, const char* what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spin = 0;; ++spin) {
+        const hipError_t q = hipStreamQuery(c->stream);
+        if (q == hipSuccess) return EPP_OK;
+        if (q != hipErrorNotReady) return hip_fail(what, q);
+        if ((spin & 63) != 63) {  // (a short spin first: the exchange is normally quick)
+            std::this_thread::yield();
+            continue;
+        }
+        ncclResult_t ae = ncclSuccess;
+        if (c->comm) (void)r->getAsyncError(c->comm, &ae);
+        if (ae != ncclSuccess && ae != ncclInProgress) {
+            const std::string why = r->errorString(ae);
+            do_abort(r, c);
+            set_error(std::string(what) + ": RCCL asynchronous error (" + why + "): communicator aborted");
+            return EPP_ERR_PEER;
+        }
+        if (c->abort_req.load()) {
+            do_abort(r, c);
+            return aborted_error(what);
+        }
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (el > c->timeout_s) {
+            do_abort(r, c);
+            set_error(std::string(what) + ": no completion within " + std::to_string(c->timeout_s) +
+                      " s (a peer did not take part): communicator aborted");
+            return EPP_ERR_TIMEOUT;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
+// Entry check of every collective: an aborted communicator (or one whose abort was
+// requested before the call) fails at once.
+epp_status comm_usable(const Rccl* r, epp_comm* c, const char* what) {
+    if (!c->aborted && c->abort_req.load()) do_abort(r, c);
+    return c->aborted ? aborted_error(what) : EPP_OK;
 }
 
 }  // namespace
@@ -191,7 +262,7 @@ epp_status epp_comm_destroy(epp_comm* c) {
     if (c->d_buf) (void)hipFree(c->d_buf);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     const Rccl* r = rccl();
-    if (r && c->comm) r->commDestroy(c->comm);
+    if (r && c->comm && !c->aborted) r->commDestroy(c->comm);
     (void)hipSetDevice(prev);
     delete c;
     return EPP_OK;
@@ -204,6 +275,24 @@ epp_status epp_comm_rank(const epp_comm* c, int32_t* rank, int32_t* n_ranks) {
     return EPP_OK;
 }
 
+epp_status epp_comm_set_timeout(epp_comm* c, double seconds) {
+    if (!c || !(seconds > 0.0)) {
+        set_error("epp_comm_set_timeout: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    c->timeout_s = seconds;
+    return EPP_OK;
+}
+
+epp_status epp_comm_abort(epp_comm* c) {
+    if (!c) {
+        set_error("epp_comm_abort: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    c->abort_req.store(true);
+    return EPP_OK;
+}
+
 epp_status epp_comm_allgather_waypoints(epp_comm* c, const double* wp, int32_t n, int32_t cap, double* out,
                                         int32_t* counts) {
     if (!c || n < -1 || cap < 0 || (n > 0 && !wp) || !counts || (cap > 0 && !out)) {
@@ -212,6 +301,7 @@ epp_status epp_comm_allgather_waypoints(epp_comm* c, const double* wp, int32_t n
     }
     const Rccl* r = rccl();
     if (!r) return EPP_ERR_UNSUPPORTED;
+    if (const epp_status us = comm_usable(r, c, "epp_comm_allgather_waypoints")) return us;
     CommScope scope(c);
     hipError_t he = scope.he;
     const int R = c->n_ranks;
@@ -223,8 +313,8 @@ epp_status epp_comm_allgather_waypoints(epp_comm* c, const double* wp, int32_t n
     ncclResult_t e = r->allGather(c->d_buf, c->d_buf + 4, 1, ncclInt32, c->comm, c->stream);
     if (e != ncclSuccess) return nccl_error(r, e, "ncclAllGather (counts)");
     he = hipMemcpyAsync(counts, c->d_buf + 4, (size_t)R * 4, hipMemcpyDeviceToHost, c->stream);
-    if (he == hipSuccess) he = hipStreamSynchronize(c->stream);
     if (he != hipSuccess) return hip_fail("epp_comm_allgather_waypoints", he);
+    if (const epp_status ws = comm_wait(r, c, "ncclAllGather (counts)")) return ws;
     // every rank holds the same counts, so every rank takes the same branch below
     int32_t maxw = 0, failed = -1, n_failed = 0;
     for (int i = 0; i < R; ++i) {
@@ -255,9 +345,8 @@ epp_status epp_comm_allgather_waypoints(epp_comm* c, const double* wp, int32_t n
         if (counts[i] > 0)
             he = hipMemcpyAsync(out + (size_t)i * cap * 3, d_recv + (size_t)i * set_b, (size_t)counts[i] * 24,
                                 hipMemcpyDeviceToHost, c->stream);
-    if (he == hipSuccess) he = hipStreamSynchronize(c->stream);
     if (he != hipSuccess) return hip_fail("epp_comm_allgather_waypoints", he);
-    return EPP_OK;
+    return comm_wait(r, c, "ncclAllGather (waypoints)");
 }
 
 epp_status epp_comm_allreduce_f64(epp_comm* c, double* x, int32_t n, int32_t op) {
@@ -268,6 +357,7 @@ epp_status epp_comm_allreduce_f64(epp_comm* c, double* x, int32_t n, int32_t op)
     const Rccl* r = rccl();
     if (!r) return EPP_ERR_UNSUPPORTED;
     if (n == 0) return EPP_OK;
+    if (const epp_status us = comm_usable(r, c, "epp_comm_allreduce_f64")) return us;
     CommScope scope(c);
     hipError_t he = scope.he;
     const size_t bytes = ((size_t)n * 8 + 255) & ~size_t(255);
@@ -278,9 +368,8 @@ epp_status epp_comm_allreduce_f64(epp_comm* c, double* x, int32_t n, int32_t op)
     const ncclResult_t e = r->allReduce(c->d_buf, c->d_buf, (size_t)n, ncclFloat64, rop, c->comm, c->stream);
     if (e != ncclSuccess) return nccl_error(r, e, "ncclAllReduce");
     he = hipMemcpyAsync(x, c->d_buf, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream);
-    if (he == hipSuccess) he = hipStreamSynchronize(c->stream);
     if (he != hipSuccess) return hip_fail("epp_comm_allreduce_f64", he);
-    return EPP_OK;
+    return comm_wait(r, c, "ncclAllReduce");
 }
 
 epp_status epp_comm_barrier(epp_comm* c) {

@@ -36,7 +36,9 @@ std::vector<TrackResult> planTracks(const std::vector<TrackProblem>& tracks, con
     std::vector<std::vector<int32_t>> counts(n, std::vector<int32_t>(n));
     // Error protocol: a rank whose plan throws still takes part in the round's exchange,
     // with count -1; every rank then gets EPP_ERR_PEER from the same all-gather and leaves
-    // the loop at the same round, so no rank is left waiting in RCCL.  The caller gets the
+    // the loop at the same round, so no rank is left waiting in RCCL.  A rank whose exchange
+    // itself fails past the counts aborts every communicator (epp_comm_abort: the others'
+    // polled waits end with EPP_ERR_PEER), and every wait has a deadline (epp.h).  The caller gets the
     // exception of the lowest failed rank (its own message, e.g. "Path not found").  A
     // capacity error is reported identically on all ranks by the all-gather as well.
     std::vector<std::exception_ptr> err(n);
@@ -73,7 +75,13 @@ std::vector<TrackResult> planTracks(const std::vector<TrackProblem>& tracks, con
                     if (!err[r])
                         err[r] = std::make_exception_ptr(std::runtime_error(std::string("planTracks: all-gather: ") +
                                                                             epp_last_error()));
-                    break;  // EPP_ERR_PEER / EPP_ERR_CAPACITY: every rank breaks at this round
+                    // EPP_ERR_PEER / EPP_ERR_CAPACITY come from the counts every rank holds:
+                    // every rank breaks at this round.  Any other failure is this rank's own
+                    // (a HIP error, a timeout) and may have left the others inside the data
+                    // all-gather: abort every communicator, so their waits return at once.
+                    if (st != EPP_ERR_PEER && st != EPP_ERR_CAPACITY)
+                        for (epp_comm* x : comms) (void)epp_comm_abort(x);
+                    break;
                 }
                 if (r == 0)  // rank 0's copy fills the results (all ranks hold the same)
                     for (int q = 0; q < n; ++q) {

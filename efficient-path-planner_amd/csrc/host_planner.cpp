@@ -84,6 +84,9 @@ PathPlanner::PathPlanner(const Matrix& gates, const Matrix& obstacles, std::shar
     : configParser(std::move(cp)) {
     worldPtr = std::make_shared<World>(configParser);
     parseGatesAndObstacles(gates, obstacles);  // src/PathPlanner.cpp:27-35
+    // the device world (index build, its HBM and pinned buffers, the upload) now, as the
+    // reference builds its World here, not inside the first planPath
+    (void)worldPtr->device();
 }
 
 // src/PathPlanner.cpp:60-78

@@ -24,6 +24,7 @@ EPP_ERR_HIP = -3
 EPP_ERR_UNSUPPORTED = -4
 EPP_ERR_CAPACITY = -5
 EPP_ERR_PEER = -6
+EPP_ERR_TIMEOUT = -7
 EPP_REDUCE_SUM, EPP_REDUCE_MAX, EPP_REDUCE_MIN = 0, 1, 2
 
 _lib = None
@@ -82,6 +83,8 @@ def lib() -> C.CDLL:
             "epp_comm_allgather_waypoints": (i32, [vp, vp, i32, i32, vp, vp]),
             "epp_comm_allreduce_f64": (i32, [vp, vp, i32, i32]),
             "epp_comm_barrier": (i32, [vp]),
+            "epp_comm_set_timeout": (i32, [vp, dp]),
+            "epp_comm_abort": (i32, [vp]),
             "epp_comm_available": (i32, []),
             "epp_check_states": (i32, [vp, vp, i64, i32, vp, vp, vp, vp]),
             "epp_check_states_mindist": (i32, [vp, vp, i64, dp, vp, vp]),
@@ -142,6 +145,7 @@ EXPORTED = [
     "epp_generate_trajectory_times_host", "epp_world_generation", "epp_world_build_index", "epp_comm_unique_id", "epp_comm_init",
     "epp_comm_init_all", "epp_comm_destroy", "epp_comm_rank", "epp_comm_allgather_waypoints",
     "epp_comm_allreduce_f64", "epp_comm_barrier", "epp_comm_available", "epp_knn_ws_box", "epp_knn_grid_ws_box",
+    "epp_comm_set_timeout", "epp_comm_abort",
 ]
 
 
@@ -581,6 +585,15 @@ class Comm:
 
     def barrier(self) -> None:
         check(lib().epp_comm_barrier(self.handle))
+
+    def set_timeout(self, seconds: float) -> None:
+        """Deadline of every later collective (epp_comm_set_timeout)."""
+        check(lib().epp_comm_set_timeout(self.handle, float(seconds)))
+
+    def abort(self) -> None:
+        """Request an abort (epp_comm_abort; any thread): the collective in flight, or the
+        next one, aborts the communicator and fails."""
+        check(lib().epp_comm_abort(self.handle))
 
     def close(self) -> None:
         if self.handle:

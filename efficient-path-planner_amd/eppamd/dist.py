@@ -252,12 +252,14 @@ class GlooGroup(Group):
     """torch.distributed "gloo" (CPU tensors): the world_size > 1 tests without a GPU."""
     kind = "gloo"
 
-    def __init__(self, ws: int, rank: int):
+    def __init__(self, ws: int, rank: int, timeout_s: float = 60.0):
+        import datetime
+
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.ws, self.rank = torch, dist, ws, rank
-        if ws > 1:
-            dist.init_process_group("gloo")
+        if ws > 1:  # (a collective a peer never joins fails after timeout_s, as epp_comm's deadline)
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=timeout_s))
 
     def barrier(self) -> None:
         if self.ws > 1:
@@ -290,7 +292,10 @@ class GlooGroup(Group):
         if len(wp):
             buf[:len(wp)] = torch.from_numpy(wp)
         outs = [torch.zeros_like(buf) for _ in range(self.ws)]
-        dist.all_gather(outs, buf)
+        try:  # a peer that dies (or hangs) past the counts: an error here, not a hang
+            dist.all_gather(outs, buf)
+        except RuntimeError as e:
+            raise LegFailed([], f"all-gather: a peer failed during the data exchange ({e})") from e
         return [o[:c].numpy() for o, c in zip(outs, counts)]
 
     def close(self) -> None:

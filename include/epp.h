@@ -47,6 +47,7 @@ typedef int32_t epp_status;
 #define EPP_ERR_UNSUPPORTED (-4)      /* rotation other than about z (src/Object.cpp:38-47) */
 #define EPP_ERR_CAPACITY (-5)         /* an output buffer was too small */
 #define EPP_ERR_PEER (-6)             /* another rank of a collective reported a failure */
+#define EPP_ERR_TIMEOUT (-7)          /* a collective did not complete within the communicator's timeout */
 
 /* An oriented bounding box after the world build (reference class OBB,
  * include/OBB.h:19-57).  rot is the row-major rotation matrix; the reference only
@@ -268,6 +269,16 @@ epp_status epp_comm_init(const uint8_t id[128], int32_t n_ranks, int32_t rank, e
 epp_status epp_comm_init_all(int32_t n_devices, const int32_t* devices, epp_comm** out /* n_devices */);
 epp_status epp_comm_destroy(epp_comm* comm);
 epp_status epp_comm_rank(const epp_comm* comm, int32_t* rank, int32_t* n_ranks);
+/* Failure safety of every collective below: the call never blocks inside RCCL.  While its
+ * collective runs it polls RCCL's asynchronous error state (a peer process died, a broken
+ * connection), an abort requested with epp_comm_abort, and a deadline (default 120 s,
+ * epp_comm_set_timeout).  On any of them it aborts the communicator (ncclCommAbort) and
+ * returns EPP_ERR_PEER (error, abort) or EPP_ERR_TIMEOUT; every later call on that
+ * communicator returns EPP_ERR_PEER at once (destroy it and create a new one).
+ * epp_comm_abort may be called from any thread (e.g. by the owner of another rank's
+ * communicator in the same process when that rank failed locally). */
+epp_status epp_comm_set_timeout(epp_comm* comm, double seconds);
+epp_status epp_comm_abort(epp_comm* comm);
 /* All-gather of every rank's waypoint set (wp: n x 3 HOST doubles): counts[r] = rank r's
  * count (n_ranks entries), out + r * cap * 3 = its points (HOST, n_ranks x cap x 3).  Every
  * rank must call it, also a rank that has no set because its own work failed: it passes

@@ -617,6 +617,31 @@ int or_minsnap_track(const double* wp, int n_wp, double v_max, double a_max, con
     return or_minsnap_solve(mask.data(), val.data(), n_wp, dim, seg_times, 4, coeffs);
 }
 
+// A batch of independent tracks (the CPU side of BASELINE C5's batched refit): track k is
+// wp[off[k] .. off[k+1]) and gets one or_minsnap_track call (v0 = a0 = 0), its segment
+// times at T + (off[k] - k) and coefficients at C + (off[k] - k) * 30, on nt threads
+// (contiguous ranges of tracks).  status[k] = or_minsnap_track's return value.
+void or_minsnap_batch_mt(const double* wp, const int32_t* off, int n_tracks, double v_max, double a_max,
+                         double* T, double* C, int32_t* status, int nt) {
+    if (nt < 1) nt = 1;
+    const double z[3] = {0.0, 0.0, 0.0};
+    auto run = [=](int b, int e) {
+        for (int k = b; k < e; ++k) {
+            const int64_t seg0 = (int64_t)off[k] - k;
+            status[k] = or_minsnap_track(wp + 3 * (int64_t)off[k], off[k + 1] - off[k], v_max, a_max, z, z,
+                                         T + seg0, C + seg0 * 30);
+        }
+    };
+    std::vector<std::thread> th;
+    const int chunk = (n_tracks + nt - 1) / nt;
+    for (int t = 0; t < nt; ++t) {
+        const int b = t * chunk, e = std::min(n_tracks, b + chunk);
+        if (b >= e) break;
+        th.emplace_back(run, b, e);
+    }
+    for (auto& x : th) x.join();
+}
+
 int64_t or_sample_traj(const double* T, const double* coeffs, int M, double dt, double t0,
                        double* rows, int64_t max_rows) {
     // Trajectory::evaluateRange(min_time=0, max_time, dt, k) — src/trajectory.cpp:81-141

@@ -93,6 +93,11 @@ int or_minsnap_solve(const uint8_t* fixed_mask, const double* fixed_val, int n_v
  * end p,0,0,0,0), Nfabian times, solve.  coeffs: (W-1) x 3 x 10. */
 int or_minsnap_track(const double* wp, int n_wp, double v_max, double a_max, const double v0[3],
                      const double a0[3], double* seg_times, double* coeffs);
+/* A batch of independent tracks: track k = wp[off[k] .. off[k+1]) (v0 = a0 = 0) through
+ * or_minsnap_track on nt threads; times at T + off[k] - k, coeffs at C + (off[k] - k) x 30,
+ * status[k] its return value (the CPU baseline of BASELINE C5's batched refit). */
+void or_minsnap_batch_mt(const double* wp, const int32_t* off, int n_tracks, double v_max, double a_max,
+                         double* T, double* C, int32_t* status, int nt);
 /* Trajectory::evaluateRange x3 -> rows x 10 [x,vx,ax,y,vy,ay,z,vz,az,t+t0].
  * Returns the number of rows (writes at most max_rows; call with rows=NULL to count). */
 int64_t or_sample_traj(const double* seg_times, const double* coeffs, int n_seg, double dt,

@@ -46,6 +46,7 @@ def lib() -> C.CDLL:
             "or_segment_times": (None, [vp, i32, i32, dp, dp, vp]),
             "or_minsnap_solve": (i32, [vp, vp, i32, i32, vp, i32, vp]),
             "or_minsnap_track": (i32, [vp, i32, dp, dp, vp, vp, vp, vp]),
+            "or_minsnap_batch_mt": (None, [vp, vp, i32, dp, dp, vp, vp, vp, i32]),
             "or_sample_traj": (i64, [vp, vp, i32, dp, dp, vp, i64]),
             "or_generate_trajectory": (i64, [vp, i32, dp, dp, dp, dp, vp, vp, vp, i64]),
             "or_mapping_matrix": (None, [dp, vp]),
@@ -148,6 +149,26 @@ def minsnap_track(wp, v_max, a_max, v0=(0, 0, 0), a0=(0, 0, 0)):
     if rc < 0:
         raise RuntimeError(f"or_minsnap_track failed {rc}")
     return T, Cf
+
+
+def minsnap_batch(tracks, v_max, a_max, threads=1):
+    """or_minsnap_batch_mt: every track (v0 = a0 = 0) solved by or_minsnap_track on
+    `threads` threads.  Returns (times list, coeff list, status array) like
+    eppamd.capi.minsnap_batch."""
+    wp = np.ascontiguousarray(np.concatenate([np.asarray(t, np.float64).reshape(-1, 3) for t in tracks]))
+    off = np.zeros(len(tracks) + 1, np.int32)
+    off[1:] = np.cumsum([len(t) for t in tracks])
+    nseg = int(off[-1]) - len(tracks)
+    T = np.zeros(max(nseg, 1))
+    Cf = np.zeros((max(nseg, 1), 3, 10))
+    st = np.zeros(len(tracks), np.int32)
+    lib().or_minsnap_batch_mt(_p(wp), _p(off), len(tracks), v_max, a_max, _p(T), _p(Cf), _p(st), int(threads))
+    Ts, Cs = [], []
+    for k in range(len(tracks)):
+        a, b = off[k] - k, off[k + 1] - k - 1
+        Ts.append(T[a:b])
+        Cs.append(Cf[a:b])
+    return Ts, Cs, st
 
 
 def sample_traj(T, coeffs, dt, t0=0.0):

@@ -119,6 +119,20 @@ def test_bench_rank_failure_at_exchange_fails_every_rank():
     assert out.stderr.count("reported a failure") >= 2, out.stderr[-2000:]
 
 
+def test_bench_rank_dying_after_counts_fails_every_rank():
+    """A rank that dies after sending its count (its peers are then inside the data
+    all-gather) must not leave them waiting: both ranks exit non-zero within the timeout,
+    rank 0 through the exchange's own error (LegFailed), not the spawner's termination."""
+    import time
+    t = time.monotonic()
+    out = _run_bench_ws2(["--fail-rank", "1", "--fail-at", "after-count"], timeout=180)
+    assert out.returncode != 0
+    assert time.monotonic() - t < 120
+    assert "rank 1: dying after the counts" in out.stderr, out.stderr[-2000:]
+    assert "bench.py rank 0: all-gather: a peer failed during the data exchange" in out.stderr, out.stderr[-2000:]
+    assert "exit codes [1, 7]" in out.stderr, out.stderr[-2000:]
+
+
 def _exchange_worker(rank, ws, d, q):
     import sys
     sys.path.insert(0, PKG)

@@ -839,6 +839,31 @@ def test_comm_failure_protocol_single_rank():
     c.close()
 
 
+def test_comm_abort_and_timeout_single_rank():
+    """The collectives' failure safety (epp.h): an abort requested from any thread makes the
+    collective in flight or the next one abort the communicator and fail with EPP_ERR_PEER
+    instead of waiting in RCCL; every later call fails at once; destroy still works.  The
+    deadline setter validates its argument."""
+    c = capi.Comm(capi.Comm.unique_id(), 1, 0)
+    c.set_timeout(5.0)
+    with pytest.raises(capi.EppError) as e:
+        c.set_timeout(0.0)
+    assert e.value.code == capi.EPP_ERR_INVALID_ARGUMENT
+    wp = synth.sample_states(6, [-6, -6, 0], [6, 6, 2], 5)
+    assert np.array_equal(c.allgather_waypoints(wp, cap=8)[0], wp)
+    c.abort()
+    with pytest.raises(capi.EppError) as e:
+        c.allgather_waypoints(wp, cap=8)
+    assert e.value.code == capi.EPP_ERR_PEER and "aborted" in str(e.value)
+    with pytest.raises(capi.EppError) as e:
+        c.barrier()
+    assert e.value.code == capi.EPP_ERR_PEER
+    c.close()
+    c2 = capi.Comm(capi.Comm.unique_id(), 1, 0)  # a new communicator works
+    c2.barrier()
+    c2.close()
+
+
 def test_rccl_group_single_rank():
     """eppamd.dist.RcclGroup (the bench's torch-free process group) on one rank."""
     from eppamd.dist import LegFailed, RcclGroup
