@@ -675,8 +675,9 @@ def c5_online(cfg_path, geom, gates, obstacles, wp, window, vmax, amax, dt, md, 
     re-check of the 100 lookahead rows (PathPlanner::checkTrajectoryValidity with
     min_dist_check_traj_collision, src/PathPlanner.cpp:267-280) -> 12-segment min-snap refit
     (W = 13, the gate's centre waypoint moved) from the current state -> sampled at dt
-    (poly_traj::generateTrajectory).  The GPU step runs the product (PathPlanner /
-    polynomial_trajectory modules); cpu=True runs the same step on the CPU oracle (world
+    (poly_traj::generateTrajectory).  The GPU step runs the product (PathPlanner:
+    update_gate_pos, then check_trajectory_validity_and_generate -- the check and the refit
+    in one launch); cpu=True runs the same step on the CPU oracle (world
     rebuild, minDistance check, min-snap + sampling).  Returns per-step microseconds."""
     gates = np.array(gates, float)
     perturb = c5_steps(window, steps)
@@ -713,10 +714,11 @@ def c5_online(cfg_path, geom, gates, obstacles, wp, window, vmax, amax, dt, md, 
         pose[1] += d[1]
         pose[5] += d[2]
         pp.update_gate_pos(g, pose)
-        pp.check_trajectory_validity(rows[:100], md)
         wp2 = wp.copy()
         wp2[wi, :2] = pose[:2]
-        rows = pt.generate_trajectory(wp2, vmax, amax, dt, 0.0, v0, a0)
+        # the A11 check of the lookahead rows and the refit in one launch (the product's
+        # online step; the same flags and rows as the two calls, tests/test_gpu_minsnap.py)
+        _, rows = pp.check_trajectory_validity_and_generate(rows[:100], md, wp2, vmax, amax, dt, 0.0, v0, a0)
         lat[s] = time.perf_counter() - t
     return lat * 1e6
 

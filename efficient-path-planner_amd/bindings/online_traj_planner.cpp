@@ -126,6 +126,28 @@ PYBIND11_MODULE(online_traj_planner, m) {
             },
             py::arg("trajectory"), py::arg("minDistance"))
         .def(
+            "check_trajectory_validity_and_generate",  // the C5 online step in one launch (this build)
+            [](const epp::PathPlanner& self, const py::object& traj, double minDistance, const py::object& waypoints,
+               double vMax, double aMax, double samplingInterval, double startTimeOffset, const py::object& v0,
+               const py::object& a0) {
+                Matrix m = to_matrix(traj), w = to_matrix(waypoints);
+                if (w.cols != 3) throw std::invalid_argument("waypoints must be an (n, 3) array");
+                std::vector<Vec3> wp;
+                for (size_t i = 0; i < w.rows; ++i) wp.emplace_back(w(i, 0), w(i, 1), w(i, 2));
+                const Vec3 v = to_vec3(v0), a = to_vec3(a0);
+                Matrix out;
+                bool valid;
+                {
+                    py::gil_scoped_release release;
+                    valid = self.checkTrajectoryValidityAndGenerate(m, minDistance, wp, vMax, aMax, samplingInterval,
+                                                                    startTimeOffset, v, a, out);
+                }
+                return py::make_tuple(valid, from_matrix(out));
+            },
+            py::arg("trajectory"), py::arg("minDistance"), py::arg("waypoints"), py::arg("v_max"), py::arg("a_max"),
+            py::arg("sampling_interval"), py::arg("startTimeOffset") = 0.0,
+            py::arg("v0") = py::make_tuple(0.0, 0.0, 0.0), py::arg("a0") = py::make_tuple(0.0, 0.0, 0.0))
+        .def(
             "check_point_validity",
             [](const epp::PathPlanner& self, const py::object& p, bool canPassGate) {
                 return self.worldPtr->checkPointValidity(to_vec3(p), canPassGate);

@@ -51,6 +51,20 @@ namespace epp {
 epp_status generate_trajectory_into(const double* wp, int32_t n_wp, const double* times, double v_max,
                                     double a_max, double dt, double t0, const double v0[3], const double a0[3],
                                     double* (*alloc)(void*, int64_t), void* ctx, int64_t* n_rows);
+// The same with the C5 online step's A11 check fused into the launch (chk != NULL): the
+// minDistance flags of chk->n points (host array) against chk->world, written to
+// chk->valid, by extra workgroups of the refit's kernel (k_check_refit).  The check must be
+// small (<= kSmallStates points, <= kSmallMaxObbs OBBs), else EPP_ERR_UNSUPPORTED.
+struct FusedCheck {
+    const epp_world* world;
+    const double* xyz;
+    int64_t n;
+    double min_distance;
+    uint8_t* valid;
+};
+epp_status check_and_generate_into(const FusedCheck* chk, const double* wp, int32_t n_wp, const double* times,
+                                   double v_max, double a_max, double dt, double t0, const double v0[3],
+                                   const double a0[3], double* (*alloc)(void*, int64_t), void* ctx, int64_t* n_rows);
 // epp_mask_edges_count without clearing `count` first: the counts are added to what it
 // holds (the planner clears them with its first upload).  out16 != NULL: also a copy of
 // the masked table as u16, 0xFFFF for no edge (node counts <= 65535).

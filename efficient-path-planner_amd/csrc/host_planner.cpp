@@ -19,6 +19,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "epp/PathPlanner.h"
+#include "epp/trajectory_generator.h"
 #include "epp_internal.h"
 #include "host_scratch.h"
 
@@ -565,6 +566,59 @@ std::vector<Vec3> PathPlanner::pruneWaypoints(const std::vector<Vec3>& w) const 
 // PathPlanner::checkTrajectoryValidity — src/PathPlanner.cpp:267-280 (one batched launch)
 bool PathPlanner::checkTrajectoryValidity(const Matrix& traj, double minDistance) const {
     return checkTrajectoryValidityOn(*worldPtr, traj, minDistance);
+}
+
+bool PathPlanner::checkTrajectoryValidityAndGenerate(const Matrix& traj, double minDistance,
+                                                     const std::vector<Vec3>& waypoints, double vMax, double aMax,
+                                                     double samplingInterval, double startTimeOffset, const Vec3& v0,
+                                                     const Vec3& a0, Matrix& result) const {
+    if (waypoints.size() < 2) throw std::invalid_argument("At least two waypoints are required");
+    thread_local std::vector<double> xyz, wp;
+    thread_local std::vector<uint8_t> ok;
+    xyz.resize(traj.rows * 3);
+    for (size_t i = 0; i < traj.rows; ++i) {
+        xyz[3 * i] = traj(i, 0);
+        xyz[3 * i + 1] = traj(i, 3);
+        xyz[3 * i + 2] = traj(i, 6);
+    }
+    wp.resize(waypoints.size() * 3);
+    for (size_t i = 0; i < waypoints.size(); ++i) {
+        wp[3 * i] = waypoints[i].x;
+        wp[3 * i + 1] = waypoints[i].y;
+        wp[3 * i + 2] = waypoints[i].z;
+    }
+    ok.assign(traj.rows, 0);
+    const double v[3] = {v0.x, v0.y, v0.z}, a[3] = {a0.x, a0.y, a0.z};
+    const FusedCheck chk{worldPtr->device(), xyz.data(), (int64_t)traj.rows, minDistance, ok.data()};
+    Matrix tmp;
+    std::swap(tmp, result);  // (result keeps its old value if the call throws)
+    auto into = [](void* ctx, int64_t R) -> double* {
+        Matrix& m = *static_cast<Matrix*>(ctx);
+        m.rows = (size_t)R;
+        m.cols = 10;
+        m.data.resize((size_t)std::max<int64_t>(R, 1) * 10);
+        return m.data.data();
+    };
+    int64_t n = 0;
+    const epp_status rc = check_and_generate_into(traj.rows ? &chk : nullptr, wp.data(), (int32_t)waypoints.size(),
+                                                  nullptr, vMax, aMax, samplingInterval, startTimeOffset, v, a, into,
+                                                  &tmp, &n);
+    if (rc == EPP_ERR_UNSUPPORTED) {  // (a large check: the two calls)
+        std::swap(tmp, result);
+        const bool valid = checkTrajectoryValidity(traj, minDistance);
+        poly_traj::generateTrajectory(waypoints, vMax, aMax, samplingInterval, startTimeOffset, v0, a0, result);
+        return valid;
+    }
+    if (rc != EPP_OK) {
+        std::swap(tmp, result);
+        if (rc == EPP_ERR_INVALID_ARGUMENT) throw std::invalid_argument(epp_last_error());
+        throw std::runtime_error(std::string("generateTrajectory: ") + epp_last_error());
+    }
+    tmp.data.resize((size_t)n * 10);
+    std::swap(tmp, result);
+    for (uint8_t v8 : ok)
+        if (!v8) return false;
+    return true;
 }
 
 bool PathPlanner::checkTrajectoryValidityOn(const World& world, const Matrix& traj, double minDistance) {

@@ -31,6 +31,7 @@
 
 #include "cached_ws.h"
 #include "epp_internal.h"
+#include "small_body.h"
 
 namespace epp {
 namespace {
@@ -715,9 +716,8 @@ __host__ __device__ inline size_t refit_lds_doubles(int M, bool lds) {
 }
 
 template <bool LDS>
-__global__ __launch_bounds__(kRefitBlock) void k_refit(RefitArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int tid = threadIdx.x, W = a.W, M = W - 1, R = a.R, g = blockIdx.x;
+__device__ __forceinline__ void refit_body(const RefitArgs& a, int g, double* smem) {
+    const int tid = threadIdx.x, W = a.W, M = W - 1, R = a.R;
     const double* h_tin = a.in + 3 * W + 6 + M;
     const double* h_tac = h_tin + R;
     const int32_t* h_seg = reinterpret_cast<const int32_t*>(h_tac + R);
@@ -813,6 +813,44 @@ __global__ __launch_bounds__(kRefitBlock) void k_refit(RefitArgs a) {
         if (g == 0) __hip_atomic_store(a.info, (int64_t)st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(a.done + g, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+template <bool LDS>
+__global__ __launch_bounds__(kRefitBlock) void k_refit(RefitArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    refit_body<LDS>(a, blockIdx.x, smem);
+}
+
+// ---- the C5 online step in one launch: A11 check + refit --------------------------------
+// PathPlanner::checkTrajectoryValidity of the lookahead rows against the world
+// (World::checkPointValidity(p, minDistance), src/World.cpp:106-128, src/PathPlanner.cpp:
+// 267-280) and the refit of the moved waypoints (poly_traj::generateTrajectory) are
+// independent: workgroups [0, writers) run the refit (refit_body), workgroups [writers,
+// writers + check groups) the brute-force minDistance check of k_states_small
+// (states_small_body, small_body.h) over the pinned points, flags into pinned memory.  Every
+// workgroup publishes `seq` in its completion slot: one launch, one host poll for both.
+static_assert(kRefitBlock == kSmallBlock, "one block size for both parts");
+struct CheckArgs {
+    const double* recs;  // OBB records (device blob or pinned host copy: SmallWorld)
+    int32_t n_obb, per;
+    double rg, ro, md;
+    const double* xyz;   // host-mapped: n x 3
+    int64_t n;
+    uint8_t* valid;      // host-mapped: n flags
+};
+
+template <bool LDS>
+__global__ __launch_bounds__(kRefitBlock) void k_check_refit(RefitArgs a, CheckArgs c) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    if ((int)blockIdx.x < a.writers) {  // (block-uniform)
+        refit_body<LDS>(a, blockIdx.x, smem);
+        return;
+    }
+    states_small_body<true, false>(smem, (int)blockIdx.x - a.writers, c.recs, c.n_obb, c.rg, c.ro, c.xyz, c.n, c.per, 0,
+                                   c.md, c.valid, nullptr, nullptr);
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(a.done + blockIdx.x, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 bool g_consts_ready[64];
@@ -927,15 +965,6 @@ epp_status read_offsets(const int32_t* d_off, int n_tracks, hipStream_t s, const
     }
     *max_m = m;
     if (total_m) *total_m = tot;
-    return EPP_OK;
-}
-
-epp_status launch_error(const char* what) {
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        set_error(std::string(what) + ": " + hipGetErrorString(e));
-        return EPP_ERR_HIP;
-    }
     return EPP_OK;
 }
 
@@ -1111,7 +1140,15 @@ epp_status epp_sample_batch(const double* seg_times, const double* coeffs, const
 epp_status epp::generate_trajectory_into(const double* wp, int32_t n_wp, const double* times, double v_max,
                                          double a_max, double dt, double t0, const double v0[3], const double a0[3],
                                          double* (*alloc)(void*, int64_t), void* ctx, int64_t* n_rows) {
-    if (!alloc || !n_rows || (n_wp > 0 && !wp)) {
+    return check_and_generate_into(nullptr, wp, n_wp, times, v_max, a_max, dt, t0, v0, a0, alloc, ctx, n_rows);
+}
+
+epp_status epp::check_and_generate_into(const FusedCheck* chk, const double* wp, int32_t n_wp, const double* times,
+                                        double v_max, double a_max, double dt, double t0, const double v0[3],
+                                        const double a0[3], double* (*alloc)(void*, int64_t), void* ctx,
+                                        int64_t* n_rows) {
+    if (!alloc || !n_rows || (n_wp > 0 && !wp) ||
+        (chk && (!chk->world || chk->n < 0 || (chk->n > 0 && (!chk->xyz || !chk->valid))))) {
         set_error("generateTrajectory: invalid argument");
         return EPP_ERR_INVALID_ARGUMENT;
     }
@@ -1150,7 +1187,25 @@ epp_status epp::generate_trajectory_into(const double* wp, int32_t n_wp, const d
     const int R = (int)c.tin.size();
     const bool lds = M <= kMaxLdsSeg;
     const int G = R ? std::min(kRefitMaxWriters, (R + kRefitRowChunk - 1) / kRefitRowChunk) : 1;
-    if ((rc = c.ensure(refit_in_doubles(n_wp, R) * 8, (size_t)R * 80 + 128,
+    // the fused check (chk): the lookahead points after the refit's inputs (h_in), their
+    // flags after the completion slots (h_out); its workgroups after the refit's.  The
+    // records' snapshot (and its lease: no update rewrites them) is held until the poll ends.
+    SmallWorld sw{};
+    const int64_t nck = chk ? chk->n : 0;
+    int per = kSmallBlock, Gc = 0;
+    if (nck > 0) {
+        sw = small_world(chk->world);
+        if (nck > kSmallStates || sw.n_obb > kSmallMaxObbs) {
+            set_error("checkAndGenerate: the check is not small (<= 4096 points, <= 256 OBBs)");
+            return EPP_ERR_UNSUPPORTED;
+        }
+        per = small_per(nck);
+        Gc = (int)((nck + per - 1) / per);
+    }
+    const size_t in_refit = (refit_in_doubles(n_wp, R) + 1) & ~size_t(1);  // (16-byte aligned points after it)
+    constexpr size_t kRowsAt = 256;  // h_out: [status | pad | slots (<= 48 x 4 B) | flags | rows]
+    const size_t rows_at = kRowsAt + (((size_t)nck + 255) & ~size_t(255));
+    if ((rc = c.ensure((in_refit + 3 * (size_t)nck) * 8, (size_t)R * 80 + rows_at,
                        lds ? 0 : (size_t)G * M * Seg::kSize * 8)))
         return rc;
     double* in = c.h_in;
@@ -1177,18 +1232,38 @@ epp_status epp::generate_trajectory_into(const double* wp, int32_t n_wp, const d
     if (n_wp <= kRefitArgW) std::memcpy(a.small, in, (size_t)(3 * n_wp + 6 + M) * 8);
     a.info = reinterpret_cast<int64_t*>(c.h_out);
     a.done = reinterpret_cast<uint32_t*>(c.h_out + 64);
-    a.out = reinterpret_cast<double*>(c.h_out + 128);
+    a.out = reinterpret_cast<double*>(c.h_out + rows_at);
     a.scratch = c.d_scr;
     a.info[0] = -100;
-    const size_t shm = refit_lds_doubles(M, lds) * sizeof(double);
-    if (lds) hipLaunchKernelGGL(k_refit<true>, dim3(G), dim3(kRefitBlock), shm, c.s, a);
-    else hipLaunchKernelGGL(k_refit<false>, dim3(G), dim3(kRefitBlock), shm, c.s, a);
+    size_t shm = refit_lds_doubles(M, lds) * sizeof(double);
+    if (Gc > 0) {
+        double* pts = in + in_refit;
+        std::memcpy(pts, chk->xyz, (size_t)nck * 24);
+        CheckArgs ck;
+        ck.recs = sw.recs;
+        ck.n_obb = sw.n_obb;
+        ck.per = per;
+        ck.rg = sw.r_gate;
+        ck.ro = sw.r_obst;
+        ck.md = chk->min_distance;
+        ck.xyz = pts;
+        ck.n = nck;
+        ck.valid = reinterpret_cast<uint8_t*>(c.h_out + kRowsAt);
+        shm = std::max(shm, small_shm(sw.n_obb));
+        if (lds) hipLaunchKernelGGL(k_check_refit<true>, dim3(G + Gc), dim3(kRefitBlock), shm, c.s, a, ck);
+        else hipLaunchKernelGGL(k_check_refit<false>, dim3(G + Gc), dim3(kRefitBlock), shm, c.s, a, ck);
+    } else if (lds) {
+        hipLaunchKernelGGL(k_refit<true>, dim3(G), dim3(kRefitBlock), shm, c.s, a);
+    } else {
+        hipLaunchKernelGGL(k_refit<false>, dim3(G), dim3(kRefitBlock), shm, c.s, a);
+    }
     hipError_t e = hipGetLastError();
     // wait for the status word and every workgroup's slot (polled; the stream is queried
     // every ~1k polls so a failed launch ends the wait)
+    const int slots = G + Gc;
     auto complete = [&]() {
         if (__atomic_load_n(a.info, __ATOMIC_ACQUIRE) == -100) return false;
-        for (int g = 0; g < a.writers; ++g)
+        for (int g = 0; g < slots; ++g)
             if (__atomic_load_n(a.done + g, __ATOMIC_ACQUIRE) != a.seq) return false;
         return true;
     };
@@ -1207,6 +1282,7 @@ epp_status epp::generate_trajectory_into(const double* wp, int32_t n_wp, const d
         set_error(std::string("generateTrajectory: ") + hipGetErrorString(e));
         return EPP_ERR_HIP;
     }
+    if (Gc > 0) std::memcpy(chk->valid, c.h_out + kRowsAt, (size_t)nck);
     if (info != 0) {
         set_error(info == -2 ? "Segment times need to be greater than zero" : "min-snap solve failed");
         return EPP_ERR_RUNTIME;
@@ -1253,6 +1329,26 @@ epp_status epp_generate_trajectory_host(const double* wp, int32_t n_wp, double v
                                         double t0, const double v0[3], const double a0[3], double** rows_out,
                                         int64_t* n_rows) {
     return generate_trajectory(wp, n_wp, nullptr, v_max, a_max, dt, t0, v0, a0, rows_out, n_rows);
+}
+
+epp_status epp_check_and_generate_trajectory_host(const epp_world* world, const double* check_xyz, int64_t n_check,
+                                                  double min_distance, uint8_t* check_valid, const double* wp,
+                                                  int32_t n_wp, double v_max, double a_max, double dt, double t0,
+                                                  const double v0[3], const double a0[3], double** rows_out,
+                                                  int64_t* n_rows) {
+    if (!rows_out || !n_rows || !world || n_check < 0 || (n_check > 0 && (!check_xyz || !check_valid))) {
+        set_error("epp_check_and_generate_trajectory_host: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    *rows_out = nullptr;
+    const FusedCheck chk{world, check_xyz, n_check, min_distance, check_valid};
+    const epp_status rc = check_and_generate_into(&chk, wp, n_wp, nullptr, v_max, a_max, dt, t0, v0, a0, malloc_rows,
+                                                  rows_out, n_rows);
+    if (rc != EPP_OK && *rows_out) {
+        std::free(*rows_out);
+        *rows_out = nullptr;
+    }
+    return rc;
 }
 
 epp_status epp_generate_trajectory_times_host(const double* wp, int32_t n_wp, const double* seg_times, double dt,

@@ -93,6 +93,8 @@ def lib() -> C.CDLL:
             "epp_minsnap_batch_times": (i32, [vp, vp, i32, vp, vp, vp, vp, vp, vp]),
             "epp_sample_count": (i32, [vp, vp, i32, dp, vp, vp]),
             "epp_sample_batch": (i32, [vp, vp, vp, i32, dp, vp, vp, vp, vp]),
+            "epp_check_and_generate_trajectory_host": (i32, [vp, vp, i64, dp, vp, vp, i32, dp, dp, dp, dp, vp, vp,
+                                                               C.POINTER(C.POINTER(C.c_double)), C.POINTER(i64)]),
             "epp_generate_trajectory_host": (i32, [vp, i32, dp, dp, dp, dp, vp, vp,
                                                    C.POINTER(C.POINTER(C.c_double)), C.POINTER(i64)]),
             "epp_generate_trajectory_times_host": (i32, [vp, i32, vp, dp, dp, vp, vp,
@@ -145,7 +147,7 @@ EXPORTED = [
     "epp_generate_trajectory_times_host", "epp_world_generation", "epp_world_build_index", "epp_comm_unique_id", "epp_comm_init",
     "epp_comm_init_all", "epp_comm_destroy", "epp_comm_rank", "epp_comm_allgather_waypoints",
     "epp_comm_allreduce_f64", "epp_comm_barrier", "epp_comm_available", "epp_knn_ws_box", "epp_knn_grid_ws_box",
-    "epp_comm_set_timeout", "epp_comm_abort",
+    "epp_comm_set_timeout", "epp_comm_abort", "epp_check_and_generate_trajectory_host",
 ]
 
 
@@ -395,6 +397,26 @@ def generate_trajectory(waypoints, v_max, a_max, dt, t0=0.0, v0=(0, 0, 0), a0=(0
     out = np.ctypeslib.as_array(rows, shape=(n.value * 10,)).copy().reshape(-1, 10)
     lib().epp_host_free(C.cast(rows, C.c_void_p))
     return out
+
+
+def check_and_generate_trajectory(world: "World", check_xyz, min_distance, waypoints, v_max, a_max, dt, t0=0.0,
+                                  v0=(0, 0, 0), a0=(0, 0, 0)):
+    """epp_check_and_generate_trajectory_host: (minDistance flags of check_xyz against the
+    world, the trajectory rows of generate_trajectory) from one launch."""
+    pts = np.ascontiguousarray(np.asarray(check_xyz, np.float64).reshape(-1, 3))
+    wp = np.ascontiguousarray(np.asarray(waypoints, np.float64).reshape(-1, 3))
+    v0 = np.ascontiguousarray(v0, np.float64)
+    a0 = np.ascontiguousarray(a0, np.float64)
+    flags = np.zeros(max(len(pts), 1), np.uint8)
+    rows = C.POINTER(C.c_double)()
+    n = C.c_int64(0)
+    check(lib().epp_check_and_generate_trajectory_host(world.handle, _ptr(pts), len(pts), float(min_distance),
+                                                       _ptr(flags), _ptr(wp), len(wp), float(v_max), float(a_max),
+                                                       float(dt), float(t0), _ptr(v0), _ptr(a0), C.byref(rows),
+                                                       C.byref(n)))
+    out = np.ctypeslib.as_array(rows, shape=(n.value * 10,)).copy().reshape(-1, 10) if n.value else np.zeros((0, 10))
+    lib().epp_host_free(C.cast(rows, C.c_void_p))
+    return flags[:len(pts)], out
 
 
 def optimal_trajectory(waypoints, v_max, a_max, dt, t0=0.0, max_deviation=0.1, pre_waypoints=()) -> np.ndarray:

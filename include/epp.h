@@ -312,6 +312,20 @@ epp_status epp_generate_trajectory_host(const double* wp, int32_t n_wp, double v
 epp_status epp_generate_trajectory_times_host(const double* wp, int32_t n_wp, const double* seg_times, double dt,
                                               double t0, const double v0[3], const double a0[3], double** rows,
                                               int64_t* n_rows);
+/* The C5 online step's two GPU calls in ONE launch (an addition of this build; the
+ * reference makes them one after the other: PathPlanner::checkTrajectoryValidity,
+ * src/PathPlanner.cpp:267-280, then poly_traj::generateTrajectory, src/
+ * OnlineTrajGenerator.cpp:374-379): check_valid[i] = World::checkPointValidity(check_xyz[i],
+ * min_distance) (src/World.cpp:106-128) for the n_check points (HOST array, e.g. the
+ * lookahead rows' positions) against `world`, and the trajectory of epp_generate_trajectory_host.
+ * The check runs on extra workgroups of the refit's kernel: one pinned upload, one
+ * completion poll.  Same answers as the two calls.  The check must be small (n_check <=
+ * 4096, <= 256 OBBs), else EPP_ERR_UNSUPPORTED (make the two calls). */
+epp_status epp_check_and_generate_trajectory_host(const epp_world* world, const double* check_xyz, int64_t n_check,
+                                                  double min_distance, uint8_t* check_valid, const double* wp,
+                                                  int32_t n_wp, double v_max, double a_max, double dt, double t0,
+                                                  const double v0[3], const double a0[3], double** rows_out,
+                                                  int64_t* n_rows);
 /* The "optimal" trajectory type (OptimalTimeParametrizer::calculateTrajectory,
  * external/time_parametrization/src/OptimalTimeParametrizer.cpp:11-108; host code: one
  * sequential phase-plane integration).  wp: n_wp x 3, pre: n_pre x 3 lead-in points

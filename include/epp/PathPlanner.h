@@ -56,6 +56,16 @@ public:
                    std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const;
     void updateGatePos(int gateId, const std::vector<double>& newPose);
     bool checkTrajectoryValidity(const Matrix& trajectory, double minDistance) const;
+    // The C5 online step in one GPU launch (an addition of this build): returns
+    // checkTrajectoryValidity(trajectory, minDistance) and sets `result` to
+    // poly_traj::generateTrajectory(waypoints, vMax, aMax, samplingInterval,
+    // startTimeOffset, v0, a0) -- the two are independent, so the check runs on extra
+    // workgroups of the refit's kernel (epp_check_and_generate_trajectory_host).  Same
+    // answers as the two calls; a check too large for the small path makes the two calls.
+    bool checkTrajectoryValidityAndGenerate(const Matrix& trajectory, double minDistance,
+                                            const std::vector<Vec3>& waypoints, double vMax, double aMax,
+                                            double samplingInterval, double startTimeOffset, const Vec3& v0,
+                                            const Vec3& a0, Matrix& result) const;
     std::vector<Vec3> includeGates2(std::vector<std::vector<Vec3>> waypoints) const;
 
     // batch-planner knobs (defaults follow the config: samples_fmt samples, k = 16)

@@ -331,3 +331,69 @@ def test_polynomial_trajectory_errors():
         pt.generate_trajectory(np.zeros((4, 2)), 1.0, 2.0, 0.1)  # not (n, 3)
     with pytest.raises(RuntimeError, match="Segment times need to be greater than zero"):
         pt.generate_trajectory(np.array([[0, 0, 1.0], [0, 0, 1.0], [1, 0, 1.0]]), 1.0, 2.0, 0.1)
+
+
+# ---- the C5 online step in one launch (epp_check_and_generate_trajectory_host) ---------
+def _c5_world(cfg, geom):
+    from eppamd import config
+    rg, ro = config.inflate_radii(cfg)
+    gates, obstacles = synth.track_world(42)
+    return gates, obstacles, rg, ro
+
+
+@pytest.mark.parametrize("n_check", [0, 1, 100, 300, 4096])
+def test_check_and_generate_equals_two_calls(cfg, geom, n_check):
+    """The fused launch gives the A11 flags of World::checkPointValidity(p, minDistance)
+    (src/World.cpp:106-128; the oracle, bit for bit) and the rows of generateTrajectory
+    (the separate call, bit for bit; the oracle within 1e-6, time column exact), on the
+    current index and after a gate update (records read from pinned host memory)."""
+    gates, obstacles, rg, ro = _c5_world(cfg, geom)
+    md = float(cfg["path_planner_properties"]["min_dist_check_traj_collision"])
+    wp = synth.random_track_waypoints(77, 12)
+    for version in range(2):
+        g = gates.copy()
+        if version:
+            g[2, :2] += 0.25
+        ref = O.world_build(geom, g, obstacles, rg, ro)
+        w = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
+        if version:
+            w.update(capi.build_obbs(geom, g, obstacles))  # index stale: pinned records
+        rows0 = O.generate_trajectory(wp, 1.0, 2.0, 0.1, 0.0, (0.3, -0.1, 0.0), (0.0, 0.2, 0.0))
+        pts = np.vstack([rows0[:, [0, 3, 6]], synth.sample_states(5 + n_check, [-6, -6, 0], [6, 6, 2], 4096)])[:n_check]
+        flags, rows = capi.check_and_generate_trajectory(w, pts, md, wp, 1.0, 2.0, 0.1, 0.0, (0.3, -0.1, 0.0),
+                                                         (0.0, 0.2, 0.0))
+        assert np.array_equal(flags, O.check_states_mindist(ref, pts, md))
+        if n_check:
+            assert np.array_equal(flags, w.check_states_mindist(pts, md))
+        sep = capi.generate_trajectory(wp, 1.0, 2.0, 0.1, 0.0, (0.3, -0.1, 0.0), (0.0, 0.2, 0.0))
+        assert np.array_equal(rows, sep)
+        assert rows.shape == rows0.shape and np.array_equal(rows[:, 9], rows0[:, 9])
+        assert np.abs(rows[:, :9] - rows0[:, :9]).max() < 1e-6
+        w.close()
+
+
+def test_check_and_generate_large_check_unsupported_and_planner_fallback(cfg, geom, tmp_path):
+    """Over the small path's limit (4096 points) the C ABI says EPP_ERR_UNSUPPORTED; the
+    C++ / pybind PathPlanner entry then makes the two calls (same answers)."""
+    import online_traj_planner as otp
+    import polynomial_trajectory as pt
+    from conftest import CONFIG
+    gates, obstacles, rg, ro = _c5_world(cfg, geom)
+    md = float(cfg["path_planner_properties"]["min_dist_check_traj_collision"])
+    w = capi.World(capi.build_obbs(geom, gates, obstacles), rg, ro)
+    wp = synth.random_track_waypoints(78, 12)
+    pts = synth.sample_states(9, [-6, -6, 0], [6, 6, 2], 4097)
+    with pytest.raises(capi.EppError) as e:
+        capi.check_and_generate_trajectory(w, pts, md, wp, 1.0, 2.0, 0.1)
+    assert e.value.code == capi.EPP_ERR_UNSUPPORTED
+    w.close()
+    pp = otp.PathPlanner(gates, obstacles, CONFIG)
+    for n in (100, 4097):
+        traj = np.zeros((n, 10))
+        traj[:, [0, 3, 6]] = synth.sample_states(10 + n, [-6, -6, 0], [6, 6, 2], n)
+        ok, rows = pp.check_trajectory_validity_and_generate(traj, md, wp, 1.0, 2.0, 0.1, 0.5, (0.1, 0, 0), (0, 0, 0))
+        assert ok == pp.check_trajectory_validity(traj, md)
+        assert np.array_equal(rows, pt.generate_trajectory(wp, 1.0, 2.0, 0.1, 0.5, (0.1, 0, 0), (0, 0, 0)))
+    traj = O.generate_trajectory(wp, 1.0, 2.0, 0.1)[:100]  # the trajectory's own lookahead
+    ok, _ = pp.check_trajectory_validity_and_generate(traj, md, wp, 1.0, 2.0, 0.1)
+    assert ok == pp.check_trajectory_validity(traj, md)

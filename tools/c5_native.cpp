@@ -11,8 +11,12 @@
 //   c5_online_native  per step: gate pose perturbed -> World update
 //                     (PathPlanner::updateGatePos, src/PathPlanner.cpp:170-173) -> A11
 //                     (checkTrajectoryValidity of the lookahead rows, src/PathPlanner.cpp:267-280)
-//                     -> 12-segment refit from the current state with the moved gate-centre
-//                     waypoint, sampled at dt
+//                     and the 12-segment refit from the current state with the moved
+//                     gate-centre waypoint, sampled at dt -- the product's online step:
+//                     PathPlanner::checkTrajectoryValidityAndGenerate, ONE launch for both
+//   c5_online_native_two_calls  the same step as two calls (checkTrajectoryValidity, then
+//                     poly_traj::generateTrajectory), as the reference sequences them;
+//                     the two loops must agree step for step (flags and rows)
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -142,32 +146,54 @@ int main(int argc, char** argv) {
             if (r >= 20) t_refit.push_back(t1 - t0);
         }
         const size_t refit_rows = traj.rows;
-        Matrix look = in.look;
-        (void)pp.checkTrajectoryValidity(look, in.md);  // first upload of the world
-        std::vector<double> t_online;
-        std::vector<Vec3> wp = in.wp;
+        (void)pp;
+        // the online loop, fused (the product's step) or as two calls; both record each
+        // step's flag and final rows so they can be compared
+        auto online = [&](bool fused, std::vector<double>& t_online, std::vector<char>& valid_of, Matrix& last) {
+            PathPlanner p2(in.gates, in.obstacles, cfg);
+            Matrix look = in.look, tr;
+            (void)p2.checkTrajectoryValidity(look, in.md);  // (warm: first launch of the check)
+            std::vector<Vec3> wp = in.wp;
+            for (const Step& s : in.steps) {
+                const double t0 = now_us();
+                std::vector<double> pose(in.gates.row(s.gate), in.gates.row(s.gate) + 6);
+                pose[0] += s.dx;
+                pose[1] += s.dy;
+                pose[5] += s.dyaw;
+                p2.updateGatePos(s.gate, pose);
+                wp = in.wp;
+                wp[s.wp_index].x = pose[0];
+                wp[s.wp_index].y = pose[1];
+                bool ok;
+                if (fused) {
+                    ok = p2.checkTrajectoryValidityAndGenerate(look, in.md, wp, in.vmax, in.amax, in.dt, 0.0, in.v0, in.a0,
+                                                               tr);
+                } else {
+                    ok = p2.checkTrajectoryValidity(look, in.md);
+                    poly_traj::generateTrajectory(wp, in.vmax, in.amax, in.dt, 0.0, in.v0, in.a0, tr);
+                }
+                for (size_t i = 0; i < look.rows && i < tr.rows; ++i)  // the next step checks the new rows
+                    for (int k = 0; k < 3; ++k) look(i, 3 * k) = tr(i, 3 * k);
+                t_online.push_back(now_us() - t0);
+                valid_of.push_back(ok ? 1 : 0);
+            }
+            last = tr;
+        };
+        std::vector<double> t_fused, t_two;
+        std::vector<char> v_fused, v_two;
+        Matrix last_fused, last_two;
+        online(false, t_two, v_two, last_two);
+        online(true, t_fused, v_fused, last_fused);
         int64_t invalid_steps = 0;
-        for (const Step& s : in.steps) {
-            const double t0 = now_us();
-            std::vector<double> pose(in.gates.row(s.gate), in.gates.row(s.gate) + 6);
-            pose[0] += s.dx;
-            pose[1] += s.dy;
-            pose[5] += s.dyaw;
-            pp.updateGatePos(s.gate, pose);
-            invalid_steps += pp.checkTrajectoryValidity(look, in.md) ? 0 : 1;
-            wp = in.wp;
-            wp[s.wp_index].x = pose[0];
-            wp[s.wp_index].y = pose[1];
-            poly_traj::generateTrajectory(wp, in.vmax, in.amax, in.dt, 0.0, in.v0, in.a0, traj);
-            for (size_t i = 0; i < look.rows && i < traj.rows; ++i)  // the next step checks the new rows
-                for (int k = 0; k < 3; ++k) look(i, 3 * k) = traj(i, 3 * k);
-            t_online.push_back(now_us() - t0);
-        }
+        for (char v : v_fused) invalid_steps += v ? 0 : 1;
+        const bool agree = v_fused == v_two && last_fused.rows == last_two.rows && last_fused.data == last_two.data;
         std::printf("{");
         print_pct("c5_refit_native", t_refit, false);
-        print_pct("c5_online_native", t_online, false);
-        std::printf("\"refit_rows\": %zu, \"online_rows\": %zu, \"online_invalid_steps\": %lld}\n", refit_rows, traj.rows,
-                    (long long)invalid_steps);
+        print_pct("c5_online_native", t_fused, false);
+        print_pct("c5_online_native_two_calls", t_two, false);
+        std::printf("\"refit_rows\": %zu, \"online_rows\": %zu, \"online_invalid_steps\": %lld, "
+                    "\"fused_equals_two_calls\": %s, \"online_step\": \"fused: one launch (A11 check + refit)\"}\n",
+                    refit_rows, last_fused.rows, (long long)invalid_steps, agree ? "true" : "false");
     } catch (const std::exception& e) {
         std::fprintf(stderr, "c5_native: %s\n", e.what());
         return 1;
