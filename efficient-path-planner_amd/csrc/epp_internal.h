@@ -51,6 +51,14 @@ namespace epp {
 epp_status generate_trajectory_into(const double* wp, int32_t n_wp, const double* times, double v_max,
                                     double a_max, double dt, double t0, const double v0[3], const double a0[3],
                                     double* (*alloc)(void*, int64_t), void* ctx, int64_t* n_rows);
+// The planner's pair of epp_sample_uniform + epp_compact_states_ws without the compaction's
+// separate clearing launch: the sampler also zeroes the workspace's status words
+// (clr_bytes: epp_compact_workspace_size), and the compaction that follows on the same
+// stream trusts them to be zero.
+epp_status sample_uniform_and_clear(uint64_t seed, const double lo[3], const double hi[3], int64_t n, double* xyz,
+                                    void* clr, uint64_t clr_bytes, void* stream);
+epp_status compact_states_cleared(const double* xyz, const uint8_t* valid, int64_t n, double* out, int64_t* n_out,
+                                  void* ws, uint64_t ws_bytes, void* stream);
 // The same with the C5 online step's A11 check fused into the launch (chk != NULL): the
 // minDistance flags of chk->n points (host array) against chk->world, written to
 // chk->valid, by extra workgroups of the refit's kernel (k_check_refit).  The check must be

@@ -151,9 +151,10 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     const double lo[3] = {wp.lowerBound.x, wp.lowerBound.y, wp.lowerBound.z};
     const double hi[3] = {wp.upperBound.x, wp.upperBound.y, wp.upperBound.z};
     const double ends[6] = {start.x, start.y, start.z, goal.x, goal.y, goal.z};
-    check(epp_sample_uniform(seed, lo, hi, samples, 0, d_s, st), "sample");
+    // (the sampler also zeroes the compaction's look-back status words)
+    check(sample_uniform_and_clear(seed, lo, hi, samples, d_s, d_cws, cws_bytes, st), "sample");
     check(epp_check_states(w, d_s, samples, canPass ? 1 : 0, d_v, nullptr, nullptr, st), "state check");
-    check(epp_compact_states_ws(d_s, d_v, samples, d_nodes + 6, d_cnt, d_cws, cws_bytes, st), "compact");
+    check(compact_states_cleared(d_s, d_v, samples, d_nodes + 6, d_cnt, d_cws, cws_bytes, st), "compact");
     // start / goal up, the valid-state count down: both queued, one synchronisation
     // (pinned staging: [ends (6 doubles) | count | edge counts (2)])
     // pinned staging: [edge counts = 0 (2) | pad (4) | ends (6) | count | edge counts (2)]

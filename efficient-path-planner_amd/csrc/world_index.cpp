@@ -774,3 +774,22 @@ extern "C" epp_status epp_dbg_build_blob(const epp_obb* obbs, int32_t n, double 
     out[5] = hw.view.slab_n;
     return EPP_OK;
 }
+
+// Debug entry (not part of include/epp.h): the class-grid layout of a world's index, host
+// build only.  out: off_aos, off_lists, off_ids, off_cls8, off_bitmap, blob_bytes, n_lists,
+// class cells (bm_words), bnx, bny, bnz, staged bytes of k_states_v5.
+extern "C" epp_status epp_dbg_class_layout(const epp_obb* obbs, int32_t n, double r_gate, double r_obst,
+                                           int64_t out[12]) {
+    if (!out || n < 0 || (n > 0 && !obbs)) return EPP_ERR_INVALID_ARGUMENT;
+    epp::HostWorld hw;
+    hw.r_gate = r_gate;
+    hw.r_obst = r_obst;
+    if (!epp::build_blob(hw, obbs, n)) return EPP_ERR_UNSUPPORTED;
+    const epp::WorldView& v = hw.view;
+    const int64_t vals[12] = {v.off_aos, v.off_lists, v.off_ids, v.off_cls8, v.off_bitmap, v.blob_bytes, v.n_lists,
+                              v.bm_words, v.bnx, v.bny, v.bnz,
+                              (int64_t)((v.off_cls8 ? ((v.off_cls8 + v.bm_words + 1 + 15u) & ~15u) : v.blob_bytes) -
+                                        v.off_aos)};
+    for (int k = 0; k < 12; ++k) out[k] = vals[k];
+    return EPP_OK;
+}
