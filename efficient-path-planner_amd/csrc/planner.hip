@@ -521,14 +521,11 @@ __global__ __launch_bounds__(256) void k_knn_grid(const KnnGrid* __restrict__ gp
 // Lanes per query: a block holds ~64..160 queries at ~2 nodes per cell; with fewer
 // queries than threads, 2 or 4 adjacent lanes share one query (cube rows split between
 // them; the histogram and the list are shared through LDS atomics), so blocks take about
-// the same time whatever their query count -- up to kTileSplitQ queries.  A crowded block
-// (more: one lane per query, the launch's slowest blocks) is split into two work units by
-// its cell layers along z (units b and nblocks + b, each with its own halo copy), so
-// neither half runs at one lane per query.  Work units come from a queue: the first
-// nblocks units are the blocks (their first halves), the next nblocks the second halves,
-// which a unit of an uncrowded block skips after one read of its 16 inner rows -- the
-// workgroups left over by the first round (the persistent grid outnumbers the blocks)
-// sweep them, so the crowded halves start early.
+// the same time whatever their query count.  Blocks come from a queue (costs differ).
+// (Splitting blocks of more than 128 queries into two z-layer work units was tried in
+// round 4: at ~1.5 nodes per cell the C4 tables have as many blocks as resident
+// workgroups, so a second half only starts once a workgroup is free -- it lengthened the
+// launch, 99 -> 110 us in the isolated trace.)
 #ifdef EPP_KNN_DIAG
 constexpr int kKnnTlBlocks = 65536;  // timeline records
 #endif
@@ -540,7 +537,6 @@ constexpr int kTileThreads = 256;
 constexpr int kTileL = 32;              // per-query list length
 constexpr int kTileNB = 16;             // histogram bins (16-bit counters, two per word)
 constexpr double kTileDelta = 1e-3;     // float error allowance, in h^2
-constexpr int kTileSplitQ = kTileThreads / 2;  // queries above which a block is split in two units
 #ifndef EPP_KNN_PASS1R2  // (diagnostics A/B builds may override; exact either way)
 #define EPP_KNN_PASS1R2 4.5
 #endif
@@ -804,8 +800,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
     __shared__ int wsum[kTileThreads / 64];
     __shared__ uint8_t s_nown[kTileThreads];  // list entries per lane (saturated)
     __shared__ int8_t s_cut[kTileThreads];    // histogram cut per query slot
-    __shared__ int s_nq, s_b, s_inner;
-    __shared__ int winner[kTileThreads / 64];
+    __shared__ int s_nq, s_b;
     const KnnGrid g = *gp;
     const int nbx = (g.dims[0] + kTileB - 1) / kTileB, nby = (g.dims[1] + kTileB - 1) / kTileB,
               nbz = (g.dims[2] + kTileB - 1) / kTileB;
@@ -822,28 +817,9 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
     for (;;) {
         if (threadIdx.x == 0) s_b = atomicAdd(&gp->next, 1);
         __syncthreads();
-        const int b = s_b;  // block-uniform: work unit b
-        if (b >= 2 * nblocks) break;
-        const bool second = b >= nblocks;  // a crowded block's second half
-        const int blk = second ? b - nblocks : b;
-        const int bx = blk % nbx, by = (blk / nbx) % nby, bz = blk / (nbx * nby);
-        if (second) {
-            // the block's query count from its 16 inner rows (each one contiguous range of
-            // the cell-sorted nodes): not crowded -> nothing to do
-            if (threadIdx.x < 64) {
-                int c = 0;
-                const int iy = threadIdx.x & 3, iz = threadIdx.x >> 2;
-                const int y = by * kTileB + iy, z = bz * kTileB + iz, x0 = bx * kTileB;
-                if (threadIdx.x < 16 && y < g.dims[1] && z < g.dims[2]) {
-                    const int a = (z * g.dims[1] + y) * g.dims[0];
-                    c = start[a + min(x0 + kTileB, g.dims[0])] - start[a + x0];
-                }
-                for (int o = 8; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-                if (threadIdx.x == 0) s_inner = c;
-            }
-            __syncthreads();
-            if (s_inner <= kTileSplitQ) continue;  // (block-uniform)
-        }
+        const int b = s_b;  // block-uniform
+        if (b >= nblocks) break;
+        const int bx = b % nbx, by = (b / nbx) % nby, bz = b / (nbx * nby);
         const int ox = bx * kTileB - kTileH, oy = by * kTileB - kTileH, oz = bz * kTileB - kTileH;
         const double cen[3] = {g.lo[0] + (ox + 0.5 * kTileE) * g.h, g.lo[1] + (oy + 0.5 * kTileE) * g.h,
                                g.lo[2] + (oz + 0.5 * kTileE) * g.h};
@@ -860,43 +836,32 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
     do {           \
     } while (0)
 #endif
-        // 1. halo cell sizes -> exclusive scan (thread t owns halo cells kPer*t ..); the
-        // block's own (inner) node count beside it
-        int cnt[kPer], cell0[kPer], tot = 0, tin = 0;
+        // 1. halo cell sizes -> exclusive scan (thread t owns halo cells kPer*t ..)
+        int cnt[kPer], cell0[kPer], tot = 0;
 #pragma unroll
         for (int u = 0; u < kPer; ++u) {
             const int t = kPer * threadIdx.x + u;
-            const int hx = t % kTileE, hy = (t / kTileE) % kTileE, hz = t / (kTileE * kTileE);
-            const int x = ox + hx, y = oy + hy, z = oz + hz;
+            const int x = ox + t % kTileE, y = oy + (t / kTileE) % kTileE, z = oz + t / (kTileE * kTileE);
             const bool in = x >= 0 && x < g.dims[0] && y >= 0 && y < g.dims[1] && z >= 0 && z < g.dims[2];
             const int cell = in ? (z * g.dims[1] + y) * g.dims[0] + x : 0;
             const int s0 = start[cell], s1 = start[cell + 1];
             cnt[u] = in ? s1 - s0 : 0;
             cell0[u] = s0;
             tot += cnt[u];
-            const bool inner = hx >= kTileH && hx < kTileH + kTileB && hy >= kTileH && hy < kTileH + kTileB &&
-                               hz >= kTileH && hz < kTileH + kTileB;
-            tin += inner ? cnt[u] : 0;
         }
         int incl = tot;
         for (int o = 1; o < 64; o <<= 1) {
             const int v = __shfl_up(incl, o, 64);
             if (lane >= o) incl += v;
         }
-        for (int o = 32; o > 0; o >>= 1) tin += __shfl_xor(tin, o, 64);
         if (lane == 63) wsum[wv] = incl;
-        if (lane == 0) winner[wv] = tin;
         __syncthreads();
-        int base = 0, total = 0, nq_block = 0;
+        int base = 0, total = 0;
 #pragma unroll
         for (int w = 0; w < kTileThreads / 64; ++w) {
             base += w < wv ? wsum[w] : 0;
             total += wsum[w];
-            nq_block += winner[w];
         }
-        // this unit's cell layers along z: all of them, or a crowded block's half
-        const bool split = nq_block > kTileSplitQ;  // (block-uniform; units b and nblocks + b agree)
-        const int zlo = split && second ? kTileB / 2 : 0, zhi = split && !second ? kTileB / 2 : kTileB;
         base += incl - tot;
         {
             int acc = base;
@@ -920,7 +885,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                 const int t = kPer * threadIdx.x + u;
                 const int hx = t % kTileE, hy = (t / kTileE) % kTileE, hz = t / (kTileE * kTileE);
                 const bool inner = hx >= kTileH && hx < kTileH + kTileB && hy >= kTileH && hy < kTileH + kTileB &&
-                                   hz >= kTileH + zlo && hz < kTileH + zhi;  // (this unit's queries)
+                                   hz >= kTileH && hz < kTileH + kTileB;
                 const int q0 = (inner && cnt[u]) ? atomicAdd(&s_nq, cnt[u]) : 0;
                 for (int q = 0; q < cnt[u]; ++q) {
                     const int sg = cell0[u] + q;
@@ -1109,11 +1074,11 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
             }
             EPP_KTL(6);
         } else {
-            // crowded halo: the unit's queries retry from global memory
+            // crowded halo: the block's queries retry from global memory
             for (int t2 = threadIdx.x; t2 < kTileB * kTileB * kTileB; t2 += kTileThreads) {
-                const int lz = t2 / (kTileB * kTileB);
-                const int x = bx * kTileB + t2 % kTileB, y = by * kTileB + (t2 / kTileB) % kTileB, z = bz * kTileB + lz;
-                if (x >= g.dims[0] || y >= g.dims[1] || z >= g.dims[2] || lz < zlo || lz >= zhi) continue;
+                const int x = bx * kTileB + t2 % kTileB, y = by * kTileB + (t2 / kTileB) % kTileB,
+                          z = bz * kTileB + t2 / (kTileB * kTileB);
+                if (x >= g.dims[0] || y >= g.dims[1] || z >= g.dims[2]) continue;
                 const int cell = (z * g.dims[1] + y) * g.dims[0] + x;
                 const int e = start[cell + 1];
                 for (int t = start[cell]; t < e; ++t) {

@@ -50,6 +50,20 @@ def report(recs):
     tot = (t[:, 7] - t[:, 0]) * 10 / 1000.0
     print(f"block   p10 {np.percentile(tot, 10):7.2f} p50 {np.percentile(tot, 50):7.2f} p90 {np.percentile(tot, 90):7.2f} "
           f"max {tot.max():7.2f} us")
+    # the slowest blocks: what they hold and where they are (grid from the workspace's KnnGrid)
+    gw = d_ws.download(np.uint8, 64)
+    dims = np.frombuffer(gw[40:52].tobytes(), np.int32)
+    nbx, nby = (dims[0] + 3) // 4, (dims[1] + 3) // 4
+    r0 = recs[0]
+    tb = (r0[:, 7] - r0[:, 0]) * 10 / 1000.0
+    b_ = idxs[0]  # block numbers
+    print(f"grid dims {dims.tolist()}, blocks {nbx}x{nby}x{(dims[2] + 3) // 4}; corr(time, queries) "
+          f"{np.corrcoef(tb, r0[:, 8])[0, 1]:.2f}, corr(time, halo) {np.corrcoef(tb, r0[:, 9])[0, 1]:.2f}")
+    for i in np.argsort(tb)[::-1][:10]:
+        bx, by, bz = b_[i] % nbx, (b_[i] // nbx) % nby, b_[i] // (nbx * nby)
+        ph = [(r0[i, j + 1] - r0[i, j]) * 10 / 1000.0 if r0[i, j] and r0[i, j + 1] else -1 for j in range(7)]
+        print(f"  block {b_[i]} ({bx},{by},{bz}) {tb[i]:.1f} us  queries {r0[i, 8]} halo {r0[i, 9]}  phases "
+              + " ".join(f"{x:.1f}" for x in ph))
     for r in recs[:3]:
         st = (r[:, 0] - r[:, 0].min()) * 10 / 1000.0
         en = (r[:, 7] - r[:, 0].min()) * 10 / 1000.0
@@ -59,13 +73,15 @@ def report(recs):
 modes = sys.argv[1:] or ["1"]  # EPP_KNN_TILE values (5, 6: no-insert ablations, diagnostics only)
 for m in modes:
     os.environ["EPP_KNN_TILE"] = m
-    recs = []
+    recs, idxs = [], []
     for r in range(12):
         capi.check(L.epp_knn_grid_ws(d_n.ptr, n, k, 0.0, d_k.ptr, d_ws.ptr, ws, None))
         capi.sync()
         if r >= 2:
             tl = np.zeros((1024, 16), np.uint64)
             capi.check(L.epp_dbg_knn_tl(tl.ctypes.data, 1024))
-            recs.append(tl[tl[:, 7] != 0].astype(np.int64))
+            keep = tl[:, 7] != 0
+            recs.append(tl[keep].astype(np.int64))
+            idxs.append(np.nonzero(keep)[0])
     print(f"== EPP_KNN_TILE={m}")
     report(recs)

@@ -42,8 +42,13 @@ f = lambda r: w.check_states_dev(d.ptr + (r % NB) * N * 24, N, 0, dv.ptr, stream
 for r in range(50):
     f(r)
 us = float(np.median([timed_kernel_ms(capi, st, f, 200) for _ in range(3)])) * 1e3
+# the flags of the last launch's batch (199 % 16): a digest to compare builds (variants must agree)
+import hashlib  # noqa: E402
+capi.check(L.epp_stream_sync(st))
+flags = dv.download(np.uint8, N)
+digest = hashlib.sha1(flags.tobytes()).hexdigest()[:12]
 print(os.path.basename(lib or "libepp.so"), " ".join(a for a in args if "=" in a),
-      f"c2 {us:.3f} us  {25 * N / us / 1e6:.2f} TB/s", flush=True)
+      f"c2 {us:.3f} us  {25 * N / us / 1e6:.2f} TB/s  valid {int(flags.sum())} sha1 {digest}", flush=True)
 if stream_floor:
     so = os.path.join(ROOT, "scripts", "dbg", "libdiag.so")
     diag = C.CDLL(so)
