@@ -508,7 +508,8 @@ __global__ __launch_bounds__(256) void k_knn_grid(const KnnGrid* __restrict__ gp
 // Selection.  The sorted top-K insert costs ~K*12 VALU per candidate, and a wave pays
 // it whenever any of its lanes inserts -- nearly always.  So the cube is scanned twice
 // on float coordinates (relative to the block centre, one 16-byte LDS record per
-// candidate): pass 1 histograms the squared distances into kTileNB quarter-octave bins;
+// candidate): pass 1 histograms the squared distances into kTileNB quarter-octave bins
+// (per-lane register counters);
 // the bin where the running count reaches K gives a bound Dcut; pass 2 lists the
 // candidates with float distance below Dcut + 2*delta (<= kTileL per query).  Only the
 // listed candidates get an exact (double, from global memory) distance and the insert.
@@ -795,7 +796,6 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
     __shared__ float4 cand[kTileCap];                      // x, y, z (block-centre relative), sorted position
     __shared__ uint16_t qh[kTileCap];                      // the block's queries (LDS positions)
     __shared__ int cst[kTileCells + 1];                    // halo cell -> LDS offset
-    __shared__ uint32_t hist[kTileNB / 2][kTileThreads];  // [bin pair][query slot]
     __shared__ uint16_t lst[kTileL][kTileThreads];         // [entry][lane]: each lane's own list
     __shared__ int wsum[kTileThreads / 64];
     __shared__ uint8_t s_nown[kTileThreads];  // list entries per lane (saturated)
@@ -930,26 +930,40 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                 // of a skipped cell has exact d > kPass1R2 h^2, float d > that - delta), so
                 // its cut stands when it ends there -- nearly always; else the whole cube.
                 int cut = -1;
-                for (int full = 0; full < 2; ++full) {  // query-uniform (the slot's lanes read one histogram)
-                    if (sub == 0) {
+                for (int full = 0; full < 2; ++full) {  // query-uniform (the slot's lanes sum one histogram)
+                    // each lane counts its candidates in registers (16-bit counters, two per
+                    // word: no LDS atomics -- pass 1 was bound by the LDS traffic of its
+                    // read + atomic per candidate), then the query's lpq adjacent lanes add
+                    // theirs with DPP quad permutes
+                    uint32_t hr[kTileNB / 2];
 #pragma unroll
-                        for (int w = 0; w < kTileNB / 2; ++w) hist[w][slot] = 0u;
-                    }
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    for (int w = 0; w < kTileNB / 2; ++w) hr[w] = 0u;
                     auto bin = [&](int, float d, int j, bool valid) {
                         const int kb = max((int)(__float_as_uint(d * inv_t0) >> 21) - (127 << 2), 0);
-                        if (valid && j != sself && kb < kTileNB) atomicAdd(&hist[kb >> 1][slot], 1u << ((kb & 1) << 4));
+                        const uint32_t inc = (valid && j != sself && kb < kTileNB) ? 1u << ((kb & 1) << 4) : 0u;
+                        const int wsel = kb >> 1;
+#pragma unroll
+                        for (int w = 0; w < kTileNB / 2; ++w) hr[w] += wsel == w ? inc : 0u;
                     };
                     if (live) {
                         if (full) tile_rows(cst, cand, h0, sub, lpq, pf, bin);
                         else tile_rows_near(cst, cand, h0, sub, lpq, pf, fr, g.h, kPass1R2 * g.h * g.h, bin);
                     }
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (lpq >= 2) {  // (block-uniform) lanes sub ^ 1: quad_perm [1,0,3,2]
+#pragma unroll
+                        for (int w = 0; w < kTileNB / 2; ++w)
+                            hr[w] += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hr[w], 0xB1, 0xf, 0xf, false);
+                    }
+                    if (lpq >= 4) {  // lanes sub ^ 2: quad_perm [2,3,0,1]
+#pragma unroll
+                        for (int w = 0; w < kTileNB / 2; ++w)
+                            hr[w] += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hr[w], 0x4E, 0xf, 0xf, false);
+                    }
                     int run = 0;
                     cut = -1;
 #pragma unroll
                     for (int w = 0; w < kTileNB / 2; ++w) {
-                        const uint32_t hv = hist[w][slot];
+                        const uint32_t hv = hr[w];
                         run += hv & 0xffff;
                         if (run >= K && cut < 0) cut = 2 * w;
                         run += hv >> 16;
