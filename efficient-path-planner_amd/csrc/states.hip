@@ -365,10 +365,7 @@ __device__ unsigned long long g_states_tl[kTlWaves][6];
 // flag store of SPL bytes.  More states per lane = fewer waves, i.e. fewer executions
 // of the per-wave fixed costs (setup, staging, the exact path).
 // SC: staging chunks (16 B) per lane: enough for the staged bytes (launcher's choice).
-// TWO (diagnostics A/B builds, -DEPP_V5_TWOPHASE; single pass only): the class table's
-// chunks are loaded first and stored behind their own barrier, the records' first chunk
-// (loaded after the group's states) behind a second one just before the exact path.
-template <bool MINDIST, bool COMPACT, int BLOCK, bool PREFETCH, int SPL, bool C8, int SC, bool TWO = false>
+template <bool MINDIST, bool COMPACT, int BLOCK, bool PREFETCH, int SPL, bool C8, int SC>
 __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict__ wv,
                                                      const double* xyz, int64_t groups, int64_t n,
                                                      int can_pass, double md, uint8_t* __restrict__ valid,
@@ -415,21 +412,6 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
 #else
     const u32x4* ssrc = reinterpret_cast<const u32x4*>(wv->blob + wv->off_aos);
 #endif
-    static_assert(!TWO || !PREFETCH, "two-phase staging: single pass");
-    if (TWO) {  // chunks SC-1 .. 1 (the table), the group, then chunk 0 (records)
-#pragma unroll
-        for (int i = kStageChunks - 1; i >= 1; --i) {
-            const uint32_t o = (uint32_t)(i * BLOCK) + threadIdx.x;
-            stg[i] = ssrc[o < n16 ? o : n16 - 1u];
-        }
-        load(g, va);
-        stg[0] = ssrc[threadIdx.x < n16 ? threadIdx.x : n16 - 1u];
-#pragma unroll
-        for (int i = kStageChunks - 1; i >= 1; --i) {
-            const uint32_t o = (uint32_t)(i * BLOCK) + threadIdx.x;
-            *reinterpret_cast<u32x4*>(lds_blob + 16u * (o < n16 ? o : n16)) = stg[i];
-        }
-    } else {
 #pragma unroll
     for (int i = 0; i < kStageChunks; ++i) {
         const uint32_t o = (uint32_t)(i * BLOCK) + threadIdx.x;
@@ -441,7 +423,6 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
         const uint32_t o = (uint32_t)(i * BLOCK) + threadIdx.x;
         // (the launch allocates 16 spare bytes after the copy: the dummy slot)
         *reinterpret_cast<u32x4*>(lds_blob + 16u * (o < n16 ? o : n16)) = stg[i];
-    }
     }
     const uint32_t lists_off = wv->off_lists - wv->off_aos, ids_off = wv->off_ids - wv->off_aos;
     // the class table: bytes (C8, staged right after the lists) or u16
@@ -479,10 +460,6 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
             total += (uint32_t)__popcll(b[k]);
         }
         EPP_STL(2);
-        if (TWO) {  // the records' first chunk, then every wave's stores before the exact path
-            *reinterpret_cast<u32x4*>(lds_blob + 16u * (threadIdx.x < n16 ? threadIdx.x : n16)) = stg[0];
-            __syncthreads();
-        }
         // the needy states' list headers, read now (one LDS round trip for all four,
         // overlapping the ballot arithmetic) and queued with the state
         uint32_t hd[SPL];
@@ -495,9 +472,6 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
         if (false) {
 #else
         if (total > 0) {  // wave-uniform
-#endif
-#ifdef EPP_V5_PRIO  // (diagnostics A/B builds) a wave in its exact path issues first
-            __builtin_amdgcn_s_setprio(2);
 #endif
             uint32_t pos[SPL];
 #pragma unroll
@@ -577,9 +551,6 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
             }
         }
         EPP_STL(3);
-#ifdef EPP_V5_PRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
         const uint32_t fl = live ? (~hits & ((1u << SPL) - 1u)) : 0u;  // bit k: state SPL gg + k valid
         if (live) {
             if (SPL == 4) {
@@ -721,32 +692,6 @@ epp_status launch_states(const WorldView& w, const WorldView* dw, const double* 
         const uint32_t sb = v5_staged(w);
         const V5Shape sh = v5_shape(n, sb);
         const uint32_t dyn = sb + 16u;  // the staged world + the dummy slot of the copy
-#if defined(EPP_V5_SPL8) || defined(EPP_V5_TWOPHASE)
-        // (diagnostics A/B builds) the headline shape only: one pass, byte classes, no compaction
-        {
-            const int64_t cus = cu_count();
-#ifdef EPP_V5_SPL8
-            // eight states per lane, one 512-thread workgroup (one staged copy) per CU
-            constexpr int kB = 512, kSpl = 8;
-            const bool two = false;
-#else
-            constexpr int kB = 512, kSpl = 4;
-            // the table's chunks must not share chunk 0 with the records
-            const bool two = w.off_cls8 && (w.off_cls8 - w.off_aos) >= 16u * kB;
-#endif
-            const int64_t gN = n / kSpl;
-            const bool one_pass = gN <= (int64_t)(2 * cus) * kB / (kSpl / 4) && w.off_cls8 && !compact_idx &&
-                                  sb <= (uint32_t)kStageBudget / 2;
-            if (one_pass && (kSpl == 8 || two)) {
-                constexpr int kSC = (int)(kStageBudget / 2 / (kB * 16));
-                const int grid = (int)std::max<int64_t>(1, (gN + kB - 1) / kB);
-                allow_lds(k_states_v5<MINDIST, false, kB, false, kSpl, true, kSC, kSpl == 4>, queue5_bytes<kB>());
-                hipLaunchKernelGGL((k_states_v5<MINDIST, false, kB, false, kSpl, true, kSC, kSpl == 4>), dim3(grid),
-                                   dim3(kB), dyn, st, dw, xyz, gN, n, can_pass, md, valid, compact_idx, nv, sb);
-                return launch_error(what);
-            }
-        }
-#endif
 #define EPP_LAUNCH_V5S(C, B, P, C8, SC)                                                                              \
     do {                                                                                                             \
         allow_lds(k_states_v5<MINDIST, C, B, P, 4, C8, SC>, queue5_bytes<B>());                                      \
