@@ -20,4 +20,8 @@ for r in list(csv.DictReader(open("gpurun_out/prof_plan/run_kernel_stats.csv")))
     n = r["Name"]; n = n[:n.find("(")] if "(" in n else n
     print(f"{n[-40:]:40s} {r['Calls']:>4} avg {float(r['AverageNs'])/1e3:8.2f} min {float(r['MinNs'])/1e3:8.2f} max {float(r['MaxNs'])/1e3:8.2f} us")
 PY
+if [ -n "${MOTIONS_PMC:-}" ]; then
+  bash scripts/gpu_pmc_motions.sh; rc=$?; stop_on_fault $rc pmc_motions
+  python3 scripts/pmc_summary.py gpurun_out/mpmc3 k_motions_v5
+fi
 echo done

@@ -6,8 +6,11 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS"
 P2="SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES SQ_INSTS_BRANCH SQ_INSTS_SMEM"
+# the VALU mix: FP64 arithmetic vs integer / conversion work (per-SE sums; the rest of
+# SQ_INSTS_VALU is compares, selects, moves, bit and lane operations)
+P3="SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT"
 i=0
-for P in "$P1" "$P2"; do
+for P in "$P1" "$P2" "$P3"; do
   i=$((i+1))
   rm -rf gpurun_out/mpmc$i
   timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d gpurun_out/mpmc$i -o run -- python3 scripts/motions_run.py > gpurun_out/mpmc$i.log 2>&1; rc=$?
