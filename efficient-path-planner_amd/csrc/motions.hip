@@ -558,11 +558,25 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
                 if (has) {
                     const double* rec = recs + (size_t)(q >> 6) * kRecDoubles;
                     bool hit;
+#ifdef EPP_MOTIONS_PF_FLUSH
+                    // the exact AABB prefilter here, on the owner's box (closed, as the rtree
+                    // query; MODE 1 widened by a hair), instead of in the candidate rounds
+                    bool keep = true;
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        const double l = (pe[k] < ps[k]) ? pe[k] : ps[k], h = (ps[k] < pe[k]) ? pe[k] : ps[k];
+                        const double bl = MODE == 1 ? l - (1e-9 + 1e-12 * fabs(l)) : l;
+                        const double bh = MODE == 1 ? h + (1e-9 + 1e-12 * fabs(h)) : h;
+                        keep = keep & !((rec[F_HIX + k] < bl) | (bh < rec[F_LOX + k]));
+                    }
+#else
+                    constexpr bool keep = true;  // (tested before queueing)
+#endif
                     if (MODE == 0) {  // (the AABB overlap was tested before queueing)
                         const uint32_t m = (uint32_t)__double_as_longlong(rec[R_META]);
-                        hit = rec_ray_hit(rec, ps, pe, (m & META_GATE) ? rg : ro);
+                        hit = keep && rec_ray_hit(rec, ps, pe, (m & META_GATE) ? rg : ro);
                     } else {
-                        hit = d32_pair_hit(rec, ps, pe, rg, ro, cp);
+                        hit = keep && d32_pair_hit(rec, ps, pe, rg, ro, cp);
                     }
                     if (hit) flags[owner] = 0;
                 }
@@ -631,6 +645,17 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
                     }
                     has = has || take;
                 }
+#ifdef EPP_MOTIONS_PF_FLUSH
+                const unsigned long long hb = __builtin_amdgcn_ballot_w64(has);
+                if (!hb) break;
+                if (has) {
+                    const uint16_t* tid = wsel < (uint32_t)W ? ida : idb;
+                    queue[qn + lanes_below(hb)] = (uint32_t)tid[32 * (wsel % (uint32_t)W) + bit] << 6 | (uint32_t)lane;
+                }
+                qn += (uint32_t)__popcll(hb);
+                if (qn > (uint32_t)(kQueueV5 - 64)) flush();
+                continue;
+#endif
                 if (!__builtin_amdgcn_ballot_w64(has)) break;
                 uint32_t id = 0;
                 bool keep = false;

@@ -689,7 +689,11 @@ epp_status launch_states(const WorldView& w, const WorldView* dw, const double* 
     const StatesKernel want = forced_kernel();
     const bool x16 = (reinterpret_cast<uintptr_t>(xyz) & 15) == 0;
     if (want == StatesKernel::V5 && v5_fits(w) && x16 && (reinterpret_cast<uintptr_t>(valid) & 3) == 0) {
+#ifdef EPP_V5_STAGECAP  // (diagnostics timing probes only: WRONG answers) stage at most this many bytes
+        const uint32_t sb = std::min<uint32_t>(v5_staged(w), EPP_V5_STAGECAP);
+#else
         const uint32_t sb = v5_staged(w);
+#endif
         const V5Shape sh = v5_shape(n, sb);
         const uint32_t dyn = sb + 16u;  // the staged world + the dummy slot of the copy
 #define EPP_LAUNCH_V5S(C, B, P, C8, SC)                                                                              \
@@ -698,11 +702,15 @@ epp_status launch_states(const WorldView& w, const WorldView* dw, const double* 
         hipLaunchKernelGGL((k_states_v5<MINDIST, C, B, P, 4, C8, SC>), dim3(sh.grid), dim3(B), dyn, st, dw, xyz, sh.gN, \
                            n, can_pass, md, valid, compact_idx, nv, sb);                                             \
     } while (0)
-        // staging chunks per lane: half the budget's when the staged bytes fit in it
+        // staging chunks per lane: as many as the staged bytes need (1, 2 or 3), else half
+        // the budget's or the whole budget's
         const bool half_stage = sb <= (uint32_t)kStageBudget / 2;
 #define EPP_LAUNCH_V5C(C, B, P, C8)                                                              \
     do {                                                                                         \
-        if (half_stage) EPP_LAUNCH_V5S(C, B, P, C8, (int)(kStageBudget / 2 / (B * 16)));         \
+        if (sb <= (uint32_t)B * 16u) EPP_LAUNCH_V5S(C, B, P, C8, 1);                              \
+        else if (sb <= (uint32_t)B * 32u) EPP_LAUNCH_V5S(C, B, P, C8, 2);                         \
+        else if (sb <= (uint32_t)B * 48u) EPP_LAUNCH_V5S(C, B, P, C8, 3);                         \
+        else if (half_stage) EPP_LAUNCH_V5S(C, B, P, C8, (int)(kStageBudget / 2 / (B * 16)));    \
         else EPP_LAUNCH_V5S(C, B, P, C8, (int)(kStageBudget / (B * 16)));                        \
     } while (0)
 #define EPP_LAUNCH_V5(C, B, P)                                 \

@@ -38,4 +38,9 @@ for mode in (0, 1):
         f(r)
     ms = [timed_kernel_ms(capi, st.value, f, 20) for _ in range(3)]
     out[mode] = float(np.median(ms)) * 1e3
-print(os.path.basename(lib or "libepp.so"), " ".join(args), f"mode0 {out[0]:.2f} us  mode1 {out[1]:.2f} us", flush=True)
+    capi.check(L.epp_stream_sync(st.value))
+    fl = dv.download(np.uint8, N)  # (a digest of the flags: builds must agree)
+    import hashlib
+    out[f"h{mode}"] = hashlib.sha1(fl.tobytes()).hexdigest()[:10]
+print(os.path.basename(lib or "libepp.so"), " ".join(args), f"mode0 {out[0]:.2f} us  mode1 {out[1]:.2f} us  "
+      f"sha1 {out['h0']} {out['h1']}", flush=True)
