@@ -134,7 +134,10 @@ struct WorldView {
     uint32_t n_lists;
     uint32_t off_bitmap;      // cls[] (u16 per fine cell)
     uint32_t bm_words;        // index of the zero sentinel class
-    uint32_t off_cls8;        // the same classes as bytes (0: more than 255 lists, none)
+    uint32_t off_cls8;        // the same classes as bytes (0: more than 255 lists, none) --
+                              // sparse: u64 [occupancy | rank] per 32 cells, then the
+                              // nonzero cells' bytes (world_index.cpp; dense with -DEPP_V5_DENSE_CLS)
+    uint32_t cls8_bytes;      // bytes of that structure
     int32_t bnx, bny, bnz;    // cells per axis
     float bofx, bofy, bofz;   // offset: cell coordinate f = fmaf((float)p, bi, bof)
     float bix, biy, biz;      // 1 / cell size (float)

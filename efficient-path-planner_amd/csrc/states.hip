@@ -427,6 +427,7 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
     const uint32_t lists_off = wv->off_lists - wv->off_aos, ids_off = wv->off_ids - wv->off_aos;
     // the class table: bytes (C8, staged right after the lists) or u16
     const unsigned char* cls_base = lds_blob + ((C8 ? wv->off_cls8 : wv->off_bitmap) - wv->off_aos);
+    [[maybe_unused]] const unsigned char* cls_nz = cls_base + ((wv->bm_words + 1u + 31u) >> 5) * 8u;  // (sparse classes)
     const uint32_t* hdrs = reinterpret_cast<const uint32_t*>(lds_blob + lists_off);
     const uint16_t* ids_all = reinterpret_cast<const uint16_t*>(lds_blob + ids_off);
     const double* recs = reinterpret_cast<const double*>(lds_blob);
@@ -439,6 +440,14 @@ __global__ __launch_bounds__(BLOCK) void k_states_v5(const WorldView* __restrict
         const uint32_t cx = cell_axis5(px, ox, ix, nx - 1), cy = cell_axis5(py, oy, iy, ny - 1),
                        cz = cell_axis5(pz, oz, iz, nz - 1);
         const uint32_t idx = __umul24(__umul24(cz, ny) + cy, nx) + cx;
+#ifndef EPP_V5_DENSE_CLS
+        if (C8) {  // sparse byte classes: the occupancy word, then (occupied cells) the class byte
+            const uint64_t wd = reinterpret_cast<const uint64_t*>(cls_base)[idx >> 5];
+            const uint32_t m = (uint32_t)wd, sh = idx & 31u;
+            const uint32_t rank = (uint32_t)(wd >> 32) + (uint32_t)__popc(m & ((1u << sh) - 1u));
+            return ((m >> sh) & 1u) ? (uint32_t)cls_nz[rank] : 0u;
+        }
+#endif
         return C8 ? (uint32_t)cls_base[idx] : (uint32_t)reinterpret_cast<const uint16_t*>(cls_base)[idx];
     };
 #ifdef EPP_STATES_TL
@@ -632,8 +641,7 @@ StatesKernel forced_kernel() {
 // k_states_v5 stages records, lists and the class table (bytes when there are, else u16):
 // [off_aos, end of the byte table) or [off_aos, blob_bytes)
 uint32_t v5_staged(const WorldView& w) {
-    const uint32_t cells = w.bm_words + 1;
-    return (w.off_cls8 ? ((w.off_cls8 + cells + 15u) & ~15u) : w.blob_bytes) - w.off_aos;
+    return (w.off_cls8 ? ((w.off_cls8 + w.cls8_bytes + 15u) & ~15u) : w.blob_bytes) - w.off_aos;
 }
 bool v5_fits(const WorldView& w) {
     const uint32_t sb = v5_staged(w);

@@ -373,10 +373,34 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
     const size_t off_aos = align16(off_soa + soa.size() * sizeof(double));
     const size_t off_lists = align16(off_aos + aos.size() * sizeof(double));
     const size_t off_ids = off_lists + hdr.size() * 4;
-    // byte classes (k_states_v5 stages them instead of the u16 table) when the lists fit
+    // byte classes (k_states_v5 stages them instead of the u16 table) when the lists fit.
+    // Sparse form (the default; -DEPP_V5_DENSE_CLS: one byte per cell): per 32 cells one u64
+    // [occupancy bits | nonzero cells before this word], then the class bytes of the nonzero
+    // cells in cell order -- 0.25 B per cell plus ~1 B per occupied cell (C2: 7 KB instead of
+    // 18.5 KB staged by every workgroup).
     const bool c8 = hdr.size() <= 256;
     const size_t off_c8 = align16(off_ids + flat.size() * 2);
-    const size_t off_bm = c8 ? align16(off_c8 + cls.size()) : off_c8;
+    std::vector<uint64_t> cwords;
+    std::vector<uint8_t> cnz;
+#ifndef EPP_V5_DENSE_CLS
+    if (c8) {
+        cwords.assign((cls.size() + 31) / 32, 0ull);
+        for (size_t w = 0; w < cwords.size(); ++w) {
+            uint32_t m = 0;
+            const uint64_t before = cnz.size();
+            for (size_t j = 0; j < 32 && 32 * w + j < cls.size(); ++j)
+                if (cls[32 * w + j]) {
+                    m |= 1u << j;
+                    cnz.push_back((uint8_t)cls[32 * w + j]);
+                }
+            cwords[w] = (uint64_t)m | (before << 32);
+        }
+    }
+    const size_t c8_bytes = c8 ? cwords.size() * 8 + cnz.size() : 0;
+#else
+    const size_t c8_bytes = c8 ? cls.size() : 0;
+#endif
+    const size_t off_bm = c8 ? align16(off_c8 + c8_bytes) : off_c8;
     // ---- motion tile filter (k_motions_v5) ------------------------------------------
     // The smallest row width W (words of OBB bits), then the fewest tiles per axis T,
     // for which every tile holds <= 32 W OBBs; S local slabs per tile and axis as many as
@@ -501,9 +525,17 @@ bool build_blob(HostWorld& hw, const epp_obb* obbs, int n) {
     std::memcpy(b + off_bm, cls.data(), cls.size() * 2);
     if (!slab.empty()) std::memcpy(b + off_slab, slab.data(), slab.size() * 4);
     v.off_slab = (uint32_t)off_slab;
+#ifndef EPP_V5_DENSE_CLS
+    if (c8) {
+        std::memcpy(b + off_c8, cwords.data(), cwords.size() * 8);
+        if (!cnz.empty()) std::memcpy(b + off_c8 + cwords.size() * 8, cnz.data(), cnz.size());
+    }
+#else
     if (c8)
         for (size_t c = 0; c < cls.size(); ++c) b[off_c8 + c] = (char)(uint8_t)cls[c];
+#endif
     v.off_cls8 = c8 ? (uint32_t)off_c8 : 0u;
+    v.cls8_bytes = (uint32_t)c8_bytes;
     v.off_lists = (uint32_t)off_lists;
     v.off_bitmap = (uint32_t)off_bm;
     v.blob_bytes = (uint32_t)total;
@@ -788,7 +820,7 @@ extern "C" epp_status epp_dbg_class_layout(const epp_obb* obbs, int32_t n, doubl
     const epp::WorldView& v = hw.view;
     const int64_t vals[12] = {v.off_aos, v.off_lists, v.off_ids, v.off_cls8, v.off_bitmap, v.blob_bytes, v.n_lists,
                               v.bm_words, v.bnx, v.bny, v.bnz,
-                              (int64_t)((v.off_cls8 ? ((v.off_cls8 + v.bm_words + 1 + 15u) & ~15u) : v.blob_bytes) -
+                              (int64_t)((v.off_cls8 ? ((v.off_cls8 + v.cls8_bytes + 15u) & ~15u) : v.blob_bytes) -
                                         v.off_aos)};
     for (int k = 0; k < 12; ++k) out[k] = vals[k];
     return EPP_OK;
