@@ -631,9 +631,21 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
             if (jp < ntiles) ida = tile_cand(jp, ca);
             if (jp + 1 < ntiles) idb = tile_cand(jp + 1, cb);
             EPP_MTL_NOW(tl_p);
+#ifdef EPP_MOTIONS_W1MASK  // (A/B) one-word tiles: both tiles' candidates as one 64-bit mask
+            uint64_t cm = W == 1 ? ((uint64_t)ca[0] | ((uint64_t)cb[0] << 32)) : 0ull;
+#endif
             for (;;) {
                 bool has = false;
                 uint32_t wsel = 0, bit = 0;
+#ifdef EPP_MOTIONS_W1MASK
+                if (W == 1) {
+                    has = cm != 0ull;
+                    const uint32_t b64 = (uint32_t)__builtin_ctzll(cm | (1ull << 63));
+                    cm &= cm - 1ull;
+                    wsel = b64 >> 5;
+                    bit = b64 & 31u;
+                } else
+#endif
 #pragma unroll
                 for (int w = 0; w < 2 * W; ++w) {
                     uint32_t& cw = w < W ? ca[w] : cb[w - W];
