@@ -17,7 +17,11 @@ from bench import timed_kernel_ms  # noqa: E402
 
 
 def main():
-    modes = sys.argv[1:] or ["1", "0"]
+    args = sys.argv[1:]
+    lib = args.pop(0) if args and args[0].endswith(".so") else None  # another build (A/B)
+    if lib:
+        capi.LIB_PATH = lib
+    modes = args or ["1", "0"]
     L = capi.lib()
     st = C.c_void_p()
     capi.check(L.epp_stream_create(C.byref(st)))
@@ -56,7 +60,7 @@ def main():
         dims = hdr[40:52].view(np.int32)
         nretry = int(hdr[60:64].view(np.int32)[0])
         why = hdr[64:80].view(np.int32).tolist()
-        print(f"EPP_KNN_TILE={m} nodes {n} k {k}: {ms * 1e3:.1f} us per call, equal to all-pairs: {same}; "
+        print(f"{os.path.basename(lib or 'libepp.so')} EPP_KNN_TILE={m} nodes {n} k {k}: {ms * 1e3:.1f} us per call, equal to all-pairs: {same}; "
               f"grid {dims.tolist()} h {float(hdr[24:32].view(np.float64)[0]):.4f}, retries {nretry} "
               f"(list/range/shell/crowded {why})", flush=True)
 
