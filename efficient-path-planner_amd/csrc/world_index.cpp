@@ -825,3 +825,36 @@ extern "C" epp_status epp_dbg_class_layout(const epp_obb* obbs, int32_t n, doubl
     for (int k = 0; k < 12; ++k) out[k] = vals[k];
     return EPP_OK;
 }
+
+// Debug entry (not part of include/epp.h): host check of k_states_v5's sparse byte-class
+// encoding -- for every class-grid cell (the zero sentinel included) the lookup the kernel
+// does (occupancy word, rank, class byte; states.hip cls_of) must give the cell's class of
+// the u16 table.  Returns the number of mismatching cells (0), or -1 when the world has no
+// byte classes.
+extern "C" int64_t epp_dbg_check_sparse_classes(const epp_obb* obbs, int32_t n, double r_gate, double r_obst) {
+    if (n < 0 || (n > 0 && !obbs)) return -2;
+    epp::HostWorld hw;
+    hw.r_gate = r_gate;
+    hw.r_obst = r_obst;
+    if (!epp::build_blob(hw, obbs, n)) return -2;
+    const epp::WorldView& v = hw.view;
+    if (!v.off_cls8) return -1;
+    const unsigned char* b = reinterpret_cast<const unsigned char*>(hw.blob.data());
+    const uint16_t* cls = reinterpret_cast<const uint16_t*>(b + v.off_bitmap);
+    const unsigned char* base = b + v.off_cls8;
+    const unsigned char* nz = base + ((v.bm_words + 1u + 31u) >> 5) * 8u;
+    int64_t bad = 0;
+    for (uint32_t idx = 0; idx <= v.bm_words; ++idx) {
+#ifndef EPP_V5_DENSE_CLS
+        uint64_t wd;
+        std::memcpy(&wd, base + (size_t)(idx >> 5) * 8, 8);
+        const uint32_t m = (uint32_t)wd, sh = idx & 31u;
+        const uint32_t rank = (uint32_t)(wd >> 32) + (uint32_t)__builtin_popcount(m & ((1u << sh) - 1u));
+        const uint32_t c = ((m >> sh) & 1u) ? (uint32_t)nz[rank] : 0u;
+#else
+        const uint32_t c = base[idx];
+#endif
+        bad += c != (uint32_t)cls[idx];
+    }
+    return bad;
+}

@@ -72,3 +72,29 @@ def test_knn_workspace_size_host_only():
     a, b = L.epp_knn_workspace_size(3000), L.epp_knn_workspace_size(65538)
     assert 0 < a < b and a % 256 == 0 and b % 256 == 0
     assert b >= 65538 * (4 + 4 + 24 + 3 * 4)
+
+
+def test_sparse_byte_classes_match_the_class_table():
+    """k_states_v5's staged byte classes (sparse: an occupancy word with the rank of its
+    first occupied cell per 32 cells, then the class bytes of the occupied cells) decode,
+    cell by cell with the kernel's lookup, to the class table of the index (host build, no
+    GPU): C1, C2, C2 with filling boxes, and a 190-OBB world."""
+    import ctypes as C
+    from eppamd import config, synth
+    from conftest import ROOT
+    L = capi.lib()
+    f = L.epp_dbg_check_sparse_classes
+    f.restype = C.c_int64
+    f.argtypes = [C.c_void_p, C.c_int32, C.c_double, C.c_double]
+    checked = 0
+    for cfg_name in ("config.json", "config_filling.json"):
+        cfg = config.load(os.path.join(ROOT, "configs", cfg_name))
+        geom = config.geometry(cfg)
+        rg, ro = config.inflate_radii(cfg)
+        g1, o1, _, _ = synth.c1_world()
+        for g, o in ((g1, o1), synth.track_world(42), synth.track_world(42, n_obstacles=150)):
+            obbs = capi.build_obbs(geom, g, o)
+            r = f(obbs.ctypes.data, len(obbs), rg, ro)
+            assert r in (0, -1), r
+            checked += r == 0
+    assert checked >= 4
