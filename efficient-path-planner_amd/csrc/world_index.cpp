@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -590,6 +591,73 @@ bool upload(HostWorld& hw) {
     return true;
 }
 
+// Buffers of destroyed worlds, kept for the next epp_world_create on the same device: a
+// fresh PathPlanner / OnlineTrajGenerator per request then reuses the pinned record slots,
+// the pinned upload staging, the device blob and the upload stream instead of allocating
+// them again (pinned allocations are the cold cost of a world; the buffers grow as needed).
+// Never freed (the pool lives until the process exits, as the HIP runtime's own caches).
+struct WorldBufs {
+    int device = 0;
+    double* rec_buf[2] = {nullptr, nullptr};
+    size_t rec_cap[2] = {0, 0};
+    std::vector<HostWorld::RecReader> readers[2];
+    void* h_stage = nullptr;
+    size_t h_capacity = 0;
+    void* d_blob = nullptr;
+    size_t d_capacity = 0;
+    hipStream_t stream = nullptr;
+};
+constexpr size_t kWorldPoolMax = 8;
+std::mutex g_world_pool_mu;
+std::vector<WorldBufs>& world_pool() {
+    static auto* pool = new std::vector<WorldBufs>();  // (intentionally leaked, see above)
+    return *pool;
+}
+
+void pool_take(HostWorld& hw) {
+    std::lock_guard<std::mutex> lk(g_world_pool_mu);
+    auto& pool = world_pool();
+    for (size_t i = 0; i < pool.size(); ++i)
+        if (pool[i].device == hw.device) {
+            WorldBufs& b = pool[i];
+            for (int k = 0; k < 2; ++k) {
+                hw.rec_buf[k] = b.rec_buf[k];
+                hw.rec_cap[k] = b.rec_cap[k];
+                hw.rec_readers[k] = std::move(b.readers[k]);
+            }
+            hw.h_stage = b.h_stage;
+            hw.h_capacity = b.h_capacity;
+            hw.d_blob = b.d_blob;
+            hw.d_capacity = b.d_capacity;
+            hw.stream = b.stream;
+            pool.erase(pool.begin() + (std::ptrdiff_t)i);
+            return;
+        }
+}
+
+// The world's buffers into the pool (the device is idle: epp_world_destroy synchronised);
+// false when the pool is full (the caller frees them).
+bool pool_give(HostWorld& hw) {
+    std::lock_guard<std::mutex> lk(g_world_pool_mu);
+    auto& pool = world_pool();
+    if (pool.size() >= kWorldPoolMax) return false;
+    WorldBufs b;
+    b.device = hw.device;
+    for (int k = 0; k < 2; ++k) {
+        b.rec_buf[k] = hw.rec_buf[k];
+        b.rec_cap[k] = hw.rec_cap[k];
+        b.readers[k] = std::move(hw.rec_readers[k]);
+        for (auto& r : b.readers[k]) r.pending = false;
+    }
+    b.h_stage = hw.h_stage;
+    b.h_capacity = hw.h_capacity;
+    b.d_blob = hw.d_blob;
+    b.d_capacity = hw.d_capacity;
+    b.stream = hw.stream;
+    pool.push_back(std::move(b));
+    return true;
+}
+
 }  // namespace
 
 }  // namespace epp
@@ -614,12 +682,14 @@ epp_status epp_world_create(const epp_obb* obbs, int32_t n, double r_gate, doubl
     w->r_gate = r_gate;
     w->r_obst = r_obst;
     (void)hipGetDevice(&w->device);
+    epp::pool_take(*w);  // (buffers of a destroyed world on this device, if any)
+    // (on failure the buffers go back to the pool or are freed; the error message stays)
     if (!epp::build_records(*w, obbs, n) || !epp::build_blob(*w, obbs, n)) {
-        delete w;
+        (void)epp_world_destroy(w);
         return EPP_ERR_UNSUPPORTED;
     }
     if (!epp::upload(*w)) {
-        delete w;
+        (void)epp_world_destroy(w);
         return EPP_ERR_HIP;
     }
     w->generation = 1;
@@ -647,6 +717,10 @@ epp_status epp_world_update(epp_world* w, const epp_obb* obbs, int32_t n) {
 epp_status epp_world_destroy(epp_world* w) {
     if (!w) return EPP_OK;
     (void)hipDeviceSynchronize();
+    if (epp::pool_give(*w)) {  // kept for the next world (no kernel reads them any more)
+        delete w;
+        return EPP_OK;
+    }
     if (w->d_blob) (void)hipFree(w->d_blob);
     if (w->h_stage) (void)hipHostFree(w->h_stage);
     for (int k = 0; k < 2; ++k) {

@@ -703,3 +703,21 @@ def test_c3_motions_full_bench_size(geom, worlds, mode, can_pass):
     assert 0 < int(exp.sum()) < len(exp)
     assert np.array_equal(got, exp), int((got != exp).sum())
     w.close()
+
+
+def test_world_buffers_reused_across_worlds(geom, worlds):
+    """Destroyed worlds leave their pinned and device buffers to the next world on the
+    device (a fresh PathPlanner per request allocates nothing): worlds of growing and
+    shrinking size created one after the other keep the oracle's answers (the device blob
+    and the record slots grow when a reused buffer is too small)."""
+    rg, ro, ws = worlds
+    lo, hi = synth.C2_BOUNDS
+    pts = synth.sample_states(31, lo, hi, 50_000)
+    small = synth.sample_states(32, lo, hi, 1000)
+    for name in ("c2", "c3", "c1", "c3", "c2"):
+        g, o, _ = ws[name]
+        ref = O.world_build(geom, g, o, rg, ro)
+        w = capi.World(capi.build_obbs(geom, g, o), rg, ro)
+        assert np.array_equal(w.check_states(pts), O.check_states(ref, rg, ro, pts, threads=8)), name
+        assert np.array_equal(w.check_states(small), O.check_states(ref, rg, ro, small)), name
+        w.close()
