@@ -663,6 +663,13 @@ V5Shape v5_shape(int64_t n, uint32_t sb) {
     const int64_t cus = cu_count();
     r.gN = n / 4;
     const int forced = env_int("EPP_V5_BLOCK", 0);
+    if (forced == 256 && 4u * (sb + 16u + queue5_bytes<256>()) <= 160u * 1024u && r.gN <= 4 * cus * 256) {
+        // (test hook / A/B) single pass on four 256-thread workgroups per CU
+        r.bs = 256;
+        r.grid = (int)std::max<int64_t>(1, (r.gN + 255) / 256);
+        r.pf = false;
+        return r;
+    }
     const bool two = forced == 0 && 2u * (sb + 16u + queue5_bytes<512>()) <= 160u * 1024u && r.gN <= 2 * cus * 512;
     if (two) {
         r.bs = 512;
@@ -702,7 +709,11 @@ epp_status launch_states(const WorldView& w, const WorldView* dw, const double* 
 #else
         const uint32_t sb = v5_staged(w);
 #endif
-        const V5Shape sh = v5_shape(n, sb);
+        V5Shape sh = v5_shape(n, sb);
+        if (sh.bs == 256 && compact_idx) {  // (the 256-thread shape is instantiated without compaction)
+            sh.bs = 512;
+            sh.grid = (int)std::max<int64_t>(1, (sh.gN + 511) / 512);
+        }
         const uint32_t dyn = sb + 16u;  // the staged world + the dummy slot of the copy
 #define EPP_LAUNCH_V5S(C, B, P, C8, SC)                                                                              \
     do {                                                                                                             \
@@ -736,7 +747,8 @@ epp_status launch_states(const WorldView& w, const WorldView* dw, const double* 
             else EPP_LAUNCH_V5(false, B, false);         \
         }                                                \
     } while (0)
-        if (sh.bs == 512) EPP_LAUNCH_V5B(512);
+        if (sh.bs == 256) EPP_LAUNCH_V5(false, 256, false);  // (EPP_V5_BLOCK=256, single pass)
+        else if (sh.bs == 512) EPP_LAUNCH_V5B(512);
         else EPP_LAUNCH_V5B(1024);
 #undef EPP_LAUNCH_V5B
 #undef EPP_LAUNCH_V5

@@ -12,6 +12,8 @@ for r in 1 2; do
     timeout -k 10 120 python scripts/states_ab.py $lib > gpurun_out/ab.log 2>&1; rc=$?
     tail -1 gpurun_out/ab.log; stop_on_fault $rc "states $lib"
   done
+  timeout -k 10 120 python scripts/states_ab.py EPP_V5_BLOCK=256 > gpurun_out/ab.log 2>&1; rc=$?
+  tail -1 gpurun_out/ab.log; stop_on_fault $rc "states 256"
   for lib in "" scripts/dbg/libepp_pfflush.so scripts/dbg/libepp_w1mask.so scripts/dbg/libepp_w1pf.so; do
     timeout -k 10 120 python scripts/motions_ab.py $lib > gpurun_out/ab.log 2>&1; rc=$?
     tail -1 gpurun_out/ab.log; stop_on_fault $rc "motions $lib"

@@ -91,7 +91,7 @@ def test_states_mindist(geom, worlds, name):
         assert np.array_equal(got, exp), md
 
 
-@pytest.mark.parametrize("impl", ["v5", "v5b512", "v5b1024", "v4", "generic"])
+@pytest.mark.parametrize("impl", ["v5", "v5b256", "v5b512", "v5b1024", "v4", "generic"])
 @pytest.mark.parametrize("name", ["c2", "c3"])
 def test_states_every_kernel_variant(geom, worlds, name, impl, monkeypatch):
     """Each state kernel (k_states_v5 = default, k_states_v4 = fallback for worlds whose
