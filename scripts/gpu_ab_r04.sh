@@ -18,9 +18,5 @@ for r in 1 2; do
     timeout -k 10 120 python scripts/motions_ab.py $lib > gpurun_out/ab.log 2>&1; rc=$?
     tail -1 gpurun_out/ab.log; stop_on_fault $rc "motions $lib"
   done
-  for lib in "" scripts/dbg/libepp_pack8.so; do
-    timeout -k 10 120 python scripts/knn_probe.py $lib 1 > gpurun_out/ab.log 2>&1; rc=$?
-    tail -1 gpurun_out/ab.log; stop_on_fault $rc "knn $lib"
-  done
 done
 echo done
