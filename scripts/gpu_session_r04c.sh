@@ -6,6 +6,10 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+# (the k-NN tests first: the previous session faulted in test_knn_grid_large)
+timeout -k 10 300 python -u -m pytest tests/test_gpu_planner.py -m gpu -x -q --timeout 120 --timeout-method thread -k knn > gpurun_out/pytest_knn.log 2>&1; rc=$?
+tail -3 gpurun_out/pytest_knn.log
+[ $rc -ne 0 ] && { echo "pytest (knn) ended with $rc: stopping"; exit $rc; }
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 tail -4 gpurun_out/pytest_gpu.log
 [ $rc -ne 0 ] && { echo "pytest ended with $rc: stopping"; exit $rc; }
