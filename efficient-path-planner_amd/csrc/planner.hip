@@ -544,23 +544,56 @@ constexpr double kTileDelta = 1e-3;     // float error allowance, in h^2
 #endif
 constexpr double kPass1R2 = EPP_KNN_PASS1R2;  // pass 1 first visits the cells within sqrt(4.5) h
 
+// A halo candidate in LDS.  Default: float x, y, z relative to the block centre + the
+// node's sorted position (16 B).  EPP_KNN_PACK8 (A/B): x, y, z as 21-bit fixed point over
+// [-4h, 4h) (quantum q = 4h / 2^20 ~ 3.8e-6 h) in 8 bytes, the sorted positions in a
+// separate array read only by the exact phase -- half the LDS bytes per candidate in
+// passes 1 and 2.  The squared distance from the integer differences (exact in float) times
+// q^2 is within ~7e-5 h^2 of the exact one (|difference| <= 3h per axis, each coordinate
+// rounded by <= q / 2), inside kTileDelta.
+#ifdef EPP_KNN_PACK8
+typedef uint2 TileCand;
+struct TileQ {
+    int x, y, z;
+};
+__device__ __forceinline__ TileQ tile_q(const uint2 c) {
+    return {(int)(c.x & 0x1FFFFFu), (int)((c.x >> 21) | ((c.y & 0x3FFu) << 11)), (int)(c.y >> 10)};
+}
+__device__ __forceinline__ float tile_d(const uint2 c, const TileQ& p, float kq2) {
+    const TileQ t = tile_q(c);
+    const float dx = (float)(t.x - p.x), dy = (float)(t.y - p.y), dz = (float)(t.z - p.z);
+    return ((dx * dx + dy * dy) + dz * dz) * kq2;
+}
+__device__ __forceinline__ int tile_key(const uint2, int q) { return q; }  // (self test: the LDS position)
+#else
+typedef float4 TileCand;
+typedef float4 TileQ;
+__device__ __forceinline__ TileQ tile_q(const float4 c) { return c; }
+__device__ __forceinline__ float tile_d(const float4 c, const float4& pf, float) {
+    const float dx = c.x - pf.x, dy = c.y - pf.y, dz = c.z - pf.z;
+    return (dx * dx + dy * dy) + dz * dz;
+}
+__device__ __forceinline__ int tile_key(const float4 c, int) { return __float_as_int(c.w); }  // (sorted position)
+#endif
+
 // Visits the candidates of cube rows row0, row0 + rstep, ... around a query (a row =
 // kTileW consecutive halo cells along x, one contiguous LDS range), four candidates at a
-// time so their LDS reads are in flight together.  f(q, d_float, id, valid).
+// time so their LDS reads are in flight together.  f(q, d_float, key, valid), key = what
+// the self test compares (tile_key).
 template <class F>
-__device__ __forceinline__ void tile_rows(const int* cst, const float4* cand, int h0, int row0, int rstep,
-                                          const float4& pf, F&& f) {
+__device__ __forceinline__ void tile_rows(const int* cst, const TileCand* cand, int h0, int row0, int rstep,
+                                          const TileQ& pf, float kq2, F&& f) {
     for (int row = row0; row < kTileRows; row += rstep) {
         const int a = h0 + ((row / kTileW) * kTileE + row % kTileW) * kTileE;
         const int q1 = cst[a + kTileW];
         for (int q = cst[a]; q < q1; q += 4) {
-            float4 c[4];
+            TileCand c[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) c[u] = cand[min(q + u, q1 - 1)];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const float dx = c[u].x - pf.x, dy = c[u].y - pf.y, dz = c[u].z - pf.z;
-                f(min(q + u, q1 - 1), (dx * dx + dy * dy) + dz * dz, __float_as_int(c[u].w), q + u < q1);
+                const int qq = min(q + u, q1 - 1);
+                f(qq, tile_d(c[u], pf, kq2), tile_key(c[u], qq), q + u < q1);
             }
         }
     }
@@ -576,8 +609,9 @@ __device__ __forceinline__ double tile_gap(int off, double fr, double h) {
 }
 
 template <class F>
-__device__ __forceinline__ void tile_rows_near(const int* cst, const float4* cand, int h0, int row0, int rstep,
-                                               const float4& pf, const double (&fr)[3], double h, double thr, F&& f) {
+__device__ __forceinline__ void tile_rows_near(const int* cst, const TileCand* cand, int h0, int row0, int rstep,
+                                               const TileQ& pf, float kq2, const double (&fr)[3], double h, double thr,
+                                               F&& f) {
     const double gx1 = tile_gap(1, fr[0], h), gx2 = tile_gap(2, fr[0], h);
     const double gxm1 = tile_gap(-1, fr[0], h), gxm2 = tile_gap(-2, fr[0], h);
     for (int row = row0; row < kTileRows; row += rstep) {
@@ -591,13 +625,13 @@ __device__ __forceinline__ void tile_rows_near(const int* cst, const float4* can
         const int a = h0 + (rz * kTileE + ry) * kTileE;
         const int q1 = cst[a + xb + 1];
         for (int q = cst[a + xa]; q < q1; q += 4) {
-            float4 c[4];
+            TileCand c[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) c[u] = cand[min(q + u, q1 - 1)];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const float dx = c[u].x - pf.x, dy = c[u].y - pf.y, dz = c[u].z - pf.z;
-                f(min(q + u, q1 - 1), (dx * dx + dy * dy) + dz * dz, __float_as_int(c[u].w), q + u < q1);
+                const int qq = min(q + u, q1 - 1);
+                f(qq, tile_d(c[u], pf, kq2), tile_key(c[u], qq), q + u < q1);
             }
         }
     }
@@ -794,7 +828,13 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                                                            int* __restrict__ retry, double* __restrict__ retry_b,
                                                            int32_t* __restrict__ nbr, int mode,
                                                            unsigned long long* __restrict__ dbg) {
-    __shared__ float4 cand[kTileCap];                      // x, y, z (block-centre relative), sorted position
+    __shared__ TileCand cand[kTileCap];                    // x, y, z (block-centre relative) [, sorted position]
+#ifdef EPP_KNN_PACK8
+    __shared__ int spos[kTileCap];                         // sorted positions (exact phase)
+#define EPP_SPOS(q) spos[q]
+#else
+#define EPP_SPOS(q) __float_as_int(cand[q].w)
+#endif
     __shared__ uint16_t qh[kTileCap];                      // the block's queries (LDS positions)
     __shared__ int cst[kTileCells + 1];                    // halo cell -> LDS offset
     __shared__ uint32_t hist[kTileNB / 2][kTileThreads];  // [bin pair][query slot]
@@ -816,6 +856,12 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
     const double t0 = g.h * g.h * 0.35 * kscale;
     const float inv_t0 = (float)(1.0 / t0);
     const double delta = kTileDelta * g.h * g.h;
+#ifdef EPP_KNN_PACK8
+    const double qs = 1048576.0 / (4.0 * g.h);              // quanta per unit length
+    const float kq2 = (float)(1.0 / (qs * qs));             // squared quantum
+#else
+    const float kq2 = 1.0f;
+#endif
     for (;;) {
         if (threadIdx.x == 0) s_b = atomicAdd(&gp->next, 1);
         __syncthreads();
@@ -892,8 +938,18 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                 for (int q = 0; q < cnt[u]; ++q) {
                     const int sg = cell0[u] + q;
                     const double x = sxyz[3 * sg], y = sxyz[3 * sg + 1], z = sxyz[3 * sg + 2];
+#ifdef EPP_KNN_PACK8
+                    auto qz = [&](double v) {
+                        const int i = (int)rint(v * qs) + (1 << 20);
+                        return (uint32_t)min(max(i, 0), (1 << 21) - 1);
+                    };
+                    const uint32_t ux = qz(x - cen[0]), uy = qz(y - cen[1]), uz = qz(z - cen[2]);
+                    cand[acc + q] = make_uint2(ux | (uy << 21), (uy >> 11) | (uz << 10));
+                    spos[acc + q] = sg;
+#else
                     cand[acc + q] = make_float4((float)(x - cen[0]), (float)(y - cen[1]), (float)(z - cen[2]),
                                                 __int_as_float(sg));  // (sorted position: see the exact phase)
+#endif
                     if (inner) qh[q0 + q] = (uint16_t)(acc + q);
                 }
                 acc += cnt[u];
@@ -916,8 +972,9 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                 const int qi = qb + slot;
                 const bool live = qi < nq;
                 const int me = live ? qh[qi] : 0;
-                const float4 pf = cand[me];
-                const int sself = __float_as_int(pf.w);  // the query's sorted position
+                const TileQ pf = tile_q(cand[me]);
+                const int sself = EPP_SPOS(me);  // the query's sorted position
+                const int skey = tile_key(cand[me], me);  // what its self test compares
                 // exact coordinates and cell (the row offsets; the final distances)
                 const double p[3] = {sxyz[3 * (int64_t)sself], sxyz[3 * (int64_t)sself + 1], sxyz[3 * (int64_t)sself + 2]};
                 const int c[3] = {knn_cell_axis(p[0], g, 0), knn_cell_axis(p[1], g, 1), knn_cell_axis(p[2], g, 2)};
@@ -940,11 +997,11 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                     auto bin = [&](int, float d, int j, bool valid) {
                         const int kb = max((int)(__float_as_uint(d * inv_t0) >> 21) - (127 << 2), 0);
-                        if (valid && j != sself && kb < kTileNB) atomicAdd(&hist[kb >> 1][slot], 1u << ((kb & 1) << 4));
+                        if (valid && j != skey && kb < kTileNB) atomicAdd(&hist[kb >> 1][slot], 1u << ((kb & 1) << 4));
                     };
                     if (live) {
-                        if (full) tile_rows(cst, cand, h0, sub, lpq, pf, bin);
-                        else tile_rows_near(cst, cand, h0, sub, lpq, pf, fr, g.h, kPass1R2 * g.h * g.h, bin);
+                        if (full) tile_rows(cst, cand, h0, sub, lpq, pf, kq2, bin);
+                        else tile_rows_near(cst, cand, h0, sub, lpq, pf, kq2, fr, g.h, kPass1R2 * g.h * g.h, bin);
                     }
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                     int run = 0;
@@ -971,8 +1028,8 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                 int nown = 0;
                 if (live) {
                     const double thr2 = cut < 0 ? INFINITY : dcut + 3.0 * delta;
-                    tile_rows_near(cst, cand, h0, sub, lpq, pf, fr, g.h, thr2, [&](int q, float d, int j, bool valid) {
-                        if (valid && j != sself && d < dlist) {
+                    tile_rows_near(cst, cand, h0, sub, lpq, pf, kq2, fr, g.h, thr2, [&](int q, float d, int j, bool valid) {
+                        if (valid && j != skey && d < dlist) {
                             if (nown < kTileL) lst[nown][threadIdx.x] = (uint16_t)q;
                             ++nown;
                         }
@@ -989,7 +1046,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                 const int qx = qb + (int)threadIdx.x;
                 if ((int)threadIdx.x < kTileThreads / lpq && qx < nq) {
                 const int tcol = (int)threadIdx.x * lpq;  // the query's first list column
-                const int sx = __float_as_int(cand[qh[qx]].w);
+                const int sx = EPP_SPOS(qh[qx]);
                 const int self = sidx[sx];
                 const double p[3] = {sxyz[3 * (int64_t)sx], sxyz[3 * (int64_t)sx + 1], sxyz[3 * (int64_t)sx + 2]};
                 const int c[3] = {knn_cell_axis(p[0], g, 0), knn_cell_axis(p[1], g, 1), knn_cell_axis(p[2], g, 2)};
@@ -1036,7 +1093,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                             // copy: these gathers hit the few KB the block's queries share in L1,
                             // where the nodes' original order scattered them over the table)
                             const int q = lst[e][tcol + col];
-                            const int sg = __float_as_int(cand[q].w);
+                            const int sg = EPP_SPOS(q);
                             jj[u] = sidx[sg];
                             const double ddx = sxyz[3 * (int64_t)sg] - p[0], ddy = sxyz[3 * (int64_t)sg + 1] - p[1],
                                          ddz = sxyz[3 * (int64_t)sg + 2] - p[2];
