@@ -123,6 +123,7 @@ struct KnnGrid {
 
 constexpr int kBoundsThreads = 1024;
 constexpr int kBoundsBlocks = 64;
+constexpr int kKnnDefaultTile = 1;     // grid k-NN kernel without EPP_KNN_TILE: 1 k_knn_tile, 2 k_knn_wave
 constexpr double kNodesPerCell = 1.5;  // mean nodes per grid cell (EPP_KNN_NPC overrides in -DEPP_KNN_DIAG builds; tuned for k_knn_tile: ~90 queries per 4^3 block -> 2 lanes each)
 
 // The grid over the box [mn, mx] for n nodes: cells of edge h with ~npc nodes each (flat
@@ -1180,6 +1181,298 @@ __global__ __launch_bounds__(64) void k_knn_retry(const KnnGrid* __restrict__ gp
         knn_retry_wave<K>(g, r2max, nodes, sxyz, sidx, start, retry[i], retry_b[i], nbr);
 }
 
+// ---- wave-per-query grid k-NN (k_knn_wave) ---------------------------------------------
+// The same 4^3-cell blocks, 2-cell halos and block queue as k_knn_tile, but the halo's
+// exact coordinates sit in LDS (SoA doubles) and one wavefront takes one query at a time:
+//   1. the query's 5^3-cell cube is five z-slabs; each slab's five y-rows are one
+//      contiguous LDS range (rows ly-2..ly+2 of the halo, x cells outside lx-2..lx+2
+//      filtered by the halo x index kept with the node id).  The ranges are concatenated
+//      and spread over the lanes, up to kWaveSlots candidates per lane, every lane doing
+//      the same work (no per-query loop lengths, no divergence);
+//   2. exact squared distance per candidate (the oracle's (dx dx + dy dy) + dz dz), and a
+//      key: one of 128 linear bins of d over [0, 8 h^2) (monotone in d: every candidate at or below
+//      the K-th distance has a key at or below the K-th one's);
+//   3. the smallest cut with >= K keys at or below it, by bisection over the bins on
+//      wave ballots (no histogram, no atomics);
+//   4. the candidates at or below the cut (K plus a fraction of a bin, on average) go to a
+//      per-wave LDS list; each listed entry's rank in (distance, index) order is counted
+//      against the list: ranks < K are the answer, the rank K-1 entry the K-th distance for
+//      the stopping rule after shell kTileH (knn_done).
+// A query whose cube holds more than 64 kWaveSlots positions or whose list exceeds
+// kWaveList, or that fails the stopping rule, goes to the retry list (k_knn_retry), as in
+// k_knn_tile.  k_knn_tile's lanes-per-query scheme runs ~375 wave-instructions per query
+// and waits on long dependent LDS chains of its busiest lane (SQ_WAIT_ANY ~66 % of its
+// wave cycles); here a query is ~10 short LDS round trips and a fixed instruction count.
+constexpr int kWaveThreads = 512;                // = kTileCells: one halo cell per thread
+constexpr int kWaveCap = 1344;                   // halo candidates (else the block's queries retry)
+constexpr int kWaveSlots = 6;                    // candidate slots per lane: 384 cube positions (~278 at 1.5 nodes per cell)
+constexpr int kWaveList = 64;                    // listed candidates per query (else retry)
+constexpr int kWaveBins = 128;                   // distance keys: linear bins over [0, 8 h^2)
+static_assert(kTileCells == kWaveThreads, "one halo cell per thread");
+
+template <int K>
+__global__ __launch_bounds__(kWaveThreads, 6) void k_knn_wave(KnnGrid* __restrict__ gp, double r2max,
+                                                              const double* __restrict__ sxyz,
+                                                              const int* __restrict__ sidx,
+                                                              const int* __restrict__ start,
+                                                              int* __restrict__ retry, double* __restrict__ retry_b,
+                                                              int32_t* __restrict__ nbr,
+                                                              unsigned long long* __restrict__ dbg) {
+    static_assert(K <= kWaveList && K <= 64, "");
+    constexpr int kWaves = kWaveThreads / 64;
+    __shared__ double hxv[kWaveCap], hyv[kWaveCap], hzv[kWaveCap];  // exact coordinates
+    __shared__ int hid[kWaveCap];                                   // node id | halo x index << 29
+    __shared__ uint32_t qh[kWaveCap];  // the block's queries: LDS position | halo x, y, z << 11, 14, 17
+    __shared__ int cst[kTileCells + 1];                              // halo cell -> LDS offset
+    __shared__ double ld[kWaves][kWaveList];                         // per-wave list: distances
+    __shared__ int lj[kWaves][kWaveList];                            //                node ids
+    __shared__ int wsum[kWaves];
+    __shared__ int s_nq, s_b;
+    __shared__ KnnGrid s_g;
+    if (threadIdx.x == 0) s_g = *gp;  // (visible after the loop's first barrier)
+    // (the grid parameters are read where they are used -- from gp or the LDS copy -- not
+    // held in registers through the query loop: the scalar register file is this kernel's
+    // tight resource)
+    const int dims0 = gp->dims[0], dims1 = gp->dims[1], dims2 = gp->dims[2];
+    const int nbx = (dims0 + kTileB - 1) / kTileB, nby = (dims1 + kTileB - 1) / kTileB,
+              nbz = (dims2 + kTileB - 1) / kTileB;
+    const int nblocks = nbx * nby * nbz;
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const double inv_w = (double)kWaveBins / (8.0 * gp->h * gp->h);  // bins per unit of squared distance
+    const int t = threadIdx.x;
+    const int hx = t % kTileE, hy = (t / kTileE) % kTileE, hz = t / (kTileE * kTileE);  // this thread's halo cell
+    for (;;) {
+        if (t == 0) s_b = atomicAdd(&gp->next, 1);
+        __syncthreads();
+        const int b = s_b;  // block-uniform
+        if (b >= nblocks) break;
+        const int bx = b % nbx, by = (b / nbx) % nby, bz = b / (nbx * nby);
+        const int ox = bx * kTileB - kTileH, oy = by * kTileB - kTileH, oz = bz * kTileB - kTileH;
+#ifdef EPP_KNN_DIAG
+        // phase timeline (diagnostics builds; scripts/knn_timeline.py): begin, halo scanned,
+        // halo copied, wave 0's first query done, wave 0's queries done, (same), all waves
+        // done, end; wave 0's query count and s_memtime cycles in its query loop
+        unsigned long long tl[8] = {__builtin_amdgcn_s_memrealtime(), 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long cyc0 = 0, nq0 = 0;
+#endif
+        // 1. halo cell sizes -> exclusive scan
+        const int x = ox + hx, y = oy + hy, z = oz + hz;
+        const bool in = x >= 0 && x < dims0 && y >= 0 && y < dims1 && z >= 0 && z < dims2;
+        const int cell = in ? (z * dims1 + y) * dims0 + x : 0;
+        const int s0 = start[cell];
+        const int cnt = in ? start[cell + 1] - s0 : 0;
+        int incl = cnt;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        if (lane == 63) wsum[wv] = incl;
+        if (t == 0) s_nq = 0;
+        __syncthreads();
+        int base = incl - cnt, total = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+            base += w < wv ? wsum[w] : 0;
+            total += wsum[w];
+        }
+        cst[t] = base;
+        if (t == 0) cst[kTileCells] = total;
+#ifdef EPP_KNN_DIAG
+        tl[1] = __builtin_amdgcn_s_memrealtime();
+#endif
+        if (total <= kWaveCap) {  // block-uniform
+            // 2. copy the halo's nodes; list the block's own as queries
+            const bool inner = hx >= kTileH && hx < kTileH + kTileB && hy >= kTileH && hy < kTileH + kTileB &&
+                               hz >= kTileH && hz < kTileH + kTileB;
+            const int q0 = (inner && cnt) ? atomicAdd(&s_nq, cnt) : 0;
+            for (int q = 0; q < cnt; ++q) {
+                const int sg = s0 + q, pos = base + q;
+                hxv[pos] = sxyz[3 * (int64_t)sg];
+                hyv[pos] = sxyz[3 * (int64_t)sg + 1];
+                hzv[pos] = sxyz[3 * (int64_t)sg + 2];
+                hid[pos] = sidx[sg] | (hx << 29);
+                if (inner) qh[q0 + q] = (uint32_t)pos | ((uint32_t)hx << 11) | ((uint32_t)hy << 14) | ((uint32_t)hz << 17);
+            }
+            __syncthreads();
+            const int nq = s_nq;
+#ifdef EPP_KNN_DIAG
+            tl[2] = __builtin_amdgcn_s_memrealtime();
+            cyc0 = __builtin_amdgcn_s_memtime();
+#endif
+            // 3. one query per wave at a time
+            for (int qi = wv; qi < nq; qi += kWaves) {  // wave-uniform
+                // (the query's values are wave-uniform: moved to scalar registers, which
+                // keeps the vector file for the candidate slots)
+                const uint32_t qv = (uint32_t)__builtin_amdgcn_readfirstlane((int)qh[qi]);
+                const int me = (int)(qv & 2047u);
+                const int lx = (int)((qv >> 11) & 7u), ly = (int)((qv >> 14) & 7u), lz = (int)((qv >> 17) & 7u);
+                auto uni = [](double v) {
+                    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                                            __builtin_amdgcn_readfirstlane(__double2loint(v)));
+                };
+                const double px = uni(hxv[me]), py = uni(hyv[me]), pz = uni(hzv[me]);
+                const int self = __builtin_amdgcn_readfirstlane(hid[me]) & 0x1fffffff;
+                double bnd;  // the stopping rule's bound after shell kTileH (knn_bound)
+                {
+                    const KnnGrid g = s_g;  // (LDS: a global load here would wait out an L2 round trip per query)
+                    const int c[3] = {ox + lx, oy + ly, oz + lz};
+                    const double p[3] = {px, py, pz};
+                    bnd = knn_bound(g, c, p, kTileH);
+                }
+                // the five slab ranges [A_d, B_d): lanes 0-4 read A, lanes 5-9 read B
+                int rv = 0;
+                if (lane < 10) {
+                    const int d = lane < 5 ? lane : lane - 5;
+                    const int row = (lz - kTileH + d) * kTileE + (lane < 5 ? ly - kTileH : ly + kTileH);
+                    rv = cst[row * kTileE + (lane < 5 ? lx - kTileH : lx + kTileH + 1)];
+                }
+                int A[5], P[6];
+                P[0] = 0;
+#pragma unroll
+                for (int d = 0; d < 5; ++d) {
+                    A[d] = __builtin_amdgcn_readlane(rv, d);
+                    P[d + 1] = P[d] + (__builtin_amdgcn_readlane(rv, 5 + d) - A[d]);
+                }
+                const int T = P[5];  // positions in the five ranges
+                int gap[5];          // v -> LDS position: v + A_0 + the gaps between ranges behind v
+#pragma unroll
+                for (int d = 1; d < 5; ++d) gap[d] = A[d] - (A[d - 1] + (P[d] - P[d - 1]));
+                bool done = false;
+                double dk = r2max;  // the K-th distance (r2max: fewer than K candidates)
+                if (T <= kWaveSlots * 64) {  // wave-uniform
+                    // per slot: the exact distance and (key << 11 | LDS position); key
+                    // kWaveBins: no candidate
+                    double dv[kWaveSlots];
+                    uint32_t kp[kWaveSlots];
+#pragma unroll
+                    for (int s = 0; s < kWaveSlots; ++s) {
+                        kp[s] = (uint32_t)kWaveBins << 11;
+                        dv[s] = 0.0;
+                        if (s * 64 < T) {  // wave-uniform
+                            const int v = s * 64 + lane;
+                            int pos = A[0] + v;
+#pragma unroll
+                            for (int d = 1; d < 5; ++d) pos += v >= P[d] ? gap[d] : 0;
+                            const bool ok = v < T;
+                            const int pc = ok ? pos : me;
+                            const double dx = hxv[pc] - px, dy = hyv[pc] - py, dz = hzv[pc] - pz;
+                            const double dd = (dx * dx + dy * dy) + dz * dz;
+                            const uint32_t cx = ((uint32_t)hid[pc] >> 29) - (uint32_t)(lx - kTileH);  // x cell in the cube?
+                            const bool el = ok & (pc != me) & (cx <= 4u) & (dd <= r2max);
+                            const double kd = dd * inv_w;
+                            const uint32_t key = el ? (kd < (double)(kWaveBins - 1) ? (uint32_t)kd : kWaveBins - 1u) : kWaveBins;
+                            kp[s] = (key << 11) | (uint32_t)pc;
+                            dv[s] = dd;
+                        }
+                    }
+                    auto count_le = [&](int c) {  // candidates with key <= c
+                        const uint32_t lim = (uint32_t)(c + 1) << 11;
+                        int n = 0;
+#pragma unroll
+                        for (int s = 0; s < kWaveSlots; ++s) n += (int)__popcll(__ballot(kp[s] < lim));  // (unused slots: never)
+                        return n;
+                    };
+                    // the smallest cut with >= K keys at or below it (all candidates when
+                    // fewer than K)
+                    int lo = 0, hi = kWaveBins - 1;
+                    if (count_le(hi) >= K) {
+                        while (lo < hi) {  // wave-uniform
+                            const int mid = (lo + hi) >> 1;
+                            if (count_le(mid) >= K) hi = mid;
+                            else lo = mid + 1;
+                        }
+                    }
+                    const uint32_t lim = (uint32_t)(hi + 1) << 11;
+                    int m = 0;
+#pragma unroll
+                    for (int s = 0; s < kWaveSlots; ++s) {
+                        const bool li = kp[s] < lim;
+                        const unsigned long long bl = __ballot(li);
+                        const int at = m + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bl >> 32),
+                                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
+                        if (li && at < kWaveList) {
+                            ld[wv][at] = dv[s];
+                            lj[wv][at] = hid[kp[s] & 2047u] & 0x1fffffff;
+                        }
+                        m += (int)__popcll(bl);
+                    }
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the list is written
+                    if (m <= kWaveList) {  // wave-uniform
+                        const bool mine = lane < m;
+                        const double di = mine ? ld[wv][lane] : 0.0;
+                        const int ji = mine ? lj[wv][lane] : 0;
+                        // entry f (on lane f) against every lane's own: v_readlane into scalar
+                        // registers, no memory round trip per entry
+                        const int dlo = __double2loint(di), dhi = __double2hiint(di);
+                        int rank = 0;
+                        for (int f = 0; f < m; ++f) {  // wave-uniform
+                            const double df = __hiloint2double(__builtin_amdgcn_readlane(dhi, f),
+                                                               __builtin_amdgcn_readlane(dlo, f));
+                            const int jf = __builtin_amdgcn_readlane(ji, f);
+                            rank += ((df < di) | ((df == di) & (jf < ji))) ? 1 : 0;
+                        }
+                        if (m >= K) {
+                            const unsigned long long bk = __ballot(mine && rank == K - 1);
+                            dk = __shfl(di, bk ? (int)__builtin_ctzll(bk) : 0, 64);  // (one lane: ranks are distinct)
+                        }
+                        done = bnd == INFINITY || dk < bnd;
+                        if (done) {
+                            if (mine && rank < K) nbr[(int64_t)self * K + rank] = ji;
+                            if (lane >= m && lane < K) nbr[(int64_t)self * K + lane] = -1;  // (fewer than K)
+                        } else if (lane == 0) {
+                            atomicAdd(&gp->why[2], 1);
+                        }
+                    } else {
+                        dk = INFINITY;  // (list over capacity: the retry walks shells)
+                        if (lane == 0) atomicAdd(&gp->why[0], 1);
+                    }
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the list is rewritten next
+                } else {
+                    dk = INFINITY;
+                    if (lane == 0) atomicAdd(&gp->why[0], 1);
+                }
+                if (!done && lane == 0) {
+                    const int at = atomicAdd(&gp->nretry, 1);
+                    retry[at] = self;
+                    retry_b[at] = dk;
+                }
+#ifdef EPP_KNN_DIAG
+                if (tl[3] == 0ull) tl[3] = __builtin_amdgcn_s_memrealtime();
+                ++nq0;
+#endif
+            }
+#ifdef EPP_KNN_DIAG
+            tl[4] = tl[5] = __builtin_amdgcn_s_memrealtime();
+            cyc0 = __builtin_amdgcn_s_memtime() - cyc0;
+#endif
+        } else {
+            // crowded halo: the block's own nodes retry from global memory
+            const bool inner = hx >= kTileH && hx < kTileH + kTileB && hy >= kTileH && hy < kTileH + kTileB &&
+                               hz >= kTileH && hz < kTileH + kTileB;
+            if (inner && cnt) {
+                const int at = atomicAdd(&gp->nretry, cnt);
+                for (int q = 0; q < cnt; ++q) {
+                    retry[at + q] = sidx[s0 + q];
+                    retry_b[at + q] = INFINITY;
+                }
+                atomicAdd(&gp->why[3], cnt);
+            }
+        }
+        __syncthreads();  // the LDS tile is rewritten by the next block
+#ifdef EPP_KNN_DIAG
+        if (dbg && threadIdx.x == 0 && b < kKnnTlBlocks) {
+            tl[6] = tl[7] = __builtin_amdgcn_s_memrealtime();
+            for (int q = 0; q < 8; ++q) dbg[16 * b + q] = tl[q];
+            dbg[16 * b + 8] = (unsigned long long)s_nq;
+            dbg[16 * b + 9] = (unsigned long long)total;
+            dbg[16 * b + 10] = blockIdx.x;
+            dbg[16 * b + 11] = nq0;
+            dbg[16 * b + 12] = cyc0;
+        }
+#endif
+    }
+}
+
 __global__ void k_knn_edges(const double* __restrict__ nodes, const int32_t* __restrict__ nbr, int64_t m,
                             int k, double* __restrict__ s1, double* __restrict__ s2) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1279,9 +1572,35 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
     // top-K in registers straight out of an LDS copy of the halo was tried: 425 us per
     // 63k-node table against k_knn_tile's 134 us -- the sorted insert then runs for nearly
     // every candidate of every lane.)
+    // one wave per retried query: EPP_KNN_RETRY_PER_CU per CU (waves without a query
+    // exit at once; more retries than waves loop)
+#ifndef EPP_KNN_RETRY_PER_CU
+#define EPP_KNN_RETRY_PER_CU 8
+#endif
     const char* tile_env = std::getenv("EPP_KNN_TILE");
-    const bool tiled = !(tile_env && *tile_env && std::atoi(tile_env) == 0);
-    if (tiled && (k == 4 || k == 8 || k == 16)) {
+    const int tile_sel = tile_env && *tile_env ? std::atoi(tile_env) : kKnnDefaultTile;
+    const bool tiled = tile_sel != 0;
+    int* const retry = cell_of;  // free once the scatter has run
+    double* const retry_b = reinterpret_cast<double*>(buf + L.rbnd);
+    // (node ids share a word with the halo x index in k_knn_wave: below 2^29)
+    if (tile_sel == 2 && (k == 4 || k == 8 || k == 16) && n < (1 << 29)) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const dim3 gw((unsigned)std::max(1, cus * 3)), bw(kWaveThreads);  // (LDS: three workgroups per CU)
+#ifdef EPP_KNN_DIAG
+        unsigned long long* d = knn_tl_buffer();
+        if (d) (void)hipMemsetAsync(d, 0, (size_t)16 * 8 * kKnnTlBlocks, s);
+#else
+        unsigned long long* d = nullptr;
+#endif
+        if (k == 4) hipLaunchKernelGGL(k_knn_wave<4>, gw, bw, 0, s, g, r2, sxyz, sidx, start, retry, retry_b, nbr, d);
+        else if (k == 8) hipLaunchKernelGGL(k_knn_wave<8>, gw, bw, 0, s, g, r2, sxyz, sidx, start, retry, retry_b, nbr, d);
+        else hipLaunchKernelGGL(k_knn_wave<16>, gw, bw, 0, s, g, r2, sxyz, sidx, start, retry, retry_b, nbr, d);
+        const dim3 gr((unsigned)std::max(1, cus * EPP_KNN_RETRY_PER_CU)), br(64);
+        if (k == 4) hipLaunchKernelGGL(k_knn_retry<4>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr);
+        else if (k == 8) hipLaunchKernelGGL(k_knn_retry<8>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr);
+        else hipLaunchKernelGGL(k_knn_retry<16>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr);
+    } else if (tiled && (k == 4 || k == 8 || k == 16)) {
         // persistent: the block count is only known on the device (grid shape)
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -1294,16 +1613,9 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
         const int mode = 1;
         unsigned long long* d = nullptr;
 #endif
-        int* retry = cell_of;  // free once the scatter has run
-        double* retry_b = reinterpret_cast<double*>(buf + L.rbnd);
         if (k == 4) hipLaunchKernelGGL(k_knn_tile<4>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr, mode, d);
         else if (k == 8) hipLaunchKernelGGL(k_knn_tile<8>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr, mode, d);
         else hipLaunchKernelGGL(k_knn_tile<16>, gt, bt, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr, mode, d);
-        // one wave per retried query: EPP_KNN_RETRY_PER_CU per CU (waves without a query
-        // exit at once; more retries than waves loop)
-#ifndef EPP_KNN_RETRY_PER_CU
-#define EPP_KNN_RETRY_PER_CU 8
-#endif
         const dim3 gr((unsigned)std::max(1, cus * EPP_KNN_RETRY_PER_CU)), br(64);
         if (k == 4) hipLaunchKernelGGL(k_knn_retry<4>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr);
         else if (k == 8) hipLaunchKernelGGL(k_knn_retry<8>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr);

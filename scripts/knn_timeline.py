@@ -47,6 +47,11 @@ def report(recs):
         v = (b[ok] - a[ok]) * 10 / 1000.0
         print(f"{nm:7s} p10 {np.percentile(v, 10):7.2f} p50 {np.percentile(v, 50):7.2f} p90 {np.percentile(v, 90):7.2f} "
               f"max {v.max():7.2f} us")
+    if (t[:, 11] > 0).any():  # k_knn_wave (EPP_KNN_TILE=2): wave 0's queries and its query-loop cycles
+        ok = t[:, 11] > 0
+        cpq = t[ok, 12] / t[ok, 11]
+        print(f"wave 0: queries p50 {np.median(t[ok, 11]):.0f}, s_memtime cycles per query p10 {np.percentile(cpq, 10):.0f} "
+              f"p50 {np.median(cpq):.0f} p90 {np.percentile(cpq, 90):.0f}")
     tot = (t[:, 7] - t[:, 0]) * 10 / 1000.0
     print(f"block   p10 {np.percentile(tot, 10):7.2f} p50 {np.percentile(tot, 50):7.2f} p90 {np.percentile(tot, 90):7.2f} "
           f"max {tot.max():7.2f} us")
@@ -70,7 +75,7 @@ def report(recs):
         print(f"launch: block starts p50 {np.median(st):.2f} max {st.max():.2f} us, ends max {en.max():.2f} us")
 
 
-modes = sys.argv[1:] or ["1"]  # EPP_KNN_TILE values (5, 6: no-insert ablations, diagnostics only)
+modes = sys.argv[1:] or ["1"]  # EPP_KNN_TILE values (2: k_knn_wave, its phases: scan, copy, first query, wave 0's rest, wait for the other waves)
 for m in modes:
     os.environ["EPP_KNN_TILE"] = m
     recs, idxs = [], []

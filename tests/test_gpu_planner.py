@@ -75,7 +75,7 @@ def test_knn_vs_bruteforce(k, method):
     assert np.array_equal(got, _knn_ref(nodes, k))
 
 
-@pytest.mark.parametrize("tile", ["1", "0"])
+@pytest.mark.parametrize("tile", ["1", "2", "0"])
 @pytest.mark.parametrize("k", [4, 8, 16, 32])
 def test_knn_grid_large(k, tile, monkeypatch):
     """Grid k-NN (used above 2048 nodes) vs the all-pairs kernel and numpy: clustered,
@@ -102,7 +102,7 @@ def test_knn_grid_large(k, tile, monkeypatch):
         assert np.array_equal(capi.knn(nodes, k, method="ws", box=box), got)
 
 
-@pytest.mark.parametrize("tile", ["1", "0"])
+@pytest.mark.parametrize("tile", ["1", "2", "0"])
 @pytest.mark.parametrize("k", [8, 16])
 def test_knn_tile_crowded_halo(k, tile, monkeypatch):
     """A cluster far denser than the grid's cell size: the tiles around it overflow their
