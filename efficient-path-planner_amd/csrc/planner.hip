@@ -118,7 +118,7 @@ struct KnnGrid {
     int ncell;
     int next;    // k_knn_tile's block queue
     int nretry;  // k_knn_tile's retry list length
-    int why[4];  // retry causes (diagnostics): list overflow, K-th beyond Dcut, shell rule, crowded
+    int why[4];  // retry causes (diagnostics): list overflow, K-th beyond Dcut, shell rule, crowded (or spilled)
 };
 
 constexpr int kBoundsThreads = 1024;
@@ -539,6 +539,7 @@ constexpr int kTileCap = 1344;          // candidates a halo may hold (else its 
 constexpr int kTileThreads = 256;
 constexpr int kTileL = 32;              // per-query list length
 constexpr int kTileNB = 16;             // histogram bins (16-bit counters, two per word)
+constexpr int kTileSpill = 32;          // queries past 128 a block sends to the retry list (see below)
 constexpr double kTileDelta = 1e-3;     // float error allowance, in h^2
 #ifndef EPP_KNN_PASS1R2  // (diagnostics A/B builds may override; exact either way)
 #define EPP_KNN_PASS1R2 4.5
@@ -660,7 +661,13 @@ __device__ __forceinline__ void knn_retry_wave(const KnnGrid& g, double r2max, c
     const int rmax = max(g.dims[0], max(g.dims[1], g.dims[2]));
     const double p[3] = {nodes[3 * (int64_t)self], nodes[3 * (int64_t)self + 1], nodes[3 * (int64_t)self + 2]};
     const int c[3] = {knn_cell_axis(p[0], g, 0), knn_cell_axis(p[1], g, 1), knn_cell_axis(p[2], g, 2)};
-    if (bound2 < 1e299) {  // wave-uniform
+    // Without a bound (a crowded or spilled tile query) a trial bound of (2h)^2 is tried
+    // first: it holds ~50 nodes at the grid's density, and the list is exact whenever it
+    // holds at least K (every node outside is farther than every listed one); else the
+    // per-lane shell walk below.
+    const bool trial = !(bound2 < 1e299);
+    const double b2 = trial ? 4.0 * g.h * g.h : bound2;
+    if (b2 < 1e299) {  // wave-uniform
         // K actual candidates lie within sqrt(bound2) (the tile pass found them, with the
         // same exact distances), so the true top K is among the candidates with
         // d <= bound2 in the box p +- sqrt(bound2) (cell mapping monotone; the radius is
@@ -675,7 +682,7 @@ __device__ __forceinline__ void knn_retry_wave(const KnnGrid& g, double r2max, c
         __shared__ int s_n;
         if (lane == 0) s_n = 0;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the clear before any append
-        const double r = sqrt(bound2) * (1.0 + 1e-9) + 1e-12 * (1.0 + fabs(p[0]) + fabs(p[1]) + fabs(p[2]));
+        const double r = sqrt(b2) * (1.0 + 1e-9) + 1e-12 * (1.0 + fabs(p[0]) + fabs(p[1]) + fabs(p[2]));
         int lo[3], hi[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
@@ -698,7 +705,7 @@ __device__ __forceinline__ void knn_retry_wave(const KnnGrid& g, double r2max, c
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
-                    if (jj[u] != self && dd[u] <= bound2 && dd[u] < r2max) {
+                    if (jj[u] != self && dd[u] <= b2 && dd[u] < r2max) {
                         const int at = atomicAdd(&s_n, 1);
                         if (at < kCap) {
                             s_d[at] = dd[u];
@@ -709,7 +716,7 @@ __device__ __forceinline__ void knn_retry_wave(const KnnGrid& g, double r2max, c
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's appends are complete
         const int cnt = s_n;
-        if (cnt <= kCap) {  // wave-uniform
+        if (cnt <= kCap && (!trial || cnt >= K)) {  // wave-uniform
             for (int i = lane; i < cnt; i += 64) {
                 const double di = s_d[i];
                 const int ji = s_j[i];
@@ -959,12 +966,24 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
             EPP_KTL(2);
             // 3. queries, lpq adjacent lanes per query
 #ifdef EPP_KNN_DIAG
-            const int nq = mode == 4 ? 0 : s_nq;  // mode 4: timing ablation (inexact; diagnostics builds only)
+            const int nq_all = mode == 4 ? 0 : s_nq;  // mode 4: timing ablation (inexact; diagnostics builds only)
 #else
-            const int nq = s_nq;
+            const int nq_all = s_nq;
 #endif
-            // block-uniform; one lane per query only above 128 queries (a second round of
-            // queries would cost the block ~45 us: the kernel's slowest blocks)
+            // block-uniform; one lane per query only above 128 + kTileSpill queries (a second
+            // round of queries would cost the block ~45 us).  A block just past 128 queries
+            // keeps two lanes per query for its first 128 and sends the rest to the retry list
+            // (one wave each in k_knn_retry, in parallel): with one lane per query such a
+            // block was the launch's slowest (~104 us against ~85 for the next).
+            const bool spill = nq_all > kTileThreads / 2 && nq_all <= kTileThreads / 2 + kTileSpill;
+            const int nq = spill ? kTileThreads / 2 : nq_all;
+            if (spill)
+                for (int q = nq + (int)threadIdx.x; q < nq_all; q += kTileThreads) {
+                    const int at = atomicAdd(&gp->nretry, 1);
+                    retry[at] = sidx[EPP_SPOS(qh[q])];
+                    retry_b[at] = INFINITY;
+                    atomicAdd(&gp->why[3], 1);
+                }
             const int lpq = nq <= kTileThreads / 4 ? 4 : nq <= kTileThreads / 2 ? 2 : 1;
             const int slot = threadIdx.x / lpq, sub = threadIdx.x % lpq;
             // (a query's lpq lanes are adjacent lanes of one wave: its histogram needs no

@@ -115,6 +115,32 @@ def test_knn_tile_crowded_halo(k, tile, monkeypatch):
     assert np.array_equal(got, capi.knn(nodes, k, method="brute"))
 
 
+@pytest.mark.parametrize("tile", ["1", "2"])
+def test_knn_tile_spilled_block(tile, monkeypatch):
+    """One 4^3-cell block holds 129..160 nodes: k_knn_tile keeps two lanes per query for its
+    first 128 and sends the rest to the retry list (k_knn_wave has no such limit); the
+    table equals the all-pairs one.  The grid is replicated here (knn_grid_shape: ~1.5
+    nodes per cell over the nodes' bounding box) to place the extra nodes in one block."""
+    monkeypatch.setenv("EPP_KNN_TILE", tile)
+    rs = np.random.RandomState(11)
+    n0 = 20000
+    nodes = rs.uniform(0.0, 8.0, (n0, 3))
+    nodes[0], nodes[1] = [0.0, 0.0, 0.0], [8.0, 8.0, 8.0]  # the bounding box
+    h = np.cbrt(1.5 * 512.0 / (n0 + 64))
+    lo, hi = 4 * h, 8 * h  # block (1, 1, 1) of 4 cells per axis
+    inside = lambda p: np.all((p >= lo) & (p < hi), axis=1)
+    extra = 140 - int(inside(nodes).sum())
+    assert 0 < extra <= 64
+    pad = rs.uniform(lo + 1e-3, hi - 1e-3, (64, 3))
+    pad[extra:] = rs.uniform(0.0, 8.0, (64 - extra, 3))  # (the rest anywhere outside)
+    pad[extra:][inside(pad[extra:])] += 8.0 * h
+    pad = np.minimum(pad, 8.0)
+    nodes = np.concatenate([nodes, pad])
+    assert 128 < int(inside(nodes).sum()) <= 160
+    got = capi.knn(nodes, 16, method="grid")
+    assert np.array_equal(got, capi.knn(nodes, 16, method="brute"))
+
+
 def test_knn_grid_many_scan_blocks():
     """300k nodes: the cell-count scan spans ~70 look-back blocks (more than one 64-block
     window); the grid table equals the all-pairs one."""
