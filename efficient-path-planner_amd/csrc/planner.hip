@@ -528,7 +528,10 @@ __global__ __launch_bounds__(256) void k_knn_grid(const KnnGrid* __restrict__ gp
 // workgroups, so a second half only starts once a workgroup is free -- it lengthened the
 // launch, 99 -> 110 us in the isolated trace.  A per-lane register histogram in pass 1
 // instead of the LDS atomics was tried too; its build faulted in the crowded-cluster test
-// and was withdrawn.)
+// and was withdrawn.  So was a first pass-1 stage over the 3^3 cells around the query: its
+// cut alone is a valid but looser bound (exact phase 22 -> 29 us p50), and completing the
+// bins below it from the rest of the cube takes two walks where one did (pass 1 19.8 ->
+// 24.2 us p50; blocks at the grid's edges, where the 3^3 cells hold fewer than K, 42-50).)
 #ifdef EPP_KNN_DIAG
 constexpr int kKnnTlBlocks = 65536;  // timeline records
 #endif
@@ -1133,6 +1136,10 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                     // suffices (stopping rule after shell kTileH)
                     const bool in_range = bd[K - 1] <= dcut;
                     ok = in_range && knn_done<K>(g, c, p, kTileH, bd);
+#ifdef EPP_KNN_DIAG
+                    if (mode == 5 || mode == 6) ok = true;  // (ablation: no retries, no answer)
+                    else
+#endif
                     if (ok) knn_store<K>(nbr, self, bi);
                     else atomicAdd(&gp->why[in_range ? 2 : 1], 1);
                     // a retry's search bound: K actual candidates within bd[K-1] (<= r2max)
