@@ -829,7 +829,11 @@ __device__ __forceinline__ void knn_retry_wave(const KnnGrid& g, double r2max, c
 }
 
 // (An LDS copy of the halo's exact coordinates for the exact phase was tried: with it two
-// workgroups fit per CU instead of three, and the kernel was slower.)
+// workgroups fit per CU instead of three, and the kernel was slower.  So was an exact phase
+// with one wavefront per query -- its candidates one per lane, ranks counted by v_readlane,
+// 145 -> 114 VGPRs: each query then waits out its own gathers one after another, ~3 us per
+// query and wave against ~22 us for all of a block's queries at once on one thread each;
+// 126 -> 185 us per table.)
 template <int K>
 __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restrict__ gp, double r2max,
                                                            const double* __restrict__ nodes,
