@@ -833,7 +833,8 @@ __device__ __forceinline__ void knn_retry_wave(const KnnGrid& g, double r2max, c
 // with one wavefront per query -- its candidates one per lane, ranks counted by v_readlane,
 // 145 -> 114 VGPRs: each query then waits out its own gathers one after another, ~3 us per
 // query and wave against ~22 us for all of a block's queries at once on one thread each;
-// 126 -> 185 us per table.)
+// 126 -> 185 us per table.  And four workgroups per CU (halo cap 992, 24-entry lane lists,
+// 128 VGPRs with 5 spilled): 126 -> 142 us per table.)
 template <int K>
 __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restrict__ gp, double r2max,
                                                            const double* __restrict__ nodes,
