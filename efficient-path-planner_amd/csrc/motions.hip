@@ -439,7 +439,8 @@ __global__ __launch_bounds__(BLOCK) void k_motions_d32b(const WorldView* __restr
 // those tiles is kept only in the first one along each axis (FX / FY rows), with
 // can_pass_gate the filling OBBs are masked out (:150-153).  The (edge, OBB) pairs go to
 // the wave's queue at offsets from a wave scan of the lanes' popcounts and are tested 64
-// at a time, after an exact AABB prefilter in doubles (the rtree's closed overlap):
+// at a time behind an exact AABB prefilter in doubles (the rtree's closed overlap; for
+// MODE 0 in the queued test, for MODE 1 before queueing):
 //   MODE 0  OBB::checkCollisionWithRay (src/OBB.cpp:10-61);
 //   MODE 1  the points s + (e - s) k/32, k = 1..32 (d32_pair_hit: only the k an interval
 //           bound admits are evaluated exactly).  The slab range and the prefilter box are
@@ -457,6 +458,16 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
                                                      uint32_t rec_bytes, uint32_t tile_bytes) {
     constexpr int BLOCK = 1024;
     constexpr int STRIDE = slab_row_stride(W);
+    // PF: the exact AABB prefilter in the queued test instead of the candidate rounds --
+    // the analytic mode (a candidate round then costs a bit-pick and an append; the queued
+    // ray test pays the 6 compares with every lane busy): 29.2-29.9 -> 28.7-29.2 us at C3.
+    // Discrete32 keeps it in the rounds: there the 12 % more queued pairs reach the heavier
+    // d32 test (35.9 -> 38.7 us with it in the queue).
+#if defined(EPP_MOTIONS_PF_FLUSH)
+    constexpr bool PF = true;  // (A/B: both modes)
+#else
+    constexpr bool PF = MODE == 0;
+#endif
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     EPP_MTL_DECL;
     {
@@ -558,21 +569,19 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
                 if (has) {
                     const double* rec = recs + (size_t)(q >> 6) * kRecDoubles;
                     bool hit;
-#ifdef EPP_MOTIONS_PF_FLUSH
-                    // the exact AABB prefilter here, on the owner's box (closed, as the rtree
-                    // query; MODE 1 widened by a hair), instead of in the candidate rounds
-                    bool keep = true;
+                    bool keep = true;  // (PF false: tested before queueing)
+                    if constexpr (PF) {
+                        // the exact AABB prefilter here, on the owner's box (closed, as the
+                        // rtree query; MODE 1 widened by a hair), instead of in the rounds
 #pragma unroll
-                    for (int k = 0; k < 3; ++k) {
-                        const double l = (pe[k] < ps[k]) ? pe[k] : ps[k], h = (ps[k] < pe[k]) ? pe[k] : ps[k];
-                        const double bl = MODE == 1 ? l - (1e-9 + 1e-12 * fabs(l)) : l;
-                        const double bh = MODE == 1 ? h + (1e-9 + 1e-12 * fabs(h)) : h;
-                        keep = keep & !((rec[F_HIX + k] < bl) | (bh < rec[F_LOX + k]));
+                        for (int k = 0; k < 3; ++k) {
+                            const double l = (pe[k] < ps[k]) ? pe[k] : ps[k], h = (ps[k] < pe[k]) ? pe[k] : ps[k];
+                            const double bl = MODE == 1 ? l - (1e-9 + 1e-12 * fabs(l)) : l;
+                            const double bh = MODE == 1 ? h + (1e-9 + 1e-12 * fabs(h)) : h;
+                            keep = keep & !((rec[F_HIX + k] < bl) | (bh < rec[F_LOX + k]));
+                        }
                     }
-#else
-                    constexpr bool keep = true;  // (tested before queueing)
-#endif
-                    if (MODE == 0) {  // (the AABB overlap was tested before queueing)
+                    if (MODE == 0) {  // (the AABB overlap: `keep`, tested above)
                         const uint32_t m = (uint32_t)__double_as_longlong(rec[R_META]);
                         hit = keep && rec_ray_hit(rec, ps, pe, (m & META_GATE) ? rg : ro);
                     } else {
@@ -657,17 +666,17 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
                     }
                     has = has || take;
                 }
-#ifdef EPP_MOTIONS_PF_FLUSH
-                const unsigned long long hb = __builtin_amdgcn_ballot_w64(has);
-                if (!hb) break;
-                if (has) {
-                    const uint16_t* tid = wsel < (uint32_t)W ? ida : idb;
-                    queue[qn + lanes_below(hb)] = (uint32_t)tid[32 * (wsel % (uint32_t)W) + bit] << 6 | (uint32_t)lane;
+                if constexpr (PF) {  // every candidate queued; the prefilter runs in the flush
+                    const unsigned long long hb = __builtin_amdgcn_ballot_w64(has);
+                    if (!hb) break;
+                    if (has) {
+                        const uint16_t* tid = wsel < (uint32_t)W ? ida : idb;
+                        queue[qn + lanes_below(hb)] = (uint32_t)tid[32 * (wsel % (uint32_t)W) + bit] << 6 | (uint32_t)lane;
+                    }
+                    qn += (uint32_t)__popcll(hb);
+                    if (qn > (uint32_t)(kQueueV5 - 64)) flush();
+                    continue;
                 }
-                qn += (uint32_t)__popcll(hb);
-                if (qn > (uint32_t)(kQueueV5 - 64)) flush();
-                continue;
-#endif
                 if (!__builtin_amdgcn_ballot_w64(has)) break;
                 uint32_t id = 0;
                 bool keep = false;
