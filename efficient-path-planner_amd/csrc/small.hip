@@ -131,7 +131,7 @@ epp_status launch_states_small(const SmallWorld& sw, bool mindist, const double*
 
 epp_status launch_motions_small(const SmallWorld& sw, int32_t mode, const double* s1, const double* s2, int64_t n,
                                 int32_t can_pass, uint8_t* valid, hipStream_t st, uint32_t* done, uint32_t seq) {
-    const int per = small_per(n), grid = (int)((n + per - 1) / per);
+    const int per = small_per_motions(n), grid = (int)((n + per - 1) / per);
     const size_t shm = small_shm(sw.n_obb);
     if (mode == 0)
         hipLaunchKernelGGL((k_motions_small<0>), dim3(grid), dim3(kSmallBlock), shm, st, sw.recs, sw.n_obb, sw.r_gate,
@@ -152,7 +152,9 @@ struct DoneSlots {
         if (p) (void)hipHostFree(p);
     }
 };
-constexpr int kMaxSmallGroups = (int)(kSmallStates / kSmallBlock);
+constexpr int kMaxSmallGroups = (int)std::max<int64_t>(kSmallStates / kSmallBlock, kSmallMotions / 16);
+static_assert(kSmallStates / kSmallBlock <= kMaxSmallGroups && kSmallMotions / 16 <= kMaxSmallGroups,
+              "completion slots for the small workgroups");
 
 // Polls the slots until every workgroup has published `seq`; a stream that completes or
 // fails without them ends the wait through hipStreamQuery (checked every ~1k polls).
@@ -179,7 +181,7 @@ epp_status wait_done(const uint32_t* done, int groups, uint32_t seq, hipStream_t
 }
 
 template <typename Launch>
-epp_status run_sync(int64_t n, hipStream_t st, const char* what, Launch&& launch) {
+epp_status run_sync(int64_t n, int per, hipStream_t st, const char* what, Launch&& launch) {
     thread_local DoneSlots ds;
     if (!ds.p && hipHostMalloc(reinterpret_cast<void**>(&ds.p), kMaxSmallGroups * sizeof(uint32_t),
                                hipHostMallocDefault) != hipSuccess) {
@@ -188,7 +190,7 @@ epp_status run_sync(int64_t n, hipStream_t st, const char* what, Launch&& launch
         return EPP_ERR_HIP;
     }
     const uint32_t seq = ++ds.seq;
-    const int groups = (int)((n + small_per(n) - 1) / small_per(n));
+    const int groups = (int)((n + per - 1) / per);
     if (const epp_status rc = launch(ds.p, seq)) return rc;
     return wait_done(ds.p, groups, seq, st, what);
 }
@@ -199,7 +201,7 @@ epp_status states_small_sync(const epp_world* world, bool mindist, const double*
     const SmallWorld sw = small_world(world);
     *handled = n > 0 && small_states(sw, n);
     if (!*handled) return EPP_OK;
-    return run_sync(n, st, mindist ? "checkPointsMinDistance" : "checkPoints", [&](uint32_t* done, uint32_t seq) {
+    return run_sync(n, small_per(n), st, mindist ? "checkPointsMinDistance" : "checkPoints", [&](uint32_t* done, uint32_t seq) {
         return launch_states_small(sw, mindist, xyz, n, can_pass, md, valid, nullptr, nullptr, st, done, seq);
     });
 }
@@ -209,7 +211,7 @@ epp_status motions_small_sync(const epp_world* world, int32_t mode, const double
     const SmallWorld sw = small_world(world);
     *handled = n > 0 && small_motions(sw, n);
     if (!*handled) return EPP_OK;
-    return run_sync(n, st, "checkRays", [&](uint32_t* done, uint32_t seq) {
+    return run_sync(n, small_per_motions(n), st, "checkRays", [&](uint32_t* done, uint32_t seq) {
         return launch_motions_small(sw, mode, s1, s2, n, can_pass, valid, st, done, seq);
     });
 }

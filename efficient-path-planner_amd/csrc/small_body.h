@@ -50,6 +50,10 @@ __device__ __forceinline__ void stage_records(double* srec, const double* recs, 
 // latency-path call keep every wave of the workgroup busy, and each wave walks a shorter
 // list.  A slice's hit marks the query's LDS flag; slice 0 writes the answers.
 __host__ __device__ inline int small_per(int64_t n) { return n <= 64 ? 64 : (n <= 128 ? 128 : kSmallBlock); }
+// Motions: a motion test costs ~10x a point test and the planner's shortcut batch (every
+// vertex pair of a path, long edges) overlaps many OBBs, so the OBB loop is split finer:
+// 16 edges per workgroup, 16 slices of the OBBs (<= 64 workgroups for kSmallMotions edges).
+__host__ __device__ inline int small_per_motions(int64_t) { return 16; }
 __host__ __device__ inline size_t small_shm(int n_obb) { return (((size_t)n_obb * kRecDoubles + 1) & ~size_t(1)) * 8 + kSmallBlock * 4; }
 
 // The body of k_states_small for logical workgroup `blk` (its queries [blk per, (blk+1)
