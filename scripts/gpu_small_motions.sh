@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 stop_on_fault() { case "$1" in 0) return 0 ;; *) echo "step $2 ended with $1: stopping"; exit "$1" ;; esac; }
-timeout -k 10 600 python -u -m pytest tests/test_gpu_collision.py tests/test_gpu_planner.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_sm.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest ${PYTEST_FILES:-tests/test_gpu_collision.py tests/test_gpu_planner.py} -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_sm.log 2>&1; rc=$?
 tail -3 gpurun_out/pytest_sm.log; stop_on_fault $rc pytest
 rm -rf gpurun_out/prof_plan
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_plan -o run -- python3 scripts/planner_isolated.py > gpurun_out/prof_plan.json 2> gpurun_out/prof_plan.err; rc=$?
