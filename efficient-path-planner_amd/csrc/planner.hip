@@ -534,6 +534,8 @@ __global__ __launch_bounds__(256) void k_knn_grid(const KnnGrid* __restrict__ gp
 // 24.2 us p50; blocks at the grid's edges, where the 3^3 cells hold fewer than K, 42-50).)
 #ifdef EPP_KNN_DIAG
 constexpr int kKnnTlBlocks = 65536;  // timeline records
+constexpr int kKnnRetryTl = 4096;    // retried queries recorded (k_knn_retry)
+__device__ unsigned long long g_knn_retry_tl[kKnnRetryTl][4];
 #endif
 constexpr int kTileB = 4, kTileH = 2, kTileE = kTileB + 2 * kTileH, kTileCells = kTileE * kTileE * kTileE;
 constexpr int kTileW = 2 * kTileH + 1;  // cube edge around the query's cell
@@ -664,12 +666,13 @@ __device__ __forceinline__ void knn_retry_wave(const KnnGrid& g, double r2max, c
     const int rmax = max(g.dims[0], max(g.dims[1], g.dims[2]));
     const double p[3] = {nodes[3 * (int64_t)self], nodes[3 * (int64_t)self + 1], nodes[3 * (int64_t)self + 2]};
     const int c[3] = {knn_cell_axis(p[0], g, 0), knn_cell_axis(p[1], g, 1), knn_cell_axis(p[2], g, 2)};
-    // Without a bound (a crowded or spilled tile query) a trial bound of (2h)^2 is tried
-    // first: it holds ~50 nodes at the grid's density, and the list is exact whenever it
-    // holds at least K (every node outside is farther than every listed one); else the
-    // per-lane shell walk below.
+    // Without a bound (a crowded or spilled tile query) a trial bound of (1.6h)^2 is tried
+    // first: it holds ~26 nodes at the grid's density (~35 in the dense blocks that spill),
+    // and the list is exact whenever it holds at least K (every node outside is farther
+    // than every listed one); else the per-lane shell walk below.  ((2h)^2 held ~70 nodes
+    // in a spilling block: those retries took 7-16 us against 4.7 for the bounded ones.)
     const bool trial = !(bound2 < 1e299);
-    const double b2 = trial ? 4.0 * g.h * g.h : bound2;
+    const double b2 = trial ? 2.56 * g.h * g.h : bound2;
     if (b2 < 1e299) {  // wave-uniform
         // K actual candidates lie within sqrt(bound2) (the tile pass found them, with the
         // same exact distances), so the true top K is among the candidates with
@@ -719,6 +722,22 @@ __device__ __forceinline__ void knn_retry_wave(const KnnGrid& g, double r2max, c
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's appends are complete
         const int cnt = s_n;
+        if (cnt <= 64 && (!trial || cnt >= K)) {  // wave-uniform: entry i on lane i
+            // ranks against the other entries read by v_readlane (no LDS round trip per
+            // entry, which the loop below waits out)
+            const bool mine = lane < cnt;
+            const double di = mine ? s_d[lane] : 0.0;
+            const int ji = mine ? s_j[lane] : 0;
+            const int dlo = __double2loint(di), dhi = __double2hiint(di);
+            int rank = 0;
+            for (int f = 0; f < cnt; ++f) {
+                const double df = __hiloint2double(__builtin_amdgcn_readlane(dhi, f), __builtin_amdgcn_readlane(dlo, f));
+                rank += ((df < di) | ((df == di) & (__builtin_amdgcn_readlane(ji, f) < ji))) ? 1 : 0;
+            }
+            if (mine && rank < K) nbr[(int64_t)self * K + rank] = ji;
+            if (lane >= cnt && lane < K) nbr[(int64_t)self * K + lane] = -1;  // (fewer than K)
+            return;
+        }
         if (cnt <= kCap && (!trial || cnt >= K)) {  // wave-uniform
             for (int i = lane; i < cnt; i += 64) {
                 const double di = s_d[i];
@@ -1208,8 +1227,21 @@ __global__ __launch_bounds__(64) void k_knn_retry(const KnnGrid* __restrict__ gp
                                                    int32_t* __restrict__ nbr) {
     const KnnGrid g = *gp;
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwaves = (gridDim.x * blockDim.x) >> 6;
-    for (int i = wave; i < g.nretry; i += nwaves)  // wave-uniform
+    for (int i = wave; i < g.nretry; i += nwaves) {  // wave-uniform
+#ifdef EPP_KNN_DIAG
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+#endif
         knn_retry_wave<K>(g, r2max, nodes, sxyz, sidx, start, retry[i], retry_b[i], nbr);
+#ifdef EPP_KNN_DIAG
+        // (diagnostics builds) per retried query: start, end (10 ns ticks), bound, node
+        if ((threadIdx.x & 63) == 0 && i < kKnnRetryTl) {
+            g_knn_retry_tl[i][0] = t0;
+            g_knn_retry_tl[i][1] = __builtin_amdgcn_s_memrealtime();
+            g_knn_retry_tl[i][2] = (unsigned long long)__double_as_longlong(retry_b[i]);
+            g_knn_retry_tl[i][3] = (unsigned long long)retry[i];
+        }
+#endif
+    }
 }
 
 // ---- wave-per-query grid k-NN (k_knn_wave) ---------------------------------------------
@@ -1840,6 +1872,12 @@ epp_status epp_dbg_knn_tl(unsigned long long* out, int64_t blocks) {
     unsigned long long* d = knn_tl_buffer();
     if (!d || blocks > kKnnTlBlocks) return EPP_ERR_RUNTIME;
     return hipMemcpy(out, d, (size_t)blocks * 16 * 8, hipMemcpyDeviceToHost) == hipSuccess ? EPP_OK : EPP_ERR_HIP;
+}
+// (diagnostics builds only) the last k_knn_retry launch: per retried query start, end,
+// bound (f64 bits), node -- 4 u64 each
+epp_status epp_dbg_knn_retry_tl(unsigned long long* out, int64_t n) {
+    if (n > kKnnRetryTl) n = kKnnRetryTl;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_knn_retry_tl), (size_t)n * 32) == hipSuccess ? EPP_OK : EPP_ERR_HIP;
 }
 #endif
 

@@ -90,3 +90,20 @@ for m in modes:
             idxs.append(np.nonzero(keep)[0])
     print(f"== EPP_KNN_TILE={m}")
     report(recs)
+    # the last launch's retried queries (k_knn_retry): duration, start/end from the first
+    # retry's start, bound in h^2
+    hdr = d_ws.download(np.uint8, 80)
+    nretry = int(hdr[60:64].view(np.int32)[0])
+    hh = float(hdr[24:32].view(np.float64)[0])
+    if nretry > 0 and hasattr(L, "epp_dbg_knn_retry_tl"):
+        L.epp_dbg_knn_retry_tl.argtypes = [C.c_void_p, C.c_int64]
+        rt = np.zeros((min(nretry, 4096), 4), np.uint64)
+        capi.check(L.epp_dbg_knn_retry_tl(rt.ctypes.data, len(rt)))
+        t0 = rt[:, 0].astype(np.int64)
+        dur = (rt[:, 1].astype(np.int64) - t0) * 10 / 1000.0
+        st = (t0 - t0.min()) * 10 / 1000.0
+        b2 = rt[:, 2].view(np.float64) / (hh * hh)
+        print(f"retry: {nretry} queries, duration p50 {np.median(dur):.2f} p90 {np.percentile(dur, 90):.2f} max {dur.max():.2f} us, "
+              f"starts span {st.max():.2f} us, last end {(st + dur).max():.2f} us")
+        for i in np.argsort(dur)[::-1][:6]:
+            print(f"  retry node {int(rt[i, 3])}: {dur[i]:.2f} us from {st[i]:.2f}, bound {b2[i]:.2f} h^2")
