@@ -1629,9 +1629,10 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
     hipLaunchKernelGGL(k_knn_scan, dim3(L.scan_blocks), dim3(kScanThreads), 0, s, g, cnt, start,
                        reinterpret_cast<unsigned long long*>(buf + L.stat), next_scan_tag());
     hipLaunchKernelGGL(k_knn_scatter, g256, b256, 0, s, nodes, n, cell_of, start, fill, sxyz, sidx);
-    // EPP_KNN_TILE=0 selects the untiled grid walk (same answer; a test hook); the product
-    // accepts only {0, 1}.  The timing ablations and the per-block dump exist only in a
-    // -DEPP_KNN_DIAG diagnostics build.  (A one-query-per-lane variant that keeps the exact
+    // EPP_KNN_TILE=0 selects the untiled grid walk, 2 the wave-per-query k_knn_wave (same
+    // answers; test hooks); the default is k_knn_tile.  The timing ablations and the
+    // per-block dump exist only in a -DEPP_KNN_DIAG diagnostics build.  (A one-query-per-
+    // lane variant that keeps the exact
     // top-K in registers straight out of an LDS copy of the halo was tried: 425 us per
     // 63k-node table against k_knn_tile's 134 us -- the sorted insert then runs for nearly
     // every candidate of every lane.)
