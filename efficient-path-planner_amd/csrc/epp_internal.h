@@ -73,6 +73,20 @@ struct FusedCheck {
 epp_status check_and_generate_into(const FusedCheck* chk, const double* wp, int32_t n_wp, const double* times,
                                    double v_max, double a_max, double dt, double t0, const double v0[3],
                                    const double a0[3], double* (*alloc)(void*, int64_t), void* ctx, int64_t* n_rows);
+// The planner's edge mask folded into the k-NN-table motion check (k_motions_v5, IDX):
+// failed entries of nbr_w -> -1, out16 (optional) the masked table as u16, count[0] / [1]
+// += kept edges / kept edges into node `target`.  count == nullptr: no mask.
+struct MotionMask {
+    int32_t* nbr_w = nullptr;
+    uint16_t* out16 = nullptr;
+    int32_t target = -1;
+    unsigned long long* count = nullptr;
+};
+// epp_check_knn_motions (mode 0) with the mask above; EPP_ERR_UNSUPPORTED as it (the
+// caller then masks with mask_edges_count_acc).
+epp_status check_knn_motions_masked(const epp_world* world, const double* nodes, int32_t* nbr, int32_t n, int32_t k,
+                                    int32_t can_pass_gate, uint8_t* valid, uint16_t* out16, int32_t target,
+                                    int64_t* count, void* stream);
 // epp_mask_edges_count without clearing `count` first: the counts are added to what it
 // holds (the planner clears them with its first upload).  out16 != NULL: also a copy of
 // the masked table as u16, 0xFFFF for no edge (node counts <= 65535).

@@ -181,21 +181,22 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     const double bhi[3] = {std::max({hi[0], start.x, goal.x}), std::max({hi[1], start.y, goal.y}),
                            std::max({hi[2], start.z, goal.z})};
     check(epp_knn_ws_box(d_nodes, n, k, 0.0, blo, bhi, d_nbr, d_ws, ws_bytes, st), "knn");
-    // motion checks straight off the k-NN table; small batches / worlds without tile tables
-    // through materialised endpoints
-    const epp_status ks = epp_check_knn_motions(w, d_nodes, d_nbr, n, k, canPass ? 1 : 0, 0, d_ev, st);
+    // Motion checks straight off the k-NN table, with the mask folded in: failed motions ->
+    // -1, the valid edges and those into the goal (node 1) counted (counters zeroed above).
+    // Up to 65535 nodes the table goes down as u16 (0xFFFF: no edge), half the bytes of the
+    // largest download, written into d_e1 (free on this path).  Small batches / worlds
+    // without tile tables: materialised endpoints, then the mask kernel.
+    const bool narrow = n <= 65535;
+    uint16_t* d_nbr16 = narrow ? reinterpret_cast<uint16_t*>(d_e1) : nullptr;
+    const epp_status ks =
+        check_knn_motions_masked(w, d_nodes, d_nbr, n, k, canPass ? 1 : 0, d_ev, d_nbr16, 1, d_ecnt, st);
     if (ks == EPP_ERR_UNSUPPORTED) {
         check(epp_knn_edges(d_nodes, d_nbr, n, k, d_e1, d_e2, st), "edges");
         check(epp_check_motions(w, d_e1, d_e2, (int64_t)m, canPass ? 1 : 0, 0, d_ev, st), "motion check");
+        check(mask_edges_count_acc(d_nbr, d_ev, (int64_t)m, 1, d_ecnt, st, d_nbr16), "mask edges");
     } else {
         check(ks, "motion check");
     }
-    // failed motions -> -1; the valid edges, and those into the goal (node 1)
-    // Up to 65535 nodes the table goes down as u16 (0xFFFF: no edge), half the bytes of the
-    // largest download; its copy is written by the mask kernel into d_e1, free by then.
-    const bool narrow = n <= 65535;
-    uint16_t* d_nbr16 = narrow ? reinterpret_cast<uint16_t*>(d_e1) : nullptr;
-    check(mask_edges_count_acc(d_nbr, d_ev, (int64_t)m, 1, d_ecnt, st, d_nbr16), "mask edges");  // (counters zeroed above)
     // the masked k-NN table into pinned host staging (sized as the nodes' staging)
     void* h_tab = ts.pinned(1, m_max * 4);
     const int32_t* nbr32 = static_cast<const int32_t*>(h_tab);

@@ -451,11 +451,16 @@ constexpr int kQueueV5 = 256;
 // IDX: the edges are given as a k-NN table instead of endpoint arrays — edge e runs from
 // node e / kk to node nbr[e] (s1 = the nodes; a missing neighbour, -1, is the degenerate
 // edge from the node to itself), as epp_knn_edges would lay them out.
+//
+// MotionMask (IDX, count != nullptr): the planner's edge mask folded in -- a failed motion's
+// table entry becomes -1, out16 (if given) receives the masked table as u16 (0xFFFF: no
+// edge), and count[0] / count[1] gain the kept edges / those into node `target` (one atomic
+// per workgroup), as k_mask_edges_count (planner.hip) would after the launch.
 template <int W, int MODE, bool IDX>
 __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict__ wv, const double* __restrict__ s1,
                                                      const double* __restrict__ s2, const int32_t* __restrict__ nbr,
                                                      int kk, int64_t n, int can_pass, uint8_t* __restrict__ valid,
-                                                     uint32_t rec_bytes, uint32_t tile_bytes) {
+                                                     uint32_t rec_bytes, uint32_t tile_bytes, MotionMask mm) {
     constexpr int BLOCK = 1024;
     constexpr int STRIDE = slab_row_stride(W);
     // PF: the exact AABB prefilter in the queued test instead of the candidate rounds --
@@ -509,14 +514,17 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
     tl_c = __builtin_readcyclecounter() - tl_t0;  // staging
 #endif
     const int64_t stride = (int64_t)gridDim.x * BLOCK;
+    uint32_t mk_keep = 0, mk_tgt = 0;  // (MotionMask counts)
     for (int64_t i0 = (int64_t)blockIdx.x * BLOCK + wave * 64; i0 < n; i0 += stride) {
         const int64_t i = i0 + lane;
         const bool act = i < n;
         double s[3] = {0.0, 0.0, 0.0}, e[3] = {0.0, 0.0, 0.0};
+        int32_t jraw = -1;  // (IDX: the table entry)
         if (act) {
             if (IDX) {
                 const int64_t u = i / kk;
                 const int32_t j = nbr[i];
+                jraw = j;
                 const int64_t v = j < 0 ? u : (int64_t)j;
 #pragma unroll
                 for (int k = 0; k < 3; ++k) {
@@ -698,7 +706,31 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
         EPP_MTL_ADD(tl_walk, tl_b);
         flush();
         if (act) valid[i] = flags[lane];
+        if (IDX && mm.count) {  // (launch-uniform)
+            const bool keep = act && flags[lane] != 0 && jraw >= 0;
+            if (act && flags[lane] == 0) mm.nbr_w[i] = -1;
+            if (act && mm.out16) mm.out16[i] = keep ? (uint16_t)jraw : (uint16_t)0xFFFF;
+            mk_keep += keep ? 1u : 0u;
+            mk_tgt += (keep && jraw == mm.target) ? 1u : 0u;
+        }
         wave_lds_sync();
+    }
+    if (IDX && mm.count) {  // one atomic per workgroup and counter
+        __shared__ uint32_t mk_part[2][BLOCK / 64];
+        for (int o = 32; o > 0; o >>= 1) {
+            mk_keep += (uint32_t)__shfl_xor((int)mk_keep, o, 64);
+            mk_tgt += (uint32_t)__shfl_xor((int)mk_tgt, o, 64);
+        }
+        if (lane == 0) {
+            mk_part[0][wave] = mk_keep;
+            mk_part[1][wave] = mk_tgt;
+        }
+        __syncthreads();
+        if (threadIdx.x < 2) {
+            uint32_t t = 0;
+            for (int w = 0; w < BLOCK / 64; ++w) t += mk_part[threadIdx.x][w];
+            if (t) atomicAdd(mm.count + threadIdx.x, (unsigned long long)t);
+        }
     }
     EPP_MTL_END;
 }
@@ -713,7 +745,7 @@ namespace {
 // fit the LDS budget; returns false (nothing launched) otherwise.
 bool launch_motions_v5(const WorldView* dw, const WorldView& w, const double* s1, const double* s2,
                        const int32_t* nbr, int kk, int64_t n, int32_t can_pass_gate, int32_t mode, uint8_t* valid,
-                       hipStream_t st) {
+                       hipStream_t st, const MotionMask& mm = MotionMask{}) {
     if (w.slab_n <= 0) return false;
     const uint32_t recb5 = (uint32_t)(((size_t)w.n_obb * kRecDoubles * 8 + 15) & ~size_t(15));
     const uint32_t tileb = (uint32_t)((size_t)w.tile_n * w.tile_n * w.tile_words * 4);
@@ -725,7 +757,7 @@ bool launch_motions_v5(const WorldView* dw, const WorldView& w, const double* s1
     do {                                                                                                          \
         allow_lds(k_motions_v5<WW, MM, II>);                                                                      \
         hipLaunchKernelGGL((k_motions_v5<WW, MM, II>), dim3(grid), dim3(1024), shm5, st, dw, s1, s2, nbr, kk, n, \
-                           can_pass_gate, valid, recb5, tileb);                                                   \
+                           can_pass_gate, valid, recb5, tileb, mm);                                               \
     } while (0)
 #define EPP_LAUNCH_M5W(MM, II)                       \
     switch (w.slab_w) {                              \
@@ -854,6 +886,40 @@ epp_status epp_check_knn_motions(const epp_world* world, const double* nodes, co
     }
     return launch_error("epp_check_knn_motions");
 }
+
+}  // extern "C"
+
+epp_status epp::check_knn_motions_masked(const epp_world* world, const double* nodes, int32_t* nbr, int32_t n,
+                                         int32_t k, int32_t can_pass_gate, uint8_t* valid, uint16_t* out16,
+                                         int32_t target, int64_t* count, void* stream) {
+    if (!world || n < 0 || k <= 0 || (n > 0 && (!nodes || !nbr || !valid || !count))) {
+        set_error("check_knn_motions_masked: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    const int64_t m = (int64_t)n * k;
+    if (m == 0) return EPP_OK;
+    SmallWorld sw = small_world(world);
+    if (small_motions(sw, m) || std::getenv("EPP_MOTIONS_KERNEL")) {
+        set_error("check_knn_motions_masked: not for this batch / world");
+        return EPP_ERR_UNSUPPORTED;
+    }
+    sw.lease = {};
+    IndexLease ix;
+    if (const epp_status st = ensure_index(world, &ix)) return st;
+    MotionMask mm;
+    mm.nbr_w = nbr;
+    mm.out16 = out16;
+    mm.target = target;
+    mm.count = reinterpret_cast<unsigned long long*>(count);
+    if (!launch_motions_v5(ix.dview, ix.view, nodes, nullptr, nbr, k, m, can_pass_gate, 0, valid, (hipStream_t)stream,
+                           mm)) {
+        set_error("check_knn_motions_masked: not for this batch / world");
+        return EPP_ERR_UNSUPPORTED;
+    }
+    return launch_error("check_knn_motions_masked");
+}
+
+extern "C" {
 
 #ifdef EPP_MOTIONS_TL
 // diagnostics builds only: the per-wave time split of the last k_motions_v4 launch
