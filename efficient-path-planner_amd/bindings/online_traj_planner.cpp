@@ -224,6 +224,7 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["edges_checked"] = s.edges_checked;
             d["edges_valid"] = s.edges_valid;
             d["attempts"] = s.attempts;
+            d["rows_downloaded"] = s.rows_downloaded;
             d["ms"] = s.ms;
             d["ms_device"] = s.ms_device;
             d["ms_search"] = s.ms_search;
@@ -386,6 +387,7 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["ms_device"] = s.ms_device;
             d["ms_search"] = s.ms_search;
             d["attempts"] = s.attempts;
+            d["rows_downloaded"] = s.rows_downloaded;
             return d;
         })
         .def("get_checkpoints", [](const epp::OnlineTrajGenerator& self) {

@@ -81,6 +81,10 @@ struct MotionMask {
     uint16_t* out16 = nullptr;
     int32_t target = -1;
     unsigned long long* count = nullptr;
+    // packed rows (the planner's row-restricted search): row r of the table is node
+    // rowmap[r], and only rows r < *rows_n are checked
+    const int32_t* rowmap = nullptr;
+    const unsigned long long* rows_n = nullptr;
 };
 // epp_check_knn_motions (mode 0) with the mask above; EPP_ERR_UNSUPPORTED as it (the
 // caller then masks with mask_edges_count_acc).
@@ -92,6 +96,24 @@ epp_status check_knn_motions_masked(const epp_world* world, const double* nodes,
 // the masked table as u16, 0xFFFF for no edge (node counts <= 65535).
 epp_status mask_edges_count_acc(int32_t* nbr, const uint8_t* valid, int64_t m, int32_t target, int64_t* count,
                                 void* stream, uint16_t* out16 = nullptr);
+// The planner's row-restricted search.  pack_ellipse_rows: the rows of the int32 k-NN table
+// `tab` (n <= 65535 nodes x k) whose node x has |x - s| + |x - g| <= bound (widened by 1e-9
+// relative + 1e-9 m), packed: ids32 / ids16[slot] = node, rows32[slot * k ..] = its row,
+// *count += the rows found (slots >= cap are not written).
+epp_status pack_ellipse_rows(const double* nodes, const int32_t* tab, int32_t n, int32_t k, const double s[3],
+                             const double g[3], double bound, int32_t cap, int32_t* ids32, uint16_t* ids16,
+                             int32_t* rows32, int64_t* count, void* stream);
+// epp_knn_ws_box (max_dist 0) whose rows are exact for every node of that ellipsoid
+// (k_knn_tile skips the blocks it cannot reach; other rows: unspecified).
+epp_status knn_ws_box_ellipse(const double* nodes, int32_t n, int32_t k, const double lo[3], const double hi[3],
+                              const double s[3], const double g[3], double bound, int32_t* nbr, void* ws,
+                              uint64_t ws_bytes, void* stream);
+// check_knn_motions_masked over the packed rows: rows32 (cap rows x k, row r = node
+// ids32[r]), rows r < min(*rows_n, cap) only; EPP_ERR_UNSUPPORTED for worlds without tile
+// tables.
+epp_status check_knn_motions_rows(const epp_world* world, const double* nodes, int32_t* rows32, const int32_t* ids32,
+                                  const int64_t* rows_n, int32_t cap, int32_t k, int32_t can_pass_gate,
+                                  uint8_t* valid, uint16_t* out16, int32_t target, int64_t* count, void* stream);
 }  // namespace epp
 
 namespace epp {

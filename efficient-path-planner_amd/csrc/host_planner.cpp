@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <iostream>
 #include <limits>
@@ -180,24 +181,38 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
                            std::min({lo[2], start.z, goal.z})};
     const double bhi[3] = {std::max({hi[0], start.x, goal.x}), std::max({hi[1], start.y, goal.y}),
                            std::max({hi[2], start.z, goal.z})};
-    check(epp_knn_ws_box(d_nodes, n, k, 0.0, blo, bhi, d_nbr, d_ws, ws_bytes, st), "knn");
-    // Motion checks straight off the k-NN table, with the mask folded in: failed motions ->
-    // -1, the valid edges and those into the goal (node 1) counted (counters zeroed above).
-    // Up to 65535 nodes the table goes down as u16 (0xFFFF: no edge), half the bytes of the
-    // largest download, written into d_e1 (free on this path).  Small batches / worlds
-    // without tile tables: materialised endpoints, then the mask kernel.
+    // Row-restricted search first (narrow tables, n <= 65535): the k-NN rows, motion checks
+    // and download only for the nodes in the ellipsoid |x - start| + |x - goal| <= bound.
+    // A* pops nodes in increasing f = g + h >= |x - start| + |x - goal|, so a search that
+    // reaches the goal with every popped f <= bound has expanded only rows held here, and
+    // pops exactly what the search over the whole table pops (a node outside the ellipsoid
+    // has f > bound >= the path's length): the same path.  Otherwise (bound passed, rows past
+    // the packing capacity, no forward edge into the goal among the rows) the whole table
+    // is built, checked and searched, as without the restriction.
+    // bound = factor * |start - goal| + 0.25 m; EPP_PLAN_ELLIPSE sets the factor (default
+    // 1.5; 0 = the whole table only).
     const bool narrow = n <= 65535;
-    uint16_t* d_nbr16 = narrow ? reinterpret_cast<uint16_t*>(d_e1) : nullptr;
-    const epp_status ks =
-        check_knn_motions_masked(w, d_nodes, d_nbr, n, k, canPass ? 1 : 0, d_ev, d_nbr16, 1, d_ecnt, st);
-    if (ks == EPP_ERR_UNSUPPORTED) {
-        check(epp_knn_edges(d_nodes, d_nbr, n, k, d_e1, d_e2, st), "edges");
-        check(epp_check_motions(w, d_e1, d_e2, (int64_t)m, canPass ? 1 : 0, 0, d_ev, st), "motion check");
-        check(mask_edges_count_acc(d_nbr, d_ev, (int64_t)m, 1, d_ecnt, st, d_nbr16), "mask edges");
-    } else {
-        check(ks, "motion check");
+    double factor = 1.5;
+    if (const char* ev = std::getenv("EPP_PLAN_ELLIPSE")) factor = std::atof(ev);
+    const double d_sg = (goal - start).norm();
+    const double bound = factor * d_sg + 0.25;
+    // packing capacity: 1.25 x the expected rows (the ellipsoid's volume, unclipped, over the
+    // sampling box's) + 1024; not worth it past half the table
+    int32_t cap = 0;
+    if (narrow && factor >= 1.0 && n > 2048) {
+        const double vbox = (hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]);
+        const double vell = M_PI * bound * (bound * bound - d_sg * d_sg) / 6.0;
+        const double frac = vbox > 0 ? std::min(1.0, vell / vbox) : 1.0;
+        const double want = 1.25 * frac * n + 1024.0;
+        if (want < 0.5 * n) cap = (int32_t)want;
     }
-    // the masked k-NN table into pinned host staging (sized as the nodes' staging)
+    // packed buffers in d_e2 (free on this path): [ids16 | rows16] (the download), ids32, rows32
+    const size_t ids_pad = ((size_t)cap + 7) & ~(size_t)7;  // (16-B aligned rows)
+    uint16_t* d_ids16 = reinterpret_cast<uint16_t*>(d_e2);
+    uint16_t* d_rows16 = d_ids16 + ids_pad;
+    const size_t pack_bytes = (ids_pad + (size_t)cap * k) * 2;
+    int32_t* d_ids32 = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(d_e2) + ((pack_bytes + 255) & ~(size_t)255));
+    int32_t* d_rows32 = d_ids32 + ids_pad;
     void* h_tab = ts.pinned(1, m_max * 4);
     const int32_t* nbr32 = static_cast<const int32_t*>(h_tab);
     const uint16_t* nbr16 = static_cast<const uint16_t*>(h_tab);
@@ -206,29 +221,69 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
         const uint16_t x = nbr16[e];
         return x == 0xFFFF ? -1 : (int)x;
     };
-    // the two downloads queued back to back, one synchronisation (and the nodes' stream)
-    int64_t* ecnt = h_cnt + 1;
-    check(epp_memcpy_d2h_async(ecnt, d_ecnt, 16, st), "download");
-    if (narrow) check(epp_memcpy_d2h_async(h_tab, d_nbr16, m * 2, st), "download");
-    else check(epp_memcpy_d2h_async(h_tab, d_nbr, m * 4, st), "download");
-    check(epp_stream_sync(st), "sync");
-    check(epp_stream_sync(cst), "sync");
-    const int64_t n_valid_edges = ecnt[0];
-    const bool goal_has_forward_edge = ecnt[1] > 0;
-    const auto t_dev1 = std::chrono::steady_clock::now();
+    int64_t* ecnt = h_cnt + 1;  // [valid edges, of which into the goal, packed rows]
+    int64_t edges_checked = 0, n_valid_edges = 0, rows_down = 0;
+    bool goal_has_forward_edge = false;
+    double ms_dev = 0.0;
+    bool restricted = false;
+    if (cap > 0) {
+        const double sv[3] = {start.x, start.y, start.z}, gv[3] = {goal.x, goal.y, goal.z};
+        check(knn_ws_box_ellipse(d_nodes, n, k, blo, bhi, sv, gv, bound, d_nbr, d_ws, ws_bytes, st), "knn");
+        check(pack_ellipse_rows(d_nodes, d_nbr, n, k, sv, gv, bound, cap, d_ids32, d_ids16, d_rows32, d_ecnt + 2, st),
+              "pack rows");
+        const epp_status ks = check_knn_motions_rows(w, d_nodes, d_rows32, d_ids32, d_ecnt + 2, cap, k,
+                                                     canPass ? 1 : 0, d_ev, d_rows16, 1, d_ecnt, st);
+        if (ks != EPP_ERR_UNSUPPORTED) {
+            check(ks, "motion check");
+            restricted = true;
+            check(epp_memcpy_d2h_async(ecnt, d_ecnt, 24, st), "download");
+            check(epp_memcpy_d2h_async(h_tab, d_ids16, pack_bytes, st), "download");
+            check(epp_stream_sync(st), "sync");
+            check(epp_stream_sync(cst), "sync");
+            const int64_t rows = std::min<int64_t>(ecnt[2], cap);
+            edges_checked += rows * k;
+            n_valid_edges += ecnt[0];
+            rows_down += rows;
+        }
+    }
+    // the whole table (as without the restriction): k-NN, motion checks straight off the
+    // table with the mask folded in (failed motions -> -1; the valid edges and those into
+    // the goal, node 1, counted), the table down (up to 65535 nodes as u16, 0xFFFF: no edge,
+    // half the bytes, written into d_e1).  Small batches / worlds without tile tables:
+    // materialised endpoints, then the mask kernel.
+    uint16_t* d_nbr16 = narrow ? reinterpret_cast<uint16_t*>(d_e1) : nullptr;
+    auto whole_table = [&] {
+        if (restricted && hipMemsetAsync(d_ecnt, 0, 16, static_cast<hipStream_t>(st)) != hipSuccess)
+            throw std::runtime_error("planPath: clearing the edge counts failed");
+        check(epp_knn_ws_box(d_nodes, n, k, 0.0, blo, bhi, d_nbr, d_ws, ws_bytes, st), "knn");
+        const epp_status ks =
+            check_knn_motions_masked(w, d_nodes, d_nbr, n, k, canPass ? 1 : 0, d_ev, d_nbr16, 1, d_ecnt, st);
+        if (ks == EPP_ERR_UNSUPPORTED) {
+            check(epp_knn_edges(d_nodes, d_nbr, n, k, d_e1, d_e2, st), "edges");
+            check(epp_check_motions(w, d_e1, d_e2, (int64_t)m, canPass ? 1 : 0, 0, d_ev, st), "motion check");
+            check(mask_edges_count_acc(d_nbr, d_ev, (int64_t)m, 1, d_ecnt, st, d_nbr16), "mask edges");
+        } else {
+            check(ks, "motion check");
+        }
+        // the downloads queued back to back, one synchronisation (and the nodes' stream)
+        check(epp_memcpy_d2h_async(ecnt, d_ecnt, 16, st), "download");
+        if (narrow) check(epp_memcpy_d2h_async(h_tab, d_nbr16, m * 2, st), "download");
+        else check(epp_memcpy_d2h_async(h_tab, d_nbr, m * 4, st), "download");
+        check(epp_stream_sync(st), "sync");
+        check(epp_stream_sync(cst), "sync");
+        edges_checked += (int64_t)m;
+        n_valid_edges += ecnt[0];
+        goal_has_forward_edge = ecnt[1] > 0;
+        rows_down += n;
+    };
+    if (!restricted) whole_table();
+    ms_dev += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_dev0).count();
     // ---- 3. shortest path over the valid edges, start = 0, goal = 1 ----------------------
     // A* with the Euclidean distance to the goal (admissible and consistent for Euclidean
     // edge costs: an optimal path of the graph searched).  First over the forward k-NN
     // edges alone, read straight from the k-NN table (no graph build: A* touches only
     // the nodes it expands); only if the goal is not reached that way, again over the
     // symmetrised graph (reverse edges added as a CSR).
-    {
-        std::lock_guard<std::mutex> lk(g_stats_mu);
-        stats_.states_sampled += samples;
-        stats_.states_valid += n - 2;
-        stats_.edges_checked += (int64_t)m;
-        stats_.edges_valid += n_valid_edges;
-    }
     auto node = [&](int v) { return Vec3(nodes[3 * v], nodes[3 * v + 1], nodes[3 * v + 2]); };
     const Vec3 gp = node(1);
     // Search state per host thread, reused across calls: a node's dist / prev hold this
@@ -252,7 +307,12 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
     std::vector<int32_t> roff, radj;  // reverse edges (second pass only)
     auto dist_of = [&](int v) { return ss.seen[v] == ss.cur ? ss.dist[v] : std::numeric_limits<double>::infinity(); };
     auto prev_of = [&](int v) { return ss.seen[v] == ss.cur ? ss.prev[v] : -1; };
-    auto astar = [&](bool with_reverse) {
+    // (restricted: rows from the packed download via row_of; -1 = a pop above the bound or
+    // of a row not held, so the caller takes the whole table)
+    thread_local std::vector<int32_t> row_of;
+    const uint16_t* pk_ids = nbr16;
+    const uint16_t* pk_rows = nbr16 + ids_pad;
+    auto astar = [&](bool with_reverse, bool restricted) -> int {
         if (++ss.cur == 0u) {  // (stamp wrap-around: clear once)
             std::fill(ss.seen.begin(), ss.seen.end(), 0u);
             std::fill(ss.done.begin(), ss.done.end(), 0u);
@@ -282,44 +342,78 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
             }
         };
         while (!q.empty()) {
+            const double f = q.front().first;
             const int u = q.front().second;
             std::pop_heap(q.begin(), q.end(), cmp);
             q.pop_back();
             if (ss.done[u] == ss.cur) continue;
+            const uint16_t* row = nullptr;
+            if (restricted) {
+                if (!(f <= bound) || row_of[u] < 0) return -1;
+                row = pk_rows + (size_t)row_of[u] * k;
+            }
             ss.done[u] = ss.cur;
-            if (u == 1) return true;
+            if (u == 1) return 1;
             const Vec3 pu = node(u);
-            const size_t e0 = (size_t)u * k;
-            for (int c = 0; c < k; ++c) {
-                const int v = nbr(e0 + c);
-                if (v >= 0) relax(u, pu, v);
+            if (restricted) {
+                for (int c = 0; c < k; ++c)
+                    if (row[c] != 0xFFFF) relax(u, pu, (int)row[c]);
+            } else {
+                const size_t e0 = (size_t)u * k;
+                for (int c = 0; c < k; ++c) {
+                    const int v = nbr(e0 + c);
+                    if (v >= 0) relax(u, pu, v);
+                }
             }
             if (with_reverse)
                 for (int32_t r = roff[u]; r < roff[u + 1]; ++r) relax(u, pu, radj[r]);
         }
-        return false;
+        return 0;
     };
-    // (no forward edge into the goal: the forward pass cannot reach it — it would only
-    // explore start's whole component first; same result, so go straight to the second)
-    if (!goal_has_forward_edge || !astar(false)) {
-        roff.assign(n + 1, 0);
-        for (size_t e = 0; e < m; ++e)
-            if (nbr(e) >= 0) ++roff[nbr(e) + 1];
-        for (int i = 0; i < n; ++i) roff[i + 1] += roff[i];
-        radj.resize(roff[n]);
-        std::vector<int32_t> fill(roff.begin(), roff.end() - 1);
-        for (int i = 0; i < n; ++i)
-            for (int c = 0; c < k; ++c) {
-                const size_t e = (size_t)i * k + c;
-                if (nbr(e) >= 0) radj[fill[nbr(e)]++] = i;
-            }
-        astar(true);
+    int found = -1;
+    if (restricted && ecnt[1] > 0 && ecnt[2] <= cap) {
+        if (row_of.size() < (size_t)n) row_of.resize(n, -1);
+        for (int64_t r = 0; r < ecnt[2]; ++r) row_of[pk_ids[r]] = (int32_t)r;
+        found = astar(false, true);
+        for (int64_t r = 0; r < ecnt[2]; ++r) row_of[pk_ids[r]] = -1;
+    }
+    if (found != 1) {
+        if (restricted) {  // the whole table after all
+            const auto t0 = std::chrono::steady_clock::now();
+            whole_table();
+            ms_dev += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        }
+        // (no forward edge into the goal: the forward pass cannot reach it — it would only
+        // explore start's whole component first; same result, so go straight to the second)
+        if (!goal_has_forward_edge || astar(false, false) != 1) {
+            roff.assign(n + 1, 0);
+            for (size_t e = 0; e < m; ++e)
+                if (nbr(e) >= 0) ++roff[nbr(e) + 1];
+            for (int i = 0; i < n; ++i) roff[i + 1] += roff[i];
+            radj.resize(roff[n]);
+            std::vector<int32_t> fill(roff.begin(), roff.end() - 1);
+            for (int i = 0; i < n; ++i)
+                for (int c = 0; c < k; ++c) {
+                    const size_t e = (size_t)i * k + c;
+                    if (nbr(e) >= 0) radj[fill[nbr(e)]++] = i;
+                }
+            astar(true, false);
+        }
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_stats_mu);
+        stats_.states_sampled += samples;
+        stats_.states_valid += n - 2;
+        stats_.edges_checked += edges_checked;
+        stats_.edges_valid += n_valid_edges;
+        stats_.rows_downloaded += rows_down;
     }
     auto account = [&] {
         const auto t_end = std::chrono::steady_clock::now();
         std::lock_guard<std::mutex> lk(g_stats_mu);
-        stats_.ms_device += std::chrono::duration<double, std::milli>(t_dev1 - t_dev0).count();
-        stats_.ms_search += std::chrono::duration<double, std::milli>(t_end - t_dev1).count();
+        const double total = std::chrono::duration<double, std::milli>(t_end - t_dev0).count();
+        stats_.ms_device += ms_dev;
+        stats_.ms_search += total - ms_dev;
     };
     if (prev_of(1) < 0) {
         account();

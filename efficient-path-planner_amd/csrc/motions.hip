@@ -515,14 +515,16 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
 #endif
     const int64_t stride = (int64_t)gridDim.x * BLOCK;
     uint32_t mk_keep = 0, mk_tgt = 0;  // (MotionMask counts)
-    for (int64_t i0 = (int64_t)blockIdx.x * BLOCK + wave * 64; i0 < n; i0 += stride) {
+    // (packed rows: only the first *rows_n rows hold a table row)
+    const int64_t ne = (IDX && mm.rows_n) ? min(n, (int64_t)min(*mm.rows_n, (unsigned long long)(n / kk)) * kk) : n;
+    for (int64_t i0 = (int64_t)blockIdx.x * BLOCK + wave * 64; i0 < ne; i0 += stride) {
         const int64_t i = i0 + lane;
-        const bool act = i < n;
+        const bool act = i < ne;
         double s[3] = {0.0, 0.0, 0.0}, e[3] = {0.0, 0.0, 0.0};
         int32_t jraw = -1;  // (IDX: the table entry)
         if (act) {
             if (IDX) {
-                const int64_t u = i / kk;
+                const int64_t u = mm.rowmap ? (int64_t)mm.rowmap[i / kk] : i / kk;
                 const int32_t j = nbr[i];
                 jraw = j;
                 const int64_t v = j < 0 ? u : (int64_t)j;
@@ -917,6 +919,33 @@ epp_status epp::check_knn_motions_masked(const epp_world* world, const double* n
         return EPP_ERR_UNSUPPORTED;
     }
     return launch_error("check_knn_motions_masked");
+}
+
+epp_status epp::check_knn_motions_rows(const epp_world* world, const double* nodes, int32_t* rows32,
+                                       const int32_t* ids32, const int64_t* rows_n, int32_t cap, int32_t k,
+                                       int32_t can_pass_gate, uint8_t* valid, uint16_t* out16, int32_t target,
+                                       int64_t* count, void* stream) {
+    if (!world || cap < 0 || k <= 0 || (cap > 0 && (!nodes || !rows32 || !ids32 || !rows_n || !valid || !count))) {
+        set_error("check_knn_motions_rows: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    const int64_t m = (int64_t)cap * k;
+    if (m == 0) return EPP_OK;
+    IndexLease ix;
+    if (const epp_status st = ensure_index(world, &ix)) return st;
+    MotionMask mm;
+    mm.nbr_w = rows32;
+    mm.out16 = out16;
+    mm.target = target;
+    mm.count = reinterpret_cast<unsigned long long*>(count);
+    mm.rowmap = ids32;
+    mm.rows_n = reinterpret_cast<const unsigned long long*>(rows_n);
+    if (!launch_motions_v5(ix.dview, ix.view, nodes, nullptr, rows32, k, m, can_pass_gate, 0, valid,
+                           (hipStream_t)stream, mm)) {
+        set_error("check_knn_motions_rows: not for this world");
+        return EPP_ERR_UNSUPPORTED;
+    }
+    return launch_error("check_knn_motions_rows");
 }
 
 extern "C" {

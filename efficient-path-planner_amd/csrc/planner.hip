@@ -119,6 +119,9 @@ struct KnnGrid {
     int next;    // k_knn_tile's block queue
     int nretry;  // k_knn_tile's retry list length
     int why[4];  // retry causes (diagnostics): list overflow, K-th beyond Dcut, shell rule, crowded (or spilled)
+    // k_knn_tile answers only the queries of blocks that may hold a node x with
+    // |x - qs| + |x - qg| <= qbound (the planner's row-restricted search; 1e300: all)
+    double qs[3], qg[3], qbound;
 };
 
 constexpr int kBoundsThreads = 1024;
@@ -161,6 +164,8 @@ __host__ __device__ inline void knn_grid_shape(const double (&mn)[3], const doub
     g->next = 0;
     g->nretry = 0;
     for (int i = 0; i < 4; ++i) g->why[i] = 0;
+    for (int d = 0; d < 3; ++d) g->qs[d] = g->qg[d] = 0.0;
+    g->qbound = 1e300;
 }
 
 // Per-block min/max of the node coordinates: part[6 * block] = (min xyz, max xyz).  Also
@@ -903,6 +908,28 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
         const int b = s_b;  // block-uniform
         if (b >= nblocks) break;
         const int bx = b % nbx, by = (b / nbx) % nby, bz = b / (nbx * nby);
+        if (g.qbound < 1e299) {
+            // the planner's row-restricted search: skip a block whose core cells (outer
+            // blocks: unbounded outwards, as the cell index clamps) hold no node within the
+            // ellipsoid -- dist(qs, box) + dist(qg, box) is a lower bound of |x - qs| +
+            // |x - qg| over the box (margins: the pack kernel's test and cell rounding)
+            const double t = kTileB * g.h;
+            const int bi[3] = {bx, by, bz}, nbv[3] = {nbx, nby, nbz};
+            double ds2 = 0.0, dg2 = 0.0;
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                const double lo_d = bi[d] == 0 ? -1e300 : g.lo[d] + bi[d] * t - 1e-6 * t;
+                const double hi_d = bi[d] == nbv[d] - 1 ? 1e300 : g.lo[d] + (bi[d] + 1) * t + 1e-6 * t;
+                const double a = fmax(fmax(lo_d - g.qs[d], g.qs[d] - hi_d), 0.0);
+                const double c = fmax(fmax(lo_d - g.qg[d], g.qg[d] - hi_d), 0.0);
+                ds2 += a * a;
+                dg2 += c * c;
+            }
+            if (sqrt(ds2) + sqrt(dg2) > g.qbound * (1.0 + 1e-8) + 1e-6) {
+                __syncthreads();  // (every thread has read s_b before thread 0 takes the next)
+                continue;
+            }
+        }
         const int ox = bx * kTileB - kTileH, oy = by * kTileB - kTileH, oz = bz * kTileB - kTileH;
         const double cen[3] = {g.lo[0] + (ox + 0.5 * kTileE) * g.h, g.lo[1] + (oy + 0.5 * kTileE) * g.h,
                                g.lo[2] + (oz + 0.5 * kTileE) * g.h};
@@ -1593,7 +1620,7 @@ unsigned long long* knn_tl_buffer() {
 
 epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, int32_t* nbr, char* buf,
                            const KnnLayout& L, hipStream_t s, const double* box_lo = nullptr,
-                           const double* box_hi = nullptr) {
+                           const double* box_hi = nullptr, const double* ellipse = nullptr) {
     KnnGrid* g = reinterpret_cast<KnnGrid*>(buf);
     int* cell_of = reinterpret_cast<int*>(buf + L.cell);
     int* sidx = reinterpret_cast<int*>(buf + L.sidx);
@@ -1619,6 +1646,13 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
         KnnGrid gv{};
         const double mn[3] = {box_lo[0], box_lo[1], box_lo[2]}, mx[3] = {box_hi[0], box_hi[1], box_hi[2]};
         knn_grid_shape(mn, mx, n, L.cap, npc, &gv);
+        if (ellipse) {  // (k_knn_tile only: its queries restricted to the blocks the ellipsoid reaches)
+            for (int d = 0; d < 3; ++d) {
+                gv.qs[d] = ellipse[d];
+                gv.qg[d] = ellipse[3 + d];
+            }
+            gv.qbound = ellipse[6];
+        }
         hipLaunchKernelGGL(k_knn_prep, dim3(nb), dim3(kBoundsThreads), 0, s, gv, g, cnt, nclr);
     } else {
         double* part = reinterpret_cast<double*>(buf + L.part);
@@ -1805,6 +1839,49 @@ __global__ __launch_bounds__(kMaskThreads) void k_mask_edges_count(int32_t* __re
         uint32_t t = 0;
         for (int w = 0; w < kMaskThreads / 64; ++w) t += part[threadIdx.x][w];
         if (t) atomicAdd(count + threadIdx.x, (unsigned long long)t);
+    }
+}
+
+// The planner's row-restricted search: the rows of the k-NN table (int32) whose node lies
+// in the ellipsoid |x - s| + |x - g| <= bound, packed in arbitrary slot order: ids32 /
+// ids16[slot] = the node, rows32[slot * k ..] = its row.  The test is widened by 1e-9
+// relative + 1e-9 m, so every node the host's A* can expand below the bound has its row
+// here.  One atomic per wave; rows past `cap` are counted, not written (the host then
+// takes the whole table).
+__global__ __launch_bounds__(256) void k_pack_ellipse_rows(const double* __restrict__ nodes,
+                                                           const int32_t* __restrict__ tab, int32_t n,
+                                                           int32_t k, double sx, double sy, double sz,
+                                                           double gx, double gy, double gz, double bound,
+                                                           int32_t cap, int32_t* __restrict__ ids32,
+                                                           uint16_t* __restrict__ ids16,
+                                                           int32_t* __restrict__ rows32,
+                                                           unsigned long long* __restrict__ count) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    bool in = false;
+    if (i < n) {
+        const double x = nodes[3 * i], y = nodes[3 * i + 1], z = nodes[3 * i + 2];
+        const double ds = sqrt((x - sx) * (x - sx) + (y - sy) * (y - sy) + (z - sz) * (z - sz));
+        const double dg = sqrt((x - gx) * (x - gx) + (y - gy) * (y - gy) + (z - gz) * (z - gz));
+        in = ds + dg <= bound * (1.0 + 1e-9) + 1e-9;
+    }
+    const unsigned long long bal = __ballot(in);
+    if (!bal) return;  // (uniform per wave)
+    const int lane = threadIdx.x & 63;
+    const int first = __ffsll(bal) - 1;
+    unsigned long long base = 0;
+    if (lane == first) base = atomicAdd(count, (unsigned long long)__popcll(bal));
+    base = __shfl(base, first, 64);
+    if (!in) return;
+    const unsigned long long slot = base + __popcll(bal & ((1ull << lane) - 1ull));
+    if (slot >= (unsigned long long)cap) return;
+    ids32[slot] = i;
+    ids16[slot] = (uint16_t)i;
+    const int32_t* src = tab + (size_t)i * k;
+    int32_t* dst = rows32 + (size_t)slot * k;
+    if ((k & 3) == 0) {
+        for (int c = 0; c < k; c += 4) *reinterpret_cast<int4*>(dst + c) = *reinterpret_cast<const int4*>(src + c);
+    } else {
+        for (int c = 0; c < k; ++c) dst[c] = src[c];
     }
 }
 
@@ -2056,6 +2133,40 @@ epp_status epp::mask_edges_count_acc(int32_t* nbr, const uint8_t* valid, int64_t
     hipLaunchKernelGGL(k_mask_edges_count, dim3((unsigned)blocks), dim3(kMaskThreads), 0, s, nbr, valid, m, target,
                        reinterpret_cast<unsigned long long*>(count), out16);
     return last("epp_mask_edges_count");
+}
+
+epp_status epp::pack_ellipse_rows(const double* nodes, const int32_t* tab, int32_t n, int32_t k, const double s[3],
+                                  const double g[3], double bound, int32_t cap, int32_t* ids32, uint16_t* ids16,
+                                  int32_t* rows32, int64_t* count, void* stream) {
+    // ids16 are u16: n <= 65535 (the narrow table); 16-B aligned rows for the vector copy
+    if (n < 0 || n > 65535 || k <= 0 || cap < 0 || !count || !s || !g ||
+        (n > 0 && (!nodes || !tab || !ids32 || !ids16 || !rows32)) || (reinterpret_cast<uintptr_t>(tab) & 15) ||
+        (reinterpret_cast<uintptr_t>(rows32) & 15)) {
+        set_error("pack_ellipse_rows: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    if (n == 0) return EPP_OK;
+    hipLaunchKernelGGL(k_pack_ellipse_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       nodes, tab, n, k, s[0], s[1], s[2], g[0], g[1], g[2], bound, cap, ids32, ids16, rows32,
+                       reinterpret_cast<unsigned long long*>(count));
+    return last("pack_ellipse_rows");
+}
+
+epp_status epp::knn_ws_box_ellipse(const double* nodes, int32_t n, int32_t k, const double lo[3], const double hi[3],
+                                   const double s[3], const double g[3], double bound, int32_t* nbr, void* ws,
+                                   uint64_t ws_bytes, void* stream) {
+    if (n <= 2048 || (k != 4 && k != 8 && k != 16)) return epp_knn_ws_box(nodes, n, k, 0.0, lo, hi, nbr, ws, ws_bytes, stream);
+    if (!nodes || !nbr || !lo || !hi || !s || !g || !(lo[0] <= hi[0] && lo[1] <= hi[1] && lo[2] <= hi[2])) {
+        set_error("knn_ws_box_ellipse: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    const KnnLayout L = knn_layout(n);
+    if (!ws || ws_bytes < L.bytes || (reinterpret_cast<uintptr_t>(ws) & 255)) {
+        set_error("knn_ws_box_ellipse: workspace missing, unaligned or too small");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    const double q[7] = {s[0], s[1], s[2], g[0], g[1], g[2], bound};
+    return knn_grid_launch(nodes, n, k, 0.0, nbr, static_cast<char*>(ws), L, (hipStream_t)stream, lo, hi, q);
 }
 
 extern "C" {

@@ -30,6 +30,7 @@ struct PlannerStats {
     int64_t edges_checked = 0;
     int64_t edges_valid = 0;
     int attempts = 0;
+    int64_t rows_downloaded = 0;  // k-NN table rows copied to the host (see planPath)
     double ms = 0;         // wall time of the last planPath
     double ms_device = 0;  // of which: sampling, checks, k-NN, transfers (GPU phases)
     double ms_search = 0;  // of which: graph build + A* + shortcut on the host

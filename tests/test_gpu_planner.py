@@ -666,8 +666,16 @@ def test_c1_plumbing_end_to_end(tmp_path, c1, geom):
 # ---- the planner against its CPU restatement (oracle/epp_oracle.cpp or_plan_once) ------
 # Same counter-RNG samples, exact k-NN with the same tie rule, the same A* and shortcut:
 # the GPU pipeline must give the SAME path, not just a valid one.
+# EPP_PLAN_ELLIPSE: the row-restricted table download (default factor 1.5), a bound the
+# paths exceed (1.0: the search falls back to the whole table) and the whole table only (0)
+ELLIPSE = ["", "1.0", "0"]
+
+
+@pytest.mark.parametrize("ellipse", ELLIPSE)
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_plan_once_equals_cpu_restatement(c1, seed):
+def test_plan_once_equals_cpu_restatement(c1, seed, ellipse, monkeypatch):
+    if ellipse:
+        monkeypatch.setenv("EPP_PLAN_ELLIPSE", ellipse)
     g, o, start, goal, w, rg, ro = c1
     pp = _ot().PathPlanner(g, o, CONFIG)
     lo, hi = synth.C1_BOUNDS
@@ -682,9 +690,12 @@ def test_plan_once_equals_cpu_restatement(c1, seed):
     assert O.plan_once(w, rg, ro, lo, hi, start, blocked, 4096, seed, 16, False, 4)[0] is None
 
 
-def test_plan_once_equals_cpu_restatement_track(track, geom):
+@pytest.mark.parametrize("ellipse", ELLIPSE)
+def test_plan_once_equals_cpu_restatement_track(track, geom, ellipse, monkeypatch):
     """Every gate-to-gate segment of the C2 track (65,536 samples, the C4 size) equal on
-    GPU and CPU."""
+    GPU and CPU, with the row-restricted table download and without."""
+    if ellipse:
+        monkeypatch.setenv("EPP_PLAN_ELLIPSE", ellipse)
     path, c, gates, obstacles, start, goal = track
     pp = _ot().PathPlanner(gates, obstacles, path)
     rg, ro = config.inflate_radii(c)
@@ -692,10 +703,17 @@ def test_plan_once_equals_cpu_restatement_track(track, geom):
     lo, hi = np.array(c["world_properties"]["lower_bound"], float), np.array(c["world_properties"]["upper_bound"], float)
     cps = synth.gate_checkpoints(gates, geom.gate_height, c["path_planner_properties"]["checkpoint_gate_offset"])
     cps = np.vstack([start, cps, goal])
+    rows = []
     for s in range(0, len(cps) - 1, 2):
+        r0 = pp.last_stats()["rows_downloaded"]  # (plan_once accumulates the stats)
         got = pp.plan_once(cps[s], cps[s + 1], 65536, 1000 + s)
-        exp, _ = O.plan_once(w, rg, ro, lo, hi, cps[s], cps[s + 1], 65536, 1000 + s, 16, False, 16)
+        exp, st = O.plan_once(w, rg, ro, lo, hi, cps[s], cps[s + 1], 65536, 1000 + s, 16, False, 16)
         assert got is not None and np.array_equal(got, exp), s
+        rows.append((pp.last_stats()["rows_downloaded"] - r0, st[1] + 2))
+    if ellipse == "0":
+        assert all(r == n for r, n in rows)
+    elif ellipse == "":  # most segments' searches stay inside the ellipsoid
+        assert sum(r < n for r, n in rows) >= len(rows) // 2, rows
     # one segment past 65,535 nodes: the k-NN table goes down as int32 instead of u16
     got = pp.plan_once(cps[1], cps[2], 80_000, 77)
     exp, st = O.plan_once(w, rg, ro, lo, hi, cps[1], cps[2], 80_000, 77, 16, False, 16)
