@@ -38,7 +38,9 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
     os.unlink(path)
     print(f"{os.path.basename(os.environ.get('EPP_PKG', '') or 'cur')} threads {os.environ.get('EPP_PLAN_THREADS', '4')} writer {os.environ.get('EPP_PATH_WRITER', '1')}: pre_compute_traj p50 {np.median(ts):.2f} ms "
           f"(mean {np.mean(ts):.2f}, min {min(ts):.2f}); planner: ms {np.median([s['ms'] for s in st]):.2f}, device sum "
-          f"{np.median([s['ms_device'] for s in st]):.2f}, search sum {np.median([s['ms_search'] for s in st]):.2f}",
+          f"{np.median([s['ms_device'] for s in st]):.2f}, search sum {np.median([s['ms_search'] for s in st]):.2f}, "
+          f"rows down per track {np.median([s['rows_downloaded'] for s in st]):.0f} "
+          f"(EPP_PLAN_ELLIPSE {os.environ.get('EPP_PLAN_ELLIPSE', 'default')})",
           flush=True)
     order = np.argsort(ts)[::-1][:6]
     print("   slowest:", ", ".join(f"#{i} {ts[i]:.1f} ms (planner {st[i]['ms']:.1f}, device {st[i]['ms_device']:.1f}, "

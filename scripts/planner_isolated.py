@@ -46,4 +46,5 @@ os.unlink(path)
 print(json.dumps({"segments": 20, "ms_p50": float(np.median(ts)), "ms_mean": float(np.mean(ts)),
                   "device_ms_p50": float(np.median([x["ms_device"] for x in st])),
                   "search_ms_p50": float(np.median([x["ms_search"] for x in st])),
-                  "nodes_p50": float(np.median([x["states_valid"] for x in st]))}), flush=True)
+                  "nodes_p50": float(np.median([x["states_valid"] for x in st])),
+                  "rows_down": [int(x["rows_downloaded"]) for x in st]}), flush=True)
