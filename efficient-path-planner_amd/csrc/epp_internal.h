@@ -103,8 +103,8 @@ epp_status mask_edges_count_acc(int32_t* nbr, const uint8_t* valid, int64_t m, i
 epp_status pack_ellipse_rows(const double* nodes, const int32_t* tab, int32_t n, int32_t k, const double s[3],
                              const double g[3], double bound, int32_t cap, int32_t* ids32, uint16_t* ids16,
                              int32_t* rows32, int64_t* count, void* stream);
-// epp_knn_ws_box (max_dist 0) whose rows are exact for every node of that ellipsoid
-// (k_knn_tile skips the blocks it cannot reach; other rows: unspecified).
+// epp_knn_ws_box (max_dist 0) whose rows are exact for every node of that ellipsoid (the
+// grid as usual, then those nodes' rows alone, one wave each; other rows: unspecified).
 epp_status knn_ws_box_ellipse(const double* nodes, int32_t n, int32_t k, const double lo[3], const double hi[3],
                               const double s[3], const double g[3], double bound, int32_t* nbr, void* ws,
                               uint64_t ws_bytes, void* stream);

@@ -119,8 +119,8 @@ struct KnnGrid {
     int next;    // k_knn_tile's block queue
     int nretry;  // k_knn_tile's retry list length
     int why[4];  // retry causes (diagnostics): list overflow, K-th beyond Dcut, shell rule, crowded (or spilled)
-    // k_knn_tile answers only the queries of blocks that may hold a node x with
-    // |x - qs| + |x - qg| <= qbound (the planner's row-restricted search; 1e300: all)
+    // the planner's row-restricted k-NN (k_knn_list_ellipse): the ellipsoid
+    // |x - qs| + |x - qg| <= qbound (1e300: unused)
     double qs[3], qg[3], qbound;
 };
 
@@ -908,28 +908,6 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
         const int b = s_b;  // block-uniform
         if (b >= nblocks) break;
         const int bx = b % nbx, by = (b / nbx) % nby, bz = b / (nbx * nby);
-        if (g.qbound < 1e299) {
-            // the planner's row-restricted search: skip a block whose core cells (outer
-            // blocks: unbounded outwards, as the cell index clamps) hold no node within the
-            // ellipsoid -- dist(qs, box) + dist(qg, box) is a lower bound of |x - qs| +
-            // |x - qg| over the box (margins: the pack kernel's test and cell rounding)
-            const double t = kTileB * g.h;
-            const int bi[3] = {bx, by, bz}, nbv[3] = {nbx, nby, nbz};
-            double ds2 = 0.0, dg2 = 0.0;
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                const double lo_d = bi[d] == 0 ? -1e300 : g.lo[d] + bi[d] * t - 1e-6 * t;
-                const double hi_d = bi[d] == nbv[d] - 1 ? 1e300 : g.lo[d] + (bi[d] + 1) * t + 1e-6 * t;
-                const double a = fmax(fmax(lo_d - g.qs[d], g.qs[d] - hi_d), 0.0);
-                const double c = fmax(fmax(lo_d - g.qg[d], g.qg[d] - hi_d), 0.0);
-                ds2 += a * a;
-                dg2 += c * c;
-            }
-            if (sqrt(ds2) + sqrt(dg2) > g.qbound * (1.0 + 1e-8) + 1e-6) {
-                __syncthreads();  // (every thread has read s_b before thread 0 takes the next)
-                continue;
-            }
-        }
         const int ox = bx * kTileB - kTileH, oy = by * kTileB - kTileH, oz = bz * kTileB - kTileH;
         const double cen[3] = {g.lo[0] + (ox + 0.5 * kTileE) * g.h, g.lo[1] + (oy + 0.5 * kTileE) * g.h,
                                g.lo[2] + (oz + 0.5 * kTileE) * g.h};
@@ -1239,11 +1217,43 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
     }
 }
 
+// The planner's row-restricted k-NN: the nodes x with |x - qs| + |x - qg| <= qbound (widened
+// by 1e-8 relative + 1e-6 m, looser than k_pack_ellipse_rows' test) listed as unbounded
+// retry queries, so k_knn_retry answers exactly them, one wave each: a few thousand
+// queries spread over the whole chip instead of k_knn_tile's blocks, each of which takes
+// the whole kernel's ~80 us latency however few of them run.  After the scatter (the retry
+// list reuses cell_of).
+__global__ __launch_bounds__(256) void k_knn_list_ellipse(KnnGrid* __restrict__ gp, const double* __restrict__ nodes,
+                                                          int n, int* __restrict__ retry,
+                                                          double* __restrict__ retry_b) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    bool in = false;
+    if (i < n) {
+        const double* q = gp->qs;
+        const double* r = gp->qg;
+        const double x = nodes[3 * i], y = nodes[3 * i + 1], z = nodes[3 * i + 2];
+        const double ds = sqrt((x - q[0]) * (x - q[0]) + (y - q[1]) * (y - q[1]) + (z - q[2]) * (z - q[2]));
+        const double dg = sqrt((x - r[0]) * (x - r[0]) + (y - r[1]) * (y - r[1]) + (z - r[2]) * (z - r[2]));
+        in = ds + dg <= gp->qbound * (1.0 + 1e-8) + 1e-6;
+    }
+    const unsigned long long bal = __ballot(in);
+    if (!bal) return;  // (uniform per wave)
+    const int lane = threadIdx.x & 63;
+    const int first = __ffsll(bal) - 1;
+    int base = 0;
+    if (lane == first) base = atomicAdd(&gp->nretry, __popcll(bal));
+    base = __shfl(base, first, 64);
+    if (!in) return;
+    const int at = base + __popcll(bal & ((1ull << lane) - 1ull));
+    retry[at] = i;
+    retry_b[at] = INFINITY;
+}
+
 // Retry list of k_knn_tile: one wave per query (knn_retry_wave).
-template <int K>
 // One wavefront per workgroup.  (knn_retry_wave is inlined: as a call it took the grid
 // parameters by reference to the caller's local copy, which then lived in scratch --
 // global-memory round trips on every cell index.)
+template <int K>
 __global__ __launch_bounds__(64) void k_knn_retry(const KnnGrid* __restrict__ gp, double r2max,
                                                    const double* __restrict__ nodes,
                                                    const double* __restrict__ sxyz,
@@ -1646,7 +1656,7 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
         KnnGrid gv{};
         const double mn[3] = {box_lo[0], box_lo[1], box_lo[2]}, mx[3] = {box_hi[0], box_hi[1], box_hi[2]};
         knn_grid_shape(mn, mx, n, L.cap, npc, &gv);
-        if (ellipse) {  // (k_knn_tile only: its queries restricted to the blocks the ellipsoid reaches)
+        if (ellipse) {  // (the row-restricted k-NN: k_knn_list_ellipse + k_knn_retry)
             for (int d = 0; d < 3; ++d) {
                 gv.qs[d] = ellipse[d];
                 gv.qg[d] = ellipse[3 + d];
@@ -1680,6 +1690,16 @@ epp_status knn_grid_launch(const double* nodes, int n, int k, double max_dist, i
     const bool tiled = tile_sel != 0;
     int* const retry = cell_of;  // free once the scatter has run
     double* const retry_b = reinterpret_cast<double*>(buf + L.rbnd);
+    if (ellipse && (k == 4 || k == 8 || k == 16)) {  // the planner's row-restricted k-NN
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        hipLaunchKernelGGL(k_knn_list_ellipse, g256, b256, 0, s, g, nodes, n, retry, retry_b);
+        const dim3 gr((unsigned)std::max(1, cus * EPP_KNN_RETRY_PER_CU)), br(64);
+        if (k == 4) hipLaunchKernelGGL(k_knn_retry<4>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr);
+        else if (k == 8) hipLaunchKernelGGL(k_knn_retry<8>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr);
+        else hipLaunchKernelGGL(k_knn_retry<16>, gr, br, 0, s, g, r2, nodes, sxyz, sidx, start, retry, retry_b, nbr);
+        return last("epp_knn_grid");
+    }
     // (node ids share a word with the halo x index in k_knn_wave: below 2^29)
     if (tile_sel == 2 && (k == 4 || k == 8 || k == 16) && n < (1 << 29)) {
         int dev = 0, cus = 256;
