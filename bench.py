@@ -211,12 +211,20 @@ def run(args, ws, rank, local, out_stream):
         capi.check(L.epp_graph_destroy(graph))
     achieved = BYTES_PER_STATE * N_STATES / (kms * 1e-3) / 1e9
     n_valid = int(d_valid.download(np.uint8, N_STATES).sum())
+    # parity: the flags of resident batch 0 (the cpu_baseline leg checks the same batch on
+    # the oracle and counts the mismatches)
+    step(0)
+    capi.check(L.epp_stream_sync(stream))
+    c2_flags = d_valid.download(np.uint8, N_STATES)
 
     traffic, traffic_src = committed_traffic()
 
     cpu = None
+    parity_gpu = dict((c5_inputs or {}).get("parity_gpu", {}), c2_flags=c2_flags)
+    if plan:
+        parity_gpu["c4_first"] = plan.pop("_first")
     if not args.no_cpu and ws == 1:
-        cpu = cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs)
+        cpu = cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs, parity_gpu)
     if c5_inputs:
         os.unlink(c5_inputs["cfg_path"])
 
@@ -248,6 +256,9 @@ def run(args, ws, rank, local, out_stream):
             "full_plan_ms_per_track": plan["ms_per_track"] if plan else None,
             "full_plan": plan,
             "cpu_baseline": cpu,
+            # the GPU results above against the CPU oracle on the same inputs (computed in the
+            # cpu_baseline leg; null without it)
+            "parity": cpu.pop("parity", None) if cpu else None,
             "side": side,
         }
         print(json.dumps(out), file=out_stream, flush=True)
@@ -271,6 +282,7 @@ def launcher_check(ws, rank, local, out_stream, fail_rank=-1, fail_at="plan"):
         return np.arange(3 * (5 + rank), dtype=np.float64).reshape(-1, 3) + 1000 * rank
 
     wp = dist.run(plan, "full plan")
+    per_rank = dist.gather(float(rank + 1))
     if rank == fail_rank and fail_at == "after-count":
         # this rank's process dies between the two steps of the exchange: its count is sent,
         # its set never is (the peers must leave the data all-gather with an error)
@@ -284,7 +296,8 @@ def launcher_check(ws, rank, local, out_stream, fail_rank=-1, fail_at="plan"):
     if rank == 0:
         print(json.dumps({"n_gpus": ws, "ranks_seen": [int(s[0, 0] // 1000) for s in sets],
                           "waypoints_per_track": [len(s) for s in sets], "max_over_ranks": t,
-                          "local_rank": local, "process_group": dist.kind}), file=out_stream, flush=True)
+                          "local_rank": local, "process_group": dist.kind, "comm_n_ranks": dist.n_ranks(),
+                          "per_rank": per_rank}), file=out_stream, flush=True)
     dist.close()
 
 
@@ -331,6 +344,9 @@ def full_plan(dist, rank, reps):
         otg = otp.OnlineTrajGenerator(cps[0], cps[-1], gates, obstacles, path)
         otg.pre_compute_traj(0.0)  # warm-up: allocations, first launches
         state["otg"] = otg
+        # the first call (planner call numbers 0..8): what the cpu_baseline leg's CPU
+        # restatement of the rank-0 track plans (parity)
+        state["first"] = {"wp": np.array(otg.get_waypoints()), "traj": np.array(otg.get_planned_traj())}
 
     def timed():
         per = []
@@ -356,13 +372,14 @@ def full_plan(dist, rank, reps):
         os.unlink(path)
     ms = float(np.mean(per))
     ms_max = dist.max(ms)
+    per_rank = dist.gather(ms)  # every rank's own mean (the headline takes the slowest)
     otg = state["otg"]
     wp = np.ascontiguousarray(otg.get_waypoints())
     traj = otg.get_planned_traj()
     # the exchange step through the product's RCCL communicator (epp_comm_allgather_waypoints):
     # the job's group at N > 1; a one-rank communicator at N = 1
     via = "RCCL (epp_comm_allgather_waypoints)"
-    gather_ms, sets = None, [wp]
+    gather_ms, sets, comm_ranks = None, [wp], None
     if isinstance(dist, RcclGroup):
         comm = dist
     else:
@@ -377,9 +394,13 @@ def full_plan(dist, rank, reps):
         t = time.perf_counter()
         sets = comm.all_gather_waypoints(wp)
         gather_ms = dist.max((time.perf_counter() - t) * 1e3)
+        comm_ranks = comm.n_ranks()  # RCCL's own rank count (epp_comm_rank), not WORLD_SIZE
         if comm is not dist:
             comm.close()
-    return {"ms_per_track": ms_max, "ms_per_track_p50": dist.max(float(np.median(per))), "tracks": dist.ws,
+    return {"_first": state["first"],
+            "ms_per_track": ms_max, "ms_per_track_p50": dist.max(float(np.median(per))), "tracks": dist.ws,
+            "ms_per_track_per_rank": per_rank, "comm_n_ranks": comm_ranks,
+            "collective_timeout_s": getattr(comm, "collective_timeout_s", None),
             "samples_per_segment": PLAN_SAMPLES, "k": 16,
             "segments_per_track": 9, "reps": reps, "waypoints_per_track": [len(x) for x in sets],
             "traj_rows": int(len(traj)), "traj_duration_s": float(traj[-1, 9] - traj[0, 9]),
@@ -446,12 +467,15 @@ def side_measurements(capi, L, stream, geom, cfg, rg, ro):
     s1, s2 = synth.edges(43, 8, lo, hi, n)
     d1, d2 = capi.DeviceBuffer.from_array(s1, stream), capi.DeviceBuffer.from_array(s2, stream)
     dv = capi.DeviceBuffer(n)
+    parity_gpu = {}
     for mode, key in ((0, "c3_motion_analytic"), (1, "c3_motion_discrete32")):
         f = lambda r: w3.check_motions_dev(d1.ptr, d2.ptr, n, 0, mode, dv.ptr, stream=stream)  # noqa: E731
         f(0)
         ms = timed_kernel_ms(capi, stream, f, 10)
         res[key] = {"edges_per_s": n / (ms * 1e-3), "kernel_ms": ms,
                     "hbm_frac": BYTES_PER_EDGE * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        capi.check(L.epp_stream_sync(stream))
+        parity_gpu[key] = dv.download(np.uint8, C3_CPU_EDGES[mode])  # (the prefix the CPU leg checks)
     res["c3_motion_discrete32"]["point_checks_per_s"] = 32 * res["c3_motion_discrete32"]["edges_per_s"]
     # C5 batched: 4096 independent 12-segment refits per launch
     nt = 4096
@@ -468,15 +492,20 @@ def side_measurements(capi, L, stream, geom, cfg, rg, ro):
     ms = timed_kernel_ms(capi, stream, ms_fn, 10)
     res["c5_minsnap_batch"] = {"problems_per_s": nt / (ms * 1e-3), "ms_per_launch": ms, "problems": nt,
                                "segments": 12}
+    capi.check(L.epp_stream_sync(stream))
+    parity_gpu["c5_batch"] = (d_T.download(np.float64, 12 * nt).reshape(nt, 12),
+                              d_C.download(np.float64, 30 * 12 * nt).reshape(nt, 12, 3, 10),
+                              d_st.download(np.int32, nt))
     # C5 single refit latency (host buffers in/out, includes sampling at dt=0.1): the
     # C++ entry through ctypes, 200 calls
     wp1 = tracks[0]
     lat = np.zeros(200)
     for r in range(len(lat)):
         t = time.perf_counter()
-        capi.generate_trajectory(wp1, 1.0, 2.0, 0.1)
+        rows1 = capi.generate_trajectory(wp1, 1.0, 2.0, 0.1)
         lat[r] = time.perf_counter() - t
     res["c5_refit"] = _pct(lat[20:] * 1e6)
+    parity_gpu["c5_refit_rows"] = np.array(rows1)
     # C5 online replanning loop (1000 steps of gate update + A11 + refit + sampling)
     tg = cfg["trajectory_generator_properties"]
     c5cfg, c5path, c5geom, c5g, c5o, wp, window = c5_setup()
@@ -498,11 +527,12 @@ def side_measurements(capi, L, stream, geom, cfg, rg, ro):
     # the same loop's inputs for the CPU leg
     c5_inputs = dict(cfg_path=c5path, geom=c5geom, gates=c5g, obstacles=c5o, wp=wp, window=window,
                      vmax=tg["max_velocity"], amax=tg["max_acceleration"], dt=tg["sampling_interval"],
-                     md=md, native_input=c5_file, cfg=c5cfg)
+                     md=md, native_input=c5_file, cfg=c5cfg, parity_gpu=parity_gpu)
     return res, c5_inputs
 
 
 C5_STEPS = 1000
+C3_CPU_EDGES = {0: 1 << 18, 1: 1 << 16}  # the CPU leg's bounded C3 samples (a prefix of the GPU's edges)
 
 
 def _track_config(samples=PLAN_SAMPLES):
@@ -759,7 +789,7 @@ def host_info():
 CPU_SHARE_THREADS = 16
 
 
-def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None):
+def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None, parity_gpu=None):
     """The CPU oracle (a port of the reference's World / min-snap semantics, kind "port") on
     bounded samples of the same workloads, ~15 s in total:
 
@@ -777,9 +807,11 @@ def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None):
     w = O.world_build(geom, gates, obstacles, rg, ro)
     pts = synth.sample_states(7, lo, hi, N_STATES)
     reps = 0
+    parity_gpu = parity_gpu or {}
+    parity = {}
     t = time.perf_counter()
     while True:
-        O.check_states(w, rg, ro, pts, False, threads=1)
+        ref_flags = O.check_states(w, rg, ro, pts, False, threads=1)
         reps += 1
         if time.perf_counter() - t > 6.0:
             break
@@ -811,15 +843,23 @@ def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None):
            "all_cores_ideal_bound": {"value": reps * N_STATES / dt * (host["nproc"] or 1),
                                      "threads": host["nproc"], "kind": "bound: 1-thread rate x nproc"},
            "states_wide": wide}
+    if "c2_flags" in parity_gpu:  # resident batch 0 = pts (rank 0)
+        parity["c2_state_mismatches"] = int(np.count_nonzero(parity_gpu["c2_flags"] != ref_flags))
+        parity["c2_states_compared"] = int(len(ref_flags))
     # C3 motions: 512 OBBs, the same edge generator as the GPU leg (bounded edge counts)
     g3, o3 = synth.track_world(42, n_obstacles=472)
     w3 = O.world_build(geom, g3, o3, rg, ro)
-    for mode, key, n in ((0, "c3_motion_analytic", 1 << 18), (1, "c3_motion_discrete32", 1 << 16)):
-        s1, s2 = synth.edges(43, 8, lo, hi, n)
+    e1, e2 = synth.edges(43, 8, lo, hi, N_STATES)  # the GPU leg's edges; the CPU checks a prefix
+    for mode, key in ((0, "c3_motion_analytic"), (1, "c3_motion_discrete32")):
+        n = C3_CPU_EDGES[mode]
+        s1, s2 = np.ascontiguousarray(e1[:n]), np.ascontiguousarray(e2[:n])
         t = time.perf_counter()
-        O.check_motions(w3, rg, ro, s1, s2, False, mode, threads=nt)
+        ref3 = O.check_motions(w3, rg, ro, s1, s2, False, mode, threads=nt)
         el = time.perf_counter() - t
         out[key] = {"edges_per_s": n / el, "threads": nt, "edges": n}
+        if key in parity_gpu:
+            parity[f"{key}_mismatches"] = int(np.count_nonzero(parity_gpu[key] != ref3))
+            parity[f"{key}_compared"] = n
         for tw in sorted({32, host["affinity_cpus"] or 1}):  # (edges per thread as at 16 threads)
             b1, b2 = np.tile(s1, (max(1, tw // 16), 1)), np.tile(s2, (max(1, tw // 16), 1))
             t = time.perf_counter()
@@ -843,6 +883,12 @@ def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None):
     wp4, rows4 = TP.plan_track(w4, rg, ro, lo4, hi4, cps, PLAN_SAMPLES, tg["max_velocity"], tg["max_acceleration"],
                                tg["sampling_interval"], threads=nt)
     out["full_plan_ms_per_track"] = (time.perf_counter() - t) * 1e3
+    if "c4_first" in parity_gpu:  # the GPU's first plan of the same track (call numbers 0..8)
+        gw, gt = parity_gpu["c4_first"]["wp"], parity_gpu["c4_first"]["traj"]
+        parity["c4_waypoints_equal"] = bool(gw.shape == wp4.shape and np.array_equal(gw, wp4))
+        same = gt.shape == rows4.shape
+        parity["c4_traj_time_column_equal"] = bool(same and np.array_equal(gt[:, 9], rows4[:, 9]))
+        parity["c4_traj_max_abs"] = float(np.abs(gt[:, :9] - rows4[:, :9]).max()) if same else None
     out["full_plan"] = {"threads": nt, "tracks": 1, "waypoints": int(len(wp4)), "traj_rows": int(len(rows4)),
                         "workload": "C4 rank-0 track: 9 batch plans (65,536 samples, k=16) + includeGates2 + "
                                     "min-snap + sampling, the planner restated on the CPU (oracle/track_planner.py)"}
@@ -875,6 +921,20 @@ def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None):
             el = (time.perf_counter() - t) / reps
             out["c5_minsnap_batch"][f"problems_per_s_{tw}_threads"] = len(tracks) / el
         out["c5_minsnap_batch"]["problems_per_s"] = out["c5_minsnap_batch"][f"problems_per_s_{nt}_threads"]
+        if "c5_batch" in parity_gpu:  # the GPU leg's 4096 problems against the oracle's solves
+            Tg, Cg, sg = parity_gpu["c5_batch"]
+            Tr, Cr, sr = O.minsnap_batch(tracks, 1.0, 2.0, threads=nt)
+            # (success: status 0 on the GPU, a non-negative return code from the oracle)
+            parity["c5_batch_solved_equal"] = bool(np.array_equal(np.asarray(sg) == 0, np.asarray(sr) >= 0))
+            parity["c5_batch_coeff_max_abs"] = float(max(np.abs(Cg[k] - Cr[k]).max() for k in range(len(tracks))))
+            parity["c5_batch_times_max_rel"] = float(max((np.abs(Tg[k] - Tr[k]) / Tr[k]).max()
+                                                         for k in range(len(tracks))))
+        if "c5_refit_rows" in parity_gpu:  # the single refit (native generateTrajectory) vs the oracle's
+            rg1 = parity_gpu["c5_refit_rows"]
+            rr1 = O.generate_trajectory(wp1, 1.0, 2.0, 0.1)
+            same = rg1.shape == rr1.shape
+            parity["c5_refit_time_column_equal"] = bool(same and np.array_equal(rg1[:, 9], rr1[:, 9]))
+            parity["c5_refit_max_abs"] = float(np.abs(rg1[:, :9] - rr1[:, :9]).max()) if same else None
         out["c5_minsnap_batch"]["threads"] = nt
         out["c5_online"]["via"] = "Python (ctypes oracle)"
         # native: the same loops from the same input file, C++ calls into the oracle
@@ -890,6 +950,13 @@ def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None):
         # perturbations (planner on nt threads)
         out["c5_update_gate_pos"] = c5_events(c["cfg_path"], c["geom"], c["gates"], c["obstacles"],
                                               cpu_threads=nt)
+    if parity:
+        parity["ok"] = bool(all(parity.get(k, 0) == 0 for k in parity if k.endswith("_mismatches")) and
+                            all(parity.get(k, True) for k in parity if k.endswith("_equal")) and
+                            all((parity.get(k) is not None and parity[k] <= 1e-6)
+                                for k in parity if k.endswith("_max_abs")))
+        parity["tolerance_f64"] = 1e-6
+        out["parity"] = parity
     return out
 
 

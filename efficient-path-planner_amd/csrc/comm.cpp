@@ -183,6 +183,16 @@ epp_status comm_wait(const Rccl* r, epp_comm* c, const char* what) {
     }
 }
 
+// A result copied to the caller's memory once its collective has completed (comm_wait):
+// nothing is queued ahead of it on the stream, so the copy cannot wait on a peer, and no
+// copy is left in flight into the caller's buffer when the call returns (an aborted
+// collective returns before any copy is queued).
+hipError_t copy_out(epp_comm* c, void* dst, const void* src, size_t bytes) {
+    hipError_t he = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(c->stream);
+    return he;
+}
+
 // Entry check of every collective: an aborted communicator (or one whose abort was
 // requested before the call) fails at once.
 epp_status comm_usable(const Rccl* r, epp_comm* c, const char* what) {
@@ -312,9 +322,12 @@ epp_status epp_comm_allgather_waypoints(epp_comm* c, const double* wp, int32_t n
     if (he != hipSuccess) return hip_fail("epp_comm_allgather_waypoints", he);
     ncclResult_t e = r->allGather(c->d_buf, c->d_buf + 4, 1, ncclInt32, c->comm, c->stream);
     if (e != ncclSuccess) return nccl_error(r, e, "ncclAllGather (counts)");
-    he = hipMemcpyAsync(counts, c->d_buf + 4, (size_t)R * 4, hipMemcpyDeviceToHost, c->stream);
-    if (he != hipSuccess) return hip_fail("epp_comm_allgather_waypoints", he);
+    // the collective is waited for (polled, see comm_wait) BEFORE anything is copied to the
+    // caller's memory: a device-to-host copy into pageable memory queued behind a hung
+    // collective would block this thread inside the runtime, out of comm_wait's reach
     if (const epp_status ws = comm_wait(r, c, "ncclAllGather (counts)")) return ws;
+    if ((he = copy_out(c, counts, c->d_buf + 4, (size_t)R * 4)) != hipSuccess)
+        return hip_fail("epp_comm_allgather_waypoints", he);
     // every rank holds the same counts, so every rank takes the same branch below
     int32_t maxw = 0, failed = -1, n_failed = 0;
     for (int i = 0; i < R; ++i) {
@@ -341,12 +354,11 @@ epp_status epp_comm_allgather_waypoints(epp_comm* c, const double* wp, int32_t n
     if (he != hipSuccess) return hip_fail("epp_comm_allgather_waypoints", he);
     e = r->allGather(d_send, d_recv, (size_t)maxw * 3, ncclFloat64, c->comm, c->stream);
     if (e != ncclSuccess) return nccl_error(r, e, "ncclAllGather (waypoints)");
+    if (const epp_status ws = comm_wait(r, c, "ncclAllGather (waypoints)")) return ws;
     for (int i = 0; i < R && he == hipSuccess; ++i)
-        if (counts[i] > 0)
-            he = hipMemcpyAsync(out + (size_t)i * cap * 3, d_recv + (size_t)i * set_b, (size_t)counts[i] * 24,
-                                hipMemcpyDeviceToHost, c->stream);
+        if (counts[i] > 0) he = copy_out(c, out + (size_t)i * cap * 3, d_recv + (size_t)i * set_b, (size_t)counts[i] * 24);
     if (he != hipSuccess) return hip_fail("epp_comm_allgather_waypoints", he);
-    return comm_wait(r, c, "ncclAllGather (waypoints)");
+    return EPP_OK;
 }
 
 epp_status epp_comm_allreduce_f64(epp_comm* c, double* x, int32_t n, int32_t op) {
@@ -367,9 +379,9 @@ epp_status epp_comm_allreduce_f64(epp_comm* c, double* x, int32_t n, int32_t op)
     const ncclRedOp_t rop = op == EPP_REDUCE_SUM ? ncclSum : op == EPP_REDUCE_MAX ? ncclMax : ncclMin;
     const ncclResult_t e = r->allReduce(c->d_buf, c->d_buf, (size_t)n, ncclFloat64, rop, c->comm, c->stream);
     if (e != ncclSuccess) return nccl_error(r, e, "ncclAllReduce");
-    he = hipMemcpyAsync(x, c->d_buf, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream);
-    if (he != hipSuccess) return hip_fail("epp_comm_allreduce_f64", he);
-    return comm_wait(r, c, "ncclAllReduce");
+    if (const epp_status ws = comm_wait(r, c, "ncclAllReduce")) return ws;
+    if ((he = copy_out(c, x, c->d_buf, (size_t)n * 8)) != hipSuccess) return hip_fail("epp_comm_allreduce_f64", he);
+    return EPP_OK;
 }
 
 epp_status epp_comm_barrier(epp_comm* c) {

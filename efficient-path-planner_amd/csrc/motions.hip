@@ -708,7 +708,7 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
         EPP_MTL_ADD(tl_walk, tl_b);
         flush();
         if (act) valid[i] = flags[lane];
-        if (IDX && mm.count) {  // (launch-uniform)
+        if (IDX && (mm.count || mm.out16)) {  // (launch-uniform)
             const bool keep = act && flags[lane] != 0 && jraw >= 0;
             if (act && flags[lane] == 0) mm.nbr_w[i] = -1;
             if (act && mm.out16) mm.out16[i] = keep ? (uint16_t)jraw : (uint16_t)0xFFFF;
@@ -925,7 +925,7 @@ epp_status epp::check_knn_motions_rows(const epp_world* world, const double* nod
                                        const int32_t* ids32, const int64_t* rows_n, int32_t cap, int32_t k,
                                        int32_t can_pass_gate, uint8_t* valid, uint16_t* out16, int32_t target,
                                        int64_t* count, void* stream) {
-    if (!world || cap < 0 || k <= 0 || (cap > 0 && (!nodes || !rows32 || !ids32 || !rows_n || !valid || !count))) {
+    if (!world || cap < 0 || k <= 0 || (cap > 0 && (!nodes || !rows32 || !ids32 || !rows_n || !valid || (!count && !out16)))) {
         set_error("check_knn_motions_rows: invalid argument");
         return EPP_ERR_INVALID_ARGUMENT;
     }

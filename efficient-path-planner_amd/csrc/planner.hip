@@ -303,15 +303,13 @@ __device__ __forceinline__ long long lb_exclusive(unsigned long long* st, int b,
 // sized for the largest possible cell count (the count itself is on the device); blocks
 // past it exit (no block waits on a later one).
 constexpr int kScanThreads = 256, kScanPer = 16, kScanTile = kScanThreads * kScanPer;
-__global__ __launch_bounds__(kScanThreads) void k_knn_scan(const KnnGrid* __restrict__ gp,
-                                                           const int* __restrict__ cnt,
-                                                           int* __restrict__ start,
-                                                           unsigned long long* __restrict__ st, uint32_t tag) {
+__device__ __forceinline__ void knn_scan_block(const KnnGrid* __restrict__ gp, const int* __restrict__ cnt,
+                                               int* __restrict__ start, unsigned long long* __restrict__ st,
+                                               uint32_t tag, const int b) {
     static_assert(kScanPer % 4 == 0, "16-byte runs");
     __shared__ int wsum[kScanThreads / 64];
     __shared__ int s_excl;
     const int nc = gp->ncell;
-    const int b = blockIdx.x;
     if (b * kScanTile > nc) return;  // (block-uniform; the block holding nc itself writes start[nc])
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int b0 = b * kScanTile + kScanPer * threadIdx.x;
@@ -373,6 +371,12 @@ __global__ __launch_bounds__(kScanThreads) void k_knn_scan(const KnnGrid* __rest
             acc += v[u];
         }
     }
+}
+__global__ __launch_bounds__(kScanThreads) void k_knn_scan(const KnnGrid* __restrict__ gp,
+                                                           const int* __restrict__ cnt,
+                                                           int* __restrict__ start,
+                                                           unsigned long long* __restrict__ st, uint32_t tag) {
+    knn_scan_block(gp, cnt, start, st, tag, blockIdx.x);
 }
 
 __global__ void k_knn_scatter(const double* __restrict__ nodes, int n, const int* __restrict__ cell_of,
@@ -1762,15 +1766,15 @@ constexpr int kCompactThreads = 256;
 constexpr int kCompactRounds = 4;
 constexpr int kCompactChunk = kCompactThreads * kCompactRounds;
 
-__global__ __launch_bounds__(kCompactThreads) void k_compact(const double* __restrict__ xyz,
-                                                             const uint8_t* __restrict__ valid, int64_t n,
-                                                             unsigned long long* __restrict__ st, uint32_t tag,
-                                                             double* __restrict__ out, int64_t* __restrict__ n_out) {
+// (block b of nb; the last block writes *n_out = the valid count + add)
+__device__ __forceinline__ void compact_block(const double* __restrict__ xyz, const uint8_t* __restrict__ valid,
+                                              int64_t n, unsigned long long* __restrict__ st, uint32_t tag,
+                                              double* __restrict__ out, int64_t* __restrict__ n_out, int64_t add,
+                                              const int b, const int nb) {
     constexpr int NW = kCompactThreads / 64;
     __shared__ int wcnt[kCompactRounds * NW];
     __shared__ long long s_excl;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int b = blockIdx.x;
     const int64_t i0 = (int64_t)b * kCompactChunk + threadIdx.x;
     bool v[kCompactRounds];
     unsigned long long bal[kCompactRounds];
@@ -1800,7 +1804,7 @@ __global__ __launch_bounds__(kCompactThreads) void k_compact(const double* __res
         if (lane == 0) {
             if (b > 0) lb_publish(st, b, tag, true, ex + total);
             s_excl = ex;
-            if (b == (int)gridDim.x - 1) *n_out = ex + total;
+            if (b == nb - 1) *n_out = ex + total + add;
         }
     }
     __syncthreads();
@@ -1817,6 +1821,12 @@ __global__ __launch_bounds__(kCompactThreads) void k_compact(const double* __res
             out[3 * p + 2] = xyz[3 * i + 2];
         }
     }
+}
+__global__ __launch_bounds__(kCompactThreads) void k_compact(const double* __restrict__ xyz,
+                                                             const uint8_t* __restrict__ valid, int64_t n,
+                                                             unsigned long long* __restrict__ st, uint32_t tag,
+                                                             double* __restrict__ out, int64_t* __restrict__ n_out) {
+    compact_block(xyz, valid, n, st, tag, out, n_out, 0, blockIdx.x, gridDim.x);
 }
 
 __global__ void k_mask_edges(int32_t* __restrict__ nbr, const uint8_t* __restrict__ valid, int64_t m) {
@@ -1902,6 +1912,295 @@ __global__ __launch_bounds__(256) void k_pack_ellipse_rows(const double* __restr
         for (int c = 0; c < k; c += 4) *reinterpret_cast<int4*>(dst + c) = *reinterpret_cast<const int4*>(src + c);
     } else {
         for (int c = 0; c < k; ++c) dst[c] = src[c];
+    }
+}
+
+// ---- the batched planner: one launch per stage for all of a batch's problems ----------
+// (epp_internal.h, PlanBatchLayout).  Problem p = blockIdx.y of the per-problem stages; its
+// samples at xyz + p ns, its nodes at nodes + p NS (NS = 2^ns_log >= 65536: a node's id in
+// its problem is the low bits of its global id p NS + node, and its low 16 bits when the
+// problem has <= 65535 nodes), its k-NN workspace at kws + p kws_stride (KnnLayout for
+// ns + 2 nodes), its k-NN rows at nbr + p NS k.  Node counts stay on the device.
+struct PlanBatchDev {
+    const PlanSeg* seg;
+    int S, k, ns_log, nbc, cap_total, nctr;
+    int64_t ns, NS, need_cap;
+    double lo[3], hi[3];
+    double* xyz;
+    uint8_t* valid;
+    double* nodes;
+    unsigned long long* cstat;
+    unsigned long long* ctr;
+    char* kws;
+    size_t kws_stride, l_cell, l_sidx, l_sxyz, l_cnt, l_start, l_fill, l_stat;
+    int l_cap, nclr, scan_blocks;
+    int32_t* nbr;
+    int32_t* retry;
+    int32_t* ids32;
+    int32_t* rows32;
+    uint16_t* rows16;
+    uint32_t* mark;
+    double* need;  // 4 doubles per entry: x, y, z, global id (u64 bits)
+};
+
+struct KnnSeg {
+    KnnGrid* g;
+    int* cell_of;
+    int* sidx;
+    double* sxyz;
+    int* cnt;
+    int* start;
+    int* fill;
+    unsigned long long* stat;
+};
+__device__ __forceinline__ KnnSeg knn_seg(const PlanBatchDev& P, int p) {
+    char* b = P.kws + (size_t)p * P.kws_stride;
+    return {reinterpret_cast<KnnGrid*>(b), reinterpret_cast<int*>(b + P.l_cell), reinterpret_cast<int*>(b + P.l_sidx),
+            reinterpret_cast<double*>(b + P.l_sxyz), reinterpret_cast<int*>(b + P.l_cnt),
+            reinterpret_cast<int*>(b + P.l_start), reinterpret_cast<int*>(b + P.l_fill),
+            reinterpret_cast<unsigned long long*>(b + P.l_stat)};
+}
+
+// samples (k_sample_uniform's arithmetic) + clears: the problem's compaction status words
+// and needed-node bits; problem 0 also the batch counters
+__global__ __launch_bounds__(256) void k_pb_sample(PlanBatchDev P) {
+    const int p = blockIdx.y;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < P.nbc) P.cstat[(int64_t)p * P.nbc + i] = 0ull;
+    if (i < (P.NS >> 5)) P.mark[(int64_t)p * (P.NS >> 5) + i] = 0u;
+    if (p == 0 && i < P.nctr) P.ctr[i] = 0ull;
+    if (i >= P.ns) return;
+    const uint64_t seed = P.seg[p].seed;
+    const uint64_t c = (uint64_t)i * 3ull;
+    const double u0 = (double)(splitmix64(seed ^ c) >> 11) * 0x1.0p-53;
+    const double u1 = (double)(splitmix64(seed ^ (c + 1)) >> 11) * 0x1.0p-53;
+    const double u2 = (double)(splitmix64(seed ^ (c + 2)) >> 11) * 0x1.0p-53;
+    double* x = P.xyz + ((int64_t)p * P.ns + i) * 3;
+    x[0] = P.lo[0] + (P.hi[0] - P.lo[0]) * u0;
+    x[1] = P.lo[1] + (P.hi[1] - P.lo[1]) * u1;
+    x[2] = P.lo[2] + (P.hi[2] - P.lo[2]) * u2;
+}
+
+// nodes = start, goal, the valid samples in sample order; ncount[p] = their number
+__global__ __launch_bounds__(kCompactThreads) void k_pb_compact(PlanBatchDev P, uint32_t tag) {
+    const int p = blockIdx.y;
+    double* out = P.nodes + (int64_t)p * P.NS * 3;
+    if (blockIdx.x == 0 && threadIdx.x < 6) out[threadIdx.x] = threadIdx.x < 3 ? P.seg[p].s[threadIdx.x] : P.seg[p].g[threadIdx.x - 3];
+    compact_block(P.xyz + (int64_t)p * P.ns * 3, P.valid + (int64_t)p * P.ns, P.ns, P.cstat + (int64_t)p * P.nbc, tag,
+                  out + 6, reinterpret_cast<int64_t*>(P.ctr) + kPbPerSeg + 3 * P.S + p, 2, blockIdx.x, gridDim.x);
+}
+
+__device__ __forceinline__ int pb_count(const PlanBatchDev& P, int p) {
+    return (int)P.ctr[kPbPerSeg + 3 * P.S + p];
+}
+
+// the problem's grid (knn_grid_shape from its node count, on the device) + cleared counters
+__global__ __launch_bounds__(kBoundsThreads) void k_pb_knn_prep(PlanBatchDev P) {
+    const int p = blockIdx.y;
+    const KnnSeg ks = knn_seg(P, p);
+    for (int i = blockIdx.x * kBoundsThreads + threadIdx.x; i < P.nclr; i += gridDim.x * kBoundsThreads) ks.cnt[i] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const PlanSeg& q = P.seg[p];
+        const double mn[3] = {q.box_lo[0], q.box_lo[1], q.box_lo[2]}, mx[3] = {q.box_hi[0], q.box_hi[1], q.box_hi[2]};
+        KnnGrid gv;
+        knn_grid_shape(mn, mx, pb_count(P, p), P.l_cap, kNodesPerCell, &gv);
+        for (int d = 0; d < 3; ++d) {
+            gv.qs[d] = q.s[d];
+            gv.qg[d] = q.g[d];
+        }
+        gv.qbound = q.bound;
+        *ks.g = gv;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pb_knn_count(PlanBatchDev P) {
+    const int p = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= pb_count(P, p)) return;
+    const KnnSeg ks = knn_seg(P, p);
+    const KnnGrid g = *ks.g;
+    const double* nd = P.nodes + ((int64_t)p * P.NS + i) * 3;
+    const int cx = knn_cell_axis(nd[0], g, 0), cy = knn_cell_axis(nd[1], g, 1), cz = knn_cell_axis(nd[2], g, 2);
+    const int c = (cz * g.dims[1] + cy) * g.dims[0] + cx;
+    ks.cell_of[i] = c;
+    atomicAdd(&ks.cnt[c], 1);
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_pb_knn_scan(PlanBatchDev P, uint32_t tag) {
+    const KnnSeg ks = knn_seg(P, blockIdx.y);
+    knn_scan_block(ks.g, ks.cnt, ks.start, ks.stat, tag, blockIdx.x);
+}
+
+__global__ __launch_bounds__(256) void k_pb_knn_scatter(PlanBatchDev P) {
+    const int p = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= pb_count(P, p)) return;
+    const KnnSeg ks = knn_seg(P, p);
+    const int c = ks.cell_of[i];
+    const int pos = ks.start[c] + atomicAdd(&ks.fill[c], 1);
+    if (pos >= ks.start[c + 1]) return;  // cannot happen with cleared counters
+    const double* nd = P.nodes + ((int64_t)p * P.NS + i) * 3;
+    ks.sidx[pos] = i;
+    ks.sxyz[3 * pos] = nd[0];
+    ks.sxyz[3 * pos + 1] = nd[1];
+    ks.sxyz[3 * pos + 2] = nd[2];
+}
+
+__device__ __forceinline__ double pb_ellipse(const PlanSeg& q, const double* x) {
+    const double ds = sqrt((x[0] - q.s[0]) * (x[0] - q.s[0]) + (x[1] - q.s[1]) * (x[1] - q.s[1]) +
+                           (x[2] - q.s[2]) * (x[2] - q.s[2]));
+    const double dg = sqrt((x[0] - q.g[0]) * (x[0] - q.g[0]) + (x[1] - q.g[1]) * (x[1] - q.g[1]) +
+                           (x[2] - q.g[2]) * (x[2] - q.g[2]));
+    return ds + dg;
+}
+
+// the nodes inside the problem's ellipsoid (widened by 1e-8 relative + 1e-6 m: looser than
+// the packing's test) listed for k_pb_retry, as global ids p NS + node; one atomic per wave
+__global__ __launch_bounds__(256) void k_pb_list(PlanBatchDev P) {
+    const int p = blockIdx.y;
+    const PlanSeg& q = P.seg[p];
+    if (q.cap <= 0) return;  // (block-uniform: no restricted rows for this problem)
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const bool in = i < pb_count(P, p) && pb_ellipse(q, P.nodes + ((int64_t)p * P.NS + i) * 3) <= q.bound * (1.0 + 1e-8) + 1e-6;
+    const unsigned long long bal = __ballot(in);
+    if (!bal) return;
+    const int lane = threadIdx.x & 63, first = __ffsll(bal) - 1;
+    unsigned long long base = 0;
+    if (lane == first) base = atomicAdd(P.ctr + kPbListed, (unsigned long long)__popcll(bal));
+    base = __shfl(base, first, 64);
+    if (in) P.retry[base + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)(((int64_t)p << P.ns_log) + i);
+}
+
+// the listed nodes' exact k-NN rows: one wave per query over its problem's grid (the
+// retry walk of k_knn_tile, knn_retry_wave, with no bound from a tile pass)
+template <int K>
+__global__ __launch_bounds__(64) void k_pb_retry(PlanBatchDev P) {
+    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwaves = (gridDim.x * blockDim.x) >> 6;
+    const int nq = (int)P.ctr[kPbListed];
+    for (int i = wave; i < nq; i += nwaves) {  // wave-uniform
+        const int e = P.retry[i];
+        const int p = e >> P.ns_log, node = e & (int)(P.NS - 1);
+        const KnnSeg ks = knn_seg(P, p);
+        const KnnGrid g = *ks.g;
+        knn_retry_wave<K>(g, 1e300, P.nodes + (int64_t)p * P.NS * 3, ks.sxyz, ks.sidx, ks.start, node, INFINITY,
+                          P.nbr + (int64_t)p * P.NS * K);
+    }
+}
+
+// k_pack_ellipse_rows for every problem at once: the rows of its nodes inside the
+// ellipsoid (widened by 1e-9 relative + 1e-9 m), up to its capacity, packed into global
+// slots with global node ids (a problem's ranks from its own counter, the slots of the
+// accepted ones from the batch's: one atomic each per wave)
+__global__ __launch_bounds__(256) void k_pb_pack(PlanBatchDev P) {
+    const int p = blockIdx.y;
+    const PlanSeg& q = P.seg[p];
+    if (q.cap <= 0) return;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const bool in = i < pb_count(P, p) && pb_ellipse(q, P.nodes + ((int64_t)p * P.NS + i) * 3) <= q.bound * (1.0 + 1e-9) + 1e-9;
+    const unsigned long long bal = __ballot(in);
+    if (!bal) return;
+    const int lane = threadIdx.x & 63, first = __ffsll(bal) - 1;
+    const int cnt = __popcll(bal);
+    unsigned long long base = 0, gbase = 0;
+    if (lane == first) {
+        base = atomicAdd(P.ctr + kPbPerSeg + p, (unsigned long long)cnt);
+        const long long acc = min((long long)cnt, max(0ll, (long long)q.cap - (long long)base));
+        if (acc > 0) gbase = atomicAdd(P.ctr + kPbPacked, (unsigned long long)acc);
+    }
+    base = __shfl(base, first, 64);
+    gbase = __shfl(gbase, first, 64);
+    const int r = __popcll(bal & ((1ull << lane) - 1ull));
+    if (!in || base + r >= (unsigned long long)q.cap) return;
+    const unsigned long long slot = gbase + r;
+    const int64_t off = (int64_t)p << P.ns_log;
+    P.ids32[slot] = (int32_t)(off + i);
+    const int32_t* src = P.nbr + (off + i) * P.k;
+    int32_t* dst = P.rows32 + slot * P.k;
+    for (int c = 0; c < P.k; ++c) {
+        const int32_t v = src[c];
+        dst[c] = v < 0 ? -1 : (int32_t)(off + v);
+    }
+}
+
+// The nodes the packed rows reference (each row's node and its kept neighbours), each once
+// (a bit per node), appended as {x, y, z, id}; and per problem the kept edges of its rows
+// and those into its goal (node 1).  One thread per row entry.
+__global__ __launch_bounds__(256) void k_pb_need(PlanBatchDev P) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t rows = (int64_t)min(P.ctr[kPbPacked], (unsigned long long)P.cap_total);
+    const bool act = e < rows * P.k;
+    const int lane = threadIdx.x & 63;
+    int p = -1;
+    bool keep = false, goal = false;
+    int64_t cand[2] = {-1, -1};  // (global ids to mark: the neighbour, and the row's node once per row)
+    if (act) {
+        const int64_t slot = e / P.k;
+        const int c = (int)(e - slot * P.k);
+        const int32_t u = P.ids32[slot];
+        p = u >> P.ns_log;
+        const uint16_t v = P.rows16[e];
+        keep = v != 0xFFFF;
+        goal = keep && v == 1;
+        if (keep) cand[0] = ((int64_t)p << P.ns_log) + v;
+        if (c == 0) cand[1] = u;
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        bool fresh = false;
+        if (cand[t] >= 0) {
+            const uint32_t bit = 1u << (cand[t] & 31);
+            fresh = !(atomicOr(P.mark + (cand[t] >> 5), bit) & bit);
+        }
+        const unsigned long long bal = __ballot(fresh);
+        if (!bal) continue;
+        const int first = __ffsll(bal) - 1;
+        unsigned long long base = 0;
+        if (lane == first) base = atomicAdd(P.ctr + kPbNeed, (unsigned long long)__popcll(bal));
+        base = __shfl(base, first, 64);
+        if (fresh) {
+            const int64_t at = (int64_t)(base + __popcll(bal & ((1ull << lane) - 1ull)));
+            if (at < P.need_cap) {
+                const double* x = P.nodes + cand[t] * 3;
+                double* d = P.need + at * 4;
+                d[0] = x[0];
+                d[1] = x[1];
+                d[2] = x[2];
+                d[3] = __longlong_as_double((long long)cand[t]);
+            }
+        }
+    }
+    // per-problem edge counts: one atomic per (wave, problem) present in the wave
+    unsigned long long todo = __ballot(act);
+    while (todo) {
+        const int p0 = __shfl(p, __ffsll(todo) - 1, 64);
+        const unsigned long long mine = __ballot(act && p == p0);
+        const int nk = __popcll(mine & __ballot(keep)), ng = __popcll(mine & __ballot(goal));
+        if (lane == __ffsll(mine) - 1) {
+            if (nk) atomicAdd(P.ctr + kPbPerSeg + P.S + p0, (unsigned long long)nk);
+            if (ng) atomicAdd(P.ctr + kPbPerSeg + 2 * P.S + p0, (unsigned long long)ng);
+        }
+        todo &= ~mine;
+    }
+}
+
+// The results into pinned host memory, only the bytes in use: the header (counters), the
+// packed rows' node ids (u32) and masked rows (u16), the needed nodes (32 B each).  16-byte
+// stores (the device parts are 16-byte padded).
+__global__ __launch_bounds__(256) void k_pb_emit(PlanBatchDev P, unsigned long long* __restrict__ hdr,
+                                                  uint4* __restrict__ h_ids, uint4* __restrict__ h_rows,
+                                                  uint4* __restrict__ h_need) {
+    const int64_t rows = (int64_t)min(P.ctr[kPbPacked], (unsigned long long)P.cap_total);
+    const int64_t need = (int64_t)min(P.ctr[kPbNeed], (unsigned long long)P.need_cap);
+    const int64_t c_ids = (rows * 4 + 15) / 16, c_rows = (rows * P.k * 2 + 15) / 16, c_need = need * 2;
+    const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (tid < P.nctr) hdr[tid] = P.ctr[tid];
+    const uint4* d_ids = reinterpret_cast<const uint4*>(P.ids32);
+    const uint4* d_rows = reinterpret_cast<const uint4*>(P.rows16);
+    const uint4* d_need = reinterpret_cast<const uint4*>(P.need);
+    for (int64_t c = tid; c < c_ids + c_rows + c_need; c += (int64_t)gridDim.x * 256) {
+        if (c < c_ids) h_ids[c] = d_ids[c];
+        else if (c < c_ids + c_rows) h_rows[c - c_ids] = d_rows[c - c_ids];
+        else h_need[c - c_ids - c_rows] = d_need[c - c_ids - c_rows];
     }
 }
 
@@ -2205,3 +2504,139 @@ epp_status epp_knn_edges(const double* nodes, const int32_t* nbr, int32_t n, int
 }
 
 }  // extern "C"
+
+// ---- the batched planner's host side (epp_internal.h) ---------------------------------
+epp::PlanBatchLayout epp::plan_batch_layout(int32_t S, int64_t ns, int32_t k, int32_t cap_total) {
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    PlanBatchLayout L;
+    L.S = S;
+    L.k = k;
+    L.ns = ns;
+    L.ns_log = 16;
+    while ((1ll << L.ns_log) < ns + 2) ++L.ns_log;
+    L.NS = 1ll << L.ns_log;
+    L.nbc = (int32_t)std::max<int64_t>(1, (ns + kCompactChunk - 1) / kCompactChunk);
+    L.cap_total = std::max(0, cap_total);
+    L.need_cap = (int64_t)L.cap_total * (k + 1);
+    L.nctr = kPbPerSeg + 4 * S;
+    const KnnLayout kl = knn_layout((int)(ns + 2));
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t at = o;
+        o += al(bytes);
+        return at;
+    };
+    L.o_seg = take((size_t)S * sizeof(PlanSeg));
+    L.o_ctr = take((size_t)L.nctr * 8);
+    L.o_xyz = take((size_t)S * ns * 24);
+    L.o_valid = take((size_t)S * ns);
+    L.o_nodes = take((size_t)S * L.NS * 24);
+    L.o_cstat = take((size_t)S * L.nbc * 8);
+    L.kws_stride = al(kl.bytes);
+    L.o_kws = take((size_t)S * L.kws_stride);
+    L.o_nbr = take((size_t)S * L.NS * k * 4);
+    L.o_retry = take((size_t)S * L.NS * 4);
+    const size_t capr = ((size_t)L.cap_total + 3) & ~size_t(3);
+    L.o_ids32 = take(capr * 4);
+    L.o_rows32 = take(capr * k * 4);
+    L.o_rows16 = take(capr * k * 2);
+    L.o_ev = take(capr * k);
+    L.o_mark = take((size_t)S * (L.NS >> 5) * 4);
+    L.o_need = take((size_t)L.need_cap * 32);
+    L.dev_bytes = o;
+    o = 0;
+    L.h_seg = take((size_t)S * sizeof(PlanSeg));
+    L.h_hdr = take((size_t)L.nctr * 8);
+    L.h_ids = take(capr * 4);
+    L.h_rows = take(capr * k * 2);
+    L.h_need = take((size_t)L.need_cap * 32);
+    L.host_bytes = o;
+    return L;
+}
+
+epp_status epp::plan_batch_launch(const epp_world* world, int32_t can_pass_gate, const double lo[3], const double hi[3],
+                                  const PlanBatchLayout& L, void* dev, void* host, void* stream) {
+    if (!world || !dev || !host || L.S < 1 || L.ns < 1 || (L.k != 4 && L.k != 8 && L.k != 16) ||
+        ((int64_t)L.S << L.ns_log) >= (1ll << 31) || (reinterpret_cast<uintptr_t>(dev) & 255) ||
+        (reinterpret_cast<uintptr_t>(host) & 255)) {
+        set_error("plan_batch_launch: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    char* d = static_cast<char*>(dev);
+    char* h = static_cast<char*>(host);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const KnnLayout kl = knn_layout((int)(L.ns + 2));
+    PlanBatchDev P{};
+    P.seg = reinterpret_cast<const PlanSeg*>(d + L.o_seg);
+    P.S = L.S;
+    P.k = L.k;
+    P.ns_log = L.ns_log;
+    P.nbc = L.nbc;
+    P.cap_total = L.cap_total;
+    P.nctr = L.nctr;
+    P.ns = L.ns;
+    P.NS = L.NS;
+    P.need_cap = L.need_cap;
+    for (int i = 0; i < 3; ++i) {
+        P.lo[i] = lo[i];
+        P.hi[i] = hi[i];
+    }
+    P.xyz = reinterpret_cast<double*>(d + L.o_xyz);
+    P.valid = reinterpret_cast<uint8_t*>(d + L.o_valid);
+    P.nodes = reinterpret_cast<double*>(d + L.o_nodes);
+    P.cstat = reinterpret_cast<unsigned long long*>(d + L.o_cstat);
+    P.ctr = reinterpret_cast<unsigned long long*>(d + L.o_ctr);
+    P.kws = d + L.o_kws;
+    P.kws_stride = L.kws_stride;
+    P.l_cell = kl.cell;
+    P.l_sidx = kl.sidx;
+    P.l_sxyz = kl.sxyz;
+    P.l_cnt = kl.cnt;
+    P.l_start = kl.start;
+    P.l_fill = kl.fill;
+    P.l_stat = kl.stat;
+    P.l_cap = kl.cap;
+    P.nclr = (int)((kl.start - kl.cnt) / sizeof(int));
+    P.scan_blocks = kl.scan_blocks;
+    P.nbr = reinterpret_cast<int32_t*>(d + L.o_nbr);
+    P.retry = reinterpret_cast<int32_t*>(d + L.o_retry);
+    P.ids32 = reinterpret_cast<int32_t*>(d + L.o_ids32);
+    P.rows32 = reinterpret_cast<int32_t*>(d + L.o_rows32);
+    P.rows16 = reinterpret_cast<uint16_t*>(d + L.o_rows16);
+    P.mark = reinterpret_cast<uint32_t*>(d + L.o_mark);
+    P.need = reinterpret_cast<double*>(d + L.o_need);
+    const unsigned S = (unsigned)L.S;
+    // the problems up (pinned), then every stage on this stream
+    if (hipMemcpyAsync(d + L.o_seg, h + L.h_seg, (size_t)L.S * sizeof(PlanSeg), hipMemcpyHostToDevice, s) != hipSuccess)
+        return last("plan_batch_launch");
+    const int64_t clr = std::max<int64_t>({L.ns, L.NS >> 5, (int64_t)L.nbc, (int64_t)L.nctr});
+    hipLaunchKernelGGL(k_pb_sample, dim3((unsigned)((clr + 255) / 256), S), dim3(256), 0, s, P);
+    if (const epp_status st = epp_check_states(world, P.xyz, (int64_t)L.S * L.ns, can_pass_gate, P.valid, nullptr,
+                                               nullptr, stream))
+        return st;
+    hipLaunchKernelGGL(k_pb_compact, dim3((unsigned)L.nbc, S), dim3(kCompactThreads), 0, s, P, next_scan_tag());
+    const unsigned gn = (unsigned)((L.ns + 2 + 255) / 256);
+    hipLaunchKernelGGL(k_pb_knn_prep, dim3(8, S), dim3(kBoundsThreads), 0, s, P);
+    hipLaunchKernelGGL(k_pb_knn_count, dim3(gn, S), dim3(256), 0, s, P);
+    hipLaunchKernelGGL(k_pb_knn_scan, dim3((unsigned)kl.scan_blocks, S), dim3(kScanThreads), 0, s, P, next_scan_tag());
+    hipLaunchKernelGGL(k_pb_knn_scatter, dim3(gn, S), dim3(256), 0, s, P);
+    char* hh = h + L.h_hdr;
+    if (L.cap_total > 0) {
+        hipLaunchKernelGGL(k_pb_list, dim3(gn, S), dim3(256), 0, s, P);
+        const dim3 gr((unsigned)std::max(1, cu_count_planner() * EPP_KNN_RETRY_PER_CU)), br(64);
+        if (L.k == 4) hipLaunchKernelGGL(k_pb_retry<4>, gr, br, 0, s, P);
+        else if (L.k == 8) hipLaunchKernelGGL(k_pb_retry<8>, gr, br, 0, s, P);
+        else hipLaunchKernelGGL(k_pb_retry<16>, gr, br, 0, s, P);
+        hipLaunchKernelGGL(k_pb_pack, dim3(gn, S), dim3(256), 0, s, P);
+        if (const epp_status st = check_knn_motions_rows(
+                world, P.nodes, P.rows32, P.ids32, reinterpret_cast<const int64_t*>(P.ctr + kPbPacked), L.cap_total,
+                L.k, can_pass_gate, reinterpret_cast<uint8_t*>(d + L.o_ev), P.rows16, -1, nullptr, stream))
+            return st;
+        const int64_t ents = (int64_t)L.cap_total * L.k;
+        hipLaunchKernelGGL(k_pb_need, dim3((unsigned)((ents + 255) / 256)), dim3(256), 0, s, P);
+    }
+    hipLaunchKernelGGL(k_pb_emit, dim3((unsigned)std::max(1, cu_count_planner())), dim3(256), 0, s, P,
+                       reinterpret_cast<unsigned long long*>(hh), reinterpret_cast<uint4*>(h + L.h_ids),
+                       reinterpret_cast<uint4*>(h + L.h_rows), reinterpret_cast<uint4*>(h + L.h_need));
+    return last("plan_batch_launch");
+}

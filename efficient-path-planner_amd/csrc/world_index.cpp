@@ -716,7 +716,13 @@ epp_status epp_world_update(epp_world* w, const epp_obb* obbs, int32_t n) {
 
 epp_status epp_world_destroy(epp_world* w) {
     if (!w) return EPP_OK;
+    // the world's own device, whichever device the calling thread has current: its buffers
+    // go to the pool (or are freed) only once no kernel on that device can still read them
+    int prev = 0;
+    const bool restore = hipGetDevice(&prev) == hipSuccess && prev != w->device;
+    if (restore) (void)hipSetDevice(w->device);
     (void)hipDeviceSynchronize();
+    if (restore) (void)hipSetDevice(prev);
     if (epp::pool_give(*w)) {  // kept for the next world (no kernel reads them any more)
         delete w;
         return EPP_OK;

@@ -155,7 +155,18 @@ class Group:
     def sum(self, x: float) -> float:
         return float(self._reduce(np.array([x], np.float64), "sum")[0])
 
+    def gather(self, x: float) -> list[float]:
+        """Every rank's value of x, in rank order (a sum over one-hot vectors)."""
+        v = np.zeros(self.ws, np.float64)
+        v[self.rank] = x
+        return [float(y) for y in self._reduce(v, "sum")]
+
     def all_gather_waypoints(self, wp: np.ndarray | None) -> list[np.ndarray]:
+        raise NotImplementedError
+
+    def n_ranks(self) -> int:
+        """The ranks the group's own communicator reports (RCCL's count on the GPU path),
+        not the launcher's WORLD_SIZE."""
         raise NotImplementedError
 
     def check(self, err: BaseException | None, what: str = "leg") -> None:
@@ -191,6 +202,9 @@ class Solo(Group):
     def _reduce(self, x, op):
         return np.asarray(x, np.float64)
 
+    def n_ranks(self) -> int:
+        return 1
+
     def all_gather_waypoints(self, wp):
         if wp is None:
             raise LegFailed([0], "all-gather: rank 0 reported a failure")
@@ -203,8 +217,11 @@ class RcclGroup(Group):
     rank 0 adds the RCCL unique id; all ranks init only if every rank is ready, else all
     raise — a rank that cannot join never leaves the others inside ncclCommInitRank."""
     kind = "rccl (epp_comm)"
+    # deadline of every collective (epp_comm_set_timeout): a peer that died without an RCCL
+    # asynchronous error fails the job after this long instead of the library's 120 s default
+    COLLECTIVE_TIMEOUT_S = 30.0
 
-    def __init__(self, ws: int, rank: int, timeout: float = 120.0):
+    def __init__(self, ws: int, rank: int, timeout: float = 120.0, collective_timeout_s: float = COLLECTIVE_TIMEOUT_S):
         from eppamd import capi
         self.capi, self.ws, self.rank = capi, ws, rank
         ok, msg, uid = True, "", ""
@@ -224,6 +241,8 @@ class RcclGroup(Group):
             if bad:
                 raise LegFailed(sorted(bad), f"RcclGroup: ranks not ready: {bad}")
         self.comm = capi.Comm(bytes.fromhex(peers[0]["uid"]), ws, rank)
+        self.comm.set_timeout(collective_timeout_s)
+        self.collective_timeout_s = collective_timeout_s
         if ws > 1:
             self.comm.barrier()  # every rank has read the rendezvous files
             if rank == 0:
@@ -231,6 +250,9 @@ class RcclGroup(Group):
 
     def barrier(self) -> None:
         self.comm.barrier()
+
+    def n_ranks(self) -> int:
+        return int(self.comm.n_ranks)  # epp_comm_rank: RCCL's own rank count
 
     def _reduce(self, x, op):
         c = self.capi
@@ -264,6 +286,9 @@ class GlooGroup(Group):
     def barrier(self) -> None:
         if self.ws > 1:
             self.dist.barrier()
+
+    def n_ranks(self) -> int:
+        return int(self.dist.get_world_size()) if self.ws > 1 else 1
 
     def _reduce(self, x, op):
         x = np.asarray(x, np.float64)

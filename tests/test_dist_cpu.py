@@ -75,6 +75,9 @@ def test_bench_spawns_ranks_gloo_ws2():
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["ranks_seen"] == [0, 1] and r["waypoints_per_track"] == [5, 6]
     assert r["max_over_ranks"] == 2.0 and r["local_rank"] == 0
+    # the fields the GPU bench line carries for the multi-GPU leg: the communicator's own
+    # rank count and every rank's value (full_plan.comm_n_ranks / ms_per_track_per_rank)
+    assert r["comm_n_ranks"] == 2 and r["per_rank"] == [1.0, 2.0]
 
 
 def test_bench_rejects_mismatched_world_size():

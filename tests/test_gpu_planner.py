@@ -741,6 +741,45 @@ def test_precompute_traj_equals_cpu_track(track, geom):
     assert np.abs(traj[:, :9] - rows[:, :9]).max() < 1e-6
 
 
+@pytest.fixture(scope="module")
+def bench_track_config(tmp_path_factory):
+    """bench.py's C4 configuration (_track_config): the shipped config with the track
+    bounds [-6,6]^2 x [0,2] and 65,536 samples per segment."""
+    c = json.load(open(CONFIG))
+    c["world_properties"]["lower_bound"] = [-6, -6, 0]
+    c["world_properties"]["upper_bound"] = [6, 6, 2]
+    c["path_planner_properties"]["samples_fmt"] = 65536
+    p = tmp_path_factory.mktemp("c4") / "config.json"
+    p.write_text(json.dumps(c))
+    return str(p), c
+
+
+@pytest.mark.parametrize("world_seed", range(100, 108))
+def test_precompute_traj_bench_tracks_equal_cpu(bench_track_config, geom, world_seed):
+    """The bench's own C4 tracks (world seeds 100..107: rank r plans seed 100 + r, bench.py
+    full_plan) through OnlineTrajGenerator::preComputeTraj with the default row-restricted
+    search, against the CPU restatement of the whole track (oracle/track_planner.py):
+    identical waypoints, trajectory within 1e-6, the time column exact.  Two calls: the
+    first (planner call numbers 0..8) and the second (9..17), as the bench repeats it."""
+    import track_planner as TP
+    path, c = bench_track_config
+    gates, obstacles = synth.track_world(world_seed)
+    cps0 = synth.gate_checkpoints(gates, geom.gate_height, 0.55)
+    otg = _ot().OnlineTrajGenerator(cps0[0], cps0[-1], gates, obstacles, path)
+    rg, ro = config.inflate_radii(c)
+    w = O.world_build(geom, gates, obstacles, rg, ro)
+    lo, hi = np.array(c["world_properties"]["lower_bound"], float), np.array(c["world_properties"]["upper_bound"], float)
+    tg = c["trajectory_generator_properties"]
+    for first_call in (0, 9):
+        otg.pre_compute_traj(0.0)
+        wp, rows = TP.plan_track(w, rg, ro, lo, hi, otg.get_checkpoints(), 65536, tg["max_velocity"],
+                                 tg["max_acceleration"], tg["sampling_interval"], threads=16, first_call=first_call)
+        assert np.array_equal(otg.get_waypoints(), wp), (world_seed, first_call)
+        traj = otg.get_planned_traj()
+        assert traj.shape == rows.shape and np.array_equal(traj[:, 9], rows[:, 9])
+        assert np.abs(traj[:, :9] - rows[:, :9]).max() < 1e-6
+
+
 # ---- multi-GPU: the exchange step (RCCL) and planTracks -----------------------------
 def test_comm_single_rank_allgather():
     """epp_comm_* on one rank (the box has one GPU): the all-gather returns the rank's own
