@@ -225,6 +225,8 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["edges_valid"] = s.edges_valid;
             d["attempts"] = s.attempts;
             d["rows_downloaded"] = s.rows_downloaded;
+            d["restricted_rows"] = s.restricted_rows;
+            d["fallbacks"] = s.fallbacks;
             d["ms"] = s.ms;
             d["ms_device"] = s.ms_device;
             d["ms_search"] = s.ms_search;
@@ -388,6 +390,8 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["ms_search"] = s.ms_search;
             d["attempts"] = s.attempts;
             d["rows_downloaded"] = s.rows_downloaded;
+            d["restricted_rows"] = s.restricted_rows;
+            d["fallbacks"] = s.fallbacks;
             return d;
         })
         .def("get_checkpoints", [](const epp::OnlineTrajGenerator& self) {

@@ -120,34 +120,39 @@ epp_status check_knn_motions_rows(const epp_world* world, const double* nodes, i
 // Stages: sample -> state check -> ordered compaction (start, goal, valid samples) -> k-NN
 // grid (count, scan, scatter) -> the rows of the nodes inside each problem's ellipsoid
 // |x - s| + |x - g| <= bound, one wave per listed node -> packed rows -> their motion checks
-// (failed edges masked) -> the nodes those rows reference -> one emit into pinned host
-// memory.  Node counts stay on the device: no host round trip before the emit.
-struct PlanSeg {                  // one problem (host -> device, 128 B)
+// (failed edges masked) -> the nodes those rows reference, renumbered per problem in a
+// compact index (0 = start, 1 = goal) -> one emit into pinned host memory.  Node counts stay
+// on the device: no host round trip before the emit.
+struct PlanSeg {                  // one problem (host -> device)
     uint64_t seed;                // the attempt's sampler seed
     double s[3], g[3];            // start, goal: nodes 0 and 1
     double box_lo[3], box_hi[3];  // k-NN grid box (the sampling box widened by s and g)
     double bound;                 // restricted rows: |x - s| + |x - g| <= bound
+    int64_t need_off;             // first slot of its referenced-node list
     int32_t cap;                  // packed-row capacity (0: no restricted rows)
-    int32_t pad_;
+    int32_t need_cap;             // referenced-node list capacity
 };
 // Header words of the emitted results (u64): [0] listed k-NN queries, [1] packed rows,
-// [2] nodes emitted, then per problem p: [3 + p] its packed rows (uncapped),
-// [3 + S + p] kept edges of its rows, [3 + 2S + p] kept edges into its goal (node 1),
-// [3 + 3S + p] its node count (valid samples + 2).
-enum : int { kPbListed = 0, kPbPacked = 1, kPbNeed = 2, kPbPerSeg = 3 };
+// then per problem p: [3 + p] its packed rows (uncapped), [3 + S + p] kept edges of its
+// rows, [3 + 2S + p] kept edges into its goal (node 1), [3 + 3S + p] its node count (valid
+// samples + 2), [3 + 4S + p] its referenced nodes (compact indices 0 .. that - 1).
+enum : int { kPbListed = 0, kPbPacked = 1, kPbPerSeg = 3 };
 struct PlanBatchLayout {
     int32_t S = 0, k = 0, ns_log = 0, nbc = 0, cap_total = 0, nctr = 0;
-    int64_t ns = 0, NS = 0, need_cap = 0;  // samples per problem, node stride (2^ns_log >= 65536)
+    int64_t ns = 0, NS = 0, need_cap = 0;  // samples per problem, node stride (2^ns_log >= 65536),
+                                          // referenced-node slots of all problems
     // device workspace (bytes from its base, 256-B aligned parts)
     size_t o_seg = 0, o_ctr = 0, o_xyz = 0, o_valid = 0, o_nodes = 0, o_cstat = 0, o_kws = 0, kws_stride = 0,
-           o_nbr = 0, o_retry = 0, o_ids32 = 0, o_rows32 = 0, o_rows16 = 0, o_ev = 0, o_mark = 0, o_need = 0,
-           dev_bytes = 0;
-    // pinned host block: the problems (uploaded), then the emitted header, row node ids
-    // (u32, global = p NS + node), masked rows (u16 local ids, 0xFFFF: no edge) and nodes
-    // ({x, y, z, global id as u64} per referenced node)
-    size_t h_seg = 0, h_hdr = 0, h_ids = 0, h_rows = 0, h_need = 0, host_bytes = 0;
+           o_nbr = 0, o_retry = 0, o_ids32 = 0, o_rows32 = 0, o_rows16 = 0, o_ev = 0, o_mark = 0, o_map = 0,
+           o_slot = 0, o_need = 0, dev_bytes = 0;
+    // pinned host block: the problems (uploaded), then the emitted header, per packed row
+    // (slot) its problem and node (p << 16 | compact index), the masked rows (compact
+    // indices, 0xFFFF: no edge) and each problem's referenced nodes ({x, y, z, node id as
+    // u64} at need_off + compact index)
+    size_t h_seg = 0, h_hdr = 0, h_slot = 0, h_rows = 0, h_need = 0, host_bytes = 0;
 };
-PlanBatchLayout plan_batch_layout(int32_t S, int64_t ns, int32_t k, int32_t cap_total);
+// caps[p]: the problems' packed-row capacities (need_off / need_cap are filled in here)
+PlanBatchLayout plan_batch_layout(int32_t S, int64_t ns, int32_t k, PlanSeg* segs);
 epp_status plan_batch_launch(const epp_world* world, int32_t can_pass_gate, const double lo[3], const double hi[3],
                              const PlanBatchLayout& L, void* dev, void* host, void* stream);
 }  // namespace epp

@@ -86,6 +86,18 @@ PathPlanner::PathPlanner(const Matrix& gates, const Matrix& obstacles, std::shar
     : configParser(std::move(cp)) {
     worldPtr = std::make_shared<World>(configParser);
     parseGatesAndObstacles(gates, obstacles);  // src/PathPlanner.cpp:27-35
+    // knobs of this build, read once: EPP_PLAN_ELLIPSE the row-restricted search's bound
+    // factor (0: the whole table only; else >= 1), EPP_PLAN_THREADS the planner threads
+    if (const char* ev = std::getenv("EPP_PLAN_ELLIPSE")) {
+        char* end = nullptr;
+        const double f = std::strtod(ev, &end);
+        if (end != ev && *end == '\0' && (f == 0.0 || f >= 1.0)) ellipse_ = f;
+        else std::cerr << "PathPlanner: EPP_PLAN_ELLIPSE=" << ev << " ignored (0, or a factor >= 1)" << std::endl;
+    }
+    if (const char* tv = std::getenv("EPP_PLAN_THREADS")) {
+        const int t = std::atoi(tv);
+        if (t >= 1 && t <= 64) threads_ = t;
+    }
     // the device world (index build, its HBM and pinned buffers, the upload) now, as the
     // reference builds its World here, not inside the first planPath
     (void)worldPtr->device();
@@ -115,105 +127,403 @@ void PathPlanner::updateGatePos(int gateId, const std::vector<double>& newPose) 
     worldPtr->updateGatePosition(gateId, newPose);  // src/PathPlanner.cpp:170-173
 }
 
-bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples, uint64_t seed,
-                           std::vector<Vec3>& out) const {
+namespace {
+// Per calling thread: the batched planner's device workspace, pinned host block and stream
+// (grown geometrically; freeing pinned memory synchronises the device).
+class BatchScratch {
+public:
+    static BatchScratch& get() {
+        thread_local BatchScratch b;
+        return b;
+    }
+    void ensure(size_t dev_bytes, size_t host_bytes) {
+        if (dev_bytes > dcap_) {
+            dev_bytes = std::max(dev_bytes, dcap_ + dcap_ / 2);
+            if (dev_) epp_free(dev_);
+            dev_ = nullptr;
+            dcap_ = 0;
+            check(epp_malloc(&dev_, dev_bytes), "planner batch workspace");
+            dcap_ = dev_bytes;
+        }
+        if (host_bytes > hcap_) {
+            host_bytes = std::max(host_bytes, hcap_ + hcap_ / 2);
+            if (host_) (void)hipHostFree(host_);
+            host_ = nullptr;
+            hcap_ = 0;
+            if (hipHostMalloc(&host_, host_bytes, hipHostMallocDefault) != hipSuccess) {
+                host_ = nullptr;
+                throw std::runtime_error("planner batch: hipHostMalloc failed");
+            }
+            hcap_ = host_bytes;
+        }
+    }
+    void* dev() const { return dev_; }
+    char* host() const { return static_cast<char*>(host_); }
+    void* stream() {
+        if (!stream_) check(epp_stream_create(&stream_), "stream");
+        return stream_;
+    }
+    ~BatchScratch() {
+        if (dev_) epp_free(dev_);
+        if (host_) (void)hipHostFree(host_);
+        if (stream_) epp_stream_destroy(stream_);
+    }
+
+private:
+    void* dev_ = nullptr;
+    void* host_ = nullptr;
+    void* stream_ = nullptr;
+    size_t dcap_ = 0, hcap_ = 0;
+};
+
+// A*'s state per host thread, reused across searches: an entry counts only when its stamp
+// is the search's (no O(n) clearing per search); the heap keeps its storage.
+struct QE {
+    double f;
+    int key;  // the node id: ties in f pop the lower id first, as std::priority_queue<pair<double, int>,
+              // ..., std::greater<>> does
+    int v;    // the search's own index of the node
+};
+struct QECmp {
+    bool operator()(const QE& a, const QE& b) const { return b.f < a.f || (!(a.f < b.f) && b.key < a.key); }
+};
+struct SearchState {
+    std::vector<double> dist;
+    std::vector<int> prev;
+    std::vector<uint32_t> seen, done;  // stamps: dist/prev valid, closed
+    std::vector<QE> heap;
+    uint32_t cur = 0;
+    void begin(size_t n) {
+        if (dist.size() < n) {
+            dist.resize(n);
+            prev.resize(n);
+            seen.resize(n, 0u);
+            done.resize(n, 0u);
+        }
+        if (++cur == 0u) {  // (stamp wrap-around: clear once)
+            std::fill(seen.begin(), seen.end(), 0u);
+            std::fill(done.begin(), done.end(), 0u);
+            cur = 1u;
+        }
+        heap.clear();
+    }
+    int prev_of(int v) const { return seen[v] == cur ? prev[v] : -1; }
+};
+
+// A* from node 0 to node 1 with the Euclidean distance to the goal (admissible and
+// consistent for Euclidean edge costs).  pos(v): coordinates; key(v): the node id that
+// breaks ties; expand(u, f, relax) calls relax(v) for u's edges and returns false to abort
+// (the caller then takes another graph).  Returns 1 (goal closed), 0 (exhausted), -1
+// (aborted).
+template <class Pos, class Key, class Expand>
+int astar(SearchState& ss, size_t nv, Pos&& pos, Key&& key, Expand&& expand) {
+    ss.begin(nv);
+    const QECmp cmp;
+    std::vector<QE>& q = ss.heap;
+    const Vec3 gp = pos(1);
+    auto push = [&](QE e) {
+        q.push_back(e);
+        std::push_heap(q.begin(), q.end(), cmp);
+    };
+    ss.seen[0] = ss.cur;
+    ss.dist[0] = 0.0;
+    ss.prev[0] = -1;
+    push({(pos(0) - gp).norm(), key(0), 0});
+    while (!q.empty()) {
+        const QE top = q.front();
+        std::pop_heap(q.begin(), q.end(), cmp);
+        q.pop_back();
+        const int u = top.v;
+        if (ss.done[u] == ss.cur) continue;
+        const Vec3 pu = pos(u);
+        auto relax = [&](int v) {
+            if (ss.done[v] == ss.cur) return;
+            const Vec3 pv = pos(v);
+            const double nd = ss.dist[u] + (pv - pu).norm();
+            if (!(ss.seen[v] == ss.cur) || nd < ss.dist[v]) {
+                ss.seen[v] = ss.cur;
+                ss.dist[v] = nd;
+                ss.prev[v] = u;
+                push({nd + (pv - gp).norm(), key(v), v});
+            }
+        };
+        if (!expand(u, top.f, relax, /*closing=*/false)) return -1;
+        ss.done[u] = ss.cur;
+        if (u == 1) return 1;
+        expand(u, top.f, relax, /*closing=*/true);
+    }
+    return 0;
+}
+}  // namespace
+
+// One attempt for a batch of problems (the same sample count; their own seeds):
+// the device stages in one launch each (plan_batch_launch), then per problem, on the
+// planner threads, A* over its emitted rows (the row-restricted search) or, when that
+// cannot decide, over the whole k-NN table of its nodes; then one batched shortcut.
+void PathPlanner::planAttempt(const std::vector<std::pair<Vec3, Vec3>>& problems, const std::vector<uint64_t>& seeds,
+                              int64_t samples, std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const {
+    const size_t np = problems.size();
+    paths.assign(np, {});
+    ok.assign(np, 0);
+    for (size_t b0 = 0; b0 < np; b0 += 64) {  // (at most 64 problems per launch set)
+        const size_t b1 = std::min(np, b0 + 64);
+        std::vector<std::pair<Vec3, Vec3>> sub(problems.begin() + b0, problems.begin() + b1);
+        std::vector<uint64_t> sseeds(seeds.begin() + b0, seeds.begin() + b1);
+        std::vector<std::vector<Vec3>> sp;
+        std::vector<char> so;
+        planChunk(sub, sseeds, samples, sp, so);
+        for (size_t i = b0; i < b1; ++i) {
+            paths[i] = std::move(sp[i - b0]);
+            ok[i] = so[i - b0];
+        }
+    }
+}
+
+void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, const std::vector<uint64_t>& seeds,
+                            int64_t samples, std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const {
     const auto& pp = configParser->getPathPlannerProperties();
     const auto& wp = configParser->getWorldProperties();
     const bool canPass = pp.canPassGate;  // validators get can_pass_gate  src/PathPlanner.cpp:47-50
     const epp_world* w = worldPtr->device();
     const int k = k_;
-    ThreadScratch& ts = ThreadScratch::get();
-    void* st = ts.stream();
+    const int S = (int)problems.size();
     const auto t_dev0 = std::chrono::steady_clock::now();
-    // ---- 1. sample + validate states (StateValidator::isValid), all on the device ------
-    // nodes = start, goal, then the valid samples in sample order (ordered compaction)
-    const size_t n_s = (size_t)samples;
-    const size_t max_nodes = n_s + 2;
-    const size_t m_max = max_nodes * (size_t)k;
-    const size_t ws_bytes = (size_t)epp_knn_workspace_size((int32_t)max_nodes);
-    const size_t cws_bytes = (size_t)epp_compact_workspace_size((int64_t)n_s);
-    ts.reset(ThreadScratch::rounded(n_s * 24) + ThreadScratch::rounded(n_s) + ThreadScratch::rounded(256 + max_nodes * 24) +
-             ThreadScratch::rounded(8) + ThreadScratch::rounded(16) + ThreadScratch::rounded(m_max * 4) + 2 * ThreadScratch::rounded(m_max * 24) +
-             ThreadScratch::rounded(m_max) + ThreadScratch::rounded(ws_bytes) + ThreadScratch::rounded(cws_bytes));
-    double* d_s = static_cast<double*>(ts.carve(n_s * 24));
-    uint8_t* d_v = static_cast<uint8_t*>(ts.carve(n_s));
-    // [.. | edge counts (16 B) | 32 B | start, goal, the valid samples]: the counters and
-    // the two end nodes are set by one upload (no separate clearing of the counters)
-    char* d_head = static_cast<char*>(ts.carve(256 + max_nodes * 24));
-    double* d_nodes = reinterpret_cast<double*>(d_head + 256);
-    int64_t* d_ecnt = reinterpret_cast<int64_t*>(d_head + 256 - 48);
-    int64_t* d_cnt = static_cast<int64_t*>(ts.carve(8));
-    int32_t* d_nbr = static_cast<int32_t*>(ts.carve(m_max * 4));
-    double* d_e1 = static_cast<double*>(ts.carve(m_max * 24));
-    double* d_e2 = static_cast<double*>(ts.carve(m_max * 24));
-    uint8_t* d_ev = static_cast<uint8_t*>(ts.carve(m_max));
-    void* d_ws = ts.carve(ws_bytes);
-    void* d_cws = ts.carve(cws_bytes);
     const double lo[3] = {wp.lowerBound.x, wp.lowerBound.y, wp.lowerBound.z};
     const double hi[3] = {wp.upperBound.x, wp.upperBound.y, wp.upperBound.z};
-    const double ends[6] = {start.x, start.y, start.z, goal.x, goal.y, goal.z};
-    // (the sampler also zeroes the compaction's look-back status words)
-    check(sample_uniform_and_clear(seed, lo, hi, samples, d_s, d_cws, cws_bytes, st), "sample");
-    check(epp_check_states(w, d_s, samples, canPass ? 1 : 0, d_v, nullptr, nullptr, st), "state check");
-    check(compact_states_cleared(d_s, d_v, samples, d_nodes + 6, d_cnt, d_cws, cws_bytes, st), "compact");
-    // start / goal up, the valid-state count down: both queued, one synchronisation
-    // (pinned staging: [ends (6 doubles) | count | edge counts (2)])
-    // pinned staging: [edge counts = 0 (2) | pad (4) | ends (6) | count | edge counts (2)]
-    double* h_small = static_cast<double*>(ts.pinned(2, 16 * sizeof(double)));
-    std::fill(h_small, h_small + 6, 0.0);
-    std::copy(ends, ends + 6, h_small + 6);
-    int64_t* h_cnt = reinterpret_cast<int64_t*>(h_small + 12);
-    check(epp_memcpy_h2d_async(d_ecnt, h_small, 12 * sizeof(double), st), "upload");
-    check(epp_memcpy_d2h_async(h_cnt, d_cnt, 8, st), "download");
-    check(epp_stream_sync(st), "sync");
-    const int64_t n_valid_states = h_cnt[0];
-    const int32_t n = (int32_t)(n_valid_states + 2);
-    // the node coordinates (final now) go down on the copy stream while the k-NN and the
-    // motion checks run on this one (pinned staging sized for the attempt's largest node
-    // count: a pinned buffer that grows is freed, and hipHostFree waits for the device)
-    void* cst = ts.copy_stream();
-    const double* nodes = static_cast<const double*>(ts.pinned(0, max_nodes * 24));
-    check(epp_memcpy_d2h_async(const_cast<double*>(nodes), d_nodes, (uint64_t)n * 24, cst), "download");
-    // ---- 2. k-NN graph + batched motion checks (MotionValidator::checkMotion) --------
-    const size_t m = (size_t)n * k;
-    // the grid over the sampling box widened by start and goal (every node lies inside)
-    const double blo[3] = {std::min({lo[0], start.x, goal.x}), std::min({lo[1], start.y, goal.y}),
-                           std::min({lo[2], start.z, goal.z})};
-    const double bhi[3] = {std::max({hi[0], start.x, goal.x}), std::max({hi[1], start.y, goal.y}),
-                           std::max({hi[2], start.z, goal.z})};
-    // Row-restricted search first (narrow tables, n <= 65535): the k-NN rows, motion checks
-    // and download only for the nodes in the ellipsoid |x - start| + |x - goal| <= bound.
-    // A* pops nodes in increasing f = g + h >= |x - start| + |x - goal|, so a search that
-    // reaches the goal with every popped f <= bound has expanded only rows held here, and
-    // pops exactly what the search over the whole table pops (a node outside the ellipsoid
-    // has f > bound >= the path's length): the same path.  Otherwise (bound passed, rows past
-    // the packing capacity, no forward edge into the goal among the rows) the whole table
-    // is built, checked and searched, as without the restriction.
-    // bound = factor * |start - goal| + 0.25 m; EPP_PLAN_ELLIPSE sets the factor (default
-    // 1.5; 0 = the whole table only).
-    const bool narrow = n <= 65535;
-    double factor = 1.5;
-    if (const char* ev = std::getenv("EPP_PLAN_ELLIPSE")) factor = std::atof(ev);
-    const double d_sg = (goal - start).norm();
-    const double bound = factor * d_sg + 0.25;
-    // packing capacity: 1.25 x the expected rows (the ellipsoid's volume, unclipped, over the
-    // sampling box's) + 1024; not worth it past half the table
-    int32_t cap = 0;
-    if (narrow && factor >= 1.0 && n > 2048) {
-        const double vbox = (hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]);
-        const double vell = M_PI * bound * (bound * bound - d_sg * d_sg) / 6.0;
-        const double frac = vbox > 0 ? std::min(1.0, vell / vbox) : 1.0;
-        const double want = 1.25 * frac * n + 1024.0;
-        if (want < 0.5 * n) cap = (int32_t)want;
+    // ---- the problems: seeds, ends, the k-NN box, the restricted rows' ellipsoid -------
+    // Row-restricted search: A* pops nodes in increasing f = g + h >= |x - start| + |x - goal|,
+    // so a search that reaches the goal with every popped f <= bound has expanded only
+    // nodes inside the ellipsoid |x - start| + |x - goal| <= bound, and pops exactly what the
+    // search over the whole table pops (a node outside has f > bound >= the path's length):
+    // the same path.  bound = ellipse_ * |start - goal| + 0.25 m; capacity 1.25 x the
+    // ellipsoid's expected rows (its volume, unclipped, over the sampling box's) + 1024, not
+    // past half the nodes.  Otherwise (a pop above the bound, rows past the capacity, no kept
+    // edge into the goal among the rows, more than 65,535 nodes) the whole table is built.
+    const int64_t nmax = samples + 2;
+    const bool restrict_ok = ellipse_ >= 1.0 && (k == 4 || k == 8 || k == 16) && nmax <= 4 * 65536;
+    std::vector<PlanSeg> segs(S);
+    for (int p = 0; p < S; ++p) {
+        const Vec3& s = problems[p].first;
+        const Vec3& g = problems[p].second;
+        PlanSeg& q = segs[p];
+        q = PlanSeg{};
+        q.seed = seeds[p];
+        for (int d = 0; d < 3; ++d) {
+            q.s[d] = s[d];
+            q.g[d] = g[d];
+            // the grid over the sampling box widened by start and goal (every node lies inside)
+            q.box_lo[d] = std::min({lo[d], s[d], g[d]});
+            q.box_hi[d] = std::max({hi[d], s[d], g[d]});
+        }
+        const double d_sg = (g - s).norm();
+        q.bound = ellipse_ * d_sg + 0.25;
+        q.cap = 0;
+        if (restrict_ok) {
+            const double vbox = (hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]);
+            const double vell = M_PI * q.bound * (q.bound * q.bound - d_sg * d_sg) / 6.0;
+            const double frac = vbox > 0 ? std::min(1.0, vell / vbox) : 1.0;
+            const double want = 1.25 * frac * (double)nmax + 1024.0;
+            if (want < 0.5 * (double)nmax) q.cap = (int32_t)want;
+        }
     }
-    // packed buffers in d_e2 (free on this path): [ids16 | rows16] (the download), ids32, rows32
-    const size_t ids_pad = ((size_t)cap + 7) & ~(size_t)7;  // (16-B aligned rows)
-    uint16_t* d_ids16 = reinterpret_cast<uint16_t*>(d_e2);
-    uint16_t* d_rows16 = d_ids16 + ids_pad;
-    const size_t pack_bytes = (ids_pad + (size_t)cap * k) * 2;
-    int32_t* d_ids32 = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(d_e2) + ((pack_bytes + 255) & ~(size_t)255));
-    int32_t* d_rows32 = d_ids32 + ids_pad;
-    void* h_tab = ts.pinned(1, m_max * 4);
+    const PlanBatchLayout L = plan_batch_layout(S, samples, k, segs.data());
+    BatchScratch& bs = BatchScratch::get();
+    bs.ensure(L.dev_bytes, L.host_bytes);
+    char* H = bs.host();
+    std::memcpy(H + L.h_seg, segs.data(), sizeof(PlanSeg) * S);
+    void* st = bs.stream();
+    check(plan_batch_launch(w, canPass ? 1 : 0, lo, hi, L, bs.dev(), H, st), "planner batch");
+    check(epp_stream_sync(st), "sync");
+    const uint64_t* hdr = reinterpret_cast<const uint64_t*>(H + L.h_hdr);
+    const uint32_t* slots = reinterpret_cast<const uint32_t*>(H + L.h_slot);
+    const uint16_t* rows = reinterpret_cast<const uint16_t*>(H + L.h_rows);
+    const double* need = reinterpret_cast<const double*>(H + L.h_need);
+    const int64_t R = (int64_t)std::min<uint64_t>(hdr[kPbPacked], (uint64_t)L.cap_total);
+    const double ms_batch = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_dev0).count();
+    const char* dev = static_cast<const char*>(bs.dev());
+
+    // ---- per problem: the restricted search, else the whole table ----------------------
+    struct Out {
+        int64_t n = 0, edges_checked = 0, edges_valid = 0, rows_down = 0, restricted_rows = 0;
+        int fallback = 0;  // 1: the whole table after the restricted rows could not decide
+        double ms_dev = 0, ms_search = 0;
+    };
+    std::vector<Out> res(S);
+    std::vector<std::vector<Vec3>> raw(S);
+    std::vector<char> found(S, 0);
+    std::vector<std::exception_ptr> err(S);
+    auto solve = [&](int p) {
+        Out& o = res[p];
+        const int64_t n = (int64_t)hdr[kPbPerSeg + 3 * S + p];
+        o.n = n;
+        const int64_t packed = (int64_t)hdr[kPbPerSeg + p];
+        const int64_t m = (int64_t)std::min<uint64_t>(hdr[kPbPerSeg + 4 * S + p], (uint64_t)segs[p].need_cap);
+        const auto t0 = std::chrono::steady_clock::now();
+        int r = 0;
+        if (segs[p].cap > 0 && n <= 65535 && packed <= segs[p].cap && hdr[kPbPerSeg + 2 * S + p] > 0 && m >= 2) {
+            // this problem's rows (slot order) and referenced nodes (compact index order)
+            const double* nd = need + 4 * segs[p].need_off;
+            thread_local std::vector<int32_t> row_of;
+            row_of.assign((size_t)m, -1);
+            for (int64_t sl = 0; sl < R; ++sl)
+                if ((int)(slots[sl] >> 16) == p) row_of[slots[sl] & 0xFFFFu] = (int32_t)sl;
+            thread_local SearchState ss;
+            const double bound = segs[p].bound;
+            auto pos = [&](int v) { return Vec3(nd[4 * v], nd[4 * v + 1], nd[4 * v + 2]); };
+            auto key = [&](int v) {
+                int64_t id;
+                std::memcpy(&id, nd + 4 * v + 3, 8);
+                return (int)id;
+            };
+            r = astar(ss, (size_t)m, pos, key, [&](int u, double f, auto&& relax, bool closing) {
+                if (!closing) return (f <= bound) && row_of[u] >= 0;
+                const uint16_t* row = rows + (size_t)row_of[u] * k;
+                for (int c = 0; c < k; ++c)
+                    if (row[c] != 0xFFFF) relax((int)row[c]);
+                return true;
+            });
+            o.restricted_rows = packed;
+            if (r == 1) {
+                std::vector<Vec3> path;
+                for (int v = 1; v >= 0; v = ss.prev_of(v)) path.push_back(pos(v));
+                std::reverse(path.begin(), path.end());
+                raw[p] = std::move(path);
+                found[p] = 1;
+                o.edges_checked = packed * k;
+                o.edges_valid = (int64_t)hdr[kPbPerSeg + S + p];
+                o.rows_down = packed;
+            }
+        }
+        o.ms_search += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (r != 1) {
+            o.fallback = segs[p].cap > 0 ? 1 : 0;
+            const double* d_nodes = reinterpret_cast<const double*>(dev + L.o_nodes) + (size_t)p * L.NS * 3;
+            found[p] = wholeTableSearch(d_nodes, (int32_t)n, segs[p].box_lo, segs[p].box_hi, raw[p], o.edges_checked,
+                                        o.edges_valid, o.ms_dev, o.ms_search)
+                           ? 1
+                           : 0;
+            o.rows_down += n;
+        }
+    };
+    auto run = [&](int p) {
+        try {
+            solve(p);
+        } catch (...) {
+            err[p] = std::current_exception();
+        }
+    };
+    // W concurrent solvers (the caller + W - 1 pool threads) pull problems in order
+    const size_t W = std::min((size_t)S, (size_t)std::max(1, threads_));
+    if (W <= 1) {
+        for (int p = 0; p < S; ++p) run(p);
+    } else {
+        int devno = 0;
+        if (hipGetDevice(&devno) != hipSuccess) devno = 0;
+        std::atomic<int> next{0};
+        auto drain = [&] {
+            for (int p = next++; p < S; p = next++) run(p);
+        };
+        std::mutex done_mu;
+        std::condition_variable done_cv;
+        size_t pending = W - 1;
+        for (size_t t = 1; t < W; ++t)
+            plan_pool().submit([&, devno] {
+                (void)hipSetDevice(devno);
+                drain();
+                std::lock_guard<std::mutex> lk(done_mu);
+                if (--pending == 0) done_cv.notify_all();
+            });
+        drain();
+        std::unique_lock<std::mutex> lk(done_mu);
+        done_cv.wait(lk, [&] { return pending == 0; });
+    }
+    for (const auto& e : err)
+        if (e) std::rethrow_exception(e);
+    // ---- one batched shortcut for every path found (reduceVertices' role) ---------------
+    const auto t_sc = std::chrono::steady_clock::now();
+    std::vector<std::vector<Vec3>> shortcut_in;
+    std::vector<int> which;
+    for (int p = 0; p < S; ++p)
+        if (found[p]) {
+            shortcut_in.push_back(std::move(raw[p]));
+            which.push_back(p);
+        }
+    std::vector<std::vector<Vec3>> shortcut_out = shortcutAll(shortcut_in);
+    paths.assign(S, {});
+    ok.assign(S, 0);
+    for (size_t i = 0; i < which.size(); ++i) {
+        paths[which[i]] = std::move(shortcut_out[i]);
+        ok[which[i]] = 1;
+    }
+    const double ms_sc = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_sc).count();
+    std::lock_guard<std::mutex> lk(g_stats_mu);
+    stats_.ms_device += ms_batch;
+    stats_.ms_search += ms_sc;
+    for (int p = 0; p < S; ++p) {
+        const Out& o = res[p];
+        stats_.states_sampled += samples;
+        stats_.states_valid += o.n - 2;
+        stats_.edges_checked += o.edges_checked;
+        stats_.edges_valid += o.edges_valid;
+        stats_.rows_downloaded += o.rows_down;
+        stats_.restricted_rows += o.restricted_rows;
+        stats_.fallbacks += o.fallback;
+        stats_.ms_device += o.ms_dev;
+        stats_.ms_search += o.ms_search;
+    }
+}
+
+// The whole k-NN table of one problem's nodes (device, start and goal first): k-NN, motion
+// checks straight off the table with the mask folded in (failed motions -> -1; the kept
+// edges and those into the goal, node 1, counted), the table down (up to 65535 nodes as
+// u16, 0xFFFF: no edge) with the nodes, then A* over the forward edges and, if that does not
+// reach the goal, over the symmetrised graph.  Runs on the calling thread's own stream.
+bool PathPlanner::wholeTableSearch(const double* d_nodes, int32_t n, const double box_lo[3], const double box_hi[3],
+                                   std::vector<Vec3>& path, int64_t& edges_checked, int64_t& edges_valid,
+                                   double& ms_dev, double& ms_search) const {
+    const auto t0 = std::chrono::steady_clock::now();
+    const bool canPass = configParser->getPathPlannerProperties().canPassGate;
+    const epp_world* w = worldPtr->device();
+    const int k = k_;
+    ThreadScratch& ts = ThreadScratch::get();
+    void* st = ts.stream();
+    const size_t m = (size_t)n * k;
+    const size_t ws_bytes = (size_t)epp_knn_workspace_size(n);
+    ts.reset(ThreadScratch::rounded(16) + ThreadScratch::rounded(m * 4) + 2 * ThreadScratch::rounded(m * 24) +
+             ThreadScratch::rounded(m) + ThreadScratch::rounded(ws_bytes));
+    int64_t* d_ecnt = static_cast<int64_t*>(ts.carve(16));
+    int32_t* d_nbr = static_cast<int32_t*>(ts.carve(m * 4));
+    double* d_e1 = static_cast<double*>(ts.carve(m * 24));
+    double* d_e2 = static_cast<double*>(ts.carve(m * 24));
+    uint8_t* d_ev = static_cast<uint8_t*>(ts.carve(m));
+    void* d_ws = ts.carve(ws_bytes);
+    const bool narrow = n <= 65535;
+    uint16_t* d_nbr16 = narrow ? reinterpret_cast<uint16_t*>(d_e1) : nullptr;
+    if (hipMemsetAsync(d_ecnt, 0, 16, static_cast<hipStream_t>(st)) != hipSuccess)
+        throw std::runtime_error("planPath: clearing the edge counts failed");
+    check(epp_knn_ws_box(d_nodes, n, k, 0.0, box_lo, box_hi, d_nbr, d_ws, ws_bytes, st), "knn");
+    const epp_status ks = check_knn_motions_masked(w, d_nodes, d_nbr, n, k, canPass ? 1 : 0, d_ev, d_nbr16, 1, d_ecnt, st);
+    if (ks == EPP_ERR_UNSUPPORTED) {
+        check(epp_knn_edges(d_nodes, d_nbr, n, k, d_e1, d_e2, st), "edges");
+        check(epp_check_motions(w, d_e1, d_e2, (int64_t)m, canPass ? 1 : 0, 0, d_ev, st), "motion check");
+        check(mask_edges_count_acc(d_nbr, d_ev, (int64_t)m, 1, d_ecnt, st, d_nbr16), "mask edges");
+    } else {
+        check(ks, "motion check");
+    }
+    // the downloads queued back to back, one synchronisation
+    int64_t* ecnt = static_cast<int64_t*>(ts.pinned(2, 16 * sizeof(double)));
+    const double* nodes = static_cast<const double*>(ts.pinned(0, (size_t)n * 24));
+    void* h_tab = ts.pinned(1, m * 4);
+    check(epp_memcpy_d2h_async(ecnt, d_ecnt, 16, st), "download");
+    check(epp_memcpy_d2h_async(const_cast<double*>(nodes), d_nodes, (uint64_t)n * 24, st), "download");
+    if (narrow) check(epp_memcpy_d2h_async(h_tab, d_nbr16, m * 2, st), "download");
+    else check(epp_memcpy_d2h_async(h_tab, d_nbr, m * 4, st), "download");
+    check(epp_stream_sync(st), "sync");
+    edges_checked = (int64_t)m;
+    edges_valid = ecnt[0];
+    const bool goal_has_forward_edge = ecnt[1] > 0;
+    const auto t1 = std::chrono::steady_clock::now();
+    ms_dev += std::chrono::duration<double, std::milli>(t1 - t0).count();
     const int32_t* nbr32 = static_cast<const int32_t*>(h_tab);
     const uint16_t* nbr16 = static_cast<const uint16_t*>(h_tab);
     auto nbr = [&](size_t e) -> int {
@@ -221,244 +531,114 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
         const uint16_t x = nbr16[e];
         return x == 0xFFFF ? -1 : (int)x;
     };
-    int64_t* ecnt = h_cnt + 1;  // [valid edges, of which into the goal, packed rows]
-    int64_t edges_checked = 0, n_valid_edges = 0, rows_down = 0;
-    bool goal_has_forward_edge = false;
-    double ms_dev = 0.0;
-    bool restricted = false;
-    if (cap > 0) {
-        const double sv[3] = {start.x, start.y, start.z}, gv[3] = {goal.x, goal.y, goal.z};
-        check(knn_ws_box_ellipse(d_nodes, n, k, blo, bhi, sv, gv, bound, d_nbr, d_ws, ws_bytes, st), "knn");
-        check(pack_ellipse_rows(d_nodes, d_nbr, n, k, sv, gv, bound, cap, d_ids32, d_ids16, d_rows32, d_ecnt + 2, st),
-              "pack rows");
-        const epp_status ks = check_knn_motions_rows(w, d_nodes, d_rows32, d_ids32, d_ecnt + 2, cap, k,
-                                                     canPass ? 1 : 0, d_ev, d_rows16, 1, d_ecnt, st);
-        if (ks != EPP_ERR_UNSUPPORTED) {
-            check(ks, "motion check");
-            restricted = true;
-            check(epp_memcpy_d2h_async(ecnt, d_ecnt, 24, st), "download");
-            check(epp_memcpy_d2h_async(h_tab, d_ids16, pack_bytes, st), "download");
-            check(epp_stream_sync(st), "sync");
-            check(epp_stream_sync(cst), "sync");
-            const int64_t rows = std::min<int64_t>(ecnt[2], cap);
-            edges_checked += rows * k;
-            n_valid_edges += ecnt[0];
-            rows_down += rows;
-        }
-    }
-    // the whole table (as without the restriction): k-NN, motion checks straight off the
-    // table with the mask folded in (failed motions -> -1; the valid edges and those into
-    // the goal, node 1, counted), the table down (up to 65535 nodes as u16, 0xFFFF: no edge,
-    // half the bytes, written into d_e1).  Small batches / worlds without tile tables:
-    // materialised endpoints, then the mask kernel.
-    uint16_t* d_nbr16 = narrow ? reinterpret_cast<uint16_t*>(d_e1) : nullptr;
-    auto whole_table = [&] {
-        if (restricted && hipMemsetAsync(d_ecnt, 0, 16, static_cast<hipStream_t>(st)) != hipSuccess)
-            throw std::runtime_error("planPath: clearing the edge counts failed");
-        check(epp_knn_ws_box(d_nodes, n, k, 0.0, blo, bhi, d_nbr, d_ws, ws_bytes, st), "knn");
-        const epp_status ks =
-            check_knn_motions_masked(w, d_nodes, d_nbr, n, k, canPass ? 1 : 0, d_ev, d_nbr16, 1, d_ecnt, st);
-        if (ks == EPP_ERR_UNSUPPORTED) {
-            check(epp_knn_edges(d_nodes, d_nbr, n, k, d_e1, d_e2, st), "edges");
-            check(epp_check_motions(w, d_e1, d_e2, (int64_t)m, canPass ? 1 : 0, 0, d_ev, st), "motion check");
-            check(mask_edges_count_acc(d_nbr, d_ev, (int64_t)m, 1, d_ecnt, st, d_nbr16), "mask edges");
-        } else {
-            check(ks, "motion check");
-        }
-        // the downloads queued back to back, one synchronisation (and the nodes' stream)
-        check(epp_memcpy_d2h_async(ecnt, d_ecnt, 16, st), "download");
-        if (narrow) check(epp_memcpy_d2h_async(h_tab, d_nbr16, m * 2, st), "download");
-        else check(epp_memcpy_d2h_async(h_tab, d_nbr, m * 4, st), "download");
-        check(epp_stream_sync(st), "sync");
-        check(epp_stream_sync(cst), "sync");
-        edges_checked += (int64_t)m;
-        n_valid_edges += ecnt[0];
-        goal_has_forward_edge = ecnt[1] > 0;
-        rows_down += n;
-    };
-    if (!restricted) whole_table();
-    ms_dev += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_dev0).count();
-    // ---- 3. shortest path over the valid edges, start = 0, goal = 1 ----------------------
-    // A* with the Euclidean distance to the goal (admissible and consistent for Euclidean
-    // edge costs: an optimal path of the graph searched).  First over the forward k-NN
-    // edges alone, read straight from the k-NN table (no graph build: A* touches only
-    // the nodes it expands); only if the goal is not reached that way, again over the
-    // symmetrised graph (reverse edges added as a CSR).
-    auto node = [&](int v) { return Vec3(nodes[3 * v], nodes[3 * v + 1], nodes[3 * v + 2]); };
-    const Vec3 gp = node(1);
-    // Search state per host thread, reused across calls: a node's dist / prev hold this
-    // search's values only when its stamp is the search's (no O(n) clearing per search:
-    // A* touches a small part of the ~63k nodes); the heap keeps its storage.
-    using QE = std::pair<double, int>;  // (g + h, node)
-    struct SearchState {
-        std::vector<double> dist;
-        std::vector<int> prev;
-        std::vector<uint32_t> seen, done;  // stamps: dist/prev valid, closed
-        std::vector<QE> heap;
-        uint32_t cur = 0;
-    };
+    auto pos = [&](int v) { return Vec3(nodes[3 * v], nodes[3 * v + 1], nodes[3 * v + 2]); };
+    auto key = [](int v) { return v; };
     thread_local SearchState ss;
-    if (ss.dist.size() < (size_t)n) {
-        ss.dist.resize(n);
-        ss.prev.resize(n);
-        ss.seen.resize(n, 0u);
-        ss.done.resize(n, 0u);
-    }
-    std::vector<int32_t> roff, radj;  // reverse edges (second pass only)
-    auto dist_of = [&](int v) { return ss.seen[v] == ss.cur ? ss.dist[v] : std::numeric_limits<double>::infinity(); };
-    auto prev_of = [&](int v) { return ss.seen[v] == ss.cur ? ss.prev[v] : -1; };
-    // (restricted: rows from the packed download via row_of; -1 = a pop above the bound or
-    // of a row not held, so the caller takes the whole table)
-    thread_local std::vector<int32_t> row_of;
-    const uint16_t* pk_ids = nbr16;
-    const uint16_t* pk_rows = nbr16 + ids_pad;
-    auto astar = [&](bool with_reverse, bool restricted) -> int {
-        if (++ss.cur == 0u) {  // (stamp wrap-around: clear once)
-            std::fill(ss.seen.begin(), ss.seen.end(), 0u);
-            std::fill(ss.done.begin(), ss.done.end(), 0u);
-            ss.cur = 1u;
-        }
-        // (the heap as std::priority_queue keeps it: push_heap / pop_heap with std::greater,
-        // over storage reused across searches)
-        std::vector<QE>& q = ss.heap;
-        q.clear();
-        const std::greater<QE> cmp;
-        auto push = [&](QE e) {
-            q.push_back(e);
-            std::push_heap(q.begin(), q.end(), cmp);
-        };
-        ss.seen[0] = ss.cur;
-        ss.dist[0] = 0.0;
-        ss.prev[0] = -1;
-        push({(node(0) - gp).norm(), 0});
-        auto relax = [&](int u, const Vec3& pu, int v) {
-            if (ss.done[v] == ss.cur) return;
-            const double nd = ss.dist[u] + (node(v) - pu).norm();
-            if (nd < dist_of(v)) {
-                ss.seen[v] = ss.cur;
-                ss.dist[v] = nd;
-                ss.prev[v] = u;
-                push({nd + (node(v) - gp).norm(), v});
-            }
-        };
-        while (!q.empty()) {
-            const double f = q.front().first;
-            const int u = q.front().second;
-            std::pop_heap(q.begin(), q.end(), cmp);
-            q.pop_back();
-            if (ss.done[u] == ss.cur) continue;
-            const uint16_t* row = nullptr;
-            if (restricted) {
-                if (!(f <= bound) || row_of[u] < 0) return -1;
-                row = pk_rows + (size_t)row_of[u] * k;
-            }
-            ss.done[u] = ss.cur;
-            if (u == 1) return 1;
-            const Vec3 pu = node(u);
-            if (restricted) {
-                for (int c = 0; c < k; ++c)
-                    if (row[c] != 0xFFFF) relax(u, pu, (int)row[c]);
-            } else {
-                const size_t e0 = (size_t)u * k;
+    // (no forward edge into the goal: the forward pass cannot reach it -- it would only
+    // explore start's whole component first; same result, so go straight to the second)
+    int r = 0;
+    if (goal_has_forward_edge)
+        r = astar(ss, (size_t)n, pos, key, [&](int u, double, auto&& relax, bool closing) {
+            if (closing)
                 for (int c = 0; c < k; ++c) {
-                    const int v = nbr(e0 + c);
-                    if (v >= 0) relax(u, pu, v);
+                    const int v = nbr((size_t)u * k + c);
+                    if (v >= 0) relax(v);
                 }
+            return true;
+        });
+    if (r != 1) {  // the symmetrised graph: reverse edges as a CSR
+        std::vector<int32_t> roff(n + 1, 0), radj;
+        for (size_t e = 0; e < m; ++e)
+            if (nbr(e) >= 0) ++roff[nbr(e) + 1];
+        for (int i = 0; i < n; ++i) roff[i + 1] += roff[i];
+        radj.resize(roff[n]);
+        std::vector<int32_t> fill(roff.begin(), roff.end() - 1);
+        for (int i = 0; i < n; ++i)
+            for (int c = 0; c < k; ++c) {
+                const size_t e = (size_t)i * k + c;
+                if (nbr(e) >= 0) radj[fill[nbr(e)]++] = i;
             }
-            if (with_reverse)
-                for (int32_t r = roff[u]; r < roff[u + 1]; ++r) relax(u, pu, radj[r]);
-        }
-        return 0;
-    };
-    int found = -1;
-    if (restricted && ecnt[1] > 0 && ecnt[2] <= cap) {
-        if (row_of.size() < (size_t)n) row_of.resize(n, -1);
-        for (int64_t r = 0; r < ecnt[2]; ++r) row_of[pk_ids[r]] = (int32_t)r;
-        found = astar(false, true);
-        for (int64_t r = 0; r < ecnt[2]; ++r) row_of[pk_ids[r]] = -1;
-    }
-    if (found != 1) {
-        if (restricted) {  // the whole table after all
-            const auto t0 = std::chrono::steady_clock::now();
-            whole_table();
-            ms_dev += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        }
-        // (no forward edge into the goal: the forward pass cannot reach it — it would only
-        // explore start's whole component first; same result, so go straight to the second)
-        if (!goal_has_forward_edge || astar(false, false) != 1) {
-            roff.assign(n + 1, 0);
-            for (size_t e = 0; e < m; ++e)
-                if (nbr(e) >= 0) ++roff[nbr(e) + 1];
-            for (int i = 0; i < n; ++i) roff[i + 1] += roff[i];
-            radj.resize(roff[n]);
-            std::vector<int32_t> fill(roff.begin(), roff.end() - 1);
-            for (int i = 0; i < n; ++i)
+        r = astar(ss, (size_t)n, pos, key, [&](int u, double, auto&& relax, bool closing) {
+            if (closing) {
                 for (int c = 0; c < k; ++c) {
-                    const size_t e = (size_t)i * k + c;
-                    if (nbr(e) >= 0) radj[fill[nbr(e)]++] = i;
+                    const int v = nbr((size_t)u * k + c);
+                    if (v >= 0) relax(v);
                 }
-            astar(true, false);
-        }
+                for (int32_t q = roff[u]; q < roff[u + 1]; ++q) relax(radj[q]);
+            }
+            return true;
+        });
     }
-    {
-        std::lock_guard<std::mutex> lk(g_stats_mu);
-        stats_.states_sampled += samples;
-        stats_.states_valid += n - 2;
-        stats_.edges_checked += edges_checked;
-        stats_.edges_valid += n_valid_edges;
-        stats_.rows_downloaded += rows_down;
+    path.clear();
+    if (r == 1) {
+        for (int v = 1; v >= 0; v = ss.prev_of(v)) path.push_back(pos(v));
+        std::reverse(path.begin(), path.end());
     }
-    auto account = [&] {
-        const auto t_end = std::chrono::steady_clock::now();
-        std::lock_guard<std::mutex> lk(g_stats_mu);
-        const double total = std::chrono::duration<double, std::milli>(t_end - t_dev0).count();
-        stats_.ms_device += ms_dev;
-        stats_.ms_search += total - ms_dev;
-    };
-    if (prev_of(1) < 0) {
-        account();
-        return false;
-    }
-    std::vector<Vec3> path;
-    for (int v = 1; v >= 0; v = prev_of(v)) path.push_back({nodes[3 * v], nodes[3 * v + 1], nodes[3 * v + 2]});
-    std::reverse(path.begin(), path.end());
-    out = shortcut(path);
-    account();
-    return true;
+    ms_search += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+    return r == 1;
 }
 
-// Greedy shortcutting with one batched check of every vertex pair (the role of
-// PathSimplifier::reduceVertices in src/PathPlanner.cpp:138-139).
-std::vector<Vec3> PathPlanner::shortcut(const std::vector<Vec3>& p) const {
-    const size_t L = p.size();
-    if (L < 3) return p;
+bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples, uint64_t seed,
+                           std::vector<Vec3>& out) const {
+    std::vector<std::vector<Vec3>> paths;
+    std::vector<char> ok;
+    planAttempt({{start, goal}}, {seed}, samples, paths, ok);
+    if (ok[0]) out = std::move(paths[0]);
+    return ok[0] != 0;
+}
+
+// Greedy shortcutting with one batched check of every vertex pair of every path (the role
+// of PathSimplifier::reduceVertices in src/PathPlanner.cpp:138-139).
+std::vector<std::vector<Vec3>> PathPlanner::shortcutAll(const std::vector<std::vector<Vec3>>& ps) const {
     std::vector<double> s1, s2;
-    std::vector<std::pair<int, int>> idx;
-    for (size_t i = 0; i < L; ++i)
-        for (size_t j = i + 2; j < L; ++j) {
-            s1.insert(s1.end(), {p[i].x, p[i].y, p[i].z});
-            s2.insert(s2.end(), {p[j].x, p[j].y, p[j].z});
-            idx.push_back({(int)i, (int)j});
-        }
-    std::vector<uint8_t> ok(idx.size());
-    worldPtr->checkRays(s1.data(), s2.data(), (int64_t)idx.size(), configParser->getPathPlannerProperties().canPassGate,
-                        ok.data());
-    std::vector<std::vector<uint8_t>> vis(L, std::vector<uint8_t>(L, 0));
-    for (size_t e = 0; e < idx.size(); ++e) vis[idx[e].first][idx[e].second] = ok[e];
-    std::vector<Vec3> out = {p[0]};
-    size_t cur = 0;
-    while (cur + 1 < L) {
-        size_t nxt = cur + 1;  // a path edge, valid by construction
-        for (size_t j = L - 1; j > cur + 1; --j)
-            if (vis[cur][j]) {
-                nxt = j;
-                break;
+    std::vector<size_t> base(ps.size() + 1, 0);
+    for (size_t q = 0; q < ps.size(); ++q) {
+        const auto& p = ps[q];
+        const size_t L = p.size();
+        base[q + 1] = base[q];
+        if (L < 3) continue;
+        for (size_t i = 0; i < L; ++i)
+            for (size_t j = i + 2; j < L; ++j) {
+                s1.insert(s1.end(), {p[i].x, p[i].y, p[i].z});
+                s2.insert(s2.end(), {p[j].x, p[j].y, p[j].z});
+                ++base[q + 1];
             }
-        out.push_back(p[nxt]);
-        cur = nxt;
+    }
+    std::vector<uint8_t> ok(base.back());
+    if (!ok.empty())
+        worldPtr->checkRays(s1.data(), s2.data(), (int64_t)ok.size(), configParser->getPathPlannerProperties().canPassGate,
+                            ok.data());
+    std::vector<std::vector<Vec3>> out(ps.size());
+    for (size_t q = 0; q < ps.size(); ++q) {
+        const auto& p = ps[q];
+        const size_t L = p.size();
+        if (L < 3) {
+            out[q] = p;
+            continue;
+        }
+        // vis(i, j) of pair (i, j), j >= i + 2, in the order they were queued
+        auto vis = [&](size_t i, size_t j) {
+            const size_t before = i * (L - 2) - (i * (i - 1)) / 2;  // pairs of rows < i: sum (L - 2 - r)
+            return ok[base[q] + before + (j - i - 2)] != 0;
+        };
+        std::vector<Vec3> o = {p[0]};
+        size_t cur = 0;
+        while (cur + 1 < L) {
+            size_t nxt = cur + 1;  // a path edge, valid by construction
+            for (size_t j = L - 1; j > cur + 1; --j)
+                if (vis(cur, j)) {
+                    nxt = j;
+                    break;
+                }
+            o.push_back(p[nxt]);
+            cur = nxt;
+        }
+        out[q] = std::move(o);
     }
     return out;
 }
+
+std::vector<Vec3> PathPlanner::shortcut(const std::vector<Vec3>& p) const { return shortcutAll({p})[0]; }
 
 // The planner choice of src/PathPlanner.cpp:106-123.  "rrt" cannot be honoured (OMPL's
 // RRT* is third-party and not part of this build; its `range` has no counterpart): it
@@ -493,38 +673,65 @@ bool PathPlanner::planPath(const Vec3& start, const Vec3& goal, double timeLimit
         stats_ = PlannerStats();
     }
     const uint64_t call = __atomic_fetch_add(&calls_, 1, __ATOMIC_RELAXED);
-    int attempts = 0;
-    const bool ok = planCall(start, goal, timeLimit, call, resultPath, attempts);
+    std::vector<std::vector<Vec3>> paths;
+    std::vector<char> ok;
+    const int attempts = planCalls({{start, goal}}, call, timeLimit, paths, ok);
+    if (ok[0]) resultPath = std::move(paths[0]);
     {
         std::lock_guard<std::mutex> lk(g_stats_mu);
         stats_.attempts = attempts;
         stats_.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
-    return ok;
+    return ok[0] != 0;
 }
 
-// One planPath problem with its call number (the seed): up to 4 attempts with doubled
-// samples while inside timeLimit (the role of solve(timeLimit), src/PathPlanner.cpp:126-136)
-bool PathPlanner::planCall(const Vec3& start, const Vec3& goal, double timeLimit, uint64_t call,
-                           std::vector<Vec3>& out, int& attempts) const {
+// Problems with the call numbers base, base + 1, ...: attempt a with samples_fmt x 2^a
+// samples and the seed mix(seed(call), a), the problems still without a path batched
+// together; up to 4 attempts while inside timeLimit (the role of solve(timeLimit),
+// src/PathPlanner.cpp:126-136).  Returns the attempts made.
+int PathPlanner::planCalls(const std::vector<std::pair<Vec3, Vec3>>& problems, uint64_t base, double timeLimit,
+                           std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const {
     const auto t0 = std::chrono::steady_clock::now();
     const auto& pp = configParser->getPathPlannerProperties();
+    const size_t n = problems.size();
+    paths.assign(n, {});
+    ok.assign(n, 0);
+    std::vector<uint64_t> seeds(n);
+    for (size_t i = 0; i < n; ++i) {
+        uint64_t seed = mix(seed_, base + i);
+        for (int d = 0; d < 3; ++d) seed = mix(mix(seed, bits_of(problems[i].first[d])), bits_of(problems[i].second[d]));
+        seeds[i] = seed;
+    }
+    std::vector<size_t> pending(n);
+    for (size_t i = 0; i < n; ++i) pending[i] = i;
     int64_t samples = pp.samplesFMT > 0 ? pp.samplesFMT : 4096;
-    uint64_t seed = mix(seed_, call);
-    for (int d = 0; d < 3; ++d) seed = mix(mix(seed, bits_of(start[d])), bits_of(goal[d]));
-    bool ok = false;
-    attempts = 0;
-    for (; attempts < 4 && !ok; ++attempts) {
-        ok = planOnce(start, goal, samples, mix(seed, attempts), out);
-        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        if (!ok && el > timeLimit) {  // out of time: give up like solve(timeLimit)
-            ++attempts;
-            break;
+    int attempts = 0;
+    for (int a = 0; a < 4 && !pending.empty(); ++a) {
+        std::vector<std::pair<Vec3, Vec3>> sub;
+        std::vector<uint64_t> sseeds;
+        for (size_t i : pending) {
+            sub.push_back(problems[i]);
+            sseeds.push_back(mix(seeds[i], (uint64_t)a));
         }
+        std::vector<std::vector<Vec3>> sp;
+        std::vector<char> so;
+        planAttempt(sub, sseeds, samples, sp, so);
+        attempts = a + 1;
+        std::vector<size_t> still;
+        for (size_t j = 0; j < pending.size(); ++j) {
+            if (so[j]) {
+                paths[pending[j]] = std::move(sp[j]);
+                ok[pending[j]] = 1;
+            } else {
+                still.push_back(pending[j]);
+            }
+        }
+        pending.swap(still);
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (!pending.empty() && el > timeLimit) break;  // out of time: give up like solve(timeLimit)
         samples *= 2;
     }
-    if (!ok) out.clear();
-    return ok;
+    return attempts;
 }
 
 void PathPlanner::planPaths(const std::vector<std::pair<Vec3, Vec3>>& problems, double timeLimit,
@@ -539,62 +746,16 @@ void PathPlanner::planPaths(const std::vector<std::pair<Vec3, Vec3>>& problems, 
         std::lock_guard<std::mutex> lk(g_stats_mu);
         stats_ = PlannerStats();
     }
+    (void)worldPtr->device();  // the device world, before the planner threads share it
     const uint64_t base = __atomic_fetch_add(&calls_, (uint64_t)n, __ATOMIC_RELAXED);
-    std::vector<int> attempts(n, 0);
-    std::vector<std::exception_ptr> err(n);
-    auto run = [&](size_t i) {
-        try {
-            ok[i] = planCall(problems[i].first, problems[i].second, timeLimit, base + i, paths[i], attempts[i]) ? 1 : 0;
-        } catch (...) {
-            err[i] = std::current_exception();
-        }
-    };
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    (void)worldPtr->device();  // build the device world once, before the threads share it
-    // problems 1.. on persistent pool threads (their ThreadScratch -- stream, device and
-    // pinned buffers -- survives between calls), problem 0 on the calling thread
-    std::mutex done_mu;
-    std::condition_variable done_cv;
-    const char* conc = std::getenv("EPP_PLAN_CONCURRENT");  // 0: one after the other (A/B)
-    if (conc && std::atoi(conc) == 0) {
-        for (size_t i = 0; i < n; ++i) run(i);
-        std::lock_guard<std::mutex> lk(g_stats_mu);
-        stats_.attempts = *std::max_element(attempts.begin(), attempts.end());
-        stats_.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        for (const auto& e : err)
-            if (e) std::rethrow_exception(e);
-        return;
-    }
-    // W concurrent planners (the caller + W-1 pool threads) pull problems in order: more
-    // than the hardware queues a process gets (4) only adds host contention
-    const char* thr = std::getenv("EPP_PLAN_THREADS");
-    const size_t W = std::min(n, (size_t)std::max(1, thr ? std::atoi(thr) : 4));
-    std::atomic<size_t> next{0};
-    auto drain = [&] {
-        for (size_t i = next++; i < n; i = next++) run(i);
-    };
-    size_t pending = W - 1;
-    for (size_t w = 1; w < W; ++w)
-        plan_pool().submit([&, dev] {
-            (void)hipSetDevice(dev);
-            drain();
-            std::lock_guard<std::mutex> lk(done_mu);
-            if (--pending == 0) done_cv.notify_all();
-        });
-    drain();
-    {
-        std::unique_lock<std::mutex> lk(done_mu);
-        done_cv.wait(lk, [&] { return pending == 0; });
-    }
-    for (const auto& e : err)
-        if (e) std::rethrow_exception(e);
+    const int attempts = planCalls(problems, base, timeLimit, paths, ok);
     std::lock_guard<std::mutex> lk(g_stats_mu);
-    stats_.attempts = *std::max_element(attempts.begin(), attempts.end());
+    stats_.attempts = attempts;
     stats_.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
-// PathPlanner::includeGates2 — src/PathPlanner.cpp:175-230
+// PathPlanner::includeGates2 — src/PathPlanner.cpp:175-230.  The segments' pruning checks
+// are one batch (pruneAll).
 std::vector<Vec3> PathPlanner::includeGates2(std::vector<std::vector<Vec3>> waypoints) const {
     std::vector<Vec3> gateCenters;
     for (size_t s = 0; s + 1 < waypoints.size(); ++s) {
@@ -607,57 +768,74 @@ std::vector<Vec3> PathPlanner::includeGates2(std::vector<std::vector<Vec3>> wayp
         waypoints[i + 1].insert(waypoints[i + 1].begin(), gateCenters[i]);
     }
     const std::string method = configParser->getPathPlannerProperties().pathSimplification;
+    std::vector<std::vector<Vec3>> pruned;
+    if (method == "none") {
+        pruned = waypoints;
+    } else if (method == "custom") {
+        pruned = pruneAll(waypoints);
+    } else if (method == "ompl") {
+        // smoothBSpline (OMPL) is not part of this build; the shortcut keeps the path valid
+        pruned = shortcutAll(waypoints);
+    } else {
+        std::cerr << "Unknown pruning method" << std::endl;
+        throw std::runtime_error("Unknown pruning method");
+    }
     std::vector<Vec3> flat;
-    for (const auto& seg : waypoints) {
-        std::vector<Vec3> pruned;
-        if (method == "none") {
-            pruned = seg;
-        } else if (method == "custom") {
-            pruned = pruneWaypoints(seg);
-        } else if (method == "ompl") {
-            // smoothBSpline (OMPL) is not part of this build; the shortcut keeps the path valid
-            pruned = shortcut(seg);
-        } else {
-            std::cerr << "Unknown pruning method" << std::endl;
-            throw std::runtime_error("Unknown pruning method");
-        }
-        for (const auto& w : pruned) {
+    for (const auto& seg : pruned)
+        for (const auto& w : seg) {
             if (!flat.empty() && (flat.back() - w).norm() < 0.05) continue;  // :222
             flat.push_back(w);
         }
-    }
     return flat;
 }
 
 // PathPlanner::pruneWaypoints — src/PathPlanner.cpp:232-265.  The reference checks
 // ray(reference, current) one at a time; every pair it could ask for is checked in one
-// batch and the same greedy walk is replayed on the answers.
-std::vector<Vec3> PathPlanner::pruneWaypoints(const std::vector<Vec3>& w) const {
-    if (w.size() < 3) return w;
-    const size_t L = w.size();
+// batch (for all segments at once) and the same greedy walk is replayed on the answers.
+std::vector<std::vector<Vec3>> PathPlanner::pruneAll(const std::vector<std::vector<Vec3>>& segs) const {
     std::vector<double> s1, s2;
-    std::vector<std::pair<int, int>> idx;
-    for (size_t i = 0; i < L; ++i)
-        for (size_t j = i + 2; j < L; ++j) {
-            s1.insert(s1.end(), {w[i].x, w[i].y, w[i].z});
-            s2.insert(s2.end(), {w[j].x, w[j].y, w[j].z});
-            idx.push_back({(int)i, (int)j});
-        }
-    std::vector<uint8_t> ok(idx.size());
-    worldPtr->checkRays(s1.data(), s2.data(), (int64_t)idx.size(), true, ok.data());  // canPassGate = true
-    std::vector<std::vector<uint8_t>> vis(L, std::vector<uint8_t>(L, 1));
-    for (size_t e = 0; e < idx.size(); ++e) vis[idx[e].first][idx[e].second] = ok[e];
-    std::vector<Vec3> pruned = {w[0]};
-    size_t ref = 0;
-    for (size_t cur = 2; cur < L; ++cur) {
-        if (!vis[ref][cur]) {
-            pruned.push_back(w[cur - 1]);
-            ref = cur - 1;
-        }
+    std::vector<size_t> base(segs.size() + 1, 0);
+    for (size_t q = 0; q < segs.size(); ++q) {
+        const auto& w = segs[q];
+        const size_t L = w.size();
+        base[q + 1] = base[q];
+        if (L < 3) continue;
+        for (size_t i = 0; i < L; ++i)
+            for (size_t j = i + 2; j < L; ++j) {
+                s1.insert(s1.end(), {w[i].x, w[i].y, w[i].z});
+                s2.insert(s2.end(), {w[j].x, w[j].y, w[j].z});
+                ++base[q + 1];
+            }
     }
-    pruned.push_back(w[L - 1]);
-    return pruned;
+    std::vector<uint8_t> ok(base.back());
+    if (!ok.empty()) worldPtr->checkRays(s1.data(), s2.data(), (int64_t)ok.size(), true, ok.data());  // canPassGate = true
+    std::vector<std::vector<Vec3>> out(segs.size());
+    for (size_t q = 0; q < segs.size(); ++q) {
+        const auto& w = segs[q];
+        const size_t L = w.size();
+        if (L < 3) {
+            out[q] = w;
+            continue;
+        }
+        auto vis = [&](size_t i, size_t j) {  // pair (i, j), j >= i + 2, in the order queued
+            const size_t before = i * (L - 2) - (i * (i - 1)) / 2;
+            return ok[base[q] + before + (j - i - 2)] != 0;
+        };
+        std::vector<Vec3> pruned = {w[0]};
+        size_t ref = 0;
+        for (size_t cur = 2; cur < L; ++cur) {
+            if (!vis(ref, cur)) {
+                pruned.push_back(w[cur - 1]);
+                ref = cur - 1;
+            }
+        }
+        pruned.push_back(w[L - 1]);
+        out[q] = std::move(pruned);
+    }
+    return out;
 }
+
+std::vector<Vec3> PathPlanner::pruneWaypoints(const std::vector<Vec3>& w) const { return pruneAll({w})[0]; }
 
 // PathPlanner::checkTrajectoryValidity — src/PathPlanner.cpp:267-280 (one batched launch)
 bool PathPlanner::checkTrajectoryValidity(const Matrix& traj, double minDistance) const {

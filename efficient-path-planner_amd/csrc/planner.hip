@@ -1939,8 +1939,10 @@ struct PlanBatchDev {
     int32_t* ids32;
     int32_t* rows32;
     uint16_t* rows16;
-    uint32_t* mark;
-    double* need;  // 4 doubles per entry: x, y, z, global id (u64 bits)
+    uint32_t* mark;     // a bit per node: referenced by a packed row
+    int32_t* map;       // node (global id) -> its compact index (referenced nodes only)
+    uint32_t* slot;     // packed row -> p << 16 | compact index of its node
+    double* need;       // 4 doubles per referenced node: x, y, z, node id (u64 bits)
 };
 
 struct KnnSeg {
@@ -1985,7 +1987,21 @@ __global__ __launch_bounds__(256) void k_pb_sample(PlanBatchDev P) {
 __global__ __launch_bounds__(kCompactThreads) void k_pb_compact(PlanBatchDev P, uint32_t tag) {
     const int p = blockIdx.y;
     double* out = P.nodes + (int64_t)p * P.NS * 3;
-    if (blockIdx.x == 0 && threadIdx.x < 6) out[threadIdx.x] = threadIdx.x < 3 ? P.seg[p].s[threadIdx.x] : P.seg[p].g[threadIdx.x - 3];
+    const PlanSeg& q = P.seg[p];
+    if (blockIdx.x == 0 && threadIdx.x < 6) out[threadIdx.x] = threadIdx.x < 3 ? q.s[threadIdx.x] : q.g[threadIdx.x - 3];
+    if (blockIdx.x == 0 && threadIdx.x < 2 && q.cap > 0) {
+        // start and goal take compact indices 0 and 1 of the referenced nodes
+        const int64_t gid = ((int64_t)p << P.ns_log) + threadIdx.x;
+        atomicOr(P.mark + (gid >> 5), 1u << (gid & 31));
+        P.map[gid] = (int32_t)threadIdx.x;
+        double* d = P.need + (q.need_off + threadIdx.x) * 4;
+        const double* x = threadIdx.x == 0 ? q.s : q.g;
+        d[0] = x[0];
+        d[1] = x[1];
+        d[2] = x[2];
+        d[3] = __longlong_as_double((long long)threadIdx.x);
+        if (threadIdx.x == 0) P.ctr[kPbPerSeg + 4 * P.S + p] = 2ull;
+    }
     compact_block(P.xyz + (int64_t)p * P.ns * 3, P.valid + (int64_t)p * P.ns, P.ns, P.cstat + (int64_t)p * P.nbc, tag,
                   out + 6, reinterpret_cast<int64_t*>(P.ctr) + kPbPerSeg + 3 * P.S + p, 2, blockIdx.x, gridDim.x);
 }
@@ -2123,8 +2139,9 @@ __global__ __launch_bounds__(256) void k_pb_pack(PlanBatchDev P) {
 }
 
 // The nodes the packed rows reference (each row's node and its kept neighbours), each once
-// (a bit per node), appended as {x, y, z, id}; and per problem the kept edges of its rows
-// and those into its goal (node 1).  One thread per row entry.
+// (a bit per node): numbered per problem in a compact index (after start 0 and goal 1, in
+// arbitrary order) and listed as {x, y, z, node id}; and per problem the kept edges of its
+// rows and those into its goal (node 1).  One thread per row entry.
 __global__ __launch_bounds__(256) void k_pb_need(PlanBatchDev P) {
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t rows = (int64_t)min(P.ctr[kPbPacked], (unsigned long long)P.cap_total);
@@ -2132,7 +2149,7 @@ __global__ __launch_bounds__(256) void k_pb_need(PlanBatchDev P) {
     const int lane = threadIdx.x & 63;
     int p = -1;
     bool keep = false, goal = false;
-    int64_t cand[2] = {-1, -1};  // (global ids to mark: the neighbour, and the row's node once per row)
+    int64_t cand[2] = {-1, -1};  // (global ids: the neighbour, and the row's node once per row)
     if (act) {
         const int64_t slot = e / P.k;
         const int c = (int)(e - slot * P.k);
@@ -2151,30 +2168,37 @@ __global__ __launch_bounds__(256) void k_pb_need(PlanBatchDev P) {
             const uint32_t bit = 1u << (cand[t] & 31);
             fresh = !(atomicOr(P.mark + (cand[t] >> 5), bit) & bit);
         }
-        const unsigned long long bal = __ballot(fresh);
-        if (!bal) continue;
-        const int first = __ffsll(bal) - 1;
-        unsigned long long base = 0;
-        if (lane == first) base = atomicAdd(P.ctr + kPbNeed, (unsigned long long)__popcll(bal));
-        base = __shfl(base, first, 64);
-        if (fresh) {
-            const int64_t at = (int64_t)(base + __popcll(bal & ((1ull << lane) - 1ull)));
-            if (at < P.need_cap) {
-                const double* x = P.nodes + cand[t] * 3;
-                double* d = P.need + at * 4;
-                d[0] = x[0];
-                d[1] = x[1];
-                d[2] = x[2];
-                d[3] = __longlong_as_double((long long)cand[t]);
+        unsigned long long todo = __ballot(fresh);
+        while (todo) {  // one atomic per (wave, problem) among the fresh lanes
+            const int p0 = __shfl(p, __ffsll(todo) - 1, 64);
+            const unsigned long long mine = __ballot(fresh && p == p0);
+            const int first = __ffsll(mine) - 1;
+            unsigned long long base = 0;
+            if (lane == first) base = atomicAdd(P.ctr + kPbPerSeg + 4 * P.S + p0, (unsigned long long)__popcll(mine));
+            base = __shfl(base, first, 64);
+            if (fresh && p == p0) {
+                const PlanSeg& q = P.seg[p0];
+                const int64_t at = (int64_t)(base + __popcll(mine & ((1ull << lane) - 1ull)));
+                P.map[cand[t]] = (int32_t)at;
+                if (at < q.need_cap) {
+                    const double* x = P.nodes + cand[t] * 3;
+                    double* d = P.need + (q.need_off + at) * 4;
+                    d[0] = x[0];
+                    d[1] = x[1];
+                    d[2] = x[2];
+                    d[3] = __longlong_as_double((long long)(cand[t] & (P.NS - 1)));
+                }
             }
+            todo &= ~mine;
         }
     }
     // per-problem edge counts: one atomic per (wave, problem) present in the wave
+    const unsigned long long kb = __ballot(keep), gb = __ballot(goal);
     unsigned long long todo = __ballot(act);
     while (todo) {
         const int p0 = __shfl(p, __ffsll(todo) - 1, 64);
         const unsigned long long mine = __ballot(act && p == p0);
-        const int nk = __popcll(mine & __ballot(keep)), ng = __popcll(mine & __ballot(goal));
+        const int nk = __popcll(mine & kb), ng = __popcll(mine & gb);
         if (lane == __ffsll(mine) - 1) {
             if (nk) atomicAdd(P.ctr + kPbPerSeg + P.S + p0, (unsigned long long)nk);
             if (ng) atomicAdd(P.ctr + kPbPerSeg + 2 * P.S + p0, (unsigned long long)ng);
@@ -2183,25 +2207,61 @@ __global__ __launch_bounds__(256) void k_pb_need(PlanBatchDev P) {
     }
 }
 
-// The results into pinned host memory, only the bytes in use: the header (counters), the
-// packed rows' node ids (u32) and masked rows (u16), the needed nodes (32 B each).  16-byte
-// stores (the device parts are 16-byte padded).
-__global__ __launch_bounds__(256) void k_pb_emit(PlanBatchDev P, unsigned long long* __restrict__ hdr,
-                                                  uint4* __restrict__ h_ids, uint4* __restrict__ h_rows,
-                                                  uint4* __restrict__ h_need) {
+// The packed rows in compact indices (in place) and each slot's problem and node.
+__global__ __launch_bounds__(256) void k_pb_remap(PlanBatchDev P) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t rows = (int64_t)min(P.ctr[kPbPacked], (unsigned long long)P.cap_total);
-    const int64_t need = (int64_t)min(P.ctr[kPbNeed], (unsigned long long)P.need_cap);
-    const int64_t c_ids = (rows * 4 + 15) / 16, c_rows = (rows * P.k * 2 + 15) / 16, c_need = need * 2;
+    if (e >= rows * P.k) return;
+    const int64_t slot = e / P.k;
+    const int32_t u = P.ids32[slot];
+    const int p = u >> P.ns_log;
+    const uint16_t v = P.rows16[e];
+    if (v != 0xFFFF) P.rows16[e] = (uint16_t)P.map[((int64_t)p << P.ns_log) + v];
+    if (e == slot * P.k) P.slot[slot] = ((uint32_t)p << 16) | ((uint32_t)P.map[u] & 0xFFFFu);
+}
+
+// The results into pinned host memory, only the bytes in use: the header (counters), the
+// slots' problem and node (u32), the masked rows (u16), every problem's referenced nodes
+// (32 B each, at its own offset).  16-byte stores (the device parts are 16-byte padded).
+__global__ __launch_bounds__(256) void k_pb_emit(PlanBatchDev P, unsigned long long* __restrict__ hdr,
+                                                  uint4* __restrict__ h_slot, uint4* __restrict__ h_rows,
+                                                  uint4* __restrict__ h_need) {
+    __shared__ long long pre[65];  // need chunks before problem p (S <= 64)
+    const int64_t rows = (int64_t)min(P.ctr[kPbPacked], (unsigned long long)P.cap_total);
+    if (threadIdx.x == 0) {
+        long long a = 0;
+        for (int p = 0; p < P.S; ++p) {
+            pre[p] = a;
+            a += 2 * min((long long)P.ctr[kPbPerSeg + 4 * P.S + p], (long long)P.seg[p].need_cap);
+        }
+        pre[P.S] = a;
+    }
+    __syncthreads();
+    const int64_t c_slot = (rows * 4 + 15) / 16, c_rows = (rows * P.k * 2 + 15) / 16, c_need = pre[P.S];
     const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (tid < P.nctr) hdr[tid] = P.ctr[tid];
-    const uint4* d_ids = reinterpret_cast<const uint4*>(P.ids32);
+    const uint4* d_slot = reinterpret_cast<const uint4*>(P.slot);
     const uint4* d_rows = reinterpret_cast<const uint4*>(P.rows16);
     const uint4* d_need = reinterpret_cast<const uint4*>(P.need);
-    for (int64_t c = tid; c < c_ids + c_rows + c_need; c += (int64_t)gridDim.x * 256) {
-        if (c < c_ids) h_ids[c] = d_ids[c];
-        else if (c < c_ids + c_rows) h_rows[c - c_ids] = d_rows[c - c_ids];
-        else h_need[c - c_ids - c_rows] = d_need[c - c_ids - c_rows];
+    for (int64_t c = tid; c < c_slot + c_rows + c_need; c += (int64_t)gridDim.x * 256) {
+        if (c < c_slot) {
+            h_slot[c] = d_slot[c];
+        } else if (c < c_slot + c_rows) {
+            h_rows[c - c_slot] = d_rows[c - c_slot];
+        } else {
+            const int64_t r = c - c_slot - c_rows;
+            int p = 0;
+            while (p + 1 < P.S && pre[p + 1] <= r) ++p;
+            const int64_t at = 2 * P.seg[p].need_off + (r - pre[p]);
+            h_need[at] = d_need[at];
+        }
     }
+}
+
+int cu_count_planner() {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return cus;
 }
 
 epp_status last(const char* what) {
@@ -2506,7 +2566,7 @@ epp_status epp_knn_edges(const double* nodes, const int32_t* nbr, int32_t n, int
 }  // extern "C"
 
 // ---- the batched planner's host side (epp_internal.h) ---------------------------------
-epp::PlanBatchLayout epp::plan_batch_layout(int32_t S, int64_t ns, int32_t k, int32_t cap_total) {
+epp::PlanBatchLayout epp::plan_batch_layout(int32_t S, int64_t ns, int32_t k, PlanSeg* segs) {
     auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
     PlanBatchLayout L;
     L.S = S;
@@ -2516,9 +2576,19 @@ epp::PlanBatchLayout epp::plan_batch_layout(int32_t S, int64_t ns, int32_t k, in
     while ((1ll << L.ns_log) < ns + 2) ++L.ns_log;
     L.NS = 1ll << L.ns_log;
     L.nbc = (int32_t)std::max<int64_t>(1, (ns + kCompactChunk - 1) / kCompactChunk);
-    L.cap_total = std::max(0, cap_total);
-    L.need_cap = (int64_t)L.cap_total * (k + 1);
-    L.nctr = kPbPerSeg + 4 * S;
+    // packed rows: the problems' capacities; referenced nodes: a row's node and its k
+    // neighbours per row, at most the problem's nodes
+    int64_t cap_total = 0, need = 0;
+    for (int p = 0; p < S; ++p) {
+        segs[p].cap = std::max(0, segs[p].cap);
+        cap_total += segs[p].cap;
+        segs[p].need_off = need;
+        segs[p].need_cap = segs[p].cap > 0 ? (int32_t)std::min<int64_t>((int64_t)segs[p].cap * (k + 1) + 2, ns + 2) : 0;
+        need += segs[p].need_cap;
+    }
+    L.cap_total = (int32_t)cap_total;
+    L.need_cap = need;
+    L.nctr = kPbPerSeg + 5 * S;
     const KnnLayout kl = knn_layout((int)(ns + 2));
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -2542,12 +2612,14 @@ epp::PlanBatchLayout epp::plan_batch_layout(int32_t S, int64_t ns, int32_t k, in
     L.o_rows16 = take(capr * k * 2);
     L.o_ev = take(capr * k);
     L.o_mark = take((size_t)S * (L.NS >> 5) * 4);
+    L.o_map = take((size_t)S * L.NS * 4);
+    L.o_slot = take(capr * 4);
     L.o_need = take((size_t)L.need_cap * 32);
     L.dev_bytes = o;
     o = 0;
     L.h_seg = take((size_t)S * sizeof(PlanSeg));
     L.h_hdr = take((size_t)L.nctr * 8);
-    L.h_ids = take(capr * 4);
+    L.h_slot = take(capr * 4);
     L.h_rows = take(capr * k * 2);
     L.h_need = take((size_t)L.need_cap * 32);
     L.host_bytes = o;
@@ -2557,7 +2629,7 @@ epp::PlanBatchLayout epp::plan_batch_layout(int32_t S, int64_t ns, int32_t k, in
 epp_status epp::plan_batch_launch(const epp_world* world, int32_t can_pass_gate, const double lo[3], const double hi[3],
                                   const PlanBatchLayout& L, void* dev, void* host, void* stream) {
     if (!world || !dev || !host || L.S < 1 || L.ns < 1 || (L.k != 4 && L.k != 8 && L.k != 16) ||
-        ((int64_t)L.S << L.ns_log) >= (1ll << 31) || (reinterpret_cast<uintptr_t>(dev) & 255) ||
+        L.S > 64 || ((int64_t)L.S << L.ns_log) >= (1ll << 31) || (reinterpret_cast<uintptr_t>(dev) & 255) ||
         (reinterpret_cast<uintptr_t>(host) & 255)) {
         set_error("plan_batch_launch: invalid argument");
         return EPP_ERR_INVALID_ARGUMENT;
@@ -2604,6 +2676,8 @@ epp_status epp::plan_batch_launch(const epp_world* world, int32_t can_pass_gate,
     P.rows32 = reinterpret_cast<int32_t*>(d + L.o_rows32);
     P.rows16 = reinterpret_cast<uint16_t*>(d + L.o_rows16);
     P.mark = reinterpret_cast<uint32_t*>(d + L.o_mark);
+    P.map = reinterpret_cast<int32_t*>(d + L.o_map);
+    P.slot = reinterpret_cast<uint32_t*>(d + L.o_slot);
     P.need = reinterpret_cast<double*>(d + L.o_need);
     const unsigned S = (unsigned)L.S;
     // the problems up (pinned), then every stage on this stream
@@ -2634,9 +2708,10 @@ epp_status epp::plan_batch_launch(const epp_world* world, int32_t can_pass_gate,
             return st;
         const int64_t ents = (int64_t)L.cap_total * L.k;
         hipLaunchKernelGGL(k_pb_need, dim3((unsigned)((ents + 255) / 256)), dim3(256), 0, s, P);
+        hipLaunchKernelGGL(k_pb_remap, dim3((unsigned)((ents + 255) / 256)), dim3(256), 0, s, P);
     }
     hipLaunchKernelGGL(k_pb_emit, dim3((unsigned)std::max(1, cu_count_planner())), dim3(256), 0, s, P,
-                       reinterpret_cast<unsigned long long*>(hh), reinterpret_cast<uint4*>(h + L.h_ids),
+                       reinterpret_cast<unsigned long long*>(hh), reinterpret_cast<uint4*>(h + L.h_slot),
                        reinterpret_cast<uint4*>(h + L.h_rows), reinterpret_cast<uint4*>(h + L.h_need));
     return last("plan_batch_launch");
 }

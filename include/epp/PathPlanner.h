@@ -27,10 +27,12 @@ namespace epp {
 struct PlannerStats {
     int64_t states_sampled = 0;
     int64_t states_valid = 0;
-    int64_t edges_checked = 0;
+    int64_t edges_checked = 0;    // edges of the graphs searched (the final table's on a fallback)
     int64_t edges_valid = 0;
     int attempts = 0;
     int64_t rows_downloaded = 0;  // k-NN table rows copied to the host (see planPath)
+    int64_t restricted_rows = 0;  // of which packed rows of the row-restricted searches
+    int64_t fallbacks = 0;        // searches that took the whole table after the restricted rows
     double ms = 0;         // wall time of the last planPath
     double ms_device = 0;  // of which: sampling, checks, k-NN, transfers (GPU phases)
     double ms_search = 0;  // of which: graph build + A* + shortcut on the host
@@ -48,11 +50,12 @@ public:
     // checkTrajectoryValidity against any World (one batched launch)
     static bool checkTrajectoryValidityOn(const World& world, const Matrix& trajectory, double minDistance);
     bool planPath(const Vec3& start, const Vec3& goal, double timeLimit, std::vector<Vec3>& resultPath) const;
-    // Independent (start, goal) problems planned concurrently, one host thread and one
-    // HIP stream each (their small kernels overlap on the GPU).  Problem i gets the seed
-    // of the i-th of consecutive planPath calls, so results do not depend on thread
-    // timing.  ok[i] / paths[i] as planPath's return value / resultPath; stats = the sum,
-    // ms = the batch's wall time.
+    // Independent (start, goal) problems planned together: every device stage runs once
+    // for all of them (one launch each, blockIdx.y = the problem), the searches run on
+    // planner threads, the shortcut checks are one batch.  Problem i gets the seed of the
+    // i-th of consecutive planPath calls, so results do not depend on the batching or on
+    // thread timing.  ok[i] / paths[i] as planPath's return value / resultPath; stats =
+    // the sum, ms = the batch's wall time.
     void planPaths(const std::vector<std::pair<Vec3, Vec3>>& problems, double timeLimit,
                    std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const;
     void updateGatePos(int gateId, const std::vector<double>& newPose);
@@ -83,12 +86,23 @@ public:
 private:
     std::vector<Vec3> pruneWaypoints(const std::vector<Vec3>& waypoints) const;
     std::vector<Vec3> shortcut(const std::vector<Vec3>& path) const;
-    bool planCall(const Vec3& start, const Vec3& goal, double timeLimit, uint64_t call, std::vector<Vec3>& out,
-                  int& attempts) const;
+    std::vector<std::vector<Vec3>> shortcutAll(const std::vector<std::vector<Vec3>>& paths) const;
+    std::vector<std::vector<Vec3>> pruneAll(const std::vector<std::vector<Vec3>>& segments) const;
+    int planCalls(const std::vector<std::pair<Vec3, Vec3>>& problems, uint64_t base, double timeLimit,
+                  std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const;
+    void planAttempt(const std::vector<std::pair<Vec3, Vec3>>& problems, const std::vector<uint64_t>& seeds,
+                     int64_t samples, std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const;
+    void planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, const std::vector<uint64_t>& seeds,
+                   int64_t samples, std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const;
+    bool wholeTableSearch(const double* d_nodes, int32_t n, const double box_lo[3], const double box_hi[3],
+                          std::vector<Vec3>& path, int64_t& edges_checked, int64_t& edges_valid, double& ms_dev,
+                          double& ms_search) const;
 
     std::shared_ptr<ConfigParser> configParser;
     uint64_t seed_ = 0x5eedull;
     int k_ = 16;
+    double ellipse_ = 1.5;  // row-restricted search: bound = ellipse_ |start - goal| + 0.25 m (0: off)
+    int threads_ = 4;       // planner threads of a batch's searches
     mutable uint64_t calls_ = 0;
     mutable PlannerStats stats_;
 };

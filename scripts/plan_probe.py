@@ -30,7 +30,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
     otg = otp.OnlineTrajGenerator(cps[0], cps[-1], gates, obstacles, path)
     otg.pre_compute_traj(0.0)
     ts, st = [], []
-    for _ in range(30):
+    for _ in range(int(os.environ.get('EPP_PROBE_CALLS', '30'))):
         t = time.perf_counter()
         otg.pre_compute_traj(0.0)
         ts.append((time.perf_counter() - t) * 1e3)
@@ -43,9 +43,12 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
           f"(EPP_PLAN_ELLIPSE {os.environ.get('EPP_PLAN_ELLIPSE', 'default')})",
           flush=True)
     order = np.argsort(ts)[::-1][:6]
-    print("   slowest:", ", ".join(f"#{i} {ts[i]:.1f} ms (planner {st[i]['ms']:.1f}, device {st[i]['ms_device']:.1f}, "
-                                   f"search {st[i]['ms_search']:.1f}, attempts {st[i]['attempts']})"
+    print("   slowest:", ", ".join(f"#{i} {ts[i]:.2f} ms (planner {st[i]['ms']:.2f}, device {st[i]['ms_device']:.2f}, "
+                                   f"search {st[i]['ms_search']:.2f}, attempts {st[i]['attempts']}, "
+                                   f"fallbacks {st[i]['fallbacks']})"
                                    for i in order), flush=True)
+    print("   fallbacks per call:", [s["fallbacks"] for s in st], "mean", np.mean([s["fallbacks"] for s in st]))
+    print("   all (ms):", " ".join(f"{t:.2f}/{s['ms']:.2f}" for t, s in zip(ts, st)), flush=True)
 else:
     for t in (sys.argv[1:] or ["4"]):
         t, _, pw = t.partition(":")  # "4" or "4:0" (EPP_PATH_WRITER=0)
