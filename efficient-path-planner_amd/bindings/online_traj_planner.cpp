@@ -227,6 +227,9 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["rows_downloaded"] = s.rows_downloaded;
             d["restricted_rows"] = s.restricted_rows;
             d["fallbacks"] = s.fallbacks;
+            d["ms_batch"] = s.ms_batch;
+            d["ms_solve"] = s.ms_solve;
+            d["ms_shortcut"] = s.ms_shortcut;
             d["ms"] = s.ms;
             d["ms_device"] = s.ms_device;
             d["ms_search"] = s.ms_search;
@@ -392,6 +395,9 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["rows_downloaded"] = s.rows_downloaded;
             d["restricted_rows"] = s.restricted_rows;
             d["fallbacks"] = s.fallbacks;
+            d["ms_batch"] = s.ms_batch;
+            d["ms_solve"] = s.ms_solve;
+            d["ms_shortcut"] = s.ms_shortcut;
             return d;
         })
         .def("get_checkpoints", [](const epp::OnlineTrajGenerator& self) {

@@ -115,43 +115,50 @@ epp_status check_knn_motions_rows(const epp_world* world, const double* nodes, i
                                   const int64_t* rows_n, int32_t cap, int32_t k, int32_t can_pass_gate,
                                   uint8_t* valid, uint16_t* out16, int32_t target, int64_t* count, void* stream);
 
-// ---- the batched planner (PathPlanner::planPaths): a track's gate-to-gate problems, one
+// ---- the batched planner (PathPlanner::planPaths): a batch of gate-to-gate problems, one
 // launch per device stage with blockIdx.y = the problem (planner.hip, plan_batch_launch).
-// Stages: sample -> state check -> ordered compaction (start, goal, valid samples) -> k-NN
-// grid (count, scan, scatter) -> the rows of the nodes inside each problem's ellipsoid
-// |x - s| + |x - g| <= bound, one wave per listed node -> packed rows -> their motion checks
-// (failed edges masked) -> the nodes those rows reference, renumbered per problem in a
-// compact index (0 = start, 1 = goal) -> one emit into pinned host memory.  Node counts stay
-// on the device: no host round trip before the emit.
+// Stages: sample -> state check -> ordered compaction (start, goal, valid samples) -> the
+// nodes inside each problem's grid ellipsoid |x - s| + |x - g| <= gbound into a small
+// k-NN grid, those inside the row ellipsoid (<= bound) listed as queries -> their exact
+// k-NN rows, one wave per query (exact because every node within the query's search
+// radius lies in the grid ellipsoid: |x - s| + |x - g| is 2-Lipschitz; else the problem is
+// flagged) -> the rows' motion checks (failed edges masked) -> the nodes the rows reference,
+// numbered per problem in node order (0 = start, 1 = goal) -> one emit into pinned host
+// memory.  Node counts stay on the device: no host round trip before the emit.
 struct PlanSeg {                  // one problem (host -> device)
     uint64_t seed;                // the attempt's sampler seed
     double s[3], g[3];            // start, goal: nodes 0 and 1
-    double box_lo[3], box_hi[3];  // k-NN grid box (the sampling box widened by s and g)
-    double bound;                 // restricted rows: |x - s| + |x - g| <= bound
+    double bound;                 // rows: |x - s| + |x - g| <= bound
+    double gbound;                // grid nodes: <= gbound (bound + a margin of cells)
+    double glo[3], ghi[3];        // the grid's box (the gbound ellipsoid's box, clipped)
+    double h;                     // the grid's cell edge
+    int64_t row_off;              // first slot of its query list (rows: dense, see hdr)
     int64_t need_off;             // first slot of its referenced-node list
-    int32_t cap;                  // packed-row capacity (0: no restricted rows)
+    int32_t cap;                  // query / row capacity (0: no restricted rows)
     int32_t need_cap;             // referenced-node list capacity
 };
-// Header words of the emitted results (u64): [0] listed k-NN queries, [1] packed rows,
-// then per problem p: [3 + p] its packed rows (uncapped), [3 + S + p] kept edges of its
-// rows, [3 + 2S + p] kept edges into its goal (node 1), [3 + 3S + p] its node count (valid
-// samples + 2), [3 + 4S + p] its referenced nodes (compact indices 0 .. that - 1).
-enum : int { kPbListed = 0, kPbPacked = 1, kPbPerSeg = 3 };
+// Header words of the emitted results (u64): [1] rows (the problems' min(queries, cap),
+// in problem order: problem p's rows follow those of problems < p), then per problem p:
+// [3 + p] its queries (uncapped), [3 + S + p] kept edges of its rows, [3 + 2S + p] kept
+// edges into its goal (node 1), [3 + 3S + p] its node count (valid samples + 2),
+// [3 + 4S + p] its referenced nodes (compact indices 0 .. that - 1, in node order),
+// [3 + 5S + p] nonzero: some query's exact rows needed nodes outside the grid ellipsoid.
+enum : int { kPbRows = 1, kPbPerSeg = 3 };
 struct PlanBatchLayout {
     int32_t S = 0, k = 0, ns_log = 0, nbc = 0, cap_total = 0, nctr = 0;
     int64_t ns = 0, NS = 0, need_cap = 0;  // samples per problem, node stride (2^ns_log >= 65536),
                                           // referenced-node slots of all problems
     // device workspace (bytes from its base, 256-B aligned parts)
     size_t o_seg = 0, o_ctr = 0, o_xyz = 0, o_valid = 0, o_nodes = 0, o_cstat = 0, o_kws = 0, kws_stride = 0,
-           o_nbr = 0, o_retry = 0, o_ids32 = 0, o_rows32 = 0, o_rows16 = 0, o_ev = 0, o_mark = 0, o_map = 0,
-           o_slot = 0, o_need = 0, dev_bytes = 0;
-    // pinned host block: the problems (uploaded), then the emitted header, per packed row
-    // (slot) its problem and node (p << 16 | compact index), the masked rows (compact
-    // indices, 0xFFFF: no edge) and each problem's referenced nodes ({x, y, z, node id as
-    // u64} at need_off + compact index)
+           o_query = 0, o_ids32 = 0, o_rows32 = 0, o_rows16 = 0, o_ev = 0, o_mark = 0, o_map = 0, o_nstat = 0, o_slot = 0,
+           o_need = 0, dev_bytes = 0;
+    // pinned host block: the problems (uploaded), then the emitted header, per row its
+    // problem and node (p << 16 | compact index), the masked rows (compact indices, 0xFFFF:
+    // no edge) and each problem's referenced nodes (x, y, z at need_off + compact index)
     size_t h_seg = 0, h_hdr = 0, h_slot = 0, h_rows = 0, h_need = 0, host_bytes = 0;
 };
-// caps[p]: the problems' packed-row capacities (need_off / need_cap are filled in here)
+// segs: the problems with seed, ends, bound, gbound, the grid box and cell, cap filled;
+// row_off / need_off / need_cap are filled in here
 PlanBatchLayout plan_batch_layout(int32_t S, int64_t ns, int32_t k, PlanSeg* segs);
 epp_status plan_batch_launch(const epp_world* world, int32_t can_pass_gate, const double lo[3], const double hi[3],
                              const PlanBatchLayout& L, void* dev, void* host, void* stream);

@@ -1,6 +1,7 @@
 // host_planner.cpp — epp::PathPlanner (drop-in for src/PathPlanner.cpp) on the batch
 // GPU planner.  See include/epp/PathPlanner.h for the algorithm.
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -159,6 +160,47 @@ public:
     }
     void* dev() const { return dev_; }
     char* host() const { return static_cast<char*>(host_); }
+    // Buffers of the whole-table search of one problem per planner thread (w), sized here
+    // for n nodes: allocated with the batch, not on the planner threads when a search falls
+    // back (a first allocation of pinned memory there took milliseconds).
+    struct Area {
+        void* dev = nullptr;
+        void* pin = nullptr;
+        void* stream = nullptr;
+        size_t dcap = 0, pcap = 0;
+    };
+    static size_t r256(size_t b) { return (b + 255) & ~size_t(255); }
+    static size_t area_dev_bytes(int64_t n, int k) {
+        const size_t m = (size_t)n * k;
+        return r256(16) + r256(m * 4) + r256(m * 2) + r256(m) + r256((size_t)epp_knn_workspace_size((int32_t)n));
+    }
+    static size_t area_pin_bytes(int64_t n, int k) { return r256(64) + r256((size_t)n * 24) + r256((size_t)n * k * 4); }
+    void ensure_areas(size_t W, int64_t n, int k) {
+        if (areas_.size() < W) areas_.resize(W);
+        const size_t db = area_dev_bytes(n, k), pb = area_pin_bytes(n, k);
+        for (size_t w = 0; w < W; ++w) {
+            Area& a = areas_[w];
+            if (!a.stream) check(epp_stream_create(&a.stream), "stream");
+            if (db > a.dcap) {
+                if (a.dev) epp_free(a.dev);
+                a.dev = nullptr;
+                a.dcap = 0;
+                check(epp_malloc(&a.dev, db), "planner fallback workspace");
+                a.dcap = db;
+            }
+            if (pb > a.pcap) {
+                if (a.pin) (void)hipHostFree(a.pin);
+                a.pin = nullptr;
+                a.pcap = 0;
+                if (hipHostMalloc(&a.pin, pb, hipHostMallocDefault) != hipSuccess) {
+                    a.pin = nullptr;
+                    throw std::runtime_error("planner fallback: hipHostMalloc failed");
+                }
+                a.pcap = pb;
+            }
+        }
+    }
+    Area& area(size_t w) { return areas_[w]; }
     void* stream() {
         if (!stream_) check(epp_stream_create(&stream_), "stream");
         return stream_;
@@ -167,9 +209,15 @@ public:
         if (dev_) epp_free(dev_);
         if (host_) (void)hipHostFree(host_);
         if (stream_) epp_stream_destroy(stream_);
+        for (Area& a : areas_) {
+            if (a.dev) epp_free(a.dev);
+            if (a.pin) (void)hipHostFree(a.pin);
+            if (a.stream) epp_stream_destroy(a.stream);
+        }
     }
 
 private:
+    std::vector<Area> areas_;
     void* dev_ = nullptr;
     void* host_ = nullptr;
     void* stream_ = nullptr;
@@ -180,8 +228,8 @@ private:
 // is the search's (no O(n) clearing per search); the heap keeps its storage.
 struct QE {
     double f;
-    int key;  // the node id: ties in f pop the lower id first, as std::priority_queue<pair<double, int>,
-              // ..., std::greater<>> does
+    int key;  // the node id, or an index in node order: ties in f pop the lower id first, as
+              // std::priority_queue<pair<double, int>, ..., std::greater<>> does
     int v;    // the search's own index of the node
 };
 struct QECmp {
@@ -301,7 +349,13 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
     // edge into the goal among the rows, more than 65,535 nodes) the whole table is built.
     const int64_t nmax = samples + 2;
     const bool restrict_ok = ellipse_ >= 1.0 && (k == 4 || k == 8 || k == 16) && nmax <= 4 * 65536;
+    // the rows' k-NN grid: cells of ~1.5 nodes (the sampling density), over the nodes of the
+    // ellipsoid bound + 7.5 cells (a query's search radius r stays below half the margin:
+    // |x - s| + |x - g| is 2-Lipschitz, so every node within r of a row's node is in it)
+    const double vbox = (hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]);
+    const double cell = std::cbrt(1.5 * std::max(vbox, 1e-12) / (double)nmax);
     std::vector<PlanSeg> segs(S);
+    std::vector<std::array<double, 6>> kbox(S);  // the whole table's k-NN box (fallback)
     for (int p = 0; p < S; ++p) {
         const Vec3& s = problems[p].first;
         const Vec3& g = problems[p].second;
@@ -312,11 +366,23 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
             q.s[d] = s[d];
             q.g[d] = g[d];
             // the grid over the sampling box widened by start and goal (every node lies inside)
-            q.box_lo[d] = std::min({lo[d], s[d], g[d]});
-            q.box_hi[d] = std::max({hi[d], s[d], g[d]});
+            kbox[p][d] = std::min({lo[d], s[d], g[d]});
+            kbox[p][3 + d] = std::max({hi[d], s[d], g[d]});
         }
         const double d_sg = (g - s).norm();
         q.bound = ellipse_ * d_sg + 0.25;
+        q.gbound = q.bound + 7.5 * cell;
+        q.h = cell;
+        {  // the gbound ellipsoid's box (foci s, g), padded, clipped to the k-NN box
+            const double a = 0.5 * q.gbound, b2 = std::max(0.0, a * a - 0.25 * d_sg * d_sg);
+            for (int d = 0; d < 3; ++d) {
+                const double u = d_sg > 0 ? (g[d] - s[d]) / d_sg : 0.0;
+                const double e = std::sqrt(a * a * u * u + b2 * (1.0 - u * u)) * (1.0 + 1e-6) + 1e-6;
+                const double c = 0.5 * (s[d] + g[d]);
+                q.glo[d] = std::max(kbox[p][d], c - e);
+                q.ghi[d] = std::min(kbox[p][3 + d], c + e);
+            }
+        }
         q.cap = 0;
         if (restrict_ok) {
             const double vbox = (hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]);
@@ -329,6 +395,9 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
     const PlanBatchLayout L = plan_batch_layout(S, samples, k, segs.data());
     BatchScratch& bs = BatchScratch::get();
     bs.ensure(L.dev_bytes, L.host_bytes);
+    // W concurrent solvers (the caller + W - 1 pool threads), each with its fallback buffers
+    const size_t W = std::min((size_t)S, (size_t)std::max(1, threads_));
+    bs.ensure_areas(W, nmax, k);
     char* H = bs.host();
     std::memcpy(H + L.h_seg, segs.data(), sizeof(PlanSeg) * S);
     void* st = bs.stream();
@@ -338,7 +407,9 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
     const uint32_t* slots = reinterpret_cast<const uint32_t*>(H + L.h_slot);
     const uint16_t* rows = reinterpret_cast<const uint16_t*>(H + L.h_rows);
     const double* need = reinterpret_cast<const double*>(H + L.h_need);
-    const int64_t R = (int64_t)std::min<uint64_t>(hdr[kPbPacked], (uint64_t)L.cap_total);
+    auto hv = [&](int field, int p) { return (int64_t)hdr[kPbPerSeg + field * S + p]; };
+    std::vector<int64_t> first(S + 1, 0);  // rows are dense in problem order
+    for (int p = 0; p < S; ++p) first[p + 1] = first[p] + std::min<int64_t>(hv(0, p), segs[p].cap);
     const double ms_batch = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_dev0).count();
     const char* dev = static_cast<const char*>(bs.dev());
 
@@ -352,29 +423,26 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
     std::vector<std::vector<Vec3>> raw(S);
     std::vector<char> found(S, 0);
     std::vector<std::exception_ptr> err(S);
-    auto solve = [&](int p) {
+    auto solve = [&](int p, size_t w) {
         Out& o = res[p];
-        const int64_t n = (int64_t)hdr[kPbPerSeg + 3 * S + p];
+        const int64_t n = hv(3, p);
         o.n = n;
-        const int64_t packed = (int64_t)hdr[kPbPerSeg + p];
-        const int64_t m = (int64_t)std::min<uint64_t>(hdr[kPbPerSeg + 4 * S + p], (uint64_t)segs[p].need_cap);
+        const int64_t packed = hv(0, p);
+        const int64_t m = std::min<int64_t>(hv(4, p), segs[p].need_cap);
         const auto t0 = std::chrono::steady_clock::now();
         int r = 0;
-        if (segs[p].cap > 0 && n <= 65535 && packed <= segs[p].cap && hdr[kPbPerSeg + 2 * S + p] > 0 && m >= 2) {
-            // this problem's rows (slot order) and referenced nodes (compact index order)
-            const double* nd = need + 4 * segs[p].need_off;
+        // (restricted: rows within capacity, exact (hv 5), a kept edge into the goal, node
+        // ids in u16; start and goal are compact indices 0 and 1: rows of their own)
+        if (segs[p].cap > 0 && n <= 65535 && packed <= segs[p].cap && hv(5, p) == 0 && hv(2, p) > 0 && m >= 2) {
+            // this problem's rows and referenced nodes (compact indices: node order)
+            const double* nd = need + 3 * segs[p].need_off;
             thread_local std::vector<int32_t> row_of;
             row_of.assign((size_t)m, -1);
-            for (int64_t sl = 0; sl < R; ++sl)
-                if ((int)(slots[sl] >> 16) == p) row_of[slots[sl] & 0xFFFFu] = (int32_t)sl;
+            for (int64_t sl = first[p]; sl < first[p + 1]; ++sl) row_of[slots[sl] & 0xFFFFu] = (int32_t)sl;
             thread_local SearchState ss;
             const double bound = segs[p].bound;
-            auto pos = [&](int v) { return Vec3(nd[4 * v], nd[4 * v + 1], nd[4 * v + 2]); };
-            auto key = [&](int v) {
-                int64_t id;
-                std::memcpy(&id, nd + 4 * v + 3, 8);
-                return (int)id;
-            };
+            auto pos = [&](int v) { return Vec3(nd[3 * v], nd[3 * v + 1], nd[3 * v + 2]); };
+            auto key = [](int v) { return v; };  // (compact indices keep the node order)
             r = astar(ss, (size_t)m, pos, key, [&](int u, double f, auto&& relax, bool closing) {
                 if (!closing) return (f <= bound) && row_of[u] >= 0;
                 const uint16_t* row = rows + (size_t)row_of[u] * k;
@@ -390,7 +458,7 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
                 raw[p] = std::move(path);
                 found[p] = 1;
                 o.edges_checked = packed * k;
-                o.edges_valid = (int64_t)hdr[kPbPerSeg + S + p];
+                o.edges_valid = hv(1, p);
                 o.rows_down = packed;
             }
         }
@@ -398,42 +466,41 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
         if (r != 1) {
             o.fallback = segs[p].cap > 0 ? 1 : 0;
             const double* d_nodes = reinterpret_cast<const double*>(dev + L.o_nodes) + (size_t)p * L.NS * 3;
-            found[p] = wholeTableSearch(d_nodes, (int32_t)n, segs[p].box_lo, segs[p].box_hi, raw[p], o.edges_checked,
-                                        o.edges_valid, o.ms_dev, o.ms_search)
+            found[p] = wholeTableSearch(d_nodes, (int32_t)n, kbox[p].data(), kbox[p].data() + 3, &bs.area(w), raw[p],
+                                        o.edges_checked, o.edges_valid, o.ms_dev, o.ms_search)
                            ? 1
                            : 0;
             o.rows_down += n;
         }
     };
-    auto run = [&](int p) {
+    auto run = [&](int p, size_t w) {
         try {
-            solve(p);
+            solve(p, w);
         } catch (...) {
             err[p] = std::current_exception();
         }
     };
-    // W concurrent solvers (the caller + W - 1 pool threads) pull problems in order
-    const size_t W = std::min((size_t)S, (size_t)std::max(1, threads_));
+    // the W solvers pull problems in order
     if (W <= 1) {
-        for (int p = 0; p < S; ++p) run(p);
+        for (int p = 0; p < S; ++p) run(p, 0);
     } else {
         int devno = 0;
         if (hipGetDevice(&devno) != hipSuccess) devno = 0;
         std::atomic<int> next{0};
-        auto drain = [&] {
-            for (int p = next++; p < S; p = next++) run(p);
+        auto drain = [&](size_t w) {
+            for (int p = next++; p < S; p = next++) run(p, w);
         };
         std::mutex done_mu;
         std::condition_variable done_cv;
         size_t pending = W - 1;
         for (size_t t = 1; t < W; ++t)
-            plan_pool().submit([&, devno] {
+            plan_pool().submit([&, devno, t] {
                 (void)hipSetDevice(devno);
-                drain();
+                drain(t);
                 std::lock_guard<std::mutex> lk(done_mu);
                 if (--pending == 0) done_cv.notify_all();
             });
-        drain();
+        drain(0);
         std::unique_lock<std::mutex> lk(done_mu);
         done_cv.wait(lk, [&] { return pending == 0; });
     }
@@ -441,6 +508,7 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
         if (e) std::rethrow_exception(e);
     // ---- one batched shortcut for every path found (reduceVertices' role) ---------------
     const auto t_sc = std::chrono::steady_clock::now();
+    const double ms_solve = std::chrono::duration<double, std::milli>(t_sc - t_dev0).count() - ms_batch;
     std::vector<std::vector<Vec3>> shortcut_in;
     std::vector<int> which;
     for (int p = 0; p < S; ++p)
@@ -459,6 +527,9 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
     std::lock_guard<std::mutex> lk(g_stats_mu);
     stats_.ms_device += ms_batch;
     stats_.ms_search += ms_sc;
+    stats_.ms_batch += ms_batch;
+    stats_.ms_solve += ms_solve;
+    stats_.ms_shortcut += ms_sc;
     for (int p = 0; p < S; ++p) {
         const Out& o = res[p];
         stats_.states_sampled += samples;
@@ -479,31 +550,35 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
 // u16, 0xFFFF: no edge) with the nodes, then A* over the forward edges and, if that does not
 // reach the goal, over the symmetrised graph.  Runs on the calling thread's own stream.
 bool PathPlanner::wholeTableSearch(const double* d_nodes, int32_t n, const double box_lo[3], const double box_hi[3],
-                                   std::vector<Vec3>& path, int64_t& edges_checked, int64_t& edges_valid,
+                                   void* area_, std::vector<Vec3>& path, int64_t& edges_checked, int64_t& edges_valid,
                                    double& ms_dev, double& ms_search) const {
     const auto t0 = std::chrono::steady_clock::now();
     const bool canPass = configParser->getPathPlannerProperties().canPassGate;
     const epp_world* w = worldPtr->device();
     const int k = k_;
-    ThreadScratch& ts = ThreadScratch::get();
-    void* st = ts.stream();
+    BatchScratch::Area& area = *static_cast<BatchScratch::Area*>(area_);
+    void* st = area.stream;
     const size_t m = (size_t)n * k;
     const size_t ws_bytes = (size_t)epp_knn_workspace_size(n);
-    ts.reset(ThreadScratch::rounded(16) + ThreadScratch::rounded(m * 4) + 2 * ThreadScratch::rounded(m * 24) +
-             ThreadScratch::rounded(m) + ThreadScratch::rounded(ws_bytes));
-    int64_t* d_ecnt = static_cast<int64_t*>(ts.carve(16));
-    int32_t* d_nbr = static_cast<int32_t*>(ts.carve(m * 4));
-    double* d_e1 = static_cast<double*>(ts.carve(m * 24));
-    double* d_e2 = static_cast<double*>(ts.carve(m * 24));
-    uint8_t* d_ev = static_cast<uint8_t*>(ts.carve(m));
-    void* d_ws = ts.carve(ws_bytes);
+    if (BatchScratch::area_dev_bytes(n, k) > area.dcap || BatchScratch::area_pin_bytes(n, k) > area.pcap)
+        throw std::runtime_error("planPath: fallback workspace too small");
+    char* dp = static_cast<char*>(area.dev);
+    int64_t* d_ecnt = reinterpret_cast<int64_t*>(dp);
+    int32_t* d_nbr = reinterpret_cast<int32_t*>(dp + BatchScratch::r256(16));
     const bool narrow = n <= 65535;
-    uint16_t* d_nbr16 = narrow ? reinterpret_cast<uint16_t*>(d_e1) : nullptr;
+    uint16_t* d_nbr16 = narrow ? reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(d_nbr) + BatchScratch::r256(m * 4))
+                               : nullptr;
+    uint8_t* d_ev = reinterpret_cast<uint8_t*>(d_nbr) + BatchScratch::r256(m * 4) + BatchScratch::r256(m * 2);
+    void* d_ws = d_ev + BatchScratch::r256(m);
     if (hipMemsetAsync(d_ecnt, 0, 16, static_cast<hipStream_t>(st)) != hipSuccess)
         throw std::runtime_error("planPath: clearing the edge counts failed");
     check(epp_knn_ws_box(d_nodes, n, k, 0.0, box_lo, box_hi, d_nbr, d_ws, ws_bytes, st), "knn");
     const epp_status ks = check_knn_motions_masked(w, d_nodes, d_nbr, n, k, canPass ? 1 : 0, d_ev, d_nbr16, 1, d_ecnt, st);
-    if (ks == EPP_ERR_UNSUPPORTED) {
+    if (ks == EPP_ERR_UNSUPPORTED) {  // (worlds without tile tables: materialised endpoints)
+        ThreadScratch& ts = ThreadScratch::get();
+        ts.reset(2 * ThreadScratch::rounded(m * 24));
+        double* d_e1 = static_cast<double*>(ts.carve(m * 24));
+        double* d_e2 = static_cast<double*>(ts.carve(m * 24));
         check(epp_knn_edges(d_nodes, d_nbr, n, k, d_e1, d_e2, st), "edges");
         check(epp_check_motions(w, d_e1, d_e2, (int64_t)m, canPass ? 1 : 0, 0, d_ev, st), "motion check");
         check(mask_edges_count_acc(d_nbr, d_ev, (int64_t)m, 1, d_ecnt, st, d_nbr16), "mask edges");
@@ -511,9 +586,10 @@ bool PathPlanner::wholeTableSearch(const double* d_nodes, int32_t n, const doubl
         check(ks, "motion check");
     }
     // the downloads queued back to back, one synchronisation
-    int64_t* ecnt = static_cast<int64_t*>(ts.pinned(2, 16 * sizeof(double)));
-    const double* nodes = static_cast<const double*>(ts.pinned(0, (size_t)n * 24));
-    void* h_tab = ts.pinned(1, m * 4);
+    char* hp = static_cast<char*>(area.pin);
+    int64_t* ecnt = reinterpret_cast<int64_t*>(hp);
+    const double* nodes = reinterpret_cast<const double*>(hp + BatchScratch::r256(64));
+    void* h_tab = hp + BatchScratch::r256(64) + BatchScratch::r256((size_t)n * 24);
     check(epp_memcpy_d2h_async(ecnt, d_ecnt, 16, st), "download");
     check(epp_memcpy_d2h_async(const_cast<double*>(nodes), d_nodes, (uint64_t)n * 24, st), "download");
     if (narrow) check(epp_memcpy_d2h_async(h_tab, d_nbr16, m * 2, st), "download");

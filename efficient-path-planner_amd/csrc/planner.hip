@@ -1918,31 +1918,31 @@ __global__ __launch_bounds__(256) void k_pack_ellipse_rows(const double* __restr
 // ---- the batched planner: one launch per stage for all of a batch's problems ----------
 // (epp_internal.h, PlanBatchLayout).  Problem p = blockIdx.y of the per-problem stages; its
 // samples at xyz + p ns, its nodes at nodes + p NS (NS = 2^ns_log >= 65536: a node's id in
-// its problem is the low bits of its global id p NS + node, and its low 16 bits when the
-// problem has <= 65535 nodes), its k-NN workspace at kws + p kws_stride (KnnLayout for
-// ns + 2 nodes), its k-NN rows at nbr + p NS k.  Node counts stay on the device.
+// its problem is the low bits of its global id p NS + node), its k-NN grid workspace at
+// kws + p kws_stride (KnnLayout for ns + 2 nodes), its queries at query + row_off.  Node
+// counts stay on the device.
 struct PlanBatchDev {
     const PlanSeg* seg;
     int S, k, ns_log, nbc, cap_total, nctr;
-    int64_t ns, NS, need_cap;
+    int64_t ns, NS;
     double lo[3], hi[3];
     double* xyz;
     uint8_t* valid;
     double* nodes;
     unsigned long long* cstat;
+    unsigned long long* nstat;  // k_pb_number's look-back status words: NS / 1024 per problem
     unsigned long long* ctr;
     char* kws;
     size_t kws_stride, l_cell, l_sidx, l_sxyz, l_cnt, l_start, l_fill, l_stat;
-    int l_cap, nclr, scan_blocks;
-    int32_t* nbr;
-    int32_t* retry;
-    int32_t* ids32;
-    int32_t* rows32;
-    uint16_t* rows16;
-    uint32_t* mark;     // a bit per node: referenced by a packed row
-    int32_t* map;       // node (global id) -> its compact index (referenced nodes only)
-    uint32_t* slot;     // packed row -> p << 16 | compact index of its node
-    double* need;       // 4 doubles per referenced node: x, y, z, node id (u64 bits)
+    int l_cap, nclr;
+    int32_t* query;     // per problem (at row_off): its listed nodes (node ids)
+    int32_t* ids32;     // row -> global node id
+    int32_t* rows32;    // row -> its k neighbours (global ids)
+    uint16_t* rows16;   // the same masked (node ids, then compact indices; 0xFFFF: none)
+    uint8_t* mark;      // a byte per node: referenced by a row
+    int32_t* map;       // node (global id) -> compact index (referenced nodes only)
+    uint32_t* slot;     // row -> p << 16 | compact index of its node
+    double* need;       // 3 doubles per referenced node (at need_off + compact index)
 };
 
 struct KnnSeg {
@@ -1962,14 +1962,21 @@ __device__ __forceinline__ KnnSeg knn_seg(const PlanBatchDev& P, int p) {
             reinterpret_cast<int*>(b + P.l_start), reinterpret_cast<int*>(b + P.l_fill),
             reinterpret_cast<unsigned long long*>(b + P.l_stat)};
 }
+__device__ __forceinline__ unsigned long long& pb_ctr(const PlanBatchDev& P, int field, int p) {
+    return P.ctr[kPbPerSeg + field * P.S + p];
+}
+enum : int { kFQueries = 0, kFKept = 1, kFGoal = 2, kFNodes = 3, kFNeed = 4, kFInexact = 5 };
 
 // samples (k_sample_uniform's arithmetic) + clears: the problem's compaction status words
-// and needed-node bits; problem 0 also the batch counters
+// and node marks; problem 0 also the batch counters
 __global__ __launch_bounds__(256) void k_pb_sample(PlanBatchDev P) {
     const int p = blockIdx.y;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i < P.nbc) P.cstat[(int64_t)p * P.nbc + i] = 0ull;
-    if (i < (P.NS >> 5)) P.mark[(int64_t)p * (P.NS >> 5) + i] = 0u;
+    if (P.cap_total > 0 && i < P.NS / kCompactChunk) P.nstat[(int64_t)p * (P.NS / kCompactChunk) + i] = 0ull;
+    // (the marks exist only when some problem has restricted rows: cap_total > 0)
+    if (P.cap_total > 0 && i < (P.NS >> 4))
+        reinterpret_cast<uint4*>(P.mark + ((int64_t)p << P.ns_log))[i] = make_uint4(0u, 0u, 0u, 0u);
     if (p == 0 && i < P.nctr) P.ctr[i] = 0ull;
     if (i >= P.ns) return;
     const uint64_t seed = P.seg[p].seed;
@@ -1983,83 +1990,39 @@ __global__ __launch_bounds__(256) void k_pb_sample(PlanBatchDev P) {
     x[2] = P.lo[2] + (P.hi[2] - P.lo[2]) * u2;
 }
 
-// nodes = start, goal, the valid samples in sample order; ncount[p] = their number
+// nodes = start, goal, the valid samples in sample order; the node count into the header;
+// the grid's shape and cleared counters (the workspace may hold anything)
 __global__ __launch_bounds__(kCompactThreads) void k_pb_compact(PlanBatchDev P, uint32_t tag) {
     const int p = blockIdx.y;
     double* out = P.nodes + (int64_t)p * P.NS * 3;
     const PlanSeg& q = P.seg[p];
     if (blockIdx.x == 0 && threadIdx.x < 6) out[threadIdx.x] = threadIdx.x < 3 ? q.s[threadIdx.x] : q.g[threadIdx.x - 3];
-    if (blockIdx.x == 0 && threadIdx.x < 2 && q.cap > 0) {
-        // start and goal take compact indices 0 and 1 of the referenced nodes
-        const int64_t gid = ((int64_t)p << P.ns_log) + threadIdx.x;
-        atomicOr(P.mark + (gid >> 5), 1u << (gid & 31));
-        P.map[gid] = (int32_t)threadIdx.x;
-        double* d = P.need + (q.need_off + threadIdx.x) * 4;
-        const double* x = threadIdx.x == 0 ? q.s : q.g;
-        d[0] = x[0];
-        d[1] = x[1];
-        d[2] = x[2];
-        d[3] = __longlong_as_double((long long)threadIdx.x);
-        if (threadIdx.x == 0) P.ctr[kPbPerSeg + 4 * P.S + p] = 2ull;
+    if (q.cap > 0) {
+        const KnnSeg ks = knn_seg(P, p);
+        for (int i = blockIdx.x * kCompactThreads + threadIdx.x; i < P.nclr; i += gridDim.x * kCompactThreads) ks.cnt[i] = 0;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            KnnGrid gv{};
+            int64_t cells = 1;
+            double h = q.h;
+            for (;;) {  // (cells bounded by the workspace's capacity; coarser if need be)
+                cells = 1;
+                for (int d = 0; d < 3; ++d) {
+                    gv.dims[d] = (int)fmin((q.ghi[d] - q.glo[d]) / h, 1023.0) + 1;
+                    cells *= gv.dims[d];
+                }
+                if (cells <= P.l_cap) break;
+                h *= 1.25;
+            }
+            for (int d = 0; d < 3; ++d) gv.lo[d] = q.glo[d];
+            gv.h = h;
+            gv.inv_h = 1.0 / h;
+            gv.ncell = (int)cells;
+            gv.qbound = 1e300;
+            *ks.g = gv;
+        }
     }
     compact_block(P.xyz + (int64_t)p * P.ns * 3, P.valid + (int64_t)p * P.ns, P.ns, P.cstat + (int64_t)p * P.nbc, tag,
-                  out + 6, reinterpret_cast<int64_t*>(P.ctr) + kPbPerSeg + 3 * P.S + p, 2, blockIdx.x, gridDim.x);
-}
-
-__device__ __forceinline__ int pb_count(const PlanBatchDev& P, int p) {
-    return (int)P.ctr[kPbPerSeg + 3 * P.S + p];
-}
-
-// the problem's grid (knn_grid_shape from its node count, on the device) + cleared counters
-__global__ __launch_bounds__(kBoundsThreads) void k_pb_knn_prep(PlanBatchDev P) {
-    const int p = blockIdx.y;
-    const KnnSeg ks = knn_seg(P, p);
-    for (int i = blockIdx.x * kBoundsThreads + threadIdx.x; i < P.nclr; i += gridDim.x * kBoundsThreads) ks.cnt[i] = 0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        const PlanSeg& q = P.seg[p];
-        const double mn[3] = {q.box_lo[0], q.box_lo[1], q.box_lo[2]}, mx[3] = {q.box_hi[0], q.box_hi[1], q.box_hi[2]};
-        KnnGrid gv;
-        knn_grid_shape(mn, mx, pb_count(P, p), P.l_cap, kNodesPerCell, &gv);
-        for (int d = 0; d < 3; ++d) {
-            gv.qs[d] = q.s[d];
-            gv.qg[d] = q.g[d];
-        }
-        gv.qbound = q.bound;
-        *ks.g = gv;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_pb_knn_count(PlanBatchDev P) {
-    const int p = blockIdx.y;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= pb_count(P, p)) return;
-    const KnnSeg ks = knn_seg(P, p);
-    const KnnGrid g = *ks.g;
-    const double* nd = P.nodes + ((int64_t)p * P.NS + i) * 3;
-    const int cx = knn_cell_axis(nd[0], g, 0), cy = knn_cell_axis(nd[1], g, 1), cz = knn_cell_axis(nd[2], g, 2);
-    const int c = (cz * g.dims[1] + cy) * g.dims[0] + cx;
-    ks.cell_of[i] = c;
-    atomicAdd(&ks.cnt[c], 1);
-}
-
-__global__ __launch_bounds__(kScanThreads) void k_pb_knn_scan(PlanBatchDev P, uint32_t tag) {
-    const KnnSeg ks = knn_seg(P, blockIdx.y);
-    knn_scan_block(ks.g, ks.cnt, ks.start, ks.stat, tag, blockIdx.x);
-}
-
-__global__ __launch_bounds__(256) void k_pb_knn_scatter(PlanBatchDev P) {
-    const int p = blockIdx.y;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= pb_count(P, p)) return;
-    const KnnSeg ks = knn_seg(P, p);
-    const int c = ks.cell_of[i];
-    const int pos = ks.start[c] + atomicAdd(&ks.fill[c], 1);
-    if (pos >= ks.start[c + 1]) return;  // cannot happen with cleared counters
-    const double* nd = P.nodes + ((int64_t)p * P.NS + i) * 3;
-    ks.sidx[pos] = i;
-    ks.sxyz[3 * pos] = nd[0];
-    ks.sxyz[3 * pos + 1] = nd[1];
-    ks.sxyz[3 * pos + 2] = nd[2];
+                  out + 6, reinterpret_cast<int64_t*>(&pb_ctr(P, kFNodes, p)), 2, blockIdx.x, gridDim.x);
 }
 
 __device__ __forceinline__ double pb_ellipse(const PlanSeg& q, const double* x) {
@@ -2070,169 +2033,343 @@ __device__ __forceinline__ double pb_ellipse(const PlanSeg& q, const double* x) 
     return ds + dg;
 }
 
-// the nodes inside the problem's ellipsoid (widened by 1e-8 relative + 1e-6 m: looser than
-// the packing's test) listed for k_pb_retry, as global ids p NS + node; one atomic per wave
-__global__ __launch_bounds__(256) void k_pb_list(PlanBatchDev P) {
+// Per node: inside the grid ellipsoid -> its cell counted (cell_of, else -1); inside the
+// row ellipsoid (widened by 1e-8 relative + 1e-6 m) -> listed as a query, ranks from one
+// atomic per workgroup.
+constexpr int kPbBlock = 1024;
+__global__ __launch_bounds__(kPbBlock) void k_pb_member(PlanBatchDev P) {
     const int p = blockIdx.y;
     const PlanSeg& q = P.seg[p];
-    if (q.cap <= 0) return;  // (block-uniform: no restricted rows for this problem)
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    const bool in = i < pb_count(P, p) && pb_ellipse(q, P.nodes + ((int64_t)p * P.NS + i) * 3) <= q.bound * (1.0 + 1e-8) + 1e-6;
-    const unsigned long long bal = __ballot(in);
-    if (!bal) return;
-    const int lane = threadIdx.x & 63, first = __ffsll(bal) - 1;
-    unsigned long long base = 0;
-    if (lane == first) base = atomicAdd(P.ctr + kPbListed, (unsigned long long)__popcll(bal));
-    base = __shfl(base, first, 64);
-    if (in) P.retry[base + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)(((int64_t)p << P.ns_log) + i);
-}
-
-// the listed nodes' exact k-NN rows: one wave per query over its problem's grid (the
-// retry walk of k_knn_tile, knn_retry_wave, with no bound from a tile pass)
-template <int K>
-__global__ __launch_bounds__(64) void k_pb_retry(PlanBatchDev P) {
-    const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwaves = (gridDim.x * blockDim.x) >> 6;
-    const int nq = (int)P.ctr[kPbListed];
-    for (int i = wave; i < nq; i += nwaves) {  // wave-uniform
-        const int e = P.retry[i];
-        const int p = e >> P.ns_log, node = e & (int)(P.NS - 1);
-        const KnnSeg ks = knn_seg(P, p);
-        const KnnGrid g = *ks.g;
-        knn_retry_wave<K>(g, 1e300, P.nodes + (int64_t)p * P.NS * 3, ks.sxyz, ks.sidx, ks.start, node, INFINITY,
-                          P.nbr + (int64_t)p * P.NS * K);
-    }
-}
-
-// k_pack_ellipse_rows for every problem at once: the rows of its nodes inside the
-// ellipsoid (widened by 1e-9 relative + 1e-9 m), up to its capacity, packed into global
-// slots with global node ids (a problem's ranks from its own counter, the slots of the
-// accepted ones from the batch's: one atomic each per wave)
-__global__ __launch_bounds__(256) void k_pb_pack(PlanBatchDev P) {
-    const int p = blockIdx.y;
-    const PlanSeg& q = P.seg[p];
-    if (q.cap <= 0) return;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    const bool in = i < pb_count(P, p) && pb_ellipse(q, P.nodes + ((int64_t)p * P.NS + i) * 3) <= q.bound * (1.0 + 1e-9) + 1e-9;
-    const unsigned long long bal = __ballot(in);
-    if (!bal) return;
-    const int lane = threadIdx.x & 63, first = __ffsll(bal) - 1;
-    const int cnt = __popcll(bal);
-    unsigned long long base = 0, gbase = 0;
-    if (lane == first) {
-        base = atomicAdd(P.ctr + kPbPerSeg + p, (unsigned long long)cnt);
-        const long long acc = min((long long)cnt, max(0ll, (long long)q.cap - (long long)base));
-        if (acc > 0) gbase = atomicAdd(P.ctr + kPbPacked, (unsigned long long)acc);
-    }
-    base = __shfl(base, first, 64);
-    gbase = __shfl(gbase, first, 64);
-    const int r = __popcll(bal & ((1ull << lane) - 1ull));
-    if (!in || base + r >= (unsigned long long)q.cap) return;
-    const unsigned long long slot = gbase + r;
-    const int64_t off = (int64_t)p << P.ns_log;
-    P.ids32[slot] = (int32_t)(off + i);
-    const int32_t* src = P.nbr + (off + i) * P.k;
-    int32_t* dst = P.rows32 + slot * P.k;
-    for (int c = 0; c < P.k; ++c) {
-        const int32_t v = src[c];
-        dst[c] = v < 0 ? -1 : (int32_t)(off + v);
-    }
-}
-
-// The nodes the packed rows reference (each row's node and its kept neighbours), each once
-// (a bit per node): numbered per problem in a compact index (after start 0 and goal 1, in
-// arbitrary order) and listed as {x, y, z, node id}; and per problem the kept edges of its
-// rows and those into its goal (node 1).  One thread per row entry.
-__global__ __launch_bounds__(256) void k_pb_need(PlanBatchDev P) {
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t rows = (int64_t)min(P.ctr[kPbPacked], (unsigned long long)P.cap_total);
-    const bool act = e < rows * P.k;
-    const int lane = threadIdx.x & 63;
-    int p = -1;
-    bool keep = false, goal = false;
-    int64_t cand[2] = {-1, -1};  // (global ids: the neighbour, and the row's node once per row)
-    if (act) {
-        const int64_t slot = e / P.k;
-        const int c = (int)(e - slot * P.k);
-        const int32_t u = P.ids32[slot];
-        p = u >> P.ns_log;
-        const uint16_t v = P.rows16[e];
-        keep = v != 0xFFFF;
-        goal = keep && v == 1;
-        if (keep) cand[0] = ((int64_t)p << P.ns_log) + v;
-        if (c == 0) cand[1] = u;
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-        bool fresh = false;
-        if (cand[t] >= 0) {
-            const uint32_t bit = 1u << (cand[t] & 31);
-            fresh = !(atomicOr(P.mark + (cand[t] >> 5), bit) & bit);
+    if (q.cap <= 0) return;  // (block-uniform)
+    __shared__ int s_cnt[kPbBlock / 64];
+    __shared__ unsigned long long s_base;
+    const int i = blockIdx.x * kPbBlock + threadIdx.x;
+    const int n = (int)pb_ctr(P, kFNodes, p);
+    const KnnSeg ks = knn_seg(P, p);
+    bool in = false;
+    if (i < n) {
+        const double* x = P.nodes + ((int64_t)p * P.NS + i) * 3;
+        const double f = pb_ellipse(q, x);
+        int c = -1;
+        if (f <= q.gbound) {
+            const KnnGrid& g = *ks.g;
+            const int cx = knn_cell_axis(x[0], g, 0), cy = knn_cell_axis(x[1], g, 1), cz = knn_cell_axis(x[2], g, 2);
+            c = (cz * g.dims[1] + cy) * g.dims[0] + cx;
+            atomicAdd(&ks.cnt[c], 1);
         }
-        unsigned long long todo = __ballot(fresh);
-        while (todo) {  // one atomic per (wave, problem) among the fresh lanes
-            const int p0 = __shfl(p, __ffsll(todo) - 1, 64);
-            const unsigned long long mine = __ballot(fresh && p == p0);
-            const int first = __ffsll(mine) - 1;
-            unsigned long long base = 0;
-            if (lane == first) base = atomicAdd(P.ctr + kPbPerSeg + 4 * P.S + p0, (unsigned long long)__popcll(mine));
-            base = __shfl(base, first, 64);
-            if (fresh && p == p0) {
-                const PlanSeg& q = P.seg[p0];
-                const int64_t at = (int64_t)(base + __popcll(mine & ((1ull << lane) - 1ull)));
-                P.map[cand[t]] = (int32_t)at;
-                if (at < q.need_cap) {
-                    const double* x = P.nodes + cand[t] * 3;
-                    double* d = P.need + (q.need_off + at) * 4;
-                    d[0] = x[0];
-                    d[1] = x[1];
-                    d[2] = x[2];
-                    d[3] = __longlong_as_double((long long)(cand[t] & (P.NS - 1)));
+        ks.cell_of[i] = c;
+        in = f <= q.bound * (1.0 + 1e-8) + 1e-6;
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const unsigned long long bal = __ballot(in);
+    if (lane == 0) s_cnt[wv] = __popcll(bal);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int w = 0; w < kPbBlock / 64; ++w) t += s_cnt[w];
+        s_base = t ? atomicAdd(&pb_ctr(P, kFQueries, p), (unsigned long long)t) : 0ull;
+    }
+    __syncthreads();
+    if (!in) return;
+    unsigned long long r = s_base + __popcll(bal & ((1ull << lane) - 1ull));
+    for (int w = 0; w < wv; ++w) r += s_cnt[w];
+    if (r < (unsigned long long)q.cap) P.query[q.row_off + (int64_t)r] = i;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_pb_knn_scan(PlanBatchDev P, uint32_t tag) {
+    if (P.seg[blockIdx.y].cap <= 0) return;
+    const KnnSeg ks = knn_seg(P, blockIdx.y);
+    knn_scan_block(ks.g, ks.cnt, ks.start, ks.stat, tag, blockIdx.x);
+}
+
+__global__ __launch_bounds__(256) void k_pb_knn_scatter(PlanBatchDev P) {
+    const int p = blockIdx.y;
+    if (P.seg[p].cap <= 0) return;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int)pb_ctr(P, kFNodes, p)) return;
+    const KnnSeg ks = knn_seg(P, p);
+    const int c = ks.cell_of[i];
+    if (c < 0) return;
+    const int pos = ks.start[c] + atomicAdd(&ks.fill[c], 1);
+    if (pos >= ks.start[c + 1]) return;  // cannot happen with cleared counters
+    const double* nd = P.nodes + ((int64_t)p * P.NS + i) * 3;
+    ks.sidx[pos] = i;
+    ks.sxyz[3 * pos] = nd[0];
+    ks.sxyz[3 * pos + 1] = nd[1];
+    ks.sxyz[3 * pos + 2] = nd[2];
+}
+
+// The exact k-NN row of one listed query from its problem's grid (whole wave).  Every node
+// within distance r of x has |y - s| + |y - g| <= f(x) + 2 r, so while f(x) + 2 r <= gbound
+// (with a margin far above the rounding) every such node is in the grid: the candidates
+// within r are all the nodes within r.  r = 1.6 h first (~26 nodes at the grid's density),
+// then x 1.5 until at least K are listed; each listed entry's rank in (distance, index)
+// order is counted against the list (the order k_knn / the oracle use).  The box's x-runs of
+// cells (one contiguous range of the cell-sorted nodes each) are laid out over all the lanes
+// by a wave scan of their lengths, kU candidates per lane in flight.  Returns false when
+// the radius would leave the grid ellipsoid or the list overflows (the row is then not
+// exact, and the caller flags the problem).
+template <int K>
+__device__ __forceinline__ bool pb_query_row(const KnnGrid& g, const double* __restrict__ sxyz,
+                                             const int* __restrict__ sidx, const int* __restrict__ start,
+                                             const double (&p)[3], double f, double gbound, int self,
+                                             int32_t* __restrict__ out, int64_t off) {
+    constexpr int kCap = 512;
+    constexpr int kU = 2;  // candidates per lane in flight (4: 87 VGPRs, five waves per SIMD)
+    __shared__ double s_d[kCap];
+    __shared__ int s_j[kCap];
+    const int lane = threadIdx.x & 63;
+    double r = 1.6 * g.h;
+    for (int it = 0; it < 4; ++it, r *= 1.5) {  // wave-uniform
+        if (!(f + 2.0 * r * (1.0 + 1e-9) + 1e-9 <= gbound)) return false;
+        const double b2 = r * r;
+        const double rb = r * (1.0 + 1e-9) + 1e-12 * (1.0 + fabs(p[0]) + fabs(p[1]) + fabs(p[2]));
+        int lo[3], hi[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            lo[d] = knn_cell_axis(p[d] - rb, g, d);
+            hi[d] = knn_cell_axis(p[d] + rb, g, d);
+        }
+        const int ny = hi[1] - lo[1] + 1, rows = ny * (hi[2] - lo[2] + 1);
+        int cnt = 0;  // (wave-uniform)
+        for (int rb0 = 0; rb0 < rows; rb0 += 64) {
+            const int row = rb0 + lane;
+            int s0 = 0, len = 0;
+            if (row < rows) {
+                const int a = ((lo[2] + row / ny) * g.dims[1] + lo[1] + row % ny) * g.dims[0];
+                s0 = start[a + lo[0]];
+                len = start[a + hi[0] + 1] - s0;
+            }
+            int incl = len;  // inclusive scan of the run lengths over the lanes
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += t;
+            }
+            const int excl = incl - len, T = __shfl(incl, 63, 64);
+            for (int t0 = 0; t0 < T; t0 += 64 * kU) {
+                double dd[kU];
+                int jj[kU];
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    const int t = t0 + u * 64 + lane;
+                    // the run holding candidate t: the last lane whose exclusive start <= t
+                    int a = 0;
+#pragma unroll
+                    for (int step = 32; step > 0; step >>= 1)
+                        if (__shfl(excl, a + step, 64) <= t) a += step;
+                    const int q = __shfl(s0, a, 64) + (t - __shfl(excl, a, 64));
+                    const bool ok = t < T;
+                    const int qq = ok ? q : 0;  // (past the list: any valid entry, skipped below)
+                    jj[u] = ok ? sidx[qq] : self;
+                    const double ddx = sxyz[3 * qq] - p[0], ddy = sxyz[3 * qq + 1] - p[1], ddz = sxyz[3 * qq + 2] - p[2];
+                    dd[u] = (ddx * ddx + ddy * ddy) + ddz * ddz;
+                }
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    const bool keep = jj[u] != self && dd[u] <= b2;
+                    const unsigned long long kb = __ballot(keep);
+                    const int at = cnt + __popcll(kb & ((1ull << lane) - 1ull));
+                    if (keep && at < kCap) {
+                        s_d[at] = dd[u];
+                        s_j[at] = jj[u];
+                    }
+                    cnt += __popcll(kb);
                 }
             }
-            todo &= ~mine;
         }
+        if (cnt > kCap) return false;
+        if (cnt < K) continue;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's list is complete
+        if (cnt <= 64) {  // entry i on lane i: ranks by v_readlane
+            const bool mine = lane < cnt;
+            const double di = mine ? s_d[lane] : 0.0;
+            const int ji = mine ? s_j[lane] : 0;
+            const int dlo = __double2loint(di), dhi = __double2hiint(di);
+            int rank = 0;
+            for (int f2 = 0; f2 < cnt; ++f2) {
+                const double df = __hiloint2double(__builtin_amdgcn_readlane(dhi, f2), __builtin_amdgcn_readlane(dlo, f2));
+                rank += ((df < di) | ((df == di) & (__builtin_amdgcn_readlane(ji, f2) < ji))) ? 1 : 0;
+            }
+            if (mine && rank < K) out[rank] = (int32_t)(off + ji);
+        } else {
+            for (int i = lane; i < cnt; i += 64) {
+                const double di = s_d[i];
+                const int ji = s_j[i];
+                int rank = 0;
+                for (int f2 = 0; f2 < cnt; ++f2) {  // (every lane reads entry f2: LDS broadcast)
+                    const double df = s_d[f2];
+                    rank += ((df < di) | ((df == di) & (s_j[f2] < ji))) ? 1 : 0;
+                }
+                if (rank < K) out[rank] = (int32_t)(off + ji);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the list is rewritten by the next query)
+        return true;
     }
-    // per-problem edge counts: one atomic per (wave, problem) present in the wave
-    const unsigned long long kb = __ballot(keep), gb = __ballot(goal);
-    unsigned long long todo = __ballot(act);
-    while (todo) {
-        const int p0 = __shfl(p, __ffsll(todo) - 1, 64);
-        const unsigned long long mine = __ballot(act && p == p0);
-        const int nk = __popcll(mine & kb), ng = __popcll(mine & gb);
-        if (lane == __ffsll(mine) - 1) {
-            if (nk) atomicAdd(P.ctr + kPbPerSeg + P.S + p0, (unsigned long long)nk);
-            if (ng) atomicAdd(P.ctr + kPbPerSeg + 2 * P.S + p0, (unsigned long long)ng);
+    return false;
+}
+
+// The listed queries' rows, dense in problem order (row d of problem p: its (d - first
+// row of p)-th query), one wave per query: the row (global ids) and the row's node.
+template <int K>
+__global__ __launch_bounds__(64) void k_pb_rows(PlanBatchDev P) {
+    const int lane = threadIdx.x;
+    const int wave = blockIdx.x, nwaves = gridDim.x;  // (one wave per workgroup)
+    // rows per problem (lane p holds problem p's) and their inclusive prefix
+    int mine = 0;
+    if (lane < P.S) mine = (int)min(pb_ctr(P, kFQueries, lane), (unsigned long long)max(P.seg[lane].cap, 0));
+    int incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    const int D = __shfl(incl, 63, 64);
+    if (wave == 0 && lane == 0) P.ctr[kPbRows] = (unsigned long long)D;
+    for (int d = wave; d < D; d += nwaves) {  // wave-uniform
+        const int p = __popcll(__ballot(lane < P.S && incl <= d));  // problems whose rows end at or before d
+        const int first = __builtin_amdgcn_readfirstlane(__shfl(incl - mine, p, 64));
+        const PlanSeg& q = P.seg[p];
+        const int self = __builtin_amdgcn_readfirstlane(P.query[q.row_off + (d - first)]);
+        const int64_t off = (int64_t)p << P.ns_log;
+        const KnnSeg ks = knn_seg(P, p);
+        const KnnGrid g = *ks.g;
+        const double* x = P.nodes + (off + self) * 3;
+        const double pt[3] = {x[0], x[1], x[2]};
+        const double f = pb_ellipse(q, pt);
+        if (lane == 0) P.ids32[d] = (int32_t)(off + self);
+        if (!pb_query_row<K>(g, ks.sxyz, ks.sidx, ks.start, pt, f, q.gbound, self, P.rows32 + (int64_t)d * K, off)) {
+            if (lane == 0) pb_ctr(P, kFInexact, p) = 1ull;
+            if (lane < K) P.rows32[(int64_t)d * K + lane] = -1;  // (the problem takes the whole table)
         }
-        todo &= ~mine;
     }
 }
 
-// The packed rows in compact indices (in place) and each slot's problem and node.
+// The nodes the rows reference (each row's node and its kept neighbours) marked (byte
+// stores: no atomics); per problem the kept edges of its rows and those into its goal
+// (node 1), summed per workgroup in LDS.
+__global__ __launch_bounds__(kPbBlock) void k_pb_mark(PlanBatchDev P) {
+    __shared__ unsigned int s_k[64], s_g[64];
+    for (int i = threadIdx.x; i < 64; i += kPbBlock) s_k[i] = s_g[i] = 0u;
+    __syncthreads();
+    const int64_t e = (int64_t)blockIdx.x * kPbBlock + threadIdx.x;
+    const int64_t rows = (int64_t)P.ctr[kPbRows];
+    if (e < rows * P.k) {
+        const int64_t r = e / P.k;
+        const int32_t u = P.ids32[r];
+        const int p = u >> P.ns_log;
+        const uint16_t v = P.rows16[e];
+        if (e == r * P.k) P.mark[u] = 1;
+        if (v != 0xFFFF) {
+            P.mark[((int64_t)p << P.ns_log) + v] = 1;
+            atomicAdd(&s_k[p], 1u);
+            if (v == 1) atomicAdd(&s_g[p], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < P.S && s_k[threadIdx.x]) {
+        atomicAdd(&pb_ctr(P, kFKept, threadIdx.x), (unsigned long long)s_k[threadIdx.x]);
+        if (s_g[threadIdx.x]) atomicAdd(&pb_ctr(P, kFGoal, threadIdx.x), (unsigned long long)s_g[threadIdx.x]);
+    }
+}
+
+// Per problem: the marked nodes numbered in node order -- an ordered compaction of the
+// marks, chunks of 1024 node ids per workgroup (4 rounds of 256), the chunk's offset by
+// decoupled look-back (lb_exclusive); map[node] = its index, its coordinates listed at
+// need_off + index.  The workgroup holding the problem's last node writes the count.
+__global__ __launch_bounds__(kCompactThreads) void k_pb_number(PlanBatchDev P, uint32_t tag) {
+    const int p = blockIdx.y;
+    const PlanSeg& q = P.seg[p];
+    if (q.cap <= 0) return;  // (block-uniform)
+    const int n = (int)pb_ctr(P, kFNodes, p);
+    const int b = blockIdx.x;
+    if (b * kCompactChunk >= n) return;  // (no later chunk waits on it)
+    constexpr int NW = kCompactThreads / 64;
+    __shared__ int wcnt[kCompactRounds * NW];
+    __shared__ long long s_excl;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t off = (int64_t)p << P.ns_log;
+    unsigned long long* st = P.nstat + (int64_t)p * (P.NS / kCompactChunk);
+    bool v[kCompactRounds];
+    unsigned long long bal[kCompactRounds];
+#pragma unroll
+    for (int r = 0; r < kCompactRounds; ++r) {
+        const int i = b * kCompactChunk + r * kCompactThreads + threadIdx.x;
+        v[r] = i < n && P.mark[off + i] != 0;
+        bal[r] = __ballot(v[r]);
+        if (lane == 0) wcnt[r * NW + wv] = __popcll(bal[r]);
+    }
+    __syncthreads();
+    int before[kCompactRounds], total = 0;
+#pragma unroll
+    for (int qq = 0; qq < kCompactRounds * NW; ++qq) {
+#pragma unroll
+        for (int r = 0; r < kCompactRounds; ++r)
+            if (qq == r * NW + wv) before[r] = total;
+        total += wcnt[qq];
+    }
+    if (wv == 0) {
+        if (lane == 0) lb_publish(st, b, tag, b == 0, total);
+        const long long ex = b == 0 ? 0ll : lb_exclusive(st, b, tag);
+        if (lane == 0) {
+            if (b > 0) lb_publish(st, b, tag, true, ex + total);
+            s_excl = ex;
+            if ((b + 1) * kCompactChunk >= n) pb_ctr(P, kFNeed, p) = (unsigned long long)(ex + total);
+        }
+    }
+    __syncthreads();
+    const long long ex = s_excl;
+#pragma unroll
+    for (int r = 0; r < kCompactRounds; ++r) {
+        if (v[r]) {
+            const int i = b * kCompactChunk + r * kCompactThreads + threadIdx.x;
+            const long long at = ex + before[r] +
+                                 (long long)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal[r] >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)bal[r], 0u));
+            P.map[off + i] = (int32_t)at;
+            if (at < q.need_cap) {
+                const double* x = P.nodes + (off + i) * 3;
+                double* d = P.need + (q.need_off + at) * 3;
+                d[0] = x[0];
+                d[1] = x[1];
+                d[2] = x[2];
+            }
+        }
+    }
+}
+
+// The rows in compact indices (in place) and each row's problem and node.
 __global__ __launch_bounds__(256) void k_pb_remap(PlanBatchDev P) {
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t rows = (int64_t)min(P.ctr[kPbPacked], (unsigned long long)P.cap_total);
+    const int64_t rows = (int64_t)P.ctr[kPbRows];
     if (e >= rows * P.k) return;
-    const int64_t slot = e / P.k;
-    const int32_t u = P.ids32[slot];
+    const int64_t r = e / P.k;
+    const int32_t u = P.ids32[r];
     const int p = u >> P.ns_log;
     const uint16_t v = P.rows16[e];
     if (v != 0xFFFF) P.rows16[e] = (uint16_t)P.map[((int64_t)p << P.ns_log) + v];
-    if (e == slot * P.k) P.slot[slot] = ((uint32_t)p << 16) | ((uint32_t)P.map[u] & 0xFFFFu);
+    if (e == r * P.k) P.slot[r] = ((uint32_t)p << 16) | ((uint32_t)P.map[u] & 0xFFFFu);
 }
 
 // The results into pinned host memory, only the bytes in use: the header (counters), the
-// slots' problem and node (u32), the masked rows (u16), every problem's referenced nodes
-// (32 B each, at its own offset).  16-byte stores (the device parts are 16-byte padded).
+// rows' problem and node (u32), the masked rows (u16), every problem's referenced nodes
+// (24 B each, at its own offset).  16-byte stores (the device parts are 16-byte padded).
 __global__ __launch_bounds__(256) void k_pb_emit(PlanBatchDev P, unsigned long long* __restrict__ hdr,
                                                   uint4* __restrict__ h_slot, uint4* __restrict__ h_rows,
                                                   uint4* __restrict__ h_need) {
-    __shared__ long long pre[65];  // need chunks before problem p (S <= 64)
-    const int64_t rows = (int64_t)min(P.ctr[kPbPacked], (unsigned long long)P.cap_total);
+    __shared__ long long pre[65];  // 16-byte chunks of the referenced nodes before problem p (S <= 64)
+    __shared__ long long first[64];
+    const int64_t rows = (int64_t)P.ctr[kPbRows];
     if (threadIdx.x == 0) {
         long long a = 0;
         for (int p = 0; p < P.S; ++p) {
             pre[p] = a;
-            a += 2 * min((long long)P.ctr[kPbPerSeg + 4 * P.S + p], (long long)P.seg[p].need_cap);
+            // problem p's slots [need_off, need_off + cnt) as 16-byte chunks (24 B per node;
+            // need_off is even, so the range starts on a chunk)
+            const long long cnt = min((long long)pb_ctr(P, kFNeed, p), (long long)P.seg[p].need_cap);
+            first[p] = P.seg[p].need_off * 3 / 2;
+            a += (cnt * 3 + 1) / 2;
         }
         pre[P.S] = a;
     }
@@ -2252,7 +2389,7 @@ __global__ __launch_bounds__(256) void k_pb_emit(PlanBatchDev P, unsigned long l
             const int64_t r = c - c_slot - c_rows;
             int p = 0;
             while (p + 1 < P.S && pre[p + 1] <= r) ++p;
-            const int64_t at = 2 * P.seg[p].need_off + (r - pre[p]);
+            const int64_t at = first[p] + (r - pre[p]);
             h_need[at] = d_need[at];
         }
     }
@@ -2576,19 +2713,22 @@ epp::PlanBatchLayout epp::plan_batch_layout(int32_t S, int64_t ns, int32_t k, Pl
     while ((1ll << L.ns_log) < ns + 2) ++L.ns_log;
     L.NS = 1ll << L.ns_log;
     L.nbc = (int32_t)std::max<int64_t>(1, (ns + kCompactChunk - 1) / kCompactChunk);
-    // packed rows: the problems' capacities; referenced nodes: a row's node and its k
-    // neighbours per row, at most the problem's nodes
-    int64_t cap_total = 0, need = 0;
+    // rows: the problems' capacities; referenced nodes: a row's node and its k neighbours
+    // per row, at most the problem's nodes (even counts: 24-byte entries on 16-byte chunks)
+    int64_t rows = 0, need = 0;
     for (int p = 0; p < S; ++p) {
         segs[p].cap = std::max(0, segs[p].cap);
-        cap_total += segs[p].cap;
+        segs[p].row_off = rows;
+        rows += segs[p].cap;
         segs[p].need_off = need;
-        segs[p].need_cap = segs[p].cap > 0 ? (int32_t)std::min<int64_t>((int64_t)segs[p].cap * (k + 1) + 2, ns + 2) : 0;
+        segs[p].need_cap =
+            segs[p].cap > 0 ? (int32_t)((std::min<int64_t>((int64_t)segs[p].cap * (k + 1) + 2, ns + 2) + 1) & ~1ll) : 0;
         need += segs[p].need_cap;
     }
-    L.cap_total = (int32_t)cap_total;
+    L.cap_total = (int32_t)rows;
     L.need_cap = need;
-    L.nctr = kPbPerSeg + 5 * S;
+    L.nctr = kPbPerSeg + 6 * S;
+    const bool R = rows > 0;
     const KnnLayout kl = knn_layout((int)(ns + 2));
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -2602,34 +2742,34 @@ epp::PlanBatchLayout epp::plan_batch_layout(int32_t S, int64_t ns, int32_t k, Pl
     L.o_valid = take((size_t)S * ns);
     L.o_nodes = take((size_t)S * L.NS * 24);
     L.o_cstat = take((size_t)S * L.nbc * 8);
-    L.kws_stride = al(kl.bytes);
+    L.kws_stride = R ? al(kl.bytes) : 0;
     L.o_kws = take((size_t)S * L.kws_stride);
-    L.o_nbr = take((size_t)S * L.NS * k * 4);
-    L.o_retry = take((size_t)S * L.NS * 4);
-    const size_t capr = ((size_t)L.cap_total + 3) & ~size_t(3);
+    const size_t capr = ((size_t)rows + 3) & ~size_t(3);
+    L.o_query = take(capr * 4);
     L.o_ids32 = take(capr * 4);
     L.o_rows32 = take(capr * k * 4);
     L.o_rows16 = take(capr * k * 2);
     L.o_ev = take(capr * k);
-    L.o_mark = take((size_t)S * (L.NS >> 5) * 4);
-    L.o_map = take((size_t)S * L.NS * 4);
+    L.o_mark = take(R ? (size_t)S * L.NS : 0);
+    L.o_map = take(R ? (size_t)S * L.NS * 4 : 0);
+    L.o_nstat = take(R ? (size_t)S * (L.NS / kCompactChunk) * 8 : 0);
     L.o_slot = take(capr * 4);
-    L.o_need = take((size_t)L.need_cap * 32);
+    L.o_need = take((size_t)L.need_cap * 24 + 16);
     L.dev_bytes = o;
     o = 0;
     L.h_seg = take((size_t)S * sizeof(PlanSeg));
     L.h_hdr = take((size_t)L.nctr * 8);
     L.h_slot = take(capr * 4);
     L.h_rows = take(capr * k * 2);
-    L.h_need = take((size_t)L.need_cap * 32);
+    L.h_need = take((size_t)L.need_cap * 24 + 16);
     L.host_bytes = o;
     return L;
 }
 
 epp_status epp::plan_batch_launch(const epp_world* world, int32_t can_pass_gate, const double lo[3], const double hi[3],
                                   const PlanBatchLayout& L, void* dev, void* host, void* stream) {
-    if (!world || !dev || !host || L.S < 1 || L.ns < 1 || (L.k != 4 && L.k != 8 && L.k != 16) ||
-        L.S > 64 || ((int64_t)L.S << L.ns_log) >= (1ll << 31) || (reinterpret_cast<uintptr_t>(dev) & 255) ||
+    if (!world || !dev || !host || L.S < 1 || L.S > 64 || L.ns < 1 || (L.k != 4 && L.k != 8 && L.k != 16) ||
+        ((int64_t)L.S << L.ns_log) >= (1ll << 31) || (reinterpret_cast<uintptr_t>(dev) & 255) ||
         (reinterpret_cast<uintptr_t>(host) & 255)) {
         set_error("plan_batch_launch: invalid argument");
         return EPP_ERR_INVALID_ARGUMENT;
@@ -2648,7 +2788,6 @@ epp_status epp::plan_batch_launch(const epp_world* world, int32_t can_pass_gate,
     P.nctr = L.nctr;
     P.ns = L.ns;
     P.NS = L.NS;
-    P.need_cap = L.need_cap;
     for (int i = 0; i < 3; ++i) {
         P.lo[i] = lo[i];
         P.hi[i] = hi[i];
@@ -2669,49 +2808,48 @@ epp_status epp::plan_batch_launch(const epp_world* world, int32_t can_pass_gate,
     P.l_stat = kl.stat;
     P.l_cap = kl.cap;
     P.nclr = (int)((kl.start - kl.cnt) / sizeof(int));
-    P.scan_blocks = kl.scan_blocks;
-    P.nbr = reinterpret_cast<int32_t*>(d + L.o_nbr);
-    P.retry = reinterpret_cast<int32_t*>(d + L.o_retry);
+    P.query = reinterpret_cast<int32_t*>(d + L.o_query);
     P.ids32 = reinterpret_cast<int32_t*>(d + L.o_ids32);
     P.rows32 = reinterpret_cast<int32_t*>(d + L.o_rows32);
     P.rows16 = reinterpret_cast<uint16_t*>(d + L.o_rows16);
-    P.mark = reinterpret_cast<uint32_t*>(d + L.o_mark);
+    P.mark = reinterpret_cast<uint8_t*>(d + L.o_mark);
+    P.nstat = reinterpret_cast<unsigned long long*>(d + L.o_nstat);
     P.map = reinterpret_cast<int32_t*>(d + L.o_map);
     P.slot = reinterpret_cast<uint32_t*>(d + L.o_slot);
     P.need = reinterpret_cast<double*>(d + L.o_need);
     const unsigned S = (unsigned)L.S;
+    const bool R = L.cap_total > 0;
     // the problems up (pinned), then every stage on this stream
     if (hipMemcpyAsync(d + L.o_seg, h + L.h_seg, (size_t)L.S * sizeof(PlanSeg), hipMemcpyHostToDevice, s) != hipSuccess)
         return last("plan_batch_launch");
-    const int64_t clr = std::max<int64_t>({L.ns, L.NS >> 5, (int64_t)L.nbc, (int64_t)L.nctr});
+    const int64_t clr = std::max<int64_t>({L.ns, R ? L.NS >> 4 : 0, (int64_t)L.nbc, (int64_t)L.nctr});
     hipLaunchKernelGGL(k_pb_sample, dim3((unsigned)((clr + 255) / 256), S), dim3(256), 0, s, P);
     if (const epp_status st = epp_check_states(world, P.xyz, (int64_t)L.S * L.ns, can_pass_gate, P.valid, nullptr,
                                                nullptr, stream))
         return st;
     hipLaunchKernelGGL(k_pb_compact, dim3((unsigned)L.nbc, S), dim3(kCompactThreads), 0, s, P, next_scan_tag());
-    const unsigned gn = (unsigned)((L.ns + 2 + 255) / 256);
-    hipLaunchKernelGGL(k_pb_knn_prep, dim3(8, S), dim3(kBoundsThreads), 0, s, P);
-    hipLaunchKernelGGL(k_pb_knn_count, dim3(gn, S), dim3(256), 0, s, P);
-    hipLaunchKernelGGL(k_pb_knn_scan, dim3((unsigned)kl.scan_blocks, S), dim3(kScanThreads), 0, s, P, next_scan_tag());
-    hipLaunchKernelGGL(k_pb_knn_scatter, dim3(gn, S), dim3(256), 0, s, P);
-    char* hh = h + L.h_hdr;
-    if (L.cap_total > 0) {
-        hipLaunchKernelGGL(k_pb_list, dim3(gn, S), dim3(256), 0, s, P);
-        const dim3 gr((unsigned)std::max(1, cu_count_planner() * EPP_KNN_RETRY_PER_CU)), br(64);
-        if (L.k == 4) hipLaunchKernelGGL(k_pb_retry<4>, gr, br, 0, s, P);
-        else if (L.k == 8) hipLaunchKernelGGL(k_pb_retry<8>, gr, br, 0, s, P);
-        else hipLaunchKernelGGL(k_pb_retry<16>, gr, br, 0, s, P);
-        hipLaunchKernelGGL(k_pb_pack, dim3(gn, S), dim3(256), 0, s, P);
+    if (R) {
+        const unsigned gn = (unsigned)((L.ns + 2 + 255) / 256), gb = (unsigned)((L.ns + 2 + kPbBlock - 1) / kPbBlock);
+        hipLaunchKernelGGL(k_pb_member, dim3(gb, S), dim3(kPbBlock), 0, s, P);
+        hipLaunchKernelGGL(k_pb_knn_scan, dim3((unsigned)kl.scan_blocks, S), dim3(kScanThreads), 0, s, P, next_scan_tag());
+        hipLaunchKernelGGL(k_pb_knn_scatter, dim3(gn, S), dim3(256), 0, s, P);
+        // one wave per workgroup, 28 per CU (72 VGPRs: seven waves per SIMD)
+        const dim3 gr((unsigned)std::max(1, cu_count_planner() * 28)), br(64);
+        if (L.k == 4) hipLaunchKernelGGL(k_pb_rows<4>, gr, br, 0, s, P);
+        else if (L.k == 8) hipLaunchKernelGGL(k_pb_rows<8>, gr, br, 0, s, P);
+        else hipLaunchKernelGGL(k_pb_rows<16>, gr, br, 0, s, P);
         if (const epp_status st = check_knn_motions_rows(
-                world, P.nodes, P.rows32, P.ids32, reinterpret_cast<const int64_t*>(P.ctr + kPbPacked), L.cap_total,
+                world, P.nodes, P.rows32, P.ids32, reinterpret_cast<const int64_t*>(P.ctr + kPbRows), L.cap_total,
                 L.k, can_pass_gate, reinterpret_cast<uint8_t*>(d + L.o_ev), P.rows16, -1, nullptr, stream))
             return st;
         const int64_t ents = (int64_t)L.cap_total * L.k;
-        hipLaunchKernelGGL(k_pb_need, dim3((unsigned)((ents + 255) / 256)), dim3(256), 0, s, P);
+        hipLaunchKernelGGL(k_pb_mark, dim3((unsigned)((ents + kPbBlock - 1) / kPbBlock)), dim3(kPbBlock), 0, s, P);
+        hipLaunchKernelGGL(k_pb_number, dim3((unsigned)((L.ns + 2 + kCompactChunk - 1) / kCompactChunk), S),
+                           dim3(kCompactThreads), 0, s, P, next_scan_tag());
         hipLaunchKernelGGL(k_pb_remap, dim3((unsigned)((ents + 255) / 256)), dim3(256), 0, s, P);
     }
     hipLaunchKernelGGL(k_pb_emit, dim3((unsigned)std::max(1, cu_count_planner())), dim3(256), 0, s, P,
-                       reinterpret_cast<unsigned long long*>(hh), reinterpret_cast<uint4*>(h + L.h_slot),
+                       reinterpret_cast<unsigned long long*>(h + L.h_hdr), reinterpret_cast<uint4*>(h + L.h_slot),
                        reinterpret_cast<uint4*>(h + L.h_rows), reinterpret_cast<uint4*>(h + L.h_need));
     return last("plan_batch_launch");
 }

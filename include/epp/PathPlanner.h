@@ -36,6 +36,9 @@ struct PlannerStats {
     double ms = 0;         // wall time of the last planPath
     double ms_device = 0;  // of which: sampling, checks, k-NN, transfers (GPU phases)
     double ms_search = 0;  // of which: graph build + A* + shortcut on the host
+    // wall time of the batched planner's phases (summed over its attempts): the device
+    // stages up to the emitted results, the searches on the planner threads, the shortcut
+    double ms_batch = 0, ms_solve = 0, ms_shortcut = 0;
 };
 
 class PathPlanner {
@@ -94,7 +97,7 @@ private:
                      int64_t samples, std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const;
     void planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, const std::vector<uint64_t>& seeds,
                    int64_t samples, std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const;
-    bool wholeTableSearch(const double* d_nodes, int32_t n, const double box_lo[3], const double box_hi[3],
+    bool wholeTableSearch(const double* d_nodes, int32_t n, const double box_lo[3], const double box_hi[3], void* area,
                           std::vector<Vec3>& path, int64_t& edges_checked, int64_t& edges_valid, double& ms_dev,
                           double& ms_search) const;
 
