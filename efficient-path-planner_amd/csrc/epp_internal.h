@@ -155,13 +155,14 @@ struct PlanBatchLayout {
     // pinned host block: the problems (uploaded), then the emitted header, per row its
     // problem and node (p << 16 | compact index), the masked rows (compact indices, 0xFFFF:
     // no edge) and each problem's referenced nodes (x, y, z at need_off + compact index)
-    size_t h_seg = 0, h_hdr = 0, h_slot = 0, h_rows = 0, h_need = 0, host_bytes = 0;
+    size_t h_seg = 0, h_hdr = 0, h_slot = 0, h_rows = 0, h_need = 0, h_done = 0, host_bytes = 0;
+    int32_t done_n = 0;  // completion slots (u32 at h_done): the emit's workgroups publish the launch's seq
 };
 // segs: the problems with seed, ends, bound, gbound, the grid box and cell, cap filled;
 // row_off / need_off / need_cap are filled in here
 PlanBatchLayout plan_batch_layout(int32_t S, int64_t ns, int32_t k, PlanSeg* segs);
 epp_status plan_batch_launch(const epp_world* world, int32_t can_pass_gate, const double lo[3], const double hi[3],
-                             const PlanBatchLayout& L, void* dev, void* host, void* stream);
+                             const PlanBatchLayout& L, void* dev, void* host, uint32_t seq, void* stream);
 }  // namespace epp
 
 namespace epp {

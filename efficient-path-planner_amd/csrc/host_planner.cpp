@@ -19,6 +19,7 @@
 #include <utility>
 
 #include <hip/hip_runtime_api.h>
+#include <immintrin.h>
 
 #include "epp/PathPlanner.h"
 #include "epp/trajectory_generator.h"
@@ -155,11 +156,13 @@ public:
                 host_ = nullptr;
                 throw std::runtime_error("planner batch: hipHostMalloc failed");
             }
+            std::memset(host_, 0, host_bytes);  // (completion slots: no stale sequence numbers)
             hcap_ = host_bytes;
         }
     }
     void* dev() const { return dev_; }
     char* host() const { return static_cast<char*>(host_); }
+    uint32_t next_seq() { return ++seq_ ? seq_ : ++seq_; }  // (never 0: fresh slots read 0)
     // Buffers of the whole-table search of one problem per planner thread (w), sized here
     // for n nodes: allocated with the batch, not on the planner threads when a search falls
     // back (a first allocation of pinned memory there took milliseconds).
@@ -229,6 +232,7 @@ private:
     void* host_ = nullptr;
     void* stream_ = nullptr;
     size_t dcap_ = 0, hcap_ = 0;
+    uint32_t seq_ = 0;
 };
 
 // A*'s state per host thread, reused across searches: an entry counts only when its stamp
@@ -408,30 +412,13 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
     char* H = bs.host();
     std::memcpy(H + L.h_seg, segs.data(), sizeof(PlanSeg) * S);
     void* st = bs.stream();
-    check(plan_batch_launch(w, canPass ? 1 : 0, lo, hi, L, bs.dev(), H, st), "planner batch");
-    check(epp_stream_sync(st), "sync");
     const uint64_t* hdr = reinterpret_cast<const uint64_t*>(H + L.h_hdr);
     const uint32_t* slots = reinterpret_cast<const uint32_t*>(H + L.h_slot);
     const uint16_t* rows = reinterpret_cast<const uint16_t*>(H + L.h_rows);
     const double* need = reinterpret_cast<const double*>(H + L.h_need);
     auto hv = [&](int field, int p) { return (int64_t)hdr[kPbPerSeg + field * S + p]; };
-    std::vector<int64_t> first(S + 1, 0);  // rows are dense in problem order
-    for (int p = 0; p < S; ++p) first[p + 1] = first[p] + std::min<int64_t>(hv(0, p), segs[p].cap);
-    const double ms_batch = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_dev0).count();
+    std::vector<int64_t> first(S + 1, 0);  // rows are dense in problem order (set once the results are in)
     const char* dev = static_cast<const char*>(bs.dev());
-    // Cold areas (this thread's first plans): one whole-table search on problem 0's nodes,
-    // so that the fallback's first launches and transfers are paid here, in the cold first
-    // plan, rather than by the first search that falls back.
-    for (size_t w = 0; w < W; ++w) {
-        BatchScratch::Area& a = bs.area(w);
-        if (!a.cold) continue;
-        a.cold = false;
-        std::vector<Vec3> dummy;
-        int64_t e0 = 0, e1 = 0;
-        double m0 = 0, m1 = 0;
-        (void)wholeTableSearch(reinterpret_cast<const double*>(dev + L.o_nodes), (int32_t)hdr[kPbPerSeg + 3 * S],
-                               kbox[0].data(), kbox[0].data() + 3, &a, dummy, e0, e1, m0, m1);
-    }
 
     // ---- per problem: the restricted search, else the whole table ----------------------
     struct Out {
@@ -500,30 +487,81 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
             err[p] = std::current_exception();
         }
     };
-    // the W solvers pull problems in order
-    if (W <= 1) {
-        for (int p = 0; p < S; ++p) run(p, 0);
-    } else {
-        int devno = 0;
-        if (hipGetDevice(&devno) != hipSuccess) devno = 0;
-        std::atomic<int> next{0};
-        auto drain = [&](size_t w) {
-            for (int p = next++; p < S; p = next++) run(p, w);
-        };
-        std::mutex done_mu;
-        std::condition_variable done_cv;
-        size_t pending = W - 1;
-        for (size_t t = 1; t < W; ++t)
-            plan_pool().submit([&, devno, t] {
-                (void)hipSetDevice(devno);
-                drain(t);
-                std::lock_guard<std::mutex> lk(done_mu);
-                if (--pending == 0) done_cv.notify_all();
-            });
-        drain(0);
+    // The W - 1 planner threads are started before the launch and wait (spinning) for the
+    // results, so their wake-up overlaps the device stages; then the W solvers pull
+    // problems in order.  go: 1 results in, -1 no results (the launch failed).
+    std::atomic<int> go{0};
+    std::atomic<int> next{0};
+    auto drain = [&](size_t w) {
+        for (int p = next++; p < S; p = next++) run(p, w);
+    };
+    std::mutex done_mu;
+    std::condition_variable done_cv;
+    size_t pending = W - 1;
+    int devno = 0;
+    if (hipGetDevice(&devno) != hipSuccess) devno = 0;
+    for (size_t t = 1; t < W; ++t)
+        plan_pool().submit([&, devno, t] {
+            (void)hipSetDevice(devno);
+            int g;
+            while ((g = go.load(std::memory_order_acquire)) == 0) _mm_pause();
+            if (g > 0) drain(t);
+            std::lock_guard<std::mutex> lk(done_mu);
+            if (--pending == 0) done_cv.notify_all();
+        });
+    auto join = [&] {
         std::unique_lock<std::mutex> lk(done_mu);
         done_cv.wait(lk, [&] { return pending == 0; });
+    };
+    try {
+        const uint32_t seq = bs.next_seq();
+        check(plan_batch_launch(w, canPass ? 1 : 0, lo, hi, L, bs.dev(), H, seq, st), "planner batch");
+        // the emit's completion slots (polled: no stream synchronisation), the stream's
+        // state every ~1k polls (a failed launch ends the wait)
+        static const bool sync_wait = [] {  // (A/B knob: EPP_PB_SYNC=1 synchronises the stream instead)
+            const char* e = std::getenv("EPP_PB_SYNC");
+            return e && std::atoi(e) == 1;
+        }();
+        if (sync_wait) check(epp_stream_sync(st), "sync");
+        const uint32_t* done = reinterpret_cast<const uint32_t*>(H + L.h_done);
+        for (uint64_t spin = 0;; ++spin) {
+            int b = 0;
+            while (b < L.done_n && __atomic_load_n(done + b, __ATOMIC_ACQUIRE) == seq) ++b;
+            if (b == L.done_n) break;
+            if ((spin & 1023) == 1023) {
+                const hipError_t q = hipStreamQuery(static_cast<hipStream_t>(st));
+                if (q == hipErrorNotReady) continue;
+                if (q != hipSuccess) throw std::runtime_error(std::string("planner batch: ") + hipGetErrorString(q));
+                b = 0;
+                while (b < L.done_n && __atomic_load_n(done + b, __ATOMIC_ACQUIRE) == seq) ++b;
+                if (b != L.done_n) throw std::runtime_error("planner batch: completed without its completion slots");
+                break;
+            }
+            _mm_pause();
+        }
+        for (int p = 0; p < S; ++p) first[p + 1] = first[p] + std::min<int64_t>(hv(0, p), segs[p].cap);
+        // Cold areas (this thread's first plans): one whole-table search on problem 0's
+        // nodes, so that the fallback's first launches and transfers are paid here, in the
+        // cold first plan, rather than by the first search that falls back.
+        for (size_t a = 0; a < W; ++a) {
+            BatchScratch::Area& ar = bs.area(a);
+            if (!ar.cold) continue;
+            ar.cold = false;
+            std::vector<Vec3> dummy;
+            int64_t e0 = 0, e1 = 0;
+            double m0 = 0, m1 = 0;
+            (void)wholeTableSearch(reinterpret_cast<const double*>(dev + L.o_nodes), (int32_t)hdr[kPbPerSeg + 3 * S],
+                                   kbox[0].data(), kbox[0].data() + 3, &ar, dummy, e0, e1, m0, m1);
+        }
+    } catch (...) {
+        go.store(-1, std::memory_order_release);
+        join();
+        throw;
     }
+    const double ms_batch = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_dev0).count();
+    go.store(1, std::memory_order_release);
+    drain(0);
+    join();
     for (const auto& e : err)
         if (e) std::rethrow_exception(e);
     // ---- one batched shortcut for every path found (reduceVertices' role) ---------------

@@ -546,6 +546,15 @@ constexpr int kKnnTlBlocks = 65536;  // timeline records
 constexpr int kKnnRetryTl = 4096;    // retried queries recorded (k_knn_retry)
 __device__ unsigned long long g_knn_retry_tl[kKnnRetryTl][4];
 #endif
+// Device asserts of k_knn_tile's invariants in the diagnostics build (-DEPP_KNN_DIAG); the
+// product guards them instead (the query then takes the retry path)
+#ifdef EPP_KNN_DIAG
+#define EPP_KNN_ASSERT(c) assert(c)
+#else
+#define EPP_KNN_ASSERT(c) \
+    do {                 \
+    } while (0)
+#endif
 constexpr int kTileB = 4, kTileH = 2, kTileE = kTileB + 2 * kTileH, kTileCells = kTileE * kTileE * kTileE;
 constexpr int kTileW = 2 * kTileH + 1;  // cube edge around the query's cell
 constexpr int kTileRows = kTileW * kTileW;
@@ -891,6 +900,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
     const int nbx = (g.dims[0] + kTileB - 1) / kTileB, nby = (g.dims[1] + kTileB - 1) / kTileB,
               nbz = (g.dims[2] + kTileB - 1) / kTileB;
     const int nblocks = nbx * nby * nbz;
+    const int n_nodes = start[g.ncell];  // (the guards below: retry appends, sorted positions)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     constexpr int kPer = kTileCells / kTileThreads;  // halo cells per thread
     static_assert(kTileCells % kTileThreads == 0, "");
@@ -1016,6 +1026,8 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
             if (spill)
                 for (int q = nq + (int)threadIdx.x; q < nq_all; q += kTileThreads) {
                     const int at = atomicAdd(&gp->nretry, 1);
+                    EPP_KNN_ASSERT(at < n_nodes);
+                    if (at >= n_nodes) continue;
                     retry[at] = sidx[EPP_SPOS(qh[q])];
                     retry_b[at] = INFINITY;
                     atomicAdd(&gp->why[3], 1);
@@ -1123,6 +1135,8 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                 if (ok) {
                     double bd[K];
                     int bi[K];
+                    bool guard_ok = true;
+                    const int tot_halo = cst[kTileCells];
 #pragma unroll
                     for (int k = 0; k < K; ++k) {
                         bd[k] = r2max;
@@ -1148,8 +1162,18 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                             // (the halo's entries are its cells' contiguous runs of the cell-sorted
                             // copy: these gathers hit the few KB the block's queries share in L1,
                             // where the nodes' original order scattered them over the table)
-                            const int q = lst[e][tcol + col];
-                            const int sg = EPP_SPOS(q);
+                            // (guards: a listed LDS position inside the halo, its sorted position
+                            // inside the table -- what a wrong pass-1 cut or list could break; a
+                            // failed guard sends the query to the retry instead of reading out of
+                            // range; the diagnostics build asserts them)
+                            const int q0 = lst[e][tcol + col];
+                            const bool qok = q0 >= 0 && q0 < tot_halo;
+                            const int q = qok ? q0 : 0;
+                            const int sg0 = EPP_SPOS(q);
+                            const bool sok = sg0 >= 0 && sg0 < n_nodes;
+                            EPP_KNN_ASSERT(qok && sok);
+                            guard_ok = guard_ok && qok && sok;
+                            const int sg = sok ? sg0 : 0;
                             jj[u] = sidx[sg];
                             const double ddx = sxyz[3 * (int64_t)sg] - p[0], ddy = sxyz[3 * (int64_t)sg + 1] - p[1],
                                          ddz = sxyz[3 * (int64_t)sg + 2] - p[2];
@@ -1168,7 +1192,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                     // exact when the K-th distance is within the listed range and the cube
                     // suffices (stopping rule after shell kTileH)
                     const bool in_range = bd[K - 1] <= dcut;
-                    ok = in_range && knn_done<K>(g, c, p, kTileH, bd);
+                    ok = guard_ok && in_range && knn_done<K>(g, c, p, kTileH, bd);
 #ifdef EPP_KNN_DIAG
                     if (mode == 5 || mode == 6) ok = true;  // (ablation: no retries, no answer)
                     else
@@ -1182,8 +1206,11 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                 }
                 if (!ok) {
                     const int at = atomicAdd(&gp->nretry, 1);
-                    retry[at] = self;
-                    retry_b[at] = rbound;
+                    EPP_KNN_ASSERT(at < n_nodes);
+                    if (at < n_nodes) {  // (each node retries at most once: at < n)
+                        retry[at] = self;
+                        retry_b[at] = rbound;
+                    }
                 }
 #ifdef EPP_KNN_DIAG
                 if (tl[5] == 0ull) tl[5] = __builtin_amdgcn_s_memrealtime();
@@ -1202,6 +1229,8 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_knn_tile(KnnGrid* __restric
                 const int e = start[cell + 1];
                 for (int t = start[cell]; t < e; ++t) {
                     const int at = atomicAdd(&gp->nretry, 1);
+                    EPP_KNN_ASSERT(at < n_nodes);
+                    if (at >= n_nodes) continue;
                     retry[at] = sidx[t];
                     retry_b[at] = INFINITY;
                 }
@@ -1268,7 +1297,8 @@ __global__ __launch_bounds__(64) void k_knn_retry(const KnnGrid* __restrict__ gp
                                                    int32_t* __restrict__ nbr) {
     const KnnGrid g = *gp;
     const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwaves = (gridDim.x * blockDim.x) >> 6;
-    for (int i = wave; i < g.nretry; i += nwaves) {  // wave-uniform
+    const int nq = min(g.nretry, start[g.ncell]);  // (the list holds at most one entry per node)
+    for (int i = wave; i < nq; i += nwaves) {  // wave-uniform
 #ifdef EPP_KNN_DIAG
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -2227,16 +2257,28 @@ __global__ __launch_bounds__(64) void k_pb_rows(PlanBatchDev P) {
     }
     const int D = __shfl(incl, 63, 64);
     if (wave == 0 && lane == 0) P.ctr[kPbRows] = (unsigned long long)D;
-    for (int d = wave; d < D; d += nwaves) {  // wave-uniform
-        const int p = __popcll(__ballot(lane < P.S && incl <= d));  // problems whose rows end at or before d
+    // The query's node and coordinates are loaded one query ahead (wave-uniform loads in
+    // flight while the current query runs: two dependent round trips off every query).
+    auto locate = [&](int d, int& p, int& self, double (&pt)[3]) {
+        p = __popcll(__ballot(lane < P.S && incl <= d));  // problems whose rows end at or before d
         const int first = __builtin_amdgcn_readfirstlane(__shfl(incl - mine, p, 64));
+        self = __builtin_amdgcn_readfirstlane(P.query[P.seg[p].row_off + (d - first)]);
+        const double* x = P.nodes + (((int64_t)p << P.ns_log) + self) * 3;
+        pt[0] = x[0];
+        pt[1] = x[1];
+        pt[2] = x[2];
+    };
+    int p_n = 0, self_n = 0;
+    double pt_n[3] = {0.0, 0.0, 0.0};
+    if (wave < D) locate(wave, p_n, self_n, pt_n);
+    for (int d = wave; d < D; d += nwaves) {  // wave-uniform
+        const int p = p_n, self = self_n;
+        const double pt[3] = {pt_n[0], pt_n[1], pt_n[2]};
+        if (d + nwaves < D) locate(d + nwaves, p_n, self_n, pt_n);
         const PlanSeg& q = P.seg[p];
-        const int self = __builtin_amdgcn_readfirstlane(P.query[q.row_off + (d - first)]);
         const int64_t off = (int64_t)p << P.ns_log;
         const KnnSeg ks = knn_seg(P, p);
         const KnnGrid g = *ks.g;
-        const double* x = P.nodes + (off + self) * 3;
-        const double pt[3] = {x[0], x[1], x[2]};
         const double f = pb_ellipse(q, pt);
         if (lane == 0) P.ids32[d] = (int32_t)(off + self);
         if (!pb_query_row<K>(g, ks.sxyz, ks.sidx, ks.start, pt, f, q.gbound, self, P.rows32 + (int64_t)d * K, off)) {
@@ -2355,9 +2397,13 @@ __global__ __launch_bounds__(256) void k_pb_remap(PlanBatchDev P) {
 // The results into pinned host memory, only the bytes in use: the header (counters), the
 // rows' problem and node (u32), the masked rows (u16), every problem's referenced nodes
 // (24 B each, at its own offset).  16-byte stores (the device parts are 16-byte padded).
+// Each workgroup then publishes `seq` in its completion slot (host memory, system scope,
+// after a system fence over its stores): the host polls the slots instead of synchronising
+// the stream.
 __global__ __launch_bounds__(256) void k_pb_emit(PlanBatchDev P, unsigned long long* __restrict__ hdr,
                                                   uint4* __restrict__ h_slot, uint4* __restrict__ h_rows,
-                                                  uint4* __restrict__ h_need) {
+                                                  uint4* __restrict__ h_need, uint32_t* __restrict__ done,
+                                                  uint32_t seq) {
     __shared__ long long pre[65];  // 16-byte chunks of the referenced nodes before problem p (S <= 64)
     __shared__ long long first[64];
     const int64_t rows = (int64_t)P.ctr[kPbRows];
@@ -2393,7 +2439,12 @@ __global__ __launch_bounds__(256) void k_pb_emit(PlanBatchDev P, unsigned long l
             h_need[at] = d_need[at];
         }
     }
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(done + blockIdx.x, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+
+constexpr int kPbEmitMax = 1024;  // emit workgroups (one completion slot each)
 
 int cu_count_planner() {
     int dev = 0, cus = 256;
@@ -2762,12 +2813,21 @@ epp::PlanBatchLayout epp::plan_batch_layout(int32_t S, int64_t ns, int32_t k, Pl
     L.h_slot = take(capr * 4);
     L.h_rows = take(capr * k * 2);
     L.h_need = take((size_t)L.need_cap * 24 + 16);
+    {  // emit workgroups: each one's system fence writes back its XCD's L2, so few of them
+        static const int eb = [] {
+            const char* e = std::getenv("EPP_PB_EMIT_BLOCKS");  // (A/B knob: same results)
+            const int v = e && *e ? std::atoi(e) : 32;
+            return std::max(1, std::min(kPbEmitMax, v));
+        }();
+        L.done_n = eb;
+    }
+    L.h_done = take((size_t)L.done_n * 4);
     L.host_bytes = o;
     return L;
 }
 
 epp_status epp::plan_batch_launch(const epp_world* world, int32_t can_pass_gate, const double lo[3], const double hi[3],
-                                  const PlanBatchLayout& L, void* dev, void* host, void* stream) {
+                                  const PlanBatchLayout& L, void* dev, void* host, uint32_t seq, void* stream) {
     if (!world || !dev || !host || L.S < 1 || L.S > 64 || L.ns < 1 || (L.k != 4 && L.k != 8 && L.k != 16) ||
         ((int64_t)L.S << L.ns_log) >= (1ll << 31) || (reinterpret_cast<uintptr_t>(dev) & 255) ||
         (reinterpret_cast<uintptr_t>(host) & 255)) {
@@ -2848,8 +2908,9 @@ epp_status epp::plan_batch_launch(const epp_world* world, int32_t can_pass_gate,
                            dim3(kCompactThreads), 0, s, P, next_scan_tag());
         hipLaunchKernelGGL(k_pb_remap, dim3((unsigned)((ents + 255) / 256)), dim3(256), 0, s, P);
     }
-    hipLaunchKernelGGL(k_pb_emit, dim3((unsigned)std::max(1, cu_count_planner())), dim3(256), 0, s, P,
+    hipLaunchKernelGGL(k_pb_emit, dim3((unsigned)L.done_n), dim3(256), 0, s, P,
                        reinterpret_cast<unsigned long long*>(h + L.h_hdr), reinterpret_cast<uint4*>(h + L.h_slot),
-                       reinterpret_cast<uint4*>(h + L.h_rows), reinterpret_cast<uint4*>(h + L.h_need));
+                       reinterpret_cast<uint4*>(h + L.h_rows), reinterpret_cast<uint4*>(h + L.h_need),
+                       reinterpret_cast<uint32_t*>(h + L.h_done), seq);
     return last("plan_batch_launch");
 }
