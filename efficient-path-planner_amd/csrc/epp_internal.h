@@ -105,6 +105,11 @@ epp_status pack_ellipse_rows(const double* nodes, const int32_t* tab, int32_t n,
                              int32_t* rows32, int64_t* count, void* stream);
 // epp_knn_ws_box (max_dist 0) whose rows are exact for every node of that ellipsoid (the
 // grid as usual, then those nodes' rows alone, one wave each; other rows: unspecified).
+// The reverse edges of the masked k-NN table nbr (n x k, -1: none) as a CSR: roff (n + 1)
+// and radj (the sources of every node's in-edges, ascending; radj16, if given, the same as
+// u16); cnt / fill: n-int workspaces.  (PathPlanner's symmetrised search.)
+epp_status reverse_csr(const int32_t* nbr, int32_t n, int32_t k, int32_t* cnt, int32_t* fill, int32_t* roff,
+                       int32_t* radj, uint16_t* radj16, void* stream);
 epp_status knn_ws_box_ellipse(const double* nodes, int32_t n, int32_t k, const double lo[3], const double hi[3],
                               const double s[3], const double g[3], double bound, int32_t* nbr, void* ws,
                               uint64_t ws_bytes, void* stream);

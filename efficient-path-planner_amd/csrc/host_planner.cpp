@@ -174,11 +174,18 @@ public:
         bool cold = true;  // no whole-table search has run on it yet
     };
     static size_t r256(size_t b) { return (b + 255) & ~size_t(255); }
+    // device: [edge counts | table (i32) | table (u16) | motion flags | k-NN workspace | the
+    // reverse CSR: counts, fill, roff (n + 1), radj (i32), radj (u16)]; pinned: [edge counts
+    // | nodes | table | roff | radj]
     static size_t area_dev_bytes(int64_t n, int k) {
         const size_t m = (size_t)n * k;
-        return r256(16) + r256(m * 4) + r256(m * 2) + r256(m) + r256((size_t)epp_knn_workspace_size((int32_t)n));
+        return r256(16) + r256(m * 4) + r256(m * 2) + r256(m) + r256((size_t)epp_knn_workspace_size((int32_t)n)) +
+               3 * r256((size_t)(n + 1) * 4) + r256(m * 4) + r256(m * 2);
     }
-    static size_t area_pin_bytes(int64_t n, int k) { return r256(64) + r256((size_t)n * 24) + r256((size_t)n * k * 4); }
+    static size_t area_pin_bytes(int64_t n, int k) {
+        return r256(64) + r256((size_t)n * 24) + r256((size_t)n * k * 4) + r256((size_t)(n + 1) * 4) +
+               r256((size_t)n * k * 4);
+    }
     void ensure_areas(size_t W, int64_t n, int k) {
         if (areas_.size() < W) areas_.resize(W);
         const size_t db = area_dev_bytes(n, k), pb = area_pin_bytes(n, k);
@@ -680,28 +687,53 @@ bool PathPlanner::wholeTableSearch(const double* d_nodes, int32_t n, const doubl
                 }
             return true;
         });
-    if (r != 1) {  // the symmetrised graph: reverse edges as a CSR
-        std::vector<int32_t> roff(n + 1, 0), radj;
-        for (size_t e = 0; e < m; ++e)
-            if (nbr(e) >= 0) ++roff[nbr(e) + 1];
-        for (int i = 0; i < n; ++i) roff[i + 1] += roff[i];
-        radj.resize(roff[n]);
-        std::vector<int32_t> fill(roff.begin(), roff.end() - 1);
-        for (int i = 0; i < n; ++i)
-            for (int c = 0; c < k; ++c) {
-                const size_t e = (size_t)i * k + c;
-                if (nbr(e) >= 0) radj[fill[nbr(e)]++] = i;
-            }
+    static const bool trace = [] {  // (diagnostics: the fallback's phases on stderr)
+        const char* e = std::getenv("EPP_PLAN_TRACE");
+        return e && std::atoi(e) == 1;
+    }();
+    const auto t_fwd = std::chrono::steady_clock::now();
+    if (r != 1) {  // the symmetrised graph: the reverse edges as a CSR, built on the device
+        // (counting sort of the masked table; every node's sources ascending, the order of a
+        // host build scanning the rows in node order) and downloaded with one synchronisation
+        char* rp = reinterpret_cast<char*>(d_ws) + BatchScratch::r256((size_t)epp_knn_workspace_size(n));
+        int32_t* d_cnt = reinterpret_cast<int32_t*>(rp);
+        int32_t* d_fill = reinterpret_cast<int32_t*>(rp + BatchScratch::r256((size_t)(n + 1) * 4));
+        int32_t* d_roff = reinterpret_cast<int32_t*>(rp + 2 * BatchScratch::r256((size_t)(n + 1) * 4));
+        int32_t* d_radj = reinterpret_cast<int32_t*>(rp + 3 * BatchScratch::r256((size_t)(n + 1) * 4));
+        uint16_t* d_radj16 = narrow ? reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(d_radj) + BatchScratch::r256(m * 4))
+                                    : nullptr;
+        check(reverse_csr(d_nbr, n, k, d_cnt, d_fill, d_roff, d_radj, d_radj16, st), "reverse edges");
+        int32_t* roff = reinterpret_cast<int32_t*>(static_cast<char*>(h_tab) + BatchScratch::r256(m * 4));
+        void* h_radj = reinterpret_cast<char*>(roff) + BatchScratch::r256((size_t)(n + 1) * 4);
+        check(epp_memcpy_d2h_async(roff, d_roff, (uint64_t)(n + 1) * 4, st), "download");
+        check(epp_stream_sync(st), "sync");
+        const int64_t ne = roff[n];
+        if (narrow) check(epp_memcpy_d2h_async(h_radj, d_radj16, (uint64_t)ne * 2, st), "download");
+        else check(epp_memcpy_d2h_async(h_radj, d_radj, (uint64_t)ne * 4, st), "download");
+        check(epp_stream_sync(st), "sync");
+        const uint16_t* radj16 = static_cast<const uint16_t*>(h_radj);
+        const int32_t* radj32 = static_cast<const int32_t*>(h_radj);
+        auto radj = [&](int64_t q) -> int { return narrow ? (int)radj16[q] : radj32[q]; };
+        const auto t_csr = std::chrono::steady_clock::now();
+        int64_t pops = 0;
         r = astar(ss, (size_t)n, pos, key, [&](int u, double, auto&& relax, bool closing) {
+            pops += closing ? 1 : 0;
             if (closing) {
                 for (int c = 0; c < k; ++c) {
                     const int v = nbr((size_t)u * k + c);
                     if (v >= 0) relax(v);
                 }
-                for (int32_t q = roff[u]; q < roff[u + 1]; ++q) relax(radj[q]);
+                for (int32_t q = roff[u]; q < roff[u + 1]; ++q) relax(radj(q));
             }
             return true;
         });
+        if (trace) {
+            auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            std::cerr << "[plan trace] whole table n " << n << " forward edge into goal " << goal_has_forward_edge
+                      << ": device " << ms(t0, t1) << " ms, forward A* " << ms(t1, t_fwd) << " ms, reverse CSR "
+                      << ms(t_fwd, t_csr) << " ms, symmetrised A* " << ms(t_csr, std::chrono::steady_clock::now())
+                      << " ms (" << pops << " closed), found " << (r == 1) << std::endl;
+        }
     }
     path.clear();
     if (r == 1) {

@@ -2446,6 +2446,77 @@ __global__ __launch_bounds__(256) void k_pb_emit(PlanBatchDev P, unsigned long l
 
 constexpr int kPbEmitMax = 1024;  // emit workgroups (one completion slot each)
 
+// ---- the reverse edges of a k-NN table as a CSR (the planner's symmetrised search) -----
+// roff[v] .. roff[v + 1]: the nodes u whose (masked) row holds v, ascending -- the order
+// the host's own build gives them (rows scanned in node order), so A* relaxes them in the
+// same order.  Counting sort: in-degrees by atomics, one workgroup's scan, a scatter by
+// atomics, then every node's run sorted (insertion sort: ~k entries).
+__global__ __launch_bounds__(256) void k_rev_count(const int32_t* __restrict__ nbr, int64_t m, int32_t* __restrict__ cnt) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e < m && nbr[e] >= 0) atomicAdd(&cnt[nbr[e]], 1);
+}
+__global__ __launch_bounds__(1024) void k_rev_scan(const int32_t* __restrict__ cnt, int32_t n, int32_t* __restrict__ roff,
+                                                   int32_t* __restrict__ fill) {
+    __shared__ int wsum[16];
+    __shared__ int s_carry;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_carry = 0;
+    for (int c0 = 0; c0 < n; c0 += 1024 * 16) {  // chunks of 16 counts per thread
+        const int b0 = c0 + (int)threadIdx.x * 16;
+        int v[16], sum = 0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            v[u] = b0 + u < n ? cnt[b0 + u] : 0;
+            sum += v[u];
+        }
+        int incl = sum;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += t;
+        }
+        __syncthreads();
+        if (lane == 63) wsum[wv] = incl;
+        __syncthreads();
+        int acc = s_carry + incl - sum;
+        for (int w = 0; w < wv; ++w) acc += wsum[w];
+        __syncthreads();
+        if (threadIdx.x == 1023) s_carry = acc + sum;
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+            if (b0 + u < n) {
+                roff[b0 + u] = acc;
+                fill[b0 + u] = acc;
+                acc += v[u];
+            }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) roff[n] = s_carry;
+}
+__global__ __launch_bounds__(256) void k_rev_fill(const int32_t* __restrict__ nbr, int64_t m, int32_t k,
+                                                  int32_t* __restrict__ fill, int32_t* __restrict__ radj) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= m) return;
+    const int32_t v = nbr[e];
+    if (v >= 0) radj[atomicAdd(&fill[v], 1)] = (int32_t)(e / k);
+}
+__global__ __launch_bounds__(256) void k_rev_sort(const int32_t* __restrict__ roff, int32_t n, int32_t* __restrict__ radj,
+                                                  uint16_t* __restrict__ radj16) {
+    const int v = blockIdx.x * 256 + threadIdx.x;
+    if (v >= n) return;
+    const int a = roff[v], b = roff[v + 1];
+    for (int i = a + 1; i < b; ++i) {  // (insertion sort of the node's run)
+        const int32_t x = radj[i];
+        int j = i - 1;
+        while (j >= a && radj[j] > x) {
+            radj[j + 1] = radj[j];
+            --j;
+        }
+        radj[j + 1] = x;
+    }
+    if (radj16)
+        for (int i = a; i < b; ++i) radj16[i] = (uint16_t)radj[i];
+}
+
 int cu_count_planner() {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -2913,4 +2984,20 @@ epp_status epp::plan_batch_launch(const epp_world* world, int32_t can_pass_gate,
                        reinterpret_cast<uint4*>(h + L.h_rows), reinterpret_cast<uint4*>(h + L.h_need),
                        reinterpret_cast<uint32_t*>(h + L.h_done), seq);
     return last("plan_batch_launch");
+}
+
+epp_status epp::reverse_csr(const int32_t* nbr, int32_t n, int32_t k, int32_t* cnt, int32_t* fill, int32_t* roff,
+                            int32_t* radj, uint16_t* radj16, void* stream) {
+    if (n <= 0 || k <= 0 || !nbr || !cnt || !fill || !roff || !radj) {
+        set_error("reverse_csr: invalid argument");
+        return EPP_ERR_INVALID_ARGUMENT;
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t m = (int64_t)n * k;
+    if (hipMemsetAsync(cnt, 0, (size_t)n * 4, s) != hipSuccess) return last("reverse_csr");
+    hipLaunchKernelGGL(k_rev_count, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, nbr, m, cnt);
+    hipLaunchKernelGGL(k_rev_scan, dim3(1), dim3(1024), 0, s, cnt, n, roff, fill);
+    hipLaunchKernelGGL(k_rev_fill, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, nbr, m, k, fill, radj);
+    hipLaunchKernelGGL(k_rev_sort, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, roff, n, radj, radj16);
+    return last("reverse_csr");
 }
