@@ -349,11 +349,13 @@ def full_plan(dist, rank, reps):
         state["first"] = {"wp": np.array(otg.get_waypoints()), "traj": np.array(otg.get_planned_traj())}
 
     def timed():
-        per = []
+        per, stats = [], []
         for _ in range(reps):
             t = time.perf_counter()
             state["otg"].pre_compute_traj(0.0)
             per.append((time.perf_counter() - t) * 1e3)
+            stats.append(state["otg"].planner_stats())
+        state["stats"] = stats
         # one gate-to-gate segment alone, with the planner's device / host split: a fresh
         # PathPlanner's first plan (cold: its construction included) and its second (warm)
         all_cps = state["otg"].get_checkpoints()
@@ -373,6 +375,15 @@ def full_plan(dist, rank, reps):
     ms = float(np.mean(per))
     ms_max = dist.max(ms)
     per_rank = dist.gather(ms)  # every rank's own mean (the headline takes the slowest)
+    st = state.get("stats", [])
+    # the batched planner's phases per call (rank 0's): device stages up to the emitted
+    # rows, the searches, the shortcut; the rest of pre_compute_traj (includeGates2, the
+    # min-snap refit and sampling, the path dump)
+    phases = {k: float(np.median([x[k] for x in st])) for k in ("ms_batch", "ms_solve", "ms_shortcut")} if st else None
+    if phases:
+        phases["ms_outside_planner"] = float(np.median([t - x["ms"] for t, x in zip(per, st)]))
+        phases["fallbacks_per_call"] = float(np.mean([x["fallbacks"] for x in st]))
+        phases["restricted_rows_per_call"] = float(np.median([x["restricted_rows"] for x in st]))
     otg = state["otg"]
     wp = np.ascontiguousarray(otg.get_waypoints())
     traj = otg.get_planned_traj()
@@ -399,7 +410,8 @@ def full_plan(dist, rank, reps):
             comm.close()
     return {"_first": state["first"],
             "ms_per_track": ms_max, "ms_per_track_p50": dist.max(float(np.median(per))), "tracks": dist.ws,
-            "ms_per_track_per_rank": per_rank, "comm_n_ranks": comm_ranks,
+            "ms_per_track_per_rank": per_rank, "comm_n_ranks": comm_ranks, "ms_per_call": per,
+            "planner_phases_p50": phases,
             "collective_timeout_s": getattr(comm, "collective_timeout_s", None),
             "samples_per_segment": PLAN_SAMPLES, "k": 16,
             "segments_per_track": 9, "reps": reps, "waypoints_per_track": [len(x) for x in sets],

@@ -19,7 +19,7 @@ root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 prof = os.path.join(root, "profiles")
 os.makedirs(prof, exist_ok=True)
 
-for sub, suffix in (("prof", "kernel_stats"), ("prof_full", "kernel_stats_full")):
+for sub, suffix in (("prof", "kernel_stats"), ("prof_full", "kernel_stats_full"), ("prof_plan", "kernel_stats_planner")):
     stats = glob.glob(os.path.join(out_dir, sub, "**", "*kernel_stats.csv"), recursive=True)
     if stats:
         shutil.copy(stats[0], os.path.join(prof, f"{tag}_{suffix}.csv"))
