@@ -160,6 +160,9 @@ def run(args, ws, rank, local, out_stream):
     # host launch path costs (an ~8 us kernel is about one host-side launch; under
     # rocprofv3's kernel trace a host loop runs at ~11 us per launch).
     graph = None
+    ev0, ev1 = C.c_void_p(), C.c_void_p()
+    for ev in (ev0, ev1):
+        capi.check(L.epp_event_create(C.byref(ev)))
     if not args.host_loop:
         g = C.c_void_p()
         try:
@@ -187,9 +190,6 @@ def run(args, ws, rank, local, out_stream):
 
     dist.barrier()
     capi.check(L.epp_stream_sync(stream))
-    ev0, ev1 = C.c_void_p(), C.c_void_p()
-    capi.check(L.epp_event_create(C.byref(ev0)))
-    capi.check(L.epp_event_create(C.byref(ev1)))
     t0 = time.perf_counter()
     capi.check(L.epp_event_record(ev0, stream))
     run_steps()
@@ -201,12 +201,15 @@ def run(args, ws, rank, local, out_stream):
     value = ws * N_STATES * args.steps / elapsed
 
     # dominant kernel's average launch time: HIP events on the launch stream bracketing
-    # the timed region's K back-to-back launches (the only kernel in it)
+    # the timed region's K back-to-back launches (the only kernel in it).  The bracket
+    # also holds the graph's launch latency (~0.5 us per kernel at K = 20); HIP gives no
+    # time for event records captured inside a graph (hipEventElapsedTime: invalid
+    # resource handle), so the kernels cannot be bracketed alone.
     evms = C.c_float()
     capi.check(L.epp_event_elapsed_ms(ev0, ev1, C.byref(evms)))
-    L.epp_event_destroy(ev0)
-    L.epp_event_destroy(ev1)
     kms = evms.value / args.steps
+    for ev in (ev0, ev1):
+        L.epp_event_destroy(ev)
     if graph is not None:
         capi.check(L.epp_graph_destroy(graph))
     achieved = BYTES_PER_STATE * N_STATES / (kms * 1e-3) / 1e9

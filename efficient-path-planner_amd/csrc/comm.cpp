@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -100,7 +101,25 @@ struct epp_comm {
 
 using namespace epp;
 
+#ifdef EPP_TEST_HOOKS
+namespace epp {
+hipError_t test_stall(hipStream_t stream, double ms);  // csrc/test_stall.hip
+}
+#endif
+
 namespace {
+
+// EPP_TEST_COMM_STALL_MS (test builds only, -DEPP_TEST_HOOKS: testhooks/): a bounded
+// stall queued on the communicator's stream just before each collective, so the
+// collective is still in flight when the deadline passes or an abort is requested
+// (tests/comm_stall_case.py).  The product build has no such hook.
+hipError_t stall_hook(hipStream_t stream) {
+#ifdef EPP_TEST_HOOKS
+    if (const char* s = std::getenv("EPP_TEST_COMM_STALL_MS")) return test_stall(stream, std::atof(s));
+#endif
+    (void)stream;
+    return hipSuccess;
+}
 
 // Binds the communicator's device and stream for one call (restores the caller's device).
 struct CommScope {
@@ -319,6 +338,7 @@ epp_status epp_comm_allgather_waypoints(epp_comm* c, const double* wp, int32_t n
     if (he == hipSuccess) he = comm_grow(c, cnt_b);
     // 1. the counts (-1: that rank failed before it had a set; every rank then stops here)
     if (he == hipSuccess) he = hipMemcpyAsync(c->d_buf, &n, 4, hipMemcpyHostToDevice, c->stream);
+    if (he == hipSuccess) he = stall_hook(c->stream);
     if (he != hipSuccess) return hip_fail("epp_comm_allgather_waypoints", he);
     ncclResult_t e = r->allGather(c->d_buf, c->d_buf + 4, 1, ncclInt32, c->comm, c->stream);
     if (e != ncclSuccess) return nccl_error(r, e, "ncclAllGather (counts)");
@@ -351,6 +371,7 @@ epp_status epp_comm_allgather_waypoints(epp_comm* c, const double* wp, int32_t n
     char* d_recv = d_send + set_b;
     if (he == hipSuccess) he = hipMemsetAsync(d_send, 0, set_b, c->stream);
     if (he == hipSuccess && n > 0) he = hipMemcpyAsync(d_send, wp, (size_t)n * 24, hipMemcpyHostToDevice, c->stream);
+    if (he == hipSuccess) he = stall_hook(c->stream);
     if (he != hipSuccess) return hip_fail("epp_comm_allgather_waypoints", he);
     e = r->allGather(d_send, d_recv, (size_t)maxw * 3, ncclFloat64, c->comm, c->stream);
     if (e != ncclSuccess) return nccl_error(r, e, "ncclAllGather (waypoints)");
@@ -375,6 +396,7 @@ epp_status epp_comm_allreduce_f64(epp_comm* c, double* x, int32_t n, int32_t op)
     const size_t bytes = ((size_t)n * 8 + 255) & ~size_t(255);
     if (he == hipSuccess) he = comm_grow(c, bytes);
     if (he == hipSuccess) he = hipMemcpyAsync(c->d_buf, x, (size_t)n * 8, hipMemcpyHostToDevice, c->stream);
+    if (he == hipSuccess) he = stall_hook(c->stream);
     if (he != hipSuccess) return hip_fail("epp_comm_allreduce_f64", he);
     const ncclRedOp_t rop = op == EPP_REDUCE_SUM ? ncclSum : op == EPP_REDUCE_MAX ? ncclMax : ncclMin;
     const ncclResult_t e = r->allReduce(c->d_buf, c->d_buf, (size_t)n, ncclFloat64, rop, c->comm, c->stream);

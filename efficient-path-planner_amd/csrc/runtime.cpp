@@ -19,6 +19,7 @@ void set_error(const std::string& msg) { g_last_error = msg; }
         hipError_t e_ = (call);                                                      \
         if (e_ != hipSuccess) {                                                      \
             epp::set_error(std::string(#call) + ": " + hipGetErrorString(e_));       \
+            (void)hipGetLastError(); /* reported here: not again at the next launch */ \
             return EPP_ERR_HIP;                                                      \
         }                                                                            \
     } while (0)
