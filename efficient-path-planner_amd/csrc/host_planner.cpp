@@ -940,8 +940,7 @@ std::vector<Vec3> PathPlanner::includeGates2(std::vector<std::vector<Vec3>> wayp
     } else if (method == "custom") {
         pruned = pruneAll(waypoints);
     } else if (method == "ompl") {
-        // smoothBSpline (OMPL) is not part of this build; the shortcut keeps the path valid
-        pruned = shortcutAll(waypoints);
+        pruned = smoothAll(waypoints);
     } else {
         std::cerr << "Unknown pruning method" << std::endl;
         throw std::runtime_error("Unknown pruning method");
@@ -953,6 +952,94 @@ std::vector<Vec3> PathPlanner::includeGates2(std::vector<std::vector<Vec3>> wayp
             flat.push_back(w);
         }
     return flat;
+}
+
+// PathPlanner::omplPrunePathAndInterpolate — src/PathPlanner.cpp:282-313: OMPL's
+// PathSimplifier::smoothBSpline(path) with its defaults (maxSteps = 5, minChange = double
+// epsilon), as OMPL 1.6 publishes it (PathSimplifier.cpp, PathGeometric::subdivide,
+// RealVectorStateSpace::interpolate / distance).  Per step every live path is subdivided
+// (a midpoint between every two states); then each even state i (2 <= i < n - 1) moves to
+// the midpoint of the midpoints (i-1, i) and (i, i+1) when state i-1 is valid, both
+// motions (i-1 -> new, new -> i+1) are valid and the move exceeds minChange.  The moves of
+// one step touch only even states and read only odd ones, so they are independent: the
+// step's state checks (all paths) are one batch, its motion checks another, on the
+// planner's validators (src/PathPlanner.cpp:47-50: can_pass_gate from the config).  A path
+// whose step moves nothing stops (OMPL's break); paths of < 3 states are returned as they
+// are.
+std::vector<std::vector<Vec3>> PathPlanner::smoothAll(const std::vector<std::vector<Vec3>>& segs) const {
+    const bool canPass = configParser->getPathPlannerProperties().canPassGate;
+    constexpr int kMaxSteps = 5;
+    const double minChange = std::numeric_limits<double>::epsilon();
+    auto half = [](const Vec3& a, const Vec3& b) {  // interpolate(a, b, 0.5): a + (b - a) * t
+        return Vec3(a.x + (b.x - a.x) * 0.5, a.y + (b.y - a.y) * 0.5, a.z + (b.z - a.z) * 0.5);
+    };
+    auto distance = [](const Vec3& a, const Vec3& b) {  // left-to-right sum of squares
+        double t = 0.0;
+        for (int d = 0; d < 3; ++d) {
+            const double diff = a[d] - b[d];
+            t += diff * diff;
+        }
+        return std::sqrt(t);
+    };
+    std::vector<std::vector<Vec3>> st = segs;
+    std::vector<char> live(st.size());
+    for (size_t q = 0; q < st.size(); ++q) live[q] = st[q].size() >= 3;
+    std::vector<double> pts, r1, r2;
+    std::vector<Vec3> cand;
+    std::vector<std::pair<uint32_t, uint32_t>> at;  // (path, state i) of each candidate move
+    std::vector<uint8_t> okp, okr;
+    for (int step = 0; step < kMaxSteps; ++step) {
+        pts.clear();
+        r1.clear();
+        r2.clear();
+        cand.clear();
+        at.clear();
+        for (size_t q = 0; q < st.size(); ++q) {
+            if (!live[q]) continue;
+            std::vector<Vec3>& s = st[q];
+            std::vector<Vec3> sub;  // PathGeometric::subdivide
+            sub.reserve(2 * s.size() - 1);
+            sub.push_back(s[0]);
+            for (size_t i = 1; i < s.size(); ++i) {
+                const Vec3 m = half(sub.back(), s[i]);
+                sub.push_back(m);
+                sub.push_back(s[i]);
+            }
+            s.swap(sub);
+            for (size_t i = 2; i + 1 < s.size(); i += 2) {
+                Vec3 t1 = half(s[i - 1], s[i]);
+                const Vec3 t2 = half(s[i], s[i + 1]);
+                t1 = half(t1, t2);
+                pts.insert(pts.end(), {s[i - 1].x, s[i - 1].y, s[i - 1].z});
+                r1.insert(r1.end(), {s[i - 1].x, s[i - 1].y, s[i - 1].z, t1.x, t1.y, t1.z});
+                r2.insert(r2.end(), {t1.x, t1.y, t1.z, s[i + 1].x, s[i + 1].y, s[i + 1].z});
+                cand.push_back(t1);
+                at.emplace_back((uint32_t)q, (uint32_t)i);
+            }
+        }
+        if (cand.empty()) break;
+        const int64_t n = (int64_t)cand.size();
+        okp.assign((size_t)n, 0);
+        okr.assign((size_t)(2 * n), 0);
+        worldPtr->checkPoints(pts.data(), n, canPass, okp.data());
+        worldPtr->checkRays(r1.data(), r2.data(), 2 * n, canPass, okr.data());
+        std::vector<int> moved(st.size(), 0);
+        for (int64_t j = 0; j < n; ++j) {
+            if (!okp[j] || !okr[2 * j] || !okr[2 * j + 1]) continue;
+            Vec3& si = st[at[j].first][at[j].second];
+            if (distance(si, cand[j]) > minChange) {
+                si = cand[j];
+                ++moved[at[j].first];
+            }
+        }
+        bool any = false;
+        for (size_t q = 0; q < st.size(); ++q) {
+            if (live[q] && moved[q] == 0) live[q] = 0;  // OMPL: a step that moved nothing ends the loop
+            any = any || live[q];
+        }
+        if (!any) break;
+    }
+    return st;
 }
 
 // PathPlanner::pruneWaypoints — src/PathPlanner.cpp:232-265.  The reference checks

@@ -700,19 +700,29 @@ struct RefitArgs {
     int64_t* info;     // host-mapped: [status]
     uint32_t* done;    // host-mapped: the workgroups' completion slots
     double* scratch;   // device: G x segment scratch (tracks longer than kMaxLdsSeg)
+    int32_t big;       // (!LDS) the vertex values, right-hand sides, times and coefficients
+                       // in the global scratch too (tracks whose LDS part would not fit)
     double small[3 * kRefitArgW + 6 + kRefitArgW - 1];  // wp | v0 | a0 | T when W <= kRefitArgW
 };
 constexpr int kRefitBlock = 256;
 constexpr int kRefitRowChunk = 128;  // rows per round (LDS staged)
+constexpr size_t kRefitLdsMax = 150 * 1024;  // dynamic LDS of one refit workgroup (of 160 KB per CU)
 __host__ __device__ inline size_t refit_in_doubles(int W, int R) {  // (+ 3: row 0 readable when R = 0)
     return (size_t)3 * W + 6 + (W - 1) + 2 * (size_t)R + ((size_t)R + 1) / 2 + 3;
 }
 __host__ __device__ inline size_t refit_nin_even(int W) { return ((size_t)3 * W + 6 + (W - 1) + 1) & ~size_t(1); }
 // LDS doubles: flag (2) | constants | wp, v0, a0, T | solve scratch | coefficients |
-// sample chunk (t_in, t, segment) | row chunk
-__host__ __device__ inline size_t refit_lds_doubles(int M, bool lds) {
-    return 2 + kNC + refit_nin_even(M + 1) + (lds ? (size_t)M * Seg::kSize : 0) + vertex_doubles(M) + (size_t)M * 30 +
-           (size_t)kRefitRowChunk * 3 + 2 + (size_t)kRefitRowChunk * 10;
+// sample chunk (t_in, t, segment) | row chunk.  big: the vertex values, right-hand sides,
+// times and coefficients live in the global scratch; LDS keeps the lane exchange (kXch).
+__host__ __device__ inline size_t refit_lds_doubles(int M, bool lds, bool big = false) {
+    return 2 + kNC + refit_nin_even(M + 1) + (lds ? (size_t)M * Seg::kSize : 0) +
+           (big ? (size_t)kXch : vertex_doubles(M) + (size_t)M * 30) + (size_t)kRefitRowChunk * 3 + 2 +
+           (size_t)kRefitRowChunk * 10;
+}
+// global scratch doubles per writer: the segment scratch, and (big) the vertex values,
+// right-hand sides, times and coefficients
+__host__ __device__ inline size_t refit_scr_doubles(int M, bool big) {
+    return (size_t)M * Seg::kSize + (big ? vertex_doubles(M) - kXch + (size_t)M * 30 : 0);
 }
 
 template <bool LDS>
@@ -724,13 +734,19 @@ __device__ __forceinline__ void refit_body(const RefitArgs& a, int g, double* sm
     int* s_err = reinterpret_cast<int*>(smem);
     double* kc = smem + 2;
     double* P = kc + kNC;  // wp | v0 | a0 | T
-    double* scr = P + refit_nin_even(W);
+    double* const after_p = P + refit_nin_even(W);  // (LDS)
+    const bool big = !LDS && a.big;
+    double* scr = after_p;
     double* dv = LDS ? scr + (size_t)M * Seg::kSize : scr;
-    if (!LDS) scr = a.scratch + (size_t)g * M * Seg::kSize;
+    if (!LDS) {
+        scr = a.scratch + (size_t)g * refit_scr_doubles(M, big);
+        if (big) dv = scr + (size_t)M * Seg::kSize;
+    }
     double* rhs = dv + (size_t)(M + 1) * 15;
     double* Tm = rhs + (size_t)(M + 1) * 12;
-    double* C = Tm + M + kXch;  // coefficients (M x 3 x 10)
-    double* s_tin = C + (size_t)M * 30;
+    double* xch = big ? after_p : Tm + M;  // the solve's lane exchange: always LDS
+    double* C = big ? Tm + M : xch + kXch;  // coefficients (M x 3 x 10)
+    double* s_tin = big ? xch + kXch : C + (size_t)M * 30;
     double* s_tac = s_tin + kRefitRowChunk;
     int32_t* s_seg = reinterpret_cast<int32_t*>(s_tac + kRefitRowChunk);
     double* rbuf = reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(s_tac + 2 * kRefitRowChunk) + 15) &
@@ -771,7 +787,7 @@ __device__ __forceinline__ void refit_body(const RefitArgs& a, int g, double* sm
     block_sync<LDS>();
     EPP_TL(8);
     const int st = solve_track<kRefitBlock, LDS>(kc, P, M, 0.0, 0.0, P + 3 * W, P + 3 * W + 3, P + 3 * W + 6, scr, dv,
-                                            rhs, Tm, Tm + M, s_err, nullptr, C);
+                                            rhs, Tm, xch, s_err, nullptr, C);
     EPP_TL(7);
     if (tid < cnt0) {
         s_tin[tid] = f_tin;
@@ -985,6 +1001,7 @@ epp_status minsnap_batch(const double* wp, const int32_t* wp_offsets, int32_t n_
     constexpr int kB = 64;  // one wavefront per track: the batch is throughput-bound
     if (max_m <= kMaxLdsSeg) {
         const size_t shm = ((size_t)max_m * Seg::kSize + vertex_doubles(max_m) + 2 + kNC) * sizeof(double);
+        allow_lds(k_minsnap<kB, true>);
         hipLaunchKernelGGL((k_minsnap<kB, true>), dim3(n_tracks), dim3(kB), shm, s, wp, wp_offsets, n_tracks, v_max,
                            a_max, v0, a0, times_in, seg_times, coeffs, status, nullptr);
         return launch_error(what);
@@ -1001,6 +1018,13 @@ epp_status minsnap_batch(const double* wp, const int32_t* wp_offsets, int32_t n_
         return EPP_ERR_HIP;
     }
     const size_t shm = (vertex_doubles(max_m) + 2 + kNC) * sizeof(double);
+    if (shm > kLdsBudget) {
+        ws.release(s);
+        set_error(std::string(what) + ": a track has too many waypoints for one workgroup's LDS (" +
+                  std::to_string(max_m + 1) + ")");
+        return EPP_ERR_UNSUPPORTED;
+    }
+    allow_lds(k_minsnap<kB, false>);
     hipLaunchKernelGGL((k_minsnap<kB, false>), dim3(n_tracks), dim3(kB), shm, s, wp, wp_offsets, n_tracks, v_max, a_max,
                        v0, a0, times_in, seg_times, coeffs, status, static_cast<double*>(ws.buf));
     st = launch_error(what);
@@ -1186,6 +1210,14 @@ epp_status epp::check_and_generate_into(const FusedCheck* chk, const double* wp,
     }
     const int R = (int)c.tin.size();
     const bool lds = M <= kMaxLdsSeg;
+    // long tracks whose vertex values and coefficients would not fit LDS beside the rest
+    // (> ~300 segments: e.g. a track smoothed by "ompl" simplification) keep them in the
+    // global scratch too
+    const bool big = !lds && refit_lds_doubles(M, false) * sizeof(double) > kRefitLdsMax;
+    if (refit_lds_doubles(M, lds, big) * sizeof(double) > kRefitLdsMax) {
+        set_error("generateTrajectory: too many waypoints for one workgroup's LDS (" + std::to_string(n_wp) + ")");
+        return EPP_ERR_UNSUPPORTED;
+    }
     const int G = R ? std::min(kRefitMaxWriters, (R + kRefitRowChunk - 1) / kRefitRowChunk) : 1;
     // the fused check (chk): the lookahead points after the refit's inputs (h_in), their
     // flags after the completion slots (h_out); its workgroups after the refit's.  The
@@ -1206,7 +1238,7 @@ epp_status epp::check_and_generate_into(const FusedCheck* chk, const double* wp,
     constexpr size_t kRowsAt = 256;  // h_out: [status | pad | slots (<= 48 x 4 B) | flags | rows]
     const size_t rows_at = kRowsAt + (((size_t)nck + 255) & ~size_t(255));
     if ((rc = c.ensure((in_refit + 3 * (size_t)nck) * 8, (size_t)R * 80 + rows_at,
-                       lds ? 0 : (size_t)G * M * Seg::kSize * 8)))
+                       lds ? 0 : (size_t)G * refit_scr_doubles(M, big) * 8)))
         return rc;
     double* in = c.h_in;
     std::memcpy(in, wp, (size_t)n_wp * 24);
@@ -1234,8 +1266,9 @@ epp_status epp::check_and_generate_into(const FusedCheck* chk, const double* wp,
     a.done = reinterpret_cast<uint32_t*>(c.h_out + 64);
     a.out = reinterpret_cast<double*>(c.h_out + rows_at);
     a.scratch = c.d_scr;
+    a.big = big ? 1 : 0;
     a.info[0] = -100;
-    size_t shm = refit_lds_doubles(M, lds) * sizeof(double);
+    size_t shm = refit_lds_doubles(M, lds, big) * sizeof(double);
     if (Gc > 0) {
         double* pts = in + in_refit;
         std::memcpy(pts, chk->xyz, (size_t)nck * 24);
@@ -1250,11 +1283,18 @@ epp_status epp::check_and_generate_into(const FusedCheck* chk, const double* wp,
         ck.n = nck;
         ck.valid = reinterpret_cast<uint8_t*>(c.h_out + kRowsAt);
         shm = std::max(shm, small_shm(sw.n_obb));
-        if (lds) hipLaunchKernelGGL(k_check_refit<true>, dim3(G + Gc), dim3(kRefitBlock), shm, c.s, a, ck);
-        else hipLaunchKernelGGL(k_check_refit<false>, dim3(G + Gc), dim3(kRefitBlock), shm, c.s, a, ck);
+        if (lds) {
+            allow_lds(k_check_refit<true>);
+            hipLaunchKernelGGL(k_check_refit<true>, dim3(G + Gc), dim3(kRefitBlock), shm, c.s, a, ck);
+        } else {
+            allow_lds(k_check_refit<false>);
+            hipLaunchKernelGGL(k_check_refit<false>, dim3(G + Gc), dim3(kRefitBlock), shm, c.s, a, ck);
+        }
     } else if (lds) {
+        allow_lds(k_refit<true>);
         hipLaunchKernelGGL(k_refit<true>, dim3(G), dim3(kRefitBlock), shm, c.s, a);
     } else {
+        allow_lds(k_refit<false>);
         hipLaunchKernelGGL(k_refit<false>, dim3(G), dim3(kRefitBlock), shm, c.s, a);
     }
     hipError_t e = hipGetLastError();

@@ -91,6 +91,10 @@ private:
     std::vector<Vec3> shortcut(const std::vector<Vec3>& path) const;
     std::vector<std::vector<Vec3>> shortcutAll(const std::vector<std::vector<Vec3>>& paths) const;
     std::vector<std::vector<Vec3>> pruneAll(const std::vector<std::vector<Vec3>>& segments) const;
+    // omplPrunePathAndInterpolate (src/PathPlanner.cpp:282-313) for every segment at once:
+    // OMPL's PathSimplifier::smoothBSpline with its defaults, each step's state and motion
+    // checks for all segments in one batch each
+    std::vector<std::vector<Vec3>> smoothAll(const std::vector<std::vector<Vec3>>& segments) const;
     int planCalls(const std::vector<std::pair<Vec3, Vec3>>& problems, uint64_t base, double timeLimit,
                   std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const;
     void planAttempt(const std::vector<std::pair<Vec3, Vec3>>& problems, const std::vector<uint64_t>& seeds,

@@ -1,7 +1,8 @@
 """TEST INFRASTRUCTURE ONLY — a whole track planned on the CPU with this build's batch
 planner restated (oracle/epp_oracle.cpp or_plan_once): PathPlanner::planPath's attempt
 loop and seed derivation (efficient-path-planner_amd/csrc/host_planner.cpp), includeGates2
-with "custom" pruning (src/PathPlanner.cpp:175-265) on the oracle's ray checks, and the
+with "custom" pruning (src/PathPlanner.cpp:175-265) on the oracle's ray checks (or
+"ompl": OMPL's smoothBSpline restated, or "none"), and the
 min-snap trajectory (poly_traj::generateTrajectory restated).  Used as the checker of
 OnlineTrajGenerator::preComputeTraj (equal waypoints) and as bench.py's CPU full-plan
 baseline.  `OnlineTrajGeneratorCPU` restates the online half as well:
@@ -64,9 +65,61 @@ def prune_waypoints(seg, w, rg, ro):
     return out
 
 
-def include_gates2(segments, w, rg, ro, method="custom"):
+def _interpolate_half(a, b):
+    """RealVectorStateSpace::interpolate(from, to, 0.5): from + (to - from) * t, per axis."""
+    return np.array([a[d] + (b[d] - a[d]) * 0.5 for d in range(3)])
+
+
+def _distance(a, b):
+    """RealVectorStateSpace::distance: sqrt of the left-to-right sum of squared differences."""
+    t = 0.0
+    for d in range(3):
+        diff = a[d] - b[d]
+        t += diff * diff
+    return math.sqrt(t)
+
+
+def smooth_bspline(seg, w, rg, ro, can_pass, max_steps=5, min_change=np.finfo(np.float64).eps):
+    """omplPrunePathAndInterpolate (src/PathPlanner.cpp:282-313): OMPL's
+    PathSimplifier::smoothBSpline(path) with its defaults (maxSteps 5, minChange = double
+    epsilon), restated from OMPL 1.6's published source (ompl/geometric/src/
+    PathSimplifier.cpp, PathGeometric::subdivide, RealVectorStateSpace): per step the path
+    is subdivided (a midpoint between every two states), then every even state i
+    (2 <= i < n - 1) moves to the midpoint of its neighbours' midpoints with it when the
+    state before it is valid and both motions to the new point are valid and it moves more
+    than minChange; a step moving nothing ends the loop.  The validators are the planner's
+    (StateValidator / MotionValidator with the config's can_pass_gate).  OMPL is not
+    importable here: parity against OMPL itself is unpinned."""
+    states = [np.asarray(p, float) for p in seg]
+    if len(states) < 3:
+        return states
+    for _ in range(max_steps):
+        sub = [states[0]]
+        for i in range(1, len(states)):  # PathGeometric::subdivide
+            sub.append(_interpolate_half(sub[-1], states[i]))
+            sub.append(states[i])
+        states = sub
+        i, u, n1 = 2, 0, len(states) - 1
+        while i < n1:
+            if O.check_states(w, rg, ro, states[i - 1][None], can_pass)[0]:
+                t1 = _interpolate_half(states[i - 1], states[i])
+                t2 = _interpolate_half(states[i], states[i + 1])
+                t1 = _interpolate_half(t1, t2)
+                if (O.check_motions(w, rg, ro, states[i - 1][None], t1[None], can_pass, 0)[0]
+                        and O.check_motions(w, rg, ro, t1[None], states[i + 1][None], can_pass, 0)[0]):
+                    if _distance(states[i], t1) > min_change:
+                        states[i] = t1
+                        u += 1
+            i += 2
+        if u == 0:
+            break
+    return states
+
+
+def include_gates2(segments, w, rg, ro, method="custom", can_pass=False):
     """includeGates2 (src/PathPlanner.cpp:175-230): gate centre = midpoint of adjacent
-    segment ends, pruning, then drop points closer than 0.05 m to the previous one."""
+    segment ends, pruning ("custom": pruneWaypoints, "ompl": smoothBSpline on the planner's
+    validators, "none"), then drop points closer than 0.05 m to the previous one."""
     segs = [list(map(np.asarray, s)) for s in segments]
     centres = [(segs[i][-1] + segs[i + 1][0]) / 2 for i in range(len(segs) - 1)]
     for i, c in enumerate(centres):
@@ -74,7 +127,12 @@ def include_gates2(segments, w, rg, ro, method="custom"):
         segs[i + 1].insert(0, c)
     flat = []
     for seg in segs:
-        pruned = prune_waypoints(seg, w, rg, ro) if method == "custom" else seg
+        if method == "custom":
+            pruned = prune_waypoints(seg, w, rg, ro)
+        elif method == "ompl":
+            pruned = smooth_bspline(seg, w, rg, ro, can_pass)
+        else:
+            pruned = seg
         for p in pruned:
             if flat:
                 d = p - flat[-1]
@@ -85,7 +143,7 @@ def include_gates2(segments, w, rg, ro, method="custom"):
 
 
 def plan_track(w, rg, ro, lo, hi, checkpoints, samples, vmax, amax, dt, takeoff=0.0, k=16, can_pass=False,
-               threads=1, first_call=0, segments_out=None):
+               threads=1, first_call=0, segments_out=None, method="custom"):
     """OnlineTrajGenerator::preComputeTraj (src/OnlineTrajGenerator.cpp:72-121) on the CPU:
     one planPath per checkpoint pair (call numbers first_call, first_call + 1, ...),
     includeGates2, the min-snap trajectory.  Returns (waypoints, trajectory rows);
@@ -99,7 +157,7 @@ def plan_track(w, rg, ro, lo, hi, checkpoints, samples, vmax, amax, dt, takeoff=
         segments.append(p)
     if segments_out is not None:
         segments_out[:] = segments
-    wp = include_gates2(segments, w, rg, ro)
+    wp = include_gates2(segments, w, rg, ro, method, can_pass)
     return wp, O.generate_trajectory(wp, vmax, amax, dt, takeoff)
 
 
@@ -230,7 +288,8 @@ class OnlineTrajGeneratorCPU:
         if post is None:
             raise RuntimeError("Post segment path not found. Exiting")
         self.segments[seg_post] = post
-        filled = include_gates2(self.segments[seg_pre:], self.world, self.rg, self.ro)
+        filled = include_gates2(self.segments[seg_pre:], self.world, self.rg, self.ro,
+                                self.pp.get("path_simplification", "custom"), bool(self.pp["can_pass_gate"]))
         post_traj = self._generate(filled, adv, vel, acc)
         self.traj = np.vstack([traj[:start_adv], post_traj])
         self.waypoints = filled

@@ -88,10 +88,13 @@ def test_generate_trajectory_vs_oracle(seed):
     np.testing.assert_allclose(got[0, [2, 5, 8]], a0, atol=1e-9)
 
 
-@pytest.mark.parametrize("n,dt", [(40, 0.1), (26, 0.01), (9, 0.003)])
+@pytest.mark.parametrize("n,dt", [(40, 0.1), (26, 0.01), (9, 0.003), (60, 0.1), (200, 0.05), (331, 0.1),
+                                  (800, 0.1), (2000, 0.2)])
 def test_generate_trajectory_long_tracks(n, dt):
-    """The single-track latency path: more than 24 segments (global scratch), many rows
-    (row buffer sized from host-side segment times)."""
+    """The single-track latency path: up to 40 segments in LDS; more: the segment scratch
+    in global memory; past ~300 segments (e.g. a track smoothed by "ompl" simplification:
+    ~330 waypoints) the vertex values and coefficients too ("big" refit); many rows (row
+    buffer sized from host-side segment times)."""
     wp = synth.random_track_waypoints(900 + n, n)
     got = capi.generate_trajectory(wp, 1.5, 2.5, dt, 0.5)
     exp = O.generate_trajectory(wp, 1.5, 2.5, dt, 0.5)

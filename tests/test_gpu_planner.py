@@ -303,8 +303,12 @@ def _include_gates2_ref(segs, w, rg, ro, method):
     return np.array(flat)
 
 
-@pytest.mark.parametrize("method", ["custom", "none"])
+@pytest.mark.parametrize("method", ["custom", "none", "ompl"])
 def test_include_gates2_matches_restatement(tmp_path, c1, method):
+    """includeGates2 with each pruning method against the restatement: "custom" and
+    "none" above, "ompl" (OMPL's smoothBSpline, src/PathPlanner.cpp:282-313) against
+    oracle/track_planner.py smooth_bspline -- the segments' states bit for bit."""
+    import track_planner as TP
     g, o, _, _, w, rg, ro = c1
     path_cfg, _ = _write_config(tmp_path, path_planner_properties__path_simplification=method)
     pp = _ot().PathPlanner(g, o, path_cfg)
@@ -315,8 +319,37 @@ def test_include_gates2_matches_restatement(tmp_path, c1, method):
         segs.append(np.cumsum(rs.uniform(-0.3, 0.3, (n, 3)), 0) + [0, 0, 1.0])
     segs[1][0] = segs[0][-1] + 0.01  # a gate centre within the 0.05 de-duplication radius
     got = pp.include_gates2(segs)
-    ref = _include_gates2_ref(segs, w, rg, ro, method)
+    if method == "ompl":
+        ref = TP.include_gates2(segs, w, rg, ro, "ompl", False)
+        assert len(got) > sum(len(x) for x in segs)  # subdivided
+    else:
+        ref = _include_gates2_ref(segs, w, rg, ro, method)
     assert np.array_equal(got, ref)
+
+
+def test_precompute_traj_ompl_simplification_equals_cpu(track, geom, tmp_path):
+    """A whole track with path_simplification "ompl": the 9 plans, smoothBSpline on every
+    segment (batched steps on the GPU), the min-snap fit -- equal to the CPU restatement
+    (waypoints bit for bit, trajectory within 1e-6, time column exact)."""
+    import track_planner as TP
+    _, c, gates, obstacles, start, goal = track
+    c = json.loads(json.dumps(c))
+    c["path_planner_properties"]["path_simplification"] = "ompl"
+    p = tmp_path / "config_ompl.json"
+    p.write_text(json.dumps(c))
+    otg = _ot().OnlineTrajGenerator(start, goal, gates, obstacles, str(p))
+    otg.pre_compute_traj(0.0)
+    rg, ro = config.inflate_radii(c)
+    w = O.world_build(geom, gates, obstacles, rg, ro)
+    lo, hi = np.array(c["world_properties"]["lower_bound"], float), np.array(c["world_properties"]["upper_bound"], float)
+    tg, pp = c["trajectory_generator_properties"], c["path_planner_properties"]
+    wp, rows = TP.plan_track(w, rg, ro, lo, hi, otg.get_checkpoints(), pp["samples_fmt"], tg["max_velocity"],
+                             tg["max_acceleration"], tg["sampling_interval"], threads=8, method="ompl",
+                             can_pass=bool(pp["can_pass_gate"]))
+    assert np.array_equal(otg.get_waypoints(), wp)
+    traj = otg.get_planned_traj()
+    assert traj.shape == rows.shape and np.array_equal(traj[:, 9], rows[:, 9])
+    assert np.abs(traj[:, :9] - rows[:, :9]).max() < 1e-6
 
 
 def test_include_gates2_unknown_method(tmp_path, c1):
