@@ -228,6 +228,7 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["restricted_rows"] = s.restricted_rows;
             d["fallbacks"] = s.fallbacks;
             d["ms_batch"] = s.ms_batch;
+            d["ms_enqueue"] = s.ms_enqueue;
             d["ms_solve"] = s.ms_solve;
             d["ms_shortcut"] = s.ms_shortcut;
             d["ms"] = s.ms;
@@ -396,6 +397,7 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["restricted_rows"] = s.restricted_rows;
             d["fallbacks"] = s.fallbacks;
             d["ms_batch"] = s.ms_batch;
+            d["ms_enqueue"] = s.ms_enqueue;
             d["ms_solve"] = s.ms_solve;
             d["ms_shortcut"] = s.ms_shortcut;
             return d;

@@ -166,6 +166,7 @@ struct PlanBatchLayout {
 // segs: the problems with seed, ends, bound, gbound, the grid box and cell, cap filled;
 // row_off / need_off / need_cap are filled in here
 PlanBatchLayout plan_batch_layout(int32_t S, int64_t ns, int32_t k, PlanSeg* segs);
+void plan_batch_trace_print();  // (EPP_PB_TRACE=1 diagnostics: the last batch's stage times)
 epp_status plan_batch_launch(const epp_world* world, int32_t can_pass_gate, const double lo[3], const double hi[3],
                              const PlanBatchLayout& L, void* dev, void* host, uint32_t seq, void* stream);
 }  // namespace epp

@@ -520,9 +520,11 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
         std::unique_lock<std::mutex> lk(done_mu);
         done_cv.wait(lk, [&] { return pending == 0; });
     };
+    double ms_enqueue = 0;
     try {
         const uint32_t seq = bs.next_seq();
         check(plan_batch_launch(w, canPass ? 1 : 0, lo, hi, L, bs.dev(), H, seq, st), "planner batch");
+        ms_enqueue = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_dev0).count();
         // the emit's completion slots (polled: no stream synchronisation), the stream's
         // state every ~1k polls (a failed launch ends the wait)
         static const bool sync_wait = [] {  // (A/B knob: EPP_PB_SYNC=1 synchronises the stream instead)
@@ -546,6 +548,7 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
             }
             _mm_pause();
         }
+        plan_batch_trace_print();
         for (int p = 0; p < S; ++p) first[p + 1] = first[p] + std::min<int64_t>(hv(0, p), segs[p].cap);
         // Cold areas (this thread's first plans): one whole-table search on problem 0's
         // nodes, so that the fallback's first launches and transfers are paid here, in the
@@ -593,6 +596,7 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
     stats_.ms_device += ms_batch;
     stats_.ms_search += ms_sc;
     stats_.ms_batch += ms_batch;
+    stats_.ms_enqueue += ms_enqueue;
     stats_.ms_solve += ms_solve;
     stats_.ms_shortcut += ms_sc;
     for (int p = 0; p < S; ++p) {

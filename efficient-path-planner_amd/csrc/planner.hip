@@ -2145,7 +2145,10 @@ __device__ __forceinline__ bool pb_query_row(const KnnGrid& g, const double* __r
                                              const double (&p)[3], double f, double gbound, int self,
                                              int32_t* __restrict__ out, int64_t off) {
     constexpr int kCap = 512;
-    constexpr int kU = 2;  // candidates per lane in flight (4: 87 VGPRs, five waves per SIMD)
+#ifndef EPP_PB_KU  // (A/B builds may override)
+#define EPP_PB_KU 2
+#endif
+    constexpr int kU = EPP_PB_KU;  // candidates per lane in flight
     __shared__ double s_d[kCap];
     __shared__ int s_j[kCap];
     const int lane = threadIdx.x & 63;
@@ -2161,14 +2164,31 @@ __device__ __forceinline__ bool pb_query_row(const KnnGrid& g, const double* __r
             hi[d] = knn_cell_axis(p[d] + rb, g, d);
         }
         const int ny = hi[1] - lo[1] + 1, rows = ny * (hi[2] - lo[2] + 1);
+        // (a row's x-run narrowed to the sphere's chord: the row's y / z cell ranges --
+        // padded, the edge cells unbounded -- are at least dy / dz from p, so a node
+        // within rb of p has |x - p.x| <= sqrt(rb^2 - dy^2 - dz^2); cells are monotone in x)
+        const double pad = 1e-9 * (g.h + fabs(p[0]) + fabs(p[1]) + fabs(p[2]));
+        auto gap = [&](int c, int d) {
+            const double a = c == 0 ? -INFINITY : g.lo[d] + (double)c * g.h - pad;
+            const double b = c == g.dims[d] - 1 ? INFINITY : g.lo[d] + (double)(c + 1) * g.h + pad;
+            return p[d] < a ? a - p[d] : (p[d] > b ? p[d] - b : 0.0);
+        };
         int cnt = 0;  // (wave-uniform)
         for (int rb0 = 0; rb0 < rows; rb0 += 64) {
             const int row = rb0 + lane;
             int s0 = 0, len = 0;
             if (row < rows) {
-                const int a = ((lo[2] + row / ny) * g.dims[1] + lo[1] + row % ny) * g.dims[0];
-                s0 = start[a + lo[0]];
-                len = start[a + hi[0] + 1] - s0;
+                const int cz = lo[2] + row / ny, cy = lo[1] + row % ny;
+                const double dy = gap(cy, 1), dz = gap(cz, 2);
+                const double rem2 = rb * rb - (dy * dy + dz * dz);
+                if (rem2 >= 0.0) {
+                    const double hx = sqrt(rem2) + pad;
+                    const int x0 = max(lo[0], knn_cell_axis(p[0] - hx, g, 0));
+                    const int x1 = min(hi[0], knn_cell_axis(p[0] + hx, g, 0));
+                    const int a = (cz * g.dims[1] + cy) * g.dims[0];
+                    s0 = start[a + x0];
+                    len = start[a + x1 + 1] - s0;
+                }
             }
             int incl = len;  // inclusive scan of the run lengths over the lanes
 #pragma unroll
@@ -2897,6 +2917,53 @@ epp::PlanBatchLayout epp::plan_batch_layout(int32_t S, int64_t ns, int32_t k, Pl
     return L;
 }
 
+// EPP_PB_TRACE=1 (diagnostics knob, read once): events between the batch's stages on its
+// stream; plan_batch_trace_print() (after the batch completed) prints each stage's time in
+// microseconds to stderr, one line per batch.
+namespace {
+struct PbTrace {
+    bool on = false;
+    int n = 0;
+    hipEvent_t ev[16] = {};
+    const char* name[16] = {};
+};
+PbTrace& pb_trace() {
+    static const bool on = [] {
+        const char* e = std::getenv("EPP_PB_TRACE");
+        return e && std::atoi(e) == 1;
+    }();
+    thread_local PbTrace t;
+    if (on && !t.on) {
+        t.on = true;
+        for (auto& e : t.ev) (void)hipEventCreate(&e);
+    }
+    return t;
+}
+void pb_mark(hipStream_t s, const char* name) {
+    PbTrace& t = pb_trace();
+    if (!t.on || t.n >= 16) return;
+    t.name[t.n] = name;
+    (void)hipEventRecord(t.ev[t.n++], s);
+}
+}  // namespace
+
+void epp::plan_batch_trace_print() {
+    PbTrace& t = pb_trace();
+    if (!t.on || t.n < 2) return;
+    (void)hipEventSynchronize(t.ev[t.n - 1]);
+    std::string line = "pb_trace:";
+    float tot = 0;
+    for (int i = 1; i < t.n; ++i) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, t.ev[i - 1], t.ev[i]);
+        tot += ms;
+        line += std::string(" ") + t.name[i] + "=" + std::to_string((int)(ms * 1000.0f + 0.5f));
+    }
+    line += " total=" + std::to_string((int)(tot * 1000.0f + 0.5f));
+    std::fprintf(stderr, "%s\n", line.c_str());
+    t.n = 0;
+}
+
 epp_status epp::plan_batch_launch(const epp_world* world, int32_t can_pass_gate, const double lo[3], const double hi[3],
                                   const PlanBatchLayout& L, void* dev, void* host, uint32_t seq, void* stream) {
     if (!world || !dev || !host || L.S < 1 || L.S > 64 || L.ns < 1 || (L.k != 4 && L.k != 8 && L.k != 16) ||
@@ -2954,35 +3021,46 @@ epp_status epp::plan_batch_launch(const epp_world* world, int32_t can_pass_gate,
     if (hipMemcpyAsync(d + L.o_seg, h + L.h_seg, (size_t)L.S * sizeof(PlanSeg), hipMemcpyHostToDevice, s) != hipSuccess)
         return last("plan_batch_launch");
     const int64_t clr = std::max<int64_t>({L.ns, R ? L.NS >> 4 : 0, (int64_t)L.nbc, (int64_t)L.nctr});
+    pb_mark(s, "begin");
     hipLaunchKernelGGL(k_pb_sample, dim3((unsigned)((clr + 255) / 256), S), dim3(256), 0, s, P);
     if (const epp_status st = epp_check_states(world, P.xyz, (int64_t)L.S * L.ns, can_pass_gate, P.valid, nullptr,
                                                nullptr, stream))
         return st;
+    pb_mark(s, "states");
     hipLaunchKernelGGL(k_pb_compact, dim3((unsigned)L.nbc, S), dim3(kCompactThreads), 0, s, P, next_scan_tag());
     if (R) {
         const unsigned gn = (unsigned)((L.ns + 2 + 255) / 256), gb = (unsigned)((L.ns + 2 + kPbBlock - 1) / kPbBlock);
+        pb_mark(s, "compact");
         hipLaunchKernelGGL(k_pb_member, dim3(gb, S), dim3(kPbBlock), 0, s, P);
+        pb_mark(s, "member");
         hipLaunchKernelGGL(k_pb_knn_scan, dim3((unsigned)kl.scan_blocks, S), dim3(kScanThreads), 0, s, P, next_scan_tag());
         hipLaunchKernelGGL(k_pb_knn_scatter, dim3(gn, S), dim3(256), 0, s, P);
-        // one wave per workgroup, 28 per CU (72 VGPRs: seven waves per SIMD)
+        pb_mark(s, "scan_scatter");
+        // one wave per workgroup, 28 per CU (16 resident at 103 VGPRs; a variant with four
+        // queries per wave, 16 lanes each, was 1.9x slower: its 16-lane shuffles and LDS
+        // ranking cost more issue than the overlapped loads saved)
         const dim3 gr((unsigned)std::max(1, cu_count_planner() * 28)), br(64);
         if (L.k == 4) hipLaunchKernelGGL(k_pb_rows<4>, gr, br, 0, s, P);
         else if (L.k == 8) hipLaunchKernelGGL(k_pb_rows<8>, gr, br, 0, s, P);
         else hipLaunchKernelGGL(k_pb_rows<16>, gr, br, 0, s, P);
+        pb_mark(s, "rows");
         if (const epp_status st = check_knn_motions_rows(
                 world, P.nodes, P.rows32, P.ids32, reinterpret_cast<const int64_t*>(P.ctr + kPbRows), L.cap_total,
                 L.k, can_pass_gate, reinterpret_cast<uint8_t*>(d + L.o_ev), P.rows16, -1, nullptr, stream))
             return st;
+        pb_mark(s, "motions");
         const int64_t ents = (int64_t)L.cap_total * L.k;
         hipLaunchKernelGGL(k_pb_mark, dim3((unsigned)((ents + kPbBlock - 1) / kPbBlock)), dim3(kPbBlock), 0, s, P);
         hipLaunchKernelGGL(k_pb_number, dim3((unsigned)((L.ns + 2 + kCompactChunk - 1) / kCompactChunk), S),
                            dim3(kCompactThreads), 0, s, P, next_scan_tag());
         hipLaunchKernelGGL(k_pb_remap, dim3((unsigned)((ents + 255) / 256)), dim3(256), 0, s, P);
+        pb_mark(s, "mark_number_remap");
     }
     hipLaunchKernelGGL(k_pb_emit, dim3((unsigned)L.done_n), dim3(256), 0, s, P,
                        reinterpret_cast<unsigned long long*>(h + L.h_hdr), reinterpret_cast<uint4*>(h + L.h_slot),
                        reinterpret_cast<uint4*>(h + L.h_rows), reinterpret_cast<uint4*>(h + L.h_need),
                        reinterpret_cast<uint32_t*>(h + L.h_done), seq);
+    pb_mark(s, "emit");
     return last("plan_batch_launch");
 }
 

@@ -39,6 +39,7 @@ struct PlannerStats {
     // wall time of the batched planner's phases (summed over its attempts): the device
     // stages up to the emitted results, the searches on the planner threads, the shortcut
     double ms_batch = 0, ms_solve = 0, ms_shortcut = 0;
+    double ms_enqueue = 0;  // of ms_batch: the host until every stage of the batch was queued
 };
 
 class PathPlanner {

@@ -48,7 +48,8 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
                                    f"fallbacks {st[i]['fallbacks']})"
                                    for i in order), flush=True)
     print("   fallbacks per call:", [s["fallbacks"] for s in st], "mean", np.mean([s["fallbacks"] for s in st]))
-    print(f"   planner phases p50 (ms): batch {np.median([s['ms_batch'] for s in st]):.3f} solve "
+    print(f"   planner phases p50 (ms): batch {np.median([s['ms_batch'] for s in st]):.3f} (enqueued by "
+          f"{np.median([s.get('ms_enqueue', float('nan')) for s in st]):.3f}) solve "
           f"{np.median([s['ms_solve'] for s in st]):.3f} shortcut {np.median([s['ms_shortcut'] for s in st]):.3f}; "
           f"outside the planner {np.median([t - s['ms'] for t, s in zip(ts, st)]):.3f}", flush=True)
     print("   all (ms):", " ".join(f"{t:.2f}/{s['ms']:.2f}" for t, s in zip(ts, st)), flush=True)
