@@ -109,7 +109,7 @@ private:
     std::shared_ptr<ConfigParser> configParser;
     uint64_t seed_ = 0x5eedull;
     int k_ = 16;
-    double ellipse_ = 1.5;  // row-restricted search: bound = ellipse_ |start - goal| + 0.25 m (0: off)
+    double ellipse_ = 1.25;  // row-restricted search: bound = ellipse_ |start - goal| + 0.25 m (0: off)
     int threads_ = 16;      // planner threads of a batch's searches (at most one per problem)
     mutable uint64_t calls_ = 0;
     mutable PlannerStats stats_;

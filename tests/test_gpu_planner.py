@@ -699,7 +699,7 @@ def test_c1_plumbing_end_to_end(tmp_path, c1, geom):
 # ---- the planner against its CPU restatement (oracle/epp_oracle.cpp or_plan_once) ------
 # Same counter-RNG samples, exact k-NN with the same tie rule, the same A* and shortcut:
 # the GPU pipeline must give the SAME path, not just a valid one.
-# EPP_PLAN_ELLIPSE: the row-restricted table download (default factor 1.5), a bound the
+# EPP_PLAN_ELLIPSE: the row-restricted table download (default factor 1.25), a bound the
 # paths exceed (1.0: the search falls back to the whole table) and the whole table only (0)
 ELLIPSE = ["", "1.0", "0"]
 
