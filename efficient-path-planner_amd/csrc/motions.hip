@@ -650,6 +650,43 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
             if (jp < ntiles) ida = tile_cand(jp, ca);
             if (jp + 1 < ntiles) idb = tile_cand(jp + 1, cb);
             EPP_MTL_NOW(tl_p);
+#ifndef EPP_MOTIONS_ROUNDS  // (A/B: the one-candidate-per-lane rounds for the analytic mode too)
+            if constexpr (PF && W <= 2) {  // (wider rows: the rounds, whose registers fit)
+                // Every candidate queued at once: a wave scan of the lanes' candidate counts
+                // gives each lane its queue slots, and each lane writes its own (a loop as
+                // long as the busiest lane's count, a few instructions per entry) instead of
+                // one candidate per lane and round through the wave (~27 instructions per
+                // round).  The order of the queue does not change the answer (any hit).
+                uint32_t c = 0;
+#pragma unroll
+                for (int w = 0; w < W; ++w) c += (uint32_t)(__popc(ca[w]) + __popc(cb[w]));
+                uint32_t tot;
+                const uint32_t off = wave_excl_scan(c, lane, tot);
+                if (tot > 0u && tot <= (uint32_t)kQueueV5) {  // wave-uniform
+                    if (qn + tot > (uint32_t)kQueueV5) flush();
+                    uint32_t at = qn + off;
+#pragma unroll
+                    for (int w = 0; w < 2 * W; ++w) {
+                        uint32_t cw = w < W ? ca[w] : cb[w - W];
+                        const uint16_t* tid = w < W ? ida : idb;  // (non-null whenever cw != 0)
+                        while (cw) {
+                            const uint32_t bit = (uint32_t)__builtin_ctz(cw);
+                            cw &= cw - 1u;
+                            queue[at++] = (uint32_t)tid[32 * (w % W) + bit] << 6 | (uint32_t)lane;
+                        }
+                    }
+                    qn += tot;
+                    if (qn > (uint32_t)(kQueueV5 - 64)) flush();
+                    EPP_MTL_ADD(tl_e, tl_p);
+                    continue;
+                }
+                if (tot == 0u) {
+                    EPP_MTL_ADD(tl_e, tl_p);
+                    continue;
+                }
+                // (more candidates than the queue holds: the rounds below)
+            }
+#endif
 #ifdef EPP_MOTIONS_W1MASK  // (A/B) one-word tiles: both tiles' candidates as one 64-bit mask
             uint64_t cm = W == 1 ? ((uint64_t)ca[0] | ((uint64_t)cb[0] << 32)) : 0ull;
 #endif
