@@ -155,7 +155,7 @@ struct PlanBatchLayout {
                                           // referenced-node slots of all problems
     // device workspace (bytes from its base, 256-B aligned parts)
     size_t o_seg = 0, o_ctr = 0, o_xyz = 0, o_valid = 0, o_nodes = 0, o_cstat = 0, o_kws = 0, kws_stride = 0,
-           o_query = 0, o_ids32 = 0, o_rows32 = 0, o_rows16 = 0, o_ev = 0, o_mark = 0, o_map = 0, o_nstat = 0, o_slot = 0,
+           o_query = 0, o_ids32 = 0, o_rows32 = 0, o_rows16 = 0, o_ev = 0, o_mark = 0, o_map = 0, o_nstat = 0,
            o_need = 0, dev_bytes = 0;
     // pinned host block: the problems (uploaded), then the emitted header, per row its
     // problem and node (p << 16 | compact index), the masked rows (compact indices, 0xFFFF:

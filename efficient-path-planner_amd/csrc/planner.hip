@@ -1971,7 +1971,6 @@ struct PlanBatchDev {
     uint16_t* rows16;   // the same masked (node ids, then compact indices; 0xFFFF: none)
     uint8_t* mark;      // a byte per node: referenced by a row
     int32_t* map;       // node (global id) -> compact index (referenced nodes only)
-    uint32_t* slot;     // row -> p << 16 | compact index of its node
     double* need;       // 3 doubles per referenced node (at need_off + compact index)
 };
 
@@ -2008,29 +2007,11 @@ __global__ __launch_bounds__(256) void k_pb_sample(PlanBatchDev P) {
     if (P.cap_total > 0 && i < (P.NS >> 4))
         reinterpret_cast<uint4*>(P.mark + ((int64_t)p << P.ns_log))[i] = make_uint4(0u, 0u, 0u, 0u);
     if (p == 0 && i < P.nctr) P.ctr[i] = 0ull;
-    if (i >= P.ns) return;
-    const uint64_t seed = P.seg[p].seed;
-    const uint64_t c = (uint64_t)i * 3ull;
-    const double u0 = (double)(splitmix64(seed ^ c) >> 11) * 0x1.0p-53;
-    const double u1 = (double)(splitmix64(seed ^ (c + 1)) >> 11) * 0x1.0p-53;
-    const double u2 = (double)(splitmix64(seed ^ (c + 2)) >> 11) * 0x1.0p-53;
-    double* x = P.xyz + ((int64_t)p * P.ns + i) * 3;
-    x[0] = P.lo[0] + (P.hi[0] - P.lo[0]) * u0;
-    x[1] = P.lo[1] + (P.hi[1] - P.lo[1]) * u1;
-    x[2] = P.lo[2] + (P.hi[2] - P.lo[2]) * u2;
-}
-
-// nodes = start, goal, the valid samples in sample order; the node count into the header;
-// the grid's shape and cleared counters (the workspace may hold anything)
-__global__ __launch_bounds__(kCompactThreads) void k_pb_compact(PlanBatchDev P, uint32_t tag) {
-    const int p = blockIdx.y;
-    double* out = P.nodes + (int64_t)p * P.NS * 3;
     const PlanSeg& q = P.seg[p];
-    if (blockIdx.x == 0 && threadIdx.x < 6) out[threadIdx.x] = threadIdx.x < 3 ? q.s[threadIdx.x] : q.g[threadIdx.x - 3];
-    if (q.cap > 0) {
+    if (q.cap > 0) {  // the problem's k-NN grid: cleared cell counters and its shape
         const KnnSeg ks = knn_seg(P, p);
-        for (int i = blockIdx.x * kCompactThreads + threadIdx.x; i < P.nclr; i += gridDim.x * kCompactThreads) ks.cnt[i] = 0;
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (i < P.nclr) ks.cnt[i] = 0;
+        if (i == 0) {
             KnnGrid gv{};
             int64_t cells = 1;
             double h = q.h;
@@ -2051,8 +2032,16 @@ __global__ __launch_bounds__(kCompactThreads) void k_pb_compact(PlanBatchDev P, 
             *ks.g = gv;
         }
     }
-    compact_block(P.xyz + (int64_t)p * P.ns * 3, P.valid + (int64_t)p * P.ns, P.ns, P.cstat + (int64_t)p * P.nbc, tag,
-                  out + 6, reinterpret_cast<int64_t*>(&pb_ctr(P, kFNodes, p)), 2, blockIdx.x, gridDim.x);
+    if (i >= P.ns) return;
+    const uint64_t seed = q.seed;
+    const uint64_t c = (uint64_t)i * 3ull;
+    const double u0 = (double)(splitmix64(seed ^ c) >> 11) * 0x1.0p-53;
+    const double u1 = (double)(splitmix64(seed ^ (c + 1)) >> 11) * 0x1.0p-53;
+    const double u2 = (double)(splitmix64(seed ^ (c + 2)) >> 11) * 0x1.0p-53;
+    double* x = P.xyz + ((int64_t)p * P.ns + i) * 3;
+    x[0] = P.lo[0] + (P.hi[0] - P.lo[0]) * u0;
+    x[1] = P.lo[1] + (P.hi[1] - P.lo[1]) * u1;
+    x[2] = P.lo[2] + (P.hi[2] - P.lo[2]) * u2;
 }
 
 __device__ __forceinline__ double pb_ellipse(const PlanSeg& q, const double* x) {
@@ -2063,47 +2052,135 @@ __device__ __forceinline__ double pb_ellipse(const PlanSeg& q, const double* x) 
     return ds + dg;
 }
 
-// Per node: inside the grid ellipsoid -> its cell counted (cell_of, else -1); inside the
-// row ellipsoid (widened by 1e-8 relative + 1e-6 m) -> listed as a query, ranks from one
-// atomic per workgroup.
+// Per node (problems with restricted rows): inside the grid ellipsoid -> its cell counted
+// (cell_of, else -1); inside the row ellipsoid (widened by 1e-8 relative + 1e-6 m) ->
+// listed as a query (ranks from one atomic per workgroup).
 constexpr int kPbBlock = 1024;
-__global__ __launch_bounds__(kPbBlock) void k_pb_member(PlanBatchDev P) {
-    const int p = blockIdx.y;
-    const PlanSeg& q = P.seg[p];
-    if (q.cap <= 0) return;  // (block-uniform)
-    __shared__ int s_cnt[kPbBlock / 64];
-    __shared__ unsigned long long s_base;
-    const int i = blockIdx.x * kPbBlock + threadIdx.x;
-    const int n = (int)pb_ctr(P, kFNodes, p);
-    const KnnSeg ks = knn_seg(P, p);
-    bool in = false;
-    if (i < n) {
-        const double* x = P.nodes + ((int64_t)p * P.NS + i) * 3;
-        const double f = pb_ellipse(q, x);
-        int c = -1;
-        if (f <= q.gbound) {
-            const KnnGrid& g = *ks.g;
-            const int cx = knn_cell_axis(x[0], g, 0), cy = knn_cell_axis(x[1], g, 1), cz = knn_cell_axis(x[2], g, 2);
-            c = (cz * g.dims[1] + cy) * g.dims[0] + cx;
-            atomicAdd(&ks.cnt[c], 1);
-        }
-        ks.cell_of[i] = c;
-        in = f <= q.bound * (1.0 + 1e-8) + 1e-6;
+__device__ __forceinline__ bool pb_member(const PlanBatchDev& P, const PlanSeg& q, const KnnSeg& ks, const KnnGrid& g,
+                                          int p, int node, const double* x) {
+    const double f = pb_ellipse(q, x);
+    int c = -1;
+    if (f <= q.gbound) {
+        const int cx = knn_cell_axis(x[0], g, 0), cy = knn_cell_axis(x[1], g, 1), cz = knn_cell_axis(x[2], g, 2);
+        c = (cz * g.dims[1] + cy) * g.dims[0] + cx;
+        atomicAdd(&ks.cnt[c], 1);
     }
+    ks.cell_of[node] = c;
+    return f <= q.bound * (1.0 + 1e-8) + 1e-6;
+}
+
+// nodes = start, goal, the valid samples in sample order (an ordered compaction, decoupled
+// look-back as compact_block); the node count into the header; each node's membership
+// (pb_member) as it is written, the queries listed.
+__global__ __launch_bounds__(kCompactThreads) void k_pb_compact(PlanBatchDev P, uint32_t tag) {
+    const int p = blockIdx.y, b = blockIdx.x, nb = gridDim.x;
+    double* out = P.nodes + (int64_t)p * P.NS * 3;
+    const PlanSeg& q = P.seg[p];
+    const bool R = q.cap > 0;  // (block-uniform)
+    const KnnSeg ks = knn_seg(P, p);
+    KnnGrid g{};
+    if (R) g = *ks.g;
+    const double* xyz = P.xyz + (int64_t)p * P.ns * 3;
+    const uint8_t* valid = P.valid + (int64_t)p * P.ns;
+    unsigned long long* st = P.cstat + (int64_t)p * P.nbc;
+    constexpr int NW = kCompactThreads / 64;
+    __shared__ int wcnt[kCompactRounds * NW];
+    __shared__ int qcnt[NW];
+    __shared__ long long s_excl;
+    __shared__ unsigned long long s_qbase;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const unsigned long long bal = __ballot(in);
-    if (lane == 0) s_cnt[wv] = __popcll(bal);
+    bool inq2 = false;  // start (thread 0) / goal (thread 1) of block 0: listed as queries
+    if (b == 0 && threadIdx.x < 2) {
+        const double* e = threadIdx.x == 0 ? q.s : q.g;
+        out[3 * threadIdx.x] = e[0];
+        out[3 * threadIdx.x + 1] = e[1];
+        out[3 * threadIdx.x + 2] = e[2];
+        if (R) inq2 = pb_member(P, q, ks, g, p, (int)threadIdx.x, e);
+    }
+    const int64_t i0 = (int64_t)b * kCompactChunk + threadIdx.x;
+    bool v[kCompactRounds];
+    unsigned long long bal[kCompactRounds];
+#pragma unroll
+    for (int r = 0; r < kCompactRounds; ++r) {
+        const int64_t i = i0 + r * kCompactThreads;
+        v[r] = i < P.ns && valid[i] != 0;
+    }
+#pragma unroll
+    for (int r = 0; r < kCompactRounds; ++r) {
+        bal[r] = __ballot(v[r]);
+        if (lane == 0) wcnt[r * NW + wv] = __popcll(bal[r]);
+    }
+    __syncthreads();
+    int before[kCompactRounds], total = 0;
+#pragma unroll
+    for (int qq = 0; qq < kCompactRounds * NW; ++qq) {
+#pragma unroll
+        for (int r = 0; r < kCompactRounds; ++r)
+            if (qq == r * NW + wv) before[r] = total;
+        total += wcnt[qq];
+    }
+    if (wv == 0) {
+        if (lane == 0) lb_publish(st, b, tag, b == 0, total);
+        const long long ex = b == 0 ? 0ll : lb_exclusive(st, b, tag);
+        if (lane == 0) {
+            if (b > 0) lb_publish(st, b, tag, true, ex + total);
+            s_excl = ex;
+            if (b == nb - 1) pb_ctr(P, kFNodes, p) = (unsigned long long)(ex + total + 2);
+        }
+    }
+    __syncthreads();
+    const long long ex = s_excl;
+    bool inq[kCompactRounds];
+    int node[kCompactRounds];
+#pragma unroll
+    for (int r = 0; r < kCompactRounds; ++r) {
+        inq[r] = false;
+        node[r] = 0;
+        if (v[r]) {
+            const int64_t i = i0 + r * kCompactThreads;
+            const int64_t at = 2 + ex + before[r] +
+                               (int64_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal[r] >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bal[r], 0u));
+            const double x[3] = {xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]};
+            out[3 * at] = x[0];
+            out[3 * at + 1] = x[1];
+            out[3 * at + 2] = x[2];
+            node[r] = (int)at;
+            if (R) inq[r] = pb_member(P, q, ks, g, p, (int)at, x);
+        }
+    }
+    if (!R) return;  // (block-uniform)
+    // the block's queries: one atomic per workgroup on the problem's query count
+    unsigned long long qb[kCompactRounds + 1];
+    int wq = 0;
+#pragma unroll
+    for (int r = 0; r < kCompactRounds; ++r) {
+        qb[r] = __ballot(inq[r]);
+        wq += __popcll(qb[r]);
+    }
+    qb[kCompactRounds] = __ballot(inq2);
+    wq += __popcll(qb[kCompactRounds]);
+    if (lane == 0) qcnt[wv] = wq;
     __syncthreads();
     if (threadIdx.x == 0) {
         int t = 0;
-        for (int w = 0; w < kPbBlock / 64; ++w) t += s_cnt[w];
-        s_base = t ? atomicAdd(&pb_ctr(P, kFQueries, p), (unsigned long long)t) : 0ull;
+        for (int w = 0; w < NW; ++w) t += qcnt[w];
+        s_qbase = t ? atomicAdd(&pb_ctr(P, kFQueries, p), (unsigned long long)t) : 0ull;
     }
     __syncthreads();
-    if (!in) return;
-    unsigned long long r = s_base + __popcll(bal & ((1ull << lane) - 1ull));
-    for (int w = 0; w < wv; ++w) r += s_cnt[w];
-    if (r < (unsigned long long)q.cap) P.query[q.row_off + (int64_t)r] = i;
+    unsigned long long rnk = s_qbase;
+    for (int w = 0; w < wv; ++w) rnk += qcnt[w];
+    const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int r = 0; r <= kCompactRounds; ++r) {
+        const bool mine = r < kCompactRounds ? inq[r] : inq2;
+        const int nd = r < kCompactRounds ? node[r] : (int)threadIdx.x;
+        if (mine) {
+            const unsigned long long at = rnk + __popcll(qb[r] & below);
+            if (at < (unsigned long long)q.cap) P.query[q.row_off + (int64_t)at] = nd;
+        }
+        rnk += __popcll(qb[r]);
+    }
 }
 
 __global__ __launch_bounds__(kScanThreads) void k_pb_knn_scan(PlanBatchDev P, uint32_t tag) {
@@ -2401,21 +2478,9 @@ __global__ __launch_bounds__(kCompactThreads) void k_pb_number(PlanBatchDev P, u
     }
 }
 
-// The rows in compact indices (in place) and each row's problem and node.
-__global__ __launch_bounds__(256) void k_pb_remap(PlanBatchDev P) {
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t rows = (int64_t)P.ctr[kPbRows];
-    if (e >= rows * P.k) return;
-    const int64_t r = e / P.k;
-    const int32_t u = P.ids32[r];
-    const int p = u >> P.ns_log;
-    const uint16_t v = P.rows16[e];
-    if (v != 0xFFFF) P.rows16[e] = (uint16_t)P.map[((int64_t)p << P.ns_log) + v];
-    if (e == r * P.k) P.slot[r] = ((uint32_t)p << 16) | ((uint32_t)P.map[u] & 0xFFFFu);
-}
-
 // The results into pinned host memory, only the bytes in use: the header (counters), the
-// rows' problem and node (u32), the masked rows (u16), every problem's referenced nodes
+// rows' problem and compact node index (u32), the masked rows in compact indices (u16,
+// renumbered here through `map` as they are copied), every problem's referenced nodes
 // (24 B each, at its own offset).  16-byte stores (the device parts are 16-byte padded).
 // Each workgroup then publishes `seq` in its completion slot (host memory, system scope,
 // after a system fence over its stores): the host polls the slots instead of synchronising
@@ -2443,14 +2508,36 @@ __global__ __launch_bounds__(256) void k_pb_emit(PlanBatchDev P, unsigned long l
     const int64_t c_slot = (rows * 4 + 15) / 16, c_rows = (rows * P.k * 2 + 15) / 16, c_need = pre[P.S];
     const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (tid < P.nctr) hdr[tid] = P.ctr[tid];
-    const uint4* d_slot = reinterpret_cast<const uint4*>(P.slot);
     const uint4* d_rows = reinterpret_cast<const uint4*>(P.rows16);
     const uint4* d_need = reinterpret_cast<const uint4*>(P.need);
+    const uint32_t lmask = (1u << P.ns_log) - 1u;
+    // a row entry (node id in its problem, 0xFFFF: none) in compact indices
+    auto remap = [&](int64_t e, uint32_t v) -> uint32_t {
+        if (v == 0xFFFFu || e >= rows * P.k) return v;
+        const int32_t u = P.ids32[e / P.k];
+        return (uint32_t)P.map[(u & ~(int32_t)lmask) + (int32_t)v] & 0xFFFFu;
+    };
     for (int64_t c = tid; c < c_slot + c_rows + c_need; c += (int64_t)gridDim.x * 256) {
-        if (c < c_slot) {
-            h_slot[c] = d_slot[c];
-        } else if (c < c_slot + c_rows) {
-            h_rows[c - c_slot] = d_rows[c - c_slot];
+        if (c < c_slot) {  // (p << 16 | the row's node, compact) for rows 4c .. 4c + 3
+            uint32_t sv[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int64_t r = 4 * c + j;
+                const int32_t u = r < rows ? P.ids32[r] : 0;
+                sv[j] = r < rows ? (((uint32_t)u >> P.ns_log) << 16) | ((uint32_t)P.map[u] & 0xFFFFu) : 0u;
+            }
+            h_slot[c] = make_uint4(sv[0], sv[1], sv[2], sv[3]);
+        } else if (c < c_slot + c_rows) {  // 8 row entries
+            const int64_t cr = c - c_slot;
+            const uint4 w = d_rows[cr];
+            const uint32_t in[4] = {w.x, w.y, w.z, w.w};
+            uint32_t o[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int64_t e = 8 * cr + 2 * j;
+                o[j] = remap(e, in[j] & 0xFFFFu) | (remap(e + 1, in[j] >> 16) << 16);
+            }
+            h_rows[cr] = make_uint4(o[0], o[1], o[2], o[3]);
         } else {
             const int64_t r = c - c_slot - c_rows;
             int p = 0;
@@ -2895,7 +2982,6 @@ epp::PlanBatchLayout epp::plan_batch_layout(int32_t S, int64_t ns, int32_t k, Pl
     L.o_mark = take(R ? (size_t)S * L.NS : 0);
     L.o_map = take(R ? (size_t)S * L.NS * 4 : 0);
     L.o_nstat = take(R ? (size_t)S * (L.NS / kCompactChunk) * 8 : 0);
-    L.o_slot = take(capr * 4);
     L.o_need = take((size_t)L.need_cap * 24 + 16);
     L.dev_bytes = o;
     o = 0;
@@ -2907,7 +2993,7 @@ epp::PlanBatchLayout epp::plan_batch_layout(int32_t S, int64_t ns, int32_t k, Pl
     {  // emit workgroups: each one's system fence writes back its XCD's L2, so few of them
         static const int eb = [] {
             const char* e = std::getenv("EPP_PB_EMIT_BLOCKS");  // (A/B knob: same results)
-            const int v = e && *e ? std::atoi(e) : 32;
+            const int v = e && *e ? std::atoi(e) : 64;
             return std::max(1, std::min(kPbEmitMax, v));
         }();
         L.done_n = eb;
@@ -3013,14 +3099,13 @@ epp_status epp::plan_batch_launch(const epp_world* world, int32_t can_pass_gate,
     P.mark = reinterpret_cast<uint8_t*>(d + L.o_mark);
     P.nstat = reinterpret_cast<unsigned long long*>(d + L.o_nstat);
     P.map = reinterpret_cast<int32_t*>(d + L.o_map);
-    P.slot = reinterpret_cast<uint32_t*>(d + L.o_slot);
     P.need = reinterpret_cast<double*>(d + L.o_need);
     const unsigned S = (unsigned)L.S;
     const bool R = L.cap_total > 0;
     // the problems up (pinned), then every stage on this stream
     if (hipMemcpyAsync(d + L.o_seg, h + L.h_seg, (size_t)L.S * sizeof(PlanSeg), hipMemcpyHostToDevice, s) != hipSuccess)
         return last("plan_batch_launch");
-    const int64_t clr = std::max<int64_t>({L.ns, R ? L.NS >> 4 : 0, (int64_t)L.nbc, (int64_t)L.nctr});
+    const int64_t clr = std::max<int64_t>({L.ns, R ? L.NS >> 4 : 0, R ? (int64_t)P.nclr : 0, (int64_t)L.nbc, (int64_t)L.nctr});
     pb_mark(s, "begin");
     hipLaunchKernelGGL(k_pb_sample, dim3((unsigned)((clr + 255) / 256), S), dim3(256), 0, s, P);
     if (const epp_status st = epp_check_states(world, P.xyz, (int64_t)L.S * L.ns, can_pass_gate, P.valid, nullptr,
@@ -3029,10 +3114,8 @@ epp_status epp::plan_batch_launch(const epp_world* world, int32_t can_pass_gate,
     pb_mark(s, "states");
     hipLaunchKernelGGL(k_pb_compact, dim3((unsigned)L.nbc, S), dim3(kCompactThreads), 0, s, P, next_scan_tag());
     if (R) {
-        const unsigned gn = (unsigned)((L.ns + 2 + 255) / 256), gb = (unsigned)((L.ns + 2 + kPbBlock - 1) / kPbBlock);
-        pb_mark(s, "compact");
-        hipLaunchKernelGGL(k_pb_member, dim3(gb, S), dim3(kPbBlock), 0, s, P);
-        pb_mark(s, "member");
+        const unsigned gn = (unsigned)((L.ns + 2 + 255) / 256);
+        pb_mark(s, "compact_member");
         hipLaunchKernelGGL(k_pb_knn_scan, dim3((unsigned)kl.scan_blocks, S), dim3(kScanThreads), 0, s, P, next_scan_tag());
         hipLaunchKernelGGL(k_pb_knn_scatter, dim3(gn, S), dim3(256), 0, s, P);
         pb_mark(s, "scan_scatter");
@@ -3053,8 +3136,7 @@ epp_status epp::plan_batch_launch(const epp_world* world, int32_t can_pass_gate,
         hipLaunchKernelGGL(k_pb_mark, dim3((unsigned)((ents + kPbBlock - 1) / kPbBlock)), dim3(kPbBlock), 0, s, P);
         hipLaunchKernelGGL(k_pb_number, dim3((unsigned)((L.ns + 2 + kCompactChunk - 1) / kCompactChunk), S),
                            dim3(kCompactThreads), 0, s, P, next_scan_tag());
-        hipLaunchKernelGGL(k_pb_remap, dim3((unsigned)((ents + 255) / 256)), dim3(256), 0, s, P);
-        pb_mark(s, "mark_number_remap");
+        pb_mark(s, "mark_number");
     }
     hipLaunchKernelGGL(k_pb_emit, dim3((unsigned)L.done_n), dim3(256), 0, s, P,
                        reinterpret_cast<unsigned long long*>(h + L.h_hdr), reinterpret_cast<uint4*>(h + L.h_slot),
