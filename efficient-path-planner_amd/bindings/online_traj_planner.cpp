@@ -227,6 +227,7 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["rows_downloaded"] = s.rows_downloaded;
             d["restricted_rows"] = s.restricted_rows;
             d["fallbacks"] = s.fallbacks;
+            d["fallback_why"] = std::vector<int64_t>(s.fallback_why, s.fallback_why + 5);
             d["ms_batch"] = s.ms_batch;
             d["ms_enqueue"] = s.ms_enqueue;
             d["ms_solve"] = s.ms_solve;
@@ -396,6 +397,7 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["rows_downloaded"] = s.rows_downloaded;
             d["restricted_rows"] = s.restricted_rows;
             d["fallbacks"] = s.fallbacks;
+            d["fallback_why"] = std::vector<int64_t>(s.fallback_why, s.fallback_why + 5);
             d["ms_batch"] = s.ms_batch;
             d["ms_enqueue"] = s.ms_enqueue;
             d["ms_solve"] = s.ms_solve;

@@ -431,6 +431,7 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
     struct Out {
         int64_t n = 0, edges_checked = 0, edges_valid = 0, rows_down = 0, restricted_rows = 0;
         int fallback = 0;  // 1: the whole table after the restricted rows could not decide
+        int why = -1;      // (PlannerStats::fallback_why)
         double ms_dev = 0, ms_search = 0;
     };
     std::vector<Out> res(S);
@@ -447,6 +448,7 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
         int r = 0;
         // (restricted: rows within capacity, exact (hv 5), a kept edge into the goal, node
         // ids in u16; start and goal are compact indices 0 and 1: rows of their own)
+        if (segs[p].cap > 0) o.why = (n > 65535 || packed > segs[p].cap || m < 2) ? 0 : hv(5, p) != 0 ? 1 : hv(2, p) <= 0 ? 2 : -1;
         if (segs[p].cap > 0 && n <= 65535 && packed <= segs[p].cap && hv(5, p) == 0 && hv(2, p) > 0 && m >= 2) {
             // this problem's rows and referenced nodes (compact indices: node order)
             const double* nd = need + 3 * segs[p].need_off;
@@ -465,6 +467,7 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
                 return true;
             });
             o.restricted_rows = packed;
+            o.why = r == -1 ? 3 : r == 0 ? 4 : -1;
             if (r == 1) {
                 std::vector<Vec3> path;
                 for (int v = 1; v >= 0; v = ss.prev_of(v)) path.push_back(pos(v));
@@ -608,6 +611,7 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
         stats_.rows_downloaded += o.rows_down;
         stats_.restricted_rows += o.restricted_rows;
         stats_.fallbacks += o.fallback;
+        if (o.fallback && o.why >= 0) ++stats_.fallback_why[o.why];
         stats_.ms_device += o.ms_dev;
         stats_.ms_search += o.ms_search;
     }

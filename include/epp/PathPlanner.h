@@ -33,6 +33,9 @@ struct PlannerStats {
     int64_t rows_downloaded = 0;  // k-NN table rows copied to the host (see planPath)
     int64_t restricted_rows = 0;  // of which packed rows of the row-restricted searches
     int64_t fallbacks = 0;        // searches that took the whole table after the restricted rows
+    // why (diagnostics): [0] rows past the capacity or > 65,535 nodes, [1] an inexact row,
+    // [2] no kept edge into the goal, [3] a pop above the bound, [4] exhausted in the rows
+    int64_t fallback_why[5] = {0, 0, 0, 0, 0};
     double ms = 0;         // wall time of the last planPath
     double ms_device = 0;  // of which: sampling, checks, k-NN, transfers (GPU phases)
     double ms_search = 0;  // of which: graph build + A* + shortcut on the host

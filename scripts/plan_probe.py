@@ -48,6 +48,8 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
                                    f"fallbacks {st[i]['fallbacks']})"
                                    for i in order), flush=True)
     print("   fallbacks per call:", [s["fallbacks"] for s in st], "mean", np.mean([s["fallbacks"] for s in st]))
+    print("   fallback reasons [capacity, inexact row, no goal edge, pop above bound, exhausted]:",
+          np.sum([s.get("fallback_why", [0] * 5) for s in st], 0).tolist())
     print(f"   planner phases p50 (ms): batch {np.median([s['ms_batch'] for s in st]):.3f} (enqueued by "
           f"{np.median([s.get('ms_enqueue', float('nan')) for s in st]):.3f}) solve "
           f"{np.median([s['ms_solve'] for s in st]):.3f} shortcut {np.median([s['ms_shortcut'] for s in st]):.3f}; "
