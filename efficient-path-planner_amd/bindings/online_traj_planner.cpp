@@ -228,6 +228,10 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["restricted_rows"] = s.restricted_rows;
             d["fallbacks"] = s.fallbacks;
             d["fallback_why"] = std::vector<int64_t>(s.fallback_why, s.fallback_why + 5);
+            d["astar_pops"] = s.astar_pops;
+            d["restricted_nodes"] = s.restricted_nodes;
+            d["ms_restricted_max"] = s.ms_restricted_max;
+            d["ms_copy_of_max"] = s.ms_copy_of_max;
             d["ms_batch"] = s.ms_batch;
             d["ms_enqueue"] = s.ms_enqueue;
             d["ms_solve"] = s.ms_solve;
@@ -398,6 +402,10 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["restricted_rows"] = s.restricted_rows;
             d["fallbacks"] = s.fallbacks;
             d["fallback_why"] = std::vector<int64_t>(s.fallback_why, s.fallback_why + 5);
+            d["astar_pops"] = s.astar_pops;
+            d["restricted_nodes"] = s.restricted_nodes;
+            d["ms_restricted_max"] = s.ms_restricted_max;
+            d["ms_copy_of_max"] = s.ms_copy_of_max;
             d["ms_batch"] = s.ms_batch;
             d["ms_enqueue"] = s.ms_enqueue;
             d["ms_solve"] = s.ms_solve;

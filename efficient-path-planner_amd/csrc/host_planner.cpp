@@ -259,6 +259,7 @@ struct SearchState {
     std::vector<uint32_t> seen, done;  // stamps: dist/prev valid, closed
     std::vector<QE> heap;
     uint32_t cur = 0;
+    int64_t pops = 0;  // (diagnostics: nodes closed by the last search)
     void begin(size_t n) {
         if (dist.size() < n) {
             dist.resize(n);
@@ -284,6 +285,7 @@ struct SearchState {
 template <class Pos, class Key, class Expand>
 int astar(SearchState& ss, size_t nv, Pos&& pos, Key&& key, Expand&& expand) {
     ss.begin(nv);
+    ss.pops = 0;
     const QECmp cmp;
     std::vector<QE>& q = ss.heap;
     const Vec3 gp = pos(1);
@@ -301,6 +303,7 @@ int astar(SearchState& ss, size_t nv, Pos&& pos, Key&& key, Expand&& expand) {
         q.pop_back();
         const int u = top.v;
         if (ss.done[u] == ss.cur) continue;
+        ++ss.pops;
         const Vec3 pu = pos(u);
         auto relax = [&](int v) {
             if (ss.done[v] == ss.cur) return;
@@ -433,6 +436,9 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
         int fallback = 0;  // 1: the whole table after the restricted rows could not decide
         int why = -1;      // (PlannerStats::fallback_why)
         double ms_dev = 0, ms_search = 0;
+        double ms_restricted = 0;  // the restricted search alone (row_of + A*)
+        double ms_copy = 0;        // (of which: the copy out of pinned memory)
+        int64_t pops = 0, nodes = 0;
     };
     std::vector<Out> res(S);
     std::vector<std::vector<Vec3>> raw(S);
@@ -450,23 +456,37 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
         // ids in u16; start and goal are compact indices 0 and 1: rows of their own)
         if (segs[p].cap > 0) o.why = (n > 65535 || packed > segs[p].cap || m < 2) ? 0 : hv(5, p) != 0 ? 1 : hv(2, p) <= 0 ? 2 : -1;
         if (segs[p].cap > 0 && n <= 65535 && packed <= segs[p].cap && hv(5, p) == 0 && hv(2, p) > 0 && m >= 2) {
-            // this problem's rows and referenced nodes (compact indices: node order)
-            const double* nd = need + 3 * segs[p].need_off;
+            // this problem's rows and referenced nodes (compact indices: node order), copied
+            // out of the pinned buffer first: the device wrote them, so they are in no CPU
+            // cache, and A*'s scattered reads would each wait out a DRAM access (~70 ns; the
+            // slowest search of a call took 0.15 ms for ~130 pops), where one sequential copy
+            // streams them in
+            const int64_t nrow = first[p + 1] - first[p];
+            thread_local std::vector<double> ndc;
+            thread_local std::vector<uint16_t> rowc;
+            ndc.resize((size_t)m * 3);
+            rowc.resize((size_t)nrow * k);
+            std::memcpy(ndc.data(), need + 3 * segs[p].need_off, (size_t)m * 24);
+            std::memcpy(rowc.data(), rows + (size_t)first[p] * k, (size_t)nrow * k * 2);
+            o.ms_copy = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            const double* nd = ndc.data();
             thread_local std::vector<int32_t> row_of;
             row_of.assign((size_t)m, -1);
-            for (int64_t sl = first[p]; sl < first[p + 1]; ++sl) row_of[slots[sl] & 0xFFFFu] = (int32_t)sl;
+            for (int64_t sl = first[p]; sl < first[p + 1]; ++sl) row_of[slots[sl] & 0xFFFFu] = (int32_t)(sl - first[p]);
             thread_local SearchState ss;
             const double bound = segs[p].bound;
             auto pos = [&](int v) { return Vec3(nd[3 * v], nd[3 * v + 1], nd[3 * v + 2]); };
             auto key = [](int v) { return v; };  // (compact indices keep the node order)
             r = astar(ss, (size_t)m, pos, key, [&](int u, double f, auto&& relax, bool closing) {
                 if (!closing) return (f <= bound) && row_of[u] >= 0;
-                const uint16_t* row = rows + (size_t)row_of[u] * k;
+                const uint16_t* row = rowc.data() + (size_t)row_of[u] * k;
                 for (int c = 0; c < k; ++c)
                     if (row[c] != 0xFFFF) relax((int)row[c]);
                 return true;
             });
             o.restricted_rows = packed;
+            o.pops = ss.pops;
+            o.nodes = m;
             o.why = r == -1 ? 3 : r == 0 ? 4 : -1;
             if (r == 1) {
                 std::vector<Vec3> path;
@@ -479,7 +499,8 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
                 o.rows_down = packed;
             }
         }
-        o.ms_search += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        o.ms_restricted = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        o.ms_search += o.ms_restricted;
         if (r != 1) {
             o.fallback = segs[p].cap > 0 ? 1 : 0;
             const double* d_nodes = reinterpret_cast<const double*>(dev + L.o_nodes) + (size_t)p * L.NS * 3;
@@ -612,6 +633,12 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
         stats_.restricted_rows += o.restricted_rows;
         stats_.fallbacks += o.fallback;
         if (o.fallback && o.why >= 0) ++stats_.fallback_why[o.why];
+        stats_.astar_pops += o.pops;
+        stats_.restricted_nodes += o.nodes;
+        if (o.ms_restricted > stats_.ms_restricted_max) {
+            stats_.ms_restricted_max = o.ms_restricted;
+            stats_.ms_copy_of_max = o.ms_copy;
+        }
         stats_.ms_device += o.ms_dev;
         stats_.ms_search += o.ms_search;
     }

@@ -36,6 +36,9 @@ struct PlannerStats {
     // why (diagnostics): [0] rows past the capacity or > 65,535 nodes, [1] an inexact row,
     // [2] no kept edge into the goal, [3] a pop above the bound, [4] exhausted in the rows
     int64_t fallback_why[5] = {0, 0, 0, 0, 0};
+    int64_t astar_pops = 0, restricted_nodes = 0;  // (diagnostics) the restricted searches' closed nodes / node lists
+    double ms_restricted_max = 0;                  // (diagnostics) the slowest problem's restricted search
+    double ms_copy_of_max = 0;                     // (diagnostics) of which its copy out of pinned memory
     double ms = 0;         // wall time of the last planPath
     double ms_device = 0;  // of which: sampling, checks, k-NN, transfers (GPU phases)
     double ms_search = 0;  // of which: graph build + A* + shortcut on the host

@@ -48,6 +48,10 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
                                    f"fallbacks {st[i]['fallbacks']})"
                                    for i in order), flush=True)
     print("   fallbacks per call:", [s["fallbacks"] for s in st], "mean", np.mean([s["fallbacks"] for s in st]))
+    print("   restricted searches per call p50: pops", np.median([s.get("astar_pops", 0) for s in st]), "nodes",
+          np.median([s.get("restricted_nodes", 0) for s in st]), "slowest problem (ms)",
+          np.median([s.get("ms_restricted_max", 0) for s in st]), "its copy (ms)",
+          np.median([s.get("ms_copy_of_max", 0) for s in st]))
     print("   fallback reasons [capacity, inexact row, no goal edge, pop above bound, exhausted]:",
           np.sum([s.get("fallback_why", [0] * 5) for s in st], 0).tolist())
     print(f"   planner phases p50 (ms): batch {np.median([s['ms_batch'] for s in st]):.3f} (enqueued by "
