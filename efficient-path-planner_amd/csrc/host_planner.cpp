@@ -261,11 +261,14 @@ struct SearchState {
     uint32_t cur = 0;
     int64_t pops = 0;  // (diagnostics: nodes closed by the last search)
     void begin(size_t n) {
-        if (dist.size() < n) {
-            dist.resize(n);
-            prev.resize(n);
-            seen.resize(n, 0u);
-            done.resize(n, 0u);
+        if (dist.size() < n) {  // (grown with room to spare, the heap's storage reserved: a
+                                // thread's first searches pay the page faults, not later ones)
+            const size_t c = std::max<size_t>(n, std::max<size_t>(2 * dist.size(), 16384));
+            dist.resize(c);
+            prev.resize(c);
+            seen.resize(c, 0u);
+            done.resize(c, 0u);
+            heap.reserve(16 * c);
         }
         if (++cur == 0u) {  // (stamp wrap-around: clear once)
             std::fill(seen.begin(), seen.end(), 0u);
@@ -464,14 +467,18 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
             const int64_t nrow = first[p + 1] - first[p];
             thread_local std::vector<double> ndc;
             thread_local std::vector<uint16_t> rowc;
-            ndc.resize((size_t)m * 3);
-            rowc.resize((size_t)nrow * k);
+            auto grow = [](auto& v, size_t need) {  // (room to spare: see SearchState::begin)
+                if (v.size() < need) v.resize(std::max<size_t>(need, std::max<size_t>(2 * v.size(), 16384 * 16)));
+            };
+            grow(ndc, (size_t)m * 3);
+            grow(rowc, (size_t)nrow * k);
             std::memcpy(ndc.data(), need + 3 * segs[p].need_off, (size_t)m * 24);
             std::memcpy(rowc.data(), rows + (size_t)first[p] * k, (size_t)nrow * k * 2);
             o.ms_copy = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             const double* nd = ndc.data();
             thread_local std::vector<int32_t> row_of;
-            row_of.assign((size_t)m, -1);
+            grow(row_of, (size_t)m);
+            std::fill(row_of.begin(), row_of.begin() + m, -1);
             for (int64_t sl = first[p]; sl < first[p + 1]; ++sl) row_of[slots[sl] & 0xFFFFu] = (int32_t)(sl - first[p]);
             thread_local SearchState ss;
             const double bound = segs[p].bound;
