@@ -6,6 +6,7 @@
 // follows; planning and the min-snap refit run on the GPU (PathPlanner,
 // poly_traj::generateTrajectory).
 #include <chrono>
+#include <cstdio>
 #include <cmath>
 #include <iostream>
 #include <limits>
@@ -134,14 +135,38 @@ void OnlineTrajGenerator::preComputeTraj(double takeoffTime) {
     for (size_t i = 0; i + 1 < checkpoints.size(); i += 2) problems.emplace_back(checkpoints[i], checkpoints[i + 1]);
     std::vector<std::vector<Vec3>> paths;
     std::vector<char> ok;
+    // (EPP_PRECOMPUTE_TRACE=1, diagnostics: the phases' times to stderr, one line per call)
+    static const bool trace = [] {
+        const char* e = std::getenv("EPP_PRECOMPUTE_TRACE");
+        return e && std::atoi(e) == 1;
+    }();
+    const auto t0 = std::chrono::steady_clock::now();
     pathPlanner.planPaths(problems, timeLimit, paths, ok);
     for (size_t s = 0; s < problems.size(); ++s) {
         if (!ok[s]) throw std::runtime_error("Path not found");
         pathSegments.push_back(paths[s]);
     }
+    const auto t1 = std::chrono::steady_clock::now();
     const std::vector<Vec3> pruned = pathPlanner.includeGates2(pathSegments);
-    pathWriter.writePath(pruned);
-    Matrix traj = generate(pruned, takeoffTime, Vec3(0, 0, 0), Vec3(0, 0, 0));
+    const auto t2 = std::chrono::steady_clock::now();
+    // the path file is written on the writer's thread while the trajectory is fitted; both
+    // are done before the call returns (src/OnlineTrajGenerator.cpp:90-93 in sequence)
+    pathWriter.writePathAsync(pruned);
+    const auto t3 = std::chrono::steady_clock::now();
+    Matrix traj;
+    try {
+        traj = generate(pruned, takeoffTime, Vec3(0, 0, 0), Vec3(0, 0, 0));
+    } catch (...) {
+        pathWriter.wait();
+        throw;
+    }
+    pathWriter.wait();
+    if (trace) {
+        const auto t4 = std::chrono::steady_clock::now();
+        auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        std::fprintf(stderr, "precompute_trace: plan=%.0f gates=%.0f write=%.0f generate=%.0f\n", us(t0, t1), us(t1, t2),
+                     us(t2, t3), us(t3, t4));
+    }
     std::lock_guard<std::mutex> lk(trajMu);
     plannedTraj = std::move(traj);
     waypoints = pruned;
