@@ -644,7 +644,7 @@ def run_native(argv, via, timeout=120):
         return {"error": f"{type(e).__name__}: {e}", "via": via}
 
 
-C5_EVENT_TRACKS = 8
+C5_EVENT_TRACKS = 24  # 192 events: ~50 replans, so the replan class has a p99 worth the name
 
 
 def c5_events(cfg_path, geom, gates, obstacles, n_tracks=C5_EVENT_TRACKS, cpu_threads=None):
