@@ -85,6 +85,13 @@ struct MotionMask {
     // rowmap[r], and only rows r < *rows_n are checked
     const int32_t* rowmap = nullptr;
     const unsigned long long* rows_n = nullptr;
+    // the planner batch (rows of several problems, node ids p << ns_log | node): mark[row's
+    // node] and mark[each kept entry] = 1; per problem p the kept edges (pkept[p]) and those
+    // into its node 1, the goal (pgoal[p]); nprob <= 64
+    uint8_t* mark = nullptr;
+    unsigned long long* pkept = nullptr;
+    unsigned long long* pgoal = nullptr;
+    int32_t ns_log = 0, nprob = 0;
 };
 // epp_check_knn_motions (mode 0) with the mask above; EPP_ERR_UNSUPPORTED as it (the
 // caller then masks with mask_edges_count_acc).
@@ -116,9 +123,11 @@ epp_status knn_ws_box_ellipse(const double* nodes, int32_t n, int32_t k, const d
 // check_knn_motions_masked over the packed rows: rows32 (cap rows x k, row r = node
 // ids32[r]), rows r < min(*rows_n, cap) only; EPP_ERR_UNSUPPORTED for worlds without tile
 // tables.  count == nullptr: the mask and out16 only (out16 = the entry's low 16 bits).
+// marks (optional): its mark / pkept / pgoal / ns_log / nprob fields (the planner batch).
 epp_status check_knn_motions_rows(const epp_world* world, const double* nodes, int32_t* rows32, const int32_t* ids32,
                                   const int64_t* rows_n, int32_t cap, int32_t k, int32_t can_pass_gate,
-                                  uint8_t* valid, uint16_t* out16, int32_t target, int64_t* count, void* stream);
+                                  uint8_t* valid, uint16_t* out16, int32_t target, int64_t* count, void* stream,
+                                  const MotionMask* marks = nullptr);
 
 // ---- the batched planner (PathPlanner::planPaths): a batch of gate-to-gate problems, one
 // launch per device stage with blockIdx.y = the problem (planner.hip, plan_batch_launch).

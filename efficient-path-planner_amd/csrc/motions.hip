@@ -509,6 +509,15 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
     const float sof[3] = {wv->sofx, wv->sofy, wv->sofz}, sinv[3] = {wv->six, wv->siy, wv->siz};
     const double rg = wv->r_gate, ro = wv->r_obst;
     const bool cp = can_pass != 0;
+    // (the planner batch's per-problem counts: kept edges, those into the goal)
+    [[maybe_unused]] uint32_t* s_pk = nullptr;
+    [[maybe_unused]] uint32_t* s_pg = nullptr;
+    if constexpr (IDX) {
+        __shared__ uint32_t s_pcnt[2][64];
+        s_pk = s_pcnt[0];
+        s_pg = s_pcnt[1];
+        if (mm.mark && threadIdx.x < 64) s_pk[threadIdx.x] = s_pg[threadIdx.x] = 0u;
+    }
     __syncthreads();
 #ifdef EPP_MOTIONS_TL
     tl_c = __builtin_readcyclecounter() - tl_t0;  // staging
@@ -751,8 +760,27 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
             if (act && mm.out16) mm.out16[i] = keep ? (uint16_t)jraw : (uint16_t)0xFFFF;
             mk_keep += keep ? 1u : 0u;
             mk_tgt += (keep && jraw == mm.target) ? 1u : 0u;
+            if (mm.mark && act) {  // (launch-uniform) the planner batch's marks and counts
+                const int32_t u = mm.rowmap[i / kk];
+                if (i % kk == 0) mm.mark[u] = 1;
+                if (keep) {
+                    mm.mark[jraw] = 1;
+                    const int pb = u >> mm.ns_log;
+                    atomicAdd(&s_pk[pb], 1u);
+                    if ((jraw & ((1 << mm.ns_log) - 1)) == 1) atomicAdd(&s_pg[pb], 1u);
+                }
+            }
         }
         wave_lds_sync();
+    }
+    if constexpr (IDX) {
+        if (mm.mark) {  // (launch-uniform) one atomic per workgroup, problem and counter
+            __syncthreads();
+            if ((int)threadIdx.x < mm.nprob) {
+                if (s_pk[threadIdx.x]) atomicAdd(mm.pkept + threadIdx.x, (unsigned long long)s_pk[threadIdx.x]);
+                if (s_pg[threadIdx.x]) atomicAdd(mm.pgoal + threadIdx.x, (unsigned long long)s_pg[threadIdx.x]);
+            }
+        }
     }
     if (IDX && mm.count) {  // one atomic per workgroup and counter
         __shared__ uint32_t mk_part[2][BLOCK / 64];
@@ -961,8 +989,9 @@ epp_status epp::check_knn_motions_masked(const epp_world* world, const double* n
 epp_status epp::check_knn_motions_rows(const epp_world* world, const double* nodes, int32_t* rows32,
                                        const int32_t* ids32, const int64_t* rows_n, int32_t cap, int32_t k,
                                        int32_t can_pass_gate, uint8_t* valid, uint16_t* out16, int32_t target,
-                                       int64_t* count, void* stream) {
-    if (!world || cap < 0 || k <= 0 || (cap > 0 && (!nodes || !rows32 || !ids32 || !rows_n || !valid || (!count && !out16)))) {
+                                       int64_t* count, void* stream, const MotionMask* marks) {
+    if (!world || cap < 0 || k <= 0 || (cap > 0 && (!nodes || !rows32 || !ids32 || !rows_n || !valid || (!count && !out16))) ||
+        (marks && marks->mark && (!out16 || !marks->pkept || !marks->pgoal || marks->nprob < 1 || marks->nprob > 64))) {
         set_error("check_knn_motions_rows: invalid argument");
         return EPP_ERR_INVALID_ARGUMENT;
     }
@@ -977,6 +1006,13 @@ epp_status epp::check_knn_motions_rows(const epp_world* world, const double* nod
     mm.count = reinterpret_cast<unsigned long long*>(count);
     mm.rowmap = ids32;
     mm.rows_n = reinterpret_cast<const unsigned long long*>(rows_n);
+    if (marks) {
+        mm.mark = marks->mark;
+        mm.pkept = marks->pkept;
+        mm.pgoal = marks->pgoal;
+        mm.ns_log = marks->ns_log;
+        mm.nprob = marks->nprob;
+    }
     if (!launch_motions_v5(ix.dview, ix.view, nodes, nullptr, rows32, k, m, can_pass_gate, 0, valid,
                            (hipStream_t)stream, mm)) {
         set_error("check_knn_motions_rows: not for this world");

@@ -2055,7 +2055,6 @@ __device__ __forceinline__ double pb_ellipse(const PlanSeg& q, const double* x) 
 // Per node (problems with restricted rows): inside the grid ellipsoid -> its cell counted
 // (cell_of, else -1); inside the row ellipsoid (widened by 1e-8 relative + 1e-6 m) ->
 // listed as a query (ranks from one atomic per workgroup).
-constexpr int kPbBlock = 1024;
 __device__ __forceinline__ bool pb_member(const PlanBatchDev& P, const PlanSeg& q, const KnnSeg& ks, const KnnGrid& g,
                                           int p, int node, const double* x) {
     const double f = pb_ellipse(q, x);
@@ -2382,34 +2381,6 @@ __global__ __launch_bounds__(64) void k_pb_rows(PlanBatchDev P) {
             if (lane == 0) pb_ctr(P, kFInexact, p) = 1ull;
             if (lane < K) P.rows32[(int64_t)d * K + lane] = -1;  // (the problem takes the whole table)
         }
-    }
-}
-
-// The nodes the rows reference (each row's node and its kept neighbours) marked (byte
-// stores: no atomics); per problem the kept edges of its rows and those into its goal
-// (node 1), summed per workgroup in LDS.
-__global__ __launch_bounds__(kPbBlock) void k_pb_mark(PlanBatchDev P) {
-    __shared__ unsigned int s_k[64], s_g[64];
-    for (int i = threadIdx.x; i < 64; i += kPbBlock) s_k[i] = s_g[i] = 0u;
-    __syncthreads();
-    const int64_t e = (int64_t)blockIdx.x * kPbBlock + threadIdx.x;
-    const int64_t rows = (int64_t)P.ctr[kPbRows];
-    if (e < rows * P.k) {
-        const int64_t r = e / P.k;
-        const int32_t u = P.ids32[r];
-        const int p = u >> P.ns_log;
-        const uint16_t v = P.rows16[e];
-        if (e == r * P.k) P.mark[u] = 1;
-        if (v != 0xFFFF) {
-            P.mark[((int64_t)p << P.ns_log) + v] = 1;
-            atomicAdd(&s_k[p], 1u);
-            if (v == 1) atomicAdd(&s_g[p], 1u);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < P.S && s_k[threadIdx.x]) {
-        atomicAdd(&pb_ctr(P, kFKept, threadIdx.x), (unsigned long long)s_k[threadIdx.x]);
-        if (s_g[threadIdx.x]) atomicAdd(&pb_ctr(P, kFGoal, threadIdx.x), (unsigned long long)s_g[threadIdx.x]);
     }
 }
 
@@ -3127,16 +3098,22 @@ epp_status epp::plan_batch_launch(const epp_world* world, int32_t can_pass_gate,
         else if (L.k == 8) hipLaunchKernelGGL(k_pb_rows<8>, gr, br, 0, s, P);
         else hipLaunchKernelGGL(k_pb_rows<16>, gr, br, 0, s, P);
         pb_mark(s, "rows");
+        // the motions, with the marks of the referenced nodes and the per-problem kept /
+        // goal edge counts folded into the launch
+        MotionMask marks;
+        marks.mark = P.mark;
+        marks.pkept = P.ctr + kPbPerSeg + kFKept * L.S;
+        marks.pgoal = P.ctr + kPbPerSeg + kFGoal * L.S;
+        marks.ns_log = L.ns_log;
+        marks.nprob = L.S;
         if (const epp_status st = check_knn_motions_rows(
                 world, P.nodes, P.rows32, P.ids32, reinterpret_cast<const int64_t*>(P.ctr + kPbRows), L.cap_total,
-                L.k, can_pass_gate, reinterpret_cast<uint8_t*>(d + L.o_ev), P.rows16, -1, nullptr, stream))
+                L.k, can_pass_gate, reinterpret_cast<uint8_t*>(d + L.o_ev), P.rows16, -1, nullptr, stream, &marks))
             return st;
-        pb_mark(s, "motions");
-        const int64_t ents = (int64_t)L.cap_total * L.k;
-        hipLaunchKernelGGL(k_pb_mark, dim3((unsigned)((ents + kPbBlock - 1) / kPbBlock)), dim3(kPbBlock), 0, s, P);
+        pb_mark(s, "motions_marks");
         hipLaunchKernelGGL(k_pb_number, dim3((unsigned)((L.ns + 2 + kCompactChunk - 1) / kCompactChunk), S),
                            dim3(kCompactThreads), 0, s, P, next_scan_tag());
-        pb_mark(s, "mark_number");
+        pb_mark(s, "number");
     }
     hipLaunchKernelGGL(k_pb_emit, dim3((unsigned)L.done_n), dim3(256), 0, s, P,
                        reinterpret_cast<unsigned long long*>(h + L.h_hdr), reinterpret_cast<uint4*>(h + L.h_slot),
