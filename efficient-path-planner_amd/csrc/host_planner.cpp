@@ -467,17 +467,17 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
             const int64_t nrow = first[p + 1] - first[p];
             thread_local std::vector<double> ndc;
             thread_local std::vector<uint16_t> rowc;
-            auto grow = [](auto& v, size_t need) {  // (room to spare: see SearchState::begin)
-                if (v.size() < need) v.resize(std::max<size_t>(need, std::max<size_t>(2 * v.size(), 16384 * 16)));
+            auto grow = [](auto& v, size_t need, size_t init) {  // (room to spare: see SearchState::begin)
+                if (v.size() < need) v.resize(std::max<size_t>(need, std::max<size_t>(2 * v.size(), init)));
             };
-            grow(ndc, (size_t)m * 3);
-            grow(rowc, (size_t)nrow * k);
+            grow(ndc, (size_t)m * 3, 3 * 16384);
+            grow(rowc, (size_t)nrow * k, (size_t)16384 * k);
             std::memcpy(ndc.data(), need + 3 * segs[p].need_off, (size_t)m * 24);
             std::memcpy(rowc.data(), rows + (size_t)first[p] * k, (size_t)nrow * k * 2);
             o.ms_copy = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             const double* nd = ndc.data();
             thread_local std::vector<int32_t> row_of;
-            grow(row_of, (size_t)m);
+            grow(row_of, (size_t)m, 16384);
             std::fill(row_of.begin(), row_of.begin() + m, -1);
             for (int64_t sl = first[p]; sl < first[p + 1]; ++sl) row_of[slots[sl] & 0xFFFFu] = (int32_t)(sl - first[p]);
             thread_local SearchState ss;

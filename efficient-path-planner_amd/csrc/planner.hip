@@ -3093,7 +3093,12 @@ epp_status epp::plan_batch_launch(const epp_world* world, int32_t can_pass_gate,
         // one wave per workgroup, 28 per CU (16 resident at 103 VGPRs; a variant with four
         // queries per wave, 16 lanes each, was 1.9x slower: its 16-lane shuffles and LDS
         // ranking cost more issue than the overlapped loads saved)
-        const dim3 gr((unsigned)std::max(1, cu_count_planner() * 28)), br(64);
+        static const int rows_wg = [] {  // (A/B knob: one-wave workgroups per CU)
+            const char* e = std::getenv("EPP_PB_ROWS_WG");
+            const int v = e && *e ? std::atoi(e) : 28;
+            return std::max(1, std::min(64, v));
+        }();
+        const dim3 gr((unsigned)std::max(1, cu_count_planner() * rows_wg)), br(64);
         if (L.k == 4) hipLaunchKernelGGL(k_pb_rows<4>, gr, br, 0, s, P);
         else if (L.k == 8) hipLaunchKernelGGL(k_pb_rows<8>, gr, br, 0, s, P);
         else hipLaunchKernelGGL(k_pb_rows<16>, gr, br, 0, s, P);
