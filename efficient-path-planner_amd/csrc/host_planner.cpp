@@ -280,6 +280,31 @@ struct SearchState {
     int prev_of(int v) const { return seen[v] == cur ? prev[v] : -1; }
 };
 
+// A planner thread's buffers of the restricted search (grown with room to spare; warmed
+// once per thread, before its first problem: a thread whose first problem came in a timed
+// call paid the page faults there -- the second plan of a generator took ~2x).
+struct SolveScratch {
+    std::vector<double> ndc;      // the problem's referenced nodes (a private copy)
+    std::vector<uint16_t> rowc;   // its rows (a private copy)
+    std::vector<int32_t> row_of;  // compact node -> row
+    SearchState ss;
+    bool warm = false;
+    static SolveScratch& get() {
+        thread_local SolveScratch s;
+        return s;
+    }
+    void warmup(int k) {
+        if (warm) return;
+        warm = true;
+        ndc.assign(3 * 16384, 0.0);
+        rowc.assign((size_t)16384 * k, 0);
+        row_of.assign(16384, -1);
+        ss.begin(16384);
+        ss.heap.resize(ss.heap.capacity() / 4);  // (touch part of the heap's storage)
+        ss.heap.clear();
+    }
+};
+
 // A* from node 0 to node 1 with the Euclidean distance to the goal (admissible and
 // consistent for Euclidean edge costs).  pos(v): coordinates; key(v): the node id that
 // breaks ties; expand(u, f, relax) calls relax(v) for u's edges and returns false to abort
@@ -465,8 +490,9 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
             // slowest search of a call took 0.15 ms for ~130 pops), where one sequential copy
             // streams them in
             const int64_t nrow = first[p + 1] - first[p];
-            thread_local std::vector<double> ndc;
-            thread_local std::vector<uint16_t> rowc;
+            SolveScratch& sc = SolveScratch::get();
+            std::vector<double>& ndc = sc.ndc;
+            std::vector<uint16_t>& rowc = sc.rowc;
             auto grow = [](auto& v, size_t need, size_t init) {  // (room to spare: see SearchState::begin)
                 if (v.size() < need) v.resize(std::max<size_t>(need, std::max<size_t>(2 * v.size(), init)));
             };
@@ -476,11 +502,11 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
             std::memcpy(rowc.data(), rows + (size_t)first[p] * k, (size_t)nrow * k * 2);
             o.ms_copy = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             const double* nd = ndc.data();
-            thread_local std::vector<int32_t> row_of;
+            std::vector<int32_t>& row_of = sc.row_of;
             grow(row_of, (size_t)m, 16384);
             std::fill(row_of.begin(), row_of.begin() + m, -1);
             for (int64_t sl = first[p]; sl < first[p + 1]; ++sl) row_of[slots[sl] & 0xFFFFu] = (int32_t)(sl - first[p]);
-            thread_local SearchState ss;
+            SearchState& ss = sc.ss;
             const double bound = segs[p].bound;
             auto pos = [&](int v) { return Vec3(nd[3 * v], nd[3 * v + 1], nd[3 * v + 2]); };
             auto key = [](int v) { return v; };  // (compact indices keep the node order)
@@ -531,6 +557,7 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
     std::atomic<int> go{0};
     std::atomic<int> next{0};
     auto drain = [&](size_t w) {
+        SolveScratch::get().warmup(k);
         for (int p = next++; p < S; p = next++) run(p, w);
     };
     std::mutex done_mu;

@@ -42,7 +42,8 @@ public:
     // by `carve` until the next reset().
     void reset(size_t bytes) {
         bytes = (bytes + 255) & ~size_t(255);
-        if (bytes > cap_) {
+        if (bytes > cap_) {  // (x2, at least 4 MB: freeing device memory synchronises the device)
+            bytes = std::max(bytes, std::max<size_t>(2 * cap_, size_t(4) << 20));
             if (buf_) epp_free(buf_);
             buf_ = nullptr;
             cap_ = 0;
@@ -61,10 +62,13 @@ public:
     static size_t rounded(size_t bytes) { return (bytes + 255) & ~size_t(255); }
     // Pinned (page-locked) host staging of at least `bytes`, slot 0, 1 or 2: device-to-host
     // copies into it run at DMA speed instead of through a pageable bounce buffer.
-    // Grows geometrically (x1.5): reallocating pinned memory synchronises the device.
+    // Grows geometrically (x1.5) from 1 MB -- what the zero-copy path of a World query needs
+    // at its largest (16,384 rays: 2 x 384 KB + 16 KB), so that path never reallocates:
+    // reallocating pinned memory takes ~0.3 ms and synchronises the device (the second plan
+    // of a generator paid it in its shortcut's checks).
     void* pinned(int slot, size_t bytes) {
         if (bytes > pcap_[slot]) {
-            bytes = std::max(bytes, pcap_[slot] + pcap_[slot] / 2);
+            bytes = std::max(bytes, std::max<size_t>(pcap_[slot] + pcap_[slot] / 2, size_t(1) << 20));
             if (pin_[slot]) (void)hipHostFree(pin_[slot]);
             pin_[slot] = nullptr;
             pcap_[slot] = 0;

@@ -28,7 +28,8 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
     gates, obstacles = synth.track_world(100)
     cps = synth.gate_checkpoints(gates, geom.gate_height, 0.55)
     otg = otp.OnlineTrajGenerator(cps[0], cps[-1], gates, obstacles, path)
-    otg.pre_compute_traj(0.0)
+    for _ in range(int(os.environ.get("EPP_PROBE_WARM", "1"))):  # untimed calls first
+        otg.pre_compute_traj(0.0)
     ts, st = [], []
     for _ in range(int(os.environ.get('EPP_PROBE_CALLS', '30'))):
         t = time.perf_counter()
