@@ -227,7 +227,8 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["rows_downloaded"] = s.rows_downloaded;
             d["restricted_rows"] = s.restricted_rows;
             d["fallbacks"] = s.fallbacks;
-            d["fallback_why"] = std::vector<int64_t>(s.fallback_why, s.fallback_why + 5);
+            d["fallback_why"] = std::vector<int64_t>(s.fallback_why, s.fallback_why + 7);
+            d["restricted_symmetrised"] = s.restricted_symmetrised;
             d["astar_pops"] = s.astar_pops;
             d["restricted_nodes"] = s.restricted_nodes;
             d["ms_restricted_max"] = s.ms_restricted_max;
@@ -401,7 +402,8 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["rows_downloaded"] = s.rows_downloaded;
             d["restricted_rows"] = s.restricted_rows;
             d["fallbacks"] = s.fallbacks;
-            d["fallback_why"] = std::vector<int64_t>(s.fallback_why, s.fallback_why + 5);
+            d["fallback_why"] = std::vector<int64_t>(s.fallback_why, s.fallback_why + 7);
+            d["restricted_symmetrised"] = s.restricted_symmetrised;
             d["astar_pops"] = s.astar_pops;
             d["restricted_nodes"] = s.restricted_nodes;
             d["ms_restricted_max"] = s.ms_restricted_max;

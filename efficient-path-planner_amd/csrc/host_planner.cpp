@@ -287,6 +287,7 @@ struct SolveScratch {
     std::vector<double> ndc;      // the problem's referenced nodes (a private copy)
     std::vector<uint16_t> rowc;   // its rows (a private copy)
     std::vector<int32_t> row_of;  // compact node -> row
+    std::vector<int32_t> roff, radj, rfill;  // the rows' reverse edges (symmetrised search)
     SearchState ss;
     bool warm = false;
     static SolveScratch& get() {
@@ -467,6 +468,7 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
         double ms_restricted = 0;  // the restricted search alone (row_of + A*)
         double ms_copy = 0;        // (of which: the copy out of pinned memory)
         int64_t pops = 0, nodes = 0;
+        int symmetrised = 0;       // the restricted rows decided the symmetrised search
     };
     std::vector<Out> res(S);
     std::vector<std::vector<Vec3>> raw(S);
@@ -480,10 +482,10 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
         const int64_t m = std::min<int64_t>(hv(4, p), segs[p].need_cap);
         const auto t0 = std::chrono::steady_clock::now();
         int r = 0;
-        // (restricted: rows within capacity, exact (hv 5), a kept edge into the goal, node
-        // ids in u16; start and goal are compact indices 0 and 1: rows of their own)
-        if (segs[p].cap > 0) o.why = (n > 65535 || packed > segs[p].cap || m < 2) ? 0 : hv(5, p) != 0 ? 1 : hv(2, p) <= 0 ? 2 : -1;
-        if (segs[p].cap > 0 && n <= 65535 && packed <= segs[p].cap && hv(5, p) == 0 && hv(2, p) > 0 && m >= 2) {
+        // (restricted: rows within capacity, exact (hv 5), node ids in u16; start and goal are
+        // compact indices 0 and 1: rows of their own)
+        if (segs[p].cap > 0) o.why = (n > 65535 || packed > segs[p].cap || m < 2) ? 0 : hv(5, p) != 0 ? 1 : -1;
+        if (segs[p].cap > 0 && n <= 65535 && packed <= segs[p].cap && hv(5, p) == 0 && m >= 2) {
             // this problem's rows and referenced nodes (compact indices: node order), copied
             // out of the pinned buffer first: the device wrote them, so they are in no CPU
             // cache, and A*'s scattered reads would each wait out a DRAM access (~70 ns; the
@@ -521,6 +523,51 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
             o.pops = ss.pops;
             o.nodes = m;
             o.why = r == -1 ? 3 : r == 0 ? 4 : -1;
+            if (r == 0) {
+                // The forward search exhausted its component with every pop inside the bound:
+                // every node it reached has its row here, so the search over the whole table
+                // reaches the same nodes and fails too (no kept edge into the goal among the
+                // rows is the usual cause).  The reference then searches the symmetrised graph
+                // (wholeTableSearch): a node's edges are its row and the reverse of every row
+                // holding it.  While the pops stay within the bound the reverse edges needed
+                // are those of rows here (a node whose row holds a popped node but is outside
+                // the bound is pushed, with f > bound, and never popped first), so the same
+                // search runs on the rows: reverse edges ascending (compact = node order), as
+                // the reverse CSR gives them.  A pop above the bound or an exhausted search
+                // still takes the whole table.
+                std::vector<int32_t>& roff = sc.roff;
+                std::vector<int32_t>& radj = sc.radj;
+                grow(roff, (size_t)m + 1, 16384);
+                std::fill(roff.begin(), roff.begin() + m + 1, 0);
+                for (int u = 0; u < m; ++u) {
+                    if (row_of[u] < 0) continue;
+                    const uint16_t* row = rowc.data() + (size_t)row_of[u] * k;
+                    for (int c = 0; c < k; ++c)
+                        if (row[c] != 0xFFFF) ++roff[(size_t)row[c] + 1];
+                }
+                for (int64_t v = 0; v < m; ++v) roff[(size_t)v + 1] += roff[(size_t)v];
+                grow(radj, (size_t)roff[(size_t)m], (size_t)16384 * k);
+                std::vector<int32_t>& fill = sc.rfill;
+                grow(fill, (size_t)m, 16384);
+                std::copy(roff.begin(), roff.begin() + m, fill.begin());
+                for (int u = 0; u < m; ++u) {  // (u ascending: every run comes out sorted)
+                    if (row_of[u] < 0) continue;
+                    const uint16_t* row = rowc.data() + (size_t)row_of[u] * k;
+                    for (int c = 0; c < k; ++c)
+                        if (row[c] != 0xFFFF) radj[(size_t)fill[row[c]]++] = u;
+                }
+                r = astar(ss, (size_t)m, pos, key, [&](int u, double f, auto&& relax, bool closing) {
+                    if (!closing) return (f <= bound) && row_of[u] >= 0;
+                    const uint16_t* row = rowc.data() + (size_t)row_of[u] * k;
+                    for (int c = 0; c < k; ++c)
+                        if (row[c] != 0xFFFF) relax((int)row[c]);
+                    for (int32_t q = roff[(size_t)u]; q < roff[(size_t)u + 1]; ++q) relax(radj[(size_t)q]);
+                    return true;
+                });
+                o.pops += ss.pops;
+                o.why = r == -1 ? 5 : r == 0 ? 6 : -1;
+                o.symmetrised = r == 1 ? 1 : 0;
+            }
             if (r == 1) {
                 std::vector<Vec3> path;
                 for (int v = 1; v >= 0; v = ss.prev_of(v)) path.push_back(pos(v));
@@ -668,6 +715,7 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
         stats_.fallbacks += o.fallback;
         if (o.fallback && o.why >= 0) ++stats_.fallback_why[o.why];
         stats_.astar_pops += o.pops;
+        stats_.restricted_symmetrised += o.symmetrised;
         stats_.restricted_nodes += o.nodes;
         if (o.ms_restricted > stats_.ms_restricted_max) {
             stats_.ms_restricted_max = o.ms_restricted;

@@ -34,8 +34,11 @@ struct PlannerStats {
     int64_t restricted_rows = 0;  // of which packed rows of the row-restricted searches
     int64_t fallbacks = 0;        // searches that took the whole table after the restricted rows
     // why (diagnostics): [0] rows past the capacity or > 65,535 nodes, [1] an inexact row,
-    // [2] no kept edge into the goal, [3] a pop above the bound, [4] exhausted in the rows
-    int64_t fallback_why[5] = {0, 0, 0, 0, 0};
+    // [2] (unused since the symmetrised search runs on the rows), [3] a pop above the bound,
+    // [4] (forward exhausted: the symmetrised search follows), [5] symmetrised: a pop above
+    // the bound, [6] symmetrised: exhausted in the rows
+    int64_t fallback_why[7] = {0, 0, 0, 0, 0, 0, 0};
+    int64_t restricted_symmetrised = 0;  // searches the rows' symmetrised graph decided
     int64_t astar_pops = 0, restricted_nodes = 0;  // (diagnostics) the restricted searches' closed nodes / node lists
     double ms_restricted_max = 0;                  // (diagnostics) the slowest problem's restricted search
     double ms_copy_of_max = 0;                     // (diagnostics) of which its copy out of pinned memory

@@ -902,7 +902,9 @@ int or_plan_once(const or_obb* w, int nw, double rg, double ro, const double lo[
         }
         return false;
     };
-    if (!astar(false)) {
+    const bool forward = astar(false);
+    if (stats) stats[4] = forward ? 0 : 1;
+    if (!forward) {
         roff.assign(n + 1, 0);
         for (size_t e = 0; e < m; ++e)
             if (nbr[e] >= 0) ++roff[nbr[e] + 1];

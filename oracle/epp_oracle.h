@@ -125,7 +125,8 @@ void or_random_vertices(int n_segments, int dim, double pos_min, double pos_max,
  * compaction (nodes = start, goal, valid samples), exact k-NN (ties to the lower index),
  * motion checks, A* (forward edges, then symmetrised), greedy shortcut.  Writes the path
  * (<= cap points) and returns its length, 0 if no path, -1 if cap is too small.
- * stats (may be NULL): samples, valid samples, edges, valid edges. */
+ * stats (may be NULL): samples, valid samples, edges, valid edges, 1 if the forward search
+ * failed (the symmetrised search ran). */
 int or_plan_once(const or_obb* w, int nw, double r_gate, double r_obst, const double lo[3], const double hi[3],
                  const double start[3], const double goal[3], int64_t samples, uint64_t seed, int k, int can_pass,
                  int threads, double* path, int cap, int64_t* stats);

@@ -211,12 +211,13 @@ def random_vertices(n_segments, dim, pos_min, pos_max, seed):
 
 def plan_once(w, r_gate, r_obst, lo, hi, start, goal, samples, seed, k=16, can_pass_gate=False, threads=1):
     """CPU restatement of PathPlanner::planOnce (this build's batch planner): the path as an
-    (L, 3) array, or None; plus (samples, valid samples, edges, valid edges)."""
+    (L, 3) array, or None; plus (samples, valid samples, edges, valid edges, 1 if the
+    symmetrised search ran)."""
     lo, hi = np.ascontiguousarray(lo, np.float64), np.ascontiguousarray(hi, np.float64)
     start, goal = np.ascontiguousarray(start, np.float64), np.ascontiguousarray(goal, np.float64)
     cap = 4096
     path = np.zeros((cap, 3))
-    stats = np.zeros(4, np.int64)
+    stats = np.zeros(5, np.int64)
     n = lib().or_plan_once(_p(w), len(w), r_gate, r_obst, _p(lo), _p(hi), _p(start), _p(goal), int(samples),
                            int(seed) & 0xFFFFFFFFFFFFFFFF, int(k), int(bool(can_pass_gate)), int(threads), _p(path),
                            cap, _p(stats))

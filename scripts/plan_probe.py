@@ -53,8 +53,12 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
           np.median([s.get("restricted_nodes", 0) for s in st]), "slowest problem (ms)",
           np.median([s.get("ms_restricted_max", 0) for s in st]), "its copy (ms)",
           np.median([s.get("ms_copy_of_max", 0) for s in st]))
-    print("   fallback reasons [capacity, inexact row, no goal edge, pop above bound, exhausted]:",
-          np.sum([s.get("fallback_why", [0] * 5) for s in st], 0).tolist())
+    print("   fallback reasons [capacity, inexact row, -, pop above bound, -, symmetrised: pop above bound,"
+          " symmetrised: exhausted]:", np.sum([s.get("fallback_why", [0] * 7) for s in st], 0).tolist(),
+          "; symmetrised searches decided on the rows:", sum(s.get("restricted_symmetrised", 0) for s in st))
+    warm = int(os.environ.get("EPP_PROBE_WARM", "1"))
+    print("   planner call numbers of the calls with symmetrised searches decided on the rows:",
+          [9 * (warm + i) for i, s in enumerate(st) if s.get("restricted_symmetrised", 0)], flush=True)
     print(f"   planner phases p50 (ms): batch {np.median([s['ms_batch'] for s in st]):.3f} (enqueued by "
           f"{np.median([s.get('ms_enqueue', float('nan')) for s in st]):.3f}) solve "
           f"{np.median([s['ms_solve'] for s in st]):.3f} shortcut {np.median([s['ms_shortcut'] for s in st]):.3f}; "

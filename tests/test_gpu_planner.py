@@ -723,6 +723,29 @@ def test_plan_once_equals_cpu_restatement(c1, seed, ellipse, monkeypatch):
     assert O.plan_once(w, rg, ro, lo, hi, start, blocked, 4096, seed, 16, False, 4)[0] is None
 
 
+def test_plan_once_symmetrised_on_rows_equals_cpu(c1):
+    """Goals outside the sampling box: no sample keeps the goal among its 16 neighbours, so
+    the forward search exhausts and the symmetrised graph (the goal's own row, reversed)
+    decides.  The planner runs that search on the downloaded rows (host_planner.cpp solve,
+    restricted_symmetrised) instead of the whole table; the path equals the CPU
+    restatement's, whose stats say the symmetrised search ran."""
+    g, o, start, goal, w, rg, ro = c1
+    pp = _ot().PathPlanner(g, o, CONFIG)
+    lo, hi = synth.C1_BOUNDS
+    sym = ran = 0
+    for off, ax in ((0.4, 0), (0.4, 1), (0.8, 2), (0.8, 0)):
+        gl = np.array(goal, float)
+        gl[ax] = hi[ax] + off
+        for samples, seed in ((4096, 0), (4096, 3), (20_000, 1)):
+            s0 = pp.last_stats().get("restricted_symmetrised", 0)
+            got = pp.plan_once(start, gl, samples, seed)
+            exp, st = O.plan_once(w, rg, ro, lo, hi, start, gl, samples, seed, 16, False, 8)
+            assert exp is not None and got is not None and np.array_equal(got, exp), (off, ax, samples, seed)
+            ran += int(st[4])
+            sym += pp.last_stats()["restricted_symmetrised"] - s0
+    assert ran >= 10 and sym >= ran // 2, (ran, sym)
+
+
 @pytest.mark.parametrize("ellipse", ELLIPSE)
 def test_plan_once_equals_cpu_restatement_track(track, geom, ellipse, monkeypatch):
     """Every gate-to-gate segment of the C2 track (65,536 samples, the C4 size) equal on
