@@ -229,6 +229,7 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["fallbacks"] = s.fallbacks;
             d["fallback_why"] = std::vector<int64_t>(s.fallback_why, s.fallback_why + 7);
             d["restricted_symmetrised"] = s.restricted_symmetrised;
+            d["symmetrised_after_census"] = s.symmetrised_after_census;
             d["astar_pops"] = s.astar_pops;
             d["restricted_nodes"] = s.restricted_nodes;
             d["ms_restricted_max"] = s.ms_restricted_max;
@@ -404,6 +405,7 @@ PYBIND11_MODULE(online_traj_planner, m) {
             d["fallbacks"] = s.fallbacks;
             d["fallback_why"] = std::vector<int64_t>(s.fallback_why, s.fallback_why + 7);
             d["restricted_symmetrised"] = s.restricted_symmetrised;
+            d["symmetrised_after_census"] = s.symmetrised_after_census;
             d["astar_pops"] = s.astar_pops;
             d["restricted_nodes"] = s.restricted_nodes;
             d["ms_restricted_max"] = s.ms_restricted_max;

@@ -300,6 +300,9 @@ struct SolveScratch {
         ndc.assign(3 * 16384, 0.0);
         rowc.assign((size_t)16384 * k, 0);
         row_of.assign(16384, -1);
+        roff.assign(16385, 0);  // (the symmetrised search's: rare, but its first use is in a timed plan)
+        rfill.assign(16384, 0);
+        radj.assign((size_t)16384 * k, 0);
         ss.begin(16384);
         ss.heap.resize(ss.heap.capacity() / 4);  // (touch part of the heap's storage)
         ss.heap.clear();
@@ -469,6 +472,7 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
         double ms_copy = 0;        // (of which: the copy out of pinned memory)
         int64_t pops = 0, nodes = 0;
         int symmetrised = 0;       // the restricted rows decided the symmetrised search
+        int census = 0;            // ... after the whole table's k-NN counted the goal's edges
     };
     std::vector<Out> res(S);
     std::vector<std::vector<Vec3>> raw(S);
@@ -523,18 +527,15 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
             o.pops = ss.pops;
             o.nodes = m;
             o.why = r == -1 ? 3 : r == 0 ? 4 : -1;
-            if (r == 0) {
-                // The forward search exhausted its component with every pop inside the bound:
-                // every node it reached has its row here, so the search over the whole table
-                // reaches the same nodes and fails too (no kept edge into the goal among the
-                // rows is the usual cause).  The reference then searches the symmetrised graph
-                // (wholeTableSearch): a node's edges are its row and the reverse of every row
-                // holding it.  While the pops stay within the bound the reverse edges needed
-                // are those of rows here (a node whose row holds a popped node but is outside
-                // the bound is pushed, with f > bound, and never popped first), so the same
-                // search runs on the rows: reverse edges ascending (compact = node order), as
-                // the reverse CSR gives them.  A pop above the bound or an exhausted search
-                // still takes the whole table.
+            // The symmetrised search on the rows.  The reference's next step after a failed
+            // forward search is the symmetrised graph (wholeTableSearch): a node's edges are
+            // its row and the reverse of every row holding it.  While the pops stay within the
+            // bound the reverse edges needed are those of rows here: a node without a row lies
+            // outside the ellipse (|s w| + |w g| > bound), so it is pushed with f > bound and
+            // never popped first.  Reverse edges ascending (compact = node order), as the
+            // device's reverse CSR gives them.  Valid only once the whole table's forward
+            // search is known to fail (below).
+            auto symmetrised = [&]() -> int {
                 std::vector<int32_t>& roff = sc.roff;
                 std::vector<int32_t>& radj = sc.radj;
                 grow(roff, (size_t)m + 1, 16384);
@@ -556,7 +557,7 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
                     for (int c = 0; c < k; ++c)
                         if (row[c] != 0xFFFF) radj[(size_t)fill[row[c]]++] = u;
                 }
-                r = astar(ss, (size_t)m, pos, key, [&](int u, double f, auto&& relax, bool closing) {
+                const int r2 = astar(ss, (size_t)m, pos, key, [&](int u, double f, auto&& relax, bool closing) {
                     if (!closing) return (f <= bound) && row_of[u] >= 0;
                     const uint16_t* row = rowc.data() + (size_t)row_of[u] * k;
                     for (int c = 0; c < k; ++c)
@@ -565,15 +566,54 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
                     return true;
                 });
                 o.pops += ss.pops;
-                o.why = r == -1 ? 5 : r == 0 ? 6 : -1;
-                o.symmetrised = r == 1 ? 1 : 0;
-            }
-            if (r == 1) {
+                o.why = r2 == -1 ? 5 : r2 == 0 ? 6 : -1;
+                o.symmetrised = r2 == 1 ? 1 : 0;
+                return r2;
+            };
+            auto take_path = [&]() {
                 std::vector<Vec3> path;
                 for (int v = 1; v >= 0; v = ss.prev_of(v)) path.push_back(pos(v));
                 std::reverse(path.begin(), path.end());
                 raw[p] = std::move(path);
                 found[p] = 1;
+            };
+            if (r == 0) {
+                // The forward search exhausted its component with every pop inside the bound:
+                // every node it reached has its row here, so the whole table's forward search
+                // reaches the same nodes and fails too.
+                r = symmetrised();
+            } else if (r == -1 && hv(2, p) == 0) {
+                // A pop above the bound, and no kept edge into the goal among the rows: the
+                // whole table's forward search fails iff no node outside the rows keeps one
+                // either.  Its masked k-NN (on the device) counts them; with none, the
+                // symmetrised search runs on the rows and the table is not downloaded.
+                o.ms_restricted = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                o.ms_search += o.ms_restricted;
+                o.fallback = 1;
+                const std::function<bool()> rows_sym = [&]() {
+                    if (symmetrised() != 1) return false;
+                    take_path();
+                    return true;
+                };
+                bool on_rows = false;
+                const double* d_nodes = reinterpret_cast<const double*>(dev + L.o_nodes) + (size_t)p * L.NS * 3;
+                found[p] = wholeTableSearch(d_nodes, (int32_t)n, kbox[p].data(), kbox[p].data() + 3, &bs.area(w),
+                                            raw[p], o.edges_checked, o.edges_valid, o.ms_dev, o.ms_search, &rows_sym,
+                                            &on_rows)
+                               ? 1
+                               : 0;
+                if (on_rows) {
+                    o.fallback = 0;
+                    o.census = 1;
+                    o.rows_down = packed;
+                } else {
+                    o.rows_down = n;
+                    o.symmetrised = 0;
+                }
+                return;
+            }
+            if (r == 1) {
+                take_path();
                 o.edges_checked = packed * k;
                 o.edges_valid = hv(1, p);
                 o.rows_down = packed;
@@ -716,6 +756,7 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
         if (o.fallback && o.why >= 0) ++stats_.fallback_why[o.why];
         stats_.astar_pops += o.pops;
         stats_.restricted_symmetrised += o.symmetrised;
+        stats_.symmetrised_after_census += o.census;
         stats_.restricted_nodes += o.nodes;
         if (o.ms_restricted > stats_.ms_restricted_max) {
             stats_.ms_restricted_max = o.ms_restricted;
@@ -733,8 +774,10 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
 // reach the goal, over the symmetrised graph.  Runs on the calling thread's own stream.
 bool PathPlanner::wholeTableSearch(const double* d_nodes, int32_t n, const double box_lo[3], const double box_hi[3],
                                    void* area_, std::vector<Vec3>& path, int64_t& edges_checked, int64_t& edges_valid,
-                                   double& ms_dev, double& ms_search) const {
+                                   double& ms_dev, double& ms_search, const std::function<bool()>* rows_sym,
+                                   bool* decided_on_rows) const {
     const auto t0 = std::chrono::steady_clock::now();
+    if (decided_on_rows) *decided_on_rows = false;
     const bool canPass = configParser->getPathPlannerProperties().canPassGate;
     const epp_world* w = worldPtr->device();
     const int k = k_;
@@ -770,6 +813,22 @@ bool PathPlanner::wholeTableSearch(const double* d_nodes, int32_t n, const doubl
     // the downloads queued back to back, one synchronisation
     char* hp = static_cast<char*>(area.pin);
     int64_t* ecnt = reinterpret_cast<int64_t*>(hp);
+    if (rows_sym) {  // the edge counts first: no kept edge into the goal lets the rows decide
+        check(epp_memcpy_d2h_async(ecnt, d_ecnt, 16, st), "download");
+        check(epp_stream_sync(st), "sync");
+        if (ecnt[1] == 0) {
+            const auto tc = std::chrono::steady_clock::now();
+            ms_dev += std::chrono::duration<double, std::milli>(tc - t0).count();
+            const bool ok = (*rows_sym)();
+            ms_search += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc).count();
+            if (ok) {
+                edges_checked = (int64_t)m;
+                edges_valid = ecnt[0];
+                if (decided_on_rows) *decided_on_rows = true;
+                return true;
+            }
+        }
+    }
     const double* nodes = reinterpret_cast<const double*>(hp + BatchScratch::r256(64));
     void* h_tab = hp + BatchScratch::r256(64) + BatchScratch::r256((size_t)n * 24);
     check(epp_memcpy_d2h_async(ecnt, d_ecnt, 16, st), "download");
@@ -781,7 +840,8 @@ bool PathPlanner::wholeTableSearch(const double* d_nodes, int32_t n, const doubl
     edges_valid = ecnt[0];
     const bool goal_has_forward_edge = ecnt[1] > 0;
     const auto t1 = std::chrono::steady_clock::now();
-    ms_dev += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    if (!(decided_on_rows && rows_sym && ecnt[1] == 0))  // (else counted above)
+        ms_dev += std::chrono::duration<double, std::milli>(t1 - t0).count();
     const int32_t* nbr32 = static_cast<const int32_t*>(h_tab);
     const uint16_t* nbr16 = static_cast<const uint16_t*>(h_tab);
     auto nbr = [&](size_t e) -> int {

@@ -16,6 +16,7 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "epp/ConfigParser.h"
@@ -39,6 +40,9 @@ struct PlannerStats {
     // the bound, [6] symmetrised: exhausted in the rows
     int64_t fallback_why[7] = {0, 0, 0, 0, 0, 0, 0};
     int64_t restricted_symmetrised = 0;  // searches the rows' symmetrised graph decided
+    // of which: after the whole table's k-NN (run for its goal-edge count only: the forward
+    // search popped above the bound with no kept edge into the goal among the rows)
+    int64_t symmetrised_after_census = 0;
     int64_t astar_pops = 0, restricted_nodes = 0;  // (diagnostics) the restricted searches' closed nodes / node lists
     double ms_restricted_max = 0;                  // (diagnostics) the slowest problem's restricted search
     double ms_copy_of_max = 0;                     // (diagnostics) of which its copy out of pinned memory
@@ -111,9 +115,13 @@ private:
                      int64_t samples, std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const;
     void planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, const std::vector<uint64_t>& seeds,
                    int64_t samples, std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const;
+    // rows_sym (optional): asked, once the whole table's masked k-NN shows no kept edge into
+    // the goal, to decide the symmetrised search on the restricted rows; true = it found the
+    // path (put in `path` by the caller's code) and the whole table is not downloaded
     bool wholeTableSearch(const double* d_nodes, int32_t n, const double box_lo[3], const double box_hi[3], void* area,
                           std::vector<Vec3>& path, int64_t& edges_checked, int64_t& edges_valid, double& ms_dev,
-                          double& ms_search) const;
+                          double& ms_search, const std::function<bool()>* rows_sym = nullptr,
+                          bool* decided_on_rows = nullptr) const;
 
     std::shared_ptr<ConfigParser> configParser;
     uint64_t seed_ = 0x5eedull;

@@ -723,27 +723,37 @@ def test_plan_once_equals_cpu_restatement(c1, seed, ellipse, monkeypatch):
     assert O.plan_once(w, rg, ro, lo, hi, start, blocked, 4096, seed, 16, False, 4)[0] is None
 
 
-def test_plan_once_symmetrised_on_rows_equals_cpu(c1):
-    """Goals outside the sampling box: no sample keeps the goal among its 16 neighbours, so
-    the forward search exhausts and the symmetrised graph (the goal's own row, reversed)
-    decides.  The planner runs that search on the downloaded rows (host_planner.cpp solve,
-    restricted_symmetrised) instead of the whole table; the path equals the CPU
-    restatement's, whose stats say the symmetrised search ran."""
-    g, o, start, goal, w, rg, ro = c1
-    pp = _ot().PathPlanner(g, o, CONFIG)
-    lo, hi = synth.C1_BOUNDS
-    sym = ran = 0
-    for off, ax in ((0.4, 0), (0.4, 1), (0.8, 2), (0.8, 0)):
-        gl = np.array(goal, float)
-        gl[ax] = hi[ax] + off
-        for samples, seed in ((4096, 0), (4096, 3), (20_000, 1)):
+def test_plan_once_symmetrised_on_rows_equals_cpu(bench_track_config, geom):
+    """Goals outside the sampling box (the C4 box, track world 100, 65,536 samples): no
+    sample keeps the goal among its 16 neighbours, so the forward search fails and the
+    symmetrised graph (the goal's own row, reversed) decides.  The planner runs that search
+    on the downloaded rows (host_planner.cpp solve, `restricted_symmetrised`) instead of the
+    whole table -- here after the whole table's masked k-NN showed no kept edge into the
+    goal (the forward search popped above the bound: `symmetrised_after_census`); the path
+    equals the CPU restatement's, whose stats say its symmetrised search ran."""
+    path, c = bench_track_config
+    gates, obstacles = synth.track_world(100)
+    pp = _ot().PathPlanner(gates, obstacles, path)
+    rg, ro = config.inflate_radii(c)
+    w = O.world_build(geom, gates, obstacles, rg, ro)
+    lo, hi = np.array(c["world_properties"]["lower_bound"], float), np.array(c["world_properties"]["upper_bound"], float)
+    cases = [((0, 5.0, 1.0), (0, 6.4, 1.0)), ((5.0, 0, 1.0), (6.4, 0.5, 1.0)), ((0, -5, 1.0), (0.5, -6.5, 1.0)),
+             ((2, 2, 1.2), (2.5, 2.5, 2.5)), ((-5, -5, 1.0), (-6.4, -6.4, 1.0))]
+    sym = ran = cen = 0
+    for s, g in cases:
+        s, g = np.array(s, float), np.array(g, float)
+        for seed in (0, 1):
             s0 = pp.last_stats().get("restricted_symmetrised", 0)
-            got = pp.plan_once(start, gl, samples, seed)
-            exp, st = O.plan_once(w, rg, ro, lo, hi, start, gl, samples, seed, 16, False, 8)
-            assert exp is not None and got is not None and np.array_equal(got, exp), (off, ax, samples, seed)
+            c0 = pp.last_stats().get("symmetrised_after_census", 0)
+            got = pp.plan_once(s, g, 65536, seed)
+            exp, st = O.plan_once(w, rg, ro, lo, hi, s, g, 65536, seed, 16, False, 16)
+            assert exp is not None and got is not None and np.array_equal(got, exp), (s, g, seed)
             ran += int(st[4])
             sym += pp.last_stats()["restricted_symmetrised"] - s0
-    assert ran >= 10 and sym >= ran // 2, (ran, sym)
+            cen += pp.last_stats()["symmetrised_after_census"] - c0
+    st = pp.last_stats()
+    assert ran == 10 and sym == ran and cen >= 1 and st["fallbacks"] == 0, (ran, sym, cen, st.get("fallback_why"), st.get("fallbacks"),
+                                      st.get("restricted_rows"), st.get("rows_downloaded"))
 
 
 @pytest.mark.parametrize("ellipse", ELLIPSE)
