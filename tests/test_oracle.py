@@ -307,6 +307,13 @@ def test_cpu_planner_restatement_basic(cfg, geom):
     assert np.array_equal(a[0], start) and np.array_equal(a[-1], goal)
     assert O.check_motions(w, rg, ro, a[:-1], a[1:]).all()
     assert O.plan_once(w, rg, ro, lo, hi, start, np.array([1.0, 0.5, 0.5]), 3000, 7)[0] is None
+    assert sa[4] == 0  # (the forward search found it)
+    # a goal 0.8 m outside the sampling box: no sample keeps it among its 16 neighbours, so
+    # the forward search fails and the symmetrised graph decides (stats[4] = 1)
+    far = np.array([0.0, hi[1] + 0.8, 0.3])
+    c, sc = O.plan_once(w, rg, ro, lo, hi, start, far, 1000, 0, 16, False, 4)
+    assert c is not None and sc[4] == 1 and np.array_equal(c[-1], far)
+    assert O.check_motions(w, rg, ro, c[:-1], c[1:]).all()
 
 
 def test_track_planner_seed_derivation():
