@@ -110,7 +110,11 @@ def main():
             return launcher_check(ws, rank, local, out_stream, args.fail_rank, args.fail_at)
         run(args, ws, rank, local, out_stream)
     except LegFailed as e:
-        sys.exit(f"bench.py rank {rank}: {e}")
+        # exit at once: a process group whose peer died can abort the interpreter's teardown
+        # (a joinable transport thread -> std::terminate, exit -6 instead of 1)
+        print(f"bench.py rank {rank}: {e}", file=sys.stderr, flush=True)
+        sys.stdout.flush()
+        os._exit(1)
 
 
 def run(args, ws, rank, local, out_stream):

@@ -309,6 +309,15 @@ struct SolveScratch {
     }
 };
 
+// EPP_PLAN_TRACE=1 (diagnostics): the fallback's phases on stderr
+bool plan_trace() {
+    static const bool t = [] {
+        const char* e = std::getenv("EPP_PLAN_TRACE");
+        return e && std::atoi(e) == 1;
+    }();
+    return t;
+}
+
 // A* from node 0 to node 1 with the Euclidean distance to the goal (admissible and
 // consistent for Euclidean edge costs).  pos(v): coordinates; key(v): the node id that
 // breaks ties; expand(u, f, relax) calls relax(v) for u's edges and returns false to abort
@@ -516,15 +525,20 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
             const double bound = segs[p].bound;
             auto pos = [&](int v) { return Vec3(nd[3 * v], nd[3 * v + 1], nd[3 * v + 2]); };
             auto key = [](int v) { return v; };  // (compact indices keep the node order)
-            r = astar(ss, (size_t)m, pos, key, [&](int u, double f, auto&& relax, bool closing) {
-                if (!closing) return (f <= bound) && row_of[u] >= 0;
-                const uint16_t* row = rowc.data() + (size_t)row_of[u] * k;
-                for (int c = 0; c < k; ++c)
-                    if (row[c] != 0xFFFF) relax((int)row[c]);
-                return true;
-            });
+            // (no kept edge into the goal among the rows: the forward search on them cannot
+            // reach it -- the goal-edge count below decides instead, r = -1)
+            const bool goal_edges = hv(2, p) > 0;
+            r = -1;
+            if (goal_edges)
+                r = astar(ss, (size_t)m, pos, key, [&](int u, double f, auto&& relax, bool closing) {
+                    if (!closing) return (f <= bound) && row_of[u] >= 0;
+                    const uint16_t* row = rowc.data() + (size_t)row_of[u] * k;
+                    for (int c = 0; c < k; ++c)
+                        if (row[c] != 0xFFFF) relax((int)row[c]);
+                    return true;
+                });
             o.restricted_rows = packed;
-            o.pops = ss.pops;
+            o.pops = goal_edges ? ss.pops : 0;
             o.nodes = m;
             o.why = r == -1 ? 3 : r == 0 ? 4 : -1;
             // The symmetrised search on the rows.  The reference's next step after a failed
@@ -582,18 +596,23 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
                 // every node it reached has its row here, so the whole table's forward search
                 // reaches the same nodes and fails too.
                 r = symmetrised();
-            } else if (r == -1 && hv(2, p) == 0) {
-                // A pop above the bound, and no kept edge into the goal among the rows: the
-                // whole table's forward search fails iff no node outside the rows keeps one
-                // either.  Its masked k-NN (on the device) counts them; with none, the
-                // symmetrised search runs on the rows and the table is not downloaded.
+            } else if (!goal_edges) {
+                // No kept edge into the goal among the rows: the whole table's forward search
+                // fails if no node outside the rows keeps one either.  Its masked k-NN (on the
+                // device) counts them while the symmetrised search runs on the rows here; with
+                // none, that search decides and the table is not downloaded.
                 o.ms_restricted = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
                 o.ms_search += o.ms_restricted;
                 o.fallback = 1;
                 const std::function<bool()> rows_sym = [&]() {
-                    if (symmetrised() != 1) return false;
-                    take_path();
-                    return true;
+                    const auto ts0 = std::chrono::steady_clock::now();
+                    const int r2 = symmetrised();
+                    if (plan_trace())
+                        std::cerr << "[plan trace] problem " << p << ": symmetrised search on " << nrow << " rows / "
+                                  << m << " nodes: " << o.pops << " closed, "
+                                  << std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count()
+                                  << " ms, result " << r2 << " (copies before: " << o.ms_restricted << " ms)" << std::endl;
+                    return r2 == 1;
                 };
                 bool on_rows = false;
                 const double* d_nodes = reinterpret_cast<const double*>(dev + L.o_nodes) + (size_t)p * L.NS * 3;
@@ -603,6 +622,7 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
                                ? 1
                                : 0;
                 if (on_rows) {
+                    take_path();
                     o.fallback = 0;
                     o.census = 1;
                     o.rows_down = packed;
@@ -813,20 +833,28 @@ bool PathPlanner::wholeTableSearch(const double* d_nodes, int32_t n, const doubl
     // the downloads queued back to back, one synchronisation
     char* hp = static_cast<char*>(area.pin);
     int64_t* ecnt = reinterpret_cast<int64_t*>(hp);
-    if (rows_sym) {  // the edge counts first: no kept edge into the goal lets the rows decide
+    double overlap_ms = 0;  // (the rows' search, while the device worked: not device time)
+    if (rows_sym) {  // the edge counts first, the caller's search on the rows meanwhile: no
+                     // kept edge into the goal lets that search decide (its path: the caller's)
         check(epp_memcpy_d2h_async(ecnt, d_ecnt, 16, st), "download");
+        const auto tc = std::chrono::steady_clock::now();
+        const bool ok = (*rows_sym)();
+        const auto tr = std::chrono::steady_clock::now();
         check(epp_stream_sync(st), "sync");
-        if (ecnt[1] == 0) {
-            const auto tc = std::chrono::steady_clock::now();
-            ms_dev += std::chrono::duration<double, std::milli>(tc - t0).count();
-            const bool ok = (*rows_sym)();
-            ms_search += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc).count();
-            if (ok) {
-                edges_checked = (int64_t)m;
-                edges_valid = ecnt[0];
-                if (decided_on_rows) *decided_on_rows = true;
-                return true;
-            }
+        const auto tw = std::chrono::steady_clock::now();
+        overlap_ms = std::chrono::duration<double, std::milli>(tr - tc).count();
+        ms_search += overlap_ms;
+        if (plan_trace())
+            std::cerr << "[plan trace] whole table n " << n << " for its goal-edge count: "
+                      << std::chrono::duration<double, std::milli>(tw - t0).count() << " ms (waited "
+                      << std::chrono::duration<double, std::milli>(tw - tr).count() << " ms after the rows' search)"
+                      << ", kept edges into the goal " << ecnt[1] << std::endl;
+        if (ecnt[1] == 0 && ok) {
+            ms_dev += std::chrono::duration<double, std::milli>(tw - t0).count() - overlap_ms;
+            edges_checked = (int64_t)m;
+            edges_valid = ecnt[0];
+            if (decided_on_rows) *decided_on_rows = true;
+            return true;
         }
     }
     const double* nodes = reinterpret_cast<const double*>(hp + BatchScratch::r256(64));
@@ -840,8 +868,7 @@ bool PathPlanner::wholeTableSearch(const double* d_nodes, int32_t n, const doubl
     edges_valid = ecnt[0];
     const bool goal_has_forward_edge = ecnt[1] > 0;
     const auto t1 = std::chrono::steady_clock::now();
-    if (!(decided_on_rows && rows_sym && ecnt[1] == 0))  // (else counted above)
-        ms_dev += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    ms_dev += std::chrono::duration<double, std::milli>(t1 - t0).count() - overlap_ms;
     const int32_t* nbr32 = static_cast<const int32_t*>(h_tab);
     const uint16_t* nbr16 = static_cast<const uint16_t*>(h_tab);
     auto nbr = [&](size_t e) -> int {
@@ -864,10 +891,7 @@ bool PathPlanner::wholeTableSearch(const double* d_nodes, int32_t n, const doubl
                 }
             return true;
         });
-    static const bool trace = [] {  // (diagnostics: the fallback's phases on stderr)
-        const char* e = std::getenv("EPP_PLAN_TRACE");
-        return e && std::atoi(e) == 1;
-    }();
+    const bool trace = plan_trace();
     const auto t_fwd = std::chrono::steady_clock::now();
     if (r != 1) {  // the symmetrised graph: the reverse edges as a CSR, built on the device
         // (counting sort of the masked table; every node's sources ascending, the order of a

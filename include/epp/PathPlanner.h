@@ -115,9 +115,10 @@ private:
                      int64_t samples, std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const;
     void planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, const std::vector<uint64_t>& seeds,
                    int64_t samples, std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const;
-    // rows_sym (optional): asked, once the whole table's masked k-NN shows no kept edge into
-    // the goal, to decide the symmetrised search on the restricted rows; true = it found the
-    // path (put in `path` by the caller's code) and the whole table is not downloaded
+    // rows_sym (optional): the caller's symmetrised search on its restricted rows, run while
+    // the device builds the whole table's masked k-NN; when that shows no kept edge into the
+    // goal and rows_sym found the path, *decided_on_rows = true and the table is neither
+    // downloaded nor searched (the caller takes its own path)
     bool wholeTableSearch(const double* d_nodes, int32_t n, const double box_lo[3], const double box_hi[3], void* area,
                           std::vector<Vec3>& path, int64_t& edges_checked, int64_t& edges_valid, double& ms_dev,
                           double& ms_search, const std::function<bool()>* rows_sym = nullptr,
