@@ -63,6 +63,11 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
           f"{np.median([s.get('ms_enqueue', float('nan')) for s in st]):.3f}) solve "
           f"{np.median([s['ms_solve'] for s in st]):.3f} shortcut {np.median([s['ms_shortcut'] for s in st]):.3f}; "
           f"outside the planner {np.median([t - s['ms'] for t, s in zip(ts, st)]):.3f}", flush=True)
+    if os.environ.get("EPP_PROBE_PERCALL"):
+        for i, (t, s) in enumerate(zip(ts, st)):
+            print(f"   #{i}: {t:.3f} ms, batch {s['ms_batch']:.3f} solve {s['ms_solve']:.3f} shortcut "
+                  f"{s['ms_shortcut']:.3f} outside {t - s['ms']:.3f}; rows {s['rows_downloaded']} pops "
+                  f"{s.get('astar_pops', 0)} slowest search {s.get('ms_restricted_max', 0):.3f}", flush=True)
     print("   all (ms):", " ".join(f"{t:.2f}/{s['ms']:.2f}" for t, s in zip(ts, st)), flush=True)
 else:
     for t in (sys.argv[1:] or ["4"]):
