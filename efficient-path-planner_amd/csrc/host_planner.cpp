@@ -604,9 +604,11 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
                 o.ms_restricted = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
                 o.ms_search += o.ms_restricted;
                 o.fallback = 1;
+                o.why = 2;
                 const std::function<bool()> rows_sym = [&]() {
                     const auto ts0 = std::chrono::steady_clock::now();
                     const int r2 = symmetrised();
+                    if (r2 == 1) o.why = 2;  // (a fallback now comes from the count: a goal edge elsewhere)
                     if (plan_trace())
                         std::cerr << "[plan trace] problem " << p << ": symmetrised search on " << nrow << " rows / "
                                   << m << " nodes: " << o.pops << " closed, "

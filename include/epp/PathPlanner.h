@@ -35,7 +35,8 @@ struct PlannerStats {
     int64_t restricted_rows = 0;  // of which packed rows of the row-restricted searches
     int64_t fallbacks = 0;        // searches that took the whole table after the restricted rows
     // why (diagnostics): [0] rows past the capacity or > 65,535 nodes, [1] an inexact row,
-    // [2] (unused since the symmetrised search runs on the rows), [3] a pop above the bound,
+    // [2] no kept edge into the goal among the rows but one elsewhere in the whole table,
+    // [3] a pop above the bound,
     // [4] (forward exhausted: the symmetrised search follows), [5] symmetrised: a pop above
     // the bound, [6] symmetrised: exhausted in the rows
     int64_t fallback_why[7] = {0, 0, 0, 0, 0, 0, 0};

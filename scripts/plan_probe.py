@@ -53,7 +53,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
           np.median([s.get("restricted_nodes", 0) for s in st]), "slowest problem (ms)",
           np.median([s.get("ms_restricted_max", 0) for s in st]), "its copy (ms)",
           np.median([s.get("ms_copy_of_max", 0) for s in st]))
-    print("   fallback reasons [capacity, inexact row, -, pop above bound, -, symmetrised: pop above bound,"
+    print("   fallback reasons [capacity, inexact row, goal edge outside the rows, pop above bound, -, symmetrised: pop above bound,"
           " symmetrised: exhausted]:", np.sum([s.get("fallback_why", [0] * 7) for s in st], 0).tolist(),
           "; symmetrised searches decided on the rows:", sum(s.get("restricted_symmetrised", 0) for s in st))
     warm = int(os.environ.get("EPP_PROBE_WARM", "1"))
