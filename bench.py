@@ -94,6 +94,8 @@ def main():
     ap.add_argument("--fail-at", choices=("plan", "exchange", "after-count"), default="plan",
                     help="with --fail-rank: fail inside the plan leg (collective check), at the all-gather (count -1) "
                          "or die right after sending its count (the peers are then inside the data all-gather)")
+    ap.add_argument("--parity-flip-rank", type=int, default=-1,
+                    help="with --launcher-check: this rank reports one C2 flag mismatch (parity reduction test)")
     args = ap.parse_args()
 
     from eppamd.dist import LegFailed, env, make_group, spawn_ranks
@@ -107,7 +109,7 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws} (launch one process per GPU)")
     try:
         if args.launcher_check:
-            return launcher_check(ws, rank, local, out_stream, args.fail_rank, args.fail_at)
+            return launcher_check(ws, rank, local, out_stream, args.fail_rank, args.fail_at, args.parity_flip_rank)
         run(args, ws, rank, local, out_stream)
     except LegFailed as e:
         # exit at once: a process group whose peer died can abort the interpreter's teardown
@@ -227,13 +229,25 @@ def run(args, ws, rank, local, out_stream):
     traffic, traffic_src = committed_traffic()
 
     cpu = None
-    parity_gpu = dict((c5_inputs or {}).get("parity_gpu", {}), c2_flags=c2_flags)
-    if plan:
-        parity_gpu["c4_first"] = plan.pop("_first")
+    parity_gpu = dict((c5_inputs or {}).get("parity_gpu", {}))
+    first = plan.pop("_first") if plan else None
+    gathered_ok = plan.pop("_gathered_own_equal", None) if plan else None
+    # every rank, at every N: its own C2 batch 0 and its own track against the oracle,
+    # reduced over the ranks (rank 0 prints the sums and every rank's counters)
+    rparity = None
+    if not args.no_cpu:
+        rparity = reduce_parity(dist, dist.run(lambda: rank_parity(
+            rank, geom, rg, ro, gates, obstacles, lo, hi, c2_flags, first, gathered_ok,
+            plan["comm_n_ranks"] if plan else None, ws), "parity"), ws)
     if not args.no_cpu and ws == 1:
         cpu = cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs, parity_gpu)
     if c5_inputs:
         os.unlink(c5_inputs["cfg_path"])
+    parity = dict(cpu.pop("parity", None) or {}) if cpu else {}
+    if rparity:
+        parity.update(rparity)
+    if parity:
+        parity.update(parity_verdict(parity))
 
     if rank == 0:
         out = {
@@ -263,9 +277,10 @@ def run(args, ws, rank, local, out_stream):
             "full_plan_ms_per_track": plan["ms_per_track"] if plan else None,
             "full_plan": plan,
             "cpu_baseline": cpu,
-            # the GPU results above against the CPU oracle on the same inputs (computed in the
-            # cpu_baseline leg; null without it)
-            "parity": cpu.pop("parity", None) if cpu else None,
+            # the GPU results above against the CPU oracle on the same inputs: every rank's
+            # own C2 batch and track (reduced over the ranks, any N), the side legs' (N = 1,
+            # in the cpu_baseline leg); null with --no-cpu
+            "parity": parity or None,
             "side": side,
         }
         print(json.dumps(out), file=out_stream, flush=True)
@@ -273,7 +288,7 @@ def run(args, ws, rank, local, out_stream):
     dist.close()
 
 
-def launcher_check(ws, rank, local, out_stream, fail_rank=-1, fail_at="plan"):
+def launcher_check(ws, rank, local, out_stream, fail_rank=-1, fail_at="plan", parity_flip_rank=-1):
     """The multi-rank plumbing of this bench without a GPU (gloo): the same launch, env,
     barrier, max-over-ranks reduction, error protocol and ragged waypoint all-gather as the
     GPU run (eppamd.dist.Group; the GPU run's group is the product's RCCL communicator).
@@ -300,11 +315,32 @@ def launcher_check(ws, rank, local, out_stream, fail_rank=-1, fail_at="plan"):
         os._exit(7)
     sets = dist.all_gather_waypoints(None if (rank == fail_rank and fail_at == "exchange") else wp)
     t = dist.max(float(rank + 1))
+    # the per-rank parity and its reduction, as the GPU run does them: this rank's C2 batch 0
+    # (a 4096-state prefix; the oracle's own flags stand in for the GPU's, with one flipped
+    # on --parity-flip-rank), the gathered set at this rank's slot, the group's rank count
+    from eppamd import config, synth
+    cfg = config.load(os.path.join(ROOT, "configs", "config.json"))
+    geom = config.geometry(cfg)
+    rg, ro = config.inflate_radii(cfg)
+    gates, obstacles = synth.track_world(42)
+    lo, hi = synth.C2_BOUNDS
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    n = 4096
+    flags = O.check_states(O.world_build(geom, gates, obstacles, rg, ro), rg, ro,
+                           synth.sample_states(7 + 1000 * rank, lo, hi, n), False, threads=2)
+    if rank == parity_flip_rank:
+        flags[17] ^= 1
+    own = len(sets) == ws and np.array_equal(np.asarray(sets[rank]), wp)
+    parity = reduce_parity(dist, dist.run(lambda: rank_parity(rank, geom, rg, ro, gates, obstacles, lo, hi, flags,
+                                                              None, own, dist.n_ranks(), ws, c2_n=n, threads=2),
+                                          "parity"), ws)
+    parity.update(parity_verdict(parity))
     if rank == 0:
         print(json.dumps({"n_gpus": ws, "ranks_seen": [int(s[0, 0] // 1000) for s in sets],
                           "waypoints_per_track": [len(s) for s in sets], "max_over_ranks": t,
                           "local_rank": local, "process_group": dist.kind, "comm_n_ranks": dist.n_ranks(),
-                          "per_rank": per_rank}), file=out_stream, flush=True)
+                          "per_rank": per_rank, "parity": parity}), file=out_stream, flush=True)
     dist.close()
 
 
@@ -415,7 +451,9 @@ def full_plan(dist, rank, reps):
         comm_ranks = comm.n_ranks()  # RCCL's own rank count (epp_comm_rank), not WORLD_SIZE
         if comm is not dist:
             comm.close()
-    return {"_first": state["first"],
+    # (parity of the exchange: this rank's slot of the gathered sets is its own set)
+    own_ok = len(sets) == dist.ws and np.array_equal(np.asarray(sets[rank if len(sets) > 1 else 0]), wp)
+    return {"_first": state["first"], "_gathered_own_equal": bool(own_ok),
             "ms_per_track": ms_max, "ms_per_track_p50": dist.max(float(np.median(per))), "tracks": dist.ws,
             "ms_per_track_per_rank": per_rank, "comm_n_ranks": comm_ranks, "ms_per_call": per,
             "planner_phases_p50": phases,
@@ -862,9 +900,6 @@ def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None, parity_
            "all_cores_ideal_bound": {"value": reps * N_STATES / dt * (host["nproc"] or 1),
                                      "threads": host["nproc"], "kind": "bound: 1-thread rate x nproc"},
            "states_wide": wide}
-    if "c2_flags" in parity_gpu:  # resident batch 0 = pts (rank 0)
-        parity["c2_state_mismatches"] = int(np.count_nonzero(parity_gpu["c2_flags"] != ref_flags))
-        parity["c2_states_compared"] = int(len(ref_flags))
     # C3 motions: 512 OBBs, the same edge generator as the GPU leg (bounded edge counts)
     g3, o3 = synth.track_world(42, n_obstacles=472)
     w3 = O.world_build(geom, g3, o3, rg, ro)
@@ -902,12 +937,6 @@ def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None, parity_
     wp4, rows4 = TP.plan_track(w4, rg, ro, lo4, hi4, cps, PLAN_SAMPLES, tg["max_velocity"], tg["max_acceleration"],
                                tg["sampling_interval"], threads=nt)
     out["full_plan_ms_per_track"] = (time.perf_counter() - t) * 1e3
-    if "c4_first" in parity_gpu:  # the GPU's first plan of the same track (call numbers 0..8)
-        gw, gt = parity_gpu["c4_first"]["wp"], parity_gpu["c4_first"]["traj"]
-        parity["c4_waypoints_equal"] = bool(gw.shape == wp4.shape and np.array_equal(gw, wp4))
-        same = gt.shape == rows4.shape
-        parity["c4_traj_time_column_equal"] = bool(same and np.array_equal(gt[:, 9], rows4[:, 9]))
-        parity["c4_traj_max_abs"] = float(np.abs(gt[:, :9] - rows4[:, :9]).max()) if same else None
     out["full_plan"] = {"threads": nt, "tracks": 1, "waypoints": int(len(wp4)), "traj_rows": int(len(rows4)),
                         "workload": "C4 rank-0 track: 9 batch plans (65,536 samples, k=16) + includeGates2 + "
                                     "min-snap + sampling, the planner restated on the CPU (oracle/track_planner.py)"}
@@ -970,13 +999,102 @@ def cpu_baseline(geom, rg, ro, gates, obstacles, lo, hi, c5_inputs=None, parity_
         out["c5_update_gate_pos"] = c5_events(c["cfg_path"], c["geom"], c["gates"], c["obstacles"],
                                               cpu_threads=nt)
     if parity:
-        parity["ok"] = bool(all(parity.get(k, 0) == 0 for k in parity if k.endswith("_mismatches")) and
-                            all(parity.get(k, True) for k in parity if k.endswith("_equal")) and
-                            all((parity.get(k) is not None and parity[k] <= 1e-6)
-                                for k in parity if k.endswith("_max_abs")))
-        parity["tolerance_f64"] = 1e-6
         out["parity"] = parity
     return out
+
+
+PARITY_THREADS = 16  # one GPU's CPU share on the pool (and on an 8-GPU node: 256 / 8 = 32)
+
+
+def rank_parity(rank, geom, rg, ro, gates, obstacles, lo, hi, c2_flags, first, gathered_ok, comm_n_ranks, ws,
+                c2_n=None, threads=PARITY_THREADS):
+    """This rank's own GPU results against the oracle on the same inputs, at any N:
+
+    * C2: the flags of its resident batch 0 (seed 7 + 1000 * rank) -- `c2_flags`, the
+      first c2_n states (all by default; ~4 ms of oracle work on 16 threads per 1M);
+    * C4: its first plan of its own track (world seed 100 + rank, planner calls 0..8) --
+      `first` = {"wp", "traj"} -- against the CPU restatement of the whole track
+      (oracle/track_planner.plan_track, ~0.4 s on 16 threads): waypoints and the time
+      column equal, the other columns' max-abs difference;
+    * the exchange: the all-gathered set at this rank's index equals its own waypoints
+      (`gathered_ok`) and RCCL's own rank count equals the world size.
+
+    Returns flat counters (reduce_parity sums / ands / maxes them over the ranks)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from eppamd import synth
+    out = {}
+    if c2_flags is not None:
+        w = O.world_build(geom, gates, obstacles, rg, ro)
+        n = len(c2_flags) if c2_n is None else c2_n
+        pts = synth.sample_states(7 + 1000 * rank, lo, hi, n)
+        ref = O.check_states(w, rg, ro, pts, False, threads=threads)
+        out["c2_batch0_mismatches"] = int(np.count_nonzero(np.asarray(c2_flags[:n]) != ref))
+        out["c2_batch0_compared"] = int(n)
+    if first is not None:
+        wp4, rows4 = _cpu_track(geom, rg, ro, rank, threads)
+        gw, gt = np.asarray(first["wp"]), np.asarray(first["traj"])
+        out["c4_waypoints_equal"] = bool(gw.shape == wp4.shape and np.array_equal(gw, wp4))
+        same = gt.shape == rows4.shape
+        out["c4_traj_time_column_equal"] = bool(same and np.array_equal(gt[:, 9], rows4[:, 9]))
+        out["c4_traj_max_abs"] = float(np.abs(gt[:, :9] - rows4[:, :9]).max()) if same else float("inf")
+    if gathered_ok is not None:
+        out["gathered_set_equal"] = bool(gathered_ok)
+    if comm_n_ranks is not None:
+        out["comm_n_ranks_equal"] = bool(comm_n_ranks == ws)
+    return out
+
+
+def _cpu_track(geom, rg, ro, rank, threads):
+    """The CPU restatement of full_plan's first plan of this rank's track (world seed
+    100 + rank, planner calls 0..8): waypoints and sampled rows."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    import track_planner as TP
+    from eppamd import config as cfgmod, synth
+    c4, c4path = _track_config()
+    os.unlink(c4path)
+    g4, o4 = synth.track_world(100 + rank)
+    w4 = O.world_build(geom, g4, o4, rg, ro)
+    ends = synth.gate_checkpoints(g4, geom.gate_height, 0.55)
+    cps = np.vstack([ends[0], synth.gate_checkpoints(g4, geom.gate_height,
+                                                     c4["path_planner_properties"]["checkpoint_gate_offset"]), ends[-1]])
+    tg = c4["trajectory_generator_properties"]
+    lo4, hi4 = cfgmod.bounds(c4)
+    return TP.plan_track(w4, rg, ro, lo4, hi4, cps, PLAN_SAMPLES, tg["max_velocity"], tg["max_acceleration"],
+                         tg["sampling_interval"], threads=threads)
+
+
+def reduce_parity(dist, local, ws):
+    """Collective: every rank's rank_parity counters -> the job's.  Sums for *_mismatches /
+    *_compared, all-ranks for *_equal, the max for *_max_abs; every rank's own value under
+    per_rank (rank order).  Every rank must hold the same keys (they come from the same
+    legs)."""
+    keys = sorted(local)
+    per_rank, red = {}, {"ranks": ws}
+    for k in keys:
+        v = local[k]
+        vals = dist.gather(float(v))
+        if k.endswith("_equal"):
+            per_rank[k] = [bool(x) for x in vals]
+            red[k] = all(per_rank[k])
+        elif k.endswith("_max_abs"):
+            per_rank[k] = vals
+            red[k] = float(max(vals))
+        else:
+            per_rank[k] = [int(x) for x in vals]
+            red[k] = int(sum(per_rank[k]))
+    red["per_rank"] = per_rank
+    return red
+
+
+def parity_verdict(parity):
+    """ok = every mismatch count 0, every *_equal true, every *_max_abs within 1e-6."""
+    return {"ok": bool(all(parity.get(k, 0) == 0 for k in parity if k.endswith("_mismatches")) and
+                       all(parity.get(k, True) for k in parity if k.endswith("_equal")) and
+                       all((parity.get(k) is not None and parity[k] <= 1e-6)
+                           for k in parity if k.endswith("_max_abs"))),
+            "tolerance_f64": 1e-6}
 
 
 if __name__ == "__main__":

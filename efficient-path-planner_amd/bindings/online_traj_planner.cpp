@@ -219,6 +219,10 @@ PYBIND11_MODULE(online_traj_planner, m) {
         .def("last_stats", [](const epp::PathPlanner& self) {
             const auto& s = self.lastStats();
             py::dict d;
+            if (s.size != sizeof(epp::PlannerStats) || s.version != epp::kPlannerAbiVersion)
+                throw std::runtime_error("PlannerStats: the library's layout differs from this module's header");
+            d["size"] = s.size;
+            d["version"] = s.version;
             d["states_sampled"] = s.states_sampled;
             d["states_valid"] = s.states_valid;
             d["edges_checked"] = s.edges_checked;
@@ -394,6 +398,10 @@ PYBIND11_MODULE(online_traj_planner, m) {
         .def("planner_stats", [](epp::OnlineTrajGenerator& self) {
             const auto& s = self.planner().lastStats();
             py::dict d;
+            if (s.size != sizeof(epp::PlannerStats) || s.version != epp::kPlannerAbiVersion)
+                throw std::runtime_error("PlannerStats: the library's layout differs from this module's header");
+            d["size"] = s.size;
+            d["version"] = s.version;
             d["states_sampled"] = s.states_sampled;
             d["edges_checked"] = s.edges_checked;
             d["ms"] = s.ms;

@@ -128,6 +128,11 @@ epp_status check_knn_motions_rows(const epp_world* world, const double* nodes, i
                                   const int64_t* rows_n, int32_t cap, int32_t k, int32_t can_pass_gate,
                                   uint8_t* valid, uint16_t* out16, int32_t target, int64_t* count, void* stream,
                                   const MotionMask* marks = nullptr);
+// Whether check_knn_motions_rows can run on this world (its index current, rebuilt if
+// stale): tile tables exist (slab_n > 0) and they, the records and the wave queues fit the
+// LDS budget.  False for worlds without OBBs or past ~1000 OBBs: the planner then builds
+// every problem's whole table instead of the restricted rows.
+bool knn_motions_rows_supported(const epp_world* world);
 
 // ---- the batched planner (PathPlanner::planPaths): a batch of gate-to-gate problems, one
 // launch per device stage with blockIdx.y = the problem (planner.hip, plan_batch_launch).

@@ -84,8 +84,17 @@ uint64_t bits_of(double d) {
 }
 }  // namespace
 
-PathPlanner::PathPlanner(const Matrix& gates, const Matrix& obstacles, std::shared_ptr<ConfigParser> cp)
+PathPlanner::PathPlanner(const Matrix& gates, const Matrix& obstacles, std::shared_ptr<ConfigParser> cp,
+                         AbiTag abi)
     : configParser(std::move(cp)) {
+    if (abi.planner_size != sizeof(PathPlanner) || abi.stats_size != sizeof(PlannerStats) ||
+        abi.version != kPlannerAbiVersion)
+        throw std::runtime_error("PathPlanner: caller built against another epp/PathPlanner.h (PathPlanner " +
+                                 std::to_string(abi.planner_size) + " B, PlannerStats " +
+                                 std::to_string(abi.stats_size) + " B, version " + std::to_string(abi.version) +
+                                 "; this library: " + std::to_string(sizeof(PathPlanner)) + " B, " +
+                                 std::to_string(sizeof(PlannerStats)) + " B, version " +
+                                 std::to_string(kPlannerAbiVersion) + "): rebuild the caller");
     worldPtr = std::make_shared<World>(configParser);
     parseGatesAndObstacles(gates, obstacles);  // src/PathPlanner.cpp:27-35
     // knobs of this build, read once: EPP_PLAN_ELLIPSE the row-restricted search's bound
@@ -213,7 +222,8 @@ public:
                 // the allocation (the cold first plan), not in a search
                 check(epp_memcpy_d2h_async(a.pin, a.dev, std::min(pb, a.dcap), a.stream), "planner fallback warm-up");
                 check(epp_stream_sync(a.stream), "planner fallback warm-up");
-                a.cold = true;
+                // (cold stays as it was: a grown area -- a retry with doubled samples -- has
+                // had its warm-up search; a new one starts cold)
             }
         }
     }
@@ -410,7 +420,10 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
     // past half the nodes.  Otherwise (a pop above the bound, rows past the capacity, no kept
     // edge into the goal among the rows, more than 65,535 nodes) the whole table is built.
     const int64_t nmax = samples + 2;
-    const bool restrict_ok = ellipse_ >= 1.0 && (k == 4 || k == 8 || k == 16) && nmax <= 4 * 65536;
+    // (the rows' motion check needs the world's tile tables: a world without OBBs or past the
+    // LDS budget builds every problem's whole table, whose check has the other kernels)
+    const bool restrict_ok = ellipse_ >= 1.0 && (k == 4 || k == 8 || k == 16) && nmax <= 4 * 65536 &&
+                             knn_motions_rows_supported(w);
     // the rows' k-NN grid: cells of ~1.5 nodes (the sampling density), over the nodes of the
     // ellipsoid bound + 7.5 cells (a query's search radius r stays below half the margin:
     // |x - s| + |x - g| is 2-Lipschitz, so every node within r of a row's node is in it)
@@ -607,8 +620,7 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
                 o.why = 2;
                 const std::function<bool()> rows_sym = [&]() {
                     const auto ts0 = std::chrono::steady_clock::now();
-                    const int r2 = symmetrised();
-                    if (r2 == 1) o.why = 2;  // (a fallback now comes from the count: a goal edge elsewhere)
+                    const int r2 = symmetrised();  // (o.why: 5 / 6 when it fails)
                     if (plan_trace())
                         std::cerr << "[plan trace] problem " << p << ": symmetrised search on " << nrow << " rows / "
                                   << m << " nodes: " << o.pops << " closed, "
@@ -617,12 +629,16 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
                     return r2 == 1;
                 };
                 bool on_rows = false;
+                int64_t census = 0;
                 const double* d_nodes = reinterpret_cast<const double*>(dev + L.o_nodes) + (size_t)p * L.NS * 3;
                 found[p] = wholeTableSearch(d_nodes, (int32_t)n, kbox[p].data(), kbox[p].data() + 3, &bs.area(w),
                                             raw[p], o.edges_checked, o.edges_valid, o.ms_dev, o.ms_search, &rows_sym,
-                                            &on_rows)
+                                            &on_rows, &census)
                                ? 1
                                : 0;
+                // why the whole table was searched: a kept goal edge outside the rows (2), else
+                // the rows' symmetrised search failed (5 / 6, set by it)
+                if (census > 0) o.why = 2;
                 if (on_rows) {
                     take_path();
                     o.fallback = 0;
@@ -660,11 +676,23 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
             err[p] = std::current_exception();
         }
     };
-    // The W - 1 planner threads are started before the launch and wait (spinning) for the
-    // results, so their wake-up overlaps the device stages; then the W solvers pull
-    // problems in order.  go: 1 results in, -1 no results (the launch failed).
+    // The W - 1 planner threads are started before the launch and wait for the results, so
+    // their wake-up overlaps the device stages; then the W solvers pull problems in order.
+    // go: 1 results in, -1 no results (the launch failed).  A thread spins for at most
+    // kSpinUs (a warm batch is ~0.17 ms: the spin keeps the wake-up off the critical path)
+    // and then blocks on go_cv, so a slow batch (the cold first plan's warm-up, a hung
+    // device) does not keep W - 1 cores busy.
     std::atomic<int> go{0};
     std::atomic<int> next{0};
+    std::mutex go_mu;
+    std::condition_variable go_cv;
+    auto set_go = [&](int v) {
+        {
+            std::lock_guard<std::mutex> lk(go_mu);
+            go.store(v, std::memory_order_release);
+        }
+        go_cv.notify_all();
+    };
     auto drain = [&](size_t w) {
         SolveScratch::get().warmup(k);
         for (int p = next++; p < S; p = next++) run(p, w);
@@ -677,8 +705,17 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
     for (size_t t = 1; t < W; ++t)
         plan_pool().submit([&, devno, t] {
             (void)hipSetDevice(devno);
+            constexpr int64_t kSpinUs = 400;
+            const auto ts = std::chrono::steady_clock::now();
             int g;
-            while ((g = go.load(std::memory_order_acquire)) == 0) _mm_pause();
+            for (uint32_t i = 0; (g = go.load(std::memory_order_acquire)) == 0; ++i) {
+                _mm_pause();
+                if ((i & 255) == 255 &&
+                    std::chrono::steady_clock::now() - ts > std::chrono::microseconds(kSpinUs)) {
+                    std::unique_lock<std::mutex> lk(go_mu);
+                    go_cv.wait(lk, [&] { return go.load(std::memory_order_acquire) != 0; });
+                }
+            }
             if (g > 0) drain(t);
             std::lock_guard<std::mutex> lk(done_mu);
             if (--pending == 0) done_cv.notify_all();
@@ -699,14 +736,22 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
             return e && std::atoi(e) == 1;
         }();
         if (sync_wait) check(epp_stream_sync(st), "sync");
+        // (a deadline: a batch that has not completed in kBatchDeadlineS raises instead of
+        // polling forever; the scratch it writes into stays allocated)
+        constexpr double kBatchDeadlineS = 30.0;
         const uint32_t* done = reinterpret_cast<const uint32_t*>(H + L.h_done);
+        const auto tw0 = std::chrono::steady_clock::now();
         for (uint64_t spin = 0;; ++spin) {
             int b = 0;
             while (b < L.done_n && __atomic_load_n(done + b, __ATOMIC_ACQUIRE) == seq) ++b;
             if (b == L.done_n) break;
             if ((spin & 1023) == 1023) {
                 const hipError_t q = hipStreamQuery(static_cast<hipStream_t>(st));
-                if (q == hipErrorNotReady) continue;
+                if (q == hipErrorNotReady) {
+                    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - tw0).count() > kBatchDeadlineS)
+                        throw std::runtime_error("planner batch: not complete after 30 s (device hung?)");
+                    continue;
+                }
                 if (q != hipSuccess) throw std::runtime_error(std::string("planner batch: ") + hipGetErrorString(q));
                 b = 0;
                 while (b < L.done_n && __atomic_load_n(done + b, __ATOMIC_ACQUIRE) == seq) ++b;
@@ -731,12 +776,12 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
                                    kbox[0].data(), kbox[0].data() + 3, &ar, dummy, e0, e1, m0, m1);
         }
     } catch (...) {
-        go.store(-1, std::memory_order_release);
+        set_go(-1);
         join();
         throw;
     }
     const double ms_batch = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_dev0).count();
-    go.store(1, std::memory_order_release);
+    set_go(1);
     drain(0);
     join();
     for (const auto& e : err)
@@ -797,7 +842,7 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
 bool PathPlanner::wholeTableSearch(const double* d_nodes, int32_t n, const double box_lo[3], const double box_hi[3],
                                    void* area_, std::vector<Vec3>& path, int64_t& edges_checked, int64_t& edges_valid,
                                    double& ms_dev, double& ms_search, const std::function<bool()>* rows_sym,
-                                   bool* decided_on_rows) const {
+                                   bool* decided_on_rows, int64_t* census_goal_edges) const {
     const auto t0 = std::chrono::steady_clock::now();
     if (decided_on_rows) *decided_on_rows = false;
     const bool canPass = configParser->getPathPlannerProperties().canPassGate;
@@ -851,6 +896,7 @@ bool PathPlanner::wholeTableSearch(const double* d_nodes, int32_t n, const doubl
                       << std::chrono::duration<double, std::milli>(tw - t0).count() << " ms (waited "
                       << std::chrono::duration<double, std::milli>(tw - tr).count() << " ms after the rows' search)"
                       << ", kept edges into the goal " << ecnt[1] << std::endl;
+        if (census_goal_edges) *census_goal_edges = ecnt[1];
         if (ecnt[1] == 0 && ok) {
             ms_dev += std::chrono::duration<double, std::milli>(tw - t0).count() - overlap_ms;
             edges_checked = (int64_t)m;
@@ -1096,6 +1142,11 @@ int PathPlanner::planCalls(const std::vector<std::pair<Vec3, Vec3>>& problems, u
             }
         }
         pending.swap(still);
+        // (every pending problem ran in each attempt, concurrently with the others, so the
+        // batch's elapsed time is each problem's own, as for concurrent planPath calls
+        // (src/OnlineTrajGenerator.cpp:324-340); consecutive planPath calls -- the
+        // reference's preComputeTraj -- would each restart the clock: a problem that keeps
+        // failing here gets at most the attempts timeLimit allows from the batch's start)
         const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         if (!pending.empty() && el > timeLimit) break;  // out of time: give up like solve(timeLimit)
         samples *= 2;

@@ -808,16 +808,25 @@ __global__ __launch_bounds__(1024) void k_motions_v5(const WorldView* __restrict
 using namespace epp;
 
 namespace {
+// LDS bytes of k_motions_v5 for this world (records, tile rows, wave queues), 0 when the
+// world has no tile tables or they do not fit the budget.
+uint32_t motions_v5_lds(const WorldView& w) {
+    if (w.slab_n <= 0) return 0;
+    const uint32_t recb5 = (uint32_t)(((size_t)w.n_obb * kRecDoubles * 8 + 15) & ~size_t(15));
+    const uint32_t tileb = (uint32_t)((size_t)w.tile_n * w.tile_n * w.tile_words * 4);
+    const uint32_t shm5 = recb5 + tileb + 16u * (kQueueV5 * 4 + 64);
+    return shm5 > kLdsBudget ? 0 : shm5;
+}
+
 // k_motions_v5 when the world has tile tables and they, the records and the wave queues
 // fit the LDS budget; returns false (nothing launched) otherwise.
 bool launch_motions_v5(const WorldView* dw, const WorldView& w, const double* s1, const double* s2,
                        const int32_t* nbr, int kk, int64_t n, int32_t can_pass_gate, int32_t mode, uint8_t* valid,
                        hipStream_t st, const MotionMask& mm = MotionMask{}) {
-    if (w.slab_n <= 0) return false;
+    const uint32_t shm5 = motions_v5_lds(w);
+    if (shm5 == 0) return false;
     const uint32_t recb5 = (uint32_t)(((size_t)w.n_obb * kRecDoubles * 8 + 15) & ~size_t(15));
     const uint32_t tileb = (uint32_t)((size_t)w.tile_n * w.tile_n * w.tile_words * 4);
-    const uint32_t shm5 = recb5 + tileb + 16u * (kQueueV5 * 4 + 64);
-    if (shm5 > kLdsBudget) return false;
     const int per_cu = std::max(1, std::min(2, (int)((160u * 1024u) / shm5)));
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((n + 1023) / 1024, (int64_t)cu_count() * per_cu));
 #define EPP_LAUNCH_M5(WW, MM, II)                                                                                 \
@@ -984,6 +993,13 @@ epp_status epp::check_knn_motions_masked(const epp_world* world, const double* n
         return EPP_ERR_UNSUPPORTED;
     }
     return launch_error("check_knn_motions_masked");
+}
+
+bool epp::knn_motions_rows_supported(const epp_world* world) {
+    if (!world) return false;
+    IndexLease ix;
+    if (ensure_index(world, &ix) != EPP_OK) return false;
+    return motions_v5_lds(ix.view) != 0;
 }
 
 epp_status epp::check_knn_motions_rows(const epp_world* world, const double* nodes, int32_t* rows32,

@@ -25,7 +25,14 @@
 
 namespace epp {
 
+// Layout version of PlannerStats / PathPlanner below: raise it whenever either changes.
+constexpr uint32_t kPlannerAbiVersion = 6;
+
 struct PlannerStats {
+    // ABI guard (first, so a caller built against any version reads it): the size of the
+    // struct the library filled in; a caller checks lastStats().size == sizeof(PlannerStats)
+    uint32_t size = sizeof(PlannerStats);
+    uint32_t version = kPlannerAbiVersion;
     int64_t states_sampled = 0;
     int64_t states_valid = 0;
     int64_t edges_checked = 0;    // edges of the graphs searched (the final table's on a fallback)
@@ -58,8 +65,19 @@ struct PlannerStats {
 
 class PathPlanner {
 public:
+    // The caller's view of the layout (sizes and version compiled into the CALLER from this
+    // header) is handed to the library, which throws std::runtime_error when it differs from
+    // its own: a caller built against a stale header (PlannerStats grew, cd38a05) fails at
+    // construction instead of reading or writing past the object.
+    struct AbiTag {
+        uint32_t planner_size, stats_size, version;
+    };
     PathPlanner(const Matrix& nominalGatePositionAndType, const Matrix& nominalObstaclePosition,
-                std::shared_ptr<ConfigParser> configParser);
+                std::shared_ptr<ConfigParser> configParser)
+        : PathPlanner(nominalGatePositionAndType, nominalObstaclePosition, std::move(configParser),
+                      AbiTag{sizeof(PathPlanner), sizeof(PlannerStats), kPlannerAbiVersion}) {}
+    PathPlanner(const Matrix& nominalGatePositionAndType, const Matrix& nominalObstaclePosition,
+                std::shared_ptr<ConfigParser> configParser, AbiTag callerAbi);
 
     void parseGatesAndObstacles(const Matrix& nominalGatePositionAndType, const Matrix& nominalObstaclePosition);
     // The world build of parseGatesAndObstacles into any World (src/PathPlanner.cpp:60-78):
@@ -119,11 +137,12 @@ private:
     // rows_sym (optional): the caller's symmetrised search on its restricted rows, run while
     // the device builds the whole table's masked k-NN; when that shows no kept edge into the
     // goal and rows_sym found the path, *decided_on_rows = true and the table is neither
-    // downloaded nor searched (the caller takes its own path)
+    // downloaded nor searched (the caller takes its own path); *census_goal_edges (with
+    // rows_sym): the whole table's kept edges into the goal
     bool wholeTableSearch(const double* d_nodes, int32_t n, const double box_lo[3], const double box_hi[3], void* area,
                           std::vector<Vec3>& path, int64_t& edges_checked, int64_t& edges_valid, double& ms_dev,
                           double& ms_search, const std::function<bool()>* rows_sym = nullptr,
-                          bool* decided_on_rows = nullptr) const;
+                          bool* decided_on_rows = nullptr, int64_t* census_goal_edges = nullptr) const;
 
     std::shared_ptr<ConfigParser> configParser;
     uint64_t seed_ = 0x5eedull;

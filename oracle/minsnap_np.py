@@ -91,6 +91,69 @@ def solve(fixed: dict, n_vertices: int, times, dim: int) -> np.ndarray:
     return out
 
 
+def track_batch(wps, times, v0=(0, 0, 0), a0=(0, 0, 0), chunk: int = 256) -> np.ndarray:
+    """`track` for B problems of the same waypoint count W at once: wps (B, W, 3), times
+    (B, W - 1) -> coefficients (B, W - 1, 3, 10), increasing powers of t.  The same KKT
+    system in normalised time as `track`, assembled for the whole batch and solved by
+    batched LU (partial pivoting), `chunk` problems at a time.  This is the accuracy
+    reference ("truth") the GPU and the oracle are both measured against: 40-digit mpmath
+    agrees with it to ~1e-12 on the bench's problems (tests/test_oracle.py), where the
+    reference's own formulation (R = C^T A^-T Q A^-1 C in the monomial basis, H formed by
+    products whose terms cancel) loses ~7 digits."""
+    wps = np.asarray(wps, float)
+    B, W, dim = wps.shape
+    M = W - 1
+    T = np.asarray(times, float).reshape(B, M)
+    nv = N * M
+    Qu = _cost_unit()
+    # constraint structure: (kind, vertex, k) per row; rows are shared by the batch, only
+    # the 1/T^k scales and the right-hand sides differ
+    fixed = {(0, k) for k in range(5)} | {(v, 0) for v in range(1, M)} | {(M, k) for k in range(5)}
+    spec = []  # (seg_end or -1, seg_beg or -1, k, sign_beg, rhs source)
+    for v in range(W):
+        for k in range(5):
+            if (v, k) in fixed:
+                if v > 0:
+                    spec.append((v - 1, -1, k, (v, k)))
+                if v < M:
+                    spec.append((-1, v, k, (v, k)))
+            elif 0 < v < M:
+                spec.append((v - 1, v, k, None))
+    nc = len(spec)
+    ones, zeros = [_deriv_row(k, 1.0) for k in range(5)], [_deriv_row(k, 0.0) for k in range(5)]
+    v0, a0 = np.asarray(v0, float), np.asarray(a0, float)
+    out = np.zeros((B, M, dim, N))
+    for b0 in range(0, B, chunk):
+        b1 = min(B, b0 + chunk)
+        nb = b1 - b0
+        Tb = T[b0:b1]
+        kkt = np.zeros((nb, nv + nc, nv + nc))
+        for i in range(M):
+            kkt[:, N * i:N * i + N, N * i:N * i + N] = 2 * Qu[None] / Tb[:, i, None, None] ** (2 * K - 1)
+        rhs = np.zeros((nb, nv + nc, dim))
+        for r, (se, sb, k, src) in enumerate(spec):
+            row = np.zeros((nb, nv))
+            if se >= 0:
+                row[:, N * se:N * se + N] += ones[k][None] / Tb[:, se, None] ** k
+            if sb >= 0:
+                row[:, N * sb:N * sb + N] -= (zeros[k][None] / Tb[:, sb, None] ** k) * (1 if se >= 0 else -1)
+            kkt[:, nv + r, :nv] = row
+            kkt[:, :nv, nv + r] = row
+            if src is not None:
+                v, kk = src
+                if kk == 0:
+                    rhs[:, nv + r] = wps[b0:b1, v]
+                elif v == 0 and kk == 1:
+                    rhs[:, nv + r] = v0
+                elif v == 0 and kk == 2:
+                    rhs[:, nv + r] = a0
+        sol = np.linalg.solve(kkt, rhs)[:, :nv]
+        for i in range(M):
+            scale = Tb[:, i, None] ** -np.arange(N, dtype=float)[None]  # (nb, N)
+            out[b0:b1, i] = np.transpose(sol[:, N * i:N * i + N] * scale[:, :, None], (0, 2, 1))
+    return out
+
+
 def track(wp, times, v0=(0, 0, 0), a0=(0, 0, 0)) -> np.ndarray:
     """generateTrajectory vertex set: start {p, v0, a0, 0, 0}, inner {p}, end {p, 0, 0, 0, 0}."""
     wp = np.asarray(wp, float)

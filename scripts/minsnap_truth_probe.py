@@ -1,0 +1,67 @@
+"""Min-snap accuracy against the truth (GPU probe, round 6).
+
+The truth is oracle/minsnap_np.track_batch (KKT in normalised time, batched LU), pinned to
+a 40-digit mpmath solve of the reference's own formulation (tests/test_oracle.py).  Prints,
+for the bench's C5 batch (4096 x 12 segments, seeds 10000..) and for sweeps with shorter
+segments (waypoints scaled down), the GPU's and the oracle's max-abs coefficient error
+against the truth, and the single-track refit's rows against rows sampled from the truth.
+
+    python scripts/minsnap_truth_probe.py [n_sweep]
+"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "oracle"), os.path.join(ROOT, "efficient-path-planner_amd")]
+
+import numpy as np  # noqa: E402
+
+import minsnap_np as MN  # noqa: E402
+import oracle as O  # noqa: E402
+from eppamd import capi, synth  # noqa: E402
+
+
+def report(name, tracks, v=1.0, a=2.0):
+    t0 = time.time()
+    Ts, Cs, st = capi.minsnap_batch(list(tracks), v, a)
+    Tr, Cr, sr = O.minsnap_batch(list(tracks), v, a, threads=16)
+    truth = MN.track_batch(np.asarray(tracks), Tr)
+    eg = np.abs(np.asarray(Cs) - truth).reshape(len(tracks), -1).max(1)
+    eo = np.abs(np.asarray(Cr) - truth).reshape(len(tracks), -1).max(1)
+    scale = np.abs(truth).reshape(len(tracks), -1).max(1)
+    print(f"{name}: problems {len(tracks)} solved {(np.asarray(st) == 0).sum()} Tmin {np.min(Tr):.3g} "
+          f"coef max {scale.max():.3g} | gpu-truth max {eg.max():.3e} (p{eg.argmax()}) p99 {np.quantile(eg, .99):.3e} "
+          f"rel {np.max(eg / scale):.3e} | oracle-truth max {eo.max():.3e} p99 {np.quantile(eo, .99):.3e} | "
+          f"gpu-oracle max {np.abs(np.asarray(Cs) - np.asarray(Cr)).max():.3e} "
+          f"excess over oracle's own {np.max(np.abs(np.asarray(Cs) - np.asarray(Cr)).reshape(len(tracks), -1).max(1) - eo):.3e} "
+          f"({time.time() - t0:.1f} s)", flush=True)
+    return eg, eo
+
+
+def main():
+    n_sweep = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+    tracks = np.array([synth.random_track_waypoints(10_000 + k, 12) for k in range(4096)])
+    report("C5 bench batch", tracks)
+    rng = np.random.default_rng(6)
+    for sc in (0.3, 0.1, 0.03):
+        base = np.array([synth.random_track_waypoints(50_000 + k, 12) for k in range(n_sweep // 3)])
+        report(f"sweep scale {sc}", base * sc)
+    # mixed: each segment its own scale (short and long segments next to each other)
+    steps = rng.uniform(0.02, 3.0, (n_sweep // 3, 12, 1)) * rng.normal(size=(n_sweep // 3, 12, 3))
+    mixed = np.concatenate([np.zeros((n_sweep // 3, 1, 3)), np.cumsum(steps, axis=1)], axis=1)
+    report("sweep mixed lengths", mixed)
+    # single-track refit (k_refit) rows against rows sampled from the truth
+    worst = 0.0
+    for k in range(64):
+        wp = tracks[k]
+        rows = np.asarray(capi.generate_trajectory(wp, 1.0, 2.0, 0.1))
+        T, _ = O.minsnap_track(wp, 1.0, 2.0)
+        tr = MN.track_batch(wp[None], T[None])[0]
+        rr = O.sample_traj(T, tr, 0.1, t0=0.0)
+        worst = max(worst, float(np.abs(rows[:, :9] - rr[:, :9]).max()))
+    print(f"refit rows (64 tracks) vs rows from the truth: max abs {worst:.3e}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

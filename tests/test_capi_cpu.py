@@ -98,3 +98,40 @@ def test_sparse_byte_classes_match_the_class_table():
             assert r in (0, -1), r
             checked += r == 0
     assert checked >= 4
+
+
+def test_planner_abi_guard_rejects_stale_caller(tmp_path):
+    """epp/PathPlanner.h hands the caller's compiled sizes of PathPlanner / PlannerStats and
+    the layout version to the library's constructor (a stale tools/c5_native
+    segfaulted after PlannerStats grew).  A caller with another layout gets
+    std::runtime_error before anything else runs (no GPU needed).  The current header's own
+    tag passes: every GPU test constructs PathPlanner through it."""
+    import subprocess
+    src = tmp_path / "abi.cpp"
+    src.write_text(r'''
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include "epp/PathPlanner.h"
+int main() {
+    epp::Matrix g(0, 7), o(0, 6);
+    using Tag = epp::PathPlanner::AbiTag;
+    const Tag stale{(uint32_t)sizeof(epp::PathPlanner), (uint32_t)sizeof(epp::PlannerStats) - 8, epp::kPlannerAbiVersion};
+    const Tag old{(uint32_t)sizeof(epp::PathPlanner), (uint32_t)sizeof(epp::PlannerStats), epp::kPlannerAbiVersion - 1};
+    int rejected = 0;
+    for (const Tag& t : {stale, old}) {
+        try { epp::PathPlanner p(g, o, nullptr, t); } catch (const std::runtime_error& e) {
+            rejected += std::strstr(e.what(), "rebuild the caller") != nullptr; }
+    }
+    epp::PlannerStats s;
+    std::printf("%d %d\n", rejected, (int)(s.size == sizeof(epp::PlannerStats) && s.version == epp::kPlannerAbiVersion));
+    return 0;
+}
+''')
+    exe = tmp_path / "abi"
+    pkg = os.path.join(ROOT, "efficient-path-planner_amd")
+    subprocess.run(["g++", "-std=c++17", "-O0", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe),
+                    "-L", pkg, "-lepp", f"-Wl,-rpath,{pkg}"], check=True, capture_output=True, timeout=120)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.split() == ["2", "1"], out.stdout

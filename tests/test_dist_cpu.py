@@ -78,6 +78,23 @@ def test_bench_spawns_ranks_gloo_ws2():
     # the fields the GPU bench line carries for the multi-GPU leg: the communicator's own
     # rank count and every rank's value (full_plan.comm_n_ranks / ms_per_track_per_rank)
     assert r["comm_n_ranks"] == 2 and r["per_rank"] == [1.0, 2.0]
+    # the bench line's parity at N > 1 (bench.py rank_parity / reduce_parity): every rank's
+    # own counters, reduced -- sums of the mismatches, all-ranks of the equalities
+    p = r["parity"]
+    assert p["ranks"] == 2 and p["ok"] is True
+    assert p["per_rank"]["c2_batch0_mismatches"] == [0, 0] and p["per_rank"]["c2_batch0_compared"] == [4096, 4096]
+    assert p["c2_batch0_mismatches"] == 0 and p["c2_batch0_compared"] == 8192
+    assert p["gathered_set_equal"] is True and p["per_rank"]["gathered_set_equal"] == [True, True]
+    assert p["comm_n_ranks_equal"] is True
+
+
+def test_bench_parity_mismatch_on_one_rank_is_reported():
+    """One rank's mismatch reaches rank 0's line: its per-rank counter, the sum, ok false."""
+    import json
+    out = _run_bench_ws2(["--parity-flip-rank", "1"])
+    assert out.returncode == 0, out.stderr[-2000:]
+    p = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])["parity"]
+    assert p["per_rank"]["c2_batch0_mismatches"] == [0, 1] and p["c2_batch0_mismatches"] == 1 and p["ok"] is False
 
 
 def test_bench_rejects_mismatched_world_size():

@@ -723,6 +723,38 @@ def test_plan_once_equals_cpu_restatement(c1, seed, ellipse, monkeypatch):
     assert O.plan_once(w, rg, ro, lo, hi, start, blocked, 4096, seed, 16, False, 4)[0] is None
 
 
+@pytest.mark.parametrize("world", ["empty", "1100_obbs"])
+def test_plan_worlds_without_tile_tables(c1, geom, cfg, world):
+    """Worlds the rows' fused motion check does not take (no OBBs: no tile tables; 1,104
+    OBBs: records past the LDS budget) plan through the whole table with the default row
+    restriction on, in planPath and the batched planPaths alike (these threw),
+    and equal the CPU restatement."""
+    g0, o0, start, goal, *_ = c1
+    if world == "empty":
+        g, o = np.zeros((0, 7)), np.zeros((0, 6))
+    else:
+        rng = np.random.default_rng(3)
+        o = np.zeros((1100, 6))
+        o[:, 0] = rng.uniform(20, 60, 1100)  # (far outside the sampling box: they count, never hit)
+        o[:, 1] = rng.uniform(-20, 20, 1100)
+        o[:4] = o0
+        g = g0
+    rg, ro = config.inflate_radii(cfg)
+    w = O.world_build(geom, g, o, rg, ro)
+    pp = _ot().PathPlanner(g, o, CONFIG)
+    lo, hi = synth.C1_BOUNDS
+    for seed in (1, 2):
+        got = pp.plan_once(start, goal, 4096, seed)
+        exp, _ = O.plan_once(w, rg, ro, lo, hi, start, goal, 4096, seed, 16, False, 8)
+        assert got is not None and np.array_equal(got, exp), (world, seed)
+    st = pp.last_stats()
+    assert st["restricted_rows"] == 0 and st["fallbacks"] == 0
+    res = pp.plan_paths([(start, goal), (goal, start)], 0.5)
+    assert all(ok for ok, _ in res)
+    for ok, path in res:
+        _path_valid(path, w, rg, ro, False)
+
+
 def test_plan_once_symmetrised_on_rows_equals_cpu(bench_track_config, geom):
     """Goals outside the sampling box (the C4 box, track world 100, 65,536 samples): no
     sample keeps the goal among its 16 neighbours, so the forward search fails and the
