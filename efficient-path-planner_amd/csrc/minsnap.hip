@@ -146,7 +146,7 @@ __device__ __forceinline__ double ainv_entry(const double* kc, const double* ipo
 // Per-segment scratch (doubles): the R_pp blocks -- W (coupling to the next inner vertex,
 // then G = S^-1 E of the block solve) and L (diagonal block) -- and the powers of T.
 struct Seg {
-    static constexpr int kW = 0, kL = 16, kPow = 32, kSize = 44;
+    static constexpr int kW = 0, kL = 16, kPow = 32, kX = 44, kSize = 56;  // kX: refinement's saved x (12)
 };
 // kPow: (1/T)^0..(1/T)^9 (A^-1's and H's negative powers) then T (H's one positive power)
 constexpr int kNPow = 11;
@@ -172,7 +172,7 @@ template <int BLOCK, bool SCR_LDS>
 __device__ __forceinline__ int solve_track(const double* __restrict__ kc, const double* __restrict__ P, int M, double vmax, double amax,
                                            const double* v0, const double* a0, const double* times_in,
                                            double* scr, double* dv, double* rhs, double* Tm, double* xch,
-                                           int* s_err, double* T_out, double* C_out) {
+                                           int* s_err, double* T_out, double* C_out, bool refine) {
     const int tid = threadIdx.x;
     // ---- phase 1: segment times, powers of T, fixed vertex values ---------------
     // (one barrier: every thread of a segment's powers takes its time itself -- the
@@ -212,35 +212,46 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ kc, const 
     // kept in the L slot of segment v-1, the coupling E_v (v -> v+1) in the W slot.
     // Segment i's H (closed form, hess) couples vertex i (rows 0..4) and i+1 (rows 5..9).
     const int nin = M - 1;
-    for (int e = tid; e < nin * 16; e += BLOCK) {
-        const int v = 1 + e / 16, p = (e % 16) / 4, q = e % 4;
-        const double* pm = scr + (size_t)(v - 1) * Seg::kSize + Seg::kPow;
-        const double* pp = scr + (size_t)v * Seg::kSize + Seg::kPow;
-        scr[(size_t)(v - 1) * Seg::kSize + Seg::kL + p * 4 + q] = hess(kc, pm, 6 + p, 6 + q) + hess(kc, pp, 1 + p, 1 + q);
-        scr[(size_t)(v - 1) * Seg::kSize + Seg::kW + p * 4 + q] = (v < nin) ? hess(kc, pp, 1 + p, 6 + q) : 0.0;
-    }
-    for (int e = tid; e < nin * 12; e += BLOCK) {
-        const int v = 1 + e / 12, p = (e % 12) / 3, d = e % 3;
+    auto build_blocks = [&]() {
+        for (int e = tid; e < nin * 16; e += BLOCK) {
+            const int v = 1 + e / 16, p = (e % 16) / 4, q = e % 4;
+            const double* pm = scr + (size_t)(v - 1) * Seg::kSize + Seg::kPow;
+            const double* pp = scr + (size_t)v * Seg::kSize + Seg::kPow;
+            scr[(size_t)(v - 1) * Seg::kSize + Seg::kL + p * 4 + q] = hess(kc, pm, 6 + p, 6 + q) + hess(kc, pp, 1 + p, 1 + q);
+            scr[(size_t)(v - 1) * Seg::kSize + Seg::kW + p * 4 + q] = (v < nin) ? hess(kc, pp, 1 + p, 6 + q) : 0.0;
+        }
+    };
+    // b = -R_pf d_f, entry (v, p+1, d).  The two position columns of a segment enter as one
+    // difference: H x u = 0 for u = e_0 + e_5 (moving both ends' positions together moves the
+    // polynomial without changing its snap), so H[r][0] p_a + H[r][5] p_b = H[r][0] (p_a - p_b)
+    // -- the same value without the cancellation of two large terms when the positions are
+    // large next to their difference (hess(., 5) := -hess(., 0)).
+    auto rhs_entry = [&](int v, int p, int d) -> double {
         double s = 0.0;
         // segment v-1: rows 0..4 = vertex v-1, rows 5..9 = vertex v; row of (v,p+1) = 6+p
         {
             const double* pw = scr + (size_t)(v - 1) * Seg::kSize + Seg::kPow;
-            for (int r = 0; r < N; ++r) {
+            s = hess(kc, pw, 6 + p, 0) * (dv[((v - 1) * HALF) * 3 + d] - dv[(v * HALF) * 3 + d]);
+            for (int r = 1; r < N; ++r) {
                 const int vv = (r < HALF) ? v - 1 : v, k = r % HALF;
-                const bool fixed = (k == 0) || vv == 0 || vv == M;
-                if (fixed) s = s + hess(kc, pw, 6 + p, r) * dv[(vv * HALF + k) * 3 + d];
+                if (k != 0 && (vv == 0 || vv == M)) s = s + hess(kc, pw, 6 + p, r) * dv[(vv * HALF + k) * 3 + d];
             }
         }
         // segment v: rows 0..4 = vertex v (row of (v,p+1) = 1+p), rows 5..9 = vertex v+1
         {
             const double* pw = scr + (size_t)v * Seg::kSize + Seg::kPow;
-            for (int r = 0; r < N; ++r) {
+            s = s + hess(kc, pw, 1 + p, 0) * (dv[(v * HALF) * 3 + d] - dv[((v + 1) * HALF) * 3 + d]);
+            for (int r = 1; r < N; ++r) {
                 const int vv = (r < HALF) ? v : v + 1, k = r % HALF;
-                const bool fixed = (k == 0) || vv == 0 || vv == M;
-                if (fixed) s = s + hess(kc, pw, 1 + p, r) * dv[(vv * HALF + k) * 3 + d];
+                if (k != 0 && (vv == 0 || vv == M)) s = s + hess(kc, pw, 1 + p, r) * dv[(vv * HALF + k) * 3 + d];
             }
         }
-        rhs[(v * 4 + p) * 3 + d] = -s;
+        return -s;
+    };
+    build_blocks();
+    for (int e = tid; e < nin * 12; e += BLOCK) {
+        const int v = 1 + e / 12, p = (e % 12) / 3, d = e % 3;
+        rhs[(v * 4 + p) * 3 + d] = rhs_entry(v, p, d);
     }
     block_sync<SCR_LDS>();
     EPP_TL(5);
@@ -273,6 +284,7 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ kc, const 
     // G_v / H_v are kept in segment v-1's L slot (D_v is consumed by then), g_v / h_v in
     // rhs[v].  xch: per group (base 48 g) S|y [0,28), adj(S) [28,44); x buffers
     // [96 + 24 g, +24).
+    auto block_solve = [&]() {
     if (tid < kWave && nin > 0) {
         const int L = tid & 31, grp = tid >> 5;
         const bool mat = L < 16, act = L < 28;
@@ -421,10 +433,46 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ kc, const 
         }
         EPP_TLI(63);
     }
+    };
+    block_solve();
     block_sync<SCR_LDS>();
     EPP_TL(6);
     EPP_TLC(15);
     if (*s_err) return -3;
+    // ---- one step of iterative refinement (refine): r = b - R_pp x (the closed-form blocks
+    // again: the solve consumed the L slots), R_pp dx = r by the same elimination, x += dx.
+    // The elimination's rounding is amplified by R_pp's condition (up to ~1e12 next to very
+    // short segments); one step brings the solution to the accuracy of the data.
+    if (refine && nin > 0) {
+        for (int e = tid; e < nin * 12; e += BLOCK) {
+            const int v = 1 + e / 12, p = (e % 12) / 3, d = e % 3;
+            const double* pm = scr + (size_t)(v - 1) * Seg::kSize + Seg::kPow;  // segment v-1
+            const double* pp = scr + (size_t)v * Seg::kSize + Seg::kPow;        // segment v
+            double r = rhs_entry(v, p, d);
+            for (int q = 0; q < 4; ++q) {
+                r = r - (hess(kc, pm, 6 + p, 6 + q) + hess(kc, pp, 1 + p, 1 + q)) * dv[(v * HALF + 1 + q) * 3 + d];
+                if (v < nin) r = r - hess(kc, pp, 1 + p, 6 + q) * dv[((v + 1) * HALF + 1 + q) * 3 + d];
+                if (v > 1) r = r - hess(kc, pm, 1 + q, 6 + p) * dv[((v - 1) * HALF + 1 + q) * 3 + d];
+            }
+            rhs[(v * 4 + p) * 3 + d] = r;
+        }
+        block_sync<SCR_LDS>();
+        for (int e = tid; e < nin * 12; e += BLOCK) {  // x kept in the segments' X slots
+            const int v = 1 + e / 12, p = (e % 12) / 3, d = e % 3;
+            scr[(size_t)(v - 1) * Seg::kSize + Seg::kX + p * 3 + d] = dv[(v * HALF + 1 + p) * 3 + d];
+        }
+        build_blocks();
+        block_sync<SCR_LDS>();
+        block_solve();
+        block_sync<SCR_LDS>();
+        if (*s_err) return -3;
+        for (int e = tid; e < nin * 12; e += BLOCK) {
+            const int v = 1 + e / 12, p = (e % 12) / 3, d = e % 3;
+            double& x = dv[(v * HALF + 1 + p) * 3 + d];
+            x = scr[(size_t)(v - 1) * Seg::kSize + Seg::kX + p * 3 + d] + x;
+        }
+        block_sync<SCR_LDS>();
+    }
     // ---- phase 4: p_i = A_i^-1 [d_i ; d_{i+1}] -------------------------------------
     for (int e = tid; e < M * 30; e += BLOCK) {
         const int i = e / 30, d = (e % 30) / 10, r = e % 10;
@@ -434,10 +482,13 @@ __device__ __forceinline__ int solve_track(const double* __restrict__ kc, const 
         if (r < HALF) {  // rows 0..4 of A^-1: diag(1 / r!)
             s = kc[kCF + r] * d0[3 * r];
         } else {  // rows 5..9: [K | B5^-1] row rr, column c scaled by (1/T)^(rr + 5 - c % 5)
+            // (the two positions as one difference: K[rr][0] = -B5^-1[rr][0], A^-1 maps equal
+            // end positions to a constant polynomial)
             const int rr = r - HALF;
-            s = 0.0;
+            s = kc[kCK + rr * HALF] * ipow[rr + HALF] * (d0[0] - d0[3 * HALF]);
 #pragma unroll
-            for (int k = 0; k < N; ++k) {
+            for (int k = 1; k < N; ++k) {
+                if (k == HALF) continue;
                 const double a = (k < HALF ? kc[kCK + rr * HALF + k] : kc[kCB5 + rr * HALF + k - HALF]) *
                                  ipow[rr + HALF - k % HALF];
                 s = s + a * d0[3 * k];
@@ -483,7 +534,7 @@ __global__ __launch_bounds__(BLOCK) void k_minsnap(const double* __restrict__ wp
     __syncthreads();
     const int st = solve_track<BLOCK, LDS>(kc, wp + (size_t)w0 * 3, M, vmax, amax, v0 ? v0 + 3 * track : nullptr,
                                       a0 ? a0 + 3 * track : nullptr, times_in ? times_in + seg0 : nullptr, scr, dv, rhs,
-                                      Tm, Tm + M, s_err, seg_times + seg0, coeffs + (size_t)seg0 * 30);
+                                      Tm, Tm + M, s_err, seg_times + seg0, coeffs + (size_t)seg0 * 30, true);
     if (threadIdx.x == 0 && status) status[track] = st;
 }
 
@@ -702,6 +753,7 @@ struct RefitArgs {
     double* scratch;   // device: G x segment scratch (tracks longer than kMaxLdsSeg)
     int32_t big;       // (!LDS) the vertex values, right-hand sides, times and coefficients
                        // in the global scratch too (tracks whose LDS part would not fit)
+    int32_t refine;    // one step of iterative refinement in the solve (solve_track)
     double small[3 * kRefitArgW + 6 + kRefitArgW - 1];  // wp | v0 | a0 | T when W <= kRefitArgW
 };
 constexpr int kRefitBlock = 256;
@@ -787,7 +839,7 @@ __device__ __forceinline__ void refit_body(const RefitArgs& a, int g, double* sm
     block_sync<LDS>();
     EPP_TL(8);
     const int st = solve_track<kRefitBlock, LDS>(kc, P, M, 0.0, 0.0, P + 3 * W, P + 3 * W + 3, P + 3 * W + 6, scr, dv,
-                                            rhs, Tm, xch, s_err, nullptr, C);
+                                            rhs, Tm, xch, s_err, nullptr, C, a.refine != 0);
     EPP_TL(7);
     if (tid < cnt0) {
         s_tin[tid] = f_tin;
@@ -1267,6 +1319,13 @@ epp_status epp::check_and_generate_into(const FusedCheck* chk, const double* wp,
     a.out = reinterpret_cast<double*>(c.h_out + rows_at);
     a.scratch = c.d_scr;
     a.big = big ? 1 : 0;
+    {  // one refinement step in the solve (EPP_REFIT_REFINE=0: without, an A/B knob)
+        static const int refine = [] {
+            const char* e = std::getenv("EPP_REFIT_REFINE");
+            return e && *e == '0' ? 0 : 1;
+        }();
+        a.refine = refine;
+    }
     a.info[0] = -100;
     size_t shm = refit_lds_doubles(M, lds, big) * sizeof(double);
     if (Gc > 0) {

@@ -11,6 +11,10 @@ from the KKT system of
 
 in time-normalised coordinates (tau = t / T_i) for conditioning.  Agreement of the
 two formulations to ~1e-9 cross-checks the oracle (see tests/test_oracle.py).
+
+track_batch_refined is the accuracy reference ("truth") the GPU and the oracle are
+measured against: the reference's own formulation in long double with iterative
+refinement, pinned to 40-digit mpmath.
 """
 from __future__ import annotations
 
@@ -95,11 +99,10 @@ def track_batch(wps, times, v0=(0, 0, 0), a0=(0, 0, 0), chunk: int = 256) -> np.
     """`track` for B problems of the same waypoint count W at once: wps (B, W, 3), times
     (B, W - 1) -> coefficients (B, W - 1, 3, 10), increasing powers of t.  The same KKT
     system in normalised time as `track`, assembled for the whole batch and solved by
-    batched LU (partial pivoting), `chunk` problems at a time.  This is the accuracy
-    reference ("truth") the GPU and the oracle are both measured against: 40-digit mpmath
-    agrees with it to ~1e-12 on the bench's problems (tests/test_oracle.py), where the
-    reference's own formulation (R = C^T A^-T Q A^-1 C in the monomial basis, H formed by
-    products whose terms cancel) loses ~7 digits."""
+    batched LU (partial pivoting), `chunk` problems at a time.  An independent formulation
+    (a cross-check of track_batch_refined, the accuracy reference): 40-digit mpmath agrees
+    with it to ~4e-12 on most of the bench's problems, but it is off by up to ~3e-9 on a
+    few (its KKT matrix is indefinite and pivoted across scales)."""
     wps = np.asarray(wps, float)
     B, W, dim = wps.shape
     M = W - 1
@@ -152,6 +155,110 @@ def track_batch(wps, times, v0=(0, 0, 0), a0=(0, 0, 0), chunk: int = 256) -> np.
             scale = Tb[:, i, None] ** -np.arange(N, dtype=float)[None]  # (nb, N)
             out[b0:b1, i] = np.transpose(sol[:, N * i:N * i + N] * scale[:, :, None], (0, 2, 1))
     return out
+
+
+_LD_CONSTS = None
+
+
+def _ld_consts():
+    """Hc (H = A^-T Q A^-1 at T = 1) and A^-1 at T = 1 in long double, from exact rational
+    arithmetic (every entry is a ratio of factorials)."""
+    global _LD_CONSTS
+    if _LD_CONSTS is None:
+        from fractions import Fraction as F
+        A = [[F(0)] * N for _ in range(N)]
+        for k in range(5):
+            A[k][k] = F(factorial(k))
+            for j in range(k, N):
+                A[5 + k][j] = F(factorial(j), factorial(j - k))
+        # exact inverse by Gauss-Jordan over the rationals
+        aug = [row[:] + [F(int(i == r)) for i in range(N)] for r, row in enumerate(A)]
+        for c in range(N):
+            piv = next(r for r in range(c, N) if aug[r][c] != 0)
+            aug[c], aug[piv] = aug[piv], aug[c]
+            pv = aug[c][c]
+            aug[c] = [x / pv for x in aug[c]]
+            for r in range(N):
+                if r != c and aug[r][c] != 0:
+                    f = aug[r][c]
+                    aug[r] = [x - f * y for x, y in zip(aug[r], aug[c])]
+        Ai = [row[N:] for row in aug]
+        Q = [[F(0)] * N for _ in range(N)]
+        for a in range(K, N):
+            for b in range(K, N):
+                Q[a][b] = F(factorial(a) // factorial(a - K) * (factorial(b) // factorial(b - K)), a + b - 7)
+        H = [[sum(Ai[a][r] * Q[a][b] * Ai[b][c] for a in range(N) for b in range(N)) for c in range(N)]
+             for r in range(N)]
+
+        def ld(x):
+            return np.longdouble(x.numerator) / np.longdouble(x.denominator)
+        _LD_CONSTS = (np.array([[ld(x) for x in row] for row in H], dtype=np.longdouble),
+                      np.array([[ld(x) for x in row] for row in Ai], dtype=np.longdouble))
+    return _LD_CONSTS
+
+
+def track_batch_refined(wps, times, v0=(0, 0, 0), a0=(0, 0, 0), iters: int = 3) -> np.ndarray:
+    """The accuracy reference ("truth"): the reference's own formulation
+    (impl/polynomial_optimization_linear_impl.h:111-379: H_i = A_i^-T Q_i A_i^-1 with
+    H[r][c] = Hc[r][c] T^((r%5)+(c%5)-7), R_pp d_p = -R_pf d_f over the inner vertices'
+    derivatives 1..4, p_i = A_i^-1 d_i) with every entry and product in long double (64-bit
+    mantissa) from exact rational constants, solved in doubles and refined `iters` times
+    against the long-double residual.  Pinned to 40-digit mpmath (tests/test_oracle.py):
+    ~1e-13 on the bench's problems, where the double-precision KKT of `track_batch` is off
+    by up to ~3e-9 on some of them.  wps (B, W, 3), times (B, W - 1) -> (B, W - 1, 3, 10)."""
+    Hc, Ai = _ld_consts()
+    wps = np.asarray(wps, np.longdouble)
+    B, W, dim = wps.shape
+    M = W - 1
+    T = np.asarray(times, np.float64).reshape(B, M).astype(np.longdouble)
+    nin = M - 1
+    # vertex values dv[b, v, k, d]: fixed ones now, the free ones from the solve
+    dv = np.zeros((B, W, 5, dim), np.longdouble)
+    dv[:, :, 0] = wps
+    dv[:, 0, 1] = np.asarray(v0, np.longdouble)
+    dv[:, 0, 2] = np.asarray(a0, np.longdouble)
+    tp = {e: T ** e for e in range(-9, 2)}  # T^e per segment, (B, M)
+
+    def hs(seg, r, c):  # H_seg[r][c], (B,)
+        return Hc[r, c] * tp[(r % 5) + (c % 5) - 7][:, seg]
+    if nin > 0:
+        n = 4 * nin
+        R = np.zeros((B, n, n), np.longdouble)
+        rhs = np.zeros((B, n, dim), np.longdouble)
+        for v in range(1, M):
+            for p in range(4):
+                for q in range(4):
+                    R[:, 4 * (v - 1) + p, 4 * (v - 1) + q] = hs(v - 1, 6 + p, 6 + q) + hs(v, 1 + p, 1 + q)
+                    if v < nin:
+                        R[:, 4 * (v - 1) + p, 4 * v + q] = hs(v, 1 + p, 6 + q)
+                        R[:, 4 * v + q, 4 * (v - 1) + p] = hs(v, 1 + p, 6 + q)
+                s = np.zeros((B, dim), np.longdouble)
+                for seg, ro, vb in ((v - 1, 6, v - 1), (v, 1, v)):
+                    for r in range(N):
+                        vv, k = vb + (1 if r >= 5 else 0), r % 5
+                        if k == 0 or vv == 0 or vv == M:
+                            s += hs(seg, ro + p, r)[:, None] * dv[:, vv, k]
+                rhs[:, 4 * (v - 1) + p] = -s
+        R64 = R.astype(np.float64)
+        x = np.linalg.solve(R64, rhs.astype(np.float64)).astype(np.longdouble)
+        for _ in range(iters):
+            res = rhs - np.einsum("bij,bjd->bid", R, x)
+            x += np.linalg.solve(R64, res.astype(np.float64)).astype(np.longdouble)
+        for v in range(1, M):
+            dv[:, v, 1:5] = x[:, 4 * (v - 1):4 * v]
+    out = np.zeros((B, M, dim, N), np.longdouble)
+    for i in range(M):
+        d0 = np.concatenate([dv[:, i], dv[:, i + 1]], axis=1)  # (B, 10, dim)
+        for r in range(N):
+            if r < 5:
+                out[:, i, :, r] = Ai[r, r] * d0[:, r]
+            else:
+                s = np.zeros((B, dim), np.longdouble)
+                for k in range(N):
+                    if Ai[r, k] != 0:
+                        s += (Ai[r, k] * tp[(k % 5) - r][:, i])[:, None] * d0[:, k]
+                out[:, i, :, r] = s
+    return out.astype(np.float64)
 
 
 def track(wp, times, v0=(0, 0, 0), a0=(0, 0, 0)) -> np.ndarray:

@@ -1,7 +1,7 @@
 """Min-snap accuracy against the truth (GPU probe, round 6).
 
-The truth is oracle/minsnap_np.track_batch (KKT in normalised time, batched LU), pinned to
-a 40-digit mpmath solve of the reference's own formulation (tests/test_oracle.py).  Prints,
+The truth is oracle/minsnap_np.track_batch_refined (the reference's formulation in long
+double with iterative refinement), pinned to a 40-digit mpmath solve (tests/test_oracle.py).  Prints,
 for the bench's C5 batch (4096 x 12 segments, seeds 10000..) and for sweeps with shorter
 segments (waypoints scaled down), the GPU's and the oracle's max-abs coefficient error
 against the truth, and the single-track refit's rows against rows sampled from the truth.
@@ -26,7 +26,7 @@ def report(name, tracks, v=1.0, a=2.0):
     t0 = time.time()
     Ts, Cs, st = capi.minsnap_batch(list(tracks), v, a)
     Tr, Cr, sr = O.minsnap_batch(list(tracks), v, a, threads=16)
-    truth = MN.track_batch(np.asarray(tracks), Tr)
+    truth = MN.track_batch_refined(np.asarray(tracks), Tr)
     eg = np.abs(np.asarray(Cs) - truth).reshape(len(tracks), -1).max(1)
     eo = np.abs(np.asarray(Cr) - truth).reshape(len(tracks), -1).max(1)
     scale = np.abs(truth).reshape(len(tracks), -1).max(1)
@@ -57,7 +57,7 @@ def main():
         wp = tracks[k]
         rows = np.asarray(capi.generate_trajectory(wp, 1.0, 2.0, 0.1))
         T, _ = O.minsnap_track(wp, 1.0, 2.0)
-        tr = MN.track_batch(wp[None], T[None])[0]
+        tr = MN.track_batch_refined(wp[None], T[None])[0]
         rr = O.sample_traj(T, tr, 0.1, t0=0.0)
         worst = max(worst, float(np.abs(rows[:, :9] - rr[:, :9]).max()))
     print(f"refit rows (64 tracks) vs rows from the truth: max abs {worst:.3e}", flush=True)
