@@ -388,6 +388,26 @@ def committed_traffic():
     return None, None
 
 
+def committed_motions_valu():
+    """Per-launch VALU instruction counts of the C3 motion kernels (analytic, discrete32)
+    from the newest committed profiles/rNN_motions_valu.json (scripts/gpu_pmc_motions.sh ->
+    scripts/motions_valu.py: rocprofv3 --pmc passes over the same C3 launch)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_motions_valu.json")))
+    if not files:
+        return None, None
+    try:
+        d = json.load(open(files[-1]))
+    except (OSError, ValueError):
+        return None, None
+    out = {}
+    for name, v in d.items():
+        if "true>" in name:  # (the planner's k-NN-table form)
+            continue
+        out.setdefault(v.get("mode"), v)
+    return out, os.path.relpath(files[-1], ROOT)
+
+
 def full_plan(dist, rank, reps):
     """C4: plan this rank's track end to end (OnlineTrajGenerator.preComputeTraj), time it,
     all-gather the waypoint sets through the product's RCCL communicator.  Returns the
@@ -553,7 +573,19 @@ def side_measurements(capi, L, stream, geom, cfg, rg, ro):
                     "hbm_frac": BYTES_PER_EDGE * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
         capi.check(L.epp_stream_sync(stream))
         parity_gpu[key] = dv.download(np.uint8, C3_CPU_EDGES[mode])  # (the prefix the CPU leg checks)
-    res["c3_motion_discrete32"]["point_checks_per_s"] = 32 * res["c3_motion_discrete32"]["edges_per_s"]
+    # (point-equivalents: 32 step points per edge, the work a plain discretised validator
+    # does; the kernel itself evaluates only the 1-3 steps per candidate pair that can hit)
+    res["c3_motion_discrete32"]["point_equivalents_per_s"] = 32 * res["c3_motion_discrete32"]["edges_per_s"]
+    # the VALU roofline of the two motion kernels (VALU-issue bound, not HBM): per-launch
+    # instruction counts from the newest committed PMC summary, over this run's duration
+    valu, valu_src = committed_motions_valu()
+    for key, mode in (("c3_motion_analytic", "analytic"), ("c3_motion_discrete32", "discrete32")):
+        v = valu.get(mode) if valu else None
+        if v:
+            s_ = res[key]["kernel_ms"] * 1e-3
+            res[key]["valu_issue_frac"] = v["valu_issue_cycles_per_launch"] / (s_ * 2.4e9 * 1024)
+            res[key]["fp64_frac"] = v["fp64_flops_per_launch"] / s_ / 78.6e12
+            res[key]["valu_source"] = valu_src
     # C5 batched: 4096 independent 12-segment refits per launch
     nt = 4096
     tracks = [synth.random_track_waypoints(10_000 + k, 12) for k in range(nt)]

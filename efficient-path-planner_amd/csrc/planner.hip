@@ -2215,11 +2215,30 @@ __global__ __launch_bounds__(256) void k_pb_knn_scatter(PlanBatchDev P) {
 // by a wave scan of their lengths, kU candidates per lane in flight.  Returns false when
 // the radius would leave the grid ellipsoid or the list overflows (the row is then not
 // exact, and the caller flags the problem).
+#ifdef EPP_PB_ROWS_TL
+// (diagnostics builds only: -DEPP_PB_ROWS_TL, scripts/pb_rows_timeline.py) per listed query
+// d < kPbTl, lane 0's s_memrealtime (100 MHz) stamps: [0] query start, [1] first radius's
+// run starts loaded, [2] its candidates listed, [3] row written, [4] radius iterations |
+// candidates << 8 | wave << 32, [5] the wave's start
+constexpr int kPbTl = 1 << 15;
+__device__ unsigned long long g_pb_rows_tl[kPbTl][6];
+#define EPP_PBTL(d, k, v)                                                     \
+    do {                                                                      \
+        if ((threadIdx.x & 63) == 0 && (d) < kPbTl) g_pb_rows_tl[(d)][(k)] = (v); \
+    } while (0)
+#define EPP_PBTL_NOW() __builtin_amdgcn_s_memrealtime()
+#else
+#define EPP_PBTL(d, k, v) \
+    do {                  \
+    } while (0)
+#define EPP_PBTL_NOW() 0ull
+#endif
+
 template <int K>
 __device__ __forceinline__ bool pb_query_row(const KnnGrid& g, const double* __restrict__ sxyz,
                                              const int* __restrict__ sidx, const int* __restrict__ start,
                                              const double (&p)[3], double f, double gbound, int self,
-                                             int32_t* __restrict__ out, int64_t off) {
+                                             int32_t* __restrict__ out, int64_t off, int tl_d = 0) {
     constexpr int kCap = 512;
 #ifndef EPP_PB_KU  // (A/B builds may override)
 #define EPP_PB_KU 2
@@ -2266,6 +2285,10 @@ __device__ __forceinline__ bool pb_query_row(const KnnGrid& g, const double* __r
                     len = start[a + x1 + 1] - s0;
                 }
             }
+            if (it == 0 && rb0 == 0) {
+                [[maybe_unused]] const int lv = __shfl(len, 0, 64);  // (waits for the loads)
+                EPP_PBTL(tl_d, 1, EPP_PBTL_NOW() + (unsigned long long)(lv & 0));
+            }
             int incl = len;  // inclusive scan of the run lengths over the lanes
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
@@ -2304,6 +2327,8 @@ __device__ __forceinline__ bool pb_query_row(const KnnGrid& g, const double* __r
                 }
             }
         }
+        if (it == 0) EPP_PBTL(tl_d, 2, EPP_PBTL_NOW());
+        EPP_PBTL(tl_d, 4, (unsigned long long)(it + 1) | ((unsigned long long)cnt << 8));
         if (cnt > kCap) return false;
         if (cnt < K) continue;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's list is complete
@@ -2366,8 +2391,11 @@ __global__ __launch_bounds__(64) void k_pb_rows(PlanBatchDev P) {
     };
     int p_n = 0, self_n = 0;
     double pt_n[3] = {0.0, 0.0, 0.0};
+    [[maybe_unused]] const unsigned long long tl_w0 = EPP_PBTL_NOW();
     if (wave < D) locate(wave, p_n, self_n, pt_n);
     for (int d = wave; d < D; d += nwaves) {  // wave-uniform
+        EPP_PBTL(d, 0, EPP_PBTL_NOW());
+        EPP_PBTL(d, 5, tl_w0);
         const int p = p_n, self = self_n;
         const double pt[3] = {pt_n[0], pt_n[1], pt_n[2]};
         if (d + nwaves < D) locate(d + nwaves, p_n, self_n, pt_n);
@@ -2377,10 +2405,15 @@ __global__ __launch_bounds__(64) void k_pb_rows(PlanBatchDev P) {
         const KnnGrid g = *ks.g;
         const double f = pb_ellipse(q, pt);
         if (lane == 0) P.ids32[d] = (int32_t)(off + self);
-        if (!pb_query_row<K>(g, ks.sxyz, ks.sidx, ks.start, pt, f, q.gbound, self, P.rows32 + (int64_t)d * K, off)) {
+        if (!pb_query_row<K>(g, ks.sxyz, ks.sidx, ks.start, pt, f, q.gbound, self, P.rows32 + (int64_t)d * K, off, d)) {
             if (lane == 0) pb_ctr(P, kFInexact, p) = 1ull;
             if (lane < K) P.rows32[(int64_t)d * K + lane] = -1;  // (the problem takes the whole table)
         }
+#ifdef EPP_PB_ROWS_TL
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        EPP_PBTL(d, 3, EPP_PBTL_NOW());
+        if ((threadIdx.x & 63) == 0 && d < kPbTl) g_pb_rows_tl[d][4] |= (unsigned long long)wave << 32;
+#endif
     }
 }
 
@@ -2659,6 +2692,14 @@ epp_status epp_knn(const double* nodes, int32_t n, int32_t k, double max_dist, i
 }
 
 uint64_t epp_knn_workspace_size(int32_t n) { return n <= 0 ? 0 : (uint64_t)knn_layout(n).bytes; }
+
+#ifdef EPP_PB_ROWS_TL
+// (diagnostics builds only) the last k_pb_rows launch's per-query stamps: 6 u64 each
+epp_status epp_dbg_pb_rows_tl(unsigned long long* out, int64_t n) {
+    if (n > kPbTl) n = kPbTl;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pb_rows_tl), (size_t)n * 48) == hipSuccess ? EPP_OK : EPP_ERR_HIP;
+}
+#endif
 
 #ifdef EPP_KNN_DIAG
 // (diagnostics builds only) the last k_knn_tile launch's phase timeline: 16 u64 per block

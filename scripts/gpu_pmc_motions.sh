@@ -17,4 +17,10 @@ for P in "$P1" "$P2" "$P3"; do
   tail -2 gpurun_out/mpmc$i.log
   [ $rc -ne 0 ] && { echo "pass $i ended with $rc"; exit $rc; }
 done
+rm -rf gpurun_out/mkt
+timeout -s KILL 90 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/mkt -o run -- python3 scripts/motions_run.py > gpurun_out/mkt.log 2>&1 || { echo "kernel trace failed"; exit 1; }
+python3 scripts/pmc_summary.py gpurun_out/mpmc1 k_motions_v5 > gpurun_out/motions_pmc.txt
+python3 scripts/pmc_summary.py gpurun_out/mpmc2 k_motions_v5 >> gpurun_out/motions_pmc.txt
+python3 scripts/pmc_summary.py gpurun_out/mpmc3 k_motions_v5 >> gpurun_out/motions_pmc.txt
+python3 scripts/motions_valu.py gpurun_out/motions_valu.json
 echo done
