@@ -31,6 +31,7 @@
 
 #include "cached_ws.h"
 #include "epp_internal.h"
+#include "minsnap_consts.h"
 #include "small_body.h"
 
 namespace epp {
@@ -936,74 +937,21 @@ epp_status ensure_consts() {
         for (int i = N - 1 - order; i < N; ++i) B[n][i] = (order - (N - 1) + i) * B[n - 1][i];
         order--;
     }
-    // B5 = B[k][j+5] (5x5), inverted by Gauss-Jordan in long double; K from it (closed-form
-    // mapping inverse, ainv_entry)
-    long double G[HALF][2 * HALF];
-    for (int k = 0; k < HALF; ++k)
-        for (int j = 0; j < 2 * HALF; ++j) G[k][j] = j < HALF ? (long double)B[k][j + HALF] : (j - HALF == k ? 1.0L : 0.0L);
-    for (int col = 0; col < HALF; ++col) {
-        int p = col;
-        for (int r = col + 1; r < HALF; ++r)
-            if (std::fabs((double)G[r][col]) > std::fabs((double)G[p][col])) p = r;
-        for (int j = 0; j < 2 * HALF; ++j) std::swap(G[col][j], G[p][j]);
-        const long double piv = G[col][col];
-        for (int j = 0; j < 2 * HALF; ++j) G[col][j] /= piv;
-        for (int r = 0; r < HALF; ++r)
-            if (r != col) {
-                const long double f = G[r][col];
-                for (int j = 0; j < 2 * HALF; ++j) G[r][j] -= f * G[col][j];
-            }
-    }
-    double B5inv[HALF][HALF], K[HALF][HALF];
-    long double fact = 1.0L;
-    for (int c = 0; c < HALF; ++c) {
-        if (c > 0) fact *= c;
-        for (int r = 0; r < HALF; ++r) {
-            long double s = 0.0L;
-            for (int k = 0; k <= c; ++k) s += G[r][HALF + k] * (long double)B[k][c];
-            K[r][c] = (double)(-s / fact);
-        }
-    }
-    for (int r = 0; r < HALF; ++r)
-        for (int c = 0; c < HALF; ++c) B5inv[r][c] = (double)G[r][HALF + c];
+    // B5^-1, K (the closed-form mapping inverse, ainv_entry) and Hc (see hess): exact
+    // rationals rounded once to double (minsnap_consts.h, scripts/gen_minsnap_consts.py).
+    // (Round 5 derived them here in long double; Hc's products cancel, and some entries
+    // were ~3e-13 off -- data error the solve amplified to ~1e-9 in the coefficients.)
     double cc[kNC] = {};
     for (int k = 0; k < N; ++k)
         for (int j = 0; j < N; ++j) cc[kCB + k * N + j] = B[k][j];
     for (int r = 0; r < HALF; ++r)
         for (int c = 0; c < HALF; ++c) {
-            cc[kCB5 + r * HALF + c] = B5inv[r][c];
-            cc[kCK + r * HALF + c] = K[r][c];
+            cc[kCB5 + r * HALF + c] = minsnap_consts::kB5inv[r * HALF + c];
+            cc[kCK + r * HALF + c] = minsnap_consts::kK[r * HALF + c];
         }
     const double inv_fact[HALF] = {1.0, 1.0, 1.0 / 2.0, 1.0 / 6.0, 1.0 / 24.0};
     for (int r = 0; r < HALF; ++r) cc[kCF + r] = inv_fact[r];
-    // Hc (see hess): the constant parts of rows 4..9 of A^-1 (ainv_entry) and of Q's snap
-    // block (B[4][a] B[4][b] 2 / (a+b-7), impl :567-583), multiplied out in long double
-    long double Ac[N][N] = {}, Qc[N][N] = {};
-    Ac[4][4] = 1.0L / 24.0L;
-    for (int a = HALF; a < N; ++a)
-        for (int c = 0; c < N; ++c) {
-            const int rr = a - HALF;
-            long double kv = 0.0L;
-            if (c < HALF) {
-                long double f = 1.0L;
-                for (int q = 2; q <= c; ++q) f *= q;
-                for (int k = 0; k <= c; ++k) kv += G[rr][HALF + k] * (long double)B[k][c];
-                kv = -kv / f;
-            } else {
-                kv = G[rr][HALF + c - HALF];
-            }
-            Ac[a][c] = kv;
-        }
-    for (int a = 4; a < N; ++a)
-        for (int b = 4; b < N; ++b)
-            Qc[a][b] = (long double)B[4][a] * (long double)B[4][b] * 2.0L / (long double)(a + b - 7);
-    for (int r = 0; r < N; ++r)
-        for (int c = 0; c < N; ++c) {
-            long double h = 0.0L;
-            for (int a = 4; a < N; ++a)
-                for (int b = 4; b < N; ++b) h += Ac[a][r] * Qc[a][b] * Ac[b][c];
-            cc[kCH + r * N + c] = (double)h;
-        }
+    for (int i = 0; i < N * N; ++i) cc[kCH + i] = minsnap_consts::kHc[i];
     hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(cC), cc, sizeof(cc));
     if (e != hipSuccess) {
         set_error(std::string("epp minsnap: constants: ") + hipGetErrorString(e));
@@ -1319,10 +1267,12 @@ epp_status epp::check_and_generate_into(const FusedCheck* chk, const double* wp,
     a.out = reinterpret_cast<double*>(c.h_out + rows_at);
     a.scratch = c.d_scr;
     a.big = big ? 1 : 0;
-    {  // one refinement step in the solve (EPP_REFIT_REFINE=0: without, an A/B knob)
+    {  // the latency path solves without the refinement step: it cost 6-7 us of a ~30 us
+       // call (scripts/refit_ab.py) for ~1e-10 of accuracy the sampled rows do not need
+       // (rows vs the truth 6e-11 either way).  EPP_REFIT_REFINE=1: with it (A/B knob)
         static const int refine = [] {
             const char* e = std::getenv("EPP_REFIT_REFINE");
-            return e && *e == '0' ? 0 : 1;
+            return e && *e == '1' ? 1 : 0;
         }();
         a.refine = refine;
     }

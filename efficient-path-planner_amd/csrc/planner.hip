@@ -2332,17 +2332,76 @@ __device__ __forceinline__ bool pb_query_row(const KnnGrid& g, const double* __r
         if (cnt > kCap) return false;
         if (cnt < K) continue;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's list is complete
-        if (cnt <= 64) {  // entry i on lane i: ranks by v_readlane
-            const bool mine = lane < cnt;
+        // entries [0, m) of the LDS list (m <= 64), entry i on lane i: each one's rank in
+        // (distance, index) order counted against the others by v_readlane; ranks < K out
+        auto rank_small = [&](int m) {
+            const bool mine = lane < m;
             const double di = mine ? s_d[lane] : 0.0;
             const int ji = mine ? s_j[lane] : 0;
             const int dlo = __double2loint(di), dhi = __double2hiint(di);
             int rank = 0;
-            for (int f2 = 0; f2 < cnt; ++f2) {
+            for (int f2 = 0; f2 < m; ++f2) {
                 const double df = __hiloint2double(__builtin_amdgcn_readlane(dhi, f2), __builtin_amdgcn_readlane(dlo, f2));
                 rank += ((df < di) | ((df == di) & (__builtin_amdgcn_readlane(ji, f2) < ji))) ? 1 : 0;
             }
             if (mine && rank < K) out[rank] = (int32_t)(off + ji);
+        };
+        if (cnt <= 64) {
+            rank_small(cnt);
+        } else if (cnt <= 4 * 64) {
+            // Longer lists (a second radius: 60-100 candidates): the K-th distance is
+            // bracketed by bisection on wave ballots (the list in registers, four slots per
+            // lane; 10 halvings of [0, r^2]), the entries at or below the bracket's top --
+            // K plus the few that share its last interval -- are listed again and ranked
+            // among themselves: an entry's preceding entries all lie in that list, so its
+            // rank is its rank in the whole list.  (Instead of ranking every entry against
+            // every other through LDS: 20 us for the slowest queries.)
+            constexpr int kSl = 4;
+            double dv[kSl];
+            int jv[kSl];
+#pragma unroll
+            for (int sl = 0; sl < kSl; ++sl) {
+                const int i = sl * 64 + lane;
+                dv[sl] = i < cnt ? s_d[i] : INFINITY;
+                jv[sl] = i < cnt ? s_j[i] : 0;
+            }
+            double lo = 0.0, hi = b2;  // count(d <= hi) >= K (every entry has d <= r^2)
+            for (int step = 0; step < 10; ++step) {
+                const double mid = 0.5 * (lo + hi);
+                int c = 0;
+#pragma unroll
+                for (int sl = 0; sl < kSl; ++sl) c += __popcll(__ballot(dv[sl] <= mid));
+                if (c >= K) hi = mid;
+                else lo = mid;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the list is read: rewritten below)
+            int m = 0;
+#pragma unroll
+            for (int sl = 0; sl < kSl; ++sl) {
+                const bool in = dv[sl] <= hi;
+                const unsigned long long b = __ballot(in);
+                const int at = m + __popcll(b & ((1ull << lane) - 1ull));
+                if (in && at < kCap) {
+                    s_d[at] = dv[sl];
+                    s_j[at] = jv[sl];
+                }
+                m += __popcll(b);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (m <= 64) {
+                rank_small(m);
+            } else {  // (many entries at one distance: rank every entry of the cut list)
+                for (int i = lane; i < m; i += 64) {
+                    const double di = s_d[i];
+                    const int ji = s_j[i];
+                    int rank = 0;
+                    for (int f2 = 0; f2 < m; ++f2) {
+                        const double df = s_d[f2];
+                        rank += ((df < di) | ((df == di) & (s_j[f2] < ji))) ? 1 : 0;
+                    }
+                    if (rank < K) out[rank] = (int32_t)(off + ji);
+                }
+            }
         } else {
             for (int i = lane; i < cnt; i += 64) {
                 const double di = s_d[i];
@@ -2393,6 +2452,9 @@ __global__ __launch_bounds__(64) void k_pb_rows(PlanBatchDev P) {
     double pt_n[3] = {0.0, 0.0, 0.0};
     [[maybe_unused]] const unsigned long long tl_w0 = EPP_PBTL_NOW();
     if (wave < D) locate(wave, p_n, self_n, pt_n);
+    // (static shares, d = wave + j nwaves: handing the queries out by one atomic counter
+    // serialised ~19k same-address atomics at one L2 channel -- 0.17 -> 0.37 ms per batch;
+    // and every load behind a pending atomic waits for it: vmcnt counts in order)
     for (int d = wave; d < D; d += nwaves) {  // wave-uniform
         EPP_PBTL(d, 0, EPP_PBTL_NOW());
         EPP_PBTL(d, 5, tl_w0);
@@ -3131,7 +3193,7 @@ epp_status epp::plan_batch_launch(const epp_world* world, int32_t can_pass_gate,
         hipLaunchKernelGGL(k_pb_knn_scan, dim3((unsigned)kl.scan_blocks, S), dim3(kScanThreads), 0, s, P, next_scan_tag());
         hipLaunchKernelGGL(k_pb_knn_scatter, dim3(gn, S), dim3(256), 0, s, P);
         pb_mark(s, "scan_scatter");
-        // one wave per workgroup, 28 per CU (16 resident at 103 VGPRs; a variant with four
+        // one wave per workgroup, 28 per CU (16 resident at ~110 VGPRs; a variant with four
         // queries per wave, 16 lanes each, was 1.9x slower: its 16-lane shuffles and LDS
         // ranking cost more issue than the overlapped loads saved)
         static const int rows_wg = [] {  // (A/B knob: one-wave workgroups per CU)

@@ -37,7 +37,9 @@ def counters():
                     continue
                 c = r["Counter_Name"]
                 acc[name][c] += float(r["Counter_Value"])
-                disp[name][c].add(r.get("Dispatch_Id", r.get("Correlation_Id", "")))
+                # (dispatch ids restart in every pass's run: a counter in two passes is
+                # averaged over both runs' dispatches)
+                disp[name][c].add((d, r.get("Dispatch_Id", r.get("Correlation_Id", ""))))
     return {n: {c: v / max(1, len(disp[n][c])) for c, v in cs.items()} for n, cs in acc.items()}
 
 
