@@ -206,32 +206,14 @@ def run(args, ws, rank, local, out_stream):
     elapsed = dist.max(t1 - t0)
     value = ws * N_STATES * args.steps / elapsed
 
-    # The timed region's own HIP events (on the launch stream, around the K launches): the
-    # bracket also holds the graph's submission (~10-15 us per region: HIP gives no time for
-    # event records captured inside a graph, so the kernels cannot be bracketed alone).
+    # dominant kernel's average launch time: HIP events on the launch stream bracketing
+    # the timed region's K back-to-back launches (the only kernel in it).  The bracket
+    # also holds the graph's submission; a replay queued behind a host-released gate
+    # kernel (events around the kernels only) measured the same per-launch time (8.40 vs
+    # 8.33 us at K = 20, round 6), so the submission is not what the short region adds.
     evms = C.c_float()
     capi.check(L.epp_event_elapsed_ms(ev0, ev1, C.byref(evms)))
-    kms_region = evms.value / args.steps
-    # The dominant kernel's average duration (roofline.achieved): the same graph replayed
-    # once more right after the timed region, queued behind a stream gate (epp_gate_hold:
-    # a one-lane kernel waiting for the host) with the events around it, so that when the
-    # host releases the gate the K kernels run back to back between the two events and the
-    # bracket holds no submission.  (The timed region above, and so `value`, is unchanged.)
-    kms, kms_src = kms_region, "timed region's events (graph submission included)"
-    if graph is not None:
-        gate = C.c_void_p()
-        capi.check(L.epp_gate_create(C.byref(gate)))
-        try:
-            capi.check(L.epp_gate_hold(gate, 5000, stream))
-            capi.check(L.epp_event_record(ev0, stream))
-            capi.check(L.epp_graph_launch(graph, stream))
-            capi.check(L.epp_event_record(ev1, stream))
-            capi.check(L.epp_gate_release(gate))
-            capi.check(L.epp_stream_sync(stream))
-        finally:
-            L.epp_gate_destroy(gate)
-        capi.check(L.epp_event_elapsed_ms(ev0, ev1, C.byref(evms)))
-        kms, kms_src = evms.value / args.steps, "gated replay of the timed graph (events around the K kernels only)"
+    kms = evms.value / args.steps
     for ev in (ev0, ev1):
         L.epp_event_destroy(ev)
     if graph is not None:
@@ -291,9 +273,7 @@ def run(args, ws, rank, local, out_stream):
                          "traffic": traffic, "traffic_unit": "bytes per launch",
                          "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": BYTES_PER_STATE * N_STATES,
-                         "bytes_per_state": BYTES_PER_STATE, "kernel_ms": kms, "kernel_ms_source": kms_src,
-                         "kernel_ms_timed_region": kms_region,
-                         "frac_timed_region": BYTES_PER_STATE * N_STATES / (kms_region * 1e-3) / 1e9 / HBM_PEAK_GBS},
+                         "bytes_per_state": BYTES_PER_STATE, "kernel_ms": kms},
             "full_plan_ms_per_track": plan["ms_per_track"] if plan else None,
             "full_plan": plan,
             "cpu_baseline": cpu,

@@ -218,86 +218,3 @@ epp_status motions_small_sync(const epp_world* world, int32_t mode, const double
 
 }  // namespace epp
 
-// ---- stream gate (epp_gate_*, a launch-overhead tool like epp_graph_*) ------------------
-// One lane waits until the host word equals `want` (system-scope acquire loads of pinned,
-// coherent host memory: vector loads, nothing written) or until `ticks` of the 100 MHz
-// real-time counter have passed, so the kernel always ends.  Work queued behind it on the
-// stream starts when it ends.
-namespace {
-__global__ __launch_bounds__(64) void k_gate(const uint32_t* flag, uint32_t want, uint64_t ticks) {
-    if (threadIdx.x != 0) return;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != want) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) break;
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
-struct Gate {
-    uint32_t* host = nullptr;  // pinned, coherent
-    uint32_t* dev = nullptr;   // its device address
-    uint32_t seq = 0;
-};
-}  // namespace
-
-using namespace epp;
-
-extern "C" {
-
-epp_status epp_gate_create(void** gate) {
-    if (!gate) {
-        set_error("epp_gate_create: invalid argument");
-        return EPP_ERR_INVALID_ARGUMENT;
-    }
-    Gate* g = new Gate;
-    void* h = nullptr;
-    if (hipHostMalloc(&h, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
-        delete g;
-        set_error("epp_gate_create: hipHostMalloc failed");
-        return EPP_ERR_HIP;
-    }
-    g->host = static_cast<uint32_t*>(h);
-    __atomic_store_n(g->host, 0u, __ATOMIC_RELEASE);
-    void* d = nullptr;
-    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
-        (void)hipHostFree(h);
-        delete g;
-        set_error("epp_gate_create: hipHostGetDevicePointer failed");
-        return EPP_ERR_HIP;
-    }
-    g->dev = static_cast<uint32_t*>(d);
-    *gate = g;
-    return EPP_OK;
-}
-
-epp_status epp_gate_destroy(void* gate) {
-    if (!gate) return EPP_OK;
-    Gate* g = static_cast<Gate*>(gate);
-    (void)hipDeviceSynchronize();  // (no gate kernel left reading the word)
-    (void)hipHostFree(g->host);
-    delete g;
-    return EPP_OK;
-}
-
-epp_status epp_gate_hold(void* gate, uint32_t timeout_ms, void* stream) {
-    if (!gate || timeout_ms == 0 || timeout_ms > 60000) {
-        set_error("epp_gate_hold: invalid argument (timeout 1..60000 ms)");
-        return EPP_ERR_INVALID_ARGUMENT;
-    }
-    Gate* g = static_cast<Gate*>(gate);
-    const uint32_t want = ++g->seq == 0 ? ++g->seq : g->seq;
-    hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, (hipStream_t)stream, (const uint32_t*)g->dev, want,
-                       (uint64_t)timeout_ms * 100000ull);
-    return launch_error("epp_gate_hold");
-}
-
-epp_status epp_gate_release(void* gate) {
-    if (!gate) {
-        set_error("epp_gate_release: invalid argument");
-        return EPP_ERR_INVALID_ARGUMENT;
-    }
-    Gate* g = static_cast<Gate*>(gate);
-    __atomic_store_n(g->host, g->seq, __ATOMIC_RELEASE);
-    return EPP_OK;
-}
-
-}  // extern "C"

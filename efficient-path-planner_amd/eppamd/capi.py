@@ -67,10 +67,6 @@ def lib() -> C.CDLL:
             "epp_graph_end": (i32, [vp, C.POINTER(vp)]),
             "epp_graph_launch": (i32, [vp, vp]),
             "epp_graph_destroy": (i32, [vp]),
-            "epp_gate_create": (i32, [C.POINTER(vp)]),
-            "epp_gate_destroy": (i32, [vp]),
-            "epp_gate_hold": (i32, [vp, C.c_uint32, vp]),
-            "epp_gate_release": (i32, [vp]),
             "epp_build_obbs": (i32, [vp, vp, i32, vp, i32, vp, i32, vp, i32, vp, i32, C.POINTER(i32)]),
             "epp_world_create": (i32, [vp, i32, dp, dp, C.POINTER(vp)]),
             "epp_world_update": (i32, [vp, vp, i32]),
@@ -152,7 +148,6 @@ EXPORTED = [
     "epp_comm_init_all", "epp_comm_destroy", "epp_comm_rank", "epp_comm_allgather_waypoints",
     "epp_comm_allreduce_f64", "epp_comm_barrier", "epp_comm_available", "epp_knn_ws_box", "epp_knn_grid_ws_box",
     "epp_comm_set_timeout", "epp_comm_abort", "epp_check_and_generate_trajectory_host",
-    "epp_gate_create", "epp_gate_destroy", "epp_gate_hold", "epp_gate_release",
 ]
 
 

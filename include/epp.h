@@ -102,15 +102,6 @@ epp_status epp_graph_begin(void* stream);
 epp_status epp_graph_end(void* stream, void** exec);
 epp_status epp_graph_launch(void* exec, void* stream);
 epp_status epp_graph_destroy(void* exec);
-/* Stream gate (a launch-overhead tool like the graph calls; no reference counterpart):
- * epp_gate_hold queues on `stream` a one-lane kernel that waits until epp_gate_release is
- * called (or timeout_ms, 1..60000, passes: it always ends); work queued behind it starts
- * when it ends.  bench.py queues a replay of its timed graph behind a gate, so the HIP
- * events around the K launches bracket the kernels rather than the graph's submission. */
-epp_status epp_gate_create(void** gate);
-epp_status epp_gate_destroy(void* gate);
-epp_status epp_gate_hold(void* gate, uint32_t timeout_ms, void* stream);
-epp_status epp_gate_release(void* gate);
 
 /* ---- world ------------------------------------------------------------------------ */
 /* World::addGate / World::addObstacle (src/World.cpp:13-55) via

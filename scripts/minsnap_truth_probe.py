@@ -30,12 +30,17 @@ def report(name, tracks, v=1.0, a=2.0):
     eg = np.abs(np.asarray(Cs) - truth).reshape(len(tracks), -1).max(1)
     eo = np.abs(np.asarray(Cr) - truth).reshape(len(tracks), -1).max(1)
     scale = np.abs(truth).reshape(len(tracks), -1).max(1)
+    # the time-normalised error (c_j T^j, over the track's largest normalised coefficient)
+    Tn = np.asarray(Tr)[:, :, None, None] ** np.arange(10)[None, None, None, :]
+    nsc = (np.abs(truth) * Tn).reshape(len(tracks), -1).max(1)
+    ng = (np.abs(np.asarray(Cs) - truth) * Tn).reshape(len(tracks), -1).max(1) / nsc
+    no = (np.abs(np.asarray(Cr) - truth) * Tn).reshape(len(tracks), -1).max(1) / nsc
     print(f"{name}: problems {len(tracks)} solved {(np.asarray(st) == 0).sum()} Tmin {np.min(Tr):.3g} "
           f"coef max {scale.max():.3g} | gpu-truth max {eg.max():.3e} (p{eg.argmax()}) p99 {np.quantile(eg, .99):.3e} "
           f"rel {np.max(eg / scale):.3e} | oracle-truth max {eo.max():.3e} p99 {np.quantile(eo, .99):.3e} | "
           f"gpu-oracle max {np.abs(np.asarray(Cs) - np.asarray(Cr)).max():.3e} "
           f"excess over oracle's own {np.max(np.abs(np.asarray(Cs) - np.asarray(Cr)).reshape(len(tracks), -1).max(1) - eo):.3e} "
-          f"({time.time() - t0:.1f} s)", flush=True)
+          f"| normalised gpu {ng.max():.2e} oracle {no.max():.2e} ({time.time() - t0:.1f} s)", flush=True)
     return eg, eo
 
 
