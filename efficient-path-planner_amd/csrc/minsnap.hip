@@ -509,7 +509,8 @@ __global__ __launch_bounds__(BLOCK) void k_minsnap(const double* __restrict__ wp
                                                    int n_tracks, double vmax, double amax, const double* __restrict__ v0,
                                                    const double* __restrict__ a0, const double* __restrict__ times_in,
                                                    double* __restrict__ seg_times, double* __restrict__ coeffs,
-                                                   int32_t* __restrict__ status, double* __restrict__ gscratch) {
+                                                   int32_t* __restrict__ status, double* __restrict__ gscratch,
+                                                   int refine) {
     // one dynamic LDS array (cdna_hip_programming.md Guideline 17): the error flag (16
     // bytes), the constants, then the solve's scratch
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -535,7 +536,7 @@ __global__ __launch_bounds__(BLOCK) void k_minsnap(const double* __restrict__ wp
     __syncthreads();
     const int st = solve_track<BLOCK, LDS>(kc, wp + (size_t)w0 * 3, M, vmax, amax, v0 ? v0 + 3 * track : nullptr,
                                       a0 ? a0 + 3 * track : nullptr, times_in ? times_in + seg0 : nullptr, scr, dv, rhs,
-                                      Tm, Tm + M, s_err, seg_times + seg0, coeffs + (size_t)seg0 * 30, true);
+                                      Tm, Tm + M, s_err, seg_times + seg0, coeffs + (size_t)seg0 * 30, refine != 0);
     if (threadIdx.x == 0 && status) status[track] = st;
 }
 
@@ -999,11 +1000,18 @@ epp_status minsnap_batch(const double* wp, const int32_t* wp_offsets, int32_t n_
     int64_t total_m = 0;
     if ((st = read_offsets(wp_offsets, n_tracks, s, what, &max_m, &total_m))) return st;
     constexpr int kB = 64;  // one wavefront per track: the batch is throughput-bound
+    // one refinement step in every track's solve (solve_track): +50 % kernel time, 10-100x
+    // the accuracy on short and mixed segments (scripts/minsnap_truth_probe.py, DESIGN.md
+    // section 4); EPP_MINSNAP_REFINE=0 skips it (A/B knob)
+    static const int refine = [] {
+        const char* e = std::getenv("EPP_MINSNAP_REFINE");
+        return e && *e == '0' ? 0 : 1;
+    }();
     if (max_m <= kMaxLdsSeg) {
         const size_t shm = ((size_t)max_m * Seg::kSize + vertex_doubles(max_m) + 2 + kNC) * sizeof(double);
         allow_lds(k_minsnap<kB, true>);
         hipLaunchKernelGGL((k_minsnap<kB, true>), dim3(n_tracks), dim3(kB), shm, s, wp, wp_offsets, n_tracks, v_max,
-                           a_max, v0, a0, times_in, seg_times, coeffs, status, nullptr);
+                           a_max, v0, a0, times_in, seg_times, coeffs, status, nullptr, refine);
         return launch_error(what);
     }
     // long tracks: segment scratch in a per-device workspace whose reuse by another stream
@@ -1026,7 +1034,7 @@ epp_status minsnap_batch(const double* wp, const int32_t* wp_offsets, int32_t n_
     }
     allow_lds(k_minsnap<kB, false>);
     hipLaunchKernelGGL((k_minsnap<kB, false>), dim3(n_tracks), dim3(kB), shm, s, wp, wp_offsets, n_tracks, v_max, a_max,
-                       v0, a0, times_in, seg_times, coeffs, status, static_cast<double*>(ws.buf));
+                       v0, a0, times_in, seg_times, coeffs, status, static_cast<double*>(ws.buf), refine);
     st = launch_error(what);
     ws.release(s);
     return st;
