@@ -55,3 +55,33 @@ for name, v in fetch.items():
                      "correction": "FETCH_SIZE x2 (gfx950 wide-load rule), WRITE_SIZE as read"}
 json.dump(summary, open(os.path.join(prof, f"{tag}_traffic.json"), "w"), indent=1)
 print(json.dumps(summary, indent=1))
+
+# The planner probe's steady state: its first pre_compute_traj call is the cold plan (a fresh
+# generator: workspaces, the fallback areas' one-time whole-table warm-up searches, first
+# launches).  <tag>_kernel_stats_planner_steady.csv drops every kernel before the second
+# call's first k_pb_sample.
+traces = glob.glob(os.path.join(out_dir, "prof_plan", "**", "*kernel_trace.csv"), recursive=True)
+if traces:
+    rows = sorted(csv.DictReader(open(traces[0])), key=lambda r: int(r["Start_Timestamp"]))
+    starts = [int(r["Start_Timestamp"]) for r in rows if "k_pb_sample" in r["Kernel_Name"]]
+    if len(starts) > 1:
+        cut = starts[1]  # (one batch per pre_compute_traj call: its 9 segments together)
+        steady = [r for r in rows if int(r["Start_Timestamp"]) >= cut]
+        agg = {}
+        for r in steady:
+            d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            a = agg.setdefault(r["Kernel_Name"], [0, 0, 1 << 62, 0])
+            a[0] += 1
+            a[1] += d
+            a[2] = min(a[2], d)
+            a[3] = max(a[3], d)
+        tot = sum(a[1] for a in agg.values()) or 1
+        path = os.path.join(prof, f"{tag}_kernel_stats_planner_steady.csv")
+        with open(path, "w", newline="") as f:
+            wr = csv.writer(f, quoting=csv.QUOTE_NONNUMERIC)
+            wr.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs"])
+            for name, a in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+                wr.writerow([name, a[0], a[1], a[1] / a[0], 100.0 * a[1] / tot, a[2], a[3]])
+        print(f"-- kernel_stats_planner_steady (from the second call: {len(steady)} of {len(rows)} dispatches)")
+        for name, a in sorted(agg.items(), key=lambda kv: -kv[1][1])[:12]:
+            print(name[:70], a[0], a[1] / a[0])
