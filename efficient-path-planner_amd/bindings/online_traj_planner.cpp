@@ -184,6 +184,48 @@ PYBIND11_MODULE(online_traj_planner, m) {
             },
             py::arg("problems"), py::arg("timeLimit"))
         .def(
+            "plan_paths_include_gates2",  // planPaths of a chain of segments + includeGates2 in one call
+            [](const epp::PathPlanner& self, const std::vector<std::pair<py::object, py::object>>& problems,
+               double timeLimit) -> py::object {
+                std::vector<std::pair<Vec3, Vec3>> pr;
+                for (const auto& p : problems) pr.emplace_back(to_vec3(p.first), to_vec3(p.second));
+                std::vector<std::vector<Vec3>> paths;
+                std::vector<char> ok;
+                std::vector<Vec3> flat;
+                bool all;
+                {
+                    py::gil_scoped_release release;
+                    all = self.planPathsIncludeGates2(pr, timeLimit, paths, ok, flat);
+                }
+                py::list segs;
+                for (size_t i = 0; i < pr.size(); ++i) {
+                    py::array_t<double> a({(py::ssize_t)paths[i].size(), (py::ssize_t)3});
+                    for (size_t j = 0; j < paths[i].size(); ++j)
+                        for (int k = 0; k < 3; ++k) a.mutable_data()[j * 3 + k] = paths[i][j][k];
+                    segs.append(py::make_tuple((bool)ok[i], a));
+                }
+                if (!all) return py::make_tuple(segs, py::none());
+                py::array_t<double> out({(py::ssize_t)flat.size(), (py::ssize_t)3});
+                for (size_t i = 0; i < flat.size(); ++i)
+                    for (int k = 0; k < 3; ++k) out.mutable_data()[i * 3 + k] = flat[i][k];
+                return py::make_tuple(segs, out);
+            },
+            py::arg("problems"), py::arg("timeLimit"))
+        .def(
+            "check_rays_both",  // World::checkRaysBoth: bit 0 canPassGate = false, bit 1 true
+            [](const epp::PathPlanner& self, const py::object& s1, const py::object& s2) {
+                Matrix a = to_matrix(s1), b = to_matrix(s2);
+                if (a.cols != 3 || b.cols != 3 || a.rows != b.rows)
+                    throw std::invalid_argument("s1 and s2 must be (n, 3) arrays of one length");
+                py::array_t<uint8_t> out((py::ssize_t)a.rows);
+                {
+                    py::gil_scoped_release release;
+                    self.worldPtr->checkRaysBoth(a.data.data(), b.data.data(), (int64_t)a.rows, out.mutable_data());
+                }
+                return out;
+            },
+            py::arg("s1"), py::arg("s2"))
+        .def(
             "plan_once",  // one batch-planner attempt with an explicit sample count and seed
             [](const epp::PathPlanner& self, const py::object& start, const py::object& goal, int64_t samples,
                uint64_t seed) -> py::object {

@@ -141,14 +141,17 @@ void OnlineTrajGenerator::preComputeTraj(double takeoffTime) {
         return e && std::atoi(e) == 1;
     }();
     const auto t0 = std::chrono::steady_clock::now();
-    pathPlanner.planPaths(problems, timeLimit, paths, ok);
+    // the plans and includeGates2 in one call: the pruning's ray checks ride in the
+    // shortcut's batch (PathPlanner::planPathsIncludeGates2; same answers as the two calls)
+    std::vector<Vec3> pruned;
+    const bool all = pathPlanner.planPathsIncludeGates2(problems, timeLimit, paths, ok, pruned);
     for (size_t s = 0; s < problems.size(); ++s) {
         if (!ok[s]) throw std::runtime_error("Path not found");
         pathSegments.push_back(paths[s]);
     }
+    if (!all) throw std::runtime_error("Path not found");
     const auto t1 = std::chrono::steady_clock::now();
-    const std::vector<Vec3> pruned = pathPlanner.includeGates2(pathSegments);
-    const auto t2 = std::chrono::steady_clock::now();
+    const auto t2 = t1;  // (includeGates2: inside the call above)
     // the path file is written on the writer's thread while the trajectory is fitted; both
     // are done before the call returns (src/OnlineTrajGenerator.cpp:90-93 in sequence)
     pathWriter.writePathAsync(pruned);

@@ -4,6 +4,7 @@
 #include <array>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <iostream>
@@ -320,6 +321,16 @@ struct SolveScratch {
 };
 
 // EPP_PLAN_TRACE=1 (diagnostics): the fallback's phases on stderr
+// EPP_PAIRS_TRACE=1 (diagnostics): the shortcut's and the pruning's batched ray checks --
+// pairs and wall time of each batch -- to stderr
+static bool pairs_trace() {
+    static const bool t = [] {
+        const char* e = std::getenv("EPP_PAIRS_TRACE");
+        return e && std::atoi(e) == 1;
+    }();
+    return t;
+}
+
 bool plan_trace() {
     static const bool t = [] {
         const char* e = std::getenv("EPP_PLAN_TRACE");
@@ -381,7 +392,8 @@ int astar(SearchState& ss, size_t nv, Pos&& pos, Key&& key, Expand&& expand) {
 // planner threads, A* over its emitted rows (the row-restricted search) or, when that
 // cannot decide, over the whole k-NN table of its nodes; then one batched shortcut.
 void PathPlanner::planAttempt(const std::vector<std::pair<Vec3, Vec3>>& problems, const std::vector<uint64_t>& seeds,
-                              int64_t samples, std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const {
+                              int64_t samples, std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok,
+                              GateEnds* ends) const {
     const size_t np = problems.size();
     paths.assign(np, {});
     ok.assign(np, 0);
@@ -391,7 +403,7 @@ void PathPlanner::planAttempt(const std::vector<std::pair<Vec3, Vec3>>& problems
         std::vector<uint64_t> sseeds(seeds.begin() + b0, seeds.begin() + b1);
         std::vector<std::vector<Vec3>> sp;
         std::vector<char> so;
-        planChunk(sub, sseeds, samples, sp, so);
+        planChunk(sub, sseeds, samples, sp, so, ends ? ends + b0 : nullptr);
         for (size_t i = b0; i < b1; ++i) {
             paths[i] = std::move(sp[i - b0]);
             ok[i] = so[i - b0];
@@ -400,7 +412,8 @@ void PathPlanner::planAttempt(const std::vector<std::pair<Vec3, Vec3>>& problems
 }
 
 void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, const std::vector<uint64_t>& seeds,
-                            int64_t samples, std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const {
+                            int64_t samples, std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok,
+                            GateEnds* ends) const {
     const auto& pp = configParser->getPathPlannerProperties();
     const auto& wp = configParser->getWorldProperties();
     const bool canPass = pp.canPassGate;  // validators get can_pass_gate  src/PathPlanner.cpp:47-50
@@ -791,12 +804,14 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
     const double ms_solve = std::chrono::duration<double, std::milli>(t_sc - t_dev0).count() - ms_batch;
     std::vector<std::vector<Vec3>> shortcut_in;
     std::vector<int> which;
+    std::vector<GateEnds*> sc_ends;  // (planPathsIncludeGates2: the pruning's pairs too)
     for (int p = 0; p < S; ++p)
         if (found[p]) {
             shortcut_in.push_back(std::move(raw[p]));
             which.push_back(p);
+            if (ends) sc_ends.push_back(ends + p);
         }
-    std::vector<std::vector<Vec3>> shortcut_out = shortcutAll(shortcut_in);
+    std::vector<std::vector<Vec3>> shortcut_out = shortcutAll(shortcut_in, ends ? &sc_ends : nullptr);
     paths.assign(S, {});
     ok.assign(S, 0);
     for (size_t i = 0; i < which.size(); ++i) {
@@ -1004,25 +1019,60 @@ bool PathPlanner::planOnce(const Vec3& start, const Vec3& goal, int64_t samples,
 
 // Greedy shortcutting with one batched check of every vertex pair of every path (the role
 // of PathSimplifier::reduceVertices in src/PathPlanner.cpp:138-139).
-std::vector<std::vector<Vec3>> PathPlanner::shortcutAll(const std::vector<std::vector<Vec3>>& ps) const {
+// (pairs (i, j), j >= i + 2, of an L-point list are queued row by row: the index of one)
+static size_t pair_index(size_t L, size_t i, size_t j) {
+    const size_t before = i * (L - 2) - (i * (i - 1)) / 2;  // pairs of rows < i: sum (L - 2 - r)
+    return before + (j - i - 2);
+}
+
+std::vector<std::vector<Vec3>> PathPlanner::shortcutAll(const std::vector<std::vector<Vec3>>& ps,
+                                                        const std::vector<GateEnds*>* ends) const {
+    // ends: each path's list is [prev] + path + [next] (the pruning's points): all its pairs
+    // are queued and each ray answers both canPassGate values (World::checkRaysBoth); the
+    // shortcut reads the path's pairs, the pruning keeps the true answers of all of them
+    const bool canPass = configParser->getPathPlannerProperties().canPassGate;
     std::vector<double> s1, s2;
-    std::vector<size_t> base(ps.size() + 1, 0);
+    std::vector<size_t> base(ps.size() + 1, 0), off(ps.size(), 0);
     for (size_t q = 0; q < ps.size(); ++q) {
         const auto& p = ps[q];
-        const size_t L = p.size();
         base[q + 1] = base[q];
-        if (L < 3) continue;
-        for (size_t i = 0; i < L; ++i)
-            for (size_t j = i + 2; j < L; ++j) {
-                s1.insert(s1.end(), {p[i].x, p[i].y, p[i].z});
-                s2.insert(s2.end(), {p[j].x, p[j].y, p[j].z});
-                ++base[q + 1];
-            }
+        std::vector<Vec3> ext;
+        if (ends) {
+            GateEnds& g = *(*ends)[q];
+            if (g.has_prev) ext.push_back(g.prev);
+            off[q] = g.has_prev ? 1 : 0;
+            ext.insert(ext.end(), p.begin(), p.end());
+            if (g.has_next) ext.push_back(g.next);
+        }
+        const std::vector<Vec3>& w = ends ? ext : p;
+        const size_t L = w.size();
+        if (L >= 3)
+            for (size_t i = 0; i < L; ++i)
+                for (size_t j = i + 2; j < L; ++j) {
+                    s1.insert(s1.end(), {w[i].x, w[i].y, w[i].z});
+                    s2.insert(s2.end(), {w[j].x, w[j].y, w[j].z});
+                    ++base[q + 1];
+                }
+        if (ends) (*ends)[q]->pts = std::move(ext);
     }
     std::vector<uint8_t> ok(base.back());
-    if (!ok.empty())
-        worldPtr->checkRays(s1.data(), s2.data(), (int64_t)ok.size(), configParser->getPathPlannerProperties().canPassGate,
-                            ok.data());
+    const auto t_rays = std::chrono::steady_clock::now();
+    if (!ok.empty()) {
+        if (ends) worldPtr->checkRaysBoth(s1.data(), s2.data(), (int64_t)ok.size(), ok.data());
+        else worldPtr->checkRays(s1.data(), s2.data(), (int64_t)ok.size(), canPass, ok.data());
+    }
+    if (pairs_trace())
+        std::fprintf(stderr, "pairs_trace: shortcut paths %zu pairs %zu rays%s %.1f us\n", ps.size(), ok.size(),
+                     ends ? " (both answers: the pruning's too)" : "",
+                     std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_rays).count());
+    const uint8_t bit = ends ? (canPass ? 2 : 1) : 0xFF;  // the shortcut's answer in a flag byte
+    if (ends)
+        for (size_t q = 0; q < ps.size(); ++q) {
+            GateEnds& g = *(*ends)[q];
+            g.vis.resize(base[q + 1] - base[q]);
+            for (size_t t = 0; t < g.vis.size(); ++t) g.vis[t] = (ok[base[q] + t] >> 1) & 1;
+            g.filled = true;
+        }
     std::vector<std::vector<Vec3>> out(ps.size());
     for (size_t q = 0; q < ps.size(); ++q) {
         const auto& p = ps[q];
@@ -1032,9 +1082,9 @@ std::vector<std::vector<Vec3>> PathPlanner::shortcutAll(const std::vector<std::v
             continue;
         }
         // vis(i, j) of pair (i, j), j >= i + 2, in the order they were queued
+        const size_t LE = ends ? (*ends)[q]->pts.size() : L;
         auto vis = [&](size_t i, size_t j) {
-            const size_t before = i * (L - 2) - (i * (i - 1)) / 2;  // pairs of rows < i: sum (L - 2 - r)
-            return ok[base[q] + before + (j - i - 2)] != 0;
+            return (ok[base[q] + pair_index(LE, i + off[q], j + off[q])] & bit) != 0;
         };
         std::vector<Vec3> o = {p[0]};
         size_t cur = 0;
@@ -1105,7 +1155,8 @@ bool PathPlanner::planPath(const Vec3& start, const Vec3& goal, double timeLimit
 // together; up to 4 attempts while inside timeLimit (the role of solve(timeLimit),
 // src/PathPlanner.cpp:126-136).  Returns the attempts made.
 int PathPlanner::planCalls(const std::vector<std::pair<Vec3, Vec3>>& problems, uint64_t base, double timeLimit,
-                           std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const {
+                           std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok,
+                           std::vector<GateEnds>* ends) const {
     const auto t0 = std::chrono::steady_clock::now();
     const auto& pp = configParser->getPathPlannerProperties();
     const size_t n = problems.size();
@@ -1130,13 +1181,17 @@ int PathPlanner::planCalls(const std::vector<std::pair<Vec3, Vec3>>& problems, u
         }
         std::vector<std::vector<Vec3>> sp;
         std::vector<char> so;
-        planAttempt(sub, sseeds, samples, sp, so);
+        std::vector<GateEnds> se;
+        if (ends)
+            for (size_t i : pending) se.push_back((*ends)[i]);
+        planAttempt(sub, sseeds, samples, sp, so, ends ? se.data() : nullptr);
         attempts = a + 1;
         std::vector<size_t> still;
         for (size_t j = 0; j < pending.size(); ++j) {
             if (so[j]) {
                 paths[pending[j]] = std::move(sp[j]);
                 ok[pending[j]] = 1;
+                if (ends) (*ends)[pending[j]] = std::move(se[j]);
             } else {
                 still.push_back(pending[j]);
             }
@@ -1156,6 +1211,36 @@ int PathPlanner::planCalls(const std::vector<std::pair<Vec3, Vec3>>& problems, u
 
 void PathPlanner::planPaths(const std::vector<std::pair<Vec3, Vec3>>& problems, double timeLimit,
                             std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const {
+    planPathsWith(problems, timeLimit, paths, ok, nullptr);
+}
+
+bool PathPlanner::planPathsIncludeGates2(const std::vector<std::pair<Vec3, Vec3>>& problems, double timeLimit,
+                                         std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok,
+                                         std::vector<Vec3>& pruned) const {
+    // (EPP_FUSED_PRUNE=0: the two calls as they are, for A/B)
+    static const bool fused = [] {
+        const char* e = std::getenv("EPP_FUSED_PRUNE");
+        return !(e && std::string(e) == "0");
+    }();
+    std::vector<GateEnds> ends;
+    if (fused && configParser->getPathPlannerProperties().pathSimplification == "custom") {
+        ends.resize(problems.size());
+        for (size_t s = 0; s + 1 < problems.size(); ++s) {  // includeGates2's (a + b) / 2 of the ends
+            const Vec3 c = (problems[s].second + problems[s + 1].first) / 2;
+            ends[s].has_next = ends[s + 1].has_prev = true;
+            ends[s].next = ends[s + 1].prev = c;
+        }
+    }
+    planPathsWith(problems, timeLimit, paths, ok, ends.empty() ? nullptr : &ends);
+    for (char o : ok)
+        if (!o) return false;
+    pruned = includeGates2With(paths, ends.empty() ? nullptr : &ends);
+    return true;
+}
+
+void PathPlanner::planPathsWith(const std::vector<std::pair<Vec3, Vec3>>& problems, double timeLimit,
+                                std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok,
+                                std::vector<GateEnds>* ends) const {
     checkPlannerConfig(configParser->getPathPlannerProperties());
     const size_t n = problems.size();
     paths.assign(n, {});
@@ -1168,7 +1253,7 @@ void PathPlanner::planPaths(const std::vector<std::pair<Vec3, Vec3>>& problems, 
     }
     (void)worldPtr->device();  // the device world, before the planner threads share it
     const uint64_t base = __atomic_fetch_add(&calls_, (uint64_t)n, __ATOMIC_RELAXED);
-    const int attempts = planCalls(problems, base, timeLimit, paths, ok);
+    const int attempts = planCalls(problems, base, timeLimit, paths, ok, ends);
     std::lock_guard<std::mutex> lk(g_stats_mu);
     stats_.attempts = attempts;
     stats_.ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1177,6 +1262,11 @@ void PathPlanner::planPaths(const std::vector<std::pair<Vec3, Vec3>>& problems, 
 // PathPlanner::includeGates2 — src/PathPlanner.cpp:175-230.  The segments' pruning checks
 // are one batch (pruneAll).
 std::vector<Vec3> PathPlanner::includeGates2(std::vector<std::vector<Vec3>> waypoints) const {
+    return includeGates2With(std::move(waypoints), nullptr);
+}
+
+std::vector<Vec3> PathPlanner::includeGates2With(std::vector<std::vector<Vec3>> waypoints,
+                                                 const std::vector<GateEnds>* ends) const {
     std::vector<Vec3> gateCenters;
     for (size_t s = 0; s + 1 < waypoints.size(); ++s) {
         const Vec3& a = waypoints[s].back();
@@ -1192,7 +1282,7 @@ std::vector<Vec3> PathPlanner::includeGates2(std::vector<std::vector<Vec3>> wayp
     if (method == "none") {
         pruned = waypoints;
     } else if (method == "custom") {
-        pruned = pruneAll(waypoints);
+        pruned = pruneAll(waypoints, ends);
     } else if (method == "ompl") {
         pruned = smoothAll(waypoints);
     } else {
@@ -1299,14 +1389,36 @@ std::vector<std::vector<Vec3>> PathPlanner::smoothAll(const std::vector<std::vec
 // PathPlanner::pruneWaypoints — src/PathPlanner.cpp:232-265.  The reference checks
 // ray(reference, current) one at a time; every pair it could ask for is checked in one
 // batch (for all segments at once) and the same greedy walk is replayed on the answers.
-std::vector<std::vector<Vec3>> PathPlanner::pruneAll(const std::vector<std::vector<Vec3>>& segs) const {
+std::vector<std::vector<Vec3>> PathPlanner::pruneAll(const std::vector<std::vector<Vec3>>& segs,
+                                                     const std::vector<GateEnds>* ends) const {
+    // ends (planPathsIncludeGates2): a segment whose points are, in order, among its
+    // GateEnds' pts (bit for bit) reads the answers the shortcut's batch already holds
+    auto same = [](const Vec3& a, const Vec3& b) { return std::memcmp(&a, &b, sizeof(Vec3)) == 0; };
+    std::vector<std::vector<size_t>> at(segs.size());  // segment point -> its index in pts
+    for (size_t q = 0; ends && q < segs.size() && q < ends->size(); ++q) {
+        const GateEnds& g = (*ends)[q];
+        if (!g.filled || segs[q].size() < 3) continue;
+        std::vector<size_t> m;
+        size_t k = 0;
+        for (const Vec3& v : segs[q]) {
+            while (k < g.pts.size() && !same(g.pts[k], v)) ++k;
+            if (k == g.pts.size()) break;
+            m.push_back(k++);
+        }
+        if (m.size() == segs[q].size()) at[q] = std::move(m);
+    }
     std::vector<double> s1, s2;
     std::vector<size_t> base(segs.size() + 1, 0);
+    size_t answered = 0;
     for (size_t q = 0; q < segs.size(); ++q) {
         const auto& w = segs[q];
         const size_t L = w.size();
         base[q + 1] = base[q];
         if (L < 3) continue;
+        if (!at[q].empty()) {
+            ++answered;
+            continue;
+        }
         for (size_t i = 0; i < L; ++i)
             for (size_t j = i + 2; j < L; ++j) {
                 s1.insert(s1.end(), {w[i].x, w[i].y, w[i].z});
@@ -1315,7 +1427,12 @@ std::vector<std::vector<Vec3>> PathPlanner::pruneAll(const std::vector<std::vect
             }
     }
     std::vector<uint8_t> ok(base.back());
+    const auto t_rays = std::chrono::steady_clock::now();
     if (!ok.empty()) worldPtr->checkRays(s1.data(), s2.data(), (int64_t)ok.size(), true, ok.data());  // canPassGate = true
+    if (pairs_trace())
+        std::fprintf(stderr, "pairs_trace: prune segments %zu (%zu answered by the shortcut's batch) pairs %zu rays %.1f us\n",
+                     segs.size(), answered, ok.size(),
+                     std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_rays).count());
     std::vector<std::vector<Vec3>> out(segs.size());
     for (size_t q = 0; q < segs.size(); ++q) {
         const auto& w = segs[q];
@@ -1325,8 +1442,11 @@ std::vector<std::vector<Vec3>> PathPlanner::pruneAll(const std::vector<std::vect
             continue;
         }
         auto vis = [&](size_t i, size_t j) {  // pair (i, j), j >= i + 2, in the order queued
-            const size_t before = i * (L - 2) - (i * (i - 1)) / 2;
-            return ok[base[q] + before + (j - i - 2)] != 0;
+            if (!at[q].empty()) {
+                const GateEnds& g = (*ends)[q];
+                return g.vis[pair_index(g.pts.size(), at[q][i], at[q][j])] != 0;
+            }
+            return ok[base[q] + pair_index(L, i, j)] != 0;
         };
         std::vector<Vec3> pruned = {w[0]};
         size_t ref = 0;

@@ -4,6 +4,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "epp/World.h"
 #include "host_scratch.h"
@@ -159,6 +160,24 @@ void World::checkRays(const double* s1, const double* s2, int64_t n, bool canPas
               "checkRays");
         return handled;
     }, in, out);
+}
+
+void World::checkRaysBoth(const double* s1, const double* s2, int64_t n, uint8_t* out) const {
+    const double* in[2] = {s1, s2};
+    bool two = false;  // (past the small path: two launches, below)
+    query(n, 2, [&](const double* const*, uint8_t*, void*) { two = true; },
+          [&](const double* const* d, uint8_t* flags, void* st) {
+              bool handled = false;
+              check(motions_small_sync(device(), 0, d[0], d[1], n, kCanPassBoth, flags, (hipStream_t)st, &handled),
+                    "checkRays");
+              return handled;
+          },
+          in, out);
+    if (!two) return;
+    std::vector<uint8_t> t((size_t)n);
+    checkRays(s1, s2, n, false, out);
+    checkRays(s1, s2, n, true, t.data());
+    for (int64_t i = 0; i < n; ++i) out[i] = (uint8_t)((out[i] ? 1 : 0) | (t[i] ? 2 : 0));
 }
 
 template <typename Launch, typename Small>

@@ -881,7 +881,8 @@ epp_status epp_check_motions(const epp_world* world, const double* s1, const dou
     if (n == 0) return EPP_OK;
     SmallWorld sw = small_world(world);
     if (small_motions(sw, n)) {
-        if (const epp_status st = launch_motions_small(sw, mode, s1, s2, n, can_pass_gate, valid, (hipStream_t)stream))
+        if (const epp_status st =
+                launch_motions_small(sw, mode, s1, s2, n, can_pass_gate != 0 ? 1 : 0, valid, (hipStream_t)stream))
             return st;
         return note_record_reader(world, sw, (hipStream_t)stream);
     }

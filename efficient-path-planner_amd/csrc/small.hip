@@ -67,6 +67,30 @@ __global__ __launch_bounds__(kSmallBlock) void k_motions_small(const double* __r
     if (t < per) s_hit[t] = 0u;
     __syncthreads();
     const int o0 = (int)((int64_t)slice * n_obb / slices), o1 = (int)((int64_t)(slice + 1) * n_obb / slices);
+    if (MODE == 0 && can_pass == kCanPassBoth) {
+        // both answers of each ray in one pass: bit 0 valid with canPassGate = false (every
+        // record), bit 1 with true (the filling records skipped, src/World.cpp:150-153).  A
+        // hit on a record other than a filling one decides both; a filling hit only bit 0.
+        bool any = false, solid = false;
+        for (int o = o0; o < o1; ++o) {
+            const double* r = srec + (size_t)o * kRecDoubles;
+            const uint32_t m = (uint32_t)__double_as_longlong(r[R_META]);
+            const bool filling = (m & META_FILLING) != 0u;
+            const bool overlap = !((r[F_HIX] < lo[0]) | (hi[0] < r[F_LOX]) | (r[F_HIY] < lo[1]) | (hi[1] < r[F_LOY]) |
+                                   (r[F_HIZ] < lo[2]) | (hi[2] < r[F_LOZ]));
+            const bool c = act & overlap & !solid & !(filling & any);
+            if (__builtin_amdgcn_ballot_w64(c) && c && rec_ray_hit(r, s, e, (m & META_GATE) ? rg : ro)) {
+                any = true;
+                solid = solid | !filling;
+            }
+        }
+        const uint32_t bits = (any ? 1u : 0u) | (solid ? 2u : 0u);
+        if (bits) atomicOr(&s_hit[j], bits);  // (LDS)
+        __syncthreads();
+        if (slice == 0 && act) valid[i] = (uint8_t)(s_hit[j] ^ 3u);
+        publish_done(done, seq);
+        return;
+    }
     const bool cp = can_pass != 0;
     auto cand_of = [&](const double* r, bool hit) {
         const uint32_t m = (uint32_t)__double_as_longlong(r[R_META]);

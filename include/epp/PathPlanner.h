@@ -107,6 +107,16 @@ public:
                                             double samplingInterval, double startTimeOffset, const Vec3& v0,
                                             const Vec3& a0, Matrix& result) const;
     std::vector<Vec3> includeGates2(std::vector<std::vector<Vec3>> waypoints) const;
+    // planPaths of consecutive gate-to-gate segments, then includeGates2 of their paths (an
+    // addition of this build, for OnlineTrajGenerator::preComputeTraj): the same answers as
+    // the two calls.  The gate centres includeGates2 inserts are the midpoints of the
+    // segments' ends, known before the plans, so with the "custom" pruning every ray the
+    // pruning can ask rides in the shortcut's batch (each ray tested once for both
+    // canPassGate answers): one synchronised launch fewer.  Returns false, `pruned`
+    // untouched, when some ok[i] is 0.
+    bool planPathsIncludeGates2(const std::vector<std::pair<Vec3, Vec3>>& problems, double timeLimit,
+                                std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok,
+                                std::vector<Vec3>& pruned) const;
 
     // batch-planner knobs (defaults follow the config: samples_fmt samples, k = 16)
     void setSeed(uint64_t seed) { seed_ = seed; }
@@ -120,20 +130,41 @@ public:
     std::shared_ptr<World> worldPtr;
 
 private:
+    // A problem of a chain of gate-to-gate segments (planPathsIncludeGates2): the gate
+    // centres includeGates2 will put before / after its path and, once the shortcut's batch
+    // has run, the canPassGate = true answers of every pair the pruning can ask.
+    struct GateEnds {
+        bool has_prev = false, has_next = false;
+        Vec3 prev, next;
+        bool filled = false;       // pts / vis hold the answers
+        std::vector<Vec3> pts;     // [prev] + the shortcut's input path + [next]
+        std::vector<uint8_t> vis;  // pair (i, j) of pts, j >= i + 2, in the shortcut's queue order
+    };
     std::vector<Vec3> pruneWaypoints(const std::vector<Vec3>& waypoints) const;
     std::vector<Vec3> shortcut(const std::vector<Vec3>& path) const;
-    std::vector<std::vector<Vec3>> shortcutAll(const std::vector<std::vector<Vec3>>& paths) const;
-    std::vector<std::vector<Vec3>> pruneAll(const std::vector<std::vector<Vec3>>& segments) const;
+    std::vector<std::vector<Vec3>> shortcutAll(const std::vector<std::vector<Vec3>>& paths,
+                                               const std::vector<GateEnds*>* ends = nullptr) const;
+    std::vector<std::vector<Vec3>> pruneAll(const std::vector<std::vector<Vec3>>& segments,
+                                            const std::vector<GateEnds>* ends = nullptr) const;
+    std::vector<Vec3> includeGates2With(std::vector<std::vector<Vec3>> waypoints,
+                                        const std::vector<GateEnds>* ends) const;
+    void planPathsWith(const std::vector<std::pair<Vec3, Vec3>>& problems, double timeLimit,
+                       std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok,
+                       std::vector<GateEnds>* ends) const;
     // omplPrunePathAndInterpolate (src/PathPlanner.cpp:282-313) for every segment at once:
     // OMPL's PathSimplifier::smoothBSpline with its defaults, each step's state and motion
     // checks for all segments in one batch each
     std::vector<std::vector<Vec3>> smoothAll(const std::vector<std::vector<Vec3>>& segments) const;
+    // ends (optional): one per problem, filled for the problems whose path is found
     int planCalls(const std::vector<std::pair<Vec3, Vec3>>& problems, uint64_t base, double timeLimit,
-                  std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const;
+                  std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok,
+                  std::vector<GateEnds>* ends = nullptr) const;
     void planAttempt(const std::vector<std::pair<Vec3, Vec3>>& problems, const std::vector<uint64_t>& seeds,
-                     int64_t samples, std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const;
+                     int64_t samples, std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok,
+                     GateEnds* ends = nullptr) const;
     void planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, const std::vector<uint64_t>& seeds,
-                   int64_t samples, std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok) const;
+                   int64_t samples, std::vector<std::vector<Vec3>>& paths, std::vector<char>& ok,
+                   GateEnds* ends = nullptr) const;
     // rows_sym (optional): the caller's symmetrised search on its restricted rows, run while
     // the device builds the whole table's masked k-NN; when that shows no kept edge into the
     // goal and rows_sym found the path, *decided_on_rows = true and the table is neither

@@ -47,6 +47,10 @@ public:
     void checkPointsMinDistance(const double* xyz, int64_t n, double minDistance, uint8_t* out) const;
     void checkRays(const double* s1, const double* s2, int64_t n, bool canPassGate, uint8_t* out,
                    int mode = 0) const;
+    // Both answers of checkRayValid per ray (an addition of this build): out[i] bit 0 = valid
+    // with canPassGate = false, bit 1 = valid with true.  One launch when the batch takes the
+    // small path (k_motions_small tests each ray once for both), else two.
+    void checkRaysBoth(const double* s1, const double* s2, int64_t n, uint8_t* out) const;
 
     // Device handle (rebuilt lazily after mutations); nullptr for an empty world.
     const epp_world* device() const;

@@ -352,6 +352,65 @@ def test_precompute_traj_ompl_simplification_equals_cpu(track, geom, tmp_path):
     assert np.abs(traj[:, :9] - rows[:, :9]).max() < 1e-6
 
 
+FILLING_CONFIG = os.path.join(ROOT, "configs", "config_filling.json")
+
+
+@pytest.mark.parametrize("n", [700, 3000])
+def test_check_rays_both(n):
+    """World::checkRaysBoth (the shortcut's batch in planPathsIncludeGates2): bit 0 = the
+    oracle's checkRayValid(.., false), bit 1 = (.., true), in a world with filling OBBs
+    (configs/config_filling.json) where the two differ -- rays through the gate openings
+    and random rays; 700 rays take the small path (one launch for both answers), 3,000 the
+    two launches past it."""
+    cfg = config.load(FILLING_CONFIG)
+    fgeom = config.geometry(cfg)
+    g, o, _, _ = synth.c1_world()
+    rg, ro = config.inflate_radii(cfg)
+    w = O.world_build(fgeom, g, o, rg, ro)
+    pp = _ot().PathPlanner(g, o, FILLING_CONFIG)
+    rs = np.random.RandomState(n)
+    m = n // 2  # through the openings: either side of the portal, along its normal
+    loc = rs.uniform([-0.3, -0.6, -0.3], [0.3, -0.3, 0.3], size=(m, 3))
+    loc2 = loc + np.c_[rs.uniform(-0.1, 0.1, m), rs.uniform(0.6, 1.2, m), rs.uniform(-0.1, 0.1, m)]
+    gt = g[0]
+    h = fgeom.gate_height[int(gt[6])]
+    c, sn = np.cos(gt[5]), np.sin(gt[5])
+
+    def world(l):
+        return np.stack([gt[0] + c * l[:, 0] - sn * l[:, 1], gt[1] + sn * l[:, 0] + c * l[:, 1], h + l[:, 2]], 1)
+
+    s1 = np.vstack([world(loc), synth.sample_states(5, [-2, -2, 0], [2, 2, 2], n - m)])
+    s2 = np.vstack([world(loc2), s1[m:] + rs.uniform(-0.8, 0.8, (n - m, 3))])
+    got = pp.check_rays_both(s1, s2)
+    e0 = O.check_motions(w, rg, ro, s1, s2, False, 0)
+    e1 = O.check_motions(w, rg, ro, s1, s2, True, 0)
+    assert (e1 > e0).sum() >= 20 and e0.min() == 0 and e1.max() == 1
+    assert np.array_equal(got, e0.astype(np.uint8) | (e1.astype(np.uint8) << 1))
+
+
+@pytest.mark.parametrize("can_pass", [False, True])
+def test_plan_paths_include_gates2_equals_two_calls(track, tmp_path, can_pass):
+    """planPathsIncludeGates2 (preComputeTraj's call: the pruning's rays in the shortcut's
+    batch) gives what planPaths followed by includeGates2 gives, on two planners with the
+    same call numbers: the same segments and the same pruned waypoints, for can_pass_gate
+    false and true (the shortcut reading the other answer bit)."""
+    _, c, gates, obstacles, start, goal = track
+    c = json.loads(json.dumps(c))
+    c["path_planner_properties"]["can_pass_gate"] = can_pass
+    p = tmp_path / "config.json"
+    p.write_text(json.dumps(c))
+    cps = synth.gate_checkpoints(gates, np.array([1.0, 0.525]), 0.55)
+    problems = [(cps[i], cps[i + 1]) for i in range(0, len(cps) - 1, 2)]
+    a, b = _ot().PathPlanner(gates, obstacles, str(p)), _ot().PathPlanner(gates, obstacles, str(p))
+    for _ in range(2):  # (the second call: the next call numbers)
+        segs = a.plan_paths(problems, 2.0)
+        assert all(ok for ok, _ in segs)
+        exp = a.include_gates2([x for _, x in segs])
+        segs2, got = b.plan_paths_include_gates2(problems, 2.0)
+        assert all(np.array_equal(x, y) and o1 == o2 for (o1, x), (o2, y) in zip(segs, segs2))
+        assert got is not None and np.array_equal(got, exp)
+
+
 def test_include_gates2_unknown_method(tmp_path, c1):
     g, o, *_ = c1
     path_cfg, _ = _write_config(tmp_path, path_planner_properties__path_simplification="bogus")
