@@ -718,13 +718,20 @@ def run_native(argv, via, timeout=120):
         return {"error": f"{type(e).__name__}: {e}", "via": via}
 
 
-C5_EVENT_TRACKS = 24  # 192 events: ~50 replans, so the replan class has a p99 worth the name
+C5_EVENT_TRACKS = 24  # 192 events: ~100 replans, so the replan class has a p99 worth the name
+# How far ahead of a gate it is observed.  The tracks pass their gate centres slowly
+# (0.08-0.4 m/s: the centre is a min-snap waypoint), so with the round-5 lead of 1 s the
+# advanced start recomputeTraj replans from (t + time_limit_online + 0.01 s,
+# src/OnlineTrajGenerator.cpp:290-310) lay within ~3-19 cm of the old centre, where the
+# +-0.1 m / 0.1 rad move put it inside the moved gate's inflated frame: 38 % of the events
+# took the no-recomputation exit (9 of 24 on 3 tracks, CPU restatement); at 2 s, 2 of 24.
+C5_EVENT_LEAD_S = 2.0
 
 
-def c5_events(cfg_path, geom, gates, obstacles, n_tracks=C5_EVENT_TRACKS, cpu_threads=None):
+def c5_events(cfg_path, geom, gates, obstacles, n_tracks=C5_EVENT_TRACKS, cpu_threads=None, lead_s=C5_EVENT_LEAD_S):
     """C5 through the reference's entry point, OnlineTrajGenerator.update_gate_pos
     (src/OnlineTrajGenerator.cpp:123-226): every gate of a planned track is observed once
-    (as the reference allows), 1 s of flight before the trajectory reaches its centre, at
+    (as the reference allows), lead_s of flight before the trajectory reaches its centre, at
     a pose perturbed by +-0.1 m / +-0.1 rad; the call checks the lookahead (checkGatePassed
     + A11) and, when the trajectory no longer passes or collides, calls recomputeTraj
     (inline: recalculate_online false).  Each event is timed and filed by what it ran:
@@ -763,7 +770,7 @@ def c5_events(cfg_path, geom, gates, obstacles, n_tracks=C5_EVENT_TRACKS, cpu_th
         for g in range(len(gates)):
             cur = traj_of()
             i_c = int(np.argmin(np.linalg.norm(cur[:, [0, 3, 6]] - centres[g], axis=1)))
-            t_obs = max(float(cur[i_c, -1]) - 1.0, 0.0)
+            t_obs = max(float(cur[i_c, -1]) - lead_s, 0.0)
             i = int(np.argmin(np.abs(cur[:, -1] - t_obs)))
             drone = cur[i, [0, 3, 6]].copy()
             pose = gates[g, :6].copy()
@@ -778,7 +785,8 @@ def c5_events(cfg_path, geom, gates, obstacles, n_tracks=C5_EVENT_TRACKS, cpu_th
     out = {"events": sum(len(v) for v in us.values()), "tracks": n_tracks,
            "counts": {k: len(v) for k, v in us.items()},
            **{k: (_pct(np.array(v)) if v else None) for k, v in us.items()},
-           "workload": "C5 via OnlineTrajGenerator.update_gate_pos: each gate observed once, 1 s ahead, pose +-0.1 m / "
+           "lead_s": lead_s,
+           "workload": f"C5 via OnlineTrajGenerator.update_gate_pos: each gate observed once, {lead_s:g} s ahead, pose +-0.1 m / "
                        "+-0.1 rad; check_only (checkGatePassed + A11, returned False), skipped_invalid_start "
                        "(returned True, the reference's no-recomputation exit) and replan (2 segment plans of "
                        f"{PLAN_SAMPLES:,} samples + includeGates2 + refit) timed separately"}
