@@ -877,8 +877,7 @@ __device__ __forceinline__ void refit_body(const RefitArgs& a, int g, double* sm
     EPP_TL(13);
     // completion: this slice's rows (and workgroup 0's status) are visible system-wide
     // before the slot is
-    __threadfence_system();
-    __syncthreads();
+    wg_stores_settled();
     if (tid == 0) {
         if (g == 0) __hip_atomic_store(a.info, (int64_t)st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(a.done + g, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -918,8 +917,7 @@ __global__ __launch_bounds__(kRefitBlock) void k_check_refit(RefitArgs a, CheckA
     }
     states_small_body<true, false>(smem, (int)blockIdx.x - a.writers, c.recs, c.n_obb, c.rg, c.ro, c.xyz, c.n, c.per, 0,
                                    c.md, c.valid, nullptr, nullptr);
-    __threadfence_system();
-    __syncthreads();
+    wg_stores_settled();
     if (threadIdx.x == 0) __hip_atomic_store(a.done + blockIdx.x, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 

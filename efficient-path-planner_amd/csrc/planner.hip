@@ -19,6 +19,7 @@
 #include <string>
 
 #include "cached_ws.h"
+#include "completion.h"
 #include "epp_internal.h"
 
 namespace epp {
@@ -2612,8 +2613,7 @@ __global__ __launch_bounds__(256) void k_pb_emit(PlanBatchDev P, unsigned long l
             h_need[at] = d_need[at];
         }
     }
-    __threadfence_system();
-    __syncthreads();
+    wg_stores_settled();
     if (threadIdx.x == 0) __hip_atomic_store(done + blockIdx.x, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 

@@ -2,6 +2,7 @@
 // with the fused check + refit kernel of the online step (minsnap.hip).  See small.hip.
 #pragma once
 #include "collision_common.h"
+#include "completion.h"
 
 namespace epp {
 namespace {
@@ -14,8 +15,7 @@ constexpr int kSmallBlock = 256;
 // synchronising the stream.
 __device__ __forceinline__ void publish_done(uint32_t* done, uint32_t seq) {
     if (!done) return;
-    __threadfence_system();
-    __syncthreads();
+    wg_stores_settled();
     if (threadIdx.x == 0) __hip_atomic_store(done + blockIdx.x, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 

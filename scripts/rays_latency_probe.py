@@ -1,6 +1,7 @@
 """Latency of the small ray batches (diagnostics): World::checkRaysBoth / checkRayValid on
 the C4 track world through the PathPlanner binding, wall time per call for batch sizes
-1..1024 (the shortcut's batch is ~700 rays).  python scripts/rays_latency_probe.py"""
+1..1024 (the shortcut's batch is ~700 rays).  python scripts/rays_latency_probe.py
+(scripts/small_rays_trace.py reads the kernel durations from a kernel trace of it)"""
 import json
 import os
 import sys
@@ -8,7 +9,8 @@ import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "efficient-path-planner_amd")]
+# EPP_PKG: another build of the package (scripts/ab_pkg.sh) for a same-box A/B
+sys.path[:0] = [ROOT, os.environ.get("EPP_PKG") or os.path.join(ROOT, "efficient-path-planner_amd")]
 import numpy as np  # noqa: E402
 
 import online_traj_planner as otp  # noqa: E402
