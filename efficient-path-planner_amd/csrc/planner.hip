@@ -3064,10 +3064,12 @@ epp::PlanBatchLayout epp::plan_batch_layout(int32_t S, int64_t ns, int32_t k, Pl
     L.h_slot = take(capr * 4);
     L.h_rows = take(capr * k * 2);
     L.h_need = take((size_t)L.need_cap * 24 + 16);
-    {  // emit workgroups: each one's system fence writes back its XCD's L2, so few of them
+    {  // emit workgroups: each one's completion release writes back its XCD's L2 (once per
+       // workgroup since completion.h; kernel trace, scripts/gpu_emit_ab.sh: 64 -> 26.6 us,
+       // 128 -> 21.6, 256 -> 23.3, 512 -> 29.1)
         static const int eb = [] {
             const char* e = std::getenv("EPP_PB_EMIT_BLOCKS");  // (A/B knob: same results)
-            const int v = e && *e ? std::atoi(e) : 64;
+            const int v = e && *e ? std::atoi(e) : 128;
             return std::max(1, std::min(kPbEmitMax, v));
         }();
         L.done_n = eb;

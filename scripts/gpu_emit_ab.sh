@@ -1,8 +1,10 @@
 #!/bin/bash
-# k_pb_emit workgroup count sweep (diagnostics): the planner probe with the stage trace
-# (EPP_PB_TRACE=1) under several EPP_PB_EMIT_BLOCKS values.
-set -u
-for eb in 16 32 64 128 256 32; do
-  EPP_PB_EMIT_BLOCKS=$eb EPP_PB_TRACE=1 EPP_PLAN_THREADS=16 EPP_PROBE_CALLS=30 timeout -k 10 120 python scripts/plan_probe.py --child > gpurun_out/pbt_$eb.log 2> gpurun_out/pbt_$eb.err || exit 1
-  echo "eb $eb: $(grep phases gpurun_out/pbt_$eb.log)"
+# k_pb_emit workgroup count sweep (diagnostics): the planner probe under several
+# EPP_PB_EMIT_BLOCKS values, each under a kernel trace (k_pb_emit's own duration) and
+# with the planner's phases.
+set -u -o pipefail
+mkdir -p gpurun_out/emit
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+for eb in 64 128 256 512; do
+  EPP_PB_EMIT_BLOCKS=$eb EPP_PROBE_CALLS=60 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/emit/eb$eb -o k -- python scripts/plan_probe.py --child > gpurun_out/emit/eb$eb.log 2>&1 || exit 1
 done
