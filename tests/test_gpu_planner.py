@@ -411,6 +411,26 @@ def test_plan_paths_include_gates2_equals_two_calls(track, tmp_path, can_pass):
         assert got is not None and np.array_equal(got, exp)
 
 
+def test_plan_paths_include_gates2_edges(c1):
+    """planPathsIncludeGates2 at the edges: one problem (no gate centres), a chain with a
+    problem that fails (pruned is None, the segments as plan_paths gives them, failures
+    included), and a chain whose second problem starts where the first ends (a gate
+    centre equal to both ends) -- each against plan_paths + include_gates2 on a planner
+    with the same call numbers."""
+    g, o, start, goal, *_ = c1
+    blocked = np.array([1.0, 0.5, 0.5])  # inside an obstacle
+    mid = (start + goal) / 2
+    for problems in ([(start, goal)], [(start, mid), (mid, blocked), (mid, goal)], [(start, mid), (mid, goal)]):
+        a, b = _ot().PathPlanner(g, o, CONFIG), _ot().PathPlanner(g, o, CONFIG)
+        segs = a.plan_paths(problems, 0.5)
+        segs2, got = b.plan_paths_include_gates2(problems, 0.5)
+        assert all(o1 == o2 and np.array_equal(x, y) for (o1, x), (o2, y) in zip(segs, segs2))
+        if all(ok for ok, _ in segs):
+            assert got is not None and np.array_equal(got, a.include_gates2([x for _, x in segs]))
+        else:
+            assert got is None
+
+
 def test_include_gates2_unknown_method(tmp_path, c1):
     g, o, *_ = c1
     path_cfg, _ = _write_config(tmp_path, path_planner_properties__path_simplification="bogus")
