@@ -179,11 +179,26 @@ int main(int argc, char** argv) {
             }
             last = tr;
         };
-        std::vector<double> t_fused, t_two;
+        std::vector<double> t_fused, t_two, t_update;
         std::vector<char> v_fused, v_two;
         Matrix last_fused, last_two;
         online(false, t_two, v_two, last_two);
         online(true, t_fused, v_fused, last_fused);
+        {  // the step's world update alone (updateGatePos and the device world's refresh the
+           // step's check then uses): the host share of the step
+            PathPlanner p3(in.gates, in.obstacles, cfg);
+            (void)p3.worldPtr->device();
+            for (const Step& s : in.steps) {
+                const double t0 = now_us();
+                std::vector<double> pose(in.gates.row(s.gate), in.gates.row(s.gate) + 6);
+                pose[0] += s.dx;
+                pose[1] += s.dy;
+                pose[5] += s.dyaw;
+                p3.updateGatePos(s.gate, pose);
+                (void)p3.worldPtr->device();
+                t_update.push_back(now_us() - t0);
+            }
+        }
         int64_t invalid_steps = 0;
         for (char v : v_fused) invalid_steps += v ? 0 : 1;
         const bool agree = v_fused == v_two && last_fused.rows == last_two.rows && last_fused.data == last_two.data;
@@ -191,6 +206,7 @@ int main(int argc, char** argv) {
         print_pct("c5_refit_native", t_refit, false);
         print_pct("c5_online_native", t_fused, false);
         print_pct("c5_online_native_two_calls", t_two, false);
+        print_pct("c5_world_update_native", t_update, false);
         std::printf("\"refit_rows\": %zu, \"online_rows\": %zu, \"online_invalid_steps\": %lld, "
                     "\"fused_equals_two_calls\": %s, \"online_step\": \"fused: one launch (A11 check + refit)\"}\n",
                     refit_rows, last_fused.rows, (long long)invalid_steps, agree ? "true" : "false");
