@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 #include <cstdio>
 #include <mutex>
@@ -1952,8 +1953,12 @@ __global__ __launch_bounds__(256) void k_pack_ellipse_rows(const double* __restr
 // its problem is the low bits of its global id p NS + node), its k-NN grid workspace at
 // kws + p kws_stride (KnnLayout for ns + 2 nodes), its queries at query + row_off.  Node
 // counts stay on the device.
+constexpr int kPbSegSmall = 16;  // batches of up to this many problems: no upload (k_pb_sample)
 struct PlanBatchDev {
     const PlanSeg* seg;
+    const PlanSeg* seg_h;         // (<= kPbSegSmall problems) the pinned host copy, else null
+    uint64_t seeds[kPbSegSmall];  // (<= kPbSegSmall problems) their seeds and capacities
+    int32_t caps[kPbSegSmall];
     int S, k, ns_log, nbc, cap_total, nctr;
     int64_t ns, NS;
     double lo[3], hi[3];
@@ -1999,20 +2004,33 @@ enum : int { kFQueries = 0, kFKept = 1, kFGoal = 2, kFNodes = 3, kFNeed = 4, kFI
 
 // samples (k_sample_uniform's arithmetic) + clears: the problem's compaction status words
 // and node marks; problem 0 also the batch counters
+// A batch of <= kPbSegSmall problems needs no upload of its own (a blit dispatch, ~5 us,
+// before round 6): every workgroup takes its problem's seed and capacity from the launch
+// arguments (P.seeds / P.caps), and workgroup (0, p) reads problem p from the pinned host
+// copy and stores it into the device copy the later stages read.  Larger batches upload
+// the problems first (P.seg_h null).
+static_assert(sizeof(PlanSeg) % 8 == 0, "PlanSeg copied as 8-byte words");
+
 __global__ __launch_bounds__(256) void k_pb_sample(PlanBatchDev P) {
     const int p = blockIdx.y;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool small = P.seg_h != nullptr;  // (uniform)
+    if (small && blockIdx.x == 0 && threadIdx.x < (int)(sizeof(PlanSeg) / 8))
+        reinterpret_cast<uint64_t*>(const_cast<PlanSeg*>(P.seg) + p)[threadIdx.x] =
+            reinterpret_cast<const uint64_t*>(P.seg_h + p)[threadIdx.x];
     if (i < P.nbc) P.cstat[(int64_t)p * P.nbc + i] = 0ull;
     if (P.cap_total > 0 && i < P.NS / kCompactChunk) P.nstat[(int64_t)p * (P.NS / kCompactChunk) + i] = 0ull;
     // (the marks exist only when some problem has restricted rows: cap_total > 0)
     if (P.cap_total > 0 && i < (P.NS >> 4))
         reinterpret_cast<uint4*>(P.mark + ((int64_t)p << P.ns_log))[i] = make_uint4(0u, 0u, 0u, 0u);
     if (p == 0 && i < P.nctr) P.ctr[i] = 0ull;
-    const PlanSeg& q = P.seg[p];
-    if (q.cap > 0) {  // the problem's k-NN grid: cleared cell counters and its shape
+    const uint64_t seed = small ? P.seeds[p] : P.seg[p].seed;
+    const int32_t cap = small ? P.caps[p] : P.seg[p].cap;
+    if (cap > 0) {  // the problem's k-NN grid: cleared cell counters and its shape
         const KnnSeg ks = knn_seg(P, p);
         if (i < P.nclr) ks.cnt[i] = 0;
         if (i == 0) {
+            const PlanSeg q = small ? P.seg_h[p] : P.seg[p];
             KnnGrid gv{};
             int64_t cells = 1;
             double h = q.h;
@@ -2034,7 +2052,6 @@ __global__ __launch_bounds__(256) void k_pb_sample(PlanBatchDev P) {
         }
     }
     if (i >= P.ns) return;
-    const uint64_t seed = q.seed;
     const uint64_t c = (uint64_t)i * 3ull;
     const double u0 = (double)(splitmix64(seed ^ c) >> 11) * 0x1.0p-53;
     const double u1 = (double)(splitmix64(seed ^ (c + 1)) >> 11) * 0x1.0p-53;
@@ -3178,9 +3195,20 @@ epp_status epp::plan_batch_launch(const epp_world* world, int32_t can_pass_gate,
     P.need = reinterpret_cast<double*>(d + L.o_need);
     const unsigned S = (unsigned)L.S;
     const bool R = L.cap_total > 0;
-    // the problems up (pinned), then every stage on this stream
-    if (hipMemcpyAsync(d + L.o_seg, h + L.h_seg, (size_t)L.S * sizeof(PlanSeg), hipMemcpyHostToDevice, s) != hipSuccess)
-        return last("plan_batch_launch");
+    // the problems: in k_pb_sample's arguments (<= kPbSegArgMax), else uploaded first; then
+    // every stage on this stream
+    P.seg_h = nullptr;
+    if (L.S <= kPbSegSmall) {
+        P.seg_h = reinterpret_cast<const PlanSeg*>(h + L.h_seg);
+        for (int p = 0; p < L.S; ++p) {
+            P.seeds[p] = P.seg_h[p].seed;
+            P.caps[p] = P.seg_h[p].cap;
+        }
+    } else {
+        if (hipMemcpyAsync(d + L.o_seg, h + L.h_seg, (size_t)L.S * sizeof(PlanSeg), hipMemcpyHostToDevice, s) !=
+            hipSuccess)
+            return last("plan_batch_launch");
+    }
     const int64_t clr = std::max<int64_t>({L.ns, R ? L.NS >> 4 : 0, R ? (int64_t)P.nclr : 0, (int64_t)L.nbc, (int64_t)L.nctr});
     pb_mark(s, "begin");
     hipLaunchKernelGGL(k_pb_sample, dim3((unsigned)((clr + 255) / 256), S), dim3(256), 0, s, P);
