@@ -255,14 +255,13 @@ private:
 
 // A*'s state per host thread, reused across searches: an entry counts only when its stamp
 // is the search's (no O(n) clearing per search); the heap keeps its storage.
-struct QE {
+struct QE {  // (16 bytes: the heap moves less than with a separate tie-break key)
     double f;
-    int key;  // the node id, or an index in node order: ties in f pop the lower id first, as
-              // std::priority_queue<pair<double, int>, ..., std::greater<>> does
-    int v;    // the search's own index of the node
+    int v;  // the node (its index is in node order): ties in f pop the lower index first, as
+            // std::priority_queue<pair<double, int>, ..., std::greater<>> does
 };
 struct QECmp {
-    bool operator()(const QE& a, const QE& b) const { return b.f < a.f || (!(a.f < b.f) && b.key < a.key); }
+    bool operator()(const QE& a, const QE& b) const { return b.f < a.f || (!(a.f < b.f) && b.v < a.v); }
 };
 struct SearchState {
     std::vector<double> dist;
@@ -340,12 +339,12 @@ bool plan_trace() {
 }
 
 // A* from node 0 to node 1 with the Euclidean distance to the goal (admissible and
-// consistent for Euclidean edge costs).  pos(v): coordinates; key(v): the node id that
-// breaks ties; expand(u, f, relax) calls relax(v) for u's edges and returns false to abort
+// consistent for Euclidean edge costs).  pos(v): coordinates (node indices in node order:
+// the lower breaks ties); expand(u, f, relax) calls relax(v) for u's edges and returns false to abort
 // (the caller then takes another graph).  Returns 1 (goal closed), 0 (exhausted), -1
 // (aborted).
-template <class Pos, class Key, class Expand>
-int astar(SearchState& ss, size_t nv, Pos&& pos, Key&& key, Expand&& expand) {
+template <class Pos, class Expand>
+int astar(SearchState& ss, size_t nv, Pos&& pos, Expand&& expand) {
     ss.begin(nv);
     ss.pops = 0;
     const QECmp cmp;
@@ -358,7 +357,7 @@ int astar(SearchState& ss, size_t nv, Pos&& pos, Key&& key, Expand&& expand) {
     ss.seen[0] = ss.cur;
     ss.dist[0] = 0.0;
     ss.prev[0] = -1;
-    push({(pos(0) - gp).norm(), key(0), 0});
+    push({(pos(0) - gp).norm(), 0});
     while (!q.empty()) {
         const QE top = q.front();
         std::pop_heap(q.begin(), q.end(), cmp);
@@ -375,7 +374,7 @@ int astar(SearchState& ss, size_t nv, Pos&& pos, Key&& key, Expand&& expand) {
                 ss.seen[v] = ss.cur;
                 ss.dist[v] = nd;
                 ss.prev[v] = u;
-                push({nd + (pv - gp).norm(), key(v), v});
+                push({nd + (pv - gp).norm(), v});
             }
         };
         if (!expand(u, top.f, relax, /*closing=*/false)) return -1;
@@ -550,13 +549,12 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
             SearchState& ss = sc.ss;
             const double bound = segs[p].bound;
             auto pos = [&](int v) { return Vec3(nd[3 * v], nd[3 * v + 1], nd[3 * v + 2]); };
-            auto key = [](int v) { return v; };  // (compact indices keep the node order)
             // (no kept edge into the goal among the rows: the forward search on them cannot
             // reach it -- the goal-edge count below decides instead, r = -1)
             const bool goal_edges = hv(2, p) > 0;
             r = -1;
             if (goal_edges)
-                r = astar(ss, (size_t)m, pos, key, [&](int u, double f, auto&& relax, bool closing) {
+                r = astar(ss, (size_t)m, pos, [&](int u, double f, auto&& relax, bool closing) {
                     if (!closing) return (f <= bound) && row_of[u] >= 0;
                     const uint16_t* row = rowc.data() + (size_t)row_of[u] * k;
                     for (int c = 0; c < k; ++c)
@@ -597,7 +595,7 @@ void PathPlanner::planChunk(const std::vector<std::pair<Vec3, Vec3>>& problems, 
                     for (int c = 0; c < k; ++c)
                         if (row[c] != 0xFFFF) radj[(size_t)fill[row[c]]++] = u;
                 }
-                const int r2 = astar(ss, (size_t)m, pos, key, [&](int u, double f, auto&& relax, bool closing) {
+                const int r2 = astar(ss, (size_t)m, pos, [&](int u, double f, auto&& relax, bool closing) {
                     if (!closing) return (f <= bound) && row_of[u] >= 0;
                     const uint16_t* row = rowc.data() + (size_t)row_of[u] * k;
                     for (int c = 0; c < k; ++c)
@@ -940,13 +938,12 @@ bool PathPlanner::wholeTableSearch(const double* d_nodes, int32_t n, const doubl
         return x == 0xFFFF ? -1 : (int)x;
     };
     auto pos = [&](int v) { return Vec3(nodes[3 * v], nodes[3 * v + 1], nodes[3 * v + 2]); };
-    auto key = [](int v) { return v; };
     thread_local SearchState ss;
     // (no forward edge into the goal: the forward pass cannot reach it -- it would only
     // explore start's whole component first; same result, so go straight to the second)
     int r = 0;
     if (goal_has_forward_edge)
-        r = astar(ss, (size_t)n, pos, key, [&](int u, double, auto&& relax, bool closing) {
+        r = astar(ss, (size_t)n, pos, [&](int u, double, auto&& relax, bool closing) {
             if (closing)
                 for (int c = 0; c < k; ++c) {
                     const int v = nbr((size_t)u * k + c);
@@ -980,7 +977,7 @@ bool PathPlanner::wholeTableSearch(const double* d_nodes, int32_t n, const doubl
         auto radj = [&](int64_t q) -> int { return narrow ? (int)radj16[q] : radj32[q]; };
         const auto t_csr = std::chrono::steady_clock::now();
         int64_t pops = 0;
-        r = astar(ss, (size_t)n, pos, key, [&](int u, double, auto&& relax, bool closing) {
+        r = astar(ss, (size_t)n, pos, [&](int u, double, auto&& relax, bool closing) {
             pops += closing ? 1 : 0;
             if (closing) {
                 for (int c = 0; c < k; ++c) {
