@@ -1,4 +1,5 @@
 # Refit writer workgroups (EPP_REFIT_ROWS_PER_WRITER): the min-snap GPU tests at 64, then
+# (a diagnostics A/B of round 6: the knob it sets was removed again after it measured slower)
 # the C5 step probe and a kernel trace of it at 128 / 64 / 43 / 32 rows per writer.
 set -u -o pipefail
 mkdir -p gpurun_out/wr
