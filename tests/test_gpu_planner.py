@@ -388,14 +388,22 @@ def test_check_rays_both(n):
     assert np.array_equal(got, e0.astype(np.uint8) | (e1.astype(np.uint8) << 1))
 
 
+@pytest.mark.parametrize("filling", [False, True])
 @pytest.mark.parametrize("can_pass", [False, True])
-def test_plan_paths_include_gates2_equals_two_calls(track, tmp_path, can_pass):
+def test_plan_paths_include_gates2_equals_two_calls(track, tmp_path, can_pass, filling):
     """planPathsIncludeGates2 (preComputeTraj's call: the pruning's rays in the shortcut's
     batch) gives what planPaths followed by includeGates2 gives, on two planners with the
     same call numbers: the same segments and the same pruned waypoints, for can_pass_gate
-    false and true (the shortcut reading the other answer bit)."""
+    false and true (the shortcut reading the other answer bit), in the track world and in
+    the same world with filling OBBs (configs/config_filling.json), where the two answers
+    differ at the portals."""
     _, c, gates, obstacles, start, goal = track
     c = json.loads(json.dumps(c))
+    if filling:
+        f = json.load(open(FILLING_CONFIG))
+        f["world_properties"]["lower_bound"] = c["world_properties"]["lower_bound"]
+        f["world_properties"]["upper_bound"] = c["world_properties"]["upper_bound"]
+        c = f
     c["path_planner_properties"]["can_pass_gate"] = can_pass
     p = tmp_path / "config.json"
     p.write_text(json.dumps(c))
